@@ -1,0 +1,227 @@
+// Per-block scans: Lyndon factorisation from the linear suffix order, BBWT gather.
+//
+// Lyndon factorisation (replaces Duval, PY:326-349 / CPP:902-933): position p starts a
+// Lyndon factor of its block iff its suffix is smaller than every suffix starting
+// before it inside the block, i.e. ISA[p] < min(ISA[base..p)) — left-to-right minima of
+// the inverse suffix array (the factors are the non-increasing Lyndon words, and the
+// last factor is the minimal suffix).  Computed as a tiled per-block prefix-min scan.
+// Then every position gets its factor's start FS and length FL (prefix-max of starts,
+// suffix-min of the next start).
+//
+// BBWT gather (PY:417: out.append(w[(i - 1) % m])): out[r] = text[prev(SA[r])] where
+// prev steps back cyclically inside the factor.
+#include "kolm_internal.h"
+
+namespace kolm {
+
+namespace {
+
+constexpr u32 BIG = 0xFFFFFFFFu;
+
+struct TileGeom {
+    Geom geo;
+    u32 tpb;  // tiles per block
+    __device__ inline bool range(u32 t, u32& lo, u32& hi, u32& b) const {
+        b = t / tpb;
+        const u32 k = t - b * tpb;
+        lo = geo.base(b) + k * TILE;
+        const u32 e = geo.end(b);
+        hi = min(lo + (u32)TILE, e);
+        return lo < e;
+    }
+};
+
+__device__ inline u32 wave_reduce_min(u32 v) {
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, (u32)__shfl_xor(v, o));
+    return v;
+}
+__device__ inline u32 wave_reduce_max(u32 v) {
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (u32)__shfl_xor(v, o));
+    return v;
+}
+
+// exclusive scan across the workgroup (min or max, forward or reverse)
+template <bool REV, bool MAX>
+__device__ inline u32 wg_excl(u32 v, u32 ident, u32* sh) {
+    const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    u32 incl = v;
+    for (u32 o = 1; o < 64; o <<= 1) {
+        u32 t = REV ? __shfl_down(incl, o) : __shfl_up(incl, o);
+        if (REV ? (lane + o < 64) : (lane >= o)) incl = MAX ? max(incl, t) : min(incl, t);
+    }
+    u32 ex = REV ? __shfl_down(incl, 1) : __shfl_up(incl, 1);
+    if (REV ? lane == 63 : lane == 0) ex = ident;
+    if (REV ? lane == 0 : lane == 63) sh[w] = incl;
+    __syncthreads();
+    u32 carry = ident;
+    if (!REV) {
+        for (u32 i = 0; i < w; ++i) carry = MAX ? max(carry, sh[i]) : min(carry, sh[i]);
+    } else {
+        for (u32 i = w + 1; i < WG / 64; ++i) carry = MAX ? max(carry, sh[i]) : min(carry, sh[i]);
+    }
+    __syncthreads();
+    return MAX ? max(carry, ex) : min(carry, ex);
+}
+
+// Phase A: per-tile min of RK.
+__global__ __launch_bounds__(WG) void k_tile_min_rk(TileGeom tg, const u32* RK, u32* tmin) {
+    __shared__ u32 sh[WG / 64];
+    u32 lo, hi, b;
+    const bool ok = tg.range(blockIdx.x, lo, hi, b);
+    u32 m = BIG;
+    if (ok)
+        for (u32 i = lo + threadIdx.x; i < hi; i += WG) m = min(m, RK[i]);
+    m = wave_reduce_min(m);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) tmin[blockIdx.x] = min(min(sh[0], sh[1]), min(sh[2], sh[3]));
+}
+
+// Phase B: per block, exclusive scan over the block's tiles (one workgroup per block).
+template <bool REV, bool MAX>
+__global__ __launch_bounds__(WG) void k_tiles_scan(const u32* in, u32* out, u32 tpb, u32 ident) {
+    __shared__ u32 sh[WG / 64];
+    const u32 b = blockIdx.x;
+    u32 carry = ident;
+    const u32 nch = (tpb + WG - 1) / WG;
+    for (u32 c = 0; c < nch; ++c) {
+        const u32 cc = REV ? nch - 1 - c : c;
+        const u32 k = cc * WG + threadIdx.x;
+        const u32 v = k < tpb ? in[b * tpb + k] : ident;
+        const u32 ex = wg_excl<REV, MAX>(v, ident, sh);
+        const u32 r = MAX ? max(carry, ex) : min(carry, ex);
+        if (k < tpb) out[b * tpb + k] = r;
+        // chunk total
+        u32 tot = MAX ? max(ex, v) : min(ex, v);  // inclusive at this thread
+        __shared__ u32 edge;
+        if (REV ? threadIdx.x == 0 : threadIdx.x == WG - 1) edge = tot;
+        __syncthreads();
+        carry = MAX ? max(carry, edge) : min(carry, edge);
+        __syncthreads();
+    }
+}
+
+// Phase C: factor-start flags.
+__global__ __launch_bounds__(WG) void k_lyn_flags(TileGeom tg, const u32* RK, const u32* tcarry,
+                                                  u8* flag) {
+    __shared__ u32 sh[WG / 64];
+    u32 lo, hi, b;
+    if (!tg.range(blockIdx.x, lo, hi, b)) return;
+    // each thread: PER_THREAD consecutive elements
+    const u32 i0 = lo + threadIdx.x * PER_THREAD;
+    u32 v[PER_THREAD];
+    u32 loc = BIG;
+#pragma unroll
+    for (int e = 0; e < PER_THREAD; ++e) {
+        v[e] = (i0 + e < hi) ? RK[i0 + e] : BIG;
+        loc = min(loc, v[e]);
+    }
+    u32 run = min(tcarry[blockIdx.x], wg_excl<false, false>(loc, BIG, sh));
+#pragma unroll
+    for (int e = 0; e < PER_THREAD; ++e) {
+        if (i0 + e < hi) flag[i0 + e] = v[e] < run ? 1 : 0;
+        run = min(run, v[e]);
+    }
+}
+
+// Phase A': per-tile max start position and min start position.
+__global__ __launch_bounds__(WG) void k_tile_starts(TileGeom tg, const u8* flag, u32* tmax, u32* tmin) {
+    __shared__ u32 sh1[WG / 64], sh2[WG / 64];
+    u32 lo, hi, b;
+    const bool ok = tg.range(blockIdx.x, lo, hi, b);
+    u32 mx = 0, mn = BIG;
+    if (ok)
+        for (u32 i = lo + threadIdx.x; i < hi; i += WG)
+            if (flag[i]) {
+                mx = max(mx, i);
+                mn = min(mn, i);
+            }
+    mx = wave_reduce_max(mx);
+    mn = wave_reduce_min(mn);
+    if ((threadIdx.x & 63) == 0) {
+        sh1[threadIdx.x >> 6] = mx;
+        sh2[threadIdx.x >> 6] = mn;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        tmax[blockIdx.x] = max(max(sh1[0], sh1[1]), max(sh1[2], sh1[3]));
+        tmin[blockIdx.x] = min(min(sh2[0], sh2[1]), min(sh2[2], sh2[3]));
+    }
+}
+
+// Phase C': FS = last start <= p, FL = (next start > p, or block end) - FS.
+__global__ __launch_bounds__(WG) void k_fsfl(TileGeom tg, const u8* flag, const u32* cmax,
+                                             const u32* cmin, u32* FS, u32* FL) {
+    __shared__ u32 sh[WG / 64];
+    u32 lo, hi, b;
+    if (!tg.range(blockIdx.x, lo, hi, b)) return;
+    const u32 bend = tg.geo.end(b);
+    const u32 i0 = lo + threadIdx.x * PER_THREAD;
+    bool f[PER_THREAD];
+    u32 lmax = 0, lmin = BIG;
+#pragma unroll
+    for (int e = 0; e < PER_THREAD; ++e) {
+        const u32 i = i0 + e;
+        f[e] = i < hi && flag[i];
+        if (f[e]) {
+            lmax = max(lmax, i);
+            lmin = min(lmin, i);
+        }
+    }
+    u32 fs = max(cmax[blockIdx.x], wg_excl<false, true>(lmax, 0u, sh));
+    u32 fe = min(cmin[blockIdx.x], wg_excl<true, false>(lmin, BIG, sh));
+    u32 fsv[PER_THREAD];
+#pragma unroll
+    for (int e = 0; e < PER_THREAD; ++e) {
+        if (f[e]) fs = i0 + e;
+        fsv[e] = fs;
+    }
+#pragma unroll
+    for (int e = PER_THREAD - 1; e >= 0; --e) {
+        const u32 i = i0 + e;
+        if (i < hi) {
+            const u32 end = fe == BIG ? bend : fe;
+            FS[i] = fsv[e];
+            FL[i] = end - fsv[e];
+        }
+        if (f[e]) fe = i0 + e;
+    }
+}
+
+__global__ void k_bbwt_gather(Geom geo, const u8* text, const u32* SA, const u32* FS, const u32* FL,
+                              u8* out) {
+    for (u32 g = blockIdx.x * blockDim.x + threadIdx.x; g < geo.N; g += gridDim.x * blockDim.x) {
+        const u32 p = SA[g];
+        const u32 fs = FS[p];
+        out[g] = text[p == fs ? fs + FL[p] - 1 : p - 1];
+    }
+}
+
+}  // namespace
+
+void launch_lyndon(const Geom& geo, const u32* RK, u8* flag, u32* FS, u32* FL, u32* tile_tmp,
+                   u32* tile_tmp2, hipStream_t s) {
+    if (!geo.N) return;
+    TileGeom tg{geo, (geo.bs + TILE - 1) / TILE};
+    const u32 nt = tg.tpb * geo.nb;
+    u32* A = tile_tmp;        // [nt]
+    u32* B = tile_tmp + nt;   // [nt]
+    u32* C2 = tile_tmp2;      // [nt]
+    u32* D = tile_tmp2 + nt;  // [nt]
+    k_tile_min_rk<<<nt, WG, 0, s>>>(tg, RK, A);
+    k_tiles_scan<false, false><<<geo.nb, WG, 0, s>>>(A, B, tg.tpb, BIG);
+    k_lyn_flags<<<nt, WG, 0, s>>>(tg, RK, B, flag);
+    k_tile_starts<<<nt, WG, 0, s>>>(tg, flag, A, C2);
+    k_tiles_scan<false, true><<<geo.nb, WG, 0, s>>>(A, B, tg.tpb, 0u);
+    k_tiles_scan<true, false><<<geo.nb, WG, 0, s>>>(C2, D, tg.tpb, BIG);
+    k_fsfl<<<nt, WG, 0, s>>>(tg, flag, B, D, FS, FL);
+}
+
+void launch_bbwt_gather(const Geom& geo, const u8* text, const u32* SA, const u32* FS, const u32* FL,
+                        u8* out, hipStream_t s) {
+    if (!geo.N) return;
+    const u32 grid = (u32)std::min<u64>((geo.N + 255) / 256, 65535);
+    k_bbwt_gather<<<grid, 256, 0, s>>>(geo, text, SA, FS, FL, out);
+}
+
+}  // namespace kolm

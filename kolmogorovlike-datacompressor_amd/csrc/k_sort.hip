@@ -1,0 +1,553 @@
+// Suffix sorting for the BBWT (gfx950): segmented prefix doubling over a batch of blocks.
+//
+// Replaces the reference's per-factor comparison-sort prefix doubling + k-way heap merge
+// (PY:351-423, CPP:939-1093).  Two passes use these kernels:
+//   * linear  — suffix order of each block (sentinel < every byte), used for the Lyndon
+//               factorisation (factor starts = left-to-right minima of the inverse SA,
+//               replacing Duval PY:326-349) and for the LZ77 3-gram chains;
+//   * cyclic  — omega-order of all rotations of all Lyndon factors of a block
+//               (succ(p) = next position inside p's factor, cyclically).  A stable sort
+//               of positions by that order with ties in position order IS the BBWT
+//               order of PY's heap merge (ties (fi, i) = position order, PY:408-409).
+//
+// State per position: SA (positions in current order), RK (rank = SA index of the start
+// of the position's group), K2 (sort key of the current round, per SA slot).  Each round
+// refines every unsorted group ("segment") by the key of this round:
+//   round 0:  packed leading characters (linear: 3 x 9-bit chars with 0 = end;
+//             cyclic: 4 chars of the rotation)
+//   round r:  RK[succ^h(p)] with h = h0 * 2^(r-1)  (prefix doubling).
+// Segments are processed by size: len <= TILE in one workgroup (LDS bitonic sort of
+// (key, position), which yields position order among equal keys), longer ones by stable
+// 8-bit MSD radix passes (LDS histograms, per-segment tile scan, stable scatter) until
+// their buckets fit a tile.  A group splitting or not is tracked per block: in cyclic
+// mode a block whose groups did not split in a doubling round can never split again
+// (E_2h == E_h => fixed point) and is retired.  See DESIGN.md §4.
+#include "kolm_internal.h"
+
+namespace kolm {
+
+void geom_init(Geom& g, u64 N, u32 bs) {
+    g.N = N;
+    g.bs = bs;
+    g.nb = bs ? (u32)((N + bs - 1) / bs) : 0;
+    u32 s = 0;
+    while ((1ull << s) < bs) ++s;
+    g.shift = 32 + s;
+    g.magic = ((1ull << g.shift) / bs) + 1;
+}
+
+// ------------------------------------------------------------------------------------
+// block-wide scans (256 threads = 4 waves of 64)
+// ------------------------------------------------------------------------------------
+struct OpMax {
+    __device__ u32 operator()(u32 a, u32 b) const { return a > b ? a : b; }
+};
+struct OpMin {
+    __device__ u32 operator()(u32 a, u32 b) const { return a < b ? a : b; }
+};
+struct OpAdd {
+    __device__ u32 operator()(u32 a, u32 b) const { return a + b; }
+};
+
+// Exclusive scan over the threads of the workgroup (REV: from the last thread down).
+template <bool REV, class Op>
+__device__ inline u32 wg_excl_scan(u32 v, Op op, u32 ident, u32* sh /*[4]*/) {
+    const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    u32 incl = v;
+#pragma unroll
+    for (u32 o = 1; o < 64; o <<= 1) {
+        u32 t = REV ? __shfl_down(incl, o) : __shfl_up(incl, o);
+        if (REV ? (lane + o < 64) : (lane >= o)) incl = op(incl, t);
+    }
+    u32 ex = REV ? __shfl_down(incl, 1) : __shfl_up(incl, 1);
+    if (REV ? lane == 63 : lane == 0) ex = ident;
+    if (REV ? lane == 0 : lane == 63) sh[w] = incl;
+    __syncthreads();
+    u32 carry = ident;
+    if (!REV) {
+        for (u32 i = 0; i < w; ++i) carry = op(carry, sh[i]);
+    } else {
+        for (u32 i = w + 1; i < WG / 64; ++i) carry = op(carry, sh[i]);
+    }
+    __syncthreads();
+    return op(carry, ex);
+}
+
+__device__ inline int size_class(u32 len) { return len <= 1 ? 0 : 32 - __clz(len - 1); }
+
+// ------------------------------------------------------------------------------------
+// keys
+// ------------------------------------------------------------------------------------
+__device__ inline u32 cyc_succ(const SortArgs& a, u32 p, u32 h) {
+    const u32 fs = a.FS[p], m = a.FL[p];
+    u32 hm = h < m ? h : h % m;
+    u32 t = (p - fs) + hm;
+    if (t >= m) t -= m;
+    return fs + t;
+}
+
+__device__ inline u32 make_key(const SortArgs& a, u32 p, u32 base, u32 end) {
+    if (a.initial) {
+        if (!a.cyclic) {
+            u32 c0 = (u32)a.text[p] + 1;
+            u32 c1 = p + 1 < end ? (u32)a.text[p + 1] + 1 : 0;
+            u32 c2 = p + 2 < end ? (u32)a.text[p + 2] + 1 : 0;
+            return (c0 << 18) | (c1 << 9) | c2;
+        }
+        const u32 fs = a.FS[p], m = a.FL[p];
+        u32 t = p - fs, k = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            k = (k << 8) | a.text[fs + t];
+            if (++t == m) t = 0;
+        }
+        return k;
+    }
+    if (!a.cyclic) {
+        const u32 q = p + a.h;
+        return q < end ? a.RK[q] - base + 1 : 0;
+    }
+    return a.RK[cyc_succ(a, p, a.h)] - base;
+}
+
+// ------------------------------------------------------------------------------------
+// setup kernels
+// ------------------------------------------------------------------------------------
+__global__ void k_iota(u32* SA, u32 N) {
+    for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) SA[i] = i;
+}
+
+__global__ void k_block_segs(Seg* segs, Geom geo) {
+    const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < geo.nb) segs[b] = Seg{geo.base(b), geo.end(b) - geo.base(b)};
+}
+
+__global__ void k_classify(const Seg* cur, u32 ncur, SortArgs a, Lists L, Level lv) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ncur) return;
+    const Seg s = cur[i];
+    if (a.cyclic && a.blk_done[a.geo.block_of(s.start)]) return;
+    atomicAdd(&L.misc[0], s.len);
+    if (s.len > (u32)TILE) {
+        const u32 nt = (s.len + TILE - 1) / TILE;
+        const u32 si = atomicAdd(lv.nseg, 1u);
+        const u32 tb = atomicAdd(lv.ntiles, nt);
+        lv.segs[si] = LSeg{s.start, s.len, tb, nt};
+        for (u32 k = 0; k < nt; ++k) lv.tiles[tb + k] = LTile{si, k};
+    } else {
+        const int c = size_class(s.len);
+        const u32 idx = atomicAdd(&L.cls_cnt[c], 1u);
+        L.cls[c][idx] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// key generation
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(WG) void k_keygen_small(const Seg* segs, u32 count, int c, SortArgs a) {
+    const u32 spt = TILE >> c;
+    const u32 first = blockIdx.x * spt;
+    const u32 mask = (1u << c) - 1;
+#pragma unroll
+    for (int j = 0; j < PER_THREAD; ++j) {
+        const u32 slot = j * WG + threadIdx.x;
+        const u32 si = first + (slot >> c);
+        const u32 k = slot & mask;
+        if (si >= count) continue;
+        const Seg s = segs[si];
+        if (k >= s.len) continue;
+        const u32 g = s.start + k;
+        const u32 b = a.geo.block_of(s.start);
+        a.K2[g] = make_key(a, a.SA[g], a.geo.base(b), a.geo.end(b));
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_keygen_large(const LTile* tiles, const LSeg* segs, SortArgs a) {
+    const LTile t = tiles[blockIdx.x];
+    const LSeg s = segs[t.seg];
+    const u32 base = s.start + t.k * TILE;
+    const u32 cnt = min((u32)TILE, s.start + s.len - base);
+    const u32 b = a.geo.block_of(s.start);
+    const u32 bb = a.geo.base(b), be = a.geo.end(b);
+#pragma unroll
+    for (int j = 0; j < PER_THREAD; ++j) {
+        const u32 e = j * WG + threadIdx.x;
+        if (e < cnt) a.K2[base + e] = make_key(a, a.SA[base + e], bb, be);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// MSD radix passes for segments longer than a tile
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(WG) void k_msd_hist(const LTile* tiles, const LSeg* segs, SortArgs a,
+                                                 u32 shift, u32 mask, u32* hist) {
+    __shared__ u32 h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const LTile t = tiles[blockIdx.x];
+    const LSeg s = segs[t.seg];
+    const u32 base = s.start + t.k * TILE;
+    const u32 cnt = min((u32)TILE, s.start + s.len - base);
+#pragma unroll
+    for (int j = 0; j < PER_THREAD; ++j) {
+        const u32 e = j * WG + threadIdx.x;
+        if (e < cnt) atomicAdd(&h[(a.K2[base + e] >> shift) & mask], 1u);
+    }
+    __syncthreads();
+    hist[(u64)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
+}
+
+// One workgroup per segment: per-digit running offsets over the segment's tiles, bucket
+// starts, and classification of the buckets (small -> class list, large -> next level,
+// large after the last digit -> equal-key run).
+__global__ __launch_bounds__(WG) void k_msd_scan(const LSeg* segs, SortArgs a, u32* hist, int last_level,
+                                                 Lists L, Level nx) {
+    __shared__ u32 sh[WG / 64];
+    const LSeg s = segs[blockIdx.x];
+    const u32 d = threadIdx.x;
+    u32 run = 0;
+    for (u32 t = s.tile_base; t < s.tile_base + s.ntiles; ++t) {
+        const u64 ix = (u64)t * 256 + d;
+        const u32 v = hist[ix];
+        hist[ix] = run;
+        run += v;
+    }
+    const u32 bstart = wg_excl_scan<false>(run, OpAdd(), 0u, sh);
+    const u32 abs0 = s.start + bstart;
+    for (u32 t = s.tile_base; t < s.tile_base + s.ntiles; ++t) hist[(u64)t * 256 + d] += abs0;
+    const int nonzero = __syncthreads_count(run > 0);
+    if (nonzero > 1 && d == 0) a.blk_split[a.geo.block_of(s.start)] = 1;
+    if (run == 0) return;
+    const Seg sub{abs0, run};
+    if (run <= (u32)TILE) {
+        const int c = size_class(run);
+        L.cls[c][atomicAdd(&L.cls_cnt[c], 1u)] = sub;
+    } else if (!last_level) {
+        const u32 nt = (run + TILE - 1) / TILE;
+        const u32 si = atomicAdd(nx.nseg, 1u);
+        const u32 tb = atomicAdd(nx.ntiles, nt);
+        nx.segs[si] = LSeg{sub.start, sub.len, tb, nt};
+        for (u32 k = 0; k < nt; ++k) nx.tiles[tb + k] = LTile{si, k};
+    } else {
+        L.eq[atomicAdd(L.eq_cnt, 1u)] = sub;
+    }
+}
+
+// Stable scatter of one tile by digit: element order inside the tile is e = j*WG + tid,
+// each wave ranks its 64 elements per digit with ballots; per-wave digit counts are
+// combined through LDS in (j, wave) order, so equal digits keep their tile order.
+__global__ __launch_bounds__(WG) void k_msd_scatter(const LTile* tiles, const LSeg* segs, SortArgs a,
+                                                    u32 shift, u32 width, const u32* hist) {
+    __shared__ u32 wcnt[WG / 64][256];
+    __shared__ u32 running[256];
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const LTile t = tiles[blockIdx.x];
+    const LSeg s = segs[t.seg];
+    const u32 base = s.start + t.k * TILE;
+    const u32 cnt = min((u32)TILE, s.start + s.len - base);
+    const u32 mask = (1u << width) - 1;
+    running[tid] = hist[(u64)blockIdx.x * 256 + tid];
+#pragma unroll
+    for (int i = 0; i < WG / 64; ++i) wcnt[i][tid] = 0;
+    __syncthreads();
+    const u64 lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int j = 0; j < PER_THREAD; ++j) {
+        const u32 e = j * WG + tid;
+        const bool valid = e < cnt;
+        u32 sa = 0, key = 0, dg = 0;
+        if (valid) {
+            sa = a.SA[base + e];
+            key = a.K2[base + e];
+            dg = (key >> shift) & mask;
+        }
+        u64 m = __ballot(valid);
+        for (u32 bit = 0; bit < width; ++bit) {
+            const u64 bal = __ballot((dg >> bit) & 1u);
+            m &= ((dg >> bit) & 1u) ? bal : ~bal;
+        }
+        const u32 rank = __popcll(m & lt_mask);
+        const bool leader = valid && rank == 0;
+        if (leader) wcnt[w][dg] = __popcll(m);
+        __syncthreads();
+        if (valid) {
+            u32 pre = running[dg];
+            for (u32 i = 0; i < w; ++i) pre += wcnt[i][dg];
+            const u32 dst = pre + rank;
+            a.SA2[dst] = sa;
+            a.K22[dst] = key;
+        }
+        __syncthreads();
+        u32 add = 0;
+#pragma unroll
+        for (int i = 0; i < WG / 64; ++i) {
+            add += wcnt[i][tid];
+            wcnt[i][tid] = 0;
+        }
+        running[tid] += add;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_copy_back(const LTile* tiles, const LSeg* segs, SortArgs a) {
+    const LTile t = tiles[blockIdx.x];
+    const LSeg s = segs[t.seg];
+    const u32 base = s.start + t.k * TILE;
+    const u32 cnt = min((u32)TILE, s.start + s.len - base);
+#pragma unroll
+    for (int j = 0; j < PER_THREAD; ++j) {
+        const u32 e = j * WG + threadIdx.x;
+        if (e < cnt) {
+            a.SA[base + e] = a.SA2[base + e];
+            a.K2[base + e] = a.K22[base + e];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// small segments: one tile = TILE/2^C segments, each padded to 2^C slots, sorted by
+// (key, position) with a bitonic network (distances >= 8 through LDS, < 8 in registers),
+// then split into runs of equal key: new groups.
+// ------------------------------------------------------------------------------------
+template <int J>
+__device__ inline void reg_stage(u64 (&r)[8], u32 tid, u32 k, u32 S) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        if (e & J) continue;
+        const u32 i = 8 * tid + e;
+        const bool up = (k == S) || ((i & k) == 0);
+        const u64 x = r[e], y = r[e + J];
+        const bool sw = (x > y) == up;
+        r[e] = sw ? y : x;
+        r[e + J] = sw ? x : y;
+    }
+}
+
+template <int C>
+__global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, SortArgs a, Lists L) {
+    constexpr u32 S = 1u << C;
+    constexpr u32 SPT = TILE / S;
+    __shared__ u64 sk[TILE];
+    __shared__ Seg ss[SPT];
+    __shared__ u32 sh[WG / 64];
+    __shared__ u32 last_hi[WG];
+    const u32 tid = threadIdx.x;
+    const u32 first = blockIdx.x * SPT;
+    const u32 nthis = min(SPT, count - first);
+    for (u32 i = tid; i < SPT; i += WG) ss[i] = i < nthis ? segs[first + i] : Seg{0, 0};
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER_THREAD; ++j) {
+        const u32 slot = j * WG + tid;
+        const u32 si = slot >> C, k = slot & (S - 1);
+        u64 key = ~0ull;
+        if (si < nthis && k < ss[si].len) {
+            const u32 g = ss[si].start + k;
+            key = ((u64)a.K2[g] << 32) | a.SA[g];
+        }
+        sk[slot] = key;
+    }
+    __syncthreads();
+    u64 r[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] = sk[8 * tid + e];
+    for (u32 k = 2; k <= S; k <<= 1) {
+        if (k > 8) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sk[8 * tid + e] = r[e];
+            __syncthreads();
+            for (u32 j = k >> 1; j >= 8; j >>= 1) {
+                const u32 lj = 31 - __clz(j);
+#pragma unroll
+                for (int q0 = 0; q0 < TILE / 2 / WG; ++q0) {
+                    const u32 q = q0 * WG + tid;
+                    const u32 i = ((q >> lj) << (lj + 1)) | (q & (j - 1));
+                    const u32 l = i + j;
+                    const bool up = (k == S) || ((i & k) == 0);
+                    const u64 x = sk[i], y = sk[l];
+                    if ((x > y) == up) {
+                        sk[i] = y;
+                        sk[l] = x;
+                    }
+                }
+                __syncthreads();
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) r[e] = sk[8 * tid + e];
+            __syncthreads();
+        }
+        if (k >= 8) reg_stage<4>(r, tid, k, S);
+        if (k >= 4) reg_stage<2>(r, tid, k, S);
+        reg_stage<1>(r, tid, k, S);
+    }
+    // runs of equal key inside each sub-array
+    last_hi[tid] = (u32)(r[7] >> 32);
+    const bool last_valid = r[7] != ~0ull;
+    __syncthreads();
+    bool valid[8], head[8], stop[8];
+    u32 prev_hi = tid ? last_hi[tid - 1] : 0;
+    bool prev_valid = tid ? true : false;
+    (void)last_valid;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const u32 i = 8 * tid + e;
+        const u32 kk = i & (S - 1);
+        valid[e] = r[e] != ~0ull;
+        const u32 hi = (u32)(r[e] >> 32);
+        head[e] = valid[e] && (kk == 0 || hi != prev_hi);
+        stop[e] = kk == 0 || head[e] || !valid[e];
+        prev_hi = hi;
+        (void)prev_valid;
+    }
+    // run start: inclusive max-scan of head indices
+    u32 loc[8];
+    u32 agg = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        if (head[e]) agg = 8 * tid + e;
+        loc[e] = agg;
+    }
+    const u32 carry = wg_excl_scan<false>(agg, OpMax(), 0u, sh);
+    u32 start_idx[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) start_idx[e] = loc[e] > carry ? loc[e] : carry;
+    // run end: exclusive suffix min of stop indices
+    u32 sagg = TILE;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+        if (stop[e] && (u32)(8 * tid + e) < sagg) sagg = 8 * tid + e;
+    const u32 scarry = wg_excl_scan<true>(sagg, OpMin(), (u32)TILE, sh);
+    u32 nxt[8];
+    u32 run_min = scarry;
+#pragma unroll
+    for (int e = 7; e >= 0; --e) {
+        nxt[e] = run_min;
+        if (stop[e]) run_min = 8 * tid + e;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        if (!valid[e]) continue;
+        const u32 i = 8 * tid + e;
+        const u32 si = i >> C, kk = i & (S - 1);
+        const Seg sg = ss[si];
+        const u32 pos = (u32)r[e];
+        a.SA[sg.start + kk] = pos;
+        a.RK[pos] = sg.start + (start_idx[e] - (si << C));
+        if (head[e]) {
+            const u32 len = nxt[e] - i;
+            if (len >= 2) L.next[atomicAdd(L.next_cnt, 1u)] = Seg{sg.start + kk, len};
+            if (kk > 0) a.blk_split[a.geo.block_of(sg.start)] = 1;
+        }
+    }
+}
+
+__global__ void k_single(const Seg* segs, u32 count, SortArgs a) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) {
+        const Seg s = segs[i];
+        a.RK[a.SA[s.start]] = s.start;
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_finalize_eq(const Seg* eq, SortArgs a, Lists L) {
+    const Seg s = eq[blockIdx.x];
+    for (u32 i = threadIdx.x; i < s.len; i += WG) a.RK[a.SA[s.start + i]] = s.start;
+    if (threadIdx.x == 0) L.next[atomicAdd(L.next_cnt, 1u)] = s;
+}
+
+__global__ void k_update_done(u32* done, const u32* split, u32 nb) {
+    const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nb && !split[b]) done[b] = 1;
+}
+
+// prev3[p] = previous position of the same 3-gram in p's block (NONE if none), read off
+// the linear SA right after round 0 (groups = 3-character classes, positions ascending).
+__global__ void k_prev3(SortArgs a, u32* prev3) {
+    const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= a.geo.N) return;
+    const u32 b = a.geo.block_of(g);
+    const u32 base = a.geo.base(b), end = a.geo.end(b);
+    const u32 p = a.SA[g];
+    u32 r = NONE;
+    if (p + 3 <= end && g > base) {
+        const u32 q = a.SA[g - 1];
+        if (a.RK[q] == a.RK[p]) r = q;
+    }
+    prev3[p] = r;
+}
+
+// ------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------
+static inline u32 cdiv(u64 a, u64 b) { return (u32)((a + b - 1) / b); }
+
+void launch_iota(u32* SA, u64 N, hipStream_t s) {
+    if (!N) return;
+    k_iota<<<std::min<u32>(cdiv(N, 256), 65535u), 256, 0, s>>>(SA, (u32)N);
+}
+void launch_block_segs(Seg* segs, const Geom& geo, hipStream_t s) {
+    if (geo.nb) k_block_segs<<<cdiv(geo.nb, 256), 256, 0, s>>>(segs, geo);
+}
+void launch_classify(const Seg* cur, u32 ncur, const SortArgs& a, const Lists& L, const Level& lv0,
+                     hipStream_t s) {
+    if (ncur) k_classify<<<cdiv(ncur, 256), 256, 0, s>>>(cur, ncur, a, L, lv0);
+}
+void launch_keygen_small(int c, const Seg* segs, u32 count, const SortArgs& a, hipStream_t s) {
+    if (count) k_keygen_small<<<cdiv(count, TILE >> c), WG, 0, s>>>(segs, count, c, a);
+}
+void launch_keygen_large(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
+                         hipStream_t s) {
+    if (ntiles) k_keygen_large<<<ntiles, WG, 0, s>>>(tiles, segs, a);
+}
+void launch_msd_hist(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a, u32 shift,
+                     u32 width, u32* hist, hipStream_t s) {
+    if (ntiles) k_msd_hist<<<ntiles, WG, 0, s>>>(tiles, segs, a, shift, (1u << width) - 1, hist);
+}
+void launch_msd_scan(const LSeg* segs, u32 nseg, const SortArgs& a, u32 width, u32* hist,
+                     bool last_level, const Lists& L, const Level& next, hipStream_t s) {
+    (void)width;
+    if (nseg) k_msd_scan<<<nseg, WG, 0, s>>>(segs, a, hist, last_level ? 1 : 0, L, next);
+}
+void launch_msd_scatter(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
+                        u32 shift, u32 width, const u32* hist, hipStream_t s) {
+    if (ntiles) k_msd_scatter<<<ntiles, WG, 0, s>>>(tiles, segs, a, shift, width, hist);
+}
+void launch_copy_back(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
+                      hipStream_t s) {
+    if (ntiles) k_copy_back<<<ntiles, WG, 0, s>>>(tiles, segs, a);
+}
+
+template <int C>
+static void small_sort_c(const Seg* segs, u32 count, const SortArgs& a, const Lists& L, hipStream_t s) {
+    k_small_sort<C><<<cdiv(count, TILE >> C), WG, 0, s>>>(segs, count, a, L);
+}
+
+void launch_small_sort(int c, const Seg* segs, u32 count, const SortArgs& a, const Lists& L,
+                       hipStream_t s) {
+    if (!count) return;
+    switch (c) {
+        case 0: k_single<<<cdiv(count, 256), 256, 0, s>>>(segs, count, a); break;
+        case 1: small_sort_c<1>(segs, count, a, L, s); break;
+        case 2: small_sort_c<2>(segs, count, a, L, s); break;
+        case 3: small_sort_c<3>(segs, count, a, L, s); break;
+        case 4: small_sort_c<4>(segs, count, a, L, s); break;
+        case 5: small_sort_c<5>(segs, count, a, L, s); break;
+        case 6: small_sort_c<6>(segs, count, a, L, s); break;
+        case 7: small_sort_c<7>(segs, count, a, L, s); break;
+        case 8: small_sort_c<8>(segs, count, a, L, s); break;
+        case 9: small_sort_c<9>(segs, count, a, L, s); break;
+        case 10: small_sort_c<10>(segs, count, a, L, s); break;
+        case 11: small_sort_c<11>(segs, count, a, L, s); break;
+        default: break;
+    }
+}
+void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists& L, hipStream_t s) {
+    if (count) k_finalize_eq<<<count, WG, 0, s>>>(eq, a, L);
+}
+void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, hipStream_t s) {
+    if (nb) k_update_done<<<cdiv(nb, 256), 256, 0, s>>>(blk_done, blk_split, nb);
+}
+void launch_prev3(const SortArgs& a, u32* prev3, hipStream_t s) {
+    if (a.geo.N) k_prev3<<<cdiv(a.geo.N, 256), 256, 0, s>>>(a, prev3);
+}
+
+}  // namespace kolm

@@ -1,0 +1,736 @@
+// libkolm_hip.so — host orchestration + C ABI (include/kolm.h).
+//
+// One kolm_ctx per device owns a HIP stream and grow-only device scratch.  A batch runs
+//   cheap sizes -> linear suffix sort (+ 3-gram chains) -> Lyndon factors -> cyclic
+//   suffix sort -> BBWT gather -> MTF -> Rice sizes (5 variants) -> LZ77 match/parse ->
+//   MDL argmin -> payload emission
+// entirely on the device; the host only reads small per-round counters (to size the
+// next launches) and the per-block results.  See DESIGN.md §2-§6.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/kolm.h"
+#include "kolm_internal.h"
+
+using namespace kolm;
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const std::string& s) { g_err = s; }
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+// counter slots in the device counter array
+enum : int {
+    C_CLS = 0,       // 12 slots
+    C_NEXT = 12,
+    C_EQ = 13,
+    C_ACTIVE = 14,
+    C_L0SEG = 16,
+    C_L0TILE = 17,
+    C_L1SEG = 18,
+    C_L1TILE = 19,
+    C_STATUS = 20,
+    C_NLONG = 21,
+    C_RICE = 22,
+    C_N = 32
+};
+
+}  // namespace
+
+struct kolm_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::map<std::string, DevBuf> bufs;
+    u32* h_cnt = nullptr;  // pinned mirror of the counters
+    hipEvent_t ev[8] = {};
+
+    void* raw(const char* name, size_t bytes) {
+        DevBuf& b = bufs[name];
+        if (bytes == 0) bytes = 16;
+        if (b.cap < bytes) {
+            if (b.p) KOLM_HIP_CHECK(hipFree(b.p));
+            b.p = nullptr;
+            const size_t cap = (bytes + 255) & ~(size_t)255;
+            KOLM_HIP_CHECK(hipMalloc(&b.p, cap));
+            b.cap = cap;
+        }
+        return b.p;
+    }
+    template <class T>
+    T* get(const char* name, size_t count) {
+        return static_cast<T*>(raw(name, count * sizeof(T)));
+    }
+    void sync() { KOLM_HIP_CHECK(hipStreamSynchronize(stream)); }
+};
+
+namespace {
+
+std::mutex g_mu;
+kolm_ctx* g_default = nullptr;
+
+u32 bitlen(u32 v) { return v ? 32 - __builtin_clz(v) : 0; }
+
+struct SortOut {
+    u32 rounds = 0;
+    u64 active = 0;
+};
+
+// Segmented prefix-doubling suffix sort of every block of the batch (k_sort.hip).
+SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, const u32* FS, const u32* FL,
+                  u32* prev3, bool round0_only) {
+    hipStream_t s = c->stream;
+    const u64 N = geo.N;
+    SortOut out;
+    SortArgs a{};
+    a.geo = geo;
+    a.text = text;
+    a.SA = c->get<u32>("SA", N);
+    a.RK = c->get<u32>("RK", N);
+    a.K2 = c->get<u32>("K2", N);
+    a.SA2 = c->get<u32>("SA2", N);
+    a.K22 = c->get<u32>("K22", N);
+    a.FS = FS;
+    a.FL = FL;
+    a.blk_split = c->get<u32>("blk_split", geo.nb);
+    u32* blk_done = c->get<u32>("blk_done", geo.nb);
+    a.blk_done = blk_done;
+    a.cyclic = cyclic ? 1 : 0;
+
+    u32* cnt = c->get<u32>("counters", C_N);
+    Lists L{};
+    for (int k = 0; k < NCLASS; ++k) {
+        const u64 cap = (k == 0 ? N : N / ((1ull << (k - 1)) + 1)) + 16;
+        char nm[16];
+        snprintf(nm, sizeof nm, "cls%d", k);
+        L.cls[k] = c->get<Seg>(nm, cap);
+    }
+    L.cls_cnt = cnt + C_CLS;
+    L.next_cnt = cnt + C_NEXT;
+    L.eq_cnt = cnt + C_EQ;
+    L.misc = cnt + C_ACTIVE;
+    L.eq = c->get<Seg>("eq", N / TILE + 16);
+    const u64 seg_cap = N / 2 + geo.nb + 16;
+    Seg* segA = c->get<Seg>("segA", seg_cap);
+    Seg* segB = c->get<Seg>("segB", seg_cap);
+    const u64 lseg_cap = N / TILE + 16;
+    const u64 ltile_cap = 2 * (N / TILE) + 16;
+    Level lv[2];
+    lv[0] = Level{c->get<LSeg>("lseg0", lseg_cap), cnt + C_L0SEG, c->get<LTile>("ltile0", ltile_cap), cnt + C_L0TILE};
+    lv[1] = Level{c->get<LSeg>("lseg1", lseg_cap), cnt + C_L1SEG, c->get<LTile>("ltile1", ltile_cap), cnt + C_L1TILE};
+    u32* hist = c->get<u32>("hist", ltile_cap * 256);
+
+    launch_iota(a.SA, N, s);
+    launch_block_segs(segA, geo, s);
+    KOLM_HIP_CHECK(hipMemsetAsync(blk_done, 0, sizeof(u32) * geo.nb, s));
+    Seg* cur = segA;
+    Seg* nxt = segB;
+    u32 ncur = geo.nb;
+    const u32 h0 = cyclic ? 4 : 3;
+    const u32 kb_rank = bitlen(geo.bs) ? bitlen(geo.bs) : 1;
+    u32* h = c->h_cnt;
+    for (u32 round = 0; round < 64 && ncur; ++round) {
+        a.initial = round == 0 ? 1 : 0;
+        a.h = round == 0 ? 0u : (h0 << (round - 1));
+        L.next = nxt;
+        KOLM_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(u32) * C_STATUS, s));
+        KOLM_HIP_CHECK(hipMemsetAsync(a.blk_split, 0, sizeof(u32) * geo.nb, s));
+        launch_classify(cur, ncur, a, L, lv[0], s);
+        KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
+        c->sync();
+        if (h[C_ACTIVE] == 0) break;
+        out.active += h[C_ACTIVE];
+        out.rounds = round + 1;
+        for (int k = 1; k < NCLASS; ++k) launch_keygen_small(k, L.cls[k], h[C_CLS + k], a, s);
+        launch_keygen_large(lv[0].tiles, h[C_L0TILE], lv[0].segs, a, s);
+        u32 nseg = h[C_L0SEG], ntiles = h[C_L0TILE];
+        u32 hi = a.initial ? (cyclic ? 32u : 27u) : kb_rank;
+        int lvl = 0;
+        while (nseg) {
+            const u32 width = std::min<u32>(8, hi);
+            const u32 shift = hi - width;
+            const bool last = shift == 0;
+            Level& lc = lv[lvl & 1];
+            Level& ln = lv[(lvl + 1) & 1];
+            KOLM_HIP_CHECK(hipMemsetAsync(ln.nseg, 0, sizeof(u32), s));
+            KOLM_HIP_CHECK(hipMemsetAsync(ln.ntiles, 0, sizeof(u32), s));
+            launch_msd_hist(lc.tiles, ntiles, lc.segs, a, shift, width, hist, s);
+            launch_msd_scan(lc.segs, nseg, a, width, hist, last, L, ln, s);
+            launch_msd_scatter(lc.tiles, ntiles, lc.segs, a, shift, width, hist, s);
+            launch_copy_back(lc.tiles, ntiles, lc.segs, a, s);
+            KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
+            c->sync();
+            nseg = *(ln.nseg == cnt + C_L0SEG ? &h[C_L0SEG] : &h[C_L1SEG]);
+            ntiles = *(ln.ntiles == cnt + C_L0TILE ? &h[C_L0TILE] : &h[C_L1TILE]);
+            hi = shift;
+            ++lvl;
+        }
+        KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
+        c->sync();
+        for (int k = 0; k < NCLASS; ++k) launch_small_sort(k, L.cls[k], h[C_CLS + k], a, L, s);
+        launch_finalize_eq(L.eq, h[C_EQ], a, L, s);
+        if (cyclic) launch_update_done(blk_done, a.blk_split, geo.nb, s);
+        if (!cyclic && round == 0 && prev3) launch_prev3(a, prev3, s);
+        KOLM_HIP_CHECK(hipMemcpyAsync(h + C_NEXT, cnt + C_NEXT, sizeof(u32), hipMemcpyDeviceToHost, s));
+        c->sync();
+        ncur = h[C_NEXT];
+        std::swap(cur, nxt);
+        if (round0_only) break;
+    }
+    return out;
+}
+
+struct Pipeline {
+    kolm_ctx* c;
+    Geom geo;
+    const u8* text;
+    kolm_stats st{};
+    float t_sa = 0, t_lz = 0, t_ent = 0, t_emit = 0;
+
+    // BBWT of every block into "bbwt"; prev3 chains into "prev3"
+    u8* bbwt() {
+        const u64 N = geo.N;
+        u32* prev3 = c->get<u32>("prev3", N);
+        u32* FS = c->get<u32>("FS", N);
+        u32* FL = c->get<u32>("FL", N);
+        u8* flag = c->get<u8>("flag", N);
+        const u64 ntiles = (u64)((geo.bs + TILE - 1) / TILE) * geo.nb + 16;
+        u32* t1 = c->get<u32>("tile_tmp", 2 * ntiles + 16);
+        u32* t2 = c->get<u32>("tile_tmp2", 2 * ntiles + 2 * geo.nb + 16);
+        SortOut lin = sort_pass(c, geo, text, false, nullptr, nullptr, prev3, false);
+        launch_lyndon(geo, c->get<u32>("RK", N), flag, FS, FL, t1, t2, c->stream);
+        SortOut cyc = sort_pass(c, geo, text, true, FS, FL, nullptr, false);
+        u8* out = c->get<u8>("bbwt", N);
+        launch_bbwt_gather(geo, text, c->get<u32>("SA", N), FS, FL, out, c->stream);
+        st.lin_rounds = lin.rounds;
+        st.cyc_rounds = cyc.rounds;
+        st.lin_active = lin.active;
+        st.cyc_active = cyc.active;
+        return out;
+    }
+
+    u8* mtf(const u8* in) {
+        const u64 N = geo.N;
+        const u64 nch = (u64)((geo.bs + MTF_CHUNK - 1) / MTF_CHUNK) * geo.nb + 1;
+        u8* out = c->get<u8>("mtf", N);
+        launch_mtf(geo, in, out, c->get<u8>("mtf_sum", nch * 256), c->get<u16>("mtf_cnt", nch),
+                   c->get<u8>("mtf_states", nch * 256), c->stream);
+        return out;
+    }
+
+    LzArgs lz_args() {
+        const u64 N = geo.N;
+        LzArgs z{};
+        z.geo = geo;
+        z.text = text;
+        z.prev3 = c->get<u32>("prev3", N);
+        z.Lc = c->get<u8>("lz_L", N);
+        z.Dc = c->get<u16>("lz_D", N);
+        z.tok_pos = c->get<u32>("tok_pos", N);
+        z.tok_len = c->get<u32>("tok_len", N);
+        z.tok_dist = c->get<u32>("tok_dist", N);
+        z.tok_off = c->get<u32>("tok_off", N);
+        z.ntok = c->get<u32>("ntok", geo.nb);
+        z.lz_size = c->get<u32>("lz_size", geo.nb);
+        z.nlong = c->get<u32>("counters", C_N) + C_NLONG;
+        return z;
+    }
+
+    void lz(const LzArgs& z) {
+        KOLM_HIP_CHECK(hipMemsetAsync(z.nlong, 0, sizeof(u32), c->stream));
+        launch_lz_match(z, c->stream);
+        launch_lz_parse(z, c->stream);
+    }
+};
+
+float ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0;
+    KOLM_HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+    return ms;
+}
+
+int check_geom(u64 N, u32 bs) {
+    if (N >= (1ull << 31)) {
+        set_err("batch larger than 2^31-1 bytes");
+        return KOLM_EARG;
+    }
+    if (bs == 0 || bs > (1u << 25)) {
+        set_err("block size must be in [1, 32 MiB]");
+        return KOLM_EARG;
+    }
+    return KOLM_OK;
+}
+
+// Full batch: sizes of candidates 0..8, MDL, emission into d_arena.
+int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const int32_t* h_force, u8* d_arena,
+                 u64 arena_cap, u32* h_sizes, u32* h_method, u64* h_off, kolm_stats* stats) {
+    if (int e = check_geom(N, bs)) return e;
+    Geom geo;
+    geom_init(geo, N, bs);
+    const u32 nb = geo.nb;
+    if (nb == 0) {
+        if (h_off) h_off[0] = 0;
+        if (stats) *stats = kolm_stats{};
+        return KOLM_OK;
+    }
+    hipStream_t s = c->stream;
+    Pipeline P{c, geo, d_text};
+    hipEvent_t* ev = c->ev;
+    KOLM_HIP_CHECK(hipEventRecord(ev[0], s));
+    u8* bw = P.bbwt();
+    KOLM_HIP_CHECK(hipEventRecord(ev[1], s));
+    u8* mt = P.mtf(bw);
+    EmitArgs e{};
+    e.geo = geo;
+    e.text = d_text;
+    e.mtf = mt;
+    e.sizes = c->get<u32>("sizes", (u64)nb * KOLM_NCAND);
+    e.bits = c->get<u64>("bits", (u64)nb * 8);
+    e.method = c->get<u32>("method", nb);
+    int32_t* d_force = nullptr;
+    if (h_force) {
+        d_force = c->get<int32_t>("force", nb);
+        KOLM_HIP_CHECK(hipMemcpyAsync(d_force, h_force, sizeof(int32_t) * nb, hipMemcpyHostToDevice, s));
+    }
+    e.force = d_force;
+    e.cand_mask = mask;
+    e.off = c->get<u64>("off", nb + 1);
+    e.arena = d_arena;
+    e.arena_cap = arena_cap;
+    const u64 ntiles = (u64)((geo.bs + TILE - 1) / TILE) * nb + 16;
+    e.tile_tmp = c->get<u32>("tile_tmp", 2 * ntiles + 16);
+    e.tile_tmp2 = c->get<u32>("tile_tmp2", 2 * ntiles + 2 * nb + 16);
+    e.rice_k = 2;
+    launch_cheap_and_rice_sizes(e, s);
+    KOLM_HIP_CHECK(hipEventRecord(ev[2], s));
+    LzArgs z = P.lz_args();
+    const bool want_lz = (mask >> KOLM_M_LZ77) & 1u || (h_force != nullptr);
+    if (want_lz) P.lz(z);
+    KOLM_HIP_CHECK(hipEventRecord(ev[3], s));
+    u32* cnt = c->get<u32>("counters", C_N);
+    KOLM_HIP_CHECK(hipMemsetAsync(cnt + C_STATUS, 0, sizeof(u32), s));
+    launch_mdl(e, want_lz ? z.lz_size : nullptr, cnt + C_STATUS, s);
+    std::vector<u64> off(nb + 1);
+    KOLM_HIP_CHECK(hipMemcpyAsync(off.data(), e.off, sizeof(u64) * (nb + 1), hipMemcpyDeviceToHost, s));
+    KOLM_HIP_CHECK(hipMemcpyAsync(c->h_cnt, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
+    c->sync();
+    if (c->h_cnt[C_STATUS] || off[nb] + 4 > arena_cap) {
+        set_err("payload arena too small");
+        return KOLM_ECAP;
+    }
+    KOLM_HIP_CHECK(hipMemsetAsync(d_arena, 0, (off[nb] + 8) & ~(u64)3, s));
+    launch_emit_simple(e, s);
+    launch_emit_rice(e, s);
+    if (want_lz) launch_lz_emit(z, e.method, e.off, d_arena, s);
+    KOLM_HIP_CHECK(hipEventRecord(ev[4], s));
+    if (h_sizes)
+        KOLM_HIP_CHECK(hipMemcpyAsync(h_sizes, e.sizes, sizeof(u32) * nb * KOLM_NCAND, hipMemcpyDeviceToHost, s));
+    if (h_method) KOLM_HIP_CHECK(hipMemcpyAsync(h_method, e.method, sizeof(u32) * nb, hipMemcpyDeviceToHost, s));
+    KOLM_HIP_CHECK(hipMemcpyAsync(c->h_cnt, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
+    c->sync();
+    if (h_off) std::memcpy(h_off, off.data(), sizeof(u64) * (nb + 1));
+    if (stats) {
+        kolm_stats& st = *stats;
+        st = P.st;
+        st.lz_long = c->h_cnt[C_NLONG];
+        st.ms_sa = ev_ms(ev[0], ev[1]);
+        st.ms_entropy = ev_ms(ev[1], ev[2]);
+        st.ms_lz = ev_ms(ev[2], ev[3]);
+        st.ms_emit = ev_ms(ev[3], ev[4]);
+        st.ms_total = ev_ms(ev[0], ev[4]);
+    }
+    return KOLM_OK;
+}
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const HipError& e) {
+        char buf[256];
+        snprintf(buf, sizeof buf, "HIP error %d (%s) at kolm_api line %d: %s", (int)e.err,
+                 hipGetErrorString(e.err), e.line, e.what);
+        set_err(buf);
+        return KOLM_EHIP;
+    } catch (const std::bad_alloc&) {
+        set_err("host allocation failed");
+        return KOLM_EHIP;
+    }
+}
+
+int ctx_create(int device, kolm_ctx** out) {
+    return guarded([&] {
+        int n = 0;
+        KOLM_HIP_CHECK(hipGetDeviceCount(&n));
+        if (device < 0 || device >= n) {
+            set_err("no such HIP device");
+            return KOLM_EARG;
+        }
+        KOLM_HIP_CHECK(hipSetDevice(device));
+        std::unique_ptr<kolm_ctx> c(new kolm_ctx);
+        c->device = device;
+        KOLM_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_cnt, sizeof(u32) * C_N, hipHostMallocDefault));
+        for (auto& e : c->ev) KOLM_HIP_CHECK(hipEventCreate(&e));
+        *out = c.release();
+        return KOLM_OK;
+    });
+}
+
+kolm_ctx* need_default() {
+    std::lock_guard<std::mutex> g(g_mu);
+    return g_default;
+}
+
+// Upload n host bytes to the context's "text" buffer (+8 bytes of zero padding).
+u8* upload(kolm_ctx* c, const uint8_t* in, size_t n) {
+    u8* d = c->get<u8>("text", n + 64);
+    if (n) KOLM_HIP_CHECK(hipMemcpyAsync(d, in, n, hipMemcpyHostToDevice, c->stream));
+    KOLM_HIP_CHECK(hipMemsetAsync(d + n, 0, 64, c->stream));
+    return d;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* kolm_last_error(void) { return g_err.c_str(); }
+
+int kolm_device_count(int* count) {
+    if (!count) return KOLM_EARG;
+    return guarded([&] {
+        KOLM_HIP_CHECK(hipGetDeviceCount(count));
+        return KOLM_OK;
+    });
+}
+
+int kolm_ctx_create(int device, kolm_ctx** out) {
+    if (!out) return KOLM_EARG;
+    return ctx_create(device, out);
+}
+
+int kolm_ctx_destroy(kolm_ctx* c) {
+    if (!c) return KOLM_EARG;
+    return guarded([&] {
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        KOLM_HIP_CHECK(hipStreamSynchronize(c->stream));
+        for (auto& kv : c->bufs)
+            if (kv.second.p) KOLM_HIP_CHECK(hipFree(kv.second.p));
+        for (auto& e : c->ev) KOLM_HIP_CHECK(hipEventDestroy(e));
+        KOLM_HIP_CHECK(hipHostFree(c->h_cnt));
+        KOLM_HIP_CHECK(hipStreamDestroy(c->stream));
+        delete c;
+        return KOLM_OK;
+    });
+}
+
+int kolm_init(int device) {
+    std::lock_guard<std::mutex> g(g_mu);
+    if (g_default) return KOLM_OK;
+    return ctx_create(device, &g_default);
+}
+
+int kolm_shutdown(void) {
+    std::lock_guard<std::mutex> g(g_mu);
+    if (!g_default) return KOLM_OK;
+    int r = kolm_ctx_destroy(g_default);
+    g_default = nullptr;
+    return r;
+}
+
+int kolm_ctx_reserve(kolm_ctx* c, uint64_t total_bytes, uint32_t max_block) {
+    (void)max_block;
+    if (!c) return KOLM_EARG;
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        c->get<u8>("text", total_bytes + 64);
+        return KOLM_OK;
+    });
+}
+
+int kolm_dev_alloc(kolm_ctx* c, uint64_t bytes, void** dptr) {
+    if (!c || !dptr) return KOLM_EARG;
+    return guarded([&] {
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        KOLM_HIP_CHECK(hipMalloc(dptr, bytes ? bytes : 16));
+        return KOLM_OK;
+    });
+}
+
+int kolm_dev_free(kolm_ctx* c, void* dptr) {
+    if (!c) return KOLM_EARG;
+    return guarded([&] {
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        KOLM_HIP_CHECK(hipFree(dptr));
+        return KOLM_OK;
+    });
+}
+
+int kolm_memcpy_h2d(kolm_ctx* c, void* dst, const void* src, uint64_t bytes) {
+    if (!c) return KOLM_EARG;
+    return guarded([&] {
+        KOLM_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+        c->sync();
+        return KOLM_OK;
+    });
+}
+
+int kolm_memcpy_d2h(kolm_ctx* c, void* dst, const void* src, uint64_t bytes) {
+    if (!c) return KOLM_EARG;
+    return guarded([&] {
+        KOLM_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        return KOLM_OK;
+    });
+}
+
+int kolm_ctx_sync(kolm_ctx* c) {
+    if (!c) return KOLM_EARG;
+    return guarded([&] {
+        c->sync();
+        return KOLM_OK;
+    });
+}
+
+int kolm_encode_blocks_device(kolm_ctx* c, const uint8_t* d_data, uint64_t total, uint32_t block_size,
+                              uint32_t cand_mask, const int32_t* force_method, uint8_t* d_arena,
+                              uint64_t arena_cap, uint32_t* h_sizes, uint32_t* h_method, uint64_t* h_off,
+                              kolm_stats* stats) {
+    if (!c || (!d_data && total) || !d_arena) return KOLM_EARG;
+    if ((cand_mask & KOLM_DEFAULT_MASK) == 0) return KOLM_EARG;
+    if (reinterpret_cast<uintptr_t>(d_arena) & 3) {
+        set_err("device arena must be 4-byte aligned");
+        return KOLM_EARG;
+    }
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        return encode_batch(c, d_data, total, block_size, cand_mask & KOLM_DEFAULT_MASK, force_method, d_arena,
+                            arena_cap, h_sizes, h_method, h_off, stats);
+    });
+}
+
+int kolm_encode_blocks(const uint8_t* data, const uint64_t* starts, const uint32_t* lens, uint32_t nblocks,
+                       uint32_t cand_mask, const int32_t* force_method, uint32_t* sizes, uint32_t* method,
+                       uint8_t* payload_arena, uint64_t arena_cap, uint64_t* payload_off, kolm_stats* stats) {
+    kolm_ctx* c = need_default();
+    if (!c) return KOLM_ENOINIT;
+    if (nblocks && (!data || !starts || !lens)) return KOLM_EARG;
+    if (!payload_off) return KOLM_EARG;
+    if ((cand_mask & KOLM_DEFAULT_MASK) == 0) return KOLM_EARG;
+    // fixed chunking only: starts[i] = i*bs, lens[i] = bs except the last
+    uint64_t total = 0;
+    const uint32_t bs = nblocks ? lens[0] : 1;
+    for (uint32_t i = 0; i < nblocks; ++i) {
+        if (starts[i] != (uint64_t)i * bs || lens[i] == 0 || (i + 1 < nblocks && lens[i] != bs) || lens[i] > bs) {
+            set_err("kolm_encode_blocks: blocks must be fixed-size and contiguous");
+            return KOLM_EARG;
+        }
+        total += lens[i];
+    }
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        if (int e = check_geom(total, bs)) return e;
+        u8* d = upload(c, data, total);
+        const bool has_raw = cand_mask & 1u;
+        const u64 dcap = (has_raw ? total : 9 * total) + 64 * (u64)nblocks + 256;
+        u8* arena = c->get<u8>("arena", dcap);
+        std::vector<u64> off(nblocks + 1);
+        int r = encode_batch(c, d, total, bs, cand_mask & KOLM_DEFAULT_MASK, force_method, arena, dcap, sizes,
+                             method, off.data(), stats);
+        if (r) return r;
+        if (off[nblocks] > arena_cap) {
+            set_err("payload_arena too small");
+            return KOLM_ECAP;
+        }
+        if (off[nblocks]) {
+            KOLM_HIP_CHECK(hipMemcpyAsync(payload_arena, arena, off[nblocks], hipMemcpyDeviceToHost, c->stream));
+            c->sync();
+        }
+        std::memcpy(payload_off, off.data(), sizeof(u64) * (nblocks + 1));
+        return KOLM_OK;
+    });
+}
+
+int kolm_bbwt_forward(const uint8_t* in, size_t n, uint8_t* out) {
+    kolm_ctx* c = need_default();
+    if (!c) return KOLM_ENOINIT;
+    if ((n && (!in || !out))) return KOLM_EARG;
+    if (n == 0) return KOLM_OK;
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        if (int e = check_geom(n, (u32)n)) return e;
+        Geom geo;
+        geom_init(geo, n, (u32)n);
+        u8* d = upload(c, in, n);
+        Pipeline P{c, geo, d};
+        u8* bw = P.bbwt();
+        KOLM_HIP_CHECK(hipMemcpyAsync(out, bw, n, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        return KOLM_OK;
+    });
+}
+
+int kolm_mtf_encode(const uint8_t* in, size_t n, uint8_t* out) {
+    kolm_ctx* c = need_default();
+    if (!c) return KOLM_ENOINIT;
+    if ((n && (!in || !out))) return KOLM_EARG;
+    if (n == 0) return KOLM_OK;
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        if (int e = check_geom(n, (u32)n)) return e;
+        Geom geo;
+        geom_init(geo, n, (u32)n);
+        u8* d = upload(c, in, n);
+        Pipeline P{c, geo, d};
+        u8* m = P.mtf(d);
+        KOLM_HIP_CHECK(hipMemcpyAsync(out, m, n, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        return KOLM_OK;
+    });
+}
+
+static int rice_common(kolm_ctx* c, const Geom& geo, const u8* d_seq, int k, uint8_t* out, size_t cap,
+                       size_t* out_len) {
+    const u64 n = geo.N;
+    const u64 worst = (n * ((255u >> k) + 1 + k) + 7) / 8 + 64;
+    u8* dout = c->get<u8>("rice_out", worst + 64);
+    KOLM_HIP_CHECK(hipMemsetAsync(dout, 0, worst + 64, c->stream));
+    const u64 ntiles = (u64)((geo.bs + TILE - 1) / TILE) * geo.nb + 16;
+    u32* t1 = c->get<u32>("tile_tmp", 2 * ntiles + 16);
+    u32* t2 = c->get<u32>("tile_tmp2", 2 * ntiles + 2 * geo.nb + 16);
+    u32* cnt = c->get<u32>("counters", C_N);
+    launch_rice_only(geo, d_seq, k, dout, t1, t2, cnt + C_RICE, c->stream);
+    KOLM_HIP_CHECK(hipMemcpyAsync(c->h_cnt, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, c->stream));
+    c->sync();
+    const u32 sz = c->h_cnt[C_RICE];
+    if (out_len) *out_len = sz;
+    if (sz > cap) {
+        set_err("rice output capacity too small");
+        return KOLM_ECAP;
+    }
+    if (sz) {
+        KOLM_HIP_CHECK(hipMemcpyAsync(out, dout, sz, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+    }
+    return KOLM_OK;
+}
+
+int kolm_rice_encode(const uint8_t* in, size_t n, int k, uint8_t* out, size_t cap, size_t* out_len) {
+    kolm_ctx* c = need_default();
+    if (!c) return KOLM_ENOINIT;
+    if (k < 0 || k > 15 || (n && (!in || !out))) return KOLM_EARG;
+    if (n == 0) {
+        if (out_len) *out_len = 0;
+        return KOLM_OK;
+    }
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        if (int e = check_geom(n, (u32)n)) return e;
+        Geom geo;
+        geom_init(geo, n, (u32)n);
+        u8* d = upload(c, in, n);
+        return rice_common(c, geo, d, k, out, cap, out_len);
+    });
+}
+
+int kolm_bbwt_mtf_rice(const uint8_t* in, size_t n, int flags, int k, uint8_t* out, size_t cap,
+                       size_t* out_len) {
+    kolm_ctx* c = need_default();
+    if (!c) return KOLM_ENOINIT;
+    if (k < 0 || k > 15 || (n && (!in || !out))) return KOLM_EARG;
+    if (flags != 0 && flags != 1 && flags != 4 && flags != 8 && flags != 16) return KOLM_EARG;
+    if (n == 0) {
+        if (out_len) *out_len = 0;
+        return KOLM_OK;
+    }
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        if (int e = check_geom(n, (u32)n)) return e;
+        Geom geo;
+        geom_init(geo, n, (u32)n);
+        u8* d = upload(c, in, n);
+        Pipeline P{c, geo, d};
+        u8* m = P.mtf(P.bbwt());
+        if (flags == 0) return rice_common(c, geo, m, k, out, cap, out_len);
+        // bitwise variant through the batched path with a forced method
+        const int32_t force = flags == 1 ? 3 : flags == 4 ? 4 : flags == 8 ? 5 : 6;
+        if (k != 2) {
+            set_err("bitwise variants are only defined with k=2 in the batched path");
+            return KOLM_EARG;
+        }
+        const u64 dcap = 9 * n + 256;
+        u8* arena = c->get<u8>("arena", dcap);
+        std::vector<u64> off(2);
+        int r = encode_batch(c, d, n, (u32)n, KOLM_DEFAULT_MASK, &force, arena, dcap, nullptr, nullptr,
+                             off.data(), nullptr);
+        if (r) return r;
+        if (out_len) *out_len = off[1];
+        if (off[1] > cap) {
+            set_err("output capacity too small");
+            return KOLM_ECAP;
+        }
+        KOLM_HIP_CHECK(hipMemcpyAsync(out, arena, off[1], hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        return KOLM_OK;
+    });
+}
+
+int kolm_lz77_encode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
+    kolm_ctx* c = need_default();
+    if (!c) return KOLM_ENOINIT;
+    if (n && (!in || !out)) return KOLM_EARG;
+    if (n == 0) {
+        if (out_len) *out_len = 0;
+        return KOLM_OK;
+    }
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        if (int e = check_geom(n, (u32)n)) return e;
+        Geom geo;
+        geom_init(geo, n, (u32)n);
+        u8* d = upload(c, in, n);
+        Pipeline P{c, geo, d};
+        sort_pass(c, geo, d, false, nullptr, nullptr, c->get<u32>("prev3", n), true);
+        LzArgs z = P.lz_args();
+        P.lz(z);
+        u32 sz = 0;
+        KOLM_HIP_CHECK(hipMemcpyAsync(&sz, z.lz_size, sizeof(u32), hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        if (out_len) *out_len = sz;
+        if (sz > cap) {
+            set_err("lz77 output capacity too small");
+            return KOLM_ECAP;
+        }
+        u8* dout = c->get<u8>("lz_out", (u64)sz + 64);
+        u64* doff = c->get<u64>("lz_off", 2);
+        KOLM_HIP_CHECK(hipMemsetAsync(doff, 0, sizeof(u64) * 2, c->stream));
+        launch_lz_emit(z, nullptr, doff, dout, c->stream);
+        KOLM_HIP_CHECK(hipMemcpyAsync(out, dout, sz, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        return KOLM_OK;
+    });
+}
+
+}  // extern "C"

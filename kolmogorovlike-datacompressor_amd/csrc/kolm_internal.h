@@ -1,0 +1,193 @@
+// Internal declarations of libkolm_hip.so (MI355X / gfx950 only).
+//
+// Data layout in HBM for one batch: the batch is the concatenation
+// of nb fixed-size blocks (block b = global positions [b*bs, min((b+1)*bs, N))).
+// Global position g and global suffix-array index i share the same index space [0, N):
+// block b's suffix array occupies SA[b*bs .. b*bs+n_b).  All per-position arrays are
+// structure-of-arrays, u32 unless noted.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kolm {
+
+using u8 = uint8_t;
+using u16 = uint16_t;
+using u32 = uint32_t;
+using u64 = uint64_t;
+
+constexpr int TILE = 2048;        // elements per sort/scan tile (one 256-thread workgroup)
+constexpr int WG = 256;           // threads per workgroup
+constexpr int PER_THREAD = TILE / WG;
+constexpr int NCLASS = 12;        // small-segment size classes: len in (2^(c-1), 2^c], c = 0..11
+constexpr u32 NONE = 0xFFFFFFFFu;
+constexpr int LZ_WINDOW = 4096;   // PY:1723 WINDOW_MAX
+constexpr int LZ_MIN = 3;         // PY:1724 MIN_MATCH
+constexpr int LZ_CAP = 64;        // capped match length of the all-positions pass
+constexpr int MTF_CHUNK = 1024;   // bytes replayed per thread by the MTF kernel
+constexpr u32 NCAND = 9;          // candidate ids 0..8 computed on the device
+
+// Segment of the suffix array still to be refined: SA[start .. start+len).
+struct Seg {
+    u32 start;
+    u32 len;
+};
+// Segment that needs MSD radix passes (len > TILE), with its tile range.
+struct LSeg {
+    u32 start;
+    u32 len;
+    u32 tile_base;
+    u32 ntiles;
+};
+// One MSD tile: segment index in the level's LSeg list and tile number k within it.
+struct LTile {
+    u32 seg;
+    u32 k;
+};
+
+// Fixed-size block geometry of a batch + a fast u32 division by bs.
+struct Geom {
+    u64 N;        // total bytes (< 2^31)
+    u32 bs;       // block size
+    u32 nb;       // number of blocks
+    u64 magic;    // fastdiv: block_of(g) = g * magic >> shift, exact for g < 2^31
+    u32 shift;
+    __host__ __device__ inline u32 block_of(u32 g) const {
+        return (u32)(((u64)g * magic) >> shift);
+    }
+    __host__ __device__ inline u32 base(u32 b) const { return b * bs; }
+    __host__ __device__ inline u32 end(u32 b) const {
+        u64 e = (u64)(b + 1) * bs;
+        return (u32)(e < N ? e : N);
+    }
+};
+
+void geom_init(Geom& g, u64 N, u32 bs);
+
+// Everything the suffix-sorting kernels touch for one pass (linear or cyclic).
+struct SortArgs {
+    Geom geo;
+    const u8* text;
+    u32* SA;
+    u32* RK;
+    u32* K2;
+    u32* SA2;
+    u32* K22;
+    const u32* FS;     // cyclic: global start of the Lyndon factor of each position
+    const u32* FL;     // cyclic: length of that factor
+    u32* blk_split;    // [nb] set to 1 when a group of block b split this round
+    const u32* blk_done;  // [nb] cyclic: block converged (no further splits possible)
+    int cyclic;
+    int initial;       // round 0: keys are packed characters
+    u32 h;             // doubling offset of this round (round >= 1)
+};
+
+// Append-only lists written by the classify / MSD / small-sort kernels.
+struct Lists {
+    Seg* cls[NCLASS];      // small segments per class
+    u32* cls_cnt;          // [NCLASS]
+    u32* next_cnt;         // [1] segments for the next round
+    Seg* next;
+    u32* eq_cnt;           // [1] equal-key runs longer than TILE (finalised directly)
+    Seg* eq;
+    u32* misc;             // [8] counters: 0 active elements, 1 ...
+};
+
+struct Level {
+    LSeg* segs;
+    u32* nseg;       // device counter
+    LTile* tiles;
+    u32* ntiles;     // device counter
+};
+
+// ---- launchers (k_sort.hip) ----
+void launch_iota(u32* SA, u64 N, hipStream_t s);
+void launch_block_segs(Seg* segs, const Geom& geo, hipStream_t s);
+void launch_classify(const Seg* cur, u32 ncur, const SortArgs& a, const Lists& L, const Level& lv0,
+                     hipStream_t s);
+void launch_keygen_small(int c, const Seg* segs, u32 count, const SortArgs& a, hipStream_t s);
+void launch_keygen_large(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
+                         hipStream_t s);
+void launch_msd_hist(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
+                     u32 shift, u32 width, u32* hist, hipStream_t s);
+void launch_msd_scan(const LSeg* segs, u32 nseg, const SortArgs& a, u32 width, u32* hist,
+                     bool last_level, const Lists& L, const Level& next, hipStream_t s);
+void launch_msd_scatter(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
+                        u32 shift, u32 width, const u32* hist, hipStream_t s);
+void launch_copy_back(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
+                      hipStream_t s);
+void launch_small_sort(int c, const Seg* segs, u32 count, const SortArgs& a, const Lists& L,
+                       hipStream_t s);
+void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists& L, hipStream_t s);
+void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, hipStream_t s);
+void launch_prev3(const SortArgs& a, u32* prev3, hipStream_t s);
+
+// ---- k_blocks.hip: per-block scans, Lyndon factors, BBWT gather ----
+void launch_lyndon(const Geom& geo, const u32* RK, u8* flag, u32* FS, u32* FL, u32* tile_tmp,
+                   u32* tile_tmp2, hipStream_t s);
+void launch_bbwt_gather(const Geom& geo, const u8* text, const u32* SA, const u32* FS,
+                        const u32* FL, u8* out, hipStream_t s);
+
+// ---- k_mtf.hip ----
+void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summary_cnt, u8* states,
+                hipStream_t s);
+
+// ---- k_entropy.hip: cheap sizes, Rice sizes / emission, MDL, emission of simple models ----
+struct EmitArgs {
+    Geom geo;
+    const u8* text;
+    const u8* mtf;
+    u32* sizes;        // [nb * 9]
+    u64* bits;         // [nb * 8] scratch (bit counters)
+    u32* method;       // [nb]
+    const int32_t* force;  // [nb] or null
+    u32 cand_mask;
+    u64* off;          // [nb + 1] payload offsets
+    u8* arena;
+    u64 arena_cap;
+    u32* tile_tmp;     // per-tile scratch
+    u32* tile_tmp2;
+    int rice_k;
+};
+void launch_cheap_and_rice_sizes(const EmitArgs& e, hipStream_t s);
+void launch_mdl(const EmitArgs& e, const u32* lz_sizes, u32* status, hipStream_t s);
+void launch_emit_simple(const EmitArgs& e, hipStream_t s);
+void launch_emit_rice(const EmitArgs& e, hipStream_t s);
+void launch_rice_only(const Geom& geo, const u8* in, int k, u8* out, u32* tile_tmp, u32* tile_tmp2,
+                      u32* out_size, hipStream_t s);
+
+// ---- k_lz77.hip ----
+struct LzArgs {
+    Geom geo;
+    const u8* text;
+    const u32* prev3;
+    u8* Lc;            // capped match length (LZ_CAP = long)
+    u16* Dc;           // distance of the capped best match
+    u32* tok_pos;      // [N] token start positions (per block region)
+    u32* tok_len;      // [N] match length (0 = literal)
+    u32* tok_dist;
+    u32* tok_off;      // [N] output byte offset of each token within the block payload
+    u32* ntok;         // [nb]
+    u32* lz_size;      // [nb] stream size
+    u32* nlong;        // [1]
+};
+void launch_lz_match(const LzArgs& z, hipStream_t s);
+void launch_lz_parse(const LzArgs& z, hipStream_t s);
+void launch_lz_emit(const LzArgs& z, const u32* method, const u64* off, u8* arena, hipStream_t s);
+
+}  // namespace kolm
+
+#define KOLM_HIP_CHECK(x)                                              \
+    do {                                                               \
+        hipError_t e_ = (x);                                           \
+        if (e_ != hipSuccess) throw ::kolm::HipError(e_, #x, __LINE__); \
+    } while (0)
+
+namespace kolm {
+struct HipError {
+    hipError_t err;
+    const char* what;
+    int line;
+    HipError(hipError_t e, const char* w, int l) : err(e), what(w), line(l) {}
+};
+}  // namespace kolm

@@ -1,0 +1,232 @@
+"""kolm — MI355X-native block-transform hot path of KolmogorovLike-DataCompressor v2-2.
+
+Drop-in for the reference's block API (PY = final_researched/kolm_final_researched_v2-2.py):
+
+    compress_blocks_fixed(data, block_size=8192) -> bytes      PY:2332-2445
+    decompress(container) -> bytes                             PY:2451-2550
+    _select_encoders() / _select_decoders()                    PY:2152-2207
+    bbwt_forward, mtf_encode, rice_encode, encode_lz77,
+    encode_bbwt_mtf_rice, encode_raw, encode_xor,
+    encode_lfsr_predict, fixed_boundaries, uleb128_encode      (same names / meaning)
+
+Every encode-side computation of candidates 0..8 runs as hand-written HIP kernels on
+the GPU (libkolm_hip.so through ctypes, include/kolm.h); the per-block MDL loop of PY
+is one batched device call for all blocks.  There is no CPU fallback: without the
+library or a HIP device the encode functions raise ``KolmUnavailable``.
+
+Candidate ids are the reference's (the list index is the on-disk method id):
+0 raw, 1 xor, 2 bbwt, 3 bbwt_bp, 4 bbwt_nib, 5 bbwt_br, 6 bbwt_gray, 7 lz77,
+8 lfsr_pred, 9 repair, 10 v2_new.  v2_new always raises in PY (NameError)
+and is never selected; repair (9) is not offloaded yet — its registry
+entry raises like a failing reference encoder, so the MDL argmin runs over ids 0..8 with
+ids unchanged (containers stay decodable by the reference).
+"""
+from __future__ import annotations
+
+import struct
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+from . import _lib
+from ._lib import KolmError, KolmUnavailable  # noqa: F401
+from .container import (MODE_CDC, MODE_FIXED, read_container, uleb128_decode_stream,  # noqa: F401
+                        uleb128_encode, write_container)
+from .decode import decode_block
+
+__all__ = [
+    "compress_blocks_fixed", "decompress", "fixed_boundaries", "bbwt_forward", "mtf_encode",
+    "rice_encode", "encode_lz77", "encode_bbwt_mtf_rice", "encode_raw", "encode_xor",
+    "encode_lfsr_predict", "uleb128_encode", "uleb128_decode_stream", "CANDIDATE_NAMES",
+    "KolmUnavailable", "KolmError", "last_stats",
+]
+
+CANDIDATE_NAMES = ["raw", "xor", "bbwt", "bbwt_bp", "bbwt_nib", "bbwt_br", "bbwt_gray", "lz77",
+                   "lfsr_pred", "repair", "v2_new"]
+GPU_CANDIDATES = 9
+
+# CLI-style switches of the reference (PY:92-96); ids stay stable (CPP:3750-3775 semantics)
+G_NO_LZ77: bool = False
+G_ONLY_METHOD: Optional[str] = None
+
+_last_stats: Dict[str, Any] = {}
+
+
+def last_stats() -> Dict[str, Any]:
+    """Device statistics of the last batched call (rounds, active positions, ms per stage)."""
+    return dict(_last_stats)
+
+
+# ---------------------------------------------------------------------------
+# chunking
+# ---------------------------------------------------------------------------
+
+def fixed_boundaries(data: bytes, block_size: int = 8192) -> List[Tuple[int, int]]:
+    """PY:314-320 (no tail merge — the reference Python does not merge)."""
+    n = len(data)
+    if n == 0:
+        return []
+    if block_size <= 0:
+        raise ValueError("block_size must be positive")
+    return [(i, min(n, i + block_size)) for i in range(0, n, block_size)]
+
+
+# ---------------------------------------------------------------------------
+# kernel-level functions (GPU)
+# ---------------------------------------------------------------------------
+
+def bbwt_forward(s: bytes) -> bytes:
+    """Bijective BWT (PY:351-423) on the GPU."""
+    return _lib.bbwt_forward(bytes(s)) if s else b""
+
+
+def mtf_encode(data: bytes) -> List[int]:
+    """Move-to-front indices (PY:460-468) on the GPU."""
+    return list(_lib.mtf_encode(bytes(data))) if data else []
+
+
+def rice_encode(seq, k: int) -> bytes:
+    """Rice code of byte values (PY:1413-1421), byte padded, on the GPU."""
+    b = bytes(seq)
+    if any(v > 255 for v in b):  # bytes() already guarantees < 256
+        raise ValueError("rice_encode: values must be bytes")
+    if not 0 <= k <= 15:
+        raise ValueError("rice_encode: k must be in [0, 15]")
+    return _lib.rice_encode(b, k) if b else b""
+
+
+def encode_lz77(block: bytes) -> Tuple[bytes, Dict[str, Any]]:
+    """LZ77, 4 KiB window, ULEB tokens (PY:1711-1763) on the GPU."""
+    return (_lib.lz77_encode(bytes(block)) if block else b""), {}
+
+
+def encode_bbwt_mtf_rice(block: bytes, use_bitplane: bool = False, use_lfsr: bool = False,
+                         use_nibble: bool = False, use_bitrev: bool = False, use_gray: bool = False,
+                         rice_param: int = 2) -> Tuple[bytes, Dict[str, Any]]:
+    """BBWT -> MTF -> [one bitwise map] -> Rice (PY:2028-2073) on the GPU.
+
+    The reference applies the maps in the order bitplane, lfsr, nibble, bitrev, gray; the
+    candidates use at most one (PY:2156-2160), which is what the device path supports.
+    """
+    flags = (1 if use_bitplane else 0) | (2 if use_lfsr else 0) | (4 if use_nibble else 0) \
+        | (8 if use_bitrev else 0) | (16 if use_gray else 0)
+    if flags not in (0, 1, 4, 8, 16):
+        raise NotImplementedError("only single bitwise maps (the reference candidates) are offloaded")
+    n = len(block)
+    payload = _lib.bbwt_mtf_rice(bytes(block), flags, rice_param) if n else b""
+    length = 8 * ((n + 7) // 8) if flags & 1 else n
+    return payload, {"flags": flags, "k": rice_param, "length": length, "orig_len": n}
+
+
+def _batched_single(block: bytes, mid: int) -> bytes:
+    if not block:
+        return b""
+    _, _, payloads, _ = _lib.encode_blocks(bytes(block), len(block), force=[mid])
+    return payloads[0]
+
+
+def encode_raw(block: bytes) -> Tuple[bytes, Dict[str, Any]]:  # PY:2098
+    return bytes(block), {}
+
+
+def encode_xor(block: bytes) -> Tuple[bytes, Dict[str, Any]]:  # PY:2105-2111 (GPU emit)
+    return _batched_single(block, 1), {}
+
+
+def encode_lfsr_predict(block: bytes) -> Tuple[bytes, Dict[str, Any]]:  # PY:1984-2003 (GPU emit)
+    return _batched_single(block, 8), {}
+
+
+def _not_offloaded(block: bytes):
+    raise NotImplementedError("repair (method 9) is not offloaded yet (SURVEY §8f row 1)")
+
+
+def _v2_new(block: bytes):
+    raise NameError("v2_new raises in the reference (PY:1037-1043); never selected")
+
+
+def _select_encoders() -> List[Tuple[Callable[[bytes], Tuple[bytes, Dict[str, Any]]], str]]:
+    """Candidate registry (PY:2152-2178); list index = on-disk method id.  Unlike PY's
+    --only/--no-lz77 (which renumber and produce undecodable containers),
+    disabled candidates keep their ids (their entries raise and are skipped)."""
+    encs = [
+        (encode_raw, "raw"),
+        (encode_xor, "xor"),
+        (lambda b: encode_bbwt_mtf_rice(b, False, False, False, False, False, rice_param=2), "bbwt"),
+        (lambda b: encode_bbwt_mtf_rice(b, True, False, False, False, False, rice_param=2), "bbwt_bp"),
+        (lambda b: encode_bbwt_mtf_rice(b, False, False, True, False, False, rice_param=2), "bbwt_nib"),
+        (lambda b: encode_bbwt_mtf_rice(b, False, False, False, True, False, rice_param=2), "bbwt_br"),
+        (lambda b: encode_bbwt_mtf_rice(b, False, False, False, False, True, rice_param=2), "bbwt_gray"),
+        (encode_lz77, "lz77"),
+        (encode_lfsr_predict, "lfsr_pred"),
+        (_not_offloaded, "repair"),
+        (_v2_new, "v2_new"),
+    ]
+    mask = candidate_mask()
+
+    def disabled(_b):
+        raise RuntimeError("candidate disabled")
+
+    return [(e if (i < GPU_CANDIDATES and (mask >> i) & 1) or i >= GPU_CANDIDATES else disabled, n)
+            for i, (e, n) in enumerate(encs)]
+
+
+def _select_decoders():
+    """Decoder registry aligned with the encoder ids (PY:2194-2207)."""
+    return [(lambda payload, n, meta=None, _m=m: decode_block(_m, payload, n)) for m in range(10)]
+
+
+def candidate_mask() -> int:
+    mask = _lib.KOLM_DEFAULT_MASK
+    if G_NO_LZ77:
+        mask &= ~(1 << 7)
+    if G_ONLY_METHOD is not None:
+        name = G_ONLY_METHOD.lower()
+        if name not in CANDIDATE_NAMES:
+            raise ValueError(f"--only={G_ONLY_METHOD} not found in candidates")
+        idx = CANDIDATE_NAMES.index(name)
+        if idx >= GPU_CANDIDATES:
+            raise ValueError(f"--only={G_ONLY_METHOD}: candidate not offloaded")
+        mask = 1 << idx
+    return mask
+
+
+# ---------------------------------------------------------------------------
+# block API
+# ---------------------------------------------------------------------------
+
+def encode_blocks(data: bytes, block_size: int, cand_mask: Optional[int] = None):
+    """Batched device MDL over fixed blocks: (method_ids, orig_lens, payloads, sizes)."""
+    if block_size <= 0:
+        raise ValueError("block_size must be positive")
+    global _last_stats
+    mask = candidate_mask() if cand_mask is None else cand_mask
+    n = len(data)
+    if n == 0:
+        return [], [], [], None
+    sizes, method, payloads, st = _lib.encode_blocks(bytes(data), block_size, mask)
+    _last_stats = st
+    orig = [min(block_size, n - i) for i in range(0, n, block_size)]
+    return [int(m) for m in method], orig, payloads, sizes
+
+
+def compress_blocks_fixed(data: bytes, block_size: int = 8192) -> bytes:
+    """Fixed-size chunking + per-block MDL selection + KOLR container (PY:2332-2445)."""
+    if block_size <= 0:
+        raise ValueError("block_size must be positive")
+    n = len(data)
+    nb = (n + block_size - 1) // block_size
+    if nb > 0xFFFF:
+        raise struct.error("'H' format requires 0 <= number <= 65535")
+    mids, orig, payloads, _ = encode_blocks(data, block_size)
+    return write_container(MODE_FIXED, block_size, n, mids, orig, payloads)
+
+
+def decompress(container: bytes) -> bytes:
+    """Inverse of compress_blocks_fixed / the reference's containers (PY:2451-2550).
+    Host decoders (decode side is outside the offloaded hot path)."""
+    mode, size_field, total_len, mids, orig, payloads = read_container(container)
+    out = bytearray()
+    for mid, n, p in zip(mids, orig, payloads):
+        out += decode_block(mid, p, n)
+    if len(out) != total_len:
+        raise ValueError(f"Length mismatch: got {len(out)}, expect {total_len}")
+    return bytes(out)

@@ -1,0 +1,216 @@
+"""ctypes binding of libkolm_hip.so (C ABI declared in include/kolm.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no HIP device is
+visible, every GPU entry point raises ``KolmUnavailable`` (an ``ImportError`` subclass
+for the loader, ``RuntimeError`` for device problems).
+
+Note on HIP runtimes: PyTorch-ROCm ships its own ``libamdhip64.so.7``.  A process that
+uses both torch and this library must import torch first, so that both share torch's
+already-loaded runtime (same SONAME) — see ``kolm.parallel``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libkolm_hip.so")
+
+KOLM_NCAND = 9
+KOLM_DEFAULT_MASK = 0x1FF
+ERRORS = {-1: "bad argument", -2: "capacity too small", -3: "HIP error", -4: "collective error",
+          -5: "not initialised"}
+
+
+class KolmUnavailable(ImportError):
+    pass
+
+
+class KolmError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"kolm error {code} ({ERRORS.get(code, '?')}): {msg}")
+        self.code = code
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("lin_rounds", ctypes.c_uint32),
+        ("cyc_rounds", ctypes.c_uint32),
+        ("lin_active", ctypes.c_uint64),
+        ("cyc_active", ctypes.c_uint64),
+        ("lz_tokens", ctypes.c_uint64),
+        ("lz_long", ctypes.c_uint64),
+        ("ms_total", ctypes.c_double),
+        ("ms_sa", ctypes.c_double),
+        ("ms_lz", ctypes.c_double),
+        ("ms_entropy", ctypes.c_double),
+        ("ms_emit", ctypes.c_double),
+        ("ms_msd_scatter", ctypes.c_double),
+        ("n_msd_scatter", ctypes.c_uint32),
+        ("msd_scatter_elems", ctypes.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+_lock = threading.Lock()
+_inited_device = None
+
+# (name, restype, argtypes) of every symbol declared in include/kolm.h
+P = ctypes.c_void_p
+U8P = ctypes.c_char_p
+SZ = ctypes.c_size_t
+U32 = ctypes.c_uint32
+U64 = ctypes.c_uint64
+I32 = ctypes.c_int
+SIGNATURES = [
+    ("kolm_init", I32, [I32]),
+    ("kolm_shutdown", I32, []),
+    ("kolm_last_error", ctypes.c_char_p, []),
+    ("kolm_device_count", I32, [ctypes.POINTER(I32)]),
+    ("kolm_bbwt_forward", I32, [U8P, SZ, P]),
+    ("kolm_mtf_encode", I32, [U8P, SZ, P]),
+    ("kolm_rice_encode", I32, [U8P, SZ, I32, P, SZ, ctypes.POINTER(SZ)]),
+    ("kolm_lz77_encode", I32, [U8P, SZ, P, SZ, ctypes.POINTER(SZ)]),
+    ("kolm_bbwt_mtf_rice", I32, [U8P, SZ, I32, I32, P, SZ, ctypes.POINTER(SZ)]),
+    ("kolm_encode_blocks", I32, [U8P, P, P, U32, U32, P, P, P, P, U64, P, P]),
+    ("kolm_ctx_create", I32, [I32, ctypes.POINTER(P)]),
+    ("kolm_ctx_destroy", I32, [P]),
+    ("kolm_ctx_reserve", I32, [P, U64, U32]),
+    ("kolm_dev_alloc", I32, [P, U64, ctypes.POINTER(P)]),
+    ("kolm_dev_free", I32, [P, P]),
+    ("kolm_memcpy_h2d", I32, [P, P, P, U64]),
+    ("kolm_memcpy_d2h", I32, [P, P, P, U64]),
+    ("kolm_ctx_sync", I32, [P]),
+    ("kolm_encode_blocks_device", I32, [P, P, U64, U32, U32, P, P, U64, P, P, P, P]),
+]
+
+
+def load():
+    """Load libkolm_hip.so (raises KolmUnavailable when it is not built)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise KolmUnavailable(
+                    f"{LIB_PATH} not built: run `make -C kolmogorovlike-datacompressor_amd` "
+                    "or __graft_entry__.build() (there is no CPU fallback)")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, res, args in SIGNATURES:
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = load().kolm_last_error()
+        raise KolmError(rc, msg.decode() if msg else "")
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = load().kolm_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def ensure_init(device: int = None):
+    """Create the default context (device from $KOLM_DEVICE, else 0)."""
+    global _inited_device
+    if _inited_device is not None:
+        return _inited_device
+    if device is None:
+        device = int(os.environ.get("KOLM_DEVICE", "0"))
+    lib = load()
+    if device_count() <= 0:
+        raise KolmUnavailable("no HIP device visible: the kolm GPU path has no CPU fallback")
+    check(lib.kolm_init(device))
+    _inited_device = device
+    return device
+
+
+def _buf(n):
+    return ctypes.create_string_buffer(max(int(n), 1))
+
+
+def bbwt_forward(data: bytes) -> bytes:
+    ensure_init()
+    n = len(data)
+    out = _buf(n)
+    check(load().kolm_bbwt_forward(data, n, out))
+    return out.raw[:n]
+
+
+def mtf_encode(data: bytes) -> bytes:
+    ensure_init()
+    n = len(data)
+    out = _buf(n)
+    check(load().kolm_mtf_encode(data, n, out))
+    return out.raw[:n]
+
+
+def rice_encode(seq: bytes, k: int) -> bytes:
+    ensure_init()
+    n = len(seq)
+    cap = (n * ((255 >> k) + 1 + k) + 7) // 8 + 16
+    out = _buf(cap)
+    ln = ctypes.c_size_t(0)
+    check(load().kolm_rice_encode(seq, n, k, out, cap, ctypes.byref(ln)))
+    return out.raw[:ln.value]
+
+
+def lz77_encode(data: bytes) -> bytes:
+    ensure_init()
+    n = len(data)
+    cap = 2 * n + 16
+    out = _buf(cap)
+    ln = ctypes.c_size_t(0)
+    check(load().kolm_lz77_encode(data, n, out, cap, ctypes.byref(ln)))
+    return out.raw[:ln.value]
+
+
+def bbwt_mtf_rice(data: bytes, flags: int, k: int = 2) -> bytes:
+    ensure_init()
+    n = len(data)
+    cap = (n + 8) * ((255 >> k) + 1 + k) // 8 + 64
+    out = _buf(cap)
+    ln = ctypes.c_size_t(0)
+    check(load().kolm_bbwt_mtf_rice(data, n, flags, k, out, cap, ctypes.byref(ln)))
+    return out.raw[:ln.value]
+
+
+def encode_blocks(data: bytes, block_size: int, cand_mask: int = KOLM_DEFAULT_MASK, force=None):
+    """Batched MDL encode of fixed-size blocks.  Returns (sizes[nb,9], method[nb],
+    payloads list, stats dict)."""
+    ensure_init()
+    n = len(data)
+    nb = (n + block_size - 1) // block_size if n else 0
+    starts = np.arange(nb, dtype=np.uint64) * np.uint64(block_size)
+    lens = np.full(nb, block_size, dtype=np.uint32)
+    if nb:
+        lens[-1] = n - (nb - 1) * block_size
+    sizes = np.zeros((max(nb, 1), KOLM_NCAND), dtype=np.uint32)
+    method = np.zeros(max(nb, 1), dtype=np.uint32)
+    off = np.zeros(nb + 1, dtype=np.uint64)
+    cap = 9 * n + 64 * nb + 64
+    arena = np.zeros(cap, dtype=np.uint8)
+    fz = None
+    if force is not None:
+        fz = np.ascontiguousarray(np.asarray(force, dtype=np.int32))
+        if fz.shape != (nb,):
+            raise ValueError("force must have one entry per block")
+    st = Stats()
+    check(load().kolm_encode_blocks(
+        data, starts.ctypes.data, lens.ctypes.data, nb, cand_mask,
+        fz.ctypes.data if fz is not None else None,
+        sizes.ctypes.data, method.ctypes.data, arena.ctypes.data, cap, off.ctypes.data,
+        ctypes.byref(st)))
+    payloads = [arena[int(off[i]):int(off[i + 1])].tobytes() for i in range(nb)]
+    return sizes[:nb], method[:nb], payloads, st.as_dict()

@@ -1,0 +1,243 @@
+"""Block decoders for ``decompress()`` — host side.
+
+The decode direction is outside the north-star hot path (SURVEY.md §8f row 4 lists GPU
+decode kernels as "next"); these host decoders exist so that ``kolm.decompress`` keeps
+the reference block API and so that round trips can be tested.  They follow the
+reference decoders (PY = kolm_final_researched_v2-2.py), with one deliberate fix:
+PY's bit-plane decoder reads ``orig_len`` Rice values although the encoder emitted
+8*ceil(n/8); here the padded count is read so every container the
+reference encoder can produce decodes.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+from .container import uleb128_decode_stream
+
+
+def decode_raw(payload: bytes, n: int) -> bytes:  # PY:2101
+    if len(payload) != n:
+        raise ValueError("raw payload length mismatch")
+    return bytes(payload)
+
+
+def _uleb_bytes(payload: bytes, n: int) -> np.ndarray:
+    """Decode n ULEB values < 2^14 (each 1 or 2 bytes)."""
+    out = np.empty(n, dtype=np.int64)
+    pos = 0
+    for i in range(n):
+        v, pos = uleb128_decode_stream(payload, pos)
+        out[i] = v
+    if pos != len(payload):
+        raise ValueError("trailing bytes in ULEB stream")
+    return out
+
+
+def decode_xor(payload: bytes, n: int) -> bytes:  # PY:2113-2122
+    d = _uleb_bytes(payload, n)
+    return (np.cumsum(d) & 0xFF).astype(np.uint8).tobytes()
+
+
+_LFSR = None
+
+
+def _lfsr_table() -> np.ndarray:
+    global _LFSR
+    if _LFSR is None:
+        s, tab = 1, []
+        for _ in range(255):
+            tab.append(s)
+            fb = 0
+            for bit in range(8):
+                if (0x96 >> bit) & 1:
+                    fb ^= (s >> bit) & 1
+            s = ((s << 1) & 0xFF) | fb
+        _LFSR = np.array(tab, dtype=np.int64)
+    return _LFSR
+
+
+def decode_lfsr(payload: bytes, n: int) -> bytes:  # PY:2005-2019
+    d = _uleb_bytes(payload, n)
+    st = _lfsr_table()[np.arange(n) % 255]
+    return ((d + st) & 0xFF).astype(np.uint8).tobytes()
+
+
+def rice_decode(data: bytes, k: int, nvals: int) -> np.ndarray:  # PY:1423-1460
+    bits = np.unpackbits(np.frombuffer(data, dtype=np.uint8))
+    zeros = np.flatnonzero(bits == 0)
+    out = np.empty(nvals, dtype=np.int64)
+    pos = 0
+    nb = bits.size
+    for i in range(nvals):
+        j = np.searchsorted(zeros, pos)
+        if j >= zeros.size:
+            raise ValueError("rice: truncated unary")
+        z = int(zeros[j])
+        q = z - pos
+        pos = z + 1
+        r = 0
+        if k:
+            if pos + k > nb:
+                raise ValueError("rice: truncated remainder")
+            for t in range(k):
+                r = (r << 1) | int(bits[pos + t])
+            pos += k
+        out[i] = (q << k) | r
+    return out
+
+
+def bitplane_deinterleave(data: bytes, orig_len: int) -> bytes:  # PY:1122-1134
+    a = np.frombuffer(data, dtype=np.uint8).reshape(-1, 8)
+    bits = np.unpackbits(a, axis=1).reshape(-1, 8, 8)  # [group][plane][byte i]
+    return np.packbits(bits.transpose(0, 2, 1).reshape(-1, 8), axis=1).ravel()[:orig_len].tobytes()
+
+
+_BITREV = np.array([int(f"{i:08b}"[::-1], 2) for i in range(256)], dtype=np.uint8)
+
+
+def mtf_decode(seq) -> bytes:  # PY:470-478
+    table = list(range(256))
+    out = bytearray(len(seq))
+    for i, idx in enumerate(seq):
+        b = table.pop(int(idx))
+        out[i] = b
+        table.insert(0, b)
+    return bytes(out)
+
+
+def bbwt_inverse(L: bytes) -> bytes:  # PY:425-454
+    n = len(L)
+    if n == 0:
+        return b""
+    arr = np.frombuffer(L, dtype=np.uint8)
+    pi = np.argsort(arr, kind="stable")
+    seen = np.zeros(n, dtype=bool)
+    factors: List[Tuple[int, bytes]] = []
+    for i in range(n):
+        if seen[i]:
+            continue
+        cyc = []
+        cur = i
+        while not seen[cur]:
+            seen[cur] = True
+            cyc.append(cur)
+            cur = int(pi[cur])
+        # i is the minimum of its cycle (cycles are discovered in increasing min order)
+        seq = arr[pi[np.array(cyc)]]
+        factors.append((i, seq.tobytes()))
+    return b"".join(f for _, f in reversed(factors))
+
+
+def decode_bbwt_mtf_rice(payload: bytes, n: int, flags: int, k: int = 2) -> bytes:  # PY:2075-2089
+    length = 8 * ((n + 7) // 8) if flags & 1 else n
+    seq = rice_decode(payload, k, length).astype(np.uint8)
+    if flags & 16:
+        g = seq.copy()
+        g ^= g >> 1
+        g ^= g >> 2
+        g ^= g >> 4
+        seq = g
+    if flags & 8:
+        seq = _BITREV[seq]
+    if flags & 4:
+        seq = ((seq & 0x0F) << 4) | (seq >> 4)
+    if flags & 1:
+        seq = np.frombuffer(bitplane_deinterleave(seq.tobytes(), n), dtype=np.uint8)
+    return bbwt_inverse(mtf_decode(seq.tolist()))
+
+
+def decode_lz77(data: bytes, orig_len: int) -> bytes:  # PY:1765-1812
+    out = bytearray()
+    i, n = 0, len(data)
+    while i < n and len(out) < orig_len:
+        flag = data[i]
+        i += 1
+        if flag == 0:
+            if i >= n:
+                raise ValueError("LZ77 truncated literal")
+            out.append(data[i])
+            i += 1
+        elif flag == 1:
+            length, i = uleb128_decode_stream(data, i)
+            dist, i = uleb128_decode_stream(data, i)
+            if dist == 0 or dist > min(len(out), 4096):
+                raise ValueError("LZ77 invalid distance")
+            start = len(out) - dist
+            for t in range(min(length, orig_len - len(out))):
+                out.append(out[start + t])
+        else:
+            raise ValueError("LZ77 unknown flag")
+    if len(out) != orig_len:
+        raise ValueError("LZ77 output length mismatch")
+    return bytes(out)
+
+
+def repair_decompress(data: bytes, orig_len: int) -> bytes:  # PY:1913-1978
+    if len(data) < 2 or data[:2] != b"RP":
+        raise ValueError("Bad magic")
+    i = 2
+    terminals, i = uleb128_decode_stream(data, i)
+    if terminals != 256:
+        raise ValueError("Unsupported terminal alphabet")
+    nrules, i = uleb128_decode_stream(data, i)
+    rules: Dict[int, Tuple[int, int]] = {}
+    for r in range(nrules):
+        a, i = uleb128_decode_stream(data, i)
+        b, i = uleb128_decode_stream(data, i)
+        rules[256 + r] = (a, b)
+    seq_len, i = uleb128_decode_stream(data, i)
+    cache: Dict[int, bytes] = {}
+
+    def expand(sym: int) -> bytes:
+        if sym < 256:
+            return bytes((sym,))
+        if sym in cache:
+            return cache[sym]
+        stack = [(sym, 0)]
+        outs: List[bytes] = []
+        while stack:
+            node, st = stack.pop()
+            if node < 256:
+                outs.append(bytes((node,)))
+                continue
+            if st == 0:
+                a, b = rules[node]
+                stack.append((node, 1))
+                stack.append((b, 0))
+                stack.append((a, 0))
+            else:
+                right = outs.pop()
+                left = outs.pop()
+                cache[node] = left + right
+                outs.append(cache[node])
+        return outs[-1]
+
+    out = bytearray()
+    for _ in range(seq_len):
+        s, i = uleb128_decode_stream(data, i)
+        out += expand(s)
+    if len(out) != orig_len:
+        raise RuntimeError("RePair output length mismatch")
+    return bytes(out)
+
+
+BBWT_FLAGS = {2: 0, 3: 1, 4: 4, 5: 8, 6: 16}
+
+
+def decode_block(mid: int, payload: bytes, n: int) -> bytes:
+    """Decoder registry aligned with the encoder ids (PY:2194-2207)."""
+    if mid == 0:
+        return decode_raw(payload, n)
+    if mid == 1:
+        return decode_xor(payload, n)
+    if mid in BBWT_FLAGS:
+        return decode_bbwt_mtf_rice(payload, n, BBWT_FLAGS[mid])
+    if mid == 7:
+        return decode_lz77(payload, n)
+    if mid == 8:
+        return decode_lfsr(payload, n)
+    if mid == 9:
+        return repair_decompress(payload, n)
+    raise ValueError(f"Unknown method_id {mid}")

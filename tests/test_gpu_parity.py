@@ -1,0 +1,182 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden vectors
+(tests/golden, produced by importing PY), PY's own 1 MiB known answers, and the oracle
+(faithful CPU restatement) on seeded inputs.  Bit-exact everywhere (integer/byte work).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from kolm import datagen as D
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+with open(os.path.join(GOLDEN, "manifest.json")) as _f:
+    _MAN = json.load(_f)
+KNAMES = sorted(_MAN["kernels"])
+CNAMES = sorted(_MAN["containers"])
+FLAG_OF_MID = {2: 0, 3: 1, 4: 4, 5: 8, 6: 16}
+
+
+def sha(b: bytes) -> str:
+    return hashlib.sha256(b).hexdigest()
+
+
+def gk(golden_kernels, name, kind) -> bytes:
+    return golden_kernels[f"{name}/{kind}"].tobytes()
+
+
+@pytest.mark.parametrize("name", KNAMES)
+def test_bbwt_golden(kolm_gpu, golden_kernels, name):
+    inp = gk(golden_kernels, name, "input")
+    assert kolm_gpu.bbwt_forward(inp) == gk(golden_kernels, name, "bbwt")
+
+
+@pytest.mark.parametrize("name", KNAMES)
+def test_mtf_golden(kolm_gpu, golden_kernels, name):
+    bw = gk(golden_kernels, name, "bbwt")
+    assert bytes(kolm_gpu.mtf_encode(bw)) == gk(golden_kernels, name, "mtf")
+
+
+@pytest.mark.parametrize("name", KNAMES)
+def test_lz77_golden(kolm_gpu, golden_kernels, name):
+    inp = gk(golden_kernels, name, "input")
+    assert kolm_gpu.encode_lz77(inp)[0] == gk(golden_kernels, name, "lz77")
+
+
+@pytest.mark.parametrize("name", KNAMES)
+def test_batched_candidates_golden(kolm_gpu, golden_kernels, name):
+    """All 9 candidate payloads of one block through the batched entry (forced method)."""
+    inp = gk(golden_kernels, name, "input")
+    if not inp:
+        return
+    from kolm import _lib
+    want = {0: inp, 1: gk(golden_kernels, name, "xor"), 7: gk(golden_kernels, name, "lz77"),
+            8: gk(golden_kernels, name, "lfsr")}
+    for mid, f in FLAG_OF_MID.items():
+        want[mid] = gk(golden_kernels, name, f"rice{f}")
+    for mid in range(9):
+        sizes, method, payloads, _ = _lib.encode_blocks(inp, len(inp), force=[mid])
+        assert int(method[0]) == mid
+        assert payloads[0] == want[mid], f"candidate {mid}"
+        assert int(sizes[0][mid]) == len(want[mid]), f"size of candidate {mid}"
+    # un-forced: MDL winner = argmin, ties -> lowest id (PY:2359)
+    sizes, method, payloads, _ = _lib.encode_blocks(inp, len(inp))
+    lens = [len(want[m]) for m in range(9)]
+    assert list(map(int, sizes[0])) == lens
+    assert int(method[0]) == int(np.argmin(lens))
+
+
+@pytest.mark.parametrize("name", ["text_hobbit", "rand4k", "enwik16k", "utf8_mixed", "zero16k"])
+@pytest.mark.parametrize("k", [0, 1, 2, 3, 5, 7])
+def test_rice_param(kolm_gpu, golden_kernels, name, k):
+    mtf = gk(golden_kernels, name, "mtf")
+    assert kolm_gpu.rice_encode(mtf, k) == O.rice_encode(mtf, k)
+
+
+@pytest.mark.parametrize("cname", CNAMES)
+def test_container_golden(kolm_gpu, golden_containers, manifest, cname):
+    inp = golden_containers[f"{cname}/input"].tobytes()
+    bs = manifest["containers"][cname]["block_size"]
+    got = kolm_gpu.compress_blocks_fixed(inp, bs)
+    assert got == golden_containers[f"{cname}/ids0_8"].tobytes()
+    assert kolm_gpu.decompress(got) == inp
+
+
+LARGE = {
+    "gradient_1m": lambda: D.gradient_bmp()[: 1 << 20],
+    "pattern_1m": lambda: D.pattern_blocks(),
+    "checker_full": lambda: D.checker_bmp(),
+    "sine_full": lambda: D.sine_wav(),
+    "enwik_256k": lambda: D.enwik_like(1 << 18),
+}
+
+
+@pytest.mark.parametrize("case", sorted(LARGE))
+def test_large_known_answers(kolm_gpu, large_known, case):
+    """1 MiB-class blocks against sha256 of PY's own outputs (tests/golden/large.json)."""
+    from kolm import _lib
+    data = LARGE[case]()
+    ref = large_known[case]
+    assert sha(data) == ref["input"]["sha256"]
+    bw = kolm_gpu.bbwt_forward(data)
+    assert sha(bw) == ref["bbwt"]["sha256"], "bbwt"
+    mt = bytes(kolm_gpu.mtf_encode(bw))
+    assert sha(mt) == ref["mtf"]["sha256"], "mtf"
+    for mid, f in FLAG_OF_MID.items():
+        _, _, payloads, _ = _lib.encode_blocks(data, len(data), force=[mid])
+        assert len(payloads[0]) == ref[f"rice{f}"]["len"], f"rice{f} len"
+        assert sha(payloads[0]) == ref[f"rice{f}"]["sha256"], f"rice{f}"
+    if "lz77" in ref:
+        z = kolm_gpu.encode_lz77(data)[0]
+        assert len(z) == ref["lz77"]["len"] and sha(z) == ref["lz77"]["sha256"], "lz77"
+
+
+def _oracle_all(block: bytes):
+    return [O.candidate(m, block) for m in range(9)]
+
+
+@pytest.mark.parametrize("seed,bs,n", [(1, 65536, 4 * 65536 + 12345), (2, 4096, 65536 + 17), (3, 1000, 20011),
+                                       (4, 7, 301), (5, 1, 40), (6, 3, 64), (7, 8, 800)])
+def test_multiblock_vs_oracle(kolm_gpu, seed, bs, n):
+    """Several blocks in one batch, all candidate sizes + the emitted winners vs oracle."""
+    from kolm import _lib
+    rng = np.random.default_rng(seed)
+    parts = [D.enwik_like(n // 2, seed=seed), rng.integers(0, 4, n // 4).astype(np.uint8).tobytes(),
+             bytes(n // 8), D.splitmix64_bytes(n, seed=seed)]
+    data = b"".join(parts)[:n]
+    sizes, method, payloads, _ = _lib.encode_blocks(data, bs)
+    nb = (n + bs - 1) // bs
+    assert len(payloads) == nb
+    for i in range(nb):
+        blk = data[i * bs:(i + 1) * bs]
+        cand = _oracle_all(blk)
+        lens = [len(c) for c in cand]
+        assert list(map(int, sizes[i])) == lens, f"block {i}"
+        m = int(np.argmin(lens))
+        assert int(method[i]) == m, f"block {i}"
+        assert payloads[i] == cand[m], f"block {i} payload"
+
+
+def test_container_vs_oracle_multiblock(kolm_gpu):
+    data = D.mixed_corpus()[:300_000]
+    bs = 65536
+    got = kolm_gpu.compress_blocks_fixed(data, bs)
+    assert got == O.compress_blocks_fixed(data, bs, range(9))
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_full_size_enwik_properties(kolm_gpu, seed):
+    """Full-size blocks (1 MiB, BASELINE configs 3/4): exact vs oracle on one block, and
+    size-independent properties on a 16-block batch (BBWT is a permutation of each
+    block, MTF round trip on a sample, container decodes)."""
+    from kolm import _lib
+    data = D.enwik_like(16 << 20, seed=seed)
+    bs = 1 << 20
+    sizes, method, payloads, st = _lib.encode_blocks(data, bs)
+    assert len(payloads) == 16
+    blk = data[:bs]
+    cand = _oracle_all(blk)
+    assert list(map(int, sizes[0])) == [len(c) for c in cand]
+    assert payloads[0] == cand[int(method[0])]
+    for i in range(16):
+        assert int(sizes[i][int(method[i])]) == len(payloads[i])
+        assert int(method[i]) == int(np.argmin(sizes[i]))
+    # BBWT of one block is a permutation and inverts back
+    from kolm import decode
+    b3 = data[3 * bs:4 * bs]
+    bw = kolm_gpu.bbwt_forward(b3)
+    assert np.array_equal(np.bincount(np.frombuffer(bw, np.uint8), minlength=256),
+                          np.bincount(np.frombuffer(b3, np.uint8), minlength=256))
+    assert decode.bbwt_inverse(bw) == b3
+
+
+@pytest.mark.parametrize("data,bs", [(b"", 16), (b"\x00", 1), (b"ab", 1), (b"abc" * 5, 4), (bytes(range(256)) * 3, 100)])
+def test_edge_cases(kolm_gpu, data, bs):
+    got = kolm_gpu.compress_blocks_fixed(data, bs)
+    assert got == O.compress_blocks_fixed(data, bs, range(9))
+    assert kolm_gpu.decompress(got) == data
