@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Benchmark: compress MB/s at fixed block size, bit-exact path, 1..8 GPUs.
+
+Workload (BASELINE.json north star / SURVEY.md §8d configs 3-4): per GPU, 256 MiB of
+synthetic enwik-style text (kolm.datagen.enwik_like, seed 20251212 + rank) resident in
+HBM, 1 MiB fixed blocks, all candidates 0..8 evaluated per block, MDL winner emitted.
+One step = one full compress of the rank's batch from HBM to a device payload arena
+(+ for N > 1 the RCCL gather of every rank's payloads and method ids to rank 0).
+Weak scaling: per-GPU work is fixed; value = all ranks' input bytes / max-over-ranks time.
+
+Also reported:
+  roofline      the dominant kernel family (largest summed device time in the timed
+                steps, HIP events on the library's stream): algorithmic bytes per launch
+                 / average launch time, against 8 TB/s HBM peak;
+                traffic = PMC-measured HBM bytes per launch from profiles/pmc_summary.json
+                when present (collected by tools/pmc_traffic.py), else null.
+  cpu_baseline  the oracle (faithful C++ restatement of the reference CPU path, 5x BBWT
+                as in PY) on a bounded sample of the same stream, rank 0 at N=1 only.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 via
+python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import torch  # first: libkolm_hip.so must bind to torch's already-loaded HIP runtime
+import torch.distributed as dist
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "kolmogorovlike-datacompressor_amd"))
+
+from kolm import _lib, datagen  # noqa: E402
+from kolm.parallel import gather_payloads  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+MB = 1e6
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(data: bytes, bs: int, budget_s: float):
+    """Oracle (reference algorithms, 1 thread) on whole 1 MiB blocks of the same stream:
+    every candidate 0..8 + MDL, as the reference's per-block loop (Re-Pair excluded)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    t0 = time.time()
+    nbytes = 0
+    blocks = 0
+    while True:
+        blk = data[blocks * bs:(blocks + 1) * bs]
+        sizes = [len(oracle.candidate(m, blk)) for m in range(9)]
+        _ = int(np.argmin(sizes))
+        nbytes += len(blk)
+        blocks += 1
+        if time.time() - t0 >= budget_s or blocks * bs >= len(data):
+            break
+    el = time.time() - t0
+    return {"value": round(nbytes / el / MB, 5), "unit": "MB/s", "cores": 1, "kind": "port",
+            "sample": f"{blocks} x {bs >> 20} MiB block(s) of the bench stream, candidates 0..8 "
+                      f"(5x BBWT, list MTF, bit-serial Rice, exhaustive 4 KiB LZ77), {el:.1f} s, 1 thread; "
+                      "Re-Pair (id 9) excluded as in the GPU path"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--mib", type=int, default=256, help="input MiB per GPU")
+    ap.add_argument("--bs", type=int, default=1 << 20, help="block size")
+    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of oracle CPU work (N=1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        log(rank, f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    n = a.mib << 20
+    t = time.time()
+    data = datagen.enwik_like(n, seed=datagen.ENWIK_SEED + rank)
+    log(rank, f"[bench] generated {a.mib} MiB per rank in {time.time() - t:.1f}s")
+
+    L = _lib.load()
+    ctx = ctypes.c_void_p()
+    _lib.check(L.kolm_ctx_create(local, ctypes.byref(ctx)))
+    d_in = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    d_in[:n].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    cap = n + (4 << 20)
+    arena = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    nb = (n + a.bs - 1) // a.bs
+    sizes = np.zeros((nb, 9), np.uint32)
+    method = np.zeros(nb, np.uint32)
+    off = np.zeros(nb + 1, np.uint64)
+    torch.cuda.synchronize()
+
+    def step(st):
+        _lib.check(L.kolm_encode_blocks_device(ctx, d_in.data_ptr(), n, a.bs, 0x1FF, None, arena.data_ptr(), cap,
+                                               sizes.ctypes.data, method.ctypes.data, off.ctypes.data,
+                                               ctypes.byref(st)))
+        if world > 1:
+            ids = torch.from_numpy(method.astype(np.int32)).cuda()
+            gather_payloads(arena, int(off[-1]), ids, dst=0)
+
+    for _ in range(a.warmup):
+        step(_lib.Stats())
+    _lib.check(L.kolm_ctx_set_timing(ctx, 1))
+    kern = {}
+    stats = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        st = _lib.Stats()
+        step(st)
+        d = st.as_dict()
+        stats.append(d)
+        for k, v in d["kernels"].items():
+            e = kern.setdefault(k, {"ms": 0.0, "launches": 0, "bytes": 0})
+            for f in ("ms", "launches", "bytes"):
+                e[f] += v[f]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    _lib.check(L.kolm_ctx_set_timing(ctx, 0))
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt[0])
+    ms_step = el / a.steps * 1e3
+    value = world * n * a.steps / el / MB
+
+    # roofline of the dominant kernel family
+    dom = max(kern.items(), key=lambda kv: kv[1]["ms"])
+    name, k = dom
+    avg_ms = k["ms"] / k["launches"]
+    bytes_per_launch = k["bytes"] / k["launches"]
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "pmc_summary.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            tr = json.load(f).get("families", {}).get(name)
+        if tr and tr.get("hbm_bytes_per_launch"):
+            traffic = tr["hbm_bytes_per_launch"]
+    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": name,
+            "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": int(bytes_per_launch),
+            "launches_per_step": k["launches"] // a.steps}
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(data, a.bs, a.cpu_budget)
+
+    if rank == 0:
+        s0 = stats[-1]
+        out = {
+            "metric": "compress MB/s at fixed block size, bit-exact vs reference; 1/2/4/8-GPU scaling",
+            "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(ms_step, 2), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "enwik-style synthetic text (kolm.datagen.enwik_like, seed 20251212+rank), "
+                                   f"{a.mib} MiB per GPU resident in HBM, {a.bs >> 20} MiB fixed blocks, "
+                                   "candidates 0..8 + MDL, payloads emitted in HBM"
+                                   + (", RCCL gather to rank 0" if world > 1 else ""),
+                       "block_size": a.bs, "bytes_per_gpu": n, "blocks_per_gpu": nb,
+                       "parallelism": f"block-shard x{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "detail": {"ratio": round(float(off[-1]) / n, 4),
+                       "methods": np.bincount(method, minlength=9).tolist(),
+                       "device_ms": {k: round(s0[k], 2) for k in ("ms_total", "ms_sa", "ms_lz", "ms_entropy", "ms_emit")},
+                       "rounds": [s0["lin_rounds"], s0["cyc_rounds"]],
+                       "kernels_ms_per_step": {kk: round(v["ms"] / a.steps, 2) for kk, v in
+                                               sorted(kern.items(), key=lambda kv: -kv[1]["ms"])}},
+        }
+        if cpu:
+            out["detail"]["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
+        print(json.dumps(out), flush=True)
+    L.kolm_ctx_destroy(ctx)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -52,6 +52,25 @@ extern "C" {
 
 typedef struct kolm_ctx kolm_ctx;
 
+/* Kernel families timed with HIP events when timing is enabled (kolm_ctx_set_timing). */
+#define KOLM_KT_CLASSIFY 0   /* k_classify */
+#define KOLM_KT_KEYGEN 1     /* k_keygen_small, k_keygen_large */
+#define KOLM_KT_MSD 2        /* k_msd_hist, k_msd_scan, k_msd_scatter, k_copy_back */
+#define KOLM_KT_SMALLSORT 3  /* k_small_sort<1..11>, k_single, k_finalize_eq */
+#define KOLM_KT_LZMATCH 4    /* k_lz_match */
+#define KOLM_KT_LZPARSE 5    /* k_lz_parse */
+#define KOLM_KT_MTF 6        /* k_mtf_summary, k_mtf_compose, k_mtf_replay */
+#define KOLM_KT_SIZES 7      /* k_sizes, k_mdl, k_offsets */
+#define KOLM_KT_EMIT 8       /* emission kernels */
+#define KOLM_KT_LYNDON 9     /* Lyndon scans + BBWT gather + prev3 */
+#define KOLM_NKT 10
+
+typedef struct kolm_ktime {
+    double ms;          /* summed launch durations (HIP events on the library stream) */
+    uint64_t launches;
+    uint64_t bytes;     /* algorithmic HBM bytes of those launches */
+} kolm_ktime;
+
 /* Per-batch statistics reported by the encode entry points. */
 typedef struct kolm_stats {
     uint32_t lin_rounds;      /* prefix-doubling rounds, linear suffix order (max over blocks) */
@@ -65,9 +84,7 @@ typedef struct kolm_stats {
     double ms_lz;             /* of which: LZ77 match + parse */
     double ms_entropy;        /* of which: BBWT gather + MTF + Rice sizes */
     double ms_emit;           /* of which: MDL + payload emission */
-    double ms_msd_scatter;    /* summed duration of the MSD scatter kernel launches */
-    uint32_t n_msd_scatter;   /* number of MSD scatter launches */
-    uint64_t msd_scatter_elems; /* elements moved by MSD scatter launches */
+    kolm_ktime kt[KOLM_NKT];  /* per kernel family, filled when timing is enabled */
 } kolm_stats;
 
 /* ---- library / default context ------------------------------------------------ */
@@ -115,6 +132,8 @@ int kolm_dev_free(kolm_ctx* ctx, void* dptr);
 int kolm_memcpy_h2d(kolm_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 int kolm_memcpy_d2h(kolm_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 int kolm_ctx_sync(kolm_ctx* ctx);
+/* Enable (1) / disable (0) per-launch HIP-event timing of the kernel families. */
+int kolm_ctx_set_timing(kolm_ctx* ctx, int enable);
 /* Fixed-size blocks of d_data (device pointer, total bytes, block_size).  Payloads go
  * to the device arena d_arena (cap bytes); h_sizes / h_method / h_off are host arrays
  * as in kolm_encode_blocks.  Blocks until the batch is complete. */

@@ -122,22 +122,50 @@ __global__ void k_block_segs(Seg* segs, Geom geo) {
     if (b < geo.nb) segs[b] = Seg{geo.base(b), geo.end(b) - geo.base(b)};
 }
 
-__global__ void k_classify(const Seg* cur, u32 ncur, SortArgs a, Lists L, Level lv) {
+// Appends are aggregated per workgroup: LDS counters per class, one global atomic per
+// class and workgroup (list order is irrelevant: every segment is refined independently).
+__global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur, SortArgs a, Lists L, Level lv) {
+    __shared__ u32 lcnt[NCLASS + 1], lbase[NCLASS + 1], lel[NCLASS + 1];
+    __shared__ u32 lact;
+    if (threadIdx.x <= NCLASS) {
+        lcnt[threadIdx.x] = 0;
+        lel[threadIdx.x] = 0;
+    }
+    if (threadIdx.x == 0) lact = 0;
+    __syncthreads();
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= ncur) return;
-    const Seg s = cur[i];
-    if (a.cyclic && a.blk_done[a.geo.block_of(s.start)]) return;
-    atomicAdd(&L.misc[0], s.len);
-    if (s.len > (u32)TILE) {
+    Seg s{0, 0};
+    int c = -1;
+    u32 li = 0;
+    if (i < ncur) {
+        s = cur[i];
+        if (!(a.cyclic && a.blk_done[a.geo.block_of(s.start)])) {
+            c = s.len > (u32)TILE ? NCLASS : size_class(s.len);
+            li = atomicAdd(&lcnt[c], 1u);
+            atomicAdd(&lel[c], s.len);
+            atomicAdd(&lact, s.len);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < NCLASS && lcnt[threadIdx.x]) {
+        lbase[threadIdx.x] = atomicAdd(&L.cls_cnt[threadIdx.x], lcnt[threadIdx.x]);
+        atomicAdd(&L.cls_elems[threadIdx.x], lel[threadIdx.x]);
+    }
+    if (threadIdx.x == NCLASS && lcnt[NCLASS]) {
+        lbase[NCLASS] = atomicAdd(lv.nseg, lcnt[NCLASS]);
+        atomicAdd(lv.nelem, lel[NCLASS]);
+    }
+    if (threadIdx.x == NCLASS + 1 && lact) atomicAdd(&L.misc[0], lact);
+    __syncthreads();
+    if (c < 0) return;
+    if (c == NCLASS) {
         const u32 nt = (s.len + TILE - 1) / TILE;
-        const u32 si = atomicAdd(lv.nseg, 1u);
+        const u32 si = lbase[NCLASS] + li;
         const u32 tb = atomicAdd(lv.ntiles, nt);
         lv.segs[si] = LSeg{s.start, s.len, tb, nt};
         for (u32 k = 0; k < nt; ++k) lv.tiles[tb + k] = LTile{si, k};
     } else {
-        const int c = size_class(s.len);
-        const u32 idx = atomicAdd(&L.cls_cnt[c], 1u);
-        L.cls[c][idx] = s;
+        L.cls[c][lbase[c] + li] = s;
     }
 }
 
@@ -222,10 +250,12 @@ __global__ __launch_bounds__(WG) void k_msd_scan(const LSeg* segs, SortArgs a, u
     if (run <= (u32)TILE) {
         const int c = size_class(run);
         L.cls[c][atomicAdd(&L.cls_cnt[c], 1u)] = sub;
+        atomicAdd(&L.cls_elems[c], run);
     } else if (!last_level) {
         const u32 nt = (run + TILE - 1) / TILE;
         const u32 si = atomicAdd(nx.nseg, 1u);
         const u32 tb = atomicAdd(nx.ntiles, nt);
+        atomicAdd(nx.nelem, run);
         nx.segs[si] = LSeg{sub.start, sub.len, tb, nt};
         for (u32 k = 0; k < nt; ++k) nx.tiles[tb + k] = LTile{si, k};
     } else {
@@ -423,6 +453,18 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
         nxt[e] = run_min;
         if (stop[e]) run_min = 8 * tid + e;
     }
+    // new groups of >= 2 elements go to the next round (one global atomic per workgroup)
+    u32 nnew = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) nnew += (valid[e] && head[e] && nxt[e] - (8 * tid + e) >= 2) ? 1u : 0u;
+    const u32 my_off = wg_excl_scan<false>(nnew, OpAdd(), 0u, sh);
+    if (tid == WG - 1) last_hi[0] = my_off + nnew;  // reuse LDS: workgroup total
+    __syncthreads();
+    const u32 total_new = last_hi[0];
+    __syncthreads();
+    if (tid == 0) last_hi[1] = total_new ? atomicAdd(L.next_cnt, total_new) : 0u;
+    __syncthreads();
+    u32 wpos = last_hi[1] + my_off;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         if (!valid[e]) continue;
@@ -434,7 +476,7 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
         a.RK[pos] = sg.start + (start_idx[e] - (si << C));
         if (head[e]) {
             const u32 len = nxt[e] - i;
-            if (len >= 2) L.next[atomicAdd(L.next_cnt, 1u)] = Seg{sg.start + kk, len};
+            if (len >= 2) L.next[wpos++] = Seg{sg.start + kk, len};
             if (kk > 0) a.blk_split[a.geo.block_of(sg.start)] = 1;
         }
     }

@@ -46,9 +46,25 @@ enum : int {
     C_STATUS = 20,
     C_NLONG = 21,
     C_RICE = 22,
-    C_N = 32
+    C_CLSE = 24,     // 12 slots: elements per small class
+    C_L0ELEM = 36,
+    C_L1ELEM = 37,
+    C_N = 48
 };
 
+}  // namespace
+
+struct kolm_ctx;
+namespace {
+// Records a HIP event pair around the launches in its scope (timing enabled only).
+struct TScope {
+    kolm_ctx* c;
+    int fam;
+    u64 bytes;
+    hipEvent_t a = nullptr;
+    TScope(kolm_ctx* c_, int fam_, u64 bytes_);
+    ~TScope() noexcept(false);
+};
 }  // namespace
 
 struct kolm_ctx {
@@ -58,6 +74,38 @@ struct kolm_ctx {
     std::map<std::string, DevBuf> bufs;
     u32* h_cnt = nullptr;  // pinned mirror of the counters
     hipEvent_t ev[8] = {};
+    // per-launch timing of kernel families (kolm_ctx_set_timing)
+    bool timing = false;
+    std::vector<hipEvent_t> evpool;
+    size_t evused = 0;
+    struct Pend {
+        int fam;
+        hipEvent_t a, b;
+        u64 bytes;
+    };
+    std::vector<Pend> pend;
+    hipEvent_t ev_take() {
+        if (evused == evpool.size()) {
+            hipEvent_t e;
+            KOLM_HIP_CHECK(hipEventCreate(&e));
+            evpool.push_back(e);
+        }
+        return evpool[evused++];
+    }
+    void timing_reset() {
+        pend.clear();
+        evused = 0;
+    }
+    void timing_collect(kolm_stats* st) {
+        for (auto& p : pend) {
+            float ms = 0;
+            KOLM_HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
+            st->kt[p.fam].ms += ms;
+            st->kt[p.fam].launches += 1;
+            st->kt[p.fam].bytes += p.bytes;
+        }
+        timing_reset();
+    }
 
     void* raw(const char* name, size_t bytes) {
         DevBuf& b = bufs[name];
@@ -79,6 +127,20 @@ struct kolm_ctx {
 };
 
 namespace {
+
+TScope::TScope(kolm_ctx* c_, int fam_, u64 bytes_) : c(c_), fam(fam_), bytes(bytes_) {
+    if (c->timing) {
+        a = c->ev_take();
+        KOLM_HIP_CHECK(hipEventRecord(a, c->stream));
+    }
+}
+TScope::~TScope() noexcept(false) {
+    if (c->timing) {
+        hipEvent_t b = c->ev_take();
+        KOLM_HIP_CHECK(hipEventRecord(b, c->stream));
+        c->pend.push_back({fam, a, b, bytes});
+    }
+}
 
 std::mutex g_mu;
 kolm_ctx* g_default = nullptr;
@@ -123,6 +185,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
     L.next_cnt = cnt + C_NEXT;
     L.eq_cnt = cnt + C_EQ;
     L.misc = cnt + C_ACTIVE;
+    L.cls_elems = cnt + C_CLSE;
     L.eq = c->get<Seg>("eq", N / TILE + 16);
     const u64 seg_cap = N / 2 + geo.nb + 16;
     Seg* segA = c->get<Seg>("segA", seg_cap);
@@ -130,8 +193,10 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
     const u64 lseg_cap = N / TILE + 16;
     const u64 ltile_cap = 2 * (N / TILE) + 16;
     Level lv[2];
-    lv[0] = Level{c->get<LSeg>("lseg0", lseg_cap), cnt + C_L0SEG, c->get<LTile>("ltile0", ltile_cap), cnt + C_L0TILE};
-    lv[1] = Level{c->get<LSeg>("lseg1", lseg_cap), cnt + C_L1SEG, c->get<LTile>("ltile1", ltile_cap), cnt + C_L1TILE};
+    lv[0] = Level{c->get<LSeg>("lseg0", lseg_cap), cnt + C_L0SEG, c->get<LTile>("ltile0", ltile_cap), cnt + C_L0TILE,
+                  cnt + C_L0ELEM};
+    lv[1] = Level{c->get<LSeg>("lseg1", lseg_cap), cnt + C_L1SEG, c->get<LTile>("ltile1", ltile_cap), cnt + C_L1TILE,
+                  cnt + C_L1ELEM};
     u32* hist = c->get<u32>("hist", ltile_cap * 256);
 
     launch_iota(a.SA, N, s);
@@ -148,15 +213,25 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
         a.h = round == 0 ? 0u : (h0 << (round - 1));
         L.next = nxt;
         KOLM_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(u32) * C_STATUS, s));
+        KOLM_HIP_CHECK(hipMemsetAsync(cnt + C_CLSE, 0, sizeof(u32) * (C_N - C_CLSE), s));
         KOLM_HIP_CHECK(hipMemsetAsync(a.blk_split, 0, sizeof(u32) * geo.nb, s));
-        launch_classify(cur, ncur, a, L, lv[0], s);
+        {
+            TScope t(c, KOLM_KT_CLASSIFY, (u64)ncur * 16);
+            launch_classify(cur, ncur, a, L, lv[0], s);
+        }
         KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
         c->sync();
         if (h[C_ACTIVE] == 0) break;
         out.active += h[C_ACTIVE];
         out.rounds = round + 1;
-        for (int k = 1; k < NCLASS; ++k) launch_keygen_small(k, L.cls[k], h[C_CLS + k], a, s);
-        launch_keygen_large(lv[0].tiles, h[C_L0TILE], lv[0].segs, a, s);
+        {
+            // algorithmic bytes per element: SA read + key inputs + K2 write
+            const u64 per = a.initial ? (cyclic ? 20 : 11) : (cyclic ? 20 : 12);
+            TScope t(c, KOLM_KT_KEYGEN, (u64)h[C_ACTIVE] * per);
+            for (int k = 1; k < NCLASS; ++k) launch_keygen_small(k, L.cls[k], h[C_CLS + k], a, s);
+            launch_keygen_large(lv[0].tiles, h[C_L0TILE], lv[0].segs, a, s);
+        }
+        u32 nelem = h[C_L0ELEM];
         u32 nseg = h[C_L0SEG], ntiles = h[C_L0TILE];
         u32 hi = a.initial ? (cyclic ? 32u : 27u) : kb_rank;
         int lvl = 0;
@@ -168,23 +243,40 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
             Level& ln = lv[(lvl + 1) & 1];
             KOLM_HIP_CHECK(hipMemsetAsync(ln.nseg, 0, sizeof(u32), s));
             KOLM_HIP_CHECK(hipMemsetAsync(ln.ntiles, 0, sizeof(u32), s));
-            launch_msd_hist(lc.tiles, ntiles, lc.segs, a, shift, width, hist, s);
-            launch_msd_scan(lc.segs, nseg, a, width, hist, last, L, ln, s);
-            launch_msd_scatter(lc.tiles, ntiles, lc.segs, a, shift, width, hist, s);
-            launch_copy_back(lc.tiles, ntiles, lc.segs, a, s);
+            KOLM_HIP_CHECK(hipMemsetAsync(ln.nelem, 0, sizeof(u32), s));
+            {
+                // hist: K2 4 B; scatter: SA+K2 read 8, write 8; copy back: 8 + 8
+                TScope t(c, KOLM_KT_MSD, (u64)nelem * 36 + (u64)ntiles * 256 * 8);
+                launch_msd_hist(lc.tiles, ntiles, lc.segs, a, shift, width, hist, s);
+                launch_msd_scan(lc.segs, nseg, a, width, hist, last, L, ln, s);
+                launch_msd_scatter(lc.tiles, ntiles, lc.segs, a, shift, width, hist, s);
+                launch_copy_back(lc.tiles, ntiles, lc.segs, a, s);
+            }
             KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
             c->sync();
-            nseg = *(ln.nseg == cnt + C_L0SEG ? &h[C_L0SEG] : &h[C_L1SEG]);
-            ntiles = *(ln.ntiles == cnt + C_L0TILE ? &h[C_L0TILE] : &h[C_L1TILE]);
+            const bool n0 = ln.nseg == cnt + C_L0SEG;
+            nseg = h[n0 ? C_L0SEG : C_L1SEG];
+            ntiles = h[n0 ? C_L0TILE : C_L1TILE];
+            nelem = h[n0 ? C_L0ELEM : C_L1ELEM];
             hi = shift;
             ++lvl;
         }
         KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
         c->sync();
-        for (int k = 0; k < NCLASS; ++k) launch_small_sort(k, L.cls[k], h[C_CLS + k], a, L, s);
-        launch_finalize_eq(L.eq, h[C_EQ], a, L, s);
+        {
+            // per element: K2 + SA read, SA + RK write (16 B); per segment record 8 B
+            u64 sb = 0;
+            for (int k = 0; k < NCLASS; ++k) sb += (u64)h[C_CLSE + k] * 16 + (u64)h[C_CLS + k] * 8;
+            sb += (u64)h[C_EQ] * TILE * 8;
+            TScope t(c, KOLM_KT_SMALLSORT, sb);
+            for (int k = 0; k < NCLASS; ++k) launch_small_sort(k, L.cls[k], h[C_CLS + k], a, L, s);
+            launch_finalize_eq(L.eq, h[C_EQ], a, L, s);
+        }
         if (cyclic) launch_update_done(blk_done, a.blk_split, geo.nb, s);
-        if (!cyclic && round == 0 && prev3) launch_prev3(a, prev3, s);
+        if (!cyclic && round == 0 && prev3) {
+            TScope t(c, KOLM_KT_LYNDON, N * 16);
+            launch_prev3(a, prev3, s);
+        }
         KOLM_HIP_CHECK(hipMemcpyAsync(h + C_NEXT, cnt + C_NEXT, sizeof(u32), hipMemcpyDeviceToHost, s));
         c->sync();
         ncur = h[C_NEXT];
@@ -212,10 +304,18 @@ struct Pipeline {
         u32* t1 = c->get<u32>("tile_tmp", 2 * ntiles + 16);
         u32* t2 = c->get<u32>("tile_tmp2", 2 * ntiles + 2 * geo.nb + 16);
         SortOut lin = sort_pass(c, geo, text, false, nullptr, nullptr, prev3, false);
-        launch_lyndon(geo, c->get<u32>("RK", N), flag, FS, FL, t1, t2, c->stream);
+        {
+            // RK read twice, flags write + 2 reads, FS/FL write
+            TScope t(c, KOLM_KT_LYNDON, N * 19);
+            launch_lyndon(geo, c->get<u32>("RK", N), flag, FS, FL, t1, t2, c->stream);
+        }
         SortOut cyc = sort_pass(c, geo, text, true, FS, FL, nullptr, false);
         u8* out = c->get<u8>("bbwt", N);
-        launch_bbwt_gather(geo, text, c->get<u32>("SA", N), FS, FL, out, c->stream);
+        {
+            // SA 4 + FS 4 + FL 4 + text 1 + out 1
+            TScope t(c, KOLM_KT_LYNDON, N * 14);
+            launch_bbwt_gather(geo, text, c->get<u32>("SA", N), FS, FL, out, c->stream);
+        }
         st.lin_rounds = lin.rounds;
         st.cyc_rounds = cyc.rounds;
         st.lin_active = lin.active;
@@ -227,6 +327,8 @@ struct Pipeline {
         const u64 N = geo.N;
         const u64 nch = (u64)((geo.bs + MTF_CHUNK - 1) / MTF_CHUNK) * geo.nb + 1;
         u8* out = c->get<u8>("mtf", N);
+        // summary: read N; compose: summaries + states 512 B/chunk; replay: N in, N out, state
+        TScope t(c, KOLM_KT_MTF, 3 * N + nch * 768);
         launch_mtf(geo, in, out, c->get<u8>("mtf_sum", nch * 256), c->get<u16>("mtf_cnt", nch),
                    c->get<u8>("mtf_states", nch * 256), c->stream);
         return out;
@@ -252,8 +354,16 @@ struct Pipeline {
 
     void lz(const LzArgs& z) {
         KOLM_HIP_CHECK(hipMemsetAsync(z.nlong, 0, sizeof(u32), c->stream));
-        launch_lz_match(z, c->stream);
-        launch_lz_parse(z, c->stream);
+        {
+            // prev3 4 + text 1 + Lc 1 + Dc 2 per position
+            TScope t(c, KOLM_KT_LZMATCH, geo.N * 8);
+            launch_lz_match(z, c->stream);
+        }
+        {
+            // Lc + Dc per position (+ 16 B per token, added after the batch)
+            TScope t(c, KOLM_KT_LZPARSE, geo.N * 3);
+            launch_lz_parse(z, c->stream);
+        }
     }
 };
 
@@ -290,6 +400,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
     hipStream_t s = c->stream;
     Pipeline P{c, geo, d_text};
     hipEvent_t* ev = c->ev;
+    c->timing_reset();
     KOLM_HIP_CHECK(hipEventRecord(ev[0], s));
     u8* bw = P.bbwt();
     KOLM_HIP_CHECK(hipEventRecord(ev[1], s));
@@ -315,7 +426,10 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
     e.tile_tmp = c->get<u32>("tile_tmp", 2 * ntiles + 16);
     e.tile_tmp2 = c->get<u32>("tile_tmp2", 2 * ntiles + 2 * nb + 16);
     e.rice_k = 2;
-    launch_cheap_and_rice_sizes(e, s);
+    {
+        TScope t(c, KOLM_KT_SIZES, 2 * N);  // text + mtf once
+        launch_cheap_and_rice_sizes(e, s);
+    }
     KOLM_HIP_CHECK(hipEventRecord(ev[2], s));
     LzArgs z = P.lz_args();
     const bool want_lz = (mask >> KOLM_M_LZ77) & 1u || (h_force != nullptr);
@@ -323,7 +437,10 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
     KOLM_HIP_CHECK(hipEventRecord(ev[3], s));
     u32* cnt = c->get<u32>("counters", C_N);
     KOLM_HIP_CHECK(hipMemsetAsync(cnt + C_STATUS, 0, sizeof(u32), s));
-    launch_mdl(e, want_lz ? z.lz_size : nullptr, cnt + C_STATUS, s);
+    {
+        TScope t(c, KOLM_KT_SIZES, (u64)nb * 120);
+        launch_mdl(e, want_lz ? z.lz_size : nullptr, cnt + C_STATUS, s);
+    }
     std::vector<u64> off(nb + 1);
     KOLM_HIP_CHECK(hipMemcpyAsync(off.data(), e.off, sizeof(u64) * (nb + 1), hipMemcpyDeviceToHost, s));
     KOLM_HIP_CHECK(hipMemcpyAsync(c->h_cnt, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
@@ -332,20 +449,30 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
         set_err("payload arena too small");
         return KOLM_ECAP;
     }
-    KOLM_HIP_CHECK(hipMemsetAsync(d_arena, 0, (off[nb] + 8) & ~(u64)3, s));
-    launch_emit_simple(e, s);
-    launch_emit_rice(e, s);
-    if (want_lz) launch_lz_emit(z, e.method, e.off, d_arena, s);
+    {
+        TScope t(c, KOLM_KT_EMIT, N + 2 * off[nb]);
+        KOLM_HIP_CHECK(hipMemsetAsync(d_arena, 0, (off[nb] + 8) & ~(u64)3, s));
+        launch_emit_simple(e, s);
+        launch_emit_rice(e, s);
+        if (want_lz) launch_lz_emit(z, e.method, e.off, d_arena, s);
+    }
     KOLM_HIP_CHECK(hipEventRecord(ev[4], s));
     if (h_sizes)
         KOLM_HIP_CHECK(hipMemcpyAsync(h_sizes, e.sizes, sizeof(u32) * nb * KOLM_NCAND, hipMemcpyDeviceToHost, s));
     if (h_method) KOLM_HIP_CHECK(hipMemcpyAsync(h_method, e.method, sizeof(u32) * nb, hipMemcpyDeviceToHost, s));
     KOLM_HIP_CHECK(hipMemcpyAsync(c->h_cnt, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
+    std::vector<u32> ntok(want_lz ? nb : 0);
+    if (want_lz) KOLM_HIP_CHECK(hipMemcpyAsync(ntok.data(), z.ntok, sizeof(u32) * nb, hipMemcpyDeviceToHost, s));
     c->sync();
     if (h_off) std::memcpy(h_off, off.data(), sizeof(u64) * (nb + 1));
+    u64 tokens = 0;
+    for (u32 v : ntok) tokens += v;
     if (stats) {
         kolm_stats& st = *stats;
         st = P.st;
+        st.lz_tokens = tokens;
+        c->timing_collect(&st);
+        st.kt[KOLM_KT_LZPARSE].bytes += tokens * 16;
         st.lz_long = c->h_cnt[C_NLONG];
         st.ms_sa = ev_ms(ev[0], ev[1]);
         st.ms_entropy = ev_ms(ev[1], ev[2]);
@@ -431,6 +558,7 @@ int kolm_ctx_destroy(kolm_ctx* c) {
         for (auto& kv : c->bufs)
             if (kv.second.p) KOLM_HIP_CHECK(hipFree(kv.second.p));
         for (auto& e : c->ev) KOLM_HIP_CHECK(hipEventDestroy(e));
+        for (auto& e : c->evpool) KOLM_HIP_CHECK(hipEventDestroy(e));
         KOLM_HIP_CHECK(hipHostFree(c->h_cnt));
         KOLM_HIP_CHECK(hipStreamDestroy(c->stream));
         delete c;
@@ -499,6 +627,13 @@ int kolm_memcpy_d2h(kolm_ctx* c, void* dst, const void* src, uint64_t bytes) {
     });
 }
 
+int kolm_ctx_set_timing(kolm_ctx* c, int enable) {
+    if (!c) return KOLM_EARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->timing = enable != 0;
+    return KOLM_OK;
+}
+
 int kolm_ctx_sync(kolm_ctx* c) {
     if (!c) return KOLM_EARG;
     return guarded([&] {
@@ -548,7 +683,7 @@ int kolm_encode_blocks(const uint8_t* data, const uint64_t* starts, const uint32
         KOLM_HIP_CHECK(hipSetDevice(c->device));
         if (int e = check_geom(total, bs)) return e;
         u8* d = upload(c, data, total);
-        const bool has_raw = cand_mask & 1u;
+        const bool has_raw = (cand_mask & 1u) && force_method == nullptr;
         const u64 dcap = (has_raw ? total : 9 * total) + 64 * (u64)nblocks + 256;
         u8* arena = c->get<u8>("arena", dcap);
         std::vector<u64> off(nblocks + 1);

@@ -90,7 +90,8 @@ struct Lists {
     Seg* next;
     u32* eq_cnt;           // [1] equal-key runs longer than TILE (finalised directly)
     Seg* eq;
-    u32* misc;             // [8] counters: 0 active elements, 1 ...
+    u32* misc;             // [1] active elements of the round
+    u32* cls_elems;        // [NCLASS] elements per small class (timing/bytes bookkeeping)
 };
 
 struct Level {
@@ -98,6 +99,7 @@ struct Level {
     u32* nseg;       // device counter
     LTile* tiles;
     u32* ntiles;     // device counter
+    u32* nelem;      // device counter: elements in the level's segments
 };
 
 // ---- launchers (k_sort.hip) ----

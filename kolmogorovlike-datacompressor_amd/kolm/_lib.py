@@ -35,6 +35,14 @@ class KolmError(RuntimeError):
         self.code = code
 
 
+KT_NAMES = ["classify", "keygen", "msd", "small_sort", "lz_match", "lz_parse", "mtf", "sizes", "emit",
+            "lyndon_gather"]
+
+
+class KTime(ctypes.Structure):
+    _fields_ = [("ms", ctypes.c_double), ("launches", ctypes.c_uint64), ("bytes", ctypes.c_uint64)]
+
+
 class Stats(ctypes.Structure):
     _fields_ = [
         ("lin_rounds", ctypes.c_uint32),
@@ -48,13 +56,15 @@ class Stats(ctypes.Structure):
         ("ms_lz", ctypes.c_double),
         ("ms_entropy", ctypes.c_double),
         ("ms_emit", ctypes.c_double),
-        ("ms_msd_scatter", ctypes.c_double),
-        ("n_msd_scatter", ctypes.c_uint32),
-        ("msd_scatter_elems", ctypes.c_uint64),
+        ("kt", KTime * len(KT_NAMES)),
     ]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "kt"}
+        d["kernels"] = {KT_NAMES[i]: {"ms": self.kt[i].ms, "launches": self.kt[i].launches,
+                                      "bytes": self.kt[i].bytes} for i in range(len(KT_NAMES))
+                        if self.kt[i].launches}
+        return d
 
 
 _lib = None
@@ -87,6 +97,7 @@ SIGNATURES = [
     ("kolm_memcpy_h2d", I32, [P, P, P, U64]),
     ("kolm_memcpy_d2h", I32, [P, P, P, U64]),
     ("kolm_ctx_sync", I32, [P]),
+    ("kolm_ctx_set_timing", I32, [P, I32]),
     ("kolm_encode_blocks_device", I32, [P, P, U64, U32, U32, P, P, U64, P, P, P, P]),
 ]
 

@@ -79,7 +79,7 @@ def mtf_encode(s: bytes) -> bytes:
 
 
 def rice_encode(seq: bytes, k: int = 2) -> bytes:
-    return _call(lib().oracle_rice, seq, len(seq) * 66 // 8 + 16, k)
+    return _call(lib().oracle_rice, seq, (len(seq) * ((255 >> k) + 1 + k) + 7) // 8 + 16, k)
 
 
 def encode_bbwt_mtf_rice(block: bytes, flags: int, k: int = 2) -> bytes:
