@@ -13,12 +13,16 @@
 //     walked from the nearest (= ascending distance);
 //   * k_lz_match: for every position, the best match capped at LZ_CAP bytes (exact when
 //     shorter than the cap; the chain walk stops once the cap is reached);
-//   * k_lz_parse: one wave per block walks the greedy path, 64 positions per window
-//     (Lc/Dc loaded by the 64 lanes, path resolved with uniform readlane steps).  A
-//     position whose capped length hit LZ_CAP ("long") is resolved exactly on the spot:
-//     the wave walks the whole chain and extends each candidate that can still beat the
-//     current best with 64-lane byte compares;
-//   * k_lz_emit: one thread per token writes its bytes at the token's offset.
+//   * the greedy parse is made parallel by speculation: k_lz_spec parses every
+//     LZ_CHUNK-byte chunk with its own wave starting at the chunk start (64-position
+//     windows of Lc/Dc loaded by the lanes and prefetched one window ahead, tokens
+//     buffered in lanes and stored 64 at a time).  k_lz_stitch then walks, per block,
+//     the TRUE path from the real entry of each chunk only until it lands on a position
+//     of that chunk's speculative path (from there both parses are identical because a
+//     token depends on its position only); greedy parses re-synchronise within a few
+//     tokens.  A position whose capped length hit LZ_CAP ("long") is resolved exactly on
+//     the spot (whole chain, candidates extended with 64-lane byte compares);
+//   * k_lz_emit: one thread per token slot writes its bytes at its final offset.
 #include "kolm_internal.h"
 
 namespace kolm {
@@ -59,6 +63,8 @@ __device__ inline u32 uleb_len(u32 v) {
     return n;
 }
 
+__device__ inline u32 tok_bytes(u32 len, u32 dist) { return len ? 1 + uleb_len(len) + uleb_len(dist) : 2; }
+
 // Exact longest match at p (wave-cooperative; all lanes call with identical arguments).
 __device__ void exact_match(const u8* t, const u32* prev3, u32 p, u32 end, u32& out_len, u32& out_dist) {
     const u32 lane = threadIdx.x & 63;
@@ -66,11 +72,10 @@ __device__ void exact_match(const u8* t, const u32* prev3, u32 p, u32 end, u32& 
     const u32 maxl = end - p;
     u32 q = prev3[p];
     while (q != NONE && p - q <= (u32)LZ_WINDOW) {
-        bool cand = true;
         if (best >= maxl) break;  // nothing can be longer
+        bool cand = true;
         if (best > 0) cand = t[p + best] == t[q + best];  // must extend past best
         if (cand) {
-            // LCP(p, q), 64 lanes x 4 bytes per step
             u32 l = 0;
             for (;;) {
                 u32 mism = 0xFFFFFFFFu;
@@ -98,57 +103,160 @@ __device__ void exact_match(const u8* t, const u32* prev3, u32 p, u32 end, u32& 
     out_dist = bd;
 }
 
-// one wave per block
-__global__ __launch_bounds__(64) void k_lz_parse(LzArgs z) {
-    const u32 b = blockIdx.x;
-    const u32 lane = threadIdx.x;
-    const u32 base = z.geo.base(b), end = z.geo.end(b);
-    u32 pos = base;
-    u32 ntok = 0, off = 0, nlong = 0;
-    u32* tp = z.tok_pos + base;
-    u32* tl = z.tok_len + base;
-    u32* td = z.tok_dist + base;
-    u32* to = z.tok_off + base;
-    while (pos < end) {
-        const u32 P = pos + lane;
-        const u32 Lw = P < end ? (u32)z.Lc[P] : 0u;
-        const u32 Dw = P < end ? (u32)z.Dc[P] : 0u;
-        u32 cur = 0;
-        while (cur < 64 && pos + cur < end) {
-            const u32 Lv = __builtin_amdgcn_readlane(Lw, cur);
-            u32 len, dist;
-            if (Lv >= (u32)LZ_CAP) {
-                exact_match(z.text, z.prev3, pos + cur, end, len, dist);
-                ++nlong;
-            } else {
-                len = Lv;
-                dist = __builtin_amdgcn_readlane(Dw, cur);
-            }
-            if (lane == 0) {
-                tp[ntok] = pos + cur;
-                to[ntok] = off;
-                if (len >= (u32)LZ_MIN) {
-                    tl[ntok] = len;
-                    td[ntok] = dist;
-                } else {
-                    tl[ntok] = 0;
-                    td[ntok] = 0;
-                }
-            }
-            ++ntok;
-            if (len >= (u32)LZ_MIN) {
-                off += 1 + uleb_len(len) + uleb_len(dist);
-                cur += len;
-            } else {
-                off += 2;
-                cur += 1;
-            }
+// token at q from its (capped) match record; len 0 = literal
+__device__ inline void token_at(const LzArgs& z, u32 q, u32 end, u32 Lv, u32 Dv, u32& len, u32& dist, u32& nlong) {
+    if (Lv >= (u32)LZ_CAP) {
+        exact_match(z.text, z.prev3, q, end, len, dist);
+        ++nlong;
+    } else {
+        len = Lv;
+        dist = Dv;
+    }
+    if (len < (u32)LZ_MIN) {
+        len = 0;
+        dist = 0;
+    }
+}
+
+// Speculative parse of one chunk per wave (4 waves per workgroup).
+__global__ __launch_bounds__(256) void k_lz_spec(LzArgs z, u32 nchunks) {
+    const u32 lane = threadIdx.x & 63;
+    const u32 c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= nchunks) return;
+    const u32 b = c / z.cpb, k = c - b * z.cpb;
+    const u32 bend = z.geo.end(b);
+    const u32 s = z.geo.base(b) + k * LZ_CHUNK;
+    if (s >= bend) {
+        if (lane == 0) {
+            z.c_ntok[c] = 0;
+            z.c_exit[c] = s;
+            z.c_bytes[c] = 0;
         }
-        pos += cur;
+        return;
+    }
+    const u32 e = min(s + (u32)LZ_CHUNK, bend);
+    u32 wbase = s;
+    u32 P = wbase + lane;
+    u32 Lw = P < bend ? (u32)z.Lc[P] : 0u, Dw = P < bend ? (u32)z.Dc[P] : 0u;
+    P += 64;
+    u32 Ln = P < bend ? (u32)z.Lc[P] : 0u, Dn = P < bend ? (u32)z.Dc[P] : 0u;
+    u32 q = s, ntok = 0, off = 0, nlong = 0, nbuf = 0;
+    u32 bpos = 0, blen = 0, bdist = 0, boff = 0;
+    while (q < e) {
+        if (q >= wbase + 64) {
+            if (q < wbase + 128) {
+                Lw = Ln;
+                Dw = Dn;
+                wbase += 64;
+            } else {
+                wbase = q;
+                const u32 P0 = wbase + lane;
+                Lw = P0 < bend ? (u32)z.Lc[P0] : 0u;
+                Dw = P0 < bend ? (u32)z.Dc[P0] : 0u;
+            }
+            const u32 P1 = wbase + 64 + lane;
+            Ln = P1 < bend ? (u32)z.Lc[P1] : 0u;
+            Dn = P1 < bend ? (u32)z.Dc[P1] : 0u;
+        }
+        const u32 cur = q - wbase;
+        const u32 Lv = __builtin_amdgcn_readlane(Lw, cur);
+        const u32 Dv = __builtin_amdgcn_readlane(Dw, cur);
+        u32 len, dist;
+        token_at(z, q, bend, Lv, Dv, len, dist, nlong);
+        if (lane == nbuf) {
+            bpos = q;
+            blen = len;
+            bdist = dist;
+            boff = off;
+        }
+        if (++nbuf == 64) {
+            const u32 slot = s + ntok + 1 - 64 + lane;
+            z.tok_pos[slot] = bpos;
+            z.tok_len[slot] = blen;
+            z.tok_dist[slot] = bdist;
+            z.tok_off[slot] = boff;
+            nbuf = 0;
+        }
+        ++ntok;
+        off += tok_bytes(len, dist);
+        q += len ? len : 1;
+    }
+    if (lane < nbuf) {
+        const u32 slot = s + ntok - nbuf + lane;
+        z.tok_pos[slot] = bpos;
+        z.tok_len[slot] = blen;
+        z.tok_dist[slot] = bdist;
+        z.tok_off[slot] = boff;
     }
     if (lane == 0) {
-        z.ntok[b] = ntok;
-        z.lz_size[b] = off;
+        z.c_ntok[c] = ntok;
+        z.c_exit[c] = q;
+        z.c_bytes[c] = off;
+        if (nlong) atomicAdd(z.nlong, nlong);
+    }
+}
+
+// Per block (one wave): real chunk entries, fix-up tokens, chunk output offsets, size.
+__global__ __launch_bounds__(64) void k_lz_stitch(LzArgs z) {
+    const u32 b = blockIdx.x;
+    const u32 lane = threadIdx.x;
+    const u32 base = z.geo.base(b), bend = z.geo.end(b);
+    u32 entry = base, boff = 0, ntot = 0, fi = 0, nlong = 0;
+    for (u32 k = 0; k < z.cpb; ++k) {
+        const u32 c = b * z.cpb + k;
+        const u32 s = base + k * LZ_CHUNK;
+        if (s >= bend) break;
+        const u32 e = min(s + (u32)LZ_CHUNK, bend);
+        const u32 nt = z.c_ntok[c];
+        u32 first, nfix = 0, fixbytes = 0, next;
+        const u32 fix0 = base + fi;
+        if (entry == s) {
+            first = 0;
+            next = z.c_exit[c];
+        } else if (entry >= e) {
+            first = nt;
+            next = entry;
+        } else {
+            u32 q = entry, j = 0;
+            bool conv = false;
+            while (q < e) {
+                while (j < nt && z.tok_pos[s + j] < q) ++j;
+                if (j < nt && z.tok_pos[s + j] == q) {
+                    conv = true;
+                    break;
+                }
+                u32 len, dist;
+                token_at(z, q, bend, z.Lc[q], z.Dc[q], len, dist, nlong);
+                if (lane == 0) {
+                    z.fix_pos[base + fi] = q;
+                    z.fix_len[base + fi] = len;
+                    z.fix_dist[base + fi] = dist;
+                    z.fix_off[base + fi] = boff + fixbytes;
+                }
+                ++fi;
+                ++nfix;
+                fixbytes += tok_bytes(len, dist);
+                q += len ? len : 1;
+            }
+            first = conv ? j : nt;
+            next = conv ? z.c_exit[c] : q;
+        }
+        const u32 spec_bytes = first < nt ? z.c_bytes[c] - z.tok_off[s + first] : 0u;
+        if (lane == 0) {
+            z.c_first[c] = first;
+            z.c_fix0[c] = fix0;
+            z.c_nfix[c] = nfix;
+            z.c_fixbytes[c] = fixbytes;
+            z.c_off[c] = boff;
+        }
+        boff += fixbytes + spec_bytes;
+        ntot += nfix + (nt - first);
+        entry = next;
+    }
+    if (lane == 0) {
+        z.lz_size[b] = boff;
+        z.ntok[b] = ntot;
+        z.b_nfix[b] = fi;
         if (nlong) atomicAdd(z.nlong, nlong);
     }
 }
@@ -167,26 +275,36 @@ __device__ inline u32 put_uleb(u8* d, u32 v) {
     }
 }
 
+__device__ inline void write_token(u8* d, const u8* text, u32 pos, u32 len, u32 dist) {
+    if (len == 0) {
+        d[0] = 0;
+        d[1] = text[pos];
+    } else {
+        d[0] = 1;
+        const u32 n1 = put_uleb(d + 1, len);
+        put_uleb(d + 1 + n1, dist);
+    }
+}
+
+// One thread per token slot g: speculative token (slot in its chunk) and fix-up token.
 __global__ __launch_bounds__(256) void k_lz_emit(LzArgs z, const u32* method, const u64* off, u8* arena,
                                                  int force_all) {
-    const u32 b = blockIdx.y;
+    const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= z.geo.N) return;
+    const u32 b = z.geo.block_of(g);
     if (!force_all && method[b] != 7u) return;
-    const u32 nt = z.ntok[b];
     const u32 base = z.geo.base(b);
     u8* dst = arena + off[b];
-    for (u32 t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
-        const u32 o = z.tok_off[base + t];
-        const u32 len = z.tok_len[base + t];
-        u8* d = dst + o;
-        if (len == 0) {
-            d[0] = 0;
-            d[1] = z.text[z.tok_pos[base + t]];
-        } else {
-            d[0] = 1;
-            const u32 n1 = put_uleb(d + 1, len);
-            put_uleb(d + 1 + n1, z.tok_dist[base + t]);
-        }
+    const u32 k = (g - base) / LZ_CHUNK;
+    const u32 c = b * z.cpb + k;
+    const u32 s = base + k * LZ_CHUNK;
+    const u32 i = g - s;
+    const u32 first = z.c_first[c];
+    if (i >= first && i < z.c_ntok[c]) {
+        const u32 o = z.c_off[c] + z.c_fixbytes[c] + (z.tok_off[g] - z.tok_off[s + first]);
+        write_token(dst + o, z.text, z.tok_pos[g], z.tok_len[g], z.tok_dist[g]);
     }
+    if (g - base < z.b_nfix[b]) write_token(dst + z.fix_off[g], z.text, z.fix_pos[g], z.fix_len[g], z.fix_dist[g]);
 }
 
 }  // namespace
@@ -198,13 +316,14 @@ void launch_lz_match(const LzArgs& z, hipStream_t s) {
 
 void launch_lz_parse(const LzArgs& z, hipStream_t s) {
     if (!z.geo.nb) return;
-    k_lz_parse<<<z.geo.nb, 64, 0, s>>>(z);
+    const u32 nchunks = z.cpb * z.geo.nb;
+    k_lz_spec<<<(nchunks + 3) / 4, 256, 0, s>>>(z, nchunks);
+    k_lz_stitch<<<z.geo.nb, 64, 0, s>>>(z);
 }
 
 void launch_lz_emit(const LzArgs& z, const u32* method, const u64* off, u8* arena, hipStream_t s) {
-    if (!z.geo.nb) return;
-    dim3 grid(64, z.geo.nb);
-    k_lz_emit<<<grid, 256, 0, s>>>(z, method, off, arena, method == nullptr ? 1 : 0);
+    if (!z.geo.N) return;
+    k_lz_emit<<<(u32)((z.geo.N + 255) / 256), 256, 0, s>>>(z, method, off, arena, method == nullptr ? 1 : 0);
 }
 
 }  // namespace kolm

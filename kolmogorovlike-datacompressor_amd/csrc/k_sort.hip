@@ -233,16 +233,31 @@ __global__ __launch_bounds__(WG) void k_msd_scan(const LSeg* segs, SortArgs a, u
     __shared__ u32 sh[WG / 64];
     const LSeg s = segs[blockIdx.x];
     const u32 d = threadIdx.x;
+    // pass 1: per-digit totals (16 independent loads in flight per thread)
+    constexpr u32 B = 16;
+    const u32 t0 = s.tile_base, t1 = s.tile_base + s.ntiles;
     u32 run = 0;
-    for (u32 t = s.tile_base; t < s.tile_base + s.ntiles; ++t) {
-        const u64 ix = (u64)t * 256 + d;
-        const u32 v = hist[ix];
-        hist[ix] = run;
-        run += v;
+    for (u32 t = t0; t < t1; t += B) {
+        u32 v[B];
+#pragma unroll
+        for (u32 j = 0; j < B; ++j) v[j] = t + j < t1 ? hist[(u64)(t + j) * 256 + d] : 0u;
+#pragma unroll
+        for (u32 j = 0; j < B; ++j) run += v[j];
     }
     const u32 bstart = wg_excl_scan<false>(run, OpAdd(), 0u, sh);
     const u32 abs0 = s.start + bstart;
-    for (u32 t = s.tile_base; t < s.tile_base + s.ntiles; ++t) hist[(u64)t * 256 + d] += abs0;
+    // pass 2: absolute scatter base of every (tile, digit)
+    u32 acc = abs0;
+    for (u32 t = t0; t < t1; t += B) {
+        u32 v[B];
+#pragma unroll
+        for (u32 j = 0; j < B; ++j) v[j] = t + j < t1 ? hist[(u64)(t + j) * 256 + d] : 0u;
+#pragma unroll
+        for (u32 j = 0; j < B; ++j) {
+            if (t + j < t1) hist[(u64)(t + j) * 256 + d] = acc;
+            acc += v[j];
+        }
+    }
     const int nonzero = __syncthreads_count(run > 0);
     if (nonzero > 1 && d == 0) a.blk_split[a.geo.block_of(s.start)] = 1;
     if (run == 0) return;

@@ -346,6 +346,21 @@ struct Pipeline {
         z.tok_len = c->get<u32>("tok_len", N);
         z.tok_dist = c->get<u32>("tok_dist", N);
         z.tok_off = c->get<u32>("tok_off", N);
+        z.fix_pos = c->get<u32>("fix_pos", N);
+        z.fix_len = c->get<u32>("fix_len", N);
+        z.fix_dist = c->get<u32>("fix_dist", N);
+        z.fix_off = c->get<u32>("fix_off", N);
+        z.cpb = (geo.bs + LZ_CHUNK - 1) / LZ_CHUNK;
+        const u64 nch = (u64)z.cpb * geo.nb + 1;
+        z.c_ntok = c->get<u32>("c_ntok", nch);
+        z.c_exit = c->get<u32>("c_exit", nch);
+        z.c_bytes = c->get<u32>("c_bytes", nch);
+        z.c_first = c->get<u32>("c_first", nch);
+        z.c_fix0 = c->get<u32>("c_fix0", nch);
+        z.c_nfix = c->get<u32>("c_nfix", nch);
+        z.c_fixbytes = c->get<u32>("c_fixbytes", nch);
+        z.c_off = c->get<u32>("c_off", nch);
+        z.b_nfix = c->get<u32>("b_nfix", geo.nb);
         z.ntok = c->get<u32>("ntok", geo.nb);
         z.lz_size = c->get<u32>("lz_size", geo.nb);
         z.nlong = c->get<u32>("counters", C_N) + C_NLONG;

@@ -159,19 +159,37 @@ void launch_rice_only(const Geom& geo, const u8* in, int k, u8* out, u32* tile_t
                       u32* out_size, hipStream_t s);
 
 // ---- k_lz77.hip ----
+constexpr int LZ_CHUNK = 8192;  // speculative-parse chunk (one wave each)
+
 struct LzArgs {
     Geom geo;
     const u8* text;
     const u32* prev3;
     u8* Lc;            // capped match length (LZ_CAP = long)
     u16* Dc;           // distance of the capped best match
-    u32* tok_pos;      // [N] token start positions (per block region)
+    // speculative tokens of chunk c live in slots [chunk start, chunk start + ntok[c])
+    u32* tok_pos;      // [N] token start position
     u32* tok_len;      // [N] match length (0 = literal)
-    u32* tok_dist;
-    u32* tok_off;      // [N] output byte offset of each token within the block payload
-    u32* ntok;         // [nb]
+    u32* tok_dist;     // [N] match distance
+    u32* tok_off;      // [N] byte offset of the token inside its chunk's speculative stream
+    // fix-up tokens (true path from the real chunk entry until it meets the speculative path)
+    u32* fix_pos;      // [N]
+    u32* fix_len;      // [N]
+    u32* fix_dist;     // [N]
+    u32* fix_off;      // [N] byte offset inside the chunk's output
+    u32* c_ntok;       // [nchunks] speculative token count
+    u32* c_exit;       // [nchunks] first path position >= chunk end
+    u32* c_bytes;      // [nchunks] speculative stream bytes
+    u32* c_first;      // [nchunks] first speculative token on the true path
+    u32* c_fix0;       // [nchunks] index of the first fix-up token (fix_* arrays)
+    u32* c_nfix;       // [nchunks]
+    u32* c_fixbytes;   // [nchunks]
+    u32* c_off;        // [nchunks] byte offset of the chunk's output in the block payload
+    u32* b_nfix;       // [nb] fix-up tokens of the block (fix_* slots [base, base + b_nfix))
+    u32* ntok;         // [nb] total tokens of the block
     u32* lz_size;      // [nb] stream size
     u32* nlong;        // [1]
+    u32 cpb;           // chunks per block
 };
 void launch_lz_match(const LzArgs& z, hipStream_t s);
 void launch_lz_parse(const LzArgs& z, hipStream_t s);

@@ -1,0 +1,119 @@
+"""Host-side product logic (no GPU): input generators, KOLR container writer/reader,
+host decoders, candidate registry semantics."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import kolm
+from kolm import container, datagen as D, decode
+from kolm.parallel import shard_blocks
+
+
+@pytest.mark.parametrize("name", sorted(D.REFERENCE_FILES))
+def test_reference_file_regenerators(name):
+    data = D.REFERENCE_FILES[name]()
+    assert hashlib.sha256(data).hexdigest() == D.REFERENCE_SHA256[name]
+
+
+def test_enwik_deterministic():
+    a = D.enwik_like(1 << 20)
+    b = D.enwik_like(1 << 20)
+    assert a == b and len(a) == 1 << 20
+    assert hashlib.sha256(a).hexdigest() == hashlib.sha256(D.enwik_like(1 << 20, seed=D.ENWIK_SEED)).hexdigest()
+    assert D.enwik_like(1 << 16, seed=1) != D.enwik_like(1 << 16, seed=2)
+    h = np.bincount(np.frombuffer(a, np.uint8), minlength=256) / len(a)
+    h = h[h > 0]
+    assert 3.5 < float(-(h * np.log2(h)).sum()) < 4.5  # text-like order-0 entropy
+
+
+def test_container_roundtrip_goldens(golden_containers, manifest):
+    """Our TOC writer re-serialises every PY container byte-for-byte; our decoders
+    decompress every PY container (full candidate list, incl. Re-Pair blocks)."""
+    for cname in manifest["containers"]:
+        for kind in ("full", "ids0_8"):
+            blob = golden_containers[f"{cname}/{kind}"].tobytes()
+            inp = golden_containers[f"{cname}/input"].tobytes()
+            mode, sz, tot, mids, orig, pays = container.read_container(blob)
+            assert container.write_container(mode, sz, tot, mids, orig, pays) == blob
+            assert kolm.decompress(blob) == inp
+
+
+def test_container_errors():
+    with pytest.raises(ValueError):
+        kolm.decompress(b"NOPE" + bytes(20))
+    blob = container.write_container(container.MODE_FIXED, 4, 3, [0], [3], [b"abc"])
+    with pytest.raises(ValueError):
+        kolm.decompress(blob + b"\x00")  # strict trailing-bytes check (PY:2545-2547)
+    import struct
+    with pytest.raises(struct.error):
+        container.write_container(container.MODE_FIXED, 1, 70000, [0] * 70000, [1] * 70000, [b"a"] * 70000)
+
+
+def test_huffman_ties_many_ids():
+    """>= 3 distinct run symbols exercise PY's heapq tie behaviour (App. C.6)."""
+    ids = [7, 7, 2, 0, 0, 0, 2, 6, 6, 1, 7, 8, 8, 2, 7]
+    pays = [bytes([i]) * (i + 1) for i in range(len(ids))]
+    blob = container.write_container(container.MODE_FIXED, 16, 16 * (len(ids) - 1) + 5, ids,
+                                     [16] * (len(ids) - 1) + [5], pays)
+    _, _, _, mids, orig, p2 = container.read_container(blob)
+    assert mids == ids and p2 == pays
+
+
+@pytest.mark.parametrize("name", ["text_hobbit", "banana", "tiny07", "zero16k", "enwik16k", "abab"])
+def test_host_decoders_invert_golden_kernels(golden_kernels, name):
+    g = lambda k: golden_kernels[f"{name}/{k}"].tobytes()  # noqa: E731
+    inp = g("input")
+    assert decode.bbwt_inverse(g("bbwt")) == inp
+    assert decode.mtf_decode(list(g("mtf"))) == g("bbwt")
+    for mid, f in decode.BBWT_FLAGS.items():
+        assert decode.decode_bbwt_mtf_rice(g(f"rice{f}"), len(inp), f) == inp
+    assert decode.decode_lz77(g("lz77"), len(inp)) == inp
+    assert decode.decode_xor(g("xor"), len(inp)) == inp
+    assert decode.decode_lfsr(g("lfsr"), len(inp)) == inp
+    assert decode.repair_decompress(g("repair"), len(inp)) == inp
+
+
+def test_fixed_boundaries_matches_reference_semantics():
+    assert kolm.fixed_boundaries(b"", 4) == []
+    assert kolm.fixed_boundaries(b"abcdefghij", 4) == [(0, 4), (4, 8), (8, 10)]
+    with pytest.raises(ValueError):
+        kolm.fixed_boundaries(b"ab", 0)
+
+
+def test_registry_ids_stable():
+    names = [n for _, n in kolm._select_encoders()]
+    assert names == kolm.CANDIDATE_NAMES
+    assert len(kolm._select_decoders()) == 10
+    kolm.G_NO_LZ77 = True
+    try:
+        assert kolm.candidate_mask() == 0x1FF & ~(1 << 7)
+        assert [n for _, n in kolm._select_encoders()] == kolm.CANDIDATE_NAMES  # ids unchanged
+    finally:
+        kolm.G_NO_LZ77 = False
+    kolm.G_ONLY_METHOD = "lz77"
+    try:
+        assert kolm.candidate_mask() == 1 << 7
+    finally:
+        kolm.G_ONLY_METHOD = None
+    with pytest.raises(NameError):
+        kolm._select_encoders()[10][0](b"x")  # v2_new raises as in PY
+
+
+@pytest.mark.parametrize("nb,world", [(0, 2), (1, 2), (7, 2), (256, 8), (5, 8), (1000, 3)])
+def test_shard_blocks_cover(nb, world):
+    seen = []
+    for r in range(world):
+        f, c = shard_blocks(nb, r, world)
+        seen.extend(range(f, f + c))
+    assert seen == list(range(nb))
+    counts = [shard_blocks(nb, r, world)[1] for r in range(world)]
+    assert max(counts) - min(counts) <= 1
+
+
+def test_uleb128():
+    for v in [0, 1, 127, 128, 255, 16383, 16384, 2 ** 31]:
+        b = kolm.uleb128_encode(v)
+        assert kolm.uleb128_decode_stream(b, 0) == (v, len(b))
+    with pytest.raises(ValueError):
+        kolm.uleb128_encode(-1)

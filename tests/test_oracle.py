@@ -1,0 +1,83 @@
+"""Pin the oracle (faithful CPU restatement, oracle/kolm_oracle.cpp) to the reference:
+every golden vector produced by importing PY (tests/golden/kernels.npz, containers.npz)
+and PY's own 1 MiB-class known answers (tests/golden/large.json)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle as O
+from kolm import datagen as D
+
+FLAGS = (0, 1, 4, 8, 16)
+
+
+def test_oracle_kernels_vs_py_goldens(golden_kernels, manifest):
+    bad = []
+    for name in manifest["kernels"]:
+        inp = golden_kernels[f"{name}/input"].tobytes()
+        got = {
+            "bbwt": O.bbwt_forward(inp),
+            "lz77": O.encode_lz77(inp),
+            "xor": O.encode_xor(inp),
+            "lfsr": O.encode_lfsr(inp),
+            "repair": O.repair_compress(inp),
+        }
+        got["mtf"] = O.mtf_encode(got["bbwt"])
+        for f in FLAGS:
+            got[f"rice{f}"] = O.encode_bbwt_mtf_rice(inp, f)
+        for k, v in got.items():
+            if golden_kernels[f"{name}/{k}"].tobytes() != v:
+                bad.append((name, k))
+        duv = golden_kernels[f"{name}/duval"].view("<i8").reshape(-1, 2)
+        if list(duv[:, 0]) != O.duval_starts(inp):
+            bad.append((name, "duval"))
+    assert not bad, bad
+
+
+def test_oracle_containers_vs_py(golden_containers, manifest):
+    for cname, e in manifest["containers"].items():
+        inp = golden_containers[f"{cname}/input"].tobytes()
+        assert O.compress_blocks_fixed(inp, e["block_size"], range(9)) == golden_containers[f"{cname}/ids0_8"].tobytes(), cname
+        assert O.compress_blocks_fixed(inp, e["block_size"], range(10)) == golden_containers[f"{cname}/full"].tobytes(), cname
+
+
+LARGE = {
+    "gradient_1m": lambda: D.gradient_bmp()[: 1 << 20],
+    "pattern_1m": lambda: D.pattern_blocks(),
+    "checker_full": lambda: D.checker_bmp(),
+    "sine_full": lambda: D.sine_wav(),
+    "enwik_256k": lambda: D.enwik_like(1 << 18),
+}
+
+
+@pytest.mark.parametrize("case", sorted(LARGE))
+def test_oracle_large_known_answers(large_known, case):
+    sha = lambda b: hashlib.sha256(b).hexdigest()  # noqa: E731
+    data = LARGE[case]()
+    ref = large_known[case]
+    assert sha(data) == ref["input"]["sha256"]
+    bw = O.bbwt_forward(data)
+    assert sha(bw) == ref["bbwt"]["sha256"]
+    mt = O.mtf_encode(bw)
+    assert sha(mt) == ref["mtf"]["sha256"]
+    assert sha(O.rice_encode(mt, 2)) == ref["rice0"]["sha256"]
+    if "lz77" in ref:
+        z = O.encode_lz77(data)
+        assert (len(z), sha(z)) == (ref["lz77"]["len"], ref["lz77"]["sha256"])
+
+
+def test_survey_lengths_gradient_lz77():
+    """gradient[0:1 MiB] LZ77 stream is 1693900 bytes (reference C++,
+    identical to PY); our restatement reproduces the length."""
+    z = O.encode_lz77(D.gradient_bmp()[: 1 << 20])
+    assert len(z) == 1693900
+
+
+def test_oracle_rice_params_small():
+    rng = np.random.default_rng(0)
+    seq = rng.integers(0, 256, 300).astype(np.uint8).tobytes()
+    for k in range(0, 8):
+        out = O.rice_encode(seq, k)
+        bits = sum((v >> k) + 1 + k for v in seq)
+        assert len(out) == (bits + 7) // 8
