@@ -151,7 +151,7 @@ __global__ __launch_bounds__(WG) void k_tile_starts(TileGeom tg, const u8* flag,
 
 // Phase C': FS = last start <= p, FL = (next start > p, or block end) - FS.
 __global__ __launch_bounds__(WG) void k_fsfl(TileGeom tg, const u8* flag, const u32* cmax,
-                                             const u32* cmin, u32* FS, u32* FL) {
+                                             const u32* cmin, u64* FSL) {
     __shared__ u32 sh[WG / 64];
     u32 lo, hi, b;
     if (!tg.range(blockIdx.x, lo, hi, b)) return;
@@ -181,26 +181,134 @@ __global__ __launch_bounds__(WG) void k_fsfl(TileGeom tg, const u8* flag, const 
         const u32 i = i0 + e;
         if (i < hi) {
             const u32 end = fe == BIG ? bend : fe;
-            FS[i] = fsv[e];
-            FL[i] = end - fsv[e];
+            FSL[i] = (u64)fsv[e] | ((u64)(end - fsv[e]) << 32);  // factor start | length << 32
         }
         if (f[e]) fe = i0 + e;
     }
 }
 
-__global__ void k_bbwt_gather(Geom geo, const u8* text, const u32* SA, const u32* FS, const u32* FL,
-                              u8* out) {
+// ---------------------------------------------------------------------------------
+// Parallel Duval (restates PY:326-349 exactly): Duval on every DUVAL_CHUNK-byte chunk
+// (one thread each), then one wave per block merges the chunk factorizations left to
+// right with the concatenation rule: for Lyndon words x < y, xy is Lyndon, so pushing
+// the next chunk's factors on the stack of the prefix's factors and merging while
+// stack[-2] < stack[-1] yields the (unique) Lyndon factorization of the concatenation;
+// once a right factor is pushed without merging the remaining right factors (which are
+// non-increasing) cannot merge either and are appended in bulk.
+// ---------------------------------------------------------------------------------
+constexpr u32 DUVAL_CHUNK = 4096;
+
+__global__ __launch_bounds__(256) void k_duval_chunks(Geom geo, u32 cpb, const u8* s, u32* fstart, u32* nfac,
+                                                      u32 nchunks) {
+    const u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchunks) return;
+    const u32 b = c / cpb, k = c - b * cpb;
+    const u32 lo = geo.base(b) + k * DUVAL_CHUNK;
+    const u32 e = geo.end(b);
+    if (lo >= e) {
+        nfac[c] = 0;
+        return;
+    }
+    const u32 hi = min(lo + DUVAL_CHUNK, e);
+    u32 i = lo, nf = 0;
+    while (i < hi) {
+        u32 j = i + 1, kk = i;
+        while (j < hi) {
+            const u8 a = s[kk], bb = s[j];
+            if (a > bb) break;
+            kk = (a < bb) ? i : kk + 1;
+            ++j;
+        }
+        const u32 p = j - kk;
+        while (i <= kk) {
+            fstart[lo + nf++] = i;
+            i += p;
+        }
+    }
+    nfac[c] = nf;
+}
+
+// x = s[a0, a1) < y = s[a1, b1) lexicographically (proper prefix smaller); wave-uniform
+__device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1) {
+    const u32 lane = threadIdx.x & 63;
+    const u32 la = a1 - a0, lb = b1 - a1, m = min(la, lb);
+    for (u32 o = 0; o < m; o += 64) {
+        const u32 t = o + lane;
+        const bool diff = t < m && s[a0 + t] != s[a1 + t];
+        const u64 bal = __ballot(diff);
+        if (bal) {
+            const u32 d = o + (__ffsll((long long)bal) - 1);
+            return s[a0 + d] < s[a1 + d];
+        }
+    }
+    return la < lb;
+}
+
+__global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8* s, const u32* fstart,
+                                                    const u32* nfac, u32* stack, u8* flag) {
+    const u32 b = blockIdx.x, lane = threadIdx.x;
+    const u32 base = geo.base(b), end = geo.end(b);
+    volatile u32* stk = stack + base;  // written by lane 0, re-read uniformly: bypass the scalar cache
+    u32 sp = 0;
+    for (u32 k = 0; k < cpb; ++k) {
+        const u32 c = b * cpb + k;
+        const u32 lo = base + k * DUVAL_CHUNK;
+        if (lo >= end) break;
+        const u32 hi = min(lo + DUVAL_CHUNK, end);
+        const u32 nf = nfac[c];
+        u32 t = 0;
+        while (t < nf) {
+            const u32 r = fstart[lo + t];
+            const u32 frontier = (t + 1 < nf) ? fstart[lo + t + 1] : hi;
+            if (lane == 0) stk[sp] = r;
+            __builtin_amdgcn_s_waitcnt(0);
+            ++sp;
+            bool merged = false;
+            while (sp >= 2) {
+                const u32 a0 = stk[sp - 2], a1 = stk[sp - 1];
+                if (!lyn_less(s, a0, a1, frontier)) break;
+                --sp;  // stack[-2] absorbs the top factor
+                merged = true;
+            }
+            ++t;
+            if (!merged) break;
+        }
+        // remaining right factors cannot merge: append in bulk
+        for (u32 o = t; o < nf; o += 64) {
+            const u32 idx = o + lane;
+            if (idx < nf) stk[sp + (idx - t)] = fstart[lo + idx];
+        }
+        if (t < nf) sp += nf - t;
+        __builtin_amdgcn_s_waitcnt(0);
+    }
+    for (u32 i = lane; i < sp; i += 64) flag[stk[i]] = 1;
+}
+
+__global__ void k_bbwt_gather(Geom geo, const u8* text, const u32* SA, const u64* FSL, u8* out) {
     for (u32 g = blockIdx.x * blockDim.x + threadIdx.x; g < geo.N; g += gridDim.x * blockDim.x) {
         const u32 p = SA[g];
-        const u32 fs = FS[p];
-        out[g] = text[p == fs ? fs + FL[p] - 1 : p - 1];
+        const u64 f = FSL[p];
+        const u32 fs = (u32)f;
+        out[g] = text[p == fs ? fs + (u32)(f >> 32) - 1 : p - 1];
     }
 }
 
 }  // namespace
 
-void launch_lyndon(const Geom& geo, const u32* RK, u8* flag, u32* FS, u32* FL, u32* tile_tmp,
-                   u32* tile_tmp2, hipStream_t s) {
+// Lyndon factor starts by the ISA left-to-right-minima rule (needs a complete linear
+// suffix order in RK); kept as an alternative to the parallel Duval path.
+void launch_lyndon_isa(const Geom& geo, const u32* RK, u8* flag, u32* tile_tmp, u32* tile_tmp2, hipStream_t s) {
+    if (!geo.N) return;
+    TileGeom tg{geo, (geo.bs + TILE - 1) / TILE};
+    const u32 nt = tg.tpb * geo.nb;
+    k_tile_min_rk<<<nt, WG, 0, s>>>(tg, RK, tile_tmp);
+    k_tiles_scan<false, false><<<geo.nb, WG, 0, s>>>(tile_tmp, tile_tmp + nt, tg.tpb, BIG);
+    k_lyn_flags<<<nt, WG, 0, s>>>(tg, RK, tile_tmp + nt, flag);
+}
+
+// Lyndon factorisation of every block (parallel Duval + merge) -> per-position FSL.
+void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u32* fstart, u32* nfac, u32* stack,
+                   u32* tile_tmp, u32* tile_tmp2, hipStream_t s) {
     if (!geo.N) return;
     TileGeom tg{geo, (geo.bs + TILE - 1) / TILE};
     const u32 nt = tg.tpb * geo.nb;
@@ -208,20 +316,22 @@ void launch_lyndon(const Geom& geo, const u32* RK, u8* flag, u32* FS, u32* FL, u
     u32* B = tile_tmp + nt;   // [nt]
     u32* C2 = tile_tmp2;      // [nt]
     u32* D = tile_tmp2 + nt;  // [nt]
-    k_tile_min_rk<<<nt, WG, 0, s>>>(tg, RK, A);
-    k_tiles_scan<false, false><<<geo.nb, WG, 0, s>>>(A, B, tg.tpb, BIG);
-    k_lyn_flags<<<nt, WG, 0, s>>>(tg, RK, B, flag);
+    const u32 cpb = (geo.bs + DUVAL_CHUNK - 1) / DUVAL_CHUNK;
+    const u32 nch = cpb * geo.nb;
+    KOLM_HIP_CHECK(hipMemsetAsync(flag, 0, geo.N, s));
+    k_duval_chunks<<<(nch + 255) / 256, 256, 0, s>>>(geo, cpb, text, fstart, nfac, nch);
+    k_duval_merge<<<geo.nb, 64, 0, s>>>(geo, cpb, text, fstart, nfac, stack, flag);
     k_tile_starts<<<nt, WG, 0, s>>>(tg, flag, A, C2);
     k_tiles_scan<false, true><<<geo.nb, WG, 0, s>>>(A, B, tg.tpb, 0u);
     k_tiles_scan<true, false><<<geo.nb, WG, 0, s>>>(C2, D, tg.tpb, BIG);
-    k_fsfl<<<nt, WG, 0, s>>>(tg, flag, B, D, FS, FL);
+    k_fsfl<<<nt, WG, 0, s>>>(tg, flag, B, D, FSL);
 }
 
-void launch_bbwt_gather(const Geom& geo, const u8* text, const u32* SA, const u32* FS, const u32* FL,
-                        u8* out, hipStream_t s) {
+void launch_bbwt_gather(const Geom& geo, const u8* text, const u32* SA, const u64* FSL, u8* out,
+                        hipStream_t s) {
     if (!geo.N) return;
     const u32 grid = (u32)std::min<u64>((geo.N + 255) / 256, 65535);
-    k_bbwt_gather<<<grid, 256, 0, s>>>(geo, text, SA, FS, FL, out);
+    k_bbwt_gather<<<grid, 256, 0, s>>>(geo, text, SA, FSL, out);
 }
 
 }  // namespace kolm

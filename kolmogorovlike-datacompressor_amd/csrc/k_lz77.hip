@@ -7,52 +7,27 @@
 // best >= 3 emits [1][ULEB len][ULEB dist], otherwise [0][byte].
 //
 // GPU formulation (bit-exact):
-//   * any match >= 3 starts with an equal 3-gram, so the candidates are exactly the
-//     previous occurrences of p's 3-gram inside the window: the chain prev3[] read off
-//     the linear suffix array right after its 3-character round (k_sort.hip k_prev3),
-//     walked from the nearest (= ascending distance);
-//   * k_lz_match: for every position, the best match capped at LZ_CAP bytes (exact when
-//     shorter than the cap; the chain walk stops once the cap is reached);
-//   * the greedy parse is made parallel by speculation: k_lz_spec parses every
-//     LZ_CHUNK-byte chunk with its own wave starting at the chunk start (64-position
-//     windows of Lc/Dc loaded by the lanes and prefetched one window ahead, tokens
-//     buffered in lanes and stored 64 at a time).  k_lz_stitch then walks, per block,
-//     the TRUE path from the real entry of each chunk only until it lands on a position
-//     of that chunk's speculative path (from there both parses are identical because a
-//     token depends on its position only); greedy parses re-synchronise within a few
-//     tokens.  A position whose capped length hit LZ_CAP ("long") is resolved exactly on
-//     the spot (whole chain, candidates extended with 64-lane byte compares);
+//   * any match >= 3 starts with an equal 3-gram, so the candidates of p are exactly the
+//     earlier members of p's 3-gram group inside the window.  Round 0 of the linear
+//     suffix sort (k_sort.hip) sorts positions by (3-gram, position): in that array SA3
+//     p's candidates are the CONTIGUOUS slots idx3[p]-1, idx3[p]-2, ... down to the group
+//     start gs3[p], in ascending distance — no pointer chasing;
+//   * matches are computed lazily, only at positions on the parse path, by a whole wave:
+//     64 lanes score 64 candidates at once (capped byte compare; later batches first
+//     test whether a candidate can beat the current best at offset `best`); the
+//     winner is a wave max-reduction of (length, -distance).  Candidates reaching the
+//     cap are extended exactly with 64-lane compares (no length limit, as PY);
+//   * the greedy parse is parallel by speculation: k_lz_spec parses every LZ_CHUNK-byte
+//     chunk with its own wave from the chunk start; k_lz_stitch walks, per block, the
+//     TRUE path from each chunk's real entry only until it lands on a position of that
+//     chunk's speculative path (a token depends on its position only, so both parses
+//     coincide from there); greedy parses re-synchronise within a few tokens;
 //   * k_lz_emit: one thread per token slot writes its bytes at its final offset.
 #include "kolm_internal.h"
 
 namespace kolm {
 
 namespace {
-
-__global__ __launch_bounds__(256) void k_lz_match(LzArgs z) {
-    const u32 p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= z.geo.N) return;
-    const u32 b = z.geo.block_of(p);
-    const u32 end = z.geo.end(b);
-    const u8* t = z.text;
-    u32 best = 0, bd = 0;
-    if (p + (u32)LZ_MIN <= end) {
-        const u32 maxl = min((u32)LZ_CAP, end - p);
-        u32 q = z.prev3[p];
-        while (q != NONE && p - q <= (u32)LZ_WINDOW) {
-            u32 l = LZ_MIN;
-            while (l < maxl && t[p + l] == t[q + l]) ++l;
-            if (l > best) {
-                best = l;
-                bd = p - q;
-                if (l >= maxl) break;
-            }
-            q = z.prev3[q];
-        }
-    }
-    z.Lc[p] = (u8)best;
-    z.Dc[p] = (u16)bd;
-}
 
 __device__ inline u32 uleb_len(u32 v) {
     u32 n = 1;
@@ -65,57 +40,80 @@ __device__ inline u32 uleb_len(u32 v) {
 
 __device__ inline u32 tok_bytes(u32 len, u32 dist) { return len ? 1 + uleb_len(len) + uleb_len(dist) : 2; }
 
-// Exact longest match at p (wave-cooperative; all lanes call with identical arguments).
-__device__ void exact_match(const u8* t, const u32* prev3, u32 p, u32 end, u32& out_len, u32& out_dist) {
+// Exact LCP(p, q) >= start, wave-cooperative (64 lanes x 4 bytes per step); maxl bounds it.
+__device__ u32 wave_lcp(const u8* t, u32 p, u32 q, u32 start, u32 maxl) {
     const u32 lane = threadIdx.x & 63;
-    u32 best = 0, bd = 0;
-    const u32 maxl = end - p;
-    u32 q = prev3[p];
-    while (q != NONE && p - q <= (u32)LZ_WINDOW) {
-        if (best >= maxl) break;  // nothing can be longer
-        bool cand = true;
-        if (best > 0) cand = t[p + best] == t[q + best];  // must extend past best
-        if (cand) {
-            u32 l = 0;
-            for (;;) {
-                u32 mism = 0xFFFFFFFFu;
+    u32 l = start;
+    for (;;) {
+        u32 mism = 0xFFFFFFFFu;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const u32 o = l + j * 64 + lane;
-                    const bool bad = (o >= maxl) || (t[p + o] != t[q + o]);
-                    const u64 bal = __ballot(bad);
-                    if (bal && mism == 0xFFFFFFFFu) mism = l + j * 64 + (__ffsll((long long)bal) - 1);
-                }
-                if (mism != 0xFFFFFFFFu) {
-                    l = mism;
-                    break;
-                }
-                l += 256;
-            }
-            if (l > best) {
-                best = l;
-                bd = p - q;
-            }
+        for (int j = 0; j < 4; ++j) {
+            const u32 o = l + j * 64 + lane;
+            const bool bad = (o >= maxl) || (t[p + o] != t[q + o]);
+            const u64 bal = __ballot(bad);
+            if (bal && mism == 0xFFFFFFFFu) mism = l + j * 64 + (__ffsll((long long)bal) - 1);
         }
-        q = prev3[q];
+        if (mism != 0xFFFFFFFFu) return mism;
+        l += 256;
+    }
+}
+
+// Longest match at p (uniform across the wave).  i = idx3[p], gs = gs3[p].
+__device__ void best_match(const LzArgs& z, u32 p, u32 end, u32 i, u32 gs, u32& out_len, u32& out_dist,
+                           u32& nlong) {
+    const u32 lane = threadIdx.x & 63;
+    const u8* t = z.text;
+    u32 best = 0, bd = 0;
+    if (p + (u32)LZ_MIN <= end && i > gs) {
+        const u32 maxl = end - p;
+        const u32 capl = min((u32)LZ_CAP, maxl);
+        u32 k0 = i;  // candidates this batch: slots k0-1-lane
+        for (;;) {
+            bool valid = k0 > gs + lane;
+            const u32 q = valid ? z.SA3[k0 - 1 - lane] : 0u;
+            valid = valid && (p - q <= (u32)LZ_WINDOW);
+            const u64 inwin = __ballot(valid);
+            if (!inwin) break;
+            u32 l = 0;
+            if (valid) {
+                // a later candidate wins only if strictly longer: it must match at `best`
+                const bool can = best == 0 || (best < maxl && t[p + best] == t[q + best]);
+                if (can) {
+                    l = LZ_MIN;
+                    while (l < capl && t[p + l] == t[q + l]) ++l;
+                }
+            }
+            u64 longm = __ballot(valid && l >= capl && capl < maxl);
+            while (longm) {
+                const u32 j = __ffsll((long long)longm) - 1;
+                const u32 qj = __builtin_amdgcn_readlane(q, j);
+                const u32 lj = wave_lcp(t, p, qj, capl, maxl);
+                if (lane == j) l = lj;
+                longm &= longm - 1;
+                ++nlong;
+            }
+            // max length, ties -> smallest lane (= smallest distance)
+            u64 key = valid ? (((u64)l << 8) | (63u - lane)) : 0ull;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                const u64 other = __shfl_xor(key, o);
+                key = other > key ? other : key;
+            }
+            const u32 lb = (u32)(key >> 8);
+            if (lb > best) {
+                best = lb;
+                bd = p - __builtin_amdgcn_readlane(q, 63u - (u32)(key & 0xFF));
+            }
+            if (best >= maxl || inwin != ~0ull) break;
+            k0 -= 64;
+        }
+    }
+    if (best < (u32)LZ_MIN) {
+        best = 0;
+        bd = 0;
     }
     out_len = best;
     out_dist = bd;
-}
-
-// token at q from its (capped) match record; len 0 = literal
-__device__ inline void token_at(const LzArgs& z, u32 q, u32 end, u32 Lv, u32 Dv, u32& len, u32& dist, u32& nlong) {
-    if (Lv >= (u32)LZ_CAP) {
-        exact_match(z.text, z.prev3, q, end, len, dist);
-        ++nlong;
-    } else {
-        len = Lv;
-        dist = Dv;
-    }
-    if (len < (u32)LZ_MIN) {
-        len = 0;
-        dist = 0;
-    }
 }
 
 // Speculative parse of one chunk per wave (4 waves per workgroup).
@@ -135,34 +133,34 @@ __global__ __launch_bounds__(256) void k_lz_spec(LzArgs z, u32 nchunks) {
         return;
     }
     const u32 e = min(s + (u32)LZ_CHUNK, bend);
+    // 64-position windows of (idx3, gs3), the next one prefetched
     u32 wbase = s;
     u32 P = wbase + lane;
-    u32 Lw = P < bend ? (u32)z.Lc[P] : 0u, Dw = P < bend ? (u32)z.Dc[P] : 0u;
+    u32 Iw = P < bend ? z.idx3[P] : 0u, Gw = P < bend ? z.gs3[P] : 0u;
     P += 64;
-    u32 Ln = P < bend ? (u32)z.Lc[P] : 0u, Dn = P < bend ? (u32)z.Dc[P] : 0u;
+    u32 In = P < bend ? z.idx3[P] : 0u, Gn = P < bend ? z.gs3[P] : 0u;
     u32 q = s, ntok = 0, off = 0, nlong = 0, nbuf = 0;
     u32 bpos = 0, blen = 0, bdist = 0, boff = 0;
     while (q < e) {
         if (q >= wbase + 64) {
             if (q < wbase + 128) {
-                Lw = Ln;
-                Dw = Dn;
+                Iw = In;
+                Gw = Gn;
                 wbase += 64;
             } else {
                 wbase = q;
                 const u32 P0 = wbase + lane;
-                Lw = P0 < bend ? (u32)z.Lc[P0] : 0u;
-                Dw = P0 < bend ? (u32)z.Dc[P0] : 0u;
+                Iw = P0 < bend ? z.idx3[P0] : 0u;
+                Gw = P0 < bend ? z.gs3[P0] : 0u;
             }
             const u32 P1 = wbase + 64 + lane;
-            Ln = P1 < bend ? (u32)z.Lc[P1] : 0u;
-            Dn = P1 < bend ? (u32)z.Dc[P1] : 0u;
+            In = P1 < bend ? z.idx3[P1] : 0u;
+            Gn = P1 < bend ? z.gs3[P1] : 0u;
         }
         const u32 cur = q - wbase;
-        const u32 Lv = __builtin_amdgcn_readlane(Lw, cur);
-        const u32 Dv = __builtin_amdgcn_readlane(Dw, cur);
         u32 len, dist;
-        token_at(z, q, bend, Lv, Dv, len, dist, nlong);
+        best_match(z, q, bend, __builtin_amdgcn_readlane(Iw, cur), __builtin_amdgcn_readlane(Gw, cur), len, dist,
+                   nlong);
         if (lane == nbuf) {
             bpos = q;
             blen = len;
@@ -226,7 +224,7 @@ __global__ __launch_bounds__(64) void k_lz_stitch(LzArgs z) {
                     break;
                 }
                 u32 len, dist;
-                token_at(z, q, bend, z.Lc[q], z.Dc[q], len, dist, nlong);
+                best_match(z, q, bend, z.idx3[q], z.gs3[q], len, dist, nlong);
                 if (lane == 0) {
                     z.fix_pos[base + fi] = q;
                     z.fix_len[base + fi] = len;
@@ -308,11 +306,6 @@ __global__ __launch_bounds__(256) void k_lz_emit(LzArgs z, const u32* method, co
 }
 
 }  // namespace
-
-void launch_lz_match(const LzArgs& z, hipStream_t s) {
-    if (!z.geo.N) return;
-    k_lz_match<<<(u32)((z.geo.N + 255) / 256), 256, 0, s>>>(z);
-}
 
 void launch_lz_parse(const LzArgs& z, hipStream_t s) {
     if (!z.geo.nb) return;

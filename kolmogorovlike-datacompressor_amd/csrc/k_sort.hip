@@ -79,7 +79,8 @@ __device__ inline int size_class(u32 len) { return len <= 1 ? 0 : 32 - __clz(len
 // keys
 // ------------------------------------------------------------------------------------
 __device__ inline u32 cyc_succ(const SortArgs& a, u32 p, u32 h) {
-    const u32 fs = a.FS[p], m = a.FL[p];
+    const u64 f = a.FSL[p];
+    const u32 fs = (u32)f, m = (u32)(f >> 32);
     u32 hm = h < m ? h : h % m;
     u32 t = (p - fs) + hm;
     if (t >= m) t -= m;
@@ -94,7 +95,8 @@ __device__ inline u32 make_key(const SortArgs& a, u32 p, u32 base, u32 end) {
             u32 c2 = p + 2 < end ? (u32)a.text[p + 2] + 1 : 0;
             return (c0 << 18) | (c1 << 9) | c2;
         }
-        const u32 fs = a.FS[p], m = a.FL[p];
+        const u64 f = a.FSL[p];
+        const u32 fs = (u32)f, m = (u32)(f >> 32);
         u32 t = p - fs, k = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -260,21 +262,49 @@ __global__ __launch_bounds__(WG) void k_msd_scan(const LSeg* segs, SortArgs a, u
     }
     const int nonzero = __syncthreads_count(run > 0);
     if (nonzero > 1 && d == 0) a.blk_split[a.geo.block_of(s.start)] = 1;
-    if (run == 0) return;
+    // classify the buckets; appends aggregated per workgroup (LDS counters, one global
+    // atomic per list) — per-bucket global atomics on a dozen hot counters serialise
+    __shared__ u32 lcnt[NCLASS + 2], lel[NCLASS + 2], lbase[NCLASS + 2], ltiles, ltb;
+    if (d < NCLASS + 2) {
+        lcnt[d] = 0;
+        lel[d] = 0;
+    }
+    if (d == 0) ltiles = 0;
+    __syncthreads();
     const Seg sub{abs0, run};
-    if (run <= (u32)TILE) {
-        const int c = size_class(run);
-        L.cls[c][atomicAdd(&L.cls_cnt[c], 1u)] = sub;
-        atomicAdd(&L.cls_elems[c], run);
-    } else if (!last_level) {
-        const u32 nt = (run + TILE - 1) / TILE;
-        const u32 si = atomicAdd(nx.nseg, 1u);
-        const u32 tb = atomicAdd(nx.ntiles, nt);
-        atomicAdd(nx.nelem, run);
+    int kind = -1;  // 0..NCLASS-1 class, NCLASS next level, NCLASS+1 equal run
+    u32 li = 0, lt = 0, nt = 0;
+    if (run > 0) {
+        kind = run <= (u32)TILE ? size_class(run) : (!last_level ? NCLASS : NCLASS + 1);
+        li = atomicAdd(&lcnt[kind], 1u);
+        atomicAdd(&lel[kind], run);
+        if (kind == NCLASS) {
+            nt = (run + TILE - 1) / TILE;
+            lt = atomicAdd(&ltiles, nt);
+        }
+    }
+    __syncthreads();
+    if (d < NCLASS && lcnt[d]) {
+        lbase[d] = atomicAdd(&L.cls_cnt[d], lcnt[d]);
+        atomicAdd(&L.cls_elems[d], lel[d]);
+    }
+    if (d == NCLASS && lcnt[d]) {
+        lbase[d] = atomicAdd(nx.nseg, lcnt[d]);
+        atomicAdd(nx.nelem, lel[d]);
+        ltb = atomicAdd(nx.ntiles, ltiles);
+    }
+    if (d == NCLASS + 1 && lcnt[d]) lbase[d] = atomicAdd(L.eq_cnt, lcnt[d]);
+    __syncthreads();
+    if (kind < 0) return;
+    if (kind < NCLASS) {
+        L.cls[kind][lbase[kind] + li] = sub;
+    } else if (kind == NCLASS) {
+        const u32 si = lbase[NCLASS] + li;
+        const u32 tb = ltb + lt;
         nx.segs[si] = LSeg{sub.start, sub.len, tb, nt};
         for (u32 k = 0; k < nt; ++k) nx.tiles[tb + k] = LTile{si, k};
     } else {
-        L.eq[atomicAdd(L.eq_cnt, 1u)] = sub;
+        L.eq[lbase[NCLASS + 1] + li] = sub;
     }
 }
 
@@ -489,6 +519,7 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
         const u32 pos = (u32)r[e];
         a.SA[sg.start + kk] = pos;
         a.RK[pos] = sg.start + (start_idx[e] - (si << C));
+        if (a.idx3) a.idx3[pos] = sg.start + kk;
         if (head[e]) {
             const u32 len = nxt[e] - i;
             if (len >= 2) L.next[wpos++] = Seg{sg.start + kk, len};
@@ -501,13 +532,19 @@ __global__ void k_single(const Seg* segs, u32 count, SortArgs a) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) {
         const Seg s = segs[i];
-        a.RK[a.SA[s.start]] = s.start;
+        const u32 p = a.SA[s.start];
+        a.RK[p] = s.start;
+        if (a.idx3) a.idx3[p] = s.start;
     }
 }
 
 __global__ __launch_bounds__(WG) void k_finalize_eq(const Seg* eq, SortArgs a, Lists L) {
     const Seg s = eq[blockIdx.x];
-    for (u32 i = threadIdx.x; i < s.len; i += WG) a.RK[a.SA[s.start + i]] = s.start;
+    for (u32 i = threadIdx.x; i < s.len; i += WG) {
+        const u32 p = a.SA[s.start + i];
+        a.RK[p] = s.start;
+        if (a.idx3) a.idx3[p] = s.start + i;
+    }
     if (threadIdx.x == 0) L.next[atomicAdd(L.next_cnt, 1u)] = s;
 }
 
@@ -516,21 +553,6 @@ __global__ void k_update_done(u32* done, const u32* split, u32 nb) {
     if (b < nb && !split[b]) done[b] = 1;
 }
 
-// prev3[p] = previous position of the same 3-gram in p's block (NONE if none), read off
-// the linear SA right after round 0 (groups = 3-character classes, positions ascending).
-__global__ void k_prev3(SortArgs a, u32* prev3) {
-    const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= a.geo.N) return;
-    const u32 b = a.geo.block_of(g);
-    const u32 base = a.geo.base(b), end = a.geo.end(b);
-    const u32 p = a.SA[g];
-    u32 r = NONE;
-    if (p + 3 <= end && g > base) {
-        const u32 q = a.SA[g - 1];
-        if (a.RK[q] == a.RK[p]) r = q;
-    }
-    prev3[p] = r;
-}
 
 // ------------------------------------------------------------------------------------
 // launchers
@@ -602,9 +624,6 @@ void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists
 }
 void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, hipStream_t s) {
     if (nb) k_update_done<<<cdiv(nb, 256), 256, 0, s>>>(blk_done, blk_split, nb);
-}
-void launch_prev3(const SortArgs& a, u32* prev3, hipStream_t s) {
-    if (a.geo.N) k_prev3<<<cdiv(a.geo.N, 256), 256, 0, s>>>(a, prev3);
 }
 
 }  // namespace kolm

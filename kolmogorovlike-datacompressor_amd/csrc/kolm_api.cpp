@@ -60,9 +60,10 @@ namespace {
 struct TScope {
     kolm_ctx* c;
     int fam;
+    const char* name;  // kernel symbol (as rocprof shows it, namespaces stripped)
     u64 bytes;
     hipEvent_t a = nullptr;
-    TScope(kolm_ctx* c_, int fam_, u64 bytes_);
+    TScope(kolm_ctx* c_, int fam_, const char* name_, u64 bytes_);
     ~TScope() noexcept(false);
 };
 }  // namespace
@@ -80,10 +81,16 @@ struct kolm_ctx {
     size_t evused = 0;
     struct Pend {
         int fam;
+        const char* name;
         hipEvent_t a, b;
         u64 bytes;
     };
     std::vector<Pend> pend;
+    struct Acc {
+        double ms = 0;
+        u64 launches = 0, bytes = 0;
+    };
+    std::map<std::string, Acc> kacc;  // per kernel, accumulated while timing is enabled
     hipEvent_t ev_take() {
         if (evused == evpool.size()) {
             hipEvent_t e;
@@ -103,6 +110,10 @@ struct kolm_ctx {
             st->kt[p.fam].ms += ms;
             st->kt[p.fam].launches += 1;
             st->kt[p.fam].bytes += p.bytes;
+            Acc& a = kacc[p.name];
+            a.ms += ms;
+            a.launches += 1;
+            a.bytes += p.bytes;
         }
         timing_reset();
     }
@@ -128,7 +139,7 @@ struct kolm_ctx {
 
 namespace {
 
-TScope::TScope(kolm_ctx* c_, int fam_, u64 bytes_) : c(c_), fam(fam_), bytes(bytes_) {
+TScope::TScope(kolm_ctx* c_, int fam_, const char* name_, u64 bytes_) : c(c_), fam(fam_), name(name_), bytes(bytes_) {
     if (c->timing) {
         a = c->ev_take();
         KOLM_HIP_CHECK(hipEventRecord(a, c->stream));
@@ -138,7 +149,7 @@ TScope::~TScope() noexcept(false) {
     if (c->timing) {
         hipEvent_t b = c->ev_take();
         KOLM_HIP_CHECK(hipEventRecord(b, c->stream));
-        c->pend.push_back({fam, a, b, bytes});
+        c->pend.push_back({fam, name, a, b, bytes});
     }
 }
 
@@ -147,14 +158,21 @@ kolm_ctx* g_default = nullptr;
 
 u32 bitlen(u32 v) { return v ? 32 - __builtin_clz(v) : 0; }
 
+const char* const kSmallSortName[NCLASS] = {
+    "k_single",          "k_small_sort<1>", "k_small_sort<2>", "k_small_sort<3>",
+    "k_small_sort<4>",   "k_small_sort<5>", "k_small_sort<6>", "k_small_sort<7>",
+    "k_small_sort<8>",   "k_small_sort<9>", "k_small_sort<10>", "k_small_sort<11>"};
+
 struct SortOut {
     u32 rounds = 0;
     u64 active = 0;
 };
 
 // Segmented prefix-doubling suffix sort of every block of the batch (k_sort.hip).
-SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, const u32* FS, const u32* FL,
-                  u32* prev3, bool round0_only) {
+// capture3 (linear pass): after round 0 (3-character groups, positions ascending) keep
+// SA3 = SA, gs3 = RK (group start slot by position) and idx3 (slot by position) for LZ77.
+SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, const u64* FSL, bool capture3,
+                  bool round0_only) {
     hipStream_t s = c->stream;
     const u64 N = geo.N;
     SortOut out;
@@ -166,8 +184,8 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
     a.K2 = c->get<u32>("K2", N);
     a.SA2 = c->get<u32>("SA2", N);
     a.K22 = c->get<u32>("K22", N);
-    a.FS = FS;
-    a.FL = FL;
+    a.FSL = FSL;
+    u32* idx3 = capture3 ? c->get<u32>("idx3", N) : nullptr;
     a.blk_split = c->get<u32>("blk_split", geo.nb);
     u32* blk_done = c->get<u32>("blk_done", geo.nb);
     a.blk_done = blk_done;
@@ -211,12 +229,13 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
     for (u32 round = 0; round < 64 && ncur; ++round) {
         a.initial = round == 0 ? 1 : 0;
         a.h = round == 0 ? 0u : (h0 << (round - 1));
+        a.idx3 = round == 0 ? idx3 : nullptr;
         L.next = nxt;
         KOLM_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(u32) * C_STATUS, s));
         KOLM_HIP_CHECK(hipMemsetAsync(cnt + C_CLSE, 0, sizeof(u32) * (C_N - C_CLSE), s));
         KOLM_HIP_CHECK(hipMemsetAsync(a.blk_split, 0, sizeof(u32) * geo.nb, s));
         {
-            TScope t(c, KOLM_KT_CLASSIFY, (u64)ncur * 16);
+            TScope t(c, KOLM_KT_CLASSIFY, "k_classify", (u64)ncur * 16);
             launch_classify(cur, ncur, a, L, lv[0], s);
         }
         KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
@@ -227,9 +246,15 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
         {
             // algorithmic bytes per element: SA read + key inputs + K2 write
             const u64 per = a.initial ? (cyclic ? 20 : 11) : (cyclic ? 20 : 12);
-            TScope t(c, KOLM_KT_KEYGEN, (u64)h[C_ACTIVE] * per);
-            for (int k = 1; k < NCLASS; ++k) launch_keygen_small(k, L.cls[k], h[C_CLS + k], a, s);
-            launch_keygen_large(lv[0].tiles, h[C_L0TILE], lv[0].segs, a, s);
+            for (int k = 1; k < NCLASS; ++k) {
+                if (!h[C_CLS + k]) continue;
+                TScope t(c, KOLM_KT_KEYGEN, "k_keygen_small", (u64)h[C_CLSE + k] * per);
+                launch_keygen_small(k, L.cls[k], h[C_CLS + k], a, s);
+            }
+            if (h[C_L0TILE]) {
+                TScope t(c, KOLM_KT_KEYGEN, "k_keygen_large", (u64)h[C_L0ELEM] * per);
+                launch_keygen_large(lv[0].tiles, h[C_L0TILE], lv[0].segs, a, s);
+            }
         }
         u32 nelem = h[C_L0ELEM];
         u32 nseg = h[C_L0SEG], ntiles = h[C_L0TILE];
@@ -245,11 +270,19 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
             KOLM_HIP_CHECK(hipMemsetAsync(ln.ntiles, 0, sizeof(u32), s));
             KOLM_HIP_CHECK(hipMemsetAsync(ln.nelem, 0, sizeof(u32), s));
             {
-                // hist: K2 4 B; scatter: SA+K2 read 8, write 8; copy back: 8 + 8
-                TScope t(c, KOLM_KT_MSD, (u64)nelem * 36 + (u64)ntiles * 256 * 8);
+                TScope t(c, KOLM_KT_MSD, "k_msd_hist", (u64)nelem * 4 + (u64)ntiles * 1024);
                 launch_msd_hist(lc.tiles, ntiles, lc.segs, a, shift, width, hist, s);
+            }
+            {
+                TScope t(c, KOLM_KT_MSD, "k_msd_scan", (u64)ntiles * 1024 * 3);
                 launch_msd_scan(lc.segs, nseg, a, width, hist, last, L, ln, s);
+            }
+            {
+                TScope t(c, KOLM_KT_MSD, "k_msd_scatter", (u64)nelem * 16 + (u64)ntiles * 1024);
                 launch_msd_scatter(lc.tiles, ntiles, lc.segs, a, shift, width, hist, s);
+            }
+            {
+                TScope t(c, KOLM_KT_MSD, "k_copy_back", (u64)nelem * 16);
                 launch_copy_back(lc.tiles, ntiles, lc.segs, a, s);
             }
             KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
@@ -263,19 +296,21 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
         }
         KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
         c->sync();
-        {
-            // per element: K2 + SA read, SA + RK write (16 B); per segment record 8 B
-            u64 sb = 0;
-            for (int k = 0; k < NCLASS; ++k) sb += (u64)h[C_CLSE + k] * 16 + (u64)h[C_CLS + k] * 8;
-            sb += (u64)h[C_EQ] * TILE * 8;
-            TScope t(c, KOLM_KT_SMALLSORT, sb);
-            for (int k = 0; k < NCLASS; ++k) launch_small_sort(k, L.cls[k], h[C_CLS + k], a, L, s);
+        // per element: K2 + SA read, SA + RK write (16 B); per segment record 8 B
+        for (int k = 0; k < NCLASS; ++k) {
+            if (!h[C_CLS + k]) continue;
+            TScope t(c, KOLM_KT_SMALLSORT, kSmallSortName[k], (u64)h[C_CLSE + k] * 16 + (u64)h[C_CLS + k] * 8);
+            launch_small_sort(k, L.cls[k], h[C_CLS + k], a, L, s);
+        }
+        if (h[C_EQ]) {
+            TScope t(c, KOLM_KT_SMALLSORT, "k_finalize_eq", (u64)h[C_EQ] * TILE * 8);
             launch_finalize_eq(L.eq, h[C_EQ], a, L, s);
         }
         if (cyclic) launch_update_done(blk_done, a.blk_split, geo.nb, s);
-        if (!cyclic && round == 0 && prev3) {
-            TScope t(c, KOLM_KT_LYNDON, N * 16);
-            launch_prev3(a, prev3, s);
+        if (round == 0 && idx3) {
+            TScope t(c, KOLM_KT_LYNDON, "copy_SA3_GS3", N * 16);
+            KOLM_HIP_CHECK(hipMemcpyAsync(c->get<u32>("SA3", N), a.SA, 4 * N, hipMemcpyDeviceToDevice, s));
+            KOLM_HIP_CHECK(hipMemcpyAsync(c->get<u32>("GS3", N), a.RK, 4 * N, hipMemcpyDeviceToDevice, s));
         }
         KOLM_HIP_CHECK(hipMemcpyAsync(h + C_NEXT, cnt + C_NEXT, sizeof(u32), hipMemcpyDeviceToHost, s));
         c->sync();
@@ -293,28 +328,29 @@ struct Pipeline {
     kolm_stats st{};
     float t_sa = 0, t_lz = 0, t_ent = 0, t_emit = 0;
 
-    // BBWT of every block into "bbwt"; prev3 chains into "prev3"
+    // BBWT of every block into "bbwt"; 3-gram candidate arrays (SA3, idx3, GS3) for LZ77
     u8* bbwt() {
         const u64 N = geo.N;
-        u32* prev3 = c->get<u32>("prev3", N);
-        u32* FS = c->get<u32>("FS", N);
-        u32* FL = c->get<u32>("FL", N);
+        u64* FSL = c->get<u64>("FSL", N);
         u8* flag = c->get<u8>("flag", N);
         const u64 ntiles = (u64)((geo.bs + TILE - 1) / TILE) * geo.nb + 16;
         u32* t1 = c->get<u32>("tile_tmp", 2 * ntiles + 16);
         u32* t2 = c->get<u32>("tile_tmp2", 2 * ntiles + 2 * geo.nb + 16);
-        SortOut lin = sort_pass(c, geo, text, false, nullptr, nullptr, prev3, false);
+        // linear suffix order is needed only at 3 characters (LZ77 candidate groups)
+        SortOut lin = sort_pass(c, geo, text, false, nullptr, true, true);
         {
-            // RK read twice, flags write + 2 reads, FS/FL write
-            TScope t(c, KOLM_KT_LYNDON, N * 19);
-            launch_lyndon(geo, c->get<u32>("RK", N), flag, FS, FL, t1, t2, c->stream);
+            // Duval: text read ~2x + factor starts 4 B; merge; flags; FSL scans write 8 B
+            TScope t(c, KOLM_KT_LYNDON, "k_duval+lyndon_scans", N * 16);
+            const u64 nch = (geo.bs + 4095) / 4096 * (u64)geo.nb + 1;
+            launch_lyndon(geo, text, flag, FSL, c->get<u32>("lyn_fstart", N), c->get<u32>("lyn_nfac", nch),
+                          c->get<u32>("lyn_stack", N), t1, t2, c->stream);
         }
-        SortOut cyc = sort_pass(c, geo, text, true, FS, FL, nullptr, false);
+        SortOut cyc = sort_pass(c, geo, text, true, FSL, false, false);
         u8* out = c->get<u8>("bbwt", N);
         {
-            // SA 4 + FS 4 + FL 4 + text 1 + out 1
-            TScope t(c, KOLM_KT_LYNDON, N * 14);
-            launch_bbwt_gather(geo, text, c->get<u32>("SA", N), FS, FL, out, c->stream);
+            // SA 4 + FSL 8 + text 1 + out 1
+            TScope t(c, KOLM_KT_LYNDON, "k_bbwt_gather", N * 14);
+            launch_bbwt_gather(geo, text, c->get<u32>("SA", N), FSL, out, c->stream);
         }
         st.lin_rounds = lin.rounds;
         st.cyc_rounds = cyc.rounds;
@@ -328,7 +364,7 @@ struct Pipeline {
         const u64 nch = (u64)((geo.bs + MTF_CHUNK - 1) / MTF_CHUNK) * geo.nb + 1;
         u8* out = c->get<u8>("mtf", N);
         // summary: read N; compose: summaries + states 512 B/chunk; replay: N in, N out, state
-        TScope t(c, KOLM_KT_MTF, 3 * N + nch * 768);
+        TScope t(c, KOLM_KT_MTF, "k_mtf_summary+compose+replay", 3 * N + nch * 768);
         launch_mtf(geo, in, out, c->get<u8>("mtf_sum", nch * 256), c->get<u16>("mtf_cnt", nch),
                    c->get<u8>("mtf_states", nch * 256), c->stream);
         return out;
@@ -339,9 +375,9 @@ struct Pipeline {
         LzArgs z{};
         z.geo = geo;
         z.text = text;
-        z.prev3 = c->get<u32>("prev3", N);
-        z.Lc = c->get<u8>("lz_L", N);
-        z.Dc = c->get<u16>("lz_D", N);
+        z.SA3 = c->get<u32>("SA3", N);
+        z.idx3 = c->get<u32>("idx3", N);
+        z.gs3 = c->get<u32>("GS3", N);
         z.tok_pos = c->get<u32>("tok_pos", N);
         z.tok_len = c->get<u32>("tok_len", N);
         z.tok_dist = c->get<u32>("tok_dist", N);
@@ -370,13 +406,8 @@ struct Pipeline {
     void lz(const LzArgs& z) {
         KOLM_HIP_CHECK(hipMemsetAsync(z.nlong, 0, sizeof(u32), c->stream));
         {
-            // prev3 4 + text 1 + Lc 1 + Dc 2 per position
-            TScope t(c, KOLM_KT_LZMATCH, geo.N * 8);
-            launch_lz_match(z, c->stream);
-        }
-        {
-            // Lc + Dc per position (+ 16 B per token, added after the batch)
-            TScope t(c, KOLM_KT_LZPARSE, geo.N * 3);
+            // idx3 + gs3 windows (8 B per position) + text; 16 B per token added after the batch
+            TScope t(c, KOLM_KT_LZPARSE, "k_lz_spec+stitch", geo.N * 9);
             launch_lz_parse(z, c->stream);
         }
     }
@@ -442,7 +473,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
     e.tile_tmp2 = c->get<u32>("tile_tmp2", 2 * ntiles + 2 * nb + 16);
     e.rice_k = 2;
     {
-        TScope t(c, KOLM_KT_SIZES, 2 * N);  // text + mtf once
+        TScope t(c, KOLM_KT_SIZES, "k_sizes", 2 * N);  // text + mtf once
         launch_cheap_and_rice_sizes(e, s);
     }
     KOLM_HIP_CHECK(hipEventRecord(ev[2], s));
@@ -453,7 +484,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
     u32* cnt = c->get<u32>("counters", C_N);
     KOLM_HIP_CHECK(hipMemsetAsync(cnt + C_STATUS, 0, sizeof(u32), s));
     {
-        TScope t(c, KOLM_KT_SIZES, (u64)nb * 120);
+        TScope t(c, KOLM_KT_SIZES, "k_mdl+offsets", (u64)nb * 120);
         launch_mdl(e, want_lz ? z.lz_size : nullptr, cnt + C_STATUS, s);
     }
     std::vector<u64> off(nb + 1);
@@ -465,7 +496,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
         return KOLM_ECAP;
     }
     {
-        TScope t(c, KOLM_KT_EMIT, N + 2 * off[nb]);
+        TScope t(c, KOLM_KT_EMIT, "emit", N + 2 * off[nb]);
         KOLM_HIP_CHECK(hipMemsetAsync(d_arena, 0, (off[nb] + 8) & ~(u64)3, s));
         launch_emit_simple(e, s);
         launch_emit_rice(e, s);
@@ -645,7 +676,28 @@ int kolm_memcpy_d2h(kolm_ctx* c, void* dst, const void* src, uint64_t bytes) {
 int kolm_ctx_set_timing(kolm_ctx* c, int enable) {
     if (!c) return KOLM_EARG;
     std::lock_guard<std::mutex> g(c->mu);
+    if (enable && !c->timing) c->kacc.clear();
     c->timing = enable != 0;
+    return KOLM_OK;
+}
+
+int kolm_ctx_kernel_times(kolm_ctx* c, char* buf, size_t cap, size_t* len) {
+    if (!c) return KOLM_EARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    std::string js = "{";
+    bool first = true;
+    for (auto& kv : c->kacc) {
+        char tmp[256];
+        snprintf(tmp, sizeof tmp, "%s\"%s\": {\"ms\": %.6f, \"launches\": %llu, \"bytes\": %llu}", first ? "" : ", ",
+                 kv.first.c_str(), kv.second.ms, (unsigned long long)kv.second.launches,
+                 (unsigned long long)kv.second.bytes);
+        js += tmp;
+        first = false;
+    }
+    js += "}";
+    if (len) *len = js.size();
+    if (!buf || cap < js.size() + 1) return buf ? KOLM_ECAP : KOLM_OK;
+    std::memcpy(buf, js.c_str(), js.size() + 1);
     return KOLM_OK;
 }
 
@@ -862,7 +914,7 @@ int kolm_lz77_encode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size
         geom_init(geo, n, (u32)n);
         u8* d = upload(c, in, n);
         Pipeline P{c, geo, d};
-        sort_pass(c, geo, d, false, nullptr, nullptr, c->get<u32>("prev3", n), true);
+        sort_pass(c, geo, d, false, nullptr, true, true);
         LzArgs z = P.lz_args();
         P.lz(z);
         u32 sz = 0;

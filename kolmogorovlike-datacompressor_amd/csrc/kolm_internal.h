@@ -23,7 +23,7 @@ constexpr int NCLASS = 12;        // small-segment size classes: len in (2^(c-1)
 constexpr u32 NONE = 0xFFFFFFFFu;
 constexpr int LZ_WINDOW = 4096;   // PY:1723 WINDOW_MAX
 constexpr int LZ_MIN = 3;         // PY:1724 MIN_MATCH
-constexpr int LZ_CAP = 64;        // capped match length of the all-positions pass
+constexpr int LZ_CAP = 32;        // per-lane capped compare; longer candidates are extended by the wave
 constexpr int MTF_CHUNK = 1024;   // bytes replayed per thread by the MTF kernel
 constexpr u32 NCAND = 9;          // candidate ids 0..8 computed on the device
 
@@ -73,13 +73,13 @@ struct SortArgs {
     u32* K2;
     u32* SA2;
     u32* K22;
-    const u32* FS;     // cyclic: global start of the Lyndon factor of each position
-    const u32* FL;     // cyclic: length of that factor
+    const u64* FSL;    // cyclic: start (low 32) | length (high 32) of each position's Lyndon factor
     u32* blk_split;    // [nb] set to 1 when a group of block b split this round
     const u32* blk_done;  // [nb] cyclic: block converged (no further splits possible)
     int cyclic;
     int initial;       // round 0: keys are packed characters
     u32 h;             // doubling offset of this round (round >= 1)
+    u32* idx3;         // linear round 0 only: idx3[p] = SA slot of p (3-gram order), else null
 };
 
 // Append-only lists written by the classify / MSD / small-sort kernels.
@@ -122,13 +122,13 @@ void launch_small_sort(int c, const Seg* segs, u32 count, const SortArgs& a, con
                        hipStream_t s);
 void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists& L, hipStream_t s);
 void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, hipStream_t s);
-void launch_prev3(const SortArgs& a, u32* prev3, hipStream_t s);
 
 // ---- k_blocks.hip: per-block scans, Lyndon factors, BBWT gather ----
-void launch_lyndon(const Geom& geo, const u32* RK, u8* flag, u32* FS, u32* FL, u32* tile_tmp,
-                   u32* tile_tmp2, hipStream_t s);
-void launch_bbwt_gather(const Geom& geo, const u8* text, const u32* SA, const u32* FS,
-                        const u32* FL, u8* out, hipStream_t s);
+void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u32* fstart, u32* nfac, u32* stack,
+                   u32* tile_tmp, u32* tile_tmp2, hipStream_t s);
+void launch_lyndon_isa(const Geom& geo, const u32* RK, u8* flag, u32* tile_tmp, u32* tile_tmp2, hipStream_t s);
+void launch_bbwt_gather(const Geom& geo, const u8* text, const u32* SA, const u64* FSL, u8* out,
+                        hipStream_t s);
 
 // ---- k_mtf.hip ----
 void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summary_cnt, u8* states,
@@ -164,9 +164,10 @@ constexpr int LZ_CHUNK = 8192;  // speculative-parse chunk (one wave each)
 struct LzArgs {
     Geom geo;
     const u8* text;
-    const u32* prev3;
-    u8* Lc;            // capped match length (LZ_CAP = long)
-    u16* Dc;           // distance of the capped best match
+    // 3-gram candidate structure captured after round 0 of the linear suffix sort:
+    const u32* SA3;    // [N] positions sorted by (3-gram key, position)
+    const u32* idx3;   // [N] idx3[p] = slot of p in SA3
+    const u32* gs3;    // [N] gs3[p] = first slot of p's 3-gram group in SA3
     // speculative tokens of chunk c live in slots [chunk start, chunk start + ntok[c])
     u32* tok_pos;      // [N] token start position
     u32* tok_len;      // [N] match length (0 = literal)
@@ -191,7 +192,6 @@ struct LzArgs {
     u32* nlong;        // [1]
     u32 cpb;           // chunks per block
 };
-void launch_lz_match(const LzArgs& z, hipStream_t s);
 void launch_lz_parse(const LzArgs& z, hipStream_t s);
 void launch_lz_emit(const LzArgs& z, const u32* method, const u64* off, u8* arena, hipStream_t s);
 

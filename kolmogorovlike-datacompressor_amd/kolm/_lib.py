@@ -98,6 +98,7 @@ SIGNATURES = [
     ("kolm_memcpy_d2h", I32, [P, P, P, U64]),
     ("kolm_ctx_sync", I32, [P]),
     ("kolm_ctx_set_timing", I32, [P, I32]),
+    ("kolm_ctx_kernel_times", I32, [P, P, SZ, ctypes.POINTER(SZ)]),
     ("kolm_encode_blocks_device", I32, [P, P, U64, U32, U32, P, P, U64, P, P, P, P]),
 ]
 
@@ -145,6 +146,16 @@ def ensure_init(device: int = None):
     check(lib.kolm_init(device))
     _inited_device = device
     return device
+
+
+def kernel_times(ctx) -> dict:
+    """Per-kernel HIP-event timing accumulated while timing was enabled on ctx."""
+    import json
+    n = ctypes.c_size_t(0)
+    check(load().kolm_ctx_kernel_times(ctx, None, 0, ctypes.byref(n)))
+    buf = ctypes.create_string_buffer(n.value + 1)
+    check(load().kolm_ctx_kernel_times(ctx, buf, n.value + 1, ctypes.byref(n)))
+    return json.loads(buf.value.decode())
 
 
 def _buf(n):
