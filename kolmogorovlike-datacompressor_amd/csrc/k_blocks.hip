@@ -284,13 +284,18 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
     for (u32 i = lane; i < sp; i += 64) flag[stk[i]] = 1;
 }
 
-__global__ void k_bbwt_gather(Geom geo, const u8* text, const u32* SA, const u64* FSL, u8* out) {
-    for (u32 g = blockIdx.x * blockDim.x + threadIdx.x; g < geo.N; g += gridDim.x * blockDim.x) {
-        const u32 p = SA[g];
+// prevc[p] = the character preceding p cyclically inside its factor (streaming pass), so
+// the BBWT gather needs one random byte per slot instead of a factor lookup + a byte.
+__global__ void k_prevc(Geom geo, const u8* text, const u64* FSL, u8* prevc) {
+    for (u32 p = blockIdx.x * blockDim.x + threadIdx.x; p < geo.N; p += gridDim.x * blockDim.x) {
         const u64 f = FSL[p];
         const u32 fs = (u32)f;
-        out[g] = text[p == fs ? fs + (u32)(f >> 32) - 1 : p - 1];
+        prevc[p] = text[p == fs ? fs + (u32)(f >> 32) - 1 : p - 1];
     }
+}
+
+__global__ void k_bbwt_gather(Geom geo, const u32* SA, const u8* prevc, u8* out) {
+    for (u32 g = blockIdx.x * blockDim.x + threadIdx.x; g < geo.N; g += gridDim.x * blockDim.x) out[g] = prevc[SA[g]];
 }
 
 }  // namespace
@@ -327,11 +332,16 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u32* fst
     k_fsfl<<<nt, WG, 0, s>>>(tg, flag, B, D, FSL);
 }
 
-void launch_bbwt_gather(const Geom& geo, const u8* text, const u32* SA, const u64* FSL, u8* out,
-                        hipStream_t s) {
+void launch_prevc(const Geom& geo, const u8* text, const u64* FSL, u8* prevc, hipStream_t s) {
     if (!geo.N) return;
     const u32 grid = (u32)std::min<u64>((geo.N + 255) / 256, 65535);
-    k_bbwt_gather<<<grid, 256, 0, s>>>(geo, text, SA, FSL, out);
+    k_prevc<<<grid, 256, 0, s>>>(geo, text, FSL, prevc);
+}
+
+void launch_bbwt_gather(const Geom& geo, const u32* SA, const u8* prevc, u8* out, hipStream_t s) {
+    if (!geo.N) return;
+    const u32 grid = (u32)std::min<u64>((geo.N + 255) / 256, 65535);
+    k_bbwt_gather<<<grid, 256, 0, s>>>(geo, SA, prevc, out);
 }
 
 }  // namespace kolm

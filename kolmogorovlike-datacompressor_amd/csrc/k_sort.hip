@@ -164,10 +164,10 @@ __global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur, Sort
         const u32 nt = (s.len + TILE - 1) / TILE;
         const u32 si = lbase[NCLASS] + li;
         const u32 tb = atomicAdd(lv.ntiles, nt);
-        lv.segs[si] = LSeg{s.start, s.len, tb, nt};
+        lv.segs[si] = LSeg{s.start, s.len | SEG_FIRST, tb, nt};
         for (u32 k = 0; k < nt; ++k) lv.tiles[tb + k] = LTile{si, k};
     } else {
-        L.cls[c][lbase[c] + li] = s;
+        L.cls[c][lbase[c] + li] = Seg{s.start, s.len | SEG_FIRST};
     }
 }
 
@@ -185,7 +185,7 @@ __global__ __launch_bounds__(WG) void k_keygen_small(const Seg* segs, u32 count,
         const u32 k = slot & mask;
         if (si >= count) continue;
         const Seg s = segs[si];
-        if (k >= s.len) continue;
+        if (k >= (s.len & SEG_LEN)) continue;
         const u32 g = s.start + k;
         const u32 b = a.geo.block_of(s.start);
         a.K2[g] = make_key(a, a.SA[g], a.geo.base(b), a.geo.end(b));
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(WG) void k_keygen_large(const LTile* tiles, const L
     const LTile t = tiles[blockIdx.x];
     const LSeg s = segs[t.seg];
     const u32 base = s.start + t.k * TILE;
-    const u32 cnt = min((u32)TILE, s.start + s.len - base);
+    const u32 cnt = min((u32)TILE, s.start + (s.len & SEG_LEN) - base);
     const u32 b = a.geo.block_of(s.start);
     const u32 bb = a.geo.base(b), be = a.geo.end(b);
 #pragma unroll
@@ -217,7 +217,7 @@ __global__ __launch_bounds__(WG) void k_msd_hist(const LTile* tiles, const LSeg*
     const LTile t = tiles[blockIdx.x];
     const LSeg s = segs[t.seg];
     const u32 base = s.start + t.k * TILE;
-    const u32 cnt = min((u32)TILE, s.start + s.len - base);
+    const u32 cnt = min((u32)TILE, s.start + (s.len & SEG_LEN) - base);
 #pragma unroll
     for (int j = 0; j < PER_THREAD; ++j) {
         const u32 e = j * WG + threadIdx.x;
@@ -271,7 +271,8 @@ __global__ __launch_bounds__(WG) void k_msd_scan(const LSeg* segs, SortArgs a, u
     }
     if (d == 0) ltiles = 0;
     __syncthreads();
-    const Seg sub{abs0, run};
+    // the first non-empty bucket of a FIRST segment starts at its round group's start
+    const Seg sub{abs0, run | (((s.len & SEG_FIRST) && bstart == 0) ? SEG_FIRST : 0u)};
     int kind = -1;  // 0..NCLASS-1 class, NCLASS next level, NCLASS+1 equal run
     u32 li = 0, lt = 0, nt = 0;
     if (run > 0) {
@@ -319,7 +320,7 @@ __global__ __launch_bounds__(WG) void k_msd_scatter(const LTile* tiles, const LS
     const LTile t = tiles[blockIdx.x];
     const LSeg s = segs[t.seg];
     const u32 base = s.start + t.k * TILE;
-    const u32 cnt = min((u32)TILE, s.start + s.len - base);
+    const u32 cnt = min((u32)TILE, s.start + (s.len & SEG_LEN) - base);
     const u32 mask = (1u << width) - 1;
     running[tid] = hist[(u64)blockIdx.x * 256 + tid];
 #pragma unroll
@@ -367,7 +368,7 @@ __global__ __launch_bounds__(WG) void k_copy_back(const LTile* tiles, const LSeg
     const LTile t = tiles[blockIdx.x];
     const LSeg s = segs[t.seg];
     const u32 base = s.start + t.k * TILE;
-    const u32 cnt = min((u32)TILE, s.start + s.len - base);
+    const u32 cnt = min((u32)TILE, s.start + (s.len & SEG_LEN) - base);
 #pragma unroll
     for (int j = 0; j < PER_THREAD; ++j) {
         const u32 e = j * WG + threadIdx.x;
@@ -405,17 +406,21 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
     __shared__ Seg ss[SPT];
     __shared__ u32 sh[WG / 64];
     __shared__ u32 last_hi[WG];
+    __shared__ u8 ssplit[SPT];  // sub-array split by this round's key
     const u32 tid = threadIdx.x;
     const u32 first = blockIdx.x * SPT;
     const u32 nthis = min(SPT, count - first);
-    for (u32 i = tid; i < SPT; i += WG) ss[i] = i < nthis ? segs[first + i] : Seg{0, 0};
+    for (u32 i = tid; i < SPT; i += WG) {
+        ss[i] = i < nthis ? segs[first + i] : Seg{0, 0};
+        ssplit[i] = 0;
+    }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < PER_THREAD; ++j) {
         const u32 slot = j * WG + tid;
         const u32 si = slot >> C, k = slot & (S - 1);
         u64 key = ~0ull;
-        if (si < nthis && k < ss[si].len) {
+        if (si < nthis && k < (ss[si].len & SEG_LEN)) {
             const u32 g = ss[si].start + k;
             key = ((u64)a.K2[g] << 32) | a.SA[g];
         }
@@ -470,6 +475,7 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
         const u32 hi = (u32)(r[e] >> 32);
         head[e] = valid[e] && (kk == 0 || hi != prev_hi);
         stop[e] = kk == 0 || head[e] || !valid[e];
+        if (head[e] && kk != 0) ssplit[i >> C] = 1;
         prev_hi = hi;
         (void)prev_valid;
     }
@@ -517,8 +523,11 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
         const u32 si = i >> C, kk = i & (S - 1);
         const Seg sg = ss[si];
         const u32 pos = (u32)r[e];
-        a.SA[sg.start + kk] = pos;
-        a.RK[pos] = sg.start + (start_idx[e] - (si << C));
+        const u32 rs = start_idx[e] - (si << C);  // run start inside the segment
+        // an unsplit segment keeps its order (ties are in position order already); the
+        // first run of a FIRST segment keeps its rank (except in round 0: RK undefined)
+        if (ssplit[si]) a.SA[sg.start + kk] = pos;
+        if (a.initial || rs != 0 || !(sg.len & SEG_FIRST)) a.RK[pos] = sg.start + rs;
         if (a.idx3) a.idx3[pos] = sg.start + kk;
         if (head[e]) {
             const u32 len = nxt[e] - i;
@@ -532,20 +541,26 @@ __global__ void k_single(const Seg* segs, u32 count, SortArgs a) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) {
         const Seg s = segs[i];
-        const u32 p = a.SA[s.start];
-        a.RK[p] = s.start;
-        if (a.idx3) a.idx3[p] = s.start;
+        if (a.initial || !(s.len & SEG_FIRST) || a.idx3) {
+            const u32 p = a.SA[s.start];
+            a.RK[p] = s.start;
+            if (a.idx3) a.idx3[p] = s.start;
+        }
     }
 }
 
 __global__ __launch_bounds__(WG) void k_finalize_eq(const Seg* eq, SortArgs a, Lists L) {
     const Seg s = eq[blockIdx.x];
-    for (u32 i = threadIdx.x; i < s.len; i += WG) {
-        const u32 p = a.SA[s.start + i];
-        a.RK[p] = s.start;
-        if (a.idx3) a.idx3[p] = s.start + i;
+    const u32 len = s.len & SEG_LEN;
+    // a FIRST run keeps its group's rank after round 0
+    if (a.initial || !(s.len & SEG_FIRST) || a.idx3) {
+        for (u32 i = threadIdx.x; i < len; i += WG) {
+            const u32 p = a.SA[s.start + i];
+            a.RK[p] = s.start;
+            if (a.idx3) a.idx3[p] = s.start + i;
+        }
     }
-    if (threadIdx.x == 0) L.next[atomicAdd(L.next_cnt, 1u)] = s;
+    if (threadIdx.x == 0) L.next[atomicAdd(L.next_cnt, 1u)] = Seg{s.start, len};
 }
 
 __global__ void k_update_done(u32* done, const u32* split, u32 nb) {

@@ -70,7 +70,10 @@ struct TScope {
 
 struct kolm_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // main stream
+    hipStream_t aux = nullptr;     // second stream: Lyndon + cyclic sort chain runs beside LZ77
+    hipStream_t active = nullptr;  // stream used by launches / TScope / sync()
+    hipEvent_t evj[4] = {};        // join events
     std::mutex mu;
     std::map<std::string, DevBuf> bufs;
     u32* h_cnt = nullptr;  // pinned mirror of the counters
@@ -134,7 +137,7 @@ struct kolm_ctx {
     T* get(const char* name, size_t count) {
         return static_cast<T*>(raw(name, count * sizeof(T)));
     }
-    void sync() { KOLM_HIP_CHECK(hipStreamSynchronize(stream)); }
+    void sync() { KOLM_HIP_CHECK(hipStreamSynchronize(active)); }
 };
 
 namespace {
@@ -142,13 +145,13 @@ namespace {
 TScope::TScope(kolm_ctx* c_, int fam_, const char* name_, u64 bytes_) : c(c_), fam(fam_), name(name_), bytes(bytes_) {
     if (c->timing) {
         a = c->ev_take();
-        KOLM_HIP_CHECK(hipEventRecord(a, c->stream));
+        KOLM_HIP_CHECK(hipEventRecord(a, c->active));
     }
 }
 TScope::~TScope() noexcept(false) {
     if (c->timing) {
         hipEvent_t b = c->ev_take();
-        KOLM_HIP_CHECK(hipEventRecord(b, c->stream));
+        KOLM_HIP_CHECK(hipEventRecord(b, c->active));
         c->pend.push_back({fam, name, a, b, bytes});
     }
 }
@@ -173,7 +176,7 @@ struct SortOut {
 // SA3 = SA, gs3 = RK (group start slot by position) and idx3 (slot by position) for LZ77.
 SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, const u64* FSL, bool capture3,
                   bool round0_only) {
-    hipStream_t s = c->stream;
+    hipStream_t s = c->active;
     const u64 N = geo.N;
     SortOut out;
     SortArgs a{};
@@ -328,35 +331,46 @@ struct Pipeline {
     kolm_stats st{};
     float t_sa = 0, t_lz = 0, t_ent = 0, t_emit = 0;
 
-    // BBWT of every block into "bbwt"; 3-gram candidate arrays (SA3, idx3, GS3) for LZ77
-    u8* bbwt() {
+    // Lyndon factorisation of every block -> FSL (on the active stream)
+    void lyndon() {
+        const u64 N = geo.N;
+        const u64 ntiles = (u64)((geo.bs + TILE - 1) / TILE) * geo.nb + 16;
+        // Duval: text read ~2x + factor starts 4 B; merge; flags; FSL scans write 8 B
+        TScope t(c, KOLM_KT_LYNDON, "k_duval+lyndon_scans", N * 16);
+        const u64 nch = (geo.bs + 4095) / 4096 * (u64)geo.nb + 1;
+        launch_lyndon(geo, text, c->get<u8>("flag", N), c->get<u64>("FSL", N), c->get<u32>("lyn_fstart", N),
+                      c->get<u32>("lyn_nfac", nch), c->get<u32>("lyn_stack", N), c->get<u32>("lyn_t1", 2 * ntiles + 16),
+                      c->get<u32>("lyn_t2", 2 * ntiles + 2 * geo.nb + 16), c->active);
+    }
+    // linear suffix order at 3 characters only: LZ77 candidate groups (SA3, idx3, GS3)
+    void linear3() {
+        SortOut lin = sort_pass(c, geo, text, false, nullptr, true, true);
+        st.lin_rounds = lin.rounds;
+        st.lin_active = lin.active;
+    }
+    // omega-order of all rotations of the Lyndon factors + BBWT gather -> "bbwt"
+    u8* cyclic() {
         const u64 N = geo.N;
         u64* FSL = c->get<u64>("FSL", N);
-        u8* flag = c->get<u8>("flag", N);
-        const u64 ntiles = (u64)((geo.bs + TILE - 1) / TILE) * geo.nb + 16;
-        u32* t1 = c->get<u32>("tile_tmp", 2 * ntiles + 16);
-        u32* t2 = c->get<u32>("tile_tmp2", 2 * ntiles + 2 * geo.nb + 16);
-        // linear suffix order is needed only at 3 characters (LZ77 candidate groups)
-        SortOut lin = sort_pass(c, geo, text, false, nullptr, true, true);
-        {
-            // Duval: text read ~2x + factor starts 4 B; merge; flags; FSL scans write 8 B
-            TScope t(c, KOLM_KT_LYNDON, "k_duval+lyndon_scans", N * 16);
-            const u64 nch = (geo.bs + 4095) / 4096 * (u64)geo.nb + 1;
-            launch_lyndon(geo, text, flag, FSL, c->get<u32>("lyn_fstart", N), c->get<u32>("lyn_nfac", nch),
-                          c->get<u32>("lyn_stack", N), t1, t2, c->stream);
-        }
         SortOut cyc = sort_pass(c, geo, text, true, FSL, false, false);
         u8* out = c->get<u8>("bbwt", N);
+        u8* prevc = c->get<u8>("prevc", N);
         {
-            // SA 4 + FSL 8 + text 1 + out 1
-            TScope t(c, KOLM_KT_LYNDON, "k_bbwt_gather", N * 14);
-            launch_bbwt_gather(geo, text, c->get<u32>("SA", N), FSL, out, c->stream);
+            TScope t(c, KOLM_KT_LYNDON, "k_prevc", N * 10);  // FSL 8 + text 1 + prevc 1 (streaming)
+            launch_prevc(geo, text, FSL, prevc, c->active);
         }
-        st.lin_rounds = lin.rounds;
+        {
+            TScope t(c, KOLM_KT_LYNDON, "k_bbwt_gather", N * 6);  // SA 4 + prevc 1 + out 1
+            launch_bbwt_gather(geo, c->get<u32>("SA", N), prevc, out, c->active);
+        }
         st.cyc_rounds = cyc.rounds;
-        st.lin_active = lin.active;
         st.cyc_active = cyc.active;
         return out;
+    }
+    u8* bbwt() {
+        linear3();
+        lyndon();
+        return cyclic();
     }
 
     u8* mtf(const u8* in) {
@@ -366,7 +380,7 @@ struct Pipeline {
         // summary: read N; compose: summaries + states 512 B/chunk; replay: N in, N out, state
         TScope t(c, KOLM_KT_MTF, "k_mtf_summary+compose+replay", 3 * N + nch * 768);
         launch_mtf(geo, in, out, c->get<u8>("mtf_sum", nch * 256), c->get<u16>("mtf_cnt", nch),
-                   c->get<u8>("mtf_states", nch * 256), c->stream);
+                   c->get<u8>("mtf_states", nch * 256), c->active);
         return out;
     }
 
@@ -404,11 +418,11 @@ struct Pipeline {
     }
 
     void lz(const LzArgs& z) {
-        KOLM_HIP_CHECK(hipMemsetAsync(z.nlong, 0, sizeof(u32), c->stream));
+        KOLM_HIP_CHECK(hipMemsetAsync(z.nlong, 0, sizeof(u32), c->active));
         {
             // idx3 + gs3 windows (8 B per position) + text; 16 B per token added after the batch
             TScope t(c, KOLM_KT_LZPARSE, "k_lz_spec+stitch", geo.N * 9);
-            launch_lz_parse(z, c->stream);
+            launch_lz_parse(z, c->active);
         }
     }
 };
@@ -443,12 +457,33 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
         if (stats) *stats = kolm_stats{};
         return KOLM_OK;
     }
-    hipStream_t s = c->stream;
+    // Two streams: main runs the 3-gram linear sort and then the LZ77 parse; aux runs the
+    // Lyndon factorisation (beside the linear sort), then the cyclic sort, BBWT, MTF and
+    // the size kernels (beside LZ77), joins LZ77 and finishes MDL + emission.
+    hipStream_t ms = c->stream, s = c->aux;
     Pipeline P{c, geo, d_text};
     hipEvent_t* ev = c->ev;
+    hipEvent_t* ej = c->evj;
     c->timing_reset();
-    KOLM_HIP_CHECK(hipEventRecord(ev[0], s));
-    u8* bw = P.bbwt();
+    struct Restore {
+        kolm_ctx* c;
+        ~Restore() { c->active = c->stream; }
+    } restore{c};
+    KOLM_HIP_CHECK(hipEventRecord(ev[0], ms));
+    KOLM_HIP_CHECK(hipStreamWaitEvent(s, ev[0], 0));
+    c->active = s;
+    P.lyndon();
+    c->active = ms;
+    P.linear3();
+    KOLM_HIP_CHECK(hipEventRecord(ej[0], ms));
+    LzArgs z = P.lz_args();
+    const bool want_lz = (mask >> KOLM_M_LZ77) & 1u || (h_force != nullptr);
+    KOLM_HIP_CHECK(hipEventRecord(ej[2], ms));
+    if (want_lz) P.lz(z);
+    KOLM_HIP_CHECK(hipEventRecord(ej[1], ms));
+    c->active = s;
+    KOLM_HIP_CHECK(hipStreamWaitEvent(s, ej[0], 0));
+    u8* bw = P.cyclic();
     KOLM_HIP_CHECK(hipEventRecord(ev[1], s));
     u8* mt = P.mtf(bw);
     EmitArgs e{};
@@ -477,9 +512,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
         launch_cheap_and_rice_sizes(e, s);
     }
     KOLM_HIP_CHECK(hipEventRecord(ev[2], s));
-    LzArgs z = P.lz_args();
-    const bool want_lz = (mask >> KOLM_M_LZ77) & 1u || (h_force != nullptr);
-    if (want_lz) P.lz(z);
+    KOLM_HIP_CHECK(hipStreamWaitEvent(s, ej[1], 0));
     KOLM_HIP_CHECK(hipEventRecord(ev[3], s));
     u32* cnt = c->get<u32>("counters", C_N);
     KOLM_HIP_CHECK(hipMemsetAsync(cnt + C_STATUS, 0, sizeof(u32), s));
@@ -522,7 +555,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
         st.lz_long = c->h_cnt[C_NLONG];
         st.ms_sa = ev_ms(ev[0], ev[1]);
         st.ms_entropy = ev_ms(ev[1], ev[2]);
-        st.ms_lz = ev_ms(ev[2], ev[3]);
+        st.ms_lz = ev_ms(ej[2], ej[1]);
         st.ms_emit = ev_ms(ev[3], ev[4]);
         st.ms_total = ev_ms(ev[0], ev[4]);
     }
@@ -557,6 +590,9 @@ int ctx_create(int device, kolm_ctx** out) {
         std::unique_ptr<kolm_ctx> c(new kolm_ctx);
         c->device = device;
         KOLM_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        KOLM_HIP_CHECK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+        c->active = c->stream;
+        for (auto& e : c->evj) KOLM_HIP_CHECK(hipEventCreate(&e));
         KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_cnt, sizeof(u32) * C_N, hipHostMallocDefault));
         for (auto& e : c->ev) KOLM_HIP_CHECK(hipEventCreate(&e));
         *out = c.release();
@@ -601,12 +637,15 @@ int kolm_ctx_destroy(kolm_ctx* c) {
     return guarded([&] {
         KOLM_HIP_CHECK(hipSetDevice(c->device));
         KOLM_HIP_CHECK(hipStreamSynchronize(c->stream));
+        KOLM_HIP_CHECK(hipStreamSynchronize(c->aux));
         for (auto& kv : c->bufs)
             if (kv.second.p) KOLM_HIP_CHECK(hipFree(kv.second.p));
         for (auto& e : c->ev) KOLM_HIP_CHECK(hipEventDestroy(e));
+        for (auto& e : c->evj) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evpool) KOLM_HIP_CHECK(hipEventDestroy(e));
         KOLM_HIP_CHECK(hipHostFree(c->h_cnt));
         KOLM_HIP_CHECK(hipStreamDestroy(c->stream));
+        KOLM_HIP_CHECK(hipStreamDestroy(c->aux));
         delete c;
         return KOLM_OK;
     });

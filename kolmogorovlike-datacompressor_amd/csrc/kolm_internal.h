@@ -27,7 +27,11 @@ constexpr int LZ_CAP = 32;        // per-lane capped compare; longer candidates 
 constexpr int MTF_CHUNK = 1024;   // bytes replayed per thread by the MTF kernel
 constexpr u32 NCAND = 9;          // candidate ids 0..8 computed on the device
 
-// Segment of the suffix array still to be refined: SA[start .. start+len).
+// Segment of the suffix array still to be refined: SA[start .. start+len).  Bit 31 of
+// len (SEG_FIRST) marks a segment that begins at the start of its round group, so its
+// first run of equal keys keeps the group's rank (no RK rewrite needed).
+constexpr u32 SEG_FIRST = 0x80000000u;
+constexpr u32 SEG_LEN = 0x7FFFFFFFu;
 struct Seg {
     u32 start;
     u32 len;
@@ -127,8 +131,8 @@ void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, hipStream_t
 void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u32* fstart, u32* nfac, u32* stack,
                    u32* tile_tmp, u32* tile_tmp2, hipStream_t s);
 void launch_lyndon_isa(const Geom& geo, const u32* RK, u8* flag, u32* tile_tmp, u32* tile_tmp2, hipStream_t s);
-void launch_bbwt_gather(const Geom& geo, const u8* text, const u32* SA, const u64* FSL, u8* out,
-                        hipStream_t s);
+void launch_prevc(const Geom& geo, const u8* text, const u64* FSL, u8* prevc, hipStream_t s);
+void launch_bbwt_gather(const Geom& geo, const u32* SA, const u8* prevc, u8* out, hipStream_t s);
 
 // ---- k_mtf.hip ----
 void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summary_cnt, u8* states,
