@@ -88,6 +88,7 @@ __device__ inline u32 cyc_succ(const SortArgs& a, u32 p, u32 h) {
 }
 
 __device__ inline u32 make_key(const SortArgs& a, u32 p, u32 base, u32 end) {
+    if (a.KP) return a.KP[p];
     if (a.initial) {
         if (!a.cyclic) {
             u32 c0 = (u32)a.text[p] + 1;
@@ -110,6 +111,16 @@ __device__ inline u32 make_key(const SortArgs& a, u32 p, u32 base, u32 end) {
         return q < end ? a.RK[q] - base + 1 : 0;
     }
     return a.RK[cyc_succ(a, p, a.h)] - base;
+}
+
+// Keys of every position in position order: the factor record and RK[succ^h(p)] are read
+// (nearly) sequentially here, so the per-slot key generation needs a single random gather.
+__global__ __launch_bounds__(256) void k_keypos(SortArgs a, u32* KP) {
+    a.KP = nullptr;
+    for (u32 p = blockIdx.x * blockDim.x + threadIdx.x; p < a.geo.N; p += gridDim.x * blockDim.x) {
+        const u32 b = a.geo.block_of(p);
+        KP[p] = make_key(a, p, a.geo.base(b), a.geo.end(b));
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -585,6 +596,12 @@ void launch_classify(const Seg* cur, u32 ncur, const SortArgs& a, const Lists& L
                      hipStream_t s) {
     if (ncur) k_classify<<<cdiv(ncur, 256), 256, 0, s>>>(cur, ncur, a, L, lv0);
 }
+void launch_keypos(const SortArgs& a, u32* KP, hipStream_t s) {
+    if (!a.geo.N) return;
+    const u32 grid = (u32)std::min<u64>((a.geo.N + 255) / 256, 8192);
+    k_keypos<<<grid, 256, 0, s>>>(a, KP);
+}
+
 void launch_keygen_small(int c, const Seg* segs, u32 count, const SortArgs& a, hipStream_t s) {
     if (count) k_keygen_small<<<cdiv(count, TILE >> c), WG, 0, s>>>(segs, count, c, a);
 }

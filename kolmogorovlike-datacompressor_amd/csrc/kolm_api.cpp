@@ -247,8 +247,18 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
         out.active += h[C_ACTIVE];
         out.rounds = round + 1;
         {
+            // Dense rounds: keys by position first (sequential pass), then one gather per
+            // slot; sparse rounds gather the key inputs per active slot directly.
+            a.KP = nullptr;
+            if ((u64)h[C_ACTIVE] * 8 > N) {
+                u32* KP = c->get<u32>("KP", N);
+                // cyclic: FSL 8 + RK 4 (or text 4) + KP 4; linear: RK 4 (text 3) + KP 4
+                TScope t(c, KOLM_KT_KEYGEN, "k_keypos", N * (cyclic ? 16 : 8));
+                launch_keypos(a, KP, s);
+                a.KP = KP;
+            }
             // algorithmic bytes per element: SA read + key inputs + K2 write
-            const u64 per = a.initial ? (cyclic ? 20 : 11) : (cyclic ? 20 : 12);
+            const u64 per = a.KP ? 12 : a.initial ? (cyclic ? 20 : 11) : (cyclic ? 20 : 12);
             for (int k = 1; k < NCLASS; ++k) {
                 if (!h[C_CLS + k]) continue;
                 TScope t(c, KOLM_KT_KEYGEN, "k_keygen_small", (u64)h[C_CLSE + k] * per);

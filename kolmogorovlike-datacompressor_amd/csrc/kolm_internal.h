@@ -84,6 +84,7 @@ struct SortArgs {
     int initial;       // round 0: keys are packed characters
     u32 h;             // doubling offset of this round (round >= 1)
     u32* idx3;         // linear round 0 only: idx3[p] = SA slot of p (3-gram order), else null
+    const u32* KP;     // [N] this round's key by position (k_keypos), or null: keys gathered directly
 };
 
 // Append-only lists written by the classify / MSD / small-sort kernels.
@@ -111,6 +112,7 @@ void launch_iota(u32* SA, u64 N, hipStream_t s);
 void launch_block_segs(Seg* segs, const Geom& geo, hipStream_t s);
 void launch_classify(const Seg* cur, u32 ncur, const SortArgs& a, const Lists& L, const Level& lv0,
                      hipStream_t s);
+void launch_keypos(const SortArgs& a, u32* KP, hipStream_t s);
 void launch_keygen_small(int c, const Seg* segs, u32 count, const SortArgs& a, hipStream_t s);
 void launch_keygen_large(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
                          hipStream_t s);
