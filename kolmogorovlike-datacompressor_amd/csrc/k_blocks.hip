@@ -188,44 +188,155 @@ __global__ __launch_bounds__(WG) void k_fsfl(TileGeom tg, const u8* flag, const 
 }
 
 // ---------------------------------------------------------------------------------
-// Parallel Duval (restates PY:326-349 exactly): Duval on every DUVAL_CHUNK-byte chunk
-// (one thread each), then one wave per block merges the chunk factorizations left to
-// right with the concatenation rule: for Lyndon words x < y, xy is Lyndon, so pushing
-// the next chunk's factors on the stack of the prefix's factors and merging while
-// stack[-2] < stack[-1] yields the (unique) Lyndon factorization of the concatenation;
-// once a right factor is pushed without merging the remaining right factors (which are
-// non-increasing) cannot merge either and are appended in bulk.
+// Parallel Duval (restates PY:326-349 exactly) in two levels.
+//   k_duval_span: one workgroup per DUVAL_SPAN-byte span of a block, staged in LDS.
+//     Every thread runs Duval on its DUVAL_CH-byte chunk, then the chunk factorizations
+//     are merged pairwise up a binary tree (8 levels) inside LDS; factor starts are kept
+//     as a bitmap.  Merge rule (concatenation of two factorizations): for Lyndon words
+//     x < y, xy is Lyndon, so pushing the right part's factors on the stack of the left
+//     part's factors and merging while stack[-2] < stack[-1] gives the (unique) Lyndon
+//     factorization of the concatenation; once a right factor is pushed without merging,
+//     the remaining right factors (non-increasing) cannot merge either.
+//   k_duval_merge: one wave per block merges the span factorizations left to right with
+//     the same rule (comparisons read the text from global memory).
 // ---------------------------------------------------------------------------------
-constexpr u32 DUVAL_CHUNK = 4096;
+constexpr u32 DUVAL_CH = 128;                 // bytes per thread
+constexpr u32 DUVAL_SPAN = DUVAL_CH * 256;    // bytes per workgroup (32 KiB)
+constexpr u32 DUVAL_PAD = 4;                  // LDS pad per chunk (bank spread)
 
-__global__ __launch_bounds__(256) void k_duval_chunks(Geom geo, u32 cpb, const u8* s, u32* fstart, u32* nfac,
-                                                      u32 nchunks) {
-    const u32 c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nchunks) return;
-    const u32 b = c / cpb, k = c - b * cpb;
-    const u32 lo = geo.base(b) + k * DUVAL_CHUNK;
+__device__ inline u32 lds_addr(u32 q) { return q + (q / DUVAL_CH) * DUVAL_PAD; }
+
+// x = t[x0, x1) < y = t[x1, y1) (span-local positions, proper prefix smaller)
+__device__ inline bool span_less(const u8* t, u32 x0, u32 x1, u32 y1) {
+    const u32 la = x1 - x0, lb = y1 - x1, m = min(la, lb);
+    for (u32 i = 0; i < m; ++i) {
+        const u8 a = t[lds_addr(x0 + i)], b = t[lds_addr(x1 + i)];
+        if (a != b) return a < b;
+    }
+    return la < lb;
+}
+
+// largest set bit position <= q (bit lo is always set)
+__device__ inline u32 bm_prev(const u32* bm, u32 q) {
+    u32 w = q >> 5;
+    u32 v = bm[w] & (0xFFFFFFFFu >> (31 - (q & 31)));
+    while (!v) v = bm[--w];
+    return (w << 5) + 31 - __clz(v);
+}
+// smallest set bit position >= q, or hi
+__device__ inline u32 bm_next(const u32* bm, u32 q, u32 hi) {
+    if (q >= hi) return hi;
+    u32 w = q >> 5;
+    u32 v = bm[w] & (0xFFFFFFFFu << (q & 31));
+    const u32 wl = (hi + 31) >> 5;
+    while (!v) {
+        if (++w >= wl) return hi;
+        v = bm[w];
+    }
+    const u32 r = (w << 5) + __ffs(v) - 1;
+    return r < hi ? r : hi;
+}
+
+__global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8* s, u32* fstart, u32* nfac) {
+    __shared__ __align__(16) u8 t[DUVAL_SPAN + 256 * DUVAL_PAD];
+    __shared__ u32 bm[DUVAL_SPAN / 32];
+    __shared__ u32 sh[WG / 64];
+    const u32 sp = blockIdx.x, tid = threadIdx.x;
+    const u32 b = sp / spb, k = sp - b * spb;
+    const u32 lo = geo.base(b) + k * DUVAL_SPAN;
     const u32 e = geo.end(b);
     if (lo >= e) {
-        nfac[c] = 0;
+        if (tid == 0) nfac[sp] = 0;
         return;
     }
-    const u32 hi = min(lo + DUVAL_CHUNK, e);
-    u32 i = lo, nf = 0;
-    while (i < hi) {
-        u32 j = i + 1, kk = i;
-        while (j < hi) {
-            const u8 a = s[kk], bb = s[j];
-            if (a > bb) break;
-            kk = (a < bb) ? i : kk + 1;
-            ++j;
+    const u32 n = min(DUVAL_SPAN, e - lo);
+    // stage the span (16-byte loads when aligned and whole)
+    if (n == DUVAL_SPAN && (lo & 15) == 0) {
+        const uint4* src = reinterpret_cast<const uint4*>(s + lo);
+        for (u32 i = tid; i < DUVAL_SPAN / 16; i += 256) {
+            const uint4 v = src[i];
+            u32* d = reinterpret_cast<u32*>(&t[lds_addr(i * 16)]);  // 4-byte aligned, inside one chunk
+            d[0] = v.x;
+            d[1] = v.y;
+            d[2] = v.z;
+            d[3] = v.w;
         }
-        const u32 p = j - kk;
-        while (i <= kk) {
-            fstart[lo + nf++] = i;
-            i += p;
+    } else {
+        for (u32 i = tid; i < n; i += 256) t[lds_addr(i)] = s[lo + i];
+    }
+    for (u32 i = tid; i < DUVAL_SPAN / 32; i += 256) bm[i] = 0;
+    __syncthreads();
+    // Duval on the thread's chunk; factor starts -> bitmap (bits of one chunk are 4 words
+    // owned by this thread only)
+    {
+        const u32 clo = tid * DUVAL_CH, chi = min(clo + DUVAL_CH, n);
+        u32 i = clo;
+        while (i < chi) {
+            u32 j = i + 1, kk = i;
+            while (j < chi) {
+                const u8 a = t[lds_addr(kk)], bb = t[lds_addr(j)];
+                if (a > bb) break;
+                kk = (a < bb) ? i : kk + 1;
+                ++j;
+            }
+            const u32 p = j - kk;
+            while (i <= kk) {
+                bm[i >> 5] |= 1u << (i & 31);
+                i += p;
+            }
         }
     }
-    nfac[c] = nf;
+    __syncthreads();
+    // tree merge of adjacent factorizations
+    for (u32 w = DUVAL_CH; w < DUVAL_SPAN; w <<= 1) {
+        const u32 a0 = tid * 2 * w, m = a0 + w;
+        if (m < n) {
+            const u32 hi = min(m + w, n);
+            u32 r = m;
+            while (r < hi) {
+                const u32 re = bm_next(bm, r + 1, hi);
+                u32 ts = r;
+                bool merged = false;
+                while (ts > a0) {
+                    const u32 ps = bm_prev(bm, ts - 1);
+                    if (!span_less(t, ps, ts, re)) break;
+                    bm[ts >> 5] &= ~(1u << (ts & 31));
+                    ts = ps;
+                    merged = true;
+                }
+                if (!merged) break;
+                r = re;
+            }
+        }
+        __syncthreads();
+    }
+    // compact the factor starts of the span into fstart[lo ...]
+    u32 cnt = 0;
+    for (u32 q = 0; q < DUVAL_CH / 32; ++q) cnt += __popc(bm[tid * (DUVAL_CH / 32) + q]);
+    u32 o = 0;
+    {
+        // exclusive scan over 256 threads
+        const u32 lane = tid & 63, wv = tid >> 6;
+        u32 incl = cnt;
+        for (u32 d = 1; d < 64; d <<= 1) {
+            const u32 x = __shfl_up(incl, d);
+            if (lane >= d) incl += x;
+        }
+        if (lane == 63) sh[wv] = incl;
+        __syncthreads();
+        u32 carry = 0;
+        for (u32 i = 0; i < wv; ++i) carry += sh[i];
+        o = carry + incl - cnt;
+        if (tid == 255) nfac[sp] = carry + incl;
+    }
+    for (u32 q = 0; q < DUVAL_CH / 32; ++q) {
+        u32 v = bm[tid * (DUVAL_CH / 32) + q];
+        while (v) {
+            const u32 bit = __ffs(v) - 1;
+            v &= v - 1;
+            fstart[lo + o++] = lo + tid * DUVAL_CH + q * 32 + bit;
+        }
+    }
 }
 
 // x = s[a0, a1) < y = s[a1, b1) lexicographically (proper prefix smaller); wave-uniform
@@ -252,9 +363,9 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
     u32 sp = 0;
     for (u32 k = 0; k < cpb; ++k) {
         const u32 c = b * cpb + k;
-        const u32 lo = base + k * DUVAL_CHUNK;
+        const u32 lo = base + k * DUVAL_SPAN;
         if (lo >= end) break;
-        const u32 hi = min(lo + DUVAL_CHUNK, end);
+        const u32 hi = min(lo + DUVAL_SPAN, end);
         const u32 nf = nfac[c];
         u32 t = 0;
         while (t < nf) {
@@ -321,10 +432,10 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u32* fst
     u32* B = tile_tmp + nt;   // [nt]
     u32* C2 = tile_tmp2;      // [nt]
     u32* D = tile_tmp2 + nt;  // [nt]
-    const u32 cpb = (geo.bs + DUVAL_CHUNK - 1) / DUVAL_CHUNK;
+    const u32 cpb = (geo.bs + DUVAL_SPAN - 1) / DUVAL_SPAN;
     const u32 nch = cpb * geo.nb;
     KOLM_HIP_CHECK(hipMemsetAsync(flag, 0, geo.N, s));
-    k_duval_chunks<<<(nch + 255) / 256, 256, 0, s>>>(geo, cpb, text, fstart, nfac, nch);
+    k_duval_span<<<nch, 256, 0, s>>>(geo, cpb, text, fstart, nfac);
     k_duval_merge<<<geo.nb, 64, 0, s>>>(geo, cpb, text, fstart, nfac, stack, flag);
     k_tile_starts<<<nt, WG, 0, s>>>(tg, flag, A, C2);
     k_tiles_scan<false, true><<<geo.nb, WG, 0, s>>>(A, B, tg.tpb, 0u);

@@ -1,0 +1,300 @@
+// 3-gram candidate index for LZ77 (gfx950): every block's positions grouped by their
+// 3-byte prefix, positions ascending inside a group.
+//
+// The reference's LZ77 (PY:1711-1763) finds, for each position, the longest earlier
+// match inside the 4096-byte window by walking previous occurrences of the current
+// 3-byte prefix (hash chain, nearest first).  Here the chain is materialised as a sorted
+// array: SA3 = the block's positions stably sorted by their 24-bit 3-gram, so the
+// candidates of p are the contiguous slots idx3[p]-1, idx3[p]-2, ... down to the group
+// start gs3[p] (ascending distance).  Positions with fewer than 3 bytes left in the
+// block (the last two) cannot start a match and become singleton groups in the block's
+// last two slots.  Group ORDER is irrelevant to LZ77; only the grouping and the
+// position order inside a group are used.
+//
+// Three stable LSD passes of 8 bits (c2, c1, c0) per block with 4096-element tiles:
+//   hist (per-wave LDS histograms) -> per-block scan over (digit, tile) -> stable scatter
+// (wave ballot ranking), then group starts by a per-block max-scan of group heads.
+// No host synchronisation: the whole index is a fixed sequence of launches that runs on
+// its own stream beside the Lyndon factorisation and the cyclic suffix sort.
+#include "kolm_internal.h"
+
+namespace kolm {
+
+namespace {
+
+constexpr u32 G3T = 4096;          // elements per tile
+constexpr u32 G3PT = G3T / WG;     // 16 per thread
+
+struct G3Geom {
+    Geom geo;
+    u32 tpb;    // tiles per block
+    bool full;  // tiles cover [base, end) (slots) instead of the full-3-gram region
+    __device__ inline u32 fend(u32 b) const {
+        const u32 s = geo.base(b), e = geo.end(b);
+        return e - s >= 2 ? e - 2 : s;
+    }
+    __device__ inline bool range(u32 t, u32& lo, u32& hi, u32& b) const {
+        b = t / tpb;
+        const u32 k = t - b * tpb;
+        lo = geo.base(b) + k * G3T;
+        const u32 e = full ? geo.end(b) : fend(b);
+        hi = min(lo + G3T, e);
+        return lo < e;
+    }
+};
+
+__device__ inline u32 key24(const u8* t, u32 p) {
+    return ((u32)t[p] << 16) | ((u32)t[p + 1] << 8) | (u32)t[p + 2];
+}
+
+template <int P>
+__device__ inline u32 digit(u32 key) {
+    return (key >> (8 * P)) & 255u;
+}
+
+template <int P>
+__global__ __launch_bounds__(WG) void k_g3_hist(G3Geom g, const u8* text, const u32* K, u32* hist) {
+    __shared__ u32 h[WG / 64][256];
+    const u32 tid = threadIdx.x, w = tid >> 6;
+#pragma unroll
+    for (int i = 0; i < WG / 64; ++i) h[i][tid] = 0;
+    __syncthreads();
+    u32 lo, hi, b;
+    if (g.range(blockIdx.x, lo, hi, b)) {
+#pragma unroll 4
+        for (u32 i = lo + tid; i < hi; i += WG) {
+            const u32 d = P == 0 ? (u32)text[i + 2] : digit<P>(K[i]);
+            atomicAdd(&h[w][d], 1u);
+        }
+    }
+    __syncthreads();
+    hist[(u64)blockIdx.x * 256 + tid] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+}
+
+// hist[t][d] -> absolute destination of the first element of digit d in tile t.
+__global__ __launch_bounds__(WG) void k_g3_scan(G3Geom g, u32* hist) {
+    __shared__ u32 sh[WG / 64];
+    const u32 b = blockIdx.x, d = threadIdx.x, lane = d & 63, w = d >> 6;
+    const u64 t0 = (u64)b * g.tpb;
+    constexpr u32 B = 16;
+    u32 acc = 0;
+    for (u32 k = 0; k < g.tpb; k += B) {
+        u32 v[B];
+#pragma unroll
+        for (u32 j = 0; j < B; ++j) v[j] = k + j < g.tpb ? hist[(t0 + k + j) * 256 + d] : 0u;
+#pragma unroll
+        for (u32 j = 0; j < B; ++j) {
+            if (k + j < g.tpb) hist[(t0 + k + j) * 256 + d] = acc;
+            acc += v[j];
+        }
+    }
+    // exclusive scan of the digit totals
+    u32 incl = acc;
+#pragma unroll
+    for (u32 o = 1; o < 64; o <<= 1) {
+        const u32 x = __shfl_up(incl, o);
+        if (lane >= o) incl += x;
+    }
+    if (lane == 63) sh[w] = incl;
+    __syncthreads();
+    u32 carry = 0;
+    for (u32 i = 0; i < w; ++i) carry += sh[i];
+    const u32 base = g.geo.base(b) + carry + incl - acc;
+    for (u32 k = 0; k < g.tpb; k += B) {
+        u32 v[B];
+#pragma unroll
+        for (u32 j = 0; j < B; ++j) v[j] = k + j < g.tpb ? hist[(t0 + k + j) * 256 + d] : 0u;
+#pragma unroll
+        for (u32 j = 0; j < B; ++j)
+            if (k + j < g.tpb) hist[(t0 + k + j) * 256 + d] = v[j] + base;
+    }
+}
+
+// Stable scatter of one tile by digit P: element order e = j*WG + tid; each wave ranks
+// its 64 elements per digit with ballots, per-wave counts are combined in (j, wave)
+// order.  P == 0 reads positions in order and builds the keys from the text.
+template <int P>
+__global__ __launch_bounds__(WG) void k_g3_scatter(G3Geom g, const u8* text, const u32* Kin, const u32* Pin,
+                                                   u32* Kout, u32* Pout, const u32* hist) {
+    __shared__ u32 wcnt[WG / 64][256];
+    __shared__ u32 running[256];
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    u32 lo, hi, b;
+    if (!g.range(blockIdx.x, lo, hi, b)) return;
+    running[tid] = hist[(u64)blockIdx.x * 256 + tid];
+#pragma unroll
+    for (int i = 0; i < WG / 64; ++i) wcnt[i][tid] = 0;
+    __syncthreads();
+    const u64 lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (u32 j = 0; j < G3PT; ++j) {
+        const u32 i = lo + j * WG + tid;
+        const bool valid = i < hi;
+        u32 key = 0, pos = 0, dg = 0;
+        if (valid) {
+            if (P == 0) {
+                key = key24(text, i);
+                pos = i;
+            } else {
+                key = Kin[i];
+                pos = Pin[i];
+            }
+            dg = digit<P>(key);
+        }
+        u64 m = __ballot(valid);
+#pragma unroll
+        for (u32 bit = 0; bit < 8; ++bit) {
+            const u64 bal = __ballot((dg >> bit) & 1u);
+            m &= ((dg >> bit) & 1u) ? bal : ~bal;
+        }
+        const u32 rank = __popcll(m & lt_mask);
+        if (valid && rank == 0) wcnt[w][dg] = __popcll(m);
+        __syncthreads();
+        if (valid) {
+            u32 pre = running[dg];
+            for (u32 q = 0; q < w; ++q) pre += wcnt[q][dg];
+            const u32 dst = pre + rank;
+            Kout[dst] = key;
+            Pout[dst] = pos;
+        }
+        __syncthreads();
+        u32 add = 0;
+#pragma unroll
+        for (int q = 0; q < WG / 64; ++q) {
+            add += wcnt[q][tid];
+            wcnt[q][tid] = 0;
+        }
+        running[tid] += add;
+        __syncthreads();
+    }
+}
+
+__device__ inline u32 wave_max(u32 v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (u32)__shfl_xor(v, o));
+    return v;
+}
+
+// slot g starts a group: first slot of the block, a tail slot, or a new 3-gram
+__device__ inline bool g3_head(const G3Geom& g, const u32* K, u32 slot, u32 base, u32 fe) {
+    return slot == base || slot >= fe || K[slot] != K[slot - 1];
+}
+
+// per slot tile: last group head (0 if none)
+__global__ __launch_bounds__(WG) void k_g3_tile_heads(G3Geom g, const u32* K, u32* tmax) {
+    __shared__ u32 sh[WG / 64];
+    u32 lo, hi, b;
+    u32 mx = 0;
+    if (g.range(blockIdx.x, lo, hi, b)) {
+        const u32 base = g.geo.base(b), fe = g.fend(b);
+        for (u32 i = lo + threadIdx.x; i < hi; i += WG)
+            if (g3_head(g, K, i, base, fe)) mx = max(mx, i);
+    }
+    mx = wave_max(mx);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) tmax[blockIdx.x] = max(max(sh[0], sh[1]), max(sh[2], sh[3]));
+}
+
+// per block: exclusive max over its tiles (one workgroup per block)
+__global__ __launch_bounds__(WG) void k_g3_tiles_scan(const u32* in, u32* out, u32 tpb) {
+    __shared__ u32 sh[WG / 64];
+    __shared__ u32 edge;
+    const u32 b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    u32 carry = 0;
+    for (u32 c0 = 0; c0 < tpb; c0 += WG) {
+        const u32 k = c0 + threadIdx.x;
+        const u32 v = k < tpb ? in[(u64)b * tpb + k] : 0u;
+        u32 incl = v;
+#pragma unroll
+        for (u32 o = 1; o < 64; o <<= 1) {
+            const u32 x = __shfl_up(incl, o);
+            if (lane >= o) incl = max(incl, x);
+        }
+        u32 ex = __shfl_up(incl, 1);
+        if (lane == 0) ex = 0;
+        if (lane == 63) sh[w] = incl;
+        __syncthreads();
+        u32 wc = carry;
+        for (u32 i = 0; i < w; ++i) wc = max(wc, sh[i]);
+        if (k < tpb) out[(u64)b * tpb + k] = max(wc, ex);
+        if (threadIdx.x == WG - 1) edge = max(wc, incl);
+        __syncthreads();
+        carry = edge;
+        __syncthreads();
+    }
+}
+
+// per slot: group start, inverse permutation; tail slots hold their own position
+__global__ __launch_bounds__(WG) void k_g3_final(G3Geom g, const u32* K, u32* SA3, const u32* tcarry, u32* idx3,
+                                                 u32* gs3) {
+    __shared__ u32 sh[WG / 64];
+    u32 lo, hi, b;
+    if (!g.range(blockIdx.x, lo, hi, b)) return;
+    const u32 base = g.geo.base(b), fe = g.fend(b);
+    const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const u32 i0 = lo + threadIdx.x * G3PT;
+    u32 hd[G3PT];
+    u32 loc = 0;
+#pragma unroll
+    for (u32 e = 0; e < G3PT; ++e) {
+        const u32 i = i0 + e;
+        hd[e] = (i < hi && g3_head(g, K, i, base, fe)) ? 1u : 0u;
+        if (hd[e]) loc = max(loc, i);
+    }
+    u32 incl = loc;
+#pragma unroll
+    for (u32 o = 1; o < 64; o <<= 1) {
+        const u32 x = __shfl_up(incl, o);
+        if (lane >= o) incl = max(incl, x);
+    }
+    u32 ex = __shfl_up(incl, 1);
+    if (lane == 0) ex = 0;
+    if (lane == 63) sh[w] = incl;
+    __syncthreads();
+    u32 run = max(tcarry[blockIdx.x], ex);
+    for (u32 i = 0; i < w; ++i) run = max(run, sh[i]);
+#pragma unroll
+    for (u32 e = 0; e < G3PT; ++e) {
+        const u32 i = i0 + e;
+        if (i < hi) {
+            if (hd[e]) run = i;
+            u32 p;
+            if (i >= fe) {
+                p = i;
+                SA3[i] = i;
+            } else {
+                p = SA3[i];
+            }
+            idx3[p] = i;
+            gs3[p] = run;
+        }
+    }
+}
+
+}  // namespace
+
+void launch_gram3(const Geom& geo, const u8* text, const G3Bufs& t, hipStream_t s) {
+    if (!geo.N) return;
+    G3Geom g{geo, (geo.bs + G3T - 1) / G3T, false};
+    const u32 nt = g.tpb * geo.nb;
+    // pass c2: text -> (Ka, Pa = idx3 scratch); c1: -> (Kb, Pb = gs3 scratch); c0: -> (Ka, SA3)
+    u32* Pa = t.idx3;
+    u32* Pb = t.gs3;
+    k_g3_hist<0><<<nt, WG, 0, s>>>(g, text, nullptr, t.hist);
+    k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
+    k_g3_scatter<0><<<nt, WG, 0, s>>>(g, text, nullptr, nullptr, t.Ka, Pa, t.hist);
+    k_g3_hist<1><<<nt, WG, 0, s>>>(g, text, t.Ka, t.hist);
+    k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
+    k_g3_scatter<1><<<nt, WG, 0, s>>>(g, text, t.Ka, Pa, t.Kb, Pb, t.hist);
+    k_g3_hist<2><<<nt, WG, 0, s>>>(g, text, t.Kb, t.hist);
+    k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
+    k_g3_scatter<2><<<nt, WG, 0, s>>>(g, text, t.Kb, Pb, t.Ka, t.SA3, t.hist);
+    G3Geom gs{geo, g.tpb, true};
+    k_g3_tile_heads<<<nt, WG, 0, s>>>(gs, t.Ka, t.tmax);
+    k_g3_tiles_scan<<<geo.nb, WG, 0, s>>>(t.tmax, t.tcarry, g.tpb);
+    k_g3_final<<<nt, WG, 0, s>>>(gs, t.Ka, t.SA3, t.tcarry, t.idx3, t.gs3);
+}
+
+u32 gram3_tiles(const Geom& geo) { return (geo.bs + G3T - 1) / G3T * geo.nb; }
+
+}  // namespace kolm

@@ -347,16 +347,24 @@ struct Pipeline {
         const u64 ntiles = (u64)((geo.bs + TILE - 1) / TILE) * geo.nb + 16;
         // Duval: text read ~2x + factor starts 4 B; merge; flags; FSL scans write 8 B
         TScope t(c, KOLM_KT_LYNDON, "k_duval+lyndon_scans", N * 16);
-        const u64 nch = (geo.bs + 4095) / 4096 * (u64)geo.nb + 1;
+        const u64 nch = (geo.bs + 32767) / 32768 * (u64)geo.nb + 1;  // DUVAL_SPAN
         launch_lyndon(geo, text, c->get<u8>("flag", N), c->get<u64>("FSL", N), c->get<u32>("lyn_fstart", N),
                       c->get<u32>("lyn_nfac", nch), c->get<u32>("lyn_stack", N), c->get<u32>("lyn_t1", 2 * ntiles + 16),
                       c->get<u32>("lyn_t2", 2 * ntiles + 2 * geo.nb + 16), c->active);
     }
     // linear suffix order at 3 characters only: LZ77 candidate groups (SA3, idx3, GS3)
     void linear3() {
-        SortOut lin = sort_pass(c, geo, text, false, nullptr, true, true);
-        st.lin_rounds = lin.rounds;
-        st.lin_active = lin.active;
+        const u64 N = geo.N;
+        const u64 nt = gram3_tiles(geo) + 1;
+        G3Bufs t{c->get<u32>("g3Ka", N), c->get<u32>("g3Kb", N), c->get<u32>("g3hist", nt * 256),
+                 c->get<u32>("g3tmax", nt), c->get<u32>("g3tcarry", nt), c->get<u32>("SA3", N),
+                 c->get<u32>("idx3", N), c->get<u32>("GS3", N)};
+        // 3 LSD passes (hist: 4 B, scatter: 8 B in + 8 B out) + heads/final (K 4 B x2, SA3 4 B,
+        // idx3 + gs3 8 B scattered)
+        TScope ts(c, KOLM_KT_LZPARSE, "k_gram3_index", N * 80);
+        launch_gram3(geo, text, t, c->active);
+        st.lin_rounds = 1;
+        st.lin_active = N;
     }
     // omega-order of all rotations of the Lyndon factors + BBWT gather -> "bbwt"
     u8* cyclic() {
@@ -492,7 +500,6 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
     if (want_lz) P.lz(z);
     KOLM_HIP_CHECK(hipEventRecord(ej[1], ms));
     c->active = s;
-    KOLM_HIP_CHECK(hipStreamWaitEvent(s, ej[0], 0));
     u8* bw = P.cyclic();
     KOLM_HIP_CHECK(hipEventRecord(ev[1], s));
     u8* mt = P.mtf(bw);

@@ -136,6 +136,20 @@ void launch_lyndon_isa(const Geom& geo, const u32* RK, u8* flag, u32* tile_tmp, 
 void launch_prevc(const Geom& geo, const u8* text, const u64* FSL, u8* prevc, hipStream_t s);
 void launch_bbwt_gather(const Geom& geo, const u32* SA, const u8* prevc, u8* out, hipStream_t s);
 
+// ---- k_gram3.hip: 3-gram candidate index for LZ77 ----
+struct G3Bufs {
+    u32* Ka;      // [N] key ping
+    u32* Kb;      // [N] key pong
+    u32* hist;    // [gram3_tiles * 256]
+    u32* tmax;    // [gram3_tiles]
+    u32* tcarry;  // [gram3_tiles]
+    u32* SA3;     // [N] out: positions grouped by 3-gram, ascending inside a group
+    u32* idx3;    // [N] out: slot of each position
+    u32* gs3;     // [N] out: first slot of each position's group
+};
+u32 gram3_tiles(const Geom& geo);
+void launch_gram3(const Geom& geo, const u8* text, const G3Bufs& t, hipStream_t s);
+
 // ---- k_mtf.hip ----
 void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summary_cnt, u8* states,
                 hipStream_t s);
