@@ -216,21 +216,39 @@ __device__ inline bool span_less(const u8* t, u32 x0, u32 x1, u32 y1) {
     return la < lb;
 }
 
-// largest set bit position <= q (bit lo is always set)
-__device__ inline u32 bm_prev(const u32* bm, u32 q) {
+// Two-level bitmap of factor starts: bm (1 bit per position) + sm (1 bit per non-zero bm
+// word), so a search across a long factor costs O(len / 1024) instead of O(len / 32).
+// largest set bit position <= q (a set bit at or below q must exist)
+__device__ inline u32 bm_prev(const u32* bm, const u32* sm, u32 q) {
     u32 w = q >> 5;
     u32 v = bm[w] & (0xFFFFFFFFu >> (31 - (q & 31)));
-    while (!v) v = bm[--w];
+    if (!v) {
+        // previous non-zero word below w
+        u32 sw = w >> 5;
+        u32 sv = (w & 31) ? (sm[sw] & (0xFFFFFFFFu >> (32 - (w & 31)))) : 0u;
+        while (!sv) sv = sm[--sw];
+        w = (sw << 5) + 31 - __clz(sv);
+        v = bm[w];
+    }
     return (w << 5) + 31 - __clz(v);
 }
 // smallest set bit position >= q, or hi
-__device__ inline u32 bm_next(const u32* bm, u32 q, u32 hi) {
+__device__ inline u32 bm_next(const u32* bm, const u32* sm, u32 q, u32 hi) {
     if (q >= hi) return hi;
     u32 w = q >> 5;
     u32 v = bm[w] & (0xFFFFFFFFu << (q & 31));
-    const u32 wl = (hi + 31) >> 5;
-    while (!v) {
-        if (++w >= wl) return hi;
+    if (!v) {
+        const u32 wl = (hi + 31) >> 5;  // words that may hold bits < hi
+        const u32 swl = (wl + 31) >> 5;
+        u32 sw = (w + 1) >> 5;
+        if (sw >= swl) return hi;
+        u32 sv = ((w + 1) & 31) ? (sm[sw] & (0xFFFFFFFFu << ((w + 1) & 31))) : sm[sw];
+        while (!sv) {
+            if (++sw >= swl) return hi;
+            sv = sm[sw];
+        }
+        w = (sw << 5) + __ffs(sv) - 1;
+        if (w >= wl) return hi;
         v = bm[w];
     }
     const u32 r = (w << 5) + __ffs(v) - 1;
@@ -240,6 +258,7 @@ __device__ inline u32 bm_next(const u32* bm, u32 q, u32 hi) {
 __global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8* s, u32* fstart, u32* nfac) {
     __shared__ __align__(16) u8 t[DUVAL_SPAN + 256 * DUVAL_PAD];
     __shared__ u32 bm[DUVAL_SPAN / 32];
+    __shared__ u32 sm[DUVAL_SPAN / 1024];
     __shared__ u32 sh[WG / 64];
     const u32 sp = blockIdx.x, tid = threadIdx.x;
     const u32 b = sp / spb, k = sp - b * spb;
@@ -287,6 +306,12 @@ __global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8*
         }
     }
     __syncthreads();
+    if (tid < DUVAL_SPAN / 1024) {
+        u32 v = 0;
+        for (u32 q = 0; q < 32; ++q) v |= (bm[tid * 32 + q] != 0) << q;
+        sm[tid] = v;
+    }
+    __syncthreads();
     // tree merge of adjacent factorizations
     for (u32 w = DUVAL_CH; w < DUVAL_SPAN; w <<= 1) {
         const u32 a0 = tid * 2 * w, m = a0 + w;
@@ -294,13 +319,15 @@ __global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8*
             const u32 hi = min(m + w, n);
             u32 r = m;
             while (r < hi) {
-                const u32 re = bm_next(bm, r + 1, hi);
+                const u32 re = bm_next(bm, sm, r + 1, hi);
                 u32 ts = r;
                 bool merged = false;
                 while (ts > a0) {
-                    const u32 ps = bm_prev(bm, ts - 1);
+                    const u32 ps = bm_prev(bm, sm, ts - 1);
                     if (!span_less(t, ps, ts, re)) break;
-                    bm[ts >> 5] &= ~(1u << (ts & 31));
+                    const u32 nw = bm[ts >> 5] & ~(1u << (ts & 31));
+                    bm[ts >> 5] = nw;
+                    if (!nw) atomicAnd(&sm[ts >> 10], ~(1u << ((ts >> 5) & 31)));
                     ts = ps;
                     merged = true;
                 }

@@ -225,8 +225,7 @@ __global__ __launch_bounds__(WG) void k_g3_tiles_scan(const u32* in, u32* out, u
 }
 
 // per slot: group start, inverse permutation; tail slots hold their own position
-__global__ __launch_bounds__(WG) void k_g3_final(G3Geom g, const u32* K, u32* SA3, const u32* tcarry, u32* idx3,
-                                                 u32* gs3) {
+__global__ __launch_bounds__(WG) void k_g3_final(G3Geom g, const u32* K, u32* SA3, const u32* tcarry, uint2* ig3) {
     __shared__ u32 sh[WG / 64];
     u32 lo, hi, b;
     if (!g.range(blockIdx.x, lo, hi, b)) return;
@@ -265,8 +264,7 @@ __global__ __launch_bounds__(WG) void k_g3_final(G3Geom g, const u32* K, u32* SA
             } else {
                 p = SA3[i];
             }
-            idx3[p] = i;
-            gs3[p] = run;
+            ig3[p] = make_uint2(i, run);  // one 8-byte scattered store
         }
     }
 }
@@ -277,9 +275,9 @@ void launch_gram3(const Geom& geo, const u8* text, const G3Bufs& t, hipStream_t 
     if (!geo.N) return;
     G3Geom g{geo, (geo.bs + G3T - 1) / G3T, false};
     const u32 nt = g.tpb * geo.nb;
-    // pass c2: text -> (Ka, Pa = idx3 scratch); c1: -> (Kb, Pb = gs3 scratch); c0: -> (Ka, SA3)
-    u32* Pa = t.idx3;
-    u32* Pb = t.gs3;
+    // pass c2: text -> (Ka, Pa); c1: -> (Kb, Pb); c0: -> (Ka, SA3); Pa/Pb live in ig3 (free until final)
+    u32* Pa = reinterpret_cast<u32*>(t.ig3);
+    u32* Pb = Pa + geo.N;
     k_g3_hist<0><<<nt, WG, 0, s>>>(g, text, nullptr, t.hist);
     k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
     k_g3_scatter<0><<<nt, WG, 0, s>>>(g, text, nullptr, nullptr, t.Ka, Pa, t.hist);
@@ -292,7 +290,7 @@ void launch_gram3(const Geom& geo, const u8* text, const G3Bufs& t, hipStream_t 
     G3Geom gs{geo, g.tpb, true};
     k_g3_tile_heads<<<nt, WG, 0, s>>>(gs, t.Ka, t.tmax);
     k_g3_tiles_scan<<<geo.nb, WG, 0, s>>>(t.tmax, t.tcarry, g.tpb);
-    k_g3_final<<<nt, WG, 0, s>>>(gs, t.Ka, t.SA3, t.tcarry, t.idx3, t.gs3);
+    k_g3_final<<<nt, WG, 0, s>>>(gs, t.Ka, t.SA3, t.tcarry, t.ig3);
 }
 
 u32 gram3_tiles(const Geom& geo) { return (geo.bs + G3T - 1) / G3T * geo.nb; }

@@ -40,8 +40,15 @@ __device__ inline u32 uleb_len(u32 v) {
 
 __device__ inline u32 tok_bytes(u32 len, u32 dist) { return len ? 1 + uleb_len(len) + uleb_len(dist) : 2; }
 
+// Text accessor (a template point for staged copies of the text).
+struct GText {
+    const u8* g;
+    __device__ inline u8 operator[](u32 x) const { return g[x]; }
+};
+
 // Exact LCP(p, q) >= start, wave-cooperative (64 lanes x 4 bytes per step); maxl bounds it.
-__device__ u32 wave_lcp(const u8* t, u32 p, u32 q, u32 start, u32 maxl) {
+template <class T>
+__device__ u32 wave_lcp(const T& t, u32 p, u32 q, u32 start, u32 maxl) {
     const u32 lane = threadIdx.x & 63;
     u32 l = start;
     for (;;) {
@@ -59,10 +66,10 @@ __device__ u32 wave_lcp(const u8* t, u32 p, u32 q, u32 start, u32 maxl) {
 }
 
 // Longest match at p (uniform across the wave).  i = idx3[p], gs = gs3[p].
-__device__ void best_match(const LzArgs& z, u32 p, u32 end, u32 i, u32 gs, u32& out_len, u32& out_dist,
-                           u32& nlong) {
+template <class T>
+__device__ void best_match(const LzArgs& z, const T& t, u32 p, u32 end, u32 i, u32 gs, u32& out_len,
+                           u32& out_dist, u32& nlong) {
     const u32 lane = threadIdx.x & 63;
-    const u8* t = z.text;
     u32 best = 0, bd = 0;
     if (p + (u32)LZ_MIN <= end && i > gs) {
         const u32 maxl = end - p;
@@ -118,12 +125,15 @@ __device__ void best_match(const LzArgs& z, u32 p, u32 end, u32 i, u32 gs, u32& 
 
 // Speculative parse of one chunk per wave (4 waves per workgroup).
 __global__ __launch_bounds__(256) void k_lz_spec(LzArgs z, u32 nchunks) {
+    // (staging the wave's 12 KiB text window in LDS measured slower: LDS-limited occupancy
+    // exposes the latency of the candidate loads, and the window is L1/L2-resident anyway)
     const u32 lane = threadIdx.x & 63;
     const u32 c = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (c >= nchunks) return;
     const u32 b = c / z.cpb, k = c - b * z.cpb;
     const u32 bend = z.geo.end(b);
     const u32 s = z.geo.base(b) + k * LZ_CHUNK;
+    const GText t{z.text};
     if (s >= bend) {
         if (lane == 0) {
             z.c_ntok[c] = 0;
@@ -136,9 +146,11 @@ __global__ __launch_bounds__(256) void k_lz_spec(LzArgs z, u32 nchunks) {
     // 64-position windows of (idx3, gs3), the next one prefetched
     u32 wbase = s;
     u32 P = wbase + lane;
-    u32 Iw = P < bend ? z.idx3[P] : 0u, Gw = P < bend ? z.gs3[P] : 0u;
+    uint2 v = P < bend ? z.ig3[P] : make_uint2(0u, 0u);
+    u32 Iw = v.x, Gw = v.y;
     P += 64;
-    u32 In = P < bend ? z.idx3[P] : 0u, Gn = P < bend ? z.gs3[P] : 0u;
+    v = P < bend ? z.ig3[P] : make_uint2(0u, 0u);
+    u32 In = v.x, Gn = v.y;
     u32 q = s, ntok = 0, off = 0, nlong = 0, nbuf = 0;
     u32 bpos = 0, blen = 0, bdist = 0, boff = 0;
     while (q < e) {
@@ -150,17 +162,19 @@ __global__ __launch_bounds__(256) void k_lz_spec(LzArgs z, u32 nchunks) {
             } else {
                 wbase = q;
                 const u32 P0 = wbase + lane;
-                Iw = P0 < bend ? z.idx3[P0] : 0u;
-                Gw = P0 < bend ? z.gs3[P0] : 0u;
+                const uint2 w0 = P0 < bend ? z.ig3[P0] : make_uint2(0u, 0u);
+                Iw = w0.x;
+                Gw = w0.y;
             }
             const u32 P1 = wbase + 64 + lane;
-            In = P1 < bend ? z.idx3[P1] : 0u;
-            Gn = P1 < bend ? z.gs3[P1] : 0u;
+            const uint2 w1 = P1 < bend ? z.ig3[P1] : make_uint2(0u, 0u);
+            In = w1.x;
+            Gn = w1.y;
         }
         const u32 cur = q - wbase;
         u32 len, dist;
-        best_match(z, q, bend, __builtin_amdgcn_readlane(Iw, cur), __builtin_amdgcn_readlane(Gw, cur), len, dist,
-                   nlong);
+        best_match(z, t, q, bend, __builtin_amdgcn_readlane(Iw, cur), __builtin_amdgcn_readlane(Gw, cur), len,
+                   dist, nlong);
         if (lane == nbuf) {
             bpos = q;
             blen = len;
@@ -224,7 +238,8 @@ __global__ __launch_bounds__(64) void k_lz_stitch(LzArgs z) {
                     break;
                 }
                 u32 len, dist;
-                best_match(z, q, bend, z.idx3[q], z.gs3[q], len, dist, nlong);
+                const uint2 ig = z.ig3[q];
+                best_match(z, GText{z.text}, q, bend, ig.x, ig.y, len, dist, nlong);
                 if (lane == 0) {
                     z.fix_pos[base + fi] = q;
                     z.fix_len[base + fi] = len;

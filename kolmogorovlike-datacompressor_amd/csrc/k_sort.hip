@@ -395,25 +395,31 @@ __global__ __launch_bounds__(WG) void k_copy_back(const LTile* tiles, const LSeg
 // (key, position) with a bitonic network (distances >= 8 through LDS, < 8 in registers),
 // then split into runs of equal key: new groups.
 // ------------------------------------------------------------------------------------
-template <int J>
-__device__ inline void reg_stage(u64 (&r)[8], u32 tid, u32 k, u32 S) {
+// Sort words: u64 = (key << 32 | position); u32 = (key << C | index in the segment) when
+// key and index fit 32 bits (keys < 2^kbits, elements of a segment are in position order,
+// so index order is position order) — half the LDS traffic and registers.
+template <int J, class KT>
+__device__ inline void reg_stage(KT (&r)[8], u32 tid, u32 k, u32 S) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         if (e & J) continue;
         const u32 i = 8 * tid + e;
         const bool up = (k == S) || ((i & k) == 0);
-        const u64 x = r[e], y = r[e + J];
+        const KT x = r[e], y = r[e + J];
         const bool sw = (x > y) == up;
         r[e] = sw ? y : x;
         r[e + J] = sw ? x : y;
     }
 }
 
-template <int C>
+template <int C, class KT>
 __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, SortArgs a, Lists L) {
     constexpr u32 S = 1u << C;
     constexpr u32 SPT = TILE / S;
-    __shared__ u64 sk[TILE];
+    constexpr bool W32 = sizeof(KT) == 4;
+    constexpr KT NONEK = ~(KT)0;
+    __shared__ KT sk[TILE];
+    __shared__ u32 sa_l[W32 ? TILE : 1];
     __shared__ Seg ss[SPT];
     __shared__ u32 sh[WG / 64];
     __shared__ u32 last_hi[WG];
@@ -430,15 +436,24 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
     for (int j = 0; j < PER_THREAD; ++j) {
         const u32 slot = j * WG + tid;
         const u32 si = slot >> C, k = slot & (S - 1);
-        u64 key = ~0ull;
+        KT key = NONEK;
         if (si < nthis && k < (ss[si].len & SEG_LEN)) {
             const u32 g = ss[si].start + k;
-            key = ((u64)a.K2[g] << 32) | a.SA[g];
+            // (gathering KP[SA[g]] here instead of in k_keygen_small measured slower: the
+            // dependent gather is exposed at the sort's LDS-limited occupancy)
+            const u32 p = a.SA[g];
+            const u32 kv = a.K2[g];
+            if constexpr (W32) {
+                key = (kv << C) | k;
+                sa_l[slot] = p;
+            } else {
+                key = ((u64)kv << 32) | p;
+            }
         }
         sk[slot] = key;
     }
     __syncthreads();
-    u64 r[8];
+    KT r[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) r[e] = sk[8 * tid + e];
     for (u32 k = 2; k <= S; k <<= 1) {
@@ -454,7 +469,7 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
                     const u32 i = ((q >> lj) << (lj + 1)) | (q & (j - 1));
                     const u32 l = i + j;
                     const bool up = (k == S) || ((i & k) == 0);
-                    const u64 x = sk[i], y = sk[l];
+                    const KT x = sk[i], y = sk[l];
                     if ((x > y) == up) {
                         sk[i] = y;
                         sk[l] = x;
@@ -470,20 +485,19 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
         if (k >= 4) reg_stage<2>(r, tid, k, S);
         reg_stage<1>(r, tid, k, S);
     }
+    constexpr u32 HS = W32 ? C : 32;  // key = word >> HS
     // runs of equal key inside each sub-array
-    last_hi[tid] = (u32)(r[7] >> 32);
-    const bool last_valid = r[7] != ~0ull;
+    last_hi[tid] = (u32)(r[7] >> HS);
     __syncthreads();
     bool valid[8], head[8], stop[8];
     u32 prev_hi = tid ? last_hi[tid - 1] : 0;
     bool prev_valid = tid ? true : false;
-    (void)last_valid;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         const u32 i = 8 * tid + e;
         const u32 kk = i & (S - 1);
-        valid[e] = r[e] != ~0ull;
-        const u32 hi = (u32)(r[e] >> 32);
+        valid[e] = r[e] != NONEK;
+        const u32 hi = (u32)(r[e] >> HS);
         head[e] = valid[e] && (kk == 0 || hi != prev_hi);
         stop[e] = kk == 0 || head[e] || !valid[e];
         if (head[e] && kk != 0) ssplit[i >> C] = 1;
@@ -533,13 +547,16 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
         const u32 i = 8 * tid + e;
         const u32 si = i >> C, kk = i & (S - 1);
         const Seg sg = ss[si];
-        const u32 pos = (u32)r[e];
+        u32 pos;
+        if constexpr (W32)
+            pos = sa_l[(si << C) + ((u32)r[e] & (S - 1))];
+        else
+            pos = (u32)r[e];
         const u32 rs = start_idx[e] - (si << C);  // run start inside the segment
         // an unsplit segment keeps its order (ties are in position order already); the
         // first run of a FIRST segment keeps its rank (except in round 0: RK undefined)
         if (ssplit[si]) a.SA[sg.start + kk] = pos;
         if (a.initial || rs != 0 || !(sg.len & SEG_FIRST)) a.RK[pos] = sg.start + rs;
-        if (a.idx3) a.idx3[pos] = sg.start + kk;
         if (head[e]) {
             const u32 len = nxt[e] - i;
             if (len >= 2) L.next[wpos++] = Seg{sg.start + kk, len};
@@ -552,10 +569,9 @@ __global__ void k_single(const Seg* segs, u32 count, SortArgs a) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) {
         const Seg s = segs[i];
-        if (a.initial || !(s.len & SEG_FIRST) || a.idx3) {
+        if (a.initial || !(s.len & SEG_FIRST)) {
             const u32 p = a.SA[s.start];
             a.RK[p] = s.start;
-            if (a.idx3) a.idx3[p] = s.start;
         }
     }
 }
@@ -564,11 +580,10 @@ __global__ __launch_bounds__(WG) void k_finalize_eq(const Seg* eq, SortArgs a, L
     const Seg s = eq[blockIdx.x];
     const u32 len = s.len & SEG_LEN;
     // a FIRST run keeps its group's rank after round 0
-    if (a.initial || !(s.len & SEG_FIRST) || a.idx3) {
+    if (a.initial || !(s.len & SEG_FIRST)) {
         for (u32 i = threadIdx.x; i < len; i += WG) {
             const u32 p = a.SA[s.start + i];
             a.RK[p] = s.start;
-            if (a.idx3) a.idx3[p] = s.start + i;
         }
     }
     if (threadIdx.x == 0) L.next[atomicAdd(L.next_cnt, 1u)] = Seg{s.start, len};
@@ -629,7 +644,10 @@ void launch_copy_back(const LTile* tiles, u32 ntiles, const LSeg* segs, const So
 
 template <int C>
 static void small_sort_c(const Seg* segs, u32 count, const SortArgs& a, const Lists& L, hipStream_t s) {
-    k_small_sort<C><<<cdiv(count, TILE >> C), WG, 0, s>>>(segs, count, a, L);
+    if (a.key_bits + C <= 31)
+        k_small_sort<C, u32><<<cdiv(count, TILE >> C), WG, 0, s>>>(segs, count, a, L);
+    else
+        k_small_sort<C, u64><<<cdiv(count, TILE >> C), WG, 0, s>>>(segs, count, a, L);
 }
 
 void launch_small_sort(int c, const Seg* segs, u32 count, const SortArgs& a, const Lists& L,

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -172,10 +173,7 @@ struct SortOut {
 };
 
 // Segmented prefix-doubling suffix sort of every block of the batch (k_sort.hip).
-// capture3 (linear pass): after round 0 (3-character groups, positions ascending) keep
-// SA3 = SA, gs3 = RK (group start slot by position) and idx3 (slot by position) for LZ77.
-SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, const u64* FSL, bool capture3,
-                  bool round0_only) {
+SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, const u64* FSL) {
     hipStream_t s = c->active;
     const u64 N = geo.N;
     SortOut out;
@@ -188,7 +186,6 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
     a.SA2 = c->get<u32>("SA2", N);
     a.K22 = c->get<u32>("K22", N);
     a.FSL = FSL;
-    u32* idx3 = capture3 ? c->get<u32>("idx3", N) : nullptr;
     a.blk_split = c->get<u32>("blk_split", geo.nb);
     u32* blk_done = c->get<u32>("blk_done", geo.nb);
     a.blk_done = blk_done;
@@ -232,7 +229,8 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
     for (u32 round = 0; round < 64 && ncur; ++round) {
         a.initial = round == 0 ? 1 : 0;
         a.h = round == 0 ? 0u : (h0 << (round - 1));
-        a.idx3 = round == 0 ? idx3 : nullptr;
+        // round 0: packed characters (cyclic 32 bits, linear 27); later: ranks (+1 linear)
+        a.key_bits = a.initial ? (cyclic ? 32u : 27u) : bitlen(cyclic ? geo.bs - 1 : geo.bs);
         L.next = nxt;
         KOLM_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(u32) * C_STATUS, s));
         KOLM_HIP_CHECK(hipMemsetAsync(cnt + C_CLSE, 0, sizeof(u32) * (C_N - C_CLSE), s));
@@ -320,16 +318,10 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
             launch_finalize_eq(L.eq, h[C_EQ], a, L, s);
         }
         if (cyclic) launch_update_done(blk_done, a.blk_split, geo.nb, s);
-        if (round == 0 && idx3) {
-            TScope t(c, KOLM_KT_LYNDON, "copy_SA3_GS3", N * 16);
-            KOLM_HIP_CHECK(hipMemcpyAsync(c->get<u32>("SA3", N), a.SA, 4 * N, hipMemcpyDeviceToDevice, s));
-            KOLM_HIP_CHECK(hipMemcpyAsync(c->get<u32>("GS3", N), a.RK, 4 * N, hipMemcpyDeviceToDevice, s));
-        }
         KOLM_HIP_CHECK(hipMemcpyAsync(h + C_NEXT, cnt + C_NEXT, sizeof(u32), hipMemcpyDeviceToHost, s));
         c->sync();
         ncur = h[C_NEXT];
         std::swap(cur, nxt);
-        if (round0_only) break;
     }
     return out;
 }
@@ -358,7 +350,7 @@ struct Pipeline {
         const u64 nt = gram3_tiles(geo) + 1;
         G3Bufs t{c->get<u32>("g3Ka", N), c->get<u32>("g3Kb", N), c->get<u32>("g3hist", nt * 256),
                  c->get<u32>("g3tmax", nt), c->get<u32>("g3tcarry", nt), c->get<u32>("SA3", N),
-                 c->get<u32>("idx3", N), c->get<u32>("GS3", N)};
+                 c->get<uint2>("ig3", N)};
         // 3 LSD passes (hist: 4 B, scatter: 8 B in + 8 B out) + heads/final (K 4 B x2, SA3 4 B,
         // idx3 + gs3 8 B scattered)
         TScope ts(c, KOLM_KT_LZPARSE, "k_gram3_index", N * 80);
@@ -370,7 +362,7 @@ struct Pipeline {
     u8* cyclic() {
         const u64 N = geo.N;
         u64* FSL = c->get<u64>("FSL", N);
-        SortOut cyc = sort_pass(c, geo, text, true, FSL, false, false);
+        SortOut cyc = sort_pass(c, geo, text, true, FSL);
         u8* out = c->get<u8>("bbwt", N);
         u8* prevc = c->get<u8>("prevc", N);
         {
@@ -408,8 +400,7 @@ struct Pipeline {
         z.geo = geo;
         z.text = text;
         z.SA3 = c->get<u32>("SA3", N);
-        z.idx3 = c->get<u32>("idx3", N);
-        z.gs3 = c->get<u32>("GS3", N);
+        z.ig3 = c->get<uint2>("ig3", N);
         z.tok_pos = c->get<u32>("tok_pos", N);
         z.tok_len = c->get<u32>("tok_len", N);
         z.tok_dist = c->get<u32>("tok_dist", N);
@@ -478,7 +469,11 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
     // Two streams: main runs the 3-gram linear sort and then the LZ77 parse; aux runs the
     // Lyndon factorisation (beside the linear sort), then the cyclic sort, BBWT, MTF and
     // the size kernels (beside LZ77), joins LZ77 and finishes MDL + emission.
-    hipStream_t ms = c->stream, s = c->aux;
+    // KOLM_SERIAL=1 runs everything on one stream (profiling); KOLM_OVERLAP selects when the
+    // 3-gram index + LZ77 start: 0 (default) at once, 1 after the Lyndon factorisation.
+    static const bool serial = getenv("KOLM_SERIAL") && atoi(getenv("KOLM_SERIAL")) != 0;
+    static const int overlap = getenv("KOLM_OVERLAP") ? atoi(getenv("KOLM_OVERLAP")) : 0;
+    hipStream_t ms = c->stream, s = serial ? c->stream : c->aux;
     Pipeline P{c, geo, d_text};
     hipEvent_t* ev = c->ev;
     hipEvent_t* ej = c->evj;
@@ -491,6 +486,10 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
     KOLM_HIP_CHECK(hipStreamWaitEvent(s, ev[0], 0));
     c->active = s;
     P.lyndon();
+    if (overlap == 1) {
+        KOLM_HIP_CHECK(hipEventRecord(ej[3], s));
+        KOLM_HIP_CHECK(hipStreamWaitEvent(ms, ej[3], 0));
+    }
     c->active = ms;
     P.linear3();
     KOLM_HIP_CHECK(hipEventRecord(ej[0], ms));
@@ -970,7 +969,7 @@ int kolm_lz77_encode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size
         geom_init(geo, n, (u32)n);
         u8* d = upload(c, in, n);
         Pipeline P{c, geo, d};
-        sort_pass(c, geo, d, false, nullptr, true, true);
+        P.linear3();
         LzArgs z = P.lz_args();
         P.lz(z);
         u32 sz = 0;

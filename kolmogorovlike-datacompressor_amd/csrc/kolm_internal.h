@@ -83,8 +83,8 @@ struct SortArgs {
     int cyclic;
     int initial;       // round 0: keys are packed characters
     u32 h;             // doubling offset of this round (round >= 1)
-    u32* idx3;         // linear round 0 only: idx3[p] = SA slot of p (3-gram order), else null
     const u32* KP;     // [N] this round's key by position (k_keypos), or null: keys gathered directly
+    u32 key_bits;      // keys of this round are < 2^key_bits (small sort packs key|index in 32 bits)
 };
 
 // Append-only lists written by the classify / MSD / small-sort kernels.
@@ -144,8 +144,7 @@ struct G3Bufs {
     u32* tmax;    // [gram3_tiles]
     u32* tcarry;  // [gram3_tiles]
     u32* SA3;     // [N] out: positions grouped by 3-gram, ascending inside a group
-    u32* idx3;    // [N] out: slot of each position
-    u32* gs3;     // [N] out: first slot of each position's group
+    uint2* ig3;   // [N] out: (slot, first slot of the group) of each position
 };
 u32 gram3_tiles(const Geom& geo);
 void launch_gram3(const Geom& geo, const u8* text, const G3Bufs& t, hipStream_t s);
@@ -186,8 +185,7 @@ struct LzArgs {
     const u8* text;
     // 3-gram candidate structure captured after round 0 of the linear suffix sort:
     const u32* SA3;    // [N] positions sorted by (3-gram key, position)
-    const u32* idx3;   // [N] idx3[p] = slot of p in SA3
-    const u32* gs3;    // [N] gs3[p] = first slot of p's 3-gram group in SA3
+    const uint2* ig3;  // [N] (idx3[p] = slot of p in SA3, gs3[p] = first slot of p's group)
     // speculative tokens of chunk c live in slots [chunk start, chunk start + ntok[c])
     u32* tok_pos;      // [N] token start position
     u32* tok_len;      // [N] match length (0 = literal)
