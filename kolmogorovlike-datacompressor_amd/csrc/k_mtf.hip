@@ -38,8 +38,7 @@ __global__ __launch_bounds__(256) void k_mtf_summary(ChunkGeom cg, const u8* in,
     if (cg.range(c, lo, hi)) {
         u32 seen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         u8* out = summary + (u64)c * 256;
-        for (u32 i = hi; i > lo; --i) {
-            const u32 b = in[i - 1];
+        auto visit = [&](u32 b) {
             const u32 w = b >> 5, bit = 1u << (b & 31);
             u32 sw = 0;
 #pragma unroll
@@ -50,6 +49,19 @@ __global__ __launch_bounds__(256) void k_mtf_summary(ChunkGeom cg, const u8* in,
                     if (k == (int)w) seen[k] |= bit;
                 out[cnt++] = (u8)b;
             }
+        };
+        if (((lo | hi) & 15) == 0) {
+            // 16-byte loads (threads are 1 KiB apart: byte loads thrash L1)
+            for (u32 i = hi; i > lo; i -= 16) {
+                const uint4 v = *reinterpret_cast<const uint4*>(in + i - 16);
+                const u32 wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int q = 3; q >= 0; --q)
+#pragma unroll
+                    for (int j = 3; j >= 0; --j) visit((wv[q] >> (8 * j)) & 0xFF);
+            }
+        } else {
+            for (u32 i = hi; i > lo; --i) visit(in[i - 1]);
         }
     }
     scnt[c] = cnt;
@@ -126,8 +138,7 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
     if (!cg.range(c, lo, hi)) return;
     const u32* s = reinterpret_cast<const u32*>(states + (u64)c * 256);
     for (int w = 0; w < 64; ++w) tab[w * RT + t] = s[w];
-    for (u32 i = lo; i < hi; ++i) {
-        const u32 b = in[i];
+    auto step = [&](u32 b) -> u32 {
         const u32 bb = b * 0x01010101u;
         u32 w = 0, x, z;
         for (;;) {
@@ -138,7 +149,6 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
             ++w;
         }
         const u32 j = (__ffs(z) - 1) >> 3;  // byte index inside word w
-        out[i] = (u8)(4 * w + j);
         // move to front: shift entries [0, 4w+j) up by one, entry 0 = b
         u32 carry = b;
         for (u32 v = 0; v < w; ++v) {
@@ -149,6 +159,25 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
         const u32 lowmask = j ? ((1u << (8 * j)) - 1) : 0u;
         const u32 highmask = j == 3 ? 0u : ~((1u << (8 * (j + 1))) - 1);
         tab[w * RT + t] = (x & highmask) | ((x & lowmask) << 8) | carry;
+        return 4 * w + j;
+    };
+    if (((lo | hi) & 15) == 0) {
+        // 16 bytes in / 16 bytes out per global access (threads are 1 KiB apart)
+        for (u32 i = lo; i < hi; i += 16) {
+            const uint4 v = *reinterpret_cast<const uint4*>(in + i);
+            const u32 wv[4] = {v.x, v.y, v.z, v.w};
+            u32 ov[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                u32 o = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o |= step((wv[q] >> (8 * j)) & 0xFF) << (8 * j);
+                ov[q] = o;
+            }
+            *reinterpret_cast<uint4*>(out + i) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+        }
+    } else {
+        for (u32 i = lo; i < hi; ++i) out[i] = (u8)step(in[i]);
     }
 }
 
