@@ -1,5 +1,10 @@
-// 3-gram candidate index for LZ77 (gfx950): every block's positions grouped by their
-// 3-byte prefix, positions ascending inside a group.
+// Per-block stable LSD radix passes (gfx950) and their two users:
+//   * the 3-gram candidate index for LZ77 (launch_gram3);
+//   * round 0 of the cyclic suffix sort (launch_round0): positions grouped by the first
+//     4 characters of their rotation, ranks + next-round segments (k_sort.hip).
+//
+// 3-gram index: every block's positions grouped by their 3-byte prefix, positions
+// ascending inside a group.
 //
 // The reference's LZ77 (PY:1711-1763) finds, for each position, the longest earlier
 // match inside the 4096-byte window by walking previous occurrences of the current
@@ -52,7 +57,10 @@ __device__ inline u32 digit(u32 key) {
     return (key >> (8 * P)) & 255u;
 }
 
-template <int P>
+// where a pass reads its (key, position) pairs
+enum Src { SRC_TEXT3 = 0, SRC_KP = 1, SRC_PAIR = 2 };
+
+template <int P, int SRC>
 __global__ __launch_bounds__(WG) void k_g3_hist(G3Geom g, const u8* text, const u32* K, u32* hist) {
     __shared__ u32 h[WG / 64][256];
     const u32 tid = threadIdx.x, w = tid >> 6;
@@ -63,7 +71,7 @@ __global__ __launch_bounds__(WG) void k_g3_hist(G3Geom g, const u8* text, const 
     if (g.range(blockIdx.x, lo, hi, b)) {
 #pragma unroll 4
         for (u32 i = lo + tid; i < hi; i += WG) {
-            const u32 d = P == 0 ? (u32)text[i + 2] : digit<P>(K[i]);
+            const u32 d = SRC == SRC_TEXT3 ? (u32)text[i + 2 - P] : digit<P>(K[i]);
             atomicAdd(&h[w][d], 1u);
         }
     }
@@ -113,7 +121,7 @@ __global__ __launch_bounds__(WG) void k_g3_scan(G3Geom g, u32* hist) {
 // Stable scatter of one tile by digit P: element order e = j*WG + tid; each wave ranks
 // its 64 elements per digit with ballots, per-wave counts are combined in (j, wave)
 // order.  P == 0 reads positions in order and builds the keys from the text.
-template <int P>
+template <int P, int SRC>
 __global__ __launch_bounds__(WG) void k_g3_scatter(G3Geom g, const u8* text, const u32* Kin, const u32* Pin,
                                                    u32* Kout, u32* Pout, const u32* hist) {
     __shared__ u32 wcnt[WG / 64][256];
@@ -131,8 +139,11 @@ __global__ __launch_bounds__(WG) void k_g3_scatter(G3Geom g, const u8* text, con
         const bool valid = i < hi;
         u32 key = 0, pos = 0, dg = 0;
         if (valid) {
-            if (P == 0) {
+            if (SRC == SRC_TEXT3) {
                 key = key24(text, i);
+                pos = i;
+            } else if (SRC == SRC_KP) {
+                key = Kin[i];
                 pos = i;
             } else {
                 key = Kin[i];
@@ -269,7 +280,197 @@ __global__ __launch_bounds__(WG) void k_g3_final(G3Geom g, const u32* K, u32* SA
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Round 0 of the cyclic suffix sort: after 4 LSD passes over the 4-character rotation
+// keys (K sorted, SA = positions), slot g starts a group iff g is the block's first slot
+// or K[g] != K[g-1].  Every position gets RK = its group's first slot (PY's (fi, i) tie
+// rule is position order, kept by the stable passes); groups of >= 2 go to the next
+// round; a block with more than one group has split.
+// ---------------------------------------------------------------------------------
+constexpr u32 BIG = 0xFFFFFFFFu;
+
+__device__ inline bool r0_head(const u32* K, u32 g, u32 base) { return g == base || K[g] != K[g - 1]; }
+
+__device__ inline u32 wave_min(u32 v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, (u32)__shfl_xor(v, o));
+    return v;
+}
+
+__global__ __launch_bounds__(WG) void k_r0_tile_heads(G3Geom g, const u32* K, u32* tmax, u32* tmin) {
+    __shared__ u32 s1[WG / 64], s2[WG / 64];
+    u32 lo, hi, b;
+    u32 mx = 0, mn = BIG;
+    if (g.range(blockIdx.x, lo, hi, b)) {
+        const u32 base = g.geo.base(b);
+        for (u32 i = lo + threadIdx.x; i < hi; i += WG)
+            if (r0_head(K, i, base)) {
+                mx = max(mx, i);
+                mn = min(mn, i);
+            }
+    }
+    mx = wave_max(mx);
+    mn = wave_min(mn);
+    if ((threadIdx.x & 63) == 0) {
+        s1[threadIdx.x >> 6] = mx;
+        s2[threadIdx.x >> 6] = mn;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        tmax[blockIdx.x] = max(max(s1[0], s1[1]), max(s1[2], s1[3]));
+        tmin[blockIdx.x] = min(min(s2[0], s2[1]), min(s2[2], s2[3]));
+    }
+}
+
+// per block: exclusive suffix min over its tiles (one workgroup per block)
+__global__ __launch_bounds__(WG) void k_r0_tiles_rscan(const u32* in, u32* out, u32 tpb) {
+    __shared__ u32 sh[WG / 64];
+    __shared__ u32 edge;
+    const u32 b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    u32 carry = BIG;
+    const u32 nch = (tpb + WG - 1) / WG;
+    for (u32 cc = 0; cc < nch; ++cc) {
+        const u32 k = (nch - 1 - cc) * WG + threadIdx.x;
+        const u32 v = k < tpb ? in[(u64)b * tpb + k] : BIG;
+        u32 incl = v;
+#pragma unroll
+        for (u32 o = 1; o < 64; o <<= 1) {
+            const u32 x = __shfl_down(incl, o);
+            if (lane + o < 64) incl = min(incl, x);
+        }
+        u32 ex = __shfl_down(incl, 1);
+        if (lane == 63) ex = BIG;
+        if (lane == 0) sh[w] = incl;
+        __syncthreads();
+        u32 wc = carry;
+        for (u32 i = w + 1; i < WG / 64; ++i) wc = min(wc, sh[i]);
+        if (k < tpb) out[(u64)b * tpb + k] = min(wc, ex);
+        if (threadIdx.x == 0) edge = min(wc, incl);
+        __syncthreads();
+        carry = edge;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_r0_final(G3Geom g, const u32* K, const u32* SA, const u32* cmax,
+                                                 const u32* cmin, u32* RK, Seg* next, u32* next_cnt,
+                                                 u32* blk_split) {
+    __shared__ u32 sh[WG / 64], sh2[WG / 64], sh3[WG / 64];
+    __shared__ u32 wbase, anysplit;
+    u32 lo, hi, b;
+    if (!g.range(blockIdx.x, lo, hi, b)) return;
+    const u32 base = g.geo.base(b), bend = g.geo.end(b);
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) anysplit = 0;
+    const u32 i0 = lo + tid * G3PT;
+    bool hd[G3PT];
+    u32 lmax = 0, lmin = BIG;
+#pragma unroll
+    for (u32 e = 0; e < G3PT; ++e) {
+        const u32 i = i0 + e;
+        hd[e] = i < hi && r0_head(K, i, base);
+        if (hd[e]) {
+            lmax = max(lmax, i);
+            lmin = min(lmin, i);
+        }
+    }
+    // forward exclusive max (group start entering the thread), reverse exclusive min
+    // (first head after the thread)
+    u32 fi = lmax, ri = lmin;
+#pragma unroll
+    for (u32 o = 1; o < 64; o <<= 1) {
+        const u32 x = __shfl_up(fi, o);
+        if (lane >= o) fi = max(fi, x);
+        const u32 y = __shfl_down(ri, o);
+        if (lane + o < 64) ri = min(ri, y);
+    }
+    u32 fex = __shfl_up(fi, 1), rex = __shfl_down(ri, 1);
+    if (lane == 0) fex = 0;
+    if (lane == 63) rex = BIG;
+    if (lane == 63) sh[w] = fi;
+    if (lane == 0) sh2[w] = ri;
+    __syncthreads();
+    u32 run = max(cmax[blockIdx.x], fex);
+    for (u32 q = 0; q < w; ++q) run = max(run, sh[q]);
+    u32 nh = min(cmin[blockIdx.x], rex);
+    for (u32 q = w + 1; q < WG / 64; ++q) nh = min(nh, sh2[q]);
+    if (nh == BIG) nh = bend;
+    // ranks
+    bool split = false;
+#pragma unroll
+    for (u32 e = 0; e < G3PT; ++e) {
+        const u32 i = i0 + e;
+        if (i < hi) {
+            if (hd[e]) {
+                run = i;
+                split |= i != base;
+            }
+            RK[SA[i]] = run;
+        }
+    }
+    // group lengths (backwards) and next-round segments, one global atomic per workgroup
+    u32 len[G3PT];
+    u32 nseg = 0;
+#pragma unroll
+    for (int e = G3PT - 1; e >= 0; --e) {
+        const u32 i = i0 + e;
+        len[e] = 0;
+        if (hd[e]) {
+            len[e] = nh - i;
+            nh = i;
+            nseg += len[e] >= 2;
+        }
+    }
+    u32 incl = nseg;
+#pragma unroll
+    for (u32 o = 1; o < 64; o <<= 1) {
+        const u32 x = __shfl_up(incl, o);
+        if (lane >= o) incl += x;
+    }
+    if (lane == 63) sh3[w] = incl;
+    if (split) anysplit = 1;
+    __syncthreads();
+    u32 off = incl - nseg;
+    for (u32 q = 0; q < w; ++q) off += sh3[q];
+    if (tid == WG - 1) {
+        const u32 tot = off + nseg;
+        wbase = tot ? atomicAdd(next_cnt, tot) : 0u;
+        if (anysplit) blk_split[b] = 1;
+    }
+    __syncthreads();
+    off += wbase;
+#pragma unroll
+    for (u32 e = 0; e < G3PT; ++e)
+        if (len[e] >= 2) next[off++] = Seg{i0 + e, len[e]};
+}
+
 }  // namespace
+
+u32 lsd_tiles(const Geom& geo) { return (geo.bs + G3T - 1) / G3T * geo.nb; }
+
+// Round 0 of the cyclic sort.  KP = 4-character keys by position (k_keypos).
+// Passes: (KP, p) -> (K2, SA) -> (K22, SA2) -> (KP, RK) -> (K2, SA); then ranks/segments.
+void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s) {
+    if (!geo.N) return;
+    G3Geom g{geo, (geo.bs + G3T - 1) / G3T, true};
+    const u32 nt = g.tpb * geo.nb;
+    k_g3_hist<0, SRC_KP><<<nt, WG, 0, s>>>(g, nullptr, t.KP, t.hist);
+    k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
+    k_g3_scatter<0, SRC_KP><<<nt, WG, 0, s>>>(g, nullptr, t.KP, nullptr, t.K2, t.SA, t.hist);
+    k_g3_hist<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, t.K2, t.hist);
+    k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
+    k_g3_scatter<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, t.K2, t.SA, t.K22, t.SA2, t.hist);
+    k_g3_hist<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, t.K22, t.hist);
+    k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
+    k_g3_scatter<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, t.K22, t.SA2, t.KP, t.RK, t.hist);
+    k_g3_hist<3, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, t.KP, t.hist);
+    k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
+    k_g3_scatter<3, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, t.KP, t.RK, t.K2, t.SA, t.hist);
+    k_r0_tile_heads<<<nt, WG, 0, s>>>(g, t.K2, t.tmax, t.tmin);
+    k_g3_tiles_scan<<<geo.nb, WG, 0, s>>>(t.tmax, t.cmax, g.tpb);
+    k_r0_tiles_rscan<<<geo.nb, WG, 0, s>>>(t.tmin, t.cmin, g.tpb);
+    k_r0_final<<<nt, WG, 0, s>>>(g, t.K2, t.SA, t.cmax, t.cmin, t.RK, next, next_cnt, blk_split);
+}
 
 void launch_gram3(const Geom& geo, const u8* text, const G3Bufs& t, hipStream_t s) {
     if (!geo.N) return;
@@ -278,21 +479,20 @@ void launch_gram3(const Geom& geo, const u8* text, const G3Bufs& t, hipStream_t 
     // pass c2: text -> (Ka, Pa); c1: -> (Kb, Pb); c0: -> (Ka, SA3); Pa/Pb live in ig3 (free until final)
     u32* Pa = reinterpret_cast<u32*>(t.ig3);
     u32* Pb = Pa + geo.N;
-    k_g3_hist<0><<<nt, WG, 0, s>>>(g, text, nullptr, t.hist);
+    k_g3_hist<0, SRC_TEXT3><<<nt, WG, 0, s>>>(g, text, nullptr, t.hist);
     k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
-    k_g3_scatter<0><<<nt, WG, 0, s>>>(g, text, nullptr, nullptr, t.Ka, Pa, t.hist);
-    k_g3_hist<1><<<nt, WG, 0, s>>>(g, text, t.Ka, t.hist);
+    k_g3_scatter<0, SRC_TEXT3><<<nt, WG, 0, s>>>(g, text, nullptr, nullptr, t.Ka, Pa, t.hist);
+    k_g3_hist<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Ka, t.hist);
     k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
-    k_g3_scatter<1><<<nt, WG, 0, s>>>(g, text, t.Ka, Pa, t.Kb, Pb, t.hist);
-    k_g3_hist<2><<<nt, WG, 0, s>>>(g, text, t.Kb, t.hist);
+    k_g3_scatter<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Ka, Pa, t.Kb, Pb, t.hist);
+    k_g3_hist<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Kb, t.hist);
     k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
-    k_g3_scatter<2><<<nt, WG, 0, s>>>(g, text, t.Kb, Pb, t.Ka, t.SA3, t.hist);
+    k_g3_scatter<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Kb, Pb, t.Ka, t.SA3, t.hist);
     G3Geom gs{geo, g.tpb, true};
     k_g3_tile_heads<<<nt, WG, 0, s>>>(gs, t.Ka, t.tmax);
     k_g3_tiles_scan<<<geo.nb, WG, 0, s>>>(t.tmax, t.tcarry, g.tpb);
     k_g3_final<<<nt, WG, 0, s>>>(gs, t.Ka, t.SA3, t.tcarry, t.ig3);
 }
 
-u32 gram3_tiles(const Geom& geo) { return (geo.bs + G3T - 1) / G3T * geo.nb; }
 
 }  // namespace kolm

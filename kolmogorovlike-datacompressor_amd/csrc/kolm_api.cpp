@@ -217,8 +217,10 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
                   cnt + C_L1ELEM};
     u32* hist = c->get<u32>("hist", ltile_cap * 256);
 
-    launch_iota(a.SA, N, s);
-    launch_block_segs(segA, geo, s);
+    if (!cyclic) {
+        launch_iota(a.SA, N, s);
+        launch_block_segs(segA, geo, s);
+    }
     KOLM_HIP_CHECK(hipMemsetAsync(blk_done, 0, sizeof(u32) * geo.nb, s));
     Seg* cur = segA;
     Seg* nxt = segB;
@@ -235,6 +237,31 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
         KOLM_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(u32) * C_STATUS, s));
         KOLM_HIP_CHECK(hipMemsetAsync(cnt + C_CLSE, 0, sizeof(u32) * (C_N - C_CLSE), s));
         KOLM_HIP_CHECK(hipMemsetAsync(a.blk_split, 0, sizeof(u32) * geo.nb, s));
+        if (round == 0 && cyclic) {
+            // round 0: 4 stable LSD passes over the 4-character keys, no host round trips
+            u32* KP = c->get<u32>("KP", N);
+            {
+                TScope t(c, KOLM_KT_KEYGEN, "k_keypos", N * 16);
+                a.KP = nullptr;
+                launch_keypos(a, KP, s);
+            }
+            const u64 nt = lsd_tiles(geo) + 1;
+            R0Bufs r{KP, a.K2, a.SA, a.K22, a.SA2, a.RK, c->get<u32>("r0hist", nt * 256), c->get<u32>("r0tmax", nt),
+                     c->get<u32>("r0tmin", nt), c->get<u32>("r0cmax", nt), c->get<u32>("r0cmin", nt)};
+            {
+                // 4 passes (hist 4 B + scatter 16 B per element) + heads 4 B + ranks (K 4, SA 4, RK 4)
+                TScope t(c, KOLM_KT_MSD, "k_round0_lsd", N * 92);
+                launch_round0(geo, r, nxt, L.next_cnt, a.blk_split, s);
+            }
+            out.active += N;
+            out.rounds = 1;
+            launch_update_done(blk_done, a.blk_split, geo.nb, s);
+            KOLM_HIP_CHECK(hipMemcpyAsync(h + C_NEXT, cnt + C_NEXT, sizeof(u32), hipMemcpyDeviceToHost, s));
+            c->sync();
+            ncur = h[C_NEXT];
+            std::swap(cur, nxt);
+            continue;
+        }
         {
             TScope t(c, KOLM_KT_CLASSIFY, "k_classify", (u64)ncur * 16);
             launch_classify(cur, ncur, a, L, lv[0], s);
@@ -347,7 +374,7 @@ struct Pipeline {
     // linear suffix order at 3 characters only: LZ77 candidate groups (SA3, idx3, GS3)
     void linear3() {
         const u64 N = geo.N;
-        const u64 nt = gram3_tiles(geo) + 1;
+        const u64 nt = lsd_tiles(geo) + 1;
         G3Bufs t{c->get<u32>("g3Ka", N), c->get<u32>("g3Kb", N), c->get<u32>("g3hist", nt * 256),
                  c->get<u32>("g3tmax", nt), c->get<u32>("g3tcarry", nt), c->get<u32>("SA3", N),
                  c->get<uint2>("ig3", N)};

@@ -136,7 +136,7 @@ void launch_lyndon_isa(const Geom& geo, const u32* RK, u8* flag, u32* tile_tmp, 
 void launch_prevc(const Geom& geo, const u8* text, const u64* FSL, u8* prevc, hipStream_t s);
 void launch_bbwt_gather(const Geom& geo, const u32* SA, const u8* prevc, u8* out, hipStream_t s);
 
-// ---- k_gram3.hip: 3-gram candidate index for LZ77 ----
+// ---- k_lsd.hip: per-block LSD radix passes: 3-gram index for LZ77, cyclic round 0 ----
 struct G3Bufs {
     u32* Ka;      // [N] key ping
     u32* Kb;      // [N] key pong
@@ -146,8 +146,19 @@ struct G3Bufs {
     u32* SA3;     // [N] out: positions grouped by 3-gram, ascending inside a group
     uint2* ig3;   // [N] out: (slot, first slot of the group) of each position
 };
-u32 gram3_tiles(const Geom& geo);
+u32 lsd_tiles(const Geom& geo);
 void launch_gram3(const Geom& geo, const u8* text, const G3Bufs& t, hipStream_t s);
+struct R0Bufs {
+    u32* KP;   // [N] in: 4-character keys by position; scratch afterwards
+    u32* K2;   // [N] out: sorted keys (scratch)
+    u32* SA;   // [N] out: positions in 4-character order (ties by position)
+    u32* K22;  // [N] scratch
+    u32* SA2;  // [N] scratch
+    u32* RK;   // [N] out: group start slot of every position
+    u32* hist;                    // [lsd_tiles * 256]
+    u32 *tmax, *tmin, *cmax, *cmin;  // [lsd_tiles]
+};
+void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s);
 
 // ---- k_mtf.hip ----
 void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summary_cnt, u8* states,
