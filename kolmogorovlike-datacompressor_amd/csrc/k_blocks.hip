@@ -432,8 +432,15 @@ __global__ void k_prevc(Geom geo, const u8* text, const u64* FSL, u8* prevc) {
     }
 }
 
-__global__ void k_bbwt_gather(Geom geo, const u32* SA, const u8* prevc, u8* out) {
-    for (u32 g = blockIdx.x * blockDim.x + threadIdx.x; g < geo.N; g += gridDim.x * blockDim.x) out[g] = prevc[SA[g]];
+// 4096 slots per workgroup, XCD-remapped so a block's slots (and its 1 MiB of prevc)
+// stay on one XCD's L2
+__global__ __launch_bounds__(256) void k_bbwt_gather(Geom geo, const u32* SA, const u8* prevc, u8* out) {
+    const u32 g0 = xcd_tile() * 4096u;
+#pragma unroll
+    for (u32 j = 0; j < 16; ++j) {
+        const u32 g = g0 + j * 256 + threadIdx.x;
+        if (g < geo.N) out[g] = prevc[SA[g]];
+    }
 }
 
 }  // namespace
@@ -478,8 +485,7 @@ void launch_prevc(const Geom& geo, const u8* text, const u64* FSL, u8* prevc, hi
 
 void launch_bbwt_gather(const Geom& geo, const u32* SA, const u8* prevc, u8* out, hipStream_t s) {
     if (!geo.N) return;
-    const u32 grid = (u32)std::min<u64>((geo.N + 255) / 256, 65535);
-    k_bbwt_gather<<<grid, 256, 0, s>>>(geo, SA, prevc, out);
+    k_bbwt_gather<<<(u32)((geo.N + 4095) / 4096), 256, 0, s>>>(geo, SA, prevc, out);
 }
 
 }  // namespace kolm

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(WG) void k_g3_hist(G3Geom g, const u8* text, const 
     for (int i = 0; i < WG / 64; ++i) h[i][tid] = 0;
     __syncthreads();
     u32 lo, hi, b;
-    if (g.range(blockIdx.x, lo, hi, b)) {
+    if (g.range(xcd_tile(), lo, hi, b)) {
 #pragma unroll 4
         for (u32 i = lo + tid; i < hi; i += WG) {
             const u32 d = SRC == SRC_TEXT3 ? (u32)text[i + 2 - P] : digit<P>(K[i]);
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(WG) void k_g3_hist(G3Geom g, const u8* text, const 
         }
     }
     __syncthreads();
-    hist[(u64)blockIdx.x * 256 + tid] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+    hist[(u64)xcd_tile() * 256 + tid] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
 }
 
 // hist[t][d] -> absolute destination of the first element of digit d in tile t.
@@ -128,8 +128,8 @@ __global__ __launch_bounds__(WG) void k_g3_scatter(G3Geom g, const u8* text, con
     __shared__ u32 running[256];
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     u32 lo, hi, b;
-    if (!g.range(blockIdx.x, lo, hi, b)) return;
-    running[tid] = hist[(u64)blockIdx.x * 256 + tid];
+    if (!g.range(xcd_tile(), lo, hi, b)) return;
+    running[tid] = hist[(u64)xcd_tile() * 256 + tid];
 #pragma unroll
     for (int i = 0; i < WG / 64; ++i) wcnt[i][tid] = 0;
     __syncthreads();
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(WG) void k_g3_tile_heads(G3Geom g, const u32* K, u3
     __shared__ u32 sh[WG / 64];
     u32 lo, hi, b;
     u32 mx = 0;
-    if (g.range(blockIdx.x, lo, hi, b)) {
+    if (g.range(xcd_tile(), lo, hi, b)) {
         const u32 base = g.geo.base(b), fe = g.fend(b);
         for (u32 i = lo + threadIdx.x; i < hi; i += WG)
             if (g3_head(g, K, i, base, fe)) mx = max(mx, i);
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(WG) void k_g3_tile_heads(G3Geom g, const u32* K, u3
     mx = wave_max(mx);
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = mx;
     __syncthreads();
-    if (threadIdx.x == 0) tmax[blockIdx.x] = max(max(sh[0], sh[1]), max(sh[2], sh[3]));
+    if (threadIdx.x == 0) tmax[xcd_tile()] = max(max(sh[0], sh[1]), max(sh[2], sh[3]));
 }
 
 // per block: exclusive max over its tiles (one workgroup per block)
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(WG) void k_r0_tile_heads(G3Geom g, const u32* K, u3
     __shared__ u32 s1[WG / 64], s2[WG / 64];
     u32 lo, hi, b;
     u32 mx = 0, mn = BIG;
-    if (g.range(blockIdx.x, lo, hi, b)) {
+    if (g.range(xcd_tile(), lo, hi, b)) {
         const u32 base = g.geo.base(b);
         for (u32 i = lo + threadIdx.x; i < hi; i += WG)
             if (r0_head(K, i, base)) {
@@ -317,8 +317,8 @@ __global__ __launch_bounds__(WG) void k_r0_tile_heads(G3Geom g, const u32* K, u3
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        tmax[blockIdx.x] = max(max(s1[0], s1[1]), max(s1[2], s1[3]));
-        tmin[blockIdx.x] = min(min(s2[0], s2[1]), min(s2[2], s2[3]));
+        tmax[xcd_tile()] = max(max(s1[0], s1[1]), max(s1[2], s1[3]));
+        tmin[xcd_tile()] = min(min(s2[0], s2[1]), min(s2[2], s2[3]));
     }
 }
 

@@ -68,6 +68,16 @@ struct Geom {
 
 void geom_init(Geom& g, u64 N, u32 bs);
 
+// XCD-aware workgroup -> tile remap (speed only, never correctness): workgroups are dealt
+// round-robin over the 8 XCDs, so give each XCD a contiguous range of tiles — tiles of
+// one block then share an L2 (random accesses inside a block's arrays stay L2-local).
+// Bijective for any grid size.
+__device__ inline u32 xcd_tile() {
+    const u32 w = blockIdx.x, G = gridDim.x;
+    const u32 x = w & 7, j = w >> 3, q = G >> 3, r = G & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
+}
+
 // Everything the suffix-sorting kernels touch for one pass (linear or cyclic).
 struct SortArgs {
     Geom geo;
