@@ -9,7 +9,7 @@ One step = one full compress of the rank's batch from HBM to a device payload ar
 Weak scaling: per-GPU work is fixed; value = all ranks' input bytes / max-over-ranks time.
 
 Also reported:
-  roofline      the dominant kernel family (largest summed device time in the timed
+  roofline      the dominant single kernel (largest summed device time in the timed
                 steps, HIP events on the library's stream): algorithmic bytes per launch
                 (DESIGN.md §5) / average launch time, against 8 TB/s HBM peak;
                 traffic = PMC-measured HBM bytes per launch from profiles/pmc_summary.json

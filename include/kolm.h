@@ -54,15 +54,15 @@ typedef struct kolm_ctx kolm_ctx;
 
 /* Kernel families timed with HIP events when timing is enabled (kolm_ctx_set_timing). */
 #define KOLM_KT_CLASSIFY 0   /* k_classify */
-#define KOLM_KT_KEYGEN 1     /* k_keygen_small, k_keygen_large */
+#define KOLM_KT_KEYGEN 1     /* k_keypos, k_keygen_small, k_keygen_large */
 #define KOLM_KT_MSD 2        /* k_msd_hist, k_msd_scan, k_msd_scatter, k_copy_back */
 #define KOLM_KT_SMALLSORT 3  /* k_small_sort<1..11>, k_single, k_finalize_eq */
-#define KOLM_KT_LZMATCH 4    /* k_lz_match */
-#define KOLM_KT_LZPARSE 5    /* k_lz_parse */
+#define KOLM_KT_LSD 4        /* per-block LSD radix passes: k_g3_* (3-gram index), k_r0_* (round 0) */
+#define KOLM_KT_LZPARSE 5    /* k_lz_spec, k_lz_stitch */
 #define KOLM_KT_MTF 6        /* k_mtf_summary, k_mtf_compose, k_mtf_replay */
 #define KOLM_KT_SIZES 7      /* k_sizes, k_mdl, k_offsets */
 #define KOLM_KT_EMIT 8       /* emission kernels */
-#define KOLM_KT_LYNDON 9     /* Lyndon scans + BBWT gather + prev3 */
+#define KOLM_KT_LYNDON 9     /* k_duval_*, Lyndon scans, k_prevc, k_bbwt_gather */
 #define KOLM_NKT 10
 
 typedef struct kolm_ktime {

@@ -458,7 +458,7 @@ void launch_lyndon_isa(const Geom& geo, const u32* RK, u8* flag, u32* tile_tmp, 
 
 // Lyndon factorisation of every block (parallel Duval + merge) -> per-position FSL.
 void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u32* fstart, u32* nfac, u32* stack,
-                   u32* tile_tmp, u32* tile_tmp2, hipStream_t s) {
+                   u32* tile_tmp, u32* tile_tmp2, hipStream_t s, KTimer* kt) {
     if (!geo.N) return;
     TileGeom tg{geo, (geo.bs + TILE - 1) / TILE};
     const u32 nt = tg.tpb * geo.nb;
@@ -468,13 +468,26 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u32* fst
     u32* D = tile_tmp2 + nt;  // [nt]
     const u32 cpb = (geo.bs + DUVAL_SPAN - 1) / DUVAL_SPAN;
     const u32 nch = cpb * geo.nb;
+    const u64 N = geo.N;
     KOLM_HIP_CHECK(hipMemsetAsync(flag, 0, geo.N, s));
-    k_duval_span<<<nch, 256, 0, s>>>(geo, cpb, text, fstart, nfac);
-    k_duval_merge<<<geo.nb, 64, 0, s>>>(geo, cpb, text, fstart, nfac, stack, flag);
-    k_tile_starts<<<nt, WG, 0, s>>>(tg, flag, A, C2);
-    k_tiles_scan<false, true><<<geo.nb, WG, 0, s>>>(A, B, tg.tpb, 0u);
-    k_tiles_scan<true, false><<<geo.nb, WG, 0, s>>>(C2, D, tg.tpb, BIG);
-    k_fsfl<<<nt, WG, 0, s>>>(tg, flag, B, D, FSL);
+    {
+        KScope k(kt, KT_LYNDON, "k_duval_span", N);  // text once (+ 4 B per factor start)
+        k_duval_span<<<nch, 256, 0, s>>>(geo, cpb, text, fstart, nfac);
+    }
+    {
+        KScope k(kt, KT_LYNDON, "k_duval_merge", (u64)nch * 8);
+        k_duval_merge<<<geo.nb, 64, 0, s>>>(geo, cpb, text, fstart, nfac, stack, flag);
+    }
+    {
+        KScope k(kt, KT_LYNDON, "k_tile_starts", N);
+        k_tile_starts<<<nt, WG, 0, s>>>(tg, flag, A, C2);
+        k_tiles_scan<false, true><<<geo.nb, WG, 0, s>>>(A, B, tg.tpb, 0u);
+        k_tiles_scan<true, false><<<geo.nb, WG, 0, s>>>(C2, D, tg.tpb, BIG);
+    }
+    {
+        KScope k(kt, KT_LYNDON, "k_fsfl", 9 * N);  // flag 1 + FSL 8
+        k_fsfl<<<nt, WG, 0, s>>>(tg, flag, B, D, FSL);
+    }
 }
 
 void launch_prevc(const Geom& geo, const u8* text, const u64* FSL, u8* prevc, hipStream_t s) {

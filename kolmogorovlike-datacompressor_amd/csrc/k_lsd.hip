@@ -450,49 +450,116 @@ u32 lsd_tiles(const Geom& geo) { return (geo.bs + G3T - 1) / G3T * geo.nb; }
 
 // Round 0 of the cyclic sort.  KP = 4-character keys by position (k_keypos).
 // Passes: (KP, p) -> (K2, SA) -> (K22, SA2) -> (KP, RK) -> (K2, SA); then ranks/segments.
-void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s) {
+void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s,
+                   KTimer* kt) {
     if (!geo.N) return;
     G3Geom g{geo, (geo.bs + G3T - 1) / G3T, true};
     const u32 nt = g.tpb * geo.nb;
-    k_g3_hist<0, SRC_KP><<<nt, WG, 0, s>>>(g, nullptr, t.KP, t.hist);
-    k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
-    k_g3_scatter<0, SRC_KP><<<nt, WG, 0, s>>>(g, nullptr, t.KP, nullptr, t.K2, t.SA, t.hist);
-    k_g3_hist<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, t.K2, t.hist);
-    k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
-    k_g3_scatter<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, t.K2, t.SA, t.K22, t.SA2, t.hist);
-    k_g3_hist<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, t.K22, t.hist);
-    k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
-    k_g3_scatter<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, t.K22, t.SA2, t.KP, t.RK, t.hist);
-    k_g3_hist<3, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, t.KP, t.hist);
-    k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
-    k_g3_scatter<3, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, t.KP, t.RK, t.K2, t.SA, t.hist);
-    k_r0_tile_heads<<<nt, WG, 0, s>>>(g, t.K2, t.tmax, t.tmin);
-    k_g3_tiles_scan<<<geo.nb, WG, 0, s>>>(t.tmax, t.cmax, g.tpb);
-    k_r0_tiles_rscan<<<geo.nb, WG, 0, s>>>(t.tmin, t.cmin, g.tpb);
-    k_r0_final<<<nt, WG, 0, s>>>(g, t.K2, t.SA, t.cmax, t.cmin, t.RK, next, next_cnt, blk_split);
+    const u64 N = geo.N, H = (u64)nt * 1024;  // H: per-tile histogram bytes
+    {
+        KScope k(kt, KT_LSD, "k_g3_hist<0, 1>", 4 * N + H);
+        k_g3_hist<0, SRC_KP><<<nt, WG, 0, s>>>(g, nullptr, t.KP, t.hist);
+    }
+    {
+        KScope k(kt, KT_LSD, "k_g3_scan", 3 * H);
+        k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
+    }
+    {
+        KScope k(kt, KT_LSD, "k_g3_scatter<0, 1>", 12 * N + H);
+        k_g3_scatter<0, SRC_KP><<<nt, WG, 0, s>>>(g, nullptr, t.KP, nullptr, t.K2, t.SA, t.hist);
+    }
+    u32* kin[3] = {t.K2, t.K22, t.KP};
+    u32* pin[3] = {t.SA, t.SA2, t.RK};
+    u32* kout[3] = {t.K22, t.KP, t.K2};
+    u32* pout[3] = {t.SA2, t.RK, t.SA};
+    static const char* const hn[3] = {"k_g3_hist<1, 2>", "k_g3_hist<2, 2>", "k_g3_hist<3, 2>"};
+    static const char* const sn[3] = {"k_g3_scatter<1, 2>", "k_g3_scatter<2, 2>", "k_g3_scatter<3, 2>"};
+    for (int q = 0; q < 3; ++q) {
+        {
+            KScope k(kt, KT_LSD, hn[q], 4 * N + H);
+            if (q == 0) k_g3_hist<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, kin[q], t.hist);
+            if (q == 1) k_g3_hist<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, kin[q], t.hist);
+            if (q == 2) k_g3_hist<3, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, kin[q], t.hist);
+        }
+        {
+            KScope k(kt, KT_LSD, "k_g3_scan", 3 * H);
+            k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
+        }
+        {
+            KScope k(kt, KT_LSD, sn[q], 16 * N + H);
+            if (q == 0) k_g3_scatter<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, kin[q], pin[q], kout[q], pout[q], t.hist);
+            if (q == 1) k_g3_scatter<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, kin[q], pin[q], kout[q], pout[q], t.hist);
+            if (q == 2) k_g3_scatter<3, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, kin[q], pin[q], kout[q], pout[q], t.hist);
+        }
+    }
+    {
+        KScope k(kt, KT_LSD, "k_r0_tile_heads", 4 * N);
+        k_r0_tile_heads<<<nt, WG, 0, s>>>(g, t.K2, t.tmax, t.tmin);
+        k_g3_tiles_scan<<<geo.nb, WG, 0, s>>>(t.tmax, t.cmax, g.tpb);
+        k_r0_tiles_rscan<<<geo.nb, WG, 0, s>>>(t.tmin, t.cmin, g.tpb);
+    }
+    {
+        // K 4 + SA 4 read, RK 4 scattered (+ 8 B per new segment)
+        KScope k(kt, KT_LSD, "k_r0_final", 12 * N);
+        k_r0_final<<<nt, WG, 0, s>>>(g, t.K2, t.SA, t.cmax, t.cmin, t.RK, next, next_cnt, blk_split);
+    }
 }
 
-void launch_gram3(const Geom& geo, const u8* text, const G3Bufs& t, hipStream_t s) {
+void launch_gram3(const Geom& geo, const u8* text, const G3Bufs& t, hipStream_t s, KTimer* kt) {
     if (!geo.N) return;
     G3Geom g{geo, (geo.bs + G3T - 1) / G3T, false};
     const u32 nt = g.tpb * geo.nb;
+    const u64 N = geo.N, H = (u64)nt * 1024;
     // pass c2: text -> (Ka, Pa); c1: -> (Kb, Pb); c0: -> (Ka, SA3); Pa/Pb live in ig3 (free until final)
     u32* Pa = reinterpret_cast<u32*>(t.ig3);
     u32* Pb = Pa + geo.N;
-    k_g3_hist<0, SRC_TEXT3><<<nt, WG, 0, s>>>(g, text, nullptr, t.hist);
-    k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
-    k_g3_scatter<0, SRC_TEXT3><<<nt, WG, 0, s>>>(g, text, nullptr, nullptr, t.Ka, Pa, t.hist);
-    k_g3_hist<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Ka, t.hist);
-    k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
-    k_g3_scatter<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Ka, Pa, t.Kb, Pb, t.hist);
-    k_g3_hist<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Kb, t.hist);
-    k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
-    k_g3_scatter<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Kb, Pb, t.Ka, t.SA3, t.hist);
+    {
+        KScope k(kt, KT_LSD, "k_g3_hist<0, 0>", N + H);
+        k_g3_hist<0, SRC_TEXT3><<<nt, WG, 0, s>>>(g, text, nullptr, t.hist);
+    }
+    {
+        KScope k(kt, KT_LSD, "k_g3_scan", 3 * H);
+        k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
+    }
+    {
+        KScope k(kt, KT_LSD, "k_g3_scatter<0, 0>", 9 * N + H);  // text 1 + (key, pos) 8
+        k_g3_scatter<0, SRC_TEXT3><<<nt, WG, 0, s>>>(g, text, nullptr, nullptr, t.Ka, Pa, t.hist);
+    }
+    {
+        KScope k(kt, KT_LSD, "k_g3_hist<1, 2>", 4 * N + H);
+        k_g3_hist<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Ka, t.hist);
+    }
+    {
+        KScope k(kt, KT_LSD, "k_g3_scan", 3 * H);
+        k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
+    }
+    {
+        KScope k(kt, KT_LSD, "k_g3_scatter<1, 2>", 16 * N + H);
+        k_g3_scatter<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Ka, Pa, t.Kb, Pb, t.hist);
+    }
+    {
+        KScope k(kt, KT_LSD, "k_g3_hist<2, 2>", 4 * N + H);
+        k_g3_hist<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Kb, t.hist);
+    }
+    {
+        KScope k(kt, KT_LSD, "k_g3_scan", 3 * H);
+        k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
+    }
+    {
+        KScope k(kt, KT_LSD, "k_g3_scatter<2, 2>", 16 * N + H);
+        k_g3_scatter<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Kb, Pb, t.Ka, t.SA3, t.hist);
+    }
     G3Geom gs{geo, g.tpb, true};
-    k_g3_tile_heads<<<nt, WG, 0, s>>>(gs, t.Ka, t.tmax);
-    k_g3_tiles_scan<<<geo.nb, WG, 0, s>>>(t.tmax, t.tcarry, g.tpb);
-    k_g3_final<<<nt, WG, 0, s>>>(gs, t.Ka, t.SA3, t.tcarry, t.ig3);
+    {
+        KScope k(kt, KT_LSD, "k_g3_tile_heads", 4 * N);
+        k_g3_tile_heads<<<nt, WG, 0, s>>>(gs, t.Ka, t.tmax);
+        k_g3_tiles_scan<<<geo.nb, WG, 0, s>>>(t.tmax, t.tcarry, g.tpb);
+    }
+    {
+        // K 4 + SA3 4 read, (slot, group start) 8 scattered
+        KScope k(kt, KT_LSD, "k_g3_final", 16 * N);
+        k_g3_final<<<nt, WG, 0, s>>>(gs, t.Ka, t.SA3, t.tcarry, t.ig3);
+    }
 }
-
 
 }  // namespace kolm

@@ -23,6 +23,8 @@
 //     chunk's speculative path (a token depends on its position only, so both parses
 //     coincide from there); greedy parses re-synchronise within a few tokens;
 //   * k_lz_emit: one thread per token slot writes its bytes at its final offset.
+#include <cstdlib>
+
 #include "kolm_internal.h"
 
 namespace kolm {
@@ -40,10 +42,16 @@ __device__ inline u32 uleb_len(u32 v) {
 
 __device__ inline u32 tok_bytes(u32 len, u32 dist) { return len ? 1 + uleb_len(len) + uleb_len(dist) : 2; }
 
-// Text accessor (a template point for staged copies of the text).
+// Text accessors: global memory, or an LDS copy of [lo, hi) with global fallback outside.
 struct GText {
     const u8* g;
     __device__ inline u8 operator[](u32 x) const { return g[x]; }
+};
+struct LText {
+    const u8* g;
+    const u8* l;
+    u32 lo, hi;
+    __device__ inline u8 operator[](u32 x) const { return (x - lo < hi - lo) ? l[x - lo] : g[x]; }
 };
 
 // Exact LCP(p, q) >= start, wave-cooperative (64 lanes x 4 bytes per step); maxl bounds it.
@@ -123,17 +131,45 @@ __device__ void best_match(const LzArgs& z, const T& t, u32 p, u32 end, u32 i, u
     out_dist = bd;
 }
 
-// Speculative parse of one chunk per wave (4 waves per workgroup).
+// Speculative parse of one chunk per wave; the 4 waves of a workgroup take 4 consecutive
+// chunks and share one LDS copy of their text windows [first chunk - 4096, last chunk
+// end + 64) (20 KiB): with 32 waves per CU each on its own window in global memory the
+// windows overflow L2 and every candidate compare re-fetches its line.
+constexpr u32 LZ_LWIN = LZ_WINDOW + 4 * LZ_CHUNK + 64;
+
+template <bool LDS>
 __global__ __launch_bounds__(256) void k_lz_spec(LzArgs z, u32 nchunks) {
-    // (staging the wave's 12 KiB text window in LDS measured slower: LDS-limited occupancy
-    // exposes the latency of the candidate loads, and the window is L1/L2-resident anyway)
+    __shared__ __align__(16) u8 win[LDS ? LZ_LWIN : 4];
     const u32 lane = threadIdx.x & 63;
     const u32 c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    LText t{z.text, win, 0u, 0u};
+    if (LDS) {
+        // the workgroup's window, from its first chunk's block
+        const u32 c0 = blockIdx.x * 4;
+        const u32 b0 = c0 / z.cpb, k0 = c0 - b0 * z.cpb;
+        const u32 bb = z.geo.base(b0), be = z.geo.end(b0);
+        const u32 s0 = bb + k0 * LZ_CHUNK;
+        const u32 lo = s0 > bb + LZ_WINDOW ? s0 - LZ_WINDOW : bb;
+        const u32 hi = min(s0 + 4 * LZ_CHUNK + 64, be);
+        if (lo < hi) {
+            const u32 n = hi - lo;
+            if ((lo & 3) == 0 && ((uintptr_t)z.text & 3) == 0) {
+                const u32* src = reinterpret_cast<const u32*>(z.text + lo);
+                u32* dst = reinterpret_cast<u32*>(win);
+                for (u32 i = threadIdx.x; i < n / 4; i += 256) dst[i] = src[i];
+                for (u32 i = (n & ~3u) + threadIdx.x; i < n; i += 256) win[i] = z.text[lo + i];
+            } else {
+                for (u32 i = threadIdx.x; i < n; i += 256) win[i] = z.text[lo + i];
+            }
+            t.lo = lo;
+            t.hi = hi;
+        }
+        __syncthreads();
+    }
     if (c >= nchunks) return;
     const u32 b = c / z.cpb, k = c - b * z.cpb;
     const u32 bend = z.geo.end(b);
     const u32 s = z.geo.base(b) + k * LZ_CHUNK;
-    const GText t{z.text};
     if (s >= bend) {
         if (lane == 0) {
             z.c_ntok[c] = 0;
@@ -322,11 +358,23 @@ __global__ __launch_bounds__(256) void k_lz_emit(LzArgs z, const u32* method, co
 
 }  // namespace
 
-void launch_lz_parse(const LzArgs& z, hipStream_t s) {
+void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
     if (!z.geo.nb) return;
     const u32 nchunks = z.cpb * z.geo.nb;
-    k_lz_spec<<<(nchunks + 3) / 4, 256, 0, s>>>(z, nchunks);
-    k_lz_stitch<<<z.geo.nb, 64, 0, s>>>(z);
+    {
+        // (slot, group start) windows 8 B + text 1 B per position (+16 B per token, added
+        // by the caller once the token count is known)
+        static const bool lds = !getenv("KOLM_LZ_LDS") || atoi(getenv("KOLM_LZ_LDS")) != 0;
+        KScope k(kt, KT_LZPARSE, lds ? "k_lz_spec<true>" : "k_lz_spec<false>", z.geo.N * 9);
+        if (lds)
+            k_lz_spec<true><<<(nchunks + 3) / 4, 256, 0, s>>>(z, nchunks);
+        else
+            k_lz_spec<false><<<(nchunks + 3) / 4, 256, 0, s>>>(z, nchunks);
+    }
+    {
+        KScope k(kt, KT_LZPARSE, "k_lz_stitch", (u64)nchunks * 32);
+        k_lz_stitch<<<z.geo.nb, 64, 0, s>>>(z);
+    }
 }
 
 void launch_lz_emit(const LzArgs& z, const u32* method, const u64* off, u8* arena, hipStream_t s) {

@@ -184,13 +184,23 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
 }  // namespace
 
 void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summary_cnt, u8* states,
-                hipStream_t s) {
+                hipStream_t s, KTimer* kt) {
     if (!geo.N) return;
     ChunkGeom cg{geo, (geo.bs + MTF_CHUNK - 1) / MTF_CHUNK};
     const u32 nchunks = cg.cpb * geo.nb;
-    k_mtf_summary<<<(nchunks + 255) / 256, 256, 0, s>>>(cg, in, summary, summary_cnt, nchunks);
-    k_mtf_compose<<<geo.nb, 64, 0, s>>>(cg, summary, summary_cnt, states);
-    k_mtf_replay<<<(nchunks + RT - 1) / RT, RT, 0, s>>>(cg, in, states, out, nchunks);
+    const u64 N = geo.N;
+    {
+        KScope k(kt, KT_MTF, "k_mtf_summary", N + (u64)nchunks * 256);
+        k_mtf_summary<<<(nchunks + 255) / 256, 256, 0, s>>>(cg, in, summary, summary_cnt, nchunks);
+    }
+    {
+        KScope k(kt, KT_MTF, "k_mtf_compose", (u64)nchunks * 512);
+        k_mtf_compose<<<geo.nb, 64, 0, s>>>(cg, summary, summary_cnt, states);
+    }
+    {
+        KScope k(kt, KT_MTF, "k_mtf_replay", 2 * N + (u64)nchunks * 256);
+        k_mtf_replay<<<(nchunks + RT - 1) / RT, RT, 0, s>>>(cg, in, states, out, nchunks);
+    }
 }
 
 }  // namespace kolm

@@ -95,6 +95,33 @@ struct kolm_ctx {
         u64 launches = 0, bytes = 0;
     };
     std::map<std::string, Acc> kacc;  // per kernel, accumulated while timing is enabled
+    // KTimer for multi-kernel launchers: events on the active stream, nested scopes allowed
+    struct Hook : KTimer {
+        kolm_ctx* c = nullptr;
+        struct Open {
+            int fam;
+            const char* name;
+            u64 bytes;
+            hipEvent_t a;
+        };
+        std::vector<Open> open;
+        void begin(int fam, const char* name, u64 bytes) override {
+            hipEvent_t a = c->ev_take();
+            KOLM_HIP_CHECK(hipEventRecord(a, c->active));
+            open.push_back({fam, name, bytes, a});
+        }
+        void end() override {
+            Open o = open.back();
+            open.pop_back();
+            hipEvent_t b = c->ev_take();
+            KOLM_HIP_CHECK(hipEventRecord(b, c->active));
+            c->pend.push_back({o.fam, o.name, o.a, b, o.bytes});
+        }
+    } hook;
+    KTimer* kt() {
+        hook.c = this;
+        return timing ? &hook : nullptr;
+    }
     hipEvent_t ev_take() {
         if (evused == evpool.size()) {
             hipEvent_t e;
@@ -162,10 +189,16 @@ kolm_ctx* g_default = nullptr;
 
 u32 bitlen(u32 v) { return v ? 32 - __builtin_clz(v) : 0; }
 
-const char* const kSmallSortName[NCLASS] = {
-    "k_single",          "k_small_sort<1>", "k_small_sort<2>", "k_small_sort<3>",
-    "k_small_sort<4>",   "k_small_sort<5>", "k_small_sort<6>", "k_small_sort<7>",
-    "k_small_sort<8>",   "k_small_sort<9>", "k_small_sort<10>", "k_small_sort<11>"};
+// kernel symbols as rocprof shows them: [32-bit sort words][class]
+const char* const kSmallSortName[2][NCLASS] = {
+    {"k_single", "k_small_sort<1, unsigned long>", "k_small_sort<2, unsigned long>",
+     "k_small_sort<3, unsigned long>", "k_small_sort<4, unsigned long>", "k_small_sort<5, unsigned long>",
+     "k_small_sort<6, unsigned long>", "k_small_sort<7, unsigned long>", "k_small_sort<8, unsigned long>",
+     "k_small_sort<9, unsigned long>", "k_small_sort<10, unsigned long>", "k_small_sort<11, unsigned long>"},
+    {"k_single", "k_small_sort<1, unsigned int>", "k_small_sort<2, unsigned int>", "k_small_sort<3, unsigned int>",
+     "k_small_sort<4, unsigned int>", "k_small_sort<5, unsigned int>", "k_small_sort<6, unsigned int>",
+     "k_small_sort<7, unsigned int>", "k_small_sort<8, unsigned int>", "k_small_sort<9, unsigned int>",
+     "k_small_sort<10, unsigned int>", "k_small_sort<11, unsigned int>"}};
 
 struct SortOut {
     u32 rounds = 0;
@@ -248,11 +281,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
             const u64 nt = lsd_tiles(geo) + 1;
             R0Bufs r{KP, a.K2, a.SA, a.K22, a.SA2, a.RK, c->get<u32>("r0hist", nt * 256), c->get<u32>("r0tmax", nt),
                      c->get<u32>("r0tmin", nt), c->get<u32>("r0cmax", nt), c->get<u32>("r0cmin", nt)};
-            {
-                // 4 passes (hist 4 B + scatter 16 B per element) + heads 4 B + ranks (K 4, SA 4, RK 4)
-                TScope t(c, KOLM_KT_MSD, "k_round0_lsd", N * 92);
-                launch_round0(geo, r, nxt, L.next_cnt, a.blk_split, s);
-            }
+            launch_round0(geo, r, nxt, L.next_cnt, a.blk_split, s, c->kt());
             out.active += N;
             out.rounds = 1;
             launch_update_done(blk_done, a.blk_split, geo.nb, s);
@@ -337,7 +366,8 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
         // per element: K2 + SA read, SA + RK write (16 B); per segment record 8 B
         for (int k = 0; k < NCLASS; ++k) {
             if (!h[C_CLS + k]) continue;
-            TScope t(c, KOLM_KT_SMALLSORT, kSmallSortName[k], (u64)h[C_CLSE + k] * 16 + (u64)h[C_CLS + k] * 8);
+            const int w32 = a.key_bits + k <= 31 ? 1 : 0;  // matches small_sort_c's choice
+            TScope t(c, KOLM_KT_SMALLSORT, kSmallSortName[w32][k], (u64)h[C_CLSE + k] * 16 + (u64)h[C_CLS + k] * 8);
             launch_small_sort(k, L.cls[k], h[C_CLS + k], a, L, s);
         }
         if (h[C_EQ]) {
@@ -364,12 +394,10 @@ struct Pipeline {
     void lyndon() {
         const u64 N = geo.N;
         const u64 ntiles = (u64)((geo.bs + TILE - 1) / TILE) * geo.nb + 16;
-        // Duval: text read ~2x + factor starts 4 B; merge; flags; FSL scans write 8 B
-        TScope t(c, KOLM_KT_LYNDON, "k_duval+lyndon_scans", N * 16);
         const u64 nch = (geo.bs + 32767) / 32768 * (u64)geo.nb + 1;  // DUVAL_SPAN
         launch_lyndon(geo, text, c->get<u8>("flag", N), c->get<u64>("FSL", N), c->get<u32>("lyn_fstart", N),
                       c->get<u32>("lyn_nfac", nch), c->get<u32>("lyn_stack", N), c->get<u32>("lyn_t1", 2 * ntiles + 16),
-                      c->get<u32>("lyn_t2", 2 * ntiles + 2 * geo.nb + 16), c->active);
+                      c->get<u32>("lyn_t2", 2 * ntiles + 2 * geo.nb + 16), c->active, c->kt());
     }
     // linear suffix order at 3 characters only: LZ77 candidate groups (SA3, idx3, GS3)
     void linear3() {
@@ -378,10 +406,7 @@ struct Pipeline {
         G3Bufs t{c->get<u32>("g3Ka", N), c->get<u32>("g3Kb", N), c->get<u32>("g3hist", nt * 256),
                  c->get<u32>("g3tmax", nt), c->get<u32>("g3tcarry", nt), c->get<u32>("SA3", N),
                  c->get<uint2>("ig3", N)};
-        // 3 LSD passes (hist: 4 B, scatter: 8 B in + 8 B out) + heads/final (K 4 B x2, SA3 4 B,
-        // idx3 + gs3 8 B scattered)
-        TScope ts(c, KOLM_KT_LZPARSE, "k_gram3_index", N * 80);
-        launch_gram3(geo, text, t, c->active);
+        launch_gram3(geo, text, t, c->active, c->kt());
         st.lin_rounds = 1;
         st.lin_active = N;
     }
@@ -414,10 +439,8 @@ struct Pipeline {
         const u64 N = geo.N;
         const u64 nch = (u64)((geo.bs + MTF_CHUNK - 1) / MTF_CHUNK) * geo.nb + 1;
         u8* out = c->get<u8>("mtf", N);
-        // summary: read N; compose: summaries + states 512 B/chunk; replay: N in, N out, state
-        TScope t(c, KOLM_KT_MTF, "k_mtf_summary+compose+replay", 3 * N + nch * 768);
         launch_mtf(geo, in, out, c->get<u8>("mtf_sum", nch * 256), c->get<u16>("mtf_cnt", nch),
-                   c->get<u8>("mtf_states", nch * 256), c->active);
+                   c->get<u8>("mtf_states", nch * 256), c->active, c->kt());
         return out;
     }
 
@@ -455,11 +478,7 @@ struct Pipeline {
 
     void lz(const LzArgs& z) {
         KOLM_HIP_CHECK(hipMemsetAsync(z.nlong, 0, sizeof(u32), c->active));
-        {
-            // idx3 + gs3 windows (8 B per position) + text; 16 B per token added after the batch
-            TScope t(c, KOLM_KT_LZPARSE, "k_lz_spec+stitch", geo.N * 9);
-            launch_lz_parse(z, c->active);
-        }
+        launch_lz_parse(z, c->active, c->kt());
     }
 };
 
@@ -595,6 +614,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
         st.lz_tokens = tokens;
         c->timing_collect(&st);
         st.kt[KOLM_KT_LZPARSE].bytes += tokens * 16;
+        if (c->timing && want_lz) c->kacc[getenv("KOLM_LZ_LDS") && !atoi(getenv("KOLM_LZ_LDS")) ? "k_lz_spec<false>" : "k_lz_spec<true>"].bytes += tokens * 16;  // token records
         st.lz_long = c->h_cnt[C_NLONG];
         st.ms_sa = ev_ms(ev[0], ev[1]);
         st.ms_entropy = ev_ms(ev[1], ev[2]);

@@ -68,6 +68,24 @@ struct Geom {
 
 void geom_init(Geom& g, u64 N, u32 bs);
 
+// Optional per-kernel timing hook for launchers that issue several kernels (null = off).
+// Families are include/kolm.h's KOLM_KT_*; names are the kernel symbols as rocprof shows
+// them; bytes are the algorithmic bytes of the launch.
+struct KTimer {
+    virtual void begin(int fam, const char* name, u64 bytes) = 0;
+    virtual void end() = 0;
+};
+struct KScope {
+    KTimer* t;
+    KScope(KTimer* t_, int fam, const char* name, u64 bytes) : t(t_) {
+        if (t) t->begin(fam, name, bytes);
+    }
+    ~KScope() {
+        if (t) t->end();
+    }
+};
+enum : int { KT_CLASSIFY = 0, KT_KEYGEN, KT_MSD, KT_SMALLSORT, KT_LSD, KT_LZPARSE, KT_MTF, KT_SIZES, KT_EMIT, KT_LYNDON };
+
 // XCD-aware workgroup -> tile remap (speed only, never correctness): workgroups are dealt
 // round-robin over the 8 XCDs, so give each XCD a contiguous range of tiles — tiles of
 // one block then share an L2 (random accesses inside a block's arrays stay L2-local).
@@ -141,7 +159,7 @@ void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, hipStream_t
 
 // ---- k_blocks.hip: per-block scans, Lyndon factors, BBWT gather ----
 void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u32* fstart, u32* nfac, u32* stack,
-                   u32* tile_tmp, u32* tile_tmp2, hipStream_t s);
+                   u32* tile_tmp, u32* tile_tmp2, hipStream_t s, KTimer* kt = nullptr);
 void launch_lyndon_isa(const Geom& geo, const u32* RK, u8* flag, u32* tile_tmp, u32* tile_tmp2, hipStream_t s);
 void launch_prevc(const Geom& geo, const u8* text, const u64* FSL, u8* prevc, hipStream_t s);
 void launch_bbwt_gather(const Geom& geo, const u32* SA, const u8* prevc, u8* out, hipStream_t s);
@@ -157,7 +175,7 @@ struct G3Bufs {
     uint2* ig3;   // [N] out: (slot, first slot of the group) of each position
 };
 u32 lsd_tiles(const Geom& geo);
-void launch_gram3(const Geom& geo, const u8* text, const G3Bufs& t, hipStream_t s);
+void launch_gram3(const Geom& geo, const u8* text, const G3Bufs& t, hipStream_t s, KTimer* kt = nullptr);
 struct R0Bufs {
     u32* KP;   // [N] in: 4-character keys by position; scratch afterwards
     u32* K2;   // [N] out: sorted keys (scratch)
@@ -168,11 +186,12 @@ struct R0Bufs {
     u32* hist;                    // [lsd_tiles * 256]
     u32 *tmax, *tmin, *cmax, *cmin;  // [lsd_tiles]
 };
-void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s);
+void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s,
+                   KTimer* kt = nullptr);
 
 // ---- k_mtf.hip ----
 void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summary_cnt, u8* states,
-                hipStream_t s);
+                hipStream_t s, KTimer* kt = nullptr);
 
 // ---- k_entropy.hip: cheap sizes, Rice sizes / emission, MDL, emission of simple models ----
 struct EmitArgs {
@@ -199,7 +218,7 @@ void launch_rice_only(const Geom& geo, const u8* in, int k, u8* out, u32* tile_t
                       u32* out_size, hipStream_t s);
 
 // ---- k_lz77.hip ----
-constexpr int LZ_CHUNK = 8192;  // speculative-parse chunk (one wave each)
+constexpr int LZ_CHUNK = 4096;  // speculative-parse chunk (one wave each)
 
 struct LzArgs {
     Geom geo;
@@ -231,7 +250,7 @@ struct LzArgs {
     u32* nlong;        // [1]
     u32 cpb;           // chunks per block
 };
-void launch_lz_parse(const LzArgs& z, hipStream_t s);
+void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr);
 void launch_lz_emit(const LzArgs& z, const u32* method, const u64* off, u8* arena, hipStream_t s);
 
 }  // namespace kolm

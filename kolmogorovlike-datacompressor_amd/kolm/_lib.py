@@ -35,7 +35,7 @@ class KolmError(RuntimeError):
         self.code = code
 
 
-KT_NAMES = ["classify", "keygen", "msd", "small_sort", "lz_match", "lz_parse", "mtf", "sizes", "emit",
+KT_NAMES = ["classify", "keygen", "msd", "small_sort", "lsd", "lz_parse", "mtf", "sizes", "emit",
             "lyndon_gather"]
 
 
