@@ -73,6 +73,23 @@ __device__ u32 wave_lcp(const T& t, u32 p, u32 q, u32 start, u32 maxl) {
     }
 }
 
+// 8 bytes at window offset x (any alignment) from three aligned LDS dwords, little-endian.
+__device__ inline u64 lds8(const u8* l, u32 x) {
+    const u32* w = reinterpret_cast<const u32*>(l) + (x >> 2);
+    const u32 sh = x & 3;
+    const u32 w0 = w[0], w1 = w[1], w2 = w[2];
+    return ((u64)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
+}
+
+template <class T>
+struct IsLds {
+    static constexpr bool value = false;
+};
+template <>
+struct IsLds<LText> {
+    static constexpr bool value = true;
+};
+
 // Longest match at p (uniform across the wave).  i = idx3[p], gs = gs3[p].
 template <class T>
 __device__ void best_match(const LzArgs& z, const T& t, u32 p, u32 end, u32 i, u32 gs, u32& out_len,
@@ -82,6 +99,14 @@ __device__ void best_match(const LzArgs& z, const T& t, u32 p, u32 end, u32 i, u
     if (p + (u32)LZ_MIN <= end && i > gs) {
         const u32 maxl = end - p;
         const u32 capl = min((u32)LZ_CAP, maxl);
+        // LDS window: capped compares 8 bytes at a time with p's bytes hoisted
+        bool wide = false;
+        u64 P8[LZ_CAP / 8];
+        if constexpr (IsLds<T>::value) {
+            wide = p >= t.lo && p + capl + 11 <= t.hi;
+#pragma unroll
+            for (int k = 0; k < LZ_CAP / 8; ++k) P8[k] = wide ? lds8(t.l, p - t.lo + 3 + 8 * k) : 0ull;
+        }
         u32 k0 = i;  // candidates this batch: slots k0-1-lane
         for (;;) {
             bool valid = k0 > gs + lane;
@@ -94,8 +119,27 @@ __device__ void best_match(const LzArgs& z, const T& t, u32 p, u32 end, u32 i, u
                 // a later candidate wins only if strictly longer: it must match at `best`
                 const bool can = best == 0 || (best < maxl && t[p + best] == t[q + best]);
                 if (can) {
-                    l = LZ_MIN;
-                    while (l < capl && t[p + l] == t[q + l]) ++l;
+                    l = LZ_MIN;  // the 3-gram is shared by the group
+                    bool done = false;
+                    if constexpr (IsLds<T>::value) {
+                        if (wide) {
+                            // q >= window start (candidates lie inside the window), q < p
+#pragma unroll
+                            for (int k = 0; k < LZ_CAP / 8; ++k) {
+                                if (l >= capl) break;
+                                const u64 d = P8[k] ^ lds8(t.l, q - t.lo + 3 + 8 * k);
+                                if (d) {
+                                    l += (u32)(__ffsll((long long)d) - 1) >> 3;
+                                    break;
+                                }
+                                l += 8;
+                            }
+                            l = min(l, capl);
+                            done = true;
+                        }
+                    }
+                    if (!done)
+                        while (l < capl && t[p + l] == t[q + l]) ++l;
                 }
             }
             u64 longm = __ballot(valid && l >= capl && capl < maxl);
@@ -108,16 +152,13 @@ __device__ void best_match(const LzArgs& z, const T& t, u32 p, u32 end, u32 i, u
                 ++nlong;
             }
             // max length, ties -> smallest lane (= smallest distance)
-            u64 key = valid ? (((u64)l << 8) | (63u - lane)) : 0ull;
+            u32 lm = valid ? l : 0u;
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {
-                const u64 other = __shfl_xor(key, o);
-                key = other > key ? other : key;
-            }
-            const u32 lb = (u32)(key >> 8);
-            if (lb > best) {
-                best = lb;
-                bd = p - __builtin_amdgcn_readlane(q, 63u - (u32)(key & 0xFF));
+            for (int o = 32; o >= 1; o >>= 1) lm = max(lm, (u32)__shfl_xor(lm, o));
+            if (lm > best) {
+                const u64 at = __ballot(valid && l == lm);
+                best = lm;
+                bd = p - __builtin_amdgcn_readlane(q, (u32)__ffsll((long long)at) - 1);
             }
             if (best >= maxl || inwin != ~0ull) break;
             k0 -= 64;
