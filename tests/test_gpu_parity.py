@@ -180,3 +180,65 @@ def test_edge_cases(kolm_gpu, data, bs):
     got = kolm_gpu.compress_blocks_fixed(data, bs)
     assert got == O.compress_blocks_fixed(data, bs, range(9))
     assert kolm_gpu.decompress(got) == data
+
+
+def _fib_word(n: int) -> bytes:
+    a, b = b"a", b"ab"
+    while len(b) < n:
+        a, b = b, b + a
+    return b[:n]
+
+
+def _thue_morse(n: int) -> bytes:
+    return bytes(97 + (bin(i).count("1") & 1) for i in range(n))
+
+
+def _adversarial(kind: str, n: int) -> bytes:
+    rng = np.random.default_rng(len(kind))
+    if kind == "decreasing":      # every byte its own Lyndon factor inside a run
+        return (bytes(range(255, -1, -1)) * (n // 256 + 1))[:n]
+    if kind == "fibonacci":       # LCPs ~ n: many doubling rounds, few factors
+        return _fib_word(n)
+    if kind == "thue_morse":
+        return _thue_morse(n)
+    if kind == "period7":         # equal factors repeated, every rotation tied
+        return (rng.integers(0, 256, 7).astype(np.uint8).tobytes() * (n // 7 + 1))[:n]
+    if kind == "runs":            # long runs with sparse breaks: huge factors spanning spans
+        out = bytearray(b"a" * n)
+        for p in rng.integers(0, n, 40):
+            out[int(p)] = 98 + int(p) % 3
+        return bytes(out)
+    if kind == "zeros":
+        return bytes(n)
+    if kind == "two_symbols":
+        return rng.integers(0, 2, n).astype(np.uint8).tobytes()
+    raise ValueError(kind)
+
+
+ADV = ["decreasing", "fibonacci", "thue_morse", "period7", "runs", "zeros", "two_symbols"]
+
+
+@pytest.mark.parametrize("kind", ADV)
+def test_adversarial_bbwt_lz77(kolm_gpu, kind):
+    """Structures the reference's own tests do not cover but the GPU formulation is
+    sensitive to: Lyndon factors spanning many 32 KiB Duval spans (or one factor per
+    byte), LCPs of the whole block (doubling to the last round), every rotation tied,
+    matches running to the block end.  One block (200 KB; 100 KB for the two slow
+    oracle cases), vs the oracle."""
+    data = _adversarial(kind, 100_000 if kind in ("fibonacci", "thue_morse") else 200_000)
+    assert kolm_gpu.bbwt_forward(data) == O.bbwt_forward(data), "bbwt"
+    assert kolm_gpu.encode_lz77(data)[0] == O.encode_lz77(data), "lz77"
+
+
+@pytest.mark.parametrize("kind", ["decreasing", "period7", "runs", "two_symbols"])
+def test_adversarial_batched(kolm_gpu, kind):
+    """Same structures through the batched entry: 4 blocks of 65536 + a ragged tail."""
+    from kolm import _lib
+    data = _adversarial(kind, 4 * 65536 + 1234)
+    bs = 65536
+    sizes, method, payloads, _ = _lib.encode_blocks(data, bs)
+    for i in range((len(data) + bs - 1) // bs):
+        blk = data[i * bs:(i + 1) * bs]
+        cand = _oracle_all(blk)
+        assert list(map(int, sizes[i])) == [len(c) for c in cand], f"block {i}"
+        assert payloads[i] == cand[int(method[i])], f"block {i}"
