@@ -613,6 +613,113 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
     }
 }
 
+// Tiny segments (class C <= TINY_C, at most 16 elements): one thread per segment, the
+// (key << 32 | position) words sorted by a bitonic network in registers (ties in position
+// order), runs -> new groups.  In dense rounds the key is gathered here from KP (no K2
+// round trip, no LDS: full occupancy hides the gather); otherwise K2 from k_keygen_small.
+// Same write rules as k_small_sort (SA only if split, RK skipped for a FIRST run).
+template <int C>
+__global__ __launch_bounds__(256) void k_tiny_sort(const Seg* segs, u32 count, SortArgs a, Lists L) {
+    constexpr u32 S = 1u << C;
+    __shared__ u32 sh[WG / 64], wtot;
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u32 i = blockIdx.x * WG + tid;
+    Seg sg{0, 0};
+    u32 len = 0;
+    if (i < count) {
+        sg = segs[i];
+        len = sg.len & SEG_LEN;
+    }
+    u64 v[S];
+#pragma unroll
+    for (u32 e = 0; e < S; ++e) {
+        v[e] = ~0ull;
+        if (e < len) {
+            const u32 g = sg.start + e;
+            const u32 p = a.SA[g];
+            const u32 kv = a.KP ? a.KP[p] : a.K2[g];
+            v[e] = ((u64)kv << 32) | p;
+        }
+    }
+#pragma unroll
+    for (u32 k = 2; k <= S; k <<= 1)
+#pragma unroll
+        for (u32 j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (u32 e = 0; e < S; ++e) {
+                const u32 l = e ^ j;
+                if (l > e) {
+                    const bool up = (e & k) == 0;
+                    const u64 x = v[e], y = v[l];
+                    if ((x > y) == up) {
+                        v[e] = y;
+                        v[l] = x;
+                    }
+                }
+            }
+    // runs
+    bool split = false;
+    u32 nnew = 0;
+    {
+        u32 prev = 0;
+#pragma unroll
+        for (u32 e = 0; e < S; ++e) {
+            if (e < len) {
+                const u32 kv = (u32)(v[e] >> 32);
+                if (e > 0 && kv != prev) split = true;
+                prev = kv;
+            }
+        }
+    }
+    {
+        u32 rs = 0;
+#pragma unroll
+        for (u32 e = 0; e < S; ++e) {
+            if (e < len) {
+                if (e > 0 && (u32)(v[e] >> 32) != (u32)(v[e - 1] >> 32)) {
+                    nnew += (e - rs >= 2) ? 1u : 0u;
+                    rs = e;
+                }
+            }
+        }
+        if (len && len - rs >= 2) ++nnew;
+    }
+    // one global atomic per workgroup for the new segments
+    u32 incl = nnew;
+#pragma unroll
+    for (u32 o = 1; o < 64; o <<= 1) {
+        const u32 x = __shfl_up(incl, o);
+        if (lane >= o) incl += x;
+    }
+    if (lane == 63) sh[w] = incl;
+    __syncthreads();
+    u32 off = incl - nnew;
+    for (u32 q = 0; q < w; ++q) off += sh[q];
+    if (tid == WG - 1) {
+        const u32 tot = off + nnew;
+        wtot = tot ? atomicAdd(L.next_cnt, tot) : 0u;
+    }
+    __syncthreads();
+    off += wtot;
+    if (!len) return;
+    const bool first = (sg.len & SEG_FIRST) != 0;
+    u32 rs = 0;
+#pragma unroll
+    for (u32 e = 0; e < S; ++e) {
+        if (e < len) {
+            const u32 kv = (u32)(v[e] >> 32), pos = (u32)v[e];
+            if (e > 0 && kv != (u32)(v[e - 1] >> 32)) {
+                if (e - rs >= 2) L.next[off++] = Seg{sg.start + rs, e - rs};
+                rs = e;
+            }
+            if (split) a.SA[sg.start + e] = pos;
+            if (a.initial || rs != 0 || !first) a.RK[pos] = sg.start + rs;
+        }
+    }
+    if (len - rs >= 2) L.next[off++] = Seg{sg.start + rs, len - rs};
+    if (split) a.blk_split[a.geo.block_of(sg.start)] = 1;
+}
+
 __global__ void k_single(const Seg* segs, u32 count, SortArgs a) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) {
@@ -696,6 +803,17 @@ static void small_sort_c(const Seg* segs, u32 count, const SortArgs& a, const Li
         k_small_sort<C, u32><<<cdiv(count, TILE >> C), WG, 0, s>>>(segs, count, a, L);
     else
         k_small_sort<C, u64><<<cdiv(count, TILE >> C), WG, 0, s>>>(segs, count, a, L);
+}
+
+void launch_tiny_sort(int c, const Seg* segs, u32 count, const SortArgs& a, const Lists& L, hipStream_t s) {
+    if (!count) return;
+    switch (c) {
+        case 1: k_tiny_sort<1><<<cdiv(count, WG), WG, 0, s>>>(segs, count, a, L); break;
+        case 2: k_tiny_sort<2><<<cdiv(count, WG), WG, 0, s>>>(segs, count, a, L); break;
+        case 3: k_tiny_sort<3><<<cdiv(count, WG), WG, 0, s>>>(segs, count, a, L); break;
+        case 4: k_tiny_sort<4><<<cdiv(count, WG), WG, 0, s>>>(segs, count, a, L); break;
+        default: break;
+    }
 }
 
 void launch_small_sort(int c, const Seg* segs, u32 count, const SortArgs& a, const Lists& L,

@@ -300,6 +300,13 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
         if (h[C_ACTIVE] == 0) break;
         out.active += h[C_ACTIVE];
         out.rounds = round + 1;
+        static const bool dbg = getenv("KOLM_DEBUG_ROUNDS") != nullptr;
+        if (dbg) {
+            fprintf(stderr, "[kolm] round %u h=%u active=%u large: segs %u elems %u | class segs/elems:", round, a.h,
+                    h[C_ACTIVE], h[C_L0SEG], h[C_L0ELEM]);
+            for (int k = 0; k < NCLASS; ++k) fprintf(stderr, " %d:%u/%u", k, h[C_CLS + k], h[C_CLSE + k]);
+            fprintf(stderr, "\n");
+        }
         {
             // Dense rounds: keys by position first (sequential pass), then one gather per
             // slot; sparse rounds gather the key inputs per active slot directly.
@@ -315,6 +322,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
             const u64 per = a.KP ? 12 : a.initial ? (cyclic ? 20 : 11) : (cyclic ? 20 : 12);
             for (int k = 1; k < NCLASS; ++k) {
                 if (!h[C_CLS + k]) continue;
+                if (a.KP && k <= TINY_C) continue;  // k_tiny_sort gathers KP itself
                 TScope t(c, KOLM_KT_KEYGEN, "k_keygen_small", (u64)h[C_CLSE + k] * per);
                 launch_keygen_small(k, L.cls[k], h[C_CLS + k], a, s);
             }
@@ -366,6 +374,14 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
         // per element: K2 + SA read, SA + RK write (16 B); per segment record 8 B
         for (int k = 0; k < NCLASS; ++k) {
             if (!h[C_CLS + k]) continue;
+            if (k >= 1 && k <= TINY_C) {
+                static const char* const tn[TINY_C + 1] = {"", "k_tiny_sort<1>", "k_tiny_sort<2>", "k_tiny_sort<3>",
+                                                           "k_tiny_sort<4>"};
+                // SA + key (KP gather or K2) read, SA + RK write per element; 8 B per segment
+                TScope t(c, KOLM_KT_SMALLSORT, tn[k], (u64)h[C_CLSE + k] * 16 + (u64)h[C_CLS + k] * 8);
+                launch_tiny_sort(k, L.cls[k], h[C_CLS + k], a, L, s);
+                continue;
+            }
             const int w32 = a.key_bits + k <= 31 ? 1 : 0;  // matches small_sort_c's choice
             TScope t(c, KOLM_KT_SMALLSORT, kSmallSortName[w32][k], (u64)h[C_CLSE + k] * 16 + (u64)h[C_CLS + k] * 8);
             launch_small_sort(k, L.cls[k], h[C_CLS + k], a, L, s);
