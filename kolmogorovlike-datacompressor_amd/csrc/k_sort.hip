@@ -812,6 +812,7 @@ void launch_tiny_sort(int c, const Seg* segs, u32 count, const SortArgs& a, cons
         case 2: k_tiny_sort<2><<<cdiv(count, WG), WG, 0, s>>>(segs, count, a, L); break;
         case 3: k_tiny_sort<3><<<cdiv(count, WG), WG, 0, s>>>(segs, count, a, L); break;
         case 4: k_tiny_sort<4><<<cdiv(count, WG), WG, 0, s>>>(segs, count, a, L); break;
+        case 5: k_tiny_sort<5><<<cdiv(count, WG), WG, 0, s>>>(segs, count, a, L); break;
         default: break;
     }
 }

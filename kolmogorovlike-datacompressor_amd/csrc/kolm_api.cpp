@@ -375,8 +375,8 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
         for (int k = 0; k < NCLASS; ++k) {
             if (!h[C_CLS + k]) continue;
             if (k >= 1 && k <= TINY_C) {
-                static const char* const tn[TINY_C + 1] = {"", "k_tiny_sort<1>", "k_tiny_sort<2>", "k_tiny_sort<3>",
-                                                           "k_tiny_sort<4>"};
+                static const char* const tn[6] = {"",          "k_tiny_sort<1>", "k_tiny_sort<2>",
+                                                  "k_tiny_sort<3>", "k_tiny_sort<4>", "k_tiny_sort<5>"};
                 // SA + key (KP gather or K2) read, SA + RK write per element; 8 B per segment
                 TScope t(c, KOLM_KT_SMALLSORT, tn[k], (u64)h[C_CLSE + k] * 16 + (u64)h[C_CLS + k] * 8);
                 launch_tiny_sort(k, L.cls[k], h[C_CLS + k], a, L, s);

@@ -152,7 +152,7 @@ void launch_msd_scatter(const LTile* tiles, u32 ntiles, const LSeg* segs, const 
                         u32 shift, u32 width, const u32* hist, hipStream_t s);
 void launch_copy_back(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
                       hipStream_t s);
-constexpr int TINY_C = 4;  // classes 1..TINY_C (<= 16 elements): one thread per segment
+constexpr int TINY_C = 5;  // classes 1..TINY_C (<= 32 elements): one thread per segment
 void launch_tiny_sort(int c, const Seg* segs, u32 count, const SortArgs& a, const Lists& L, hipStream_t s);
 void launch_small_sort(int c, const Seg* segs, u32 count, const SortArgs& a, const Lists& L,
                        hipStream_t s);
