@@ -101,12 +101,7 @@ __device__ void best_match(const LzArgs& z, const T& t, u32 p, u32 end, u32 i, u
         const u32 capl = min((u32)LZ_CAP, maxl);
         // LDS window: capped compares 8 bytes at a time with p's bytes hoisted
         bool wide = false;
-        u64 P8[LZ_CAP / 8];
-        if constexpr (IsLds<T>::value) {
-            wide = p >= t.lo && p + capl + 11 <= t.hi;
-#pragma unroll
-            for (int k = 0; k < LZ_CAP / 8; ++k) P8[k] = wide ? lds8(t.l, p - t.lo + 3 + 8 * k) : 0ull;
-        }
+        if constexpr (IsLds<T>::value) wide = p >= t.lo && p + capl + 11 <= t.hi;
         u32 k0 = i;  // candidates this batch: slots k0-1-lane
         for (;;) {
             bool valid = k0 > gs + lane;
@@ -127,7 +122,8 @@ __device__ void best_match(const LzArgs& z, const T& t, u32 p, u32 end, u32 i, u
 #pragma unroll
                             for (int k = 0; k < LZ_CAP / 8; ++k) {
                                 if (l >= capl) break;
-                                const u64 d = P8[k] ^ lds8(t.l, q - t.lo + 3 + 8 * k);
+                                // p's bytes loaded lazily: most candidates differ in the first 8
+                                const u64 d = lds8(t.l, p - t.lo + 3 + 8 * k) ^ lds8(t.l, q - t.lo + 3 + 8 * k);
                                 if (d) {
                                     l += (u32)(__ffsll((long long)d) - 1) >> 3;
                                     break;
@@ -151,14 +147,27 @@ __device__ void best_match(const LzArgs& z, const T& t, u32 p, u32 end, u32 i, u
                 longm &= longm - 1;
                 ++nlong;
             }
-            // max length, ties -> smallest lane (= smallest distance)
-            u32 lm = valid ? l : 0u;
+            // max length, ties -> smallest lane (= smallest distance).  Lengths below 64
+            // (all but extended matches): bit-serial over ballots, no cross-lane data
+            // movement (__shfl_xor is an LDS permute + address math per step)
+            const u32 lv = valid ? l : 0u;
+            u64 cand = __ballot(lv > best);
+            if (cand) {
+                if (__ballot(lv >= 64u)) {
+                    u32 lm = lv;
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) lm = max(lm, (u32)__shfl_xor(lm, o));
-            if (lm > best) {
-                const u64 at = __ballot(valid && l == lm);
-                best = lm;
-                bd = p - __builtin_amdgcn_readlane(q, (u32)__ffsll((long long)at) - 1);
+                    for (int o = 32; o >= 1; o >>= 1) lm = max(lm, (u32)__shfl_xor(lm, o));
+                    cand = __ballot(lv == lm);
+                } else {
+#pragma unroll
+                    for (int b = 5; b >= 0; --b) {
+                        const u64 tb = __ballot((lv >> b) & 1u) & cand;
+                        if (tb) cand = tb;
+                    }
+                }
+                const u32 wl = (u32)__ffsll((long long)cand) - 1;
+                best = __builtin_amdgcn_readlane(lv, wl);
+                bd = p - __builtin_amdgcn_readlane(q, wl);
             }
             if (best >= maxl || inwin != ~0ull) break;
             k0 -= 64;
