@@ -31,26 +31,20 @@ struct TileGeom {
     }
 };
 
-__device__ inline u32 wave_reduce_min(u32 v) {
-    for (int o = 32; o >= 1; o >>= 1) v = min(v, (u32)__shfl_xor(v, o));
-    return v;
-}
-__device__ inline u32 wave_reduce_max(u32 v) {
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, (u32)__shfl_xor(v, o));
-    return v;
-}
+__device__ inline u32 wave_reduce_min(u32 v) { return wave_reduce(v, OpMinU(), BIG); }
+__device__ inline u32 wave_reduce_max(u32 v) { return wave_reduce(v, OpMaxU(), 0u); }
 
-// exclusive scan across the workgroup (min or max, forward or reverse)
+// exclusive scan across the workgroup (min or max, forward or reverse); DPP within waves
 template <bool REV, bool MAX>
 __device__ inline u32 wg_excl(u32 v, u32 ident, u32* sh) {
     const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    u32 incl = v;
-    for (u32 o = 1; o < 64; o <<= 1) {
-        u32 t = REV ? __shfl_down(incl, o) : __shfl_up(incl, o);
-        if (REV ? (lane + o < 64) : (lane >= o)) incl = MAX ? max(incl, t) : min(incl, t);
+    u32 incl, ex;
+    if (MAX) {
+        incl = REV ? wave_incl_scan_rev(v, OpMaxU(), ident) : wave_incl_scan(v, OpMaxU(), ident);
+    } else {
+        incl = REV ? wave_incl_scan_rev(v, OpMinU(), ident) : wave_incl_scan(v, OpMinU(), ident);
     }
-    u32 ex = REV ? __shfl_down(incl, 1) : __shfl_up(incl, 1);
-    if (REV ? lane == 63 : lane == 0) ex = ident;
+    ex = REV ? KOLM_DPP(ident, incl, DPP_WAVE_SHL1, 0xF) : KOLM_DPP(ident, incl, DPP_WAVE_SHR1, 0xF);
     if (REV ? lane == 0 : lane == 63) sh[w] = incl;
     __syncthreads();
     u32 carry = ident;

@@ -97,12 +97,7 @@ __global__ __launch_bounds__(WG) void k_g3_scan(G3Geom g, u32* hist) {
         }
     }
     // exclusive scan of the digit totals
-    u32 incl = acc;
-#pragma unroll
-    for (u32 o = 1; o < 64; o <<= 1) {
-        const u32 x = __shfl_up(incl, o);
-        if (lane >= o) incl += x;
-    }
+    const u32 incl = wave_incl_scan(acc, OpAddU(), 0u);
     if (lane == 63) sh[w] = incl;
     __syncthreads();
     u32 carry = 0;
@@ -179,11 +174,7 @@ __global__ __launch_bounds__(WG) void k_g3_scatter(G3Geom g, const u8* text, con
     }
 }
 
-__device__ inline u32 wave_max(u32 v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, (u32)__shfl_xor(v, o));
-    return v;
-}
+__device__ inline u32 wave_max(u32 v) { return wave_reduce(v, OpMaxU(), 0u); }
 
 // slot g starts a group: first slot of the block, a tail slot, or a new 3-gram
 __device__ inline bool g3_head(const G3Geom& g, const u32* K, u32 slot, u32 base, u32 fe) {
@@ -215,14 +206,8 @@ __global__ __launch_bounds__(WG) void k_g3_tiles_scan(const u32* in, u32* out, u
     for (u32 c0 = 0; c0 < tpb; c0 += WG) {
         const u32 k = c0 + threadIdx.x;
         const u32 v = k < tpb ? in[(u64)b * tpb + k] : 0u;
-        u32 incl = v;
-#pragma unroll
-        for (u32 o = 1; o < 64; o <<= 1) {
-            const u32 x = __shfl_up(incl, o);
-            if (lane >= o) incl = max(incl, x);
-        }
-        u32 ex = __shfl_up(incl, 1);
-        if (lane == 0) ex = 0;
+        const u32 incl = wave_incl_scan(v, OpMaxU(), 0u);
+        const u32 ex = KOLM_DPP(0u, incl, DPP_WAVE_SHR1, 0xF);
         if (lane == 63) sh[w] = incl;
         __syncthreads();
         u32 wc = carry;
@@ -251,14 +236,8 @@ __global__ __launch_bounds__(WG) void k_g3_final(G3Geom g, const u32* K, u32* SA
         hd[e] = (i < hi && g3_head(g, K, i, base, fe)) ? 1u : 0u;
         if (hd[e]) loc = max(loc, i);
     }
-    u32 incl = loc;
-#pragma unroll
-    for (u32 o = 1; o < 64; o <<= 1) {
-        const u32 x = __shfl_up(incl, o);
-        if (lane >= o) incl = max(incl, x);
-    }
-    u32 ex = __shfl_up(incl, 1);
-    if (lane == 0) ex = 0;
+    const u32 incl = wave_incl_scan(loc, OpMaxU(), 0u);
+    const u32 ex = KOLM_DPP(0u, incl, DPP_WAVE_SHR1, 0xF);
     if (lane == 63) sh[w] = incl;
     __syncthreads();
     u32 run = max(tcarry[blockIdx.x], ex);
@@ -291,11 +270,7 @@ constexpr u32 BIG = 0xFFFFFFFFu;
 
 __device__ inline bool r0_head(const u32* K, u32 g, u32 base) { return g == base || K[g] != K[g - 1]; }
 
-__device__ inline u32 wave_min(u32 v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = min(v, (u32)__shfl_xor(v, o));
-    return v;
-}
+__device__ inline u32 wave_min(u32 v) { return wave_reduce(v, OpMinU(), BIG); }
 
 __global__ __launch_bounds__(WG) void k_r0_tile_heads(G3Geom g, const u32* K, u32* tmax, u32* tmin) {
     __shared__ u32 s1[WG / 64], s2[WG / 64];
@@ -332,14 +307,8 @@ __global__ __launch_bounds__(WG) void k_r0_tiles_rscan(const u32* in, u32* out, 
     for (u32 cc = 0; cc < nch; ++cc) {
         const u32 k = (nch - 1 - cc) * WG + threadIdx.x;
         const u32 v = k < tpb ? in[(u64)b * tpb + k] : BIG;
-        u32 incl = v;
-#pragma unroll
-        for (u32 o = 1; o < 64; o <<= 1) {
-            const u32 x = __shfl_down(incl, o);
-            if (lane + o < 64) incl = min(incl, x);
-        }
-        u32 ex = __shfl_down(incl, 1);
-        if (lane == 63) ex = BIG;
+        const u32 incl = wave_incl_scan_rev(v, OpMinU(), BIG);
+        const u32 ex = KOLM_DPP(BIG, incl, DPP_WAVE_SHL1, 0xF);
         if (lane == 0) sh[w] = incl;
         __syncthreads();
         u32 wc = carry;
@@ -376,17 +345,8 @@ __global__ __launch_bounds__(WG) void k_r0_final(G3Geom g, const u32* K, const u
     }
     // forward exclusive max (group start entering the thread), reverse exclusive min
     // (first head after the thread)
-    u32 fi = lmax, ri = lmin;
-#pragma unroll
-    for (u32 o = 1; o < 64; o <<= 1) {
-        const u32 x = __shfl_up(fi, o);
-        if (lane >= o) fi = max(fi, x);
-        const u32 y = __shfl_down(ri, o);
-        if (lane + o < 64) ri = min(ri, y);
-    }
-    u32 fex = __shfl_up(fi, 1), rex = __shfl_down(ri, 1);
-    if (lane == 0) fex = 0;
-    if (lane == 63) rex = BIG;
+    const u32 fi = wave_incl_scan(lmax, OpMaxU(), 0u), ri = wave_incl_scan_rev(lmin, OpMinU(), BIG);
+    const u32 fex = KOLM_DPP(0u, fi, DPP_WAVE_SHR1, 0xF), rex = KOLM_DPP(BIG, ri, DPP_WAVE_SHL1, 0xF);
     if (lane == 63) sh[w] = fi;
     if (lane == 0) sh2[w] = ri;
     __syncthreads();
@@ -421,12 +381,7 @@ __global__ __launch_bounds__(WG) void k_r0_final(G3Geom g, const u32* K, const u
             nseg += len[e] >= 2;
         }
     }
-    u32 incl = nseg;
-#pragma unroll
-    for (u32 o = 1; o < 64; o <<= 1) {
-        const u32 x = __shfl_up(incl, o);
-        if (lane >= o) incl += x;
-    }
+    const u32 incl = wave_incl_scan(nseg, OpAddU(), 0u);
     if (lane == 63) sh3[w] = incl;
     if (split) anysplit = 1;
     __syncthreads();

@@ -53,14 +53,8 @@ struct OpAdd {
 template <bool REV, class Op>
 __device__ inline u32 wg_excl_scan(u32 v, Op op, u32 ident, u32* sh /*[4]*/) {
     const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    u32 incl = v;
-#pragma unroll
-    for (u32 o = 1; o < 64; o <<= 1) {
-        u32 t = REV ? __shfl_down(incl, o) : __shfl_up(incl, o);
-        if (REV ? (lane + o < 64) : (lane >= o)) incl = op(incl, t);
-    }
-    u32 ex = REV ? __shfl_down(incl, 1) : __shfl_up(incl, 1);
-    if (REV ? lane == 63 : lane == 0) ex = ident;
+    const u32 incl = REV ? wave_incl_scan_rev(v, op, ident) : wave_incl_scan(v, op, ident);
+    const u32 ex = REV ? KOLM_DPP(ident, incl, DPP_WAVE_SHL1, 0xF) : KOLM_DPP(ident, incl, DPP_WAVE_SHR1, 0xF);
     if (REV ? lane == 0 : lane == 63) sh[w] = incl;
     __syncthreads();
     u32 carry = ident;
@@ -171,16 +165,13 @@ __global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur, Sort
         const int c = seg_class(a, cur, ncur, i0 + tid, s);
         u64 pend = __ballot(c >= 0);
         u32 nt = c == NCLASS ? (s.len + TILE - 1) / TILE : 0u;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) nt += __shfl_xor(nt, o);
+        nt = wave_reduce(nt, OpAddU(), 0u);
         if (lane == 0 && nt) atomicAdd(&ltiles, nt);
         while (pend) {
             const u32 f = (u32)__ffsll((long long)pend) - 1;
-            const int cc = __shfl(c, f);
+            const int cc = __builtin_amdgcn_readlane(c, f);
             const u64 m = __ballot(c == cc);
-            u32 v = c == cc ? s.len : 0u;
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+            const u32 v = wave_reduce(c == cc ? s.len : 0u, OpAddU(), 0u);
             if (lane == f) {
                 atomicAdd(&lcnt[cc], (u32)__popcll(m));
                 atomicAdd(&lel[cc], v);
@@ -210,11 +201,11 @@ __global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur, Sort
         u32 li = 0;
         while (pend) {
             const u32 f = (u32)__ffsll((long long)pend) - 1;
-            const int cc = __shfl(c, f);
+            const int cc = __builtin_amdgcn_readlane(c, f);
             const u64 m = __ballot(c == cc);
             u32 base = 0;
             if (lane == f) base = atomicAdd(&lcur[cc], (u32)__popcll(m));
-            base = __shfl(base, f);
+            base = __builtin_amdgcn_readlane(base, f);
             if (c == cc) li = base + (u32)__popcll(m & lt);
             pend &= ~m;
         }
@@ -685,12 +676,7 @@ __global__ __launch_bounds__(256) void k_tiny_sort(const Seg* segs, u32 count, S
         if (len && len - rs >= 2) ++nnew;
     }
     // one global atomic per workgroup for the new segments
-    u32 incl = nnew;
-#pragma unroll
-    for (u32 o = 1; o < 64; o <<= 1) {
-        const u32 x = __shfl_up(incl, o);
-        if (lane >= o) incl += x;
-    }
+    const u32 incl = wave_incl_scan(nnew, OpAddU(), 0u);
     if (lane == 63) sh[w] = incl;
     __syncthreads();
     u32 off = incl - nnew;

@@ -68,6 +68,58 @@ struct Geom {
 
 void geom_init(Geom& g, u64 N, u32 bs);
 
+// ---- wave64 scans on DPP (gfx9 row shifts + row broadcasts): VALU only, no LDS permute
+// (__shfl_up/__shfl_xor compile to ds_bpermute + address math per step) ----
+constexpr int DPP_ROW_SHR1 = 0x111, DPP_ROW_SHR2 = 0x112, DPP_ROW_SHR4 = 0x114, DPP_ROW_SHR8 = 0x118;
+constexpr int DPP_ROW_SHL1 = 0x101, DPP_ROW_SHL2 = 0x102, DPP_ROW_SHL4 = 0x104, DPP_ROW_SHL8 = 0x108;
+constexpr int DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143, DPP_WAVE_SHR1 = 0x138, DPP_WAVE_SHL1 = 0x130;
+
+#define KOLM_DPP(old, v, ctrl, rmask) \
+    ((u32)__builtin_amdgcn_update_dpp((int)(old), (int)(v), (ctrl), (rmask), 0xF, false))
+
+// inclusive scan in lane order (lane 63 ends with the total)
+template <class Op>
+__device__ inline u32 wave_incl_scan(u32 v, Op op, u32 ident) {
+    v = op(v, KOLM_DPP(ident, v, DPP_ROW_SHR1, 0xF));
+    v = op(v, KOLM_DPP(ident, v, DPP_ROW_SHR2, 0xF));
+    v = op(v, KOLM_DPP(ident, v, DPP_ROW_SHR4, 0xF));
+    v = op(v, KOLM_DPP(ident, v, DPP_ROW_SHR8, 0xF));
+    v = op(v, KOLM_DPP(ident, v, DPP_ROW_BCAST15, 0xA));
+    v = op(v, KOLM_DPP(ident, v, DPP_ROW_BCAST31, 0xC));
+    return v;
+}
+template <class Op>
+__device__ inline u32 wave_excl_scan(u32 v, Op op, u32 ident) {
+    return KOLM_DPP(ident, wave_incl_scan(v, op, ident), DPP_WAVE_SHR1, 0xF);
+}
+// reverse order (lane 0 ends with the total): mirror the lane index through the scan
+template <class Op>
+__device__ inline u32 wave_incl_scan_rev(u32 v, Op op, u32 ident) {
+    const u32 lane = __lane_id();
+    // bpermute-free reversal is not available in DPP across rows; use one permute each way
+    const u32 r = (u32)__builtin_amdgcn_ds_bpermute((int)((63 - lane) << 2), (int)v);
+    const u32 s = wave_incl_scan(r, op, ident);
+    return (u32)__builtin_amdgcn_ds_bpermute((int)((63 - lane) << 2), (int)s);
+}
+template <class Op>
+__device__ inline u32 wave_excl_scan_rev(u32 v, Op op, u32 ident) {
+    return KOLM_DPP(ident, wave_incl_scan_rev(v, op, ident), DPP_WAVE_SHL1, 0xF);
+}
+
+template <class Op>
+__device__ inline u32 wave_reduce(u32 v, Op op, u32 ident) {
+    return (u32)__builtin_amdgcn_readlane((int)wave_incl_scan(v, op, ident), 63);
+}
+struct OpAddU {
+    __device__ u32 operator()(u32 a, u32 b) const { return a + b; }
+};
+struct OpMaxU {
+    __device__ u32 operator()(u32 a, u32 b) const { return a > b ? a : b; }
+};
+struct OpMinU {
+    __device__ u32 operator()(u32 a, u32 b) const { return a < b ? a : b; }
+};
+
 // Optional per-kernel timing hook for launchers that issue several kernels (null = off).
 // Families are include/kolm.h's KOLM_KT_*; names are the kernel symbols as rocprof shows
 // them; bytes are the algorithmic bytes of the launch.
