@@ -451,13 +451,16 @@ __device__ inline void reg_stage(KT (&r)[8], u32 tid, u32 k, u32 S) {
     }
 }
 
+__device__ inline u32 SKI(u32 i) { return i + (i >> 6); }
+
 template <int C, class KT>
 __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, SortArgs a, Lists L) {
     constexpr u32 S = 1u << C;
     constexpr u32 SPT = TILE / S;
     constexpr bool W32 = sizeof(KT) == 4;
     constexpr KT NONEK = ~(KT)0;
-    __shared__ KT sk[TILE];
+    // one pad word per 64: the per-thread 8-element runs (8*tid + e) hit 64 distinct banks
+    __shared__ KT sk[TILE + TILE / 64];
     __shared__ u32 sa_l[W32 ? TILE : 1];
     __shared__ Seg ss[SPT];
     __shared__ u32 sh[WG / 64];
@@ -489,16 +492,16 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
                 key = ((u64)kv << 32) | p;
             }
         }
-        sk[slot] = key;
+        sk[SKI(slot)] = key;
     }
     __syncthreads();
     KT r[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) r[e] = sk[8 * tid + e];
+    for (int e = 0; e < 8; ++e) r[e] = sk[SKI(8 * tid + e)];
     for (u32 k = 2; k <= S; k <<= 1) {
         if (k > 8) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) sk[8 * tid + e] = r[e];
+            for (int e = 0; e < 8; ++e) sk[SKI(8 * tid + e)] = r[e];
             __syncthreads();
             for (u32 j = k >> 1; j >= 8; j >>= 1) {
                 const u32 lj = 31 - __clz(j);
@@ -508,16 +511,16 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
                     const u32 i = ((q >> lj) << (lj + 1)) | (q & (j - 1));
                     const u32 l = i + j;
                     const bool up = (k == S) || ((i & k) == 0);
-                    const KT x = sk[i], y = sk[l];
+                    const KT x = sk[SKI(i)], y = sk[SKI(l)];
                     if ((x > y) == up) {
-                        sk[i] = y;
-                        sk[l] = x;
+                        sk[SKI(i)] = y;
+                        sk[SKI(l)] = x;
                     }
                 }
                 __syncthreads();
             }
 #pragma unroll
-            for (int e = 0; e < 8; ++e) r[e] = sk[8 * tid + e];
+            for (int e = 0; e < 8; ++e) r[e] = sk[SKI(8 * tid + e)];
             __syncthreads();
         }
         if (k >= 8) reg_stage<4>(r, tid, k, S);
