@@ -46,27 +46,59 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(data: bytes, bs: int, budget_s: float):
-    """Oracle (reference algorithms, 1 thread) on whole 1 MiB blocks of the same stream:
-    every candidate 0..8 + MDL, as the reference's per-block loop (Re-Pair excluded)."""
+    """Oracle (reference algorithms) on whole 1 MiB blocks of the same stream: every
+    candidate 0..8 + MDL, as the reference's per-block loop (Re-Pair excluded).  Timed
+    block-parallel on T threads (ctypes releases the GIL; blocks are independent, SURVEY
+    §8d) and on 1 thread, each for about half the budget."""
+    from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
-    t0 = time.time()
-    nbytes = 0
-    blocks = 0
-    while True:
-        blk = data[blocks * bs:(blocks + 1) * bs]
+    nblk = max(1, len(data) // bs)
+
+    def one(i):
+        blk = data[(i % nblk) * bs:(i % nblk + 1) * bs]
         sizes = [len(oracle.candidate(m, blk)) for m in range(9)]
         _ = int(np.argmin(sizes))
-        nbytes += len(blk)
-        blocks += 1
-        if time.time() - t0 >= budget_s or blocks * bs >= len(data):
+        return len(blk)
+
+    # 1 thread
+    t0 = time.time()
+    n1 = b1 = 0
+    while True:
+        n1 += one(b1)
+        b1 += 1
+        if time.time() - t0 >= budget_s / 2 or b1 >= nblk:
             break
-    el = time.time() - t0
-    return {"value": round(nbytes / el / MB, 5), "unit": "MB/s", "cores": 1, "kind": "port",
-            "sample": f"{blocks} x {bs >> 20} MiB block(s) of the bench stream, candidates 0..8 "
-                      f"(5x BBWT, list MTF, bit-serial Rice, exhaustive 4 KiB LZ77), {el:.1f} s, 1 thread; "
-                      "Re-Pair (id 9) excluded as in the GPU path"}
+    el1 = time.time() - t0
+    # T threads, whole waves of T blocks
+    T = max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16
+    t0 = time.time()
+    nt = bt = 0
+    with ThreadPoolExecutor(T) as ex:
+        while True:
+            nt += sum(ex.map(one, range(bt, bt + T)))
+            bt += T
+            if time.time() - t0 >= budget_s / 2:
+                break
+    elt = time.time() - t0
+    model = _cpu_model()
+    return {"value": round(nt / elt / MB, 5), "unit": "MB/s", "cores": T, "kind": "port",
+            "sample": f"{bt} x {bs >> 20} MiB blocks on {T} threads ({elt:.1f} s) and {b1} on 1 thread "
+                      f"({el1:.1f} s) of the bench stream, candidates 0..8 (5x BBWT, list MTF, bit-serial "
+                      f"Rice, exhaustive 4 KiB LZ77), Re-Pair (id 9) excluded as in the GPU path; {model}",
+            "single_thread": {"value": round(n1 / el1 / MB, 5), "cores": 1}}
 
 
 def main():
@@ -163,6 +195,12 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": name,
             "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": int(bytes_per_launch),
             "launches_per_step": k["launches"] // a.steps}
+    # whole pipeline: every kernel's algorithmic bytes per step / wall time per step (the two
+    # streams overlap, so this is the chip-level rate the path sustains)
+    alg_step = sum(v["bytes"] for v in ktimes.values()) / a.steps
+    pipe = {"algorithmic_bytes_per_step": int(alg_step),
+            "achieved_GBs": round(alg_step / (ms_step * 1e-3) / 1e9, 2),
+            "frac": round(alg_step / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -187,6 +225,7 @@ def main():
                        "methods": np.bincount(method, minlength=9).tolist(),
                        "device_ms": {k: round(s0[k], 2) for k in ("ms_total", "ms_sa", "ms_lz", "ms_entropy", "ms_emit")},
                        "rounds": [s0["lin_rounds"], s0["cyc_rounds"]],
+                       "pipeline_roofline": pipe,
                        "families_ms_per_step": {kk: round(v["ms"] / a.steps, 2) for kk, v in
                                                 sorted(kern.items(), key=lambda kv: -kv[1]["ms"])},
                        "kernels_ms_per_step": {kk: round(v["ms"] / a.steps, 3) for kk, v in

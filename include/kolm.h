@@ -12,6 +12,9 @@
  *                             ties -> lowest id)                        PY:2152-2178, 2332-2369
  *   kolm_encode_blocks_device: same, input already resident in device memory
  *                             (bench / multi-GPU path; PY has no equivalent).
+ *   kolm_encode_blocks_multi: same as kolm_encode_blocks over several devices of one
+ *                             process (contiguous block shards, one host thread and
+ *                             context per device).
  * The container/TOC writer stays on the host (PY:2375-2445), see kolm/container.py.
  *
  * Conventions: plain pointers and sizes; caller-allocated buffers with explicit
@@ -119,6 +122,16 @@ int kolm_encode_blocks(const uint8_t* data, const uint64_t* starts, const uint32
                        uint32_t nblocks, uint32_t cand_mask, const int32_t* force_method,
                        uint32_t* sizes, uint32_t* method, uint8_t* payload_arena,
                        uint64_t arena_cap, uint64_t* payload_off, kolm_stats* stats);
+
+/* kolm_encode_blocks over ngpu devices (0..ngpu-1, clamped to the device count and the
+ * block count) of this process: fixed blocks of block_size over data[0, total), block i
+ * of shard r lives on device r, shards are contiguous block ranges.  Outputs exactly as
+ * kolm_encode_blocks (block order; sizes [nblocks*9], method [nblocks], payload_off
+ * [nblocks+1]).  stats (optional) sums counts and takes the max of times over devices. */
+int kolm_encode_blocks_multi(int ngpu, const uint8_t* data, uint64_t total, uint32_t block_size,
+                             uint32_t cand_mask, const int32_t* force_method, uint32_t* sizes,
+                             uint32_t* method, uint8_t* payload_arena, uint64_t arena_cap,
+                             uint64_t* payload_off, kolm_stats* stats);
 
 /* ---- explicit contexts and device-resident batches ------------------------------ */
 int kolm_ctx_create(int device, kolm_ctx** out);

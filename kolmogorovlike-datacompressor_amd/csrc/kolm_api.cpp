@@ -16,6 +16,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/kolm.h"
@@ -186,6 +187,7 @@ TScope::~TScope() noexcept(false) {
 
 std::mutex g_mu;
 kolm_ctx* g_default = nullptr;
+std::vector<kolm_ctx*> g_multi;  // per-device contexts of kolm_encode_blocks_multi
 
 u32 bitlen(u32 v) { return v ? 32 - __builtin_clz(v) : 0; }
 
@@ -738,10 +740,18 @@ int kolm_init(int device) {
 
 int kolm_shutdown(void) {
     std::lock_guard<std::mutex> g(g_mu);
-    if (!g_default) return KOLM_OK;
-    int r = kolm_ctx_destroy(g_default);
+    int r = KOLM_OK;
+    for (kolm_ctx*& c : g_multi)
+        if (c) {
+            const int e = kolm_ctx_destroy(c);
+            if (e) r = e;
+            c = nullptr;
+        }
+    g_multi.clear();
+    if (!g_default) return r;
+    const int e = kolm_ctx_destroy(g_default);
     g_default = nullptr;
-    return r;
+    return e ? e : r;
 }
 
 int kolm_ctx_reserve(kolm_ctx* c, uint64_t total_bytes, uint32_t max_block) {
@@ -886,6 +896,125 @@ int kolm_encode_blocks(const uint8_t* data, const uint64_t* starts, const uint32
         std::memcpy(payload_off, off.data(), sizeof(u64) * (nblocks + 1));
         return KOLM_OK;
     });
+}
+
+int kolm_encode_blocks_multi(int ngpu, const uint8_t* data, uint64_t total, uint32_t block_size,
+                             uint32_t cand_mask, const int32_t* force_method, uint32_t* sizes, uint32_t* method,
+                             uint8_t* payload_arena, uint64_t arena_cap, uint64_t* payload_off, kolm_stats* stats) {
+    if (ngpu < 1 || (total && !data) || !payload_off || block_size == 0) return KOLM_EARG;
+    if ((cand_mask & KOLM_DEFAULT_MASK) == 0) return KOLM_EARG;
+    const u64 nb64 = (total + block_size - 1) / block_size;
+    if (nb64 > 0xFFFFFFFFull) return KOLM_EARG;
+    const u32 nb = (u32)nb64;
+    int ndev = 0;
+    if (int e = guarded([&] {
+            KOLM_HIP_CHECK(hipGetDeviceCount(&ndev));
+            return KOLM_OK;
+        }))
+        return e;
+    if (ndev < 1) {
+        set_err("no HIP device");
+        return KOLM_ENOINIT;
+    }
+    const u32 G = (u32)std::max<u64>(1, std::min<u64>({(u64)ngpu, (u64)ndev, std::max<u64>(nb, 1)}));
+    // contiguous shards of whole blocks (the last block may be short)
+    std::vector<u32> b0(G + 1);
+    for (u32 r = 0; r <= G; ++r) b0[r] = (u32)((u64)nb * r / G);
+    struct Part {
+        int rc = KOLM_OK;
+        std::string err;
+        std::vector<u8> pay;
+        std::vector<u64> off;
+        kolm_stats st{};
+    };
+    std::vector<Part> part(G);
+    auto run = [&](u32 r) {
+        Part& P = part[r];
+        const u32 nbr = b0[r + 1] - b0[r];
+        if (!nbr) {
+            P.off.assign(1, 0);
+            return;
+        }
+        const u64 lo = (u64)b0[r] * block_size, hi = std::min<u64>(total, (u64)b0[r + 1] * block_size);
+        const u64 n = hi - lo;
+        kolm_ctx* c = nullptr;
+        {
+            std::lock_guard<std::mutex> g(g_mu);
+            if (g_multi.size() < G) g_multi.resize(G, nullptr);
+            if (!g_multi[r] && (P.rc = ctx_create((int)r, &g_multi[r])) != KOLM_OK) {
+                P.err = g_err;
+                return;
+            }
+            c = g_multi[r];
+        }
+        P.rc = guarded([&] {
+            std::lock_guard<std::mutex> g(c->mu);
+            KOLM_HIP_CHECK(hipSetDevice(c->device));
+            if (int e = check_geom(n, block_size)) return e;
+            u8* d = upload(c, data + lo, n);
+            const bool has_raw = (cand_mask & 1u) && force_method == nullptr;
+            const u64 dcap = (has_raw ? n : 9 * n) + 64 * (u64)nbr + 256;
+            u8* arena = c->get<u8>("arena", dcap);
+            P.off.assign(nbr + 1, 0);
+            int rc = encode_batch(c, d, n, block_size, cand_mask & KOLM_DEFAULT_MASK,
+                                  force_method ? force_method + b0[r] : nullptr, arena, dcap,
+                                  sizes ? sizes + (u64)b0[r] * KOLM_NCAND : nullptr, method ? method + b0[r] : nullptr,
+                                  P.off.data(), stats ? &P.st : nullptr);
+            if (rc) return rc;
+            P.pay.resize(P.off[nbr]);
+            if (P.off[nbr]) {
+                KOLM_HIP_CHECK(hipMemcpyAsync(P.pay.data(), arena, P.off[nbr], hipMemcpyDeviceToHost, c->stream));
+                c->sync();
+            }
+            return KOLM_OK;
+        });
+        if (P.rc) P.err = g_err;
+    };
+    std::vector<std::thread> th;
+    for (u32 r = 1; r < G; ++r) th.emplace_back(run, r);
+    run(0);
+    for (auto& t : th) t.join();
+    for (u32 r = 0; r < G; ++r)
+        if (part[r].rc) {
+            set_err(part[r].err);
+            return part[r].rc;
+        }
+    u64 pos = 0;
+    payload_off[0] = 0;
+    for (u32 r = 0; r < G; ++r) {
+        const u32 nbr = b0[r + 1] - b0[r];
+        if (pos + part[r].pay.size() > arena_cap) {
+            set_err("payload_arena too small");
+            return KOLM_ECAP;
+        }
+        if (!part[r].pay.empty()) std::memcpy(payload_arena + pos, part[r].pay.data(), part[r].pay.size());
+        for (u32 i = 1; i <= nbr; ++i) payload_off[b0[r] + i] = pos + part[r].off[i];
+        pos += part[r].pay.size();
+    }
+    if (stats) {
+        kolm_stats agg{};
+        for (u32 r = 0; r < G; ++r) {
+            const kolm_stats& s = part[r].st;
+            agg.lin_rounds = std::max(agg.lin_rounds, s.lin_rounds);
+            agg.cyc_rounds = std::max(agg.cyc_rounds, s.cyc_rounds);
+            agg.lin_active += s.lin_active;
+            agg.cyc_active += s.cyc_active;
+            agg.lz_tokens += s.lz_tokens;
+            agg.lz_long += s.lz_long;
+            agg.ms_total = std::max(agg.ms_total, s.ms_total);
+            agg.ms_sa = std::max(agg.ms_sa, s.ms_sa);
+            agg.ms_lz = std::max(agg.ms_lz, s.ms_lz);
+            agg.ms_entropy = std::max(agg.ms_entropy, s.ms_entropy);
+            agg.ms_emit = std::max(agg.ms_emit, s.ms_emit);
+            for (int k = 0; k < KOLM_NKT; ++k) {
+                agg.kt[k].ms += s.kt[k].ms;
+                agg.kt[k].launches += s.kt[k].launches;
+                agg.kt[k].bytes += s.kt[k].bytes;
+            }
+        }
+        *stats = agg;
+    }
+    return KOLM_OK;
 }
 
 int kolm_bbwt_forward(const uint8_t* in, size_t n, uint8_t* out) {

@@ -193,8 +193,9 @@ def candidate_mask() -> int:
 # block API
 # ---------------------------------------------------------------------------
 
-def encode_blocks(data: bytes, block_size: int, cand_mask: Optional[int] = None):
-    """Batched device MDL over fixed blocks: (method_ids, orig_lens, payloads, sizes)."""
+def encode_blocks(data: bytes, block_size: int, cand_mask: Optional[int] = None, devices: int = 1):
+    """Batched device MDL over fixed blocks: (method_ids, orig_lens, payloads, sizes).
+    devices > 1 shards the blocks over that many GPUs of this process."""
     if block_size <= 0:
         raise ValueError("block_size must be positive")
     global _last_stats
@@ -202,21 +203,25 @@ def encode_blocks(data: bytes, block_size: int, cand_mask: Optional[int] = None)
     n = len(data)
     if n == 0:
         return [], [], [], None
-    sizes, method, payloads, st = _lib.encode_blocks(bytes(data), block_size, mask)
+    if devices > 1:
+        sizes, method, payloads, st = _lib.encode_blocks_multi(bytes(data), block_size, devices, mask)
+    else:
+        sizes, method, payloads, st = _lib.encode_blocks(bytes(data), block_size, mask)
     _last_stats = st
     orig = [min(block_size, n - i) for i in range(0, n, block_size)]
     return [int(m) for m in method], orig, payloads, sizes
 
 
-def compress_blocks_fixed(data: bytes, block_size: int = 8192) -> bytes:
-    """Fixed-size chunking + per-block MDL selection + KOLR container (PY:2332-2445)."""
+def compress_blocks_fixed(data: bytes, block_size: int = 8192, devices: int = 1) -> bytes:
+    """Fixed-size chunking + per-block MDL selection + KOLR container (PY:2332-2445).
+    `devices` (not in PY) spreads the blocks over that many GPUs of this process."""
     if block_size <= 0:
         raise ValueError("block_size must be positive")
     n = len(data)
     nb = (n + block_size - 1) // block_size
     if nb > 0xFFFF:
         raise struct.error("'H' format requires 0 <= number <= 65535")
-    mids, orig, payloads, _ = encode_blocks(data, block_size)
+    mids, orig, payloads, _ = encode_blocks(data, block_size, devices=devices)
     return write_container(MODE_FIXED, block_size, n, mids, orig, payloads)
 
 

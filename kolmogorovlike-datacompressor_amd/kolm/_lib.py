@@ -89,6 +89,7 @@ SIGNATURES = [
     ("kolm_lz77_encode", I32, [U8P, SZ, P, SZ, ctypes.POINTER(SZ)]),
     ("kolm_bbwt_mtf_rice", I32, [U8P, SZ, I32, I32, P, SZ, ctypes.POINTER(SZ)]),
     ("kolm_encode_blocks", I32, [U8P, P, P, U32, U32, P, P, P, P, U64, P, P]),
+    ("kolm_encode_blocks_multi", I32, [I32, U8P, U64, U32, U32, P, P, P, P, U64, P, P]),
     ("kolm_ctx_create", I32, [I32, ctypes.POINTER(P)]),
     ("kolm_ctx_destroy", I32, [P]),
     ("kolm_ctx_reserve", I32, [P, U64, U32]),
@@ -234,5 +235,24 @@ def encode_blocks(data: bytes, block_size: int, cand_mask: int = KOLM_DEFAULT_MA
         fz.ctypes.data if fz is not None else None,
         sizes.ctypes.data, method.ctypes.data, arena.ctypes.data, cap, off.ctypes.data,
         ctypes.byref(st)))
+    payloads = [arena[int(off[i]):int(off[i + 1])].tobytes() for i in range(nb)]
+    return sizes[:nb], method[:nb], payloads, st.as_dict()
+
+
+def encode_blocks_multi(data: bytes, block_size: int, ngpu: int, cand_mask: int = KOLM_DEFAULT_MASK):
+    """encode_blocks over ngpu devices of this process (contiguous block shards, one host
+    thread per device; kolm_encode_blocks_multi).  Same return value."""
+    ensure_init()
+    n = len(data)
+    nb = (n + block_size - 1) // block_size if n else 0
+    sizes = np.zeros((max(nb, 1), KOLM_NCAND), dtype=np.uint32)
+    method = np.zeros(max(nb, 1), dtype=np.uint32)
+    off = np.zeros(nb + 1, dtype=np.uint64)
+    cap = 9 * n + 64 * nb + 64
+    arena = np.zeros(cap, dtype=np.uint8)
+    st = Stats()
+    check(load().kolm_encode_blocks_multi(
+        int(ngpu), data, n, block_size, cand_mask, None, sizes.ctypes.data, method.ctypes.data,
+        arena.ctypes.data, cap, off.ctypes.data, ctypes.byref(st)))
     payloads = [arena[int(off[i]):int(off[i + 1])].tobytes() for i in range(nb)]
     return sizes[:nb], method[:nb], payloads, st.as_dict()

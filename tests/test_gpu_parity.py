@@ -242,3 +242,16 @@ def test_adversarial_batched(kolm_gpu, kind):
         cand = _oracle_all(blk)
         assert list(map(int, sizes[i])) == [len(c) for c in cand], f"block {i}"
         assert payloads[i] == cand[int(method[i])], f"block {i}"
+
+
+@pytest.mark.parametrize("ngpu", [1, 2])
+def test_encode_blocks_multi(kolm_gpu, ngpu):
+    """Single-process multi-device entry (kolm_encode_blocks_multi): same outputs as the
+    single-device batch (ngpu is clamped to the visible device count)."""
+    from kolm import _lib
+    data = D.mixed_corpus()[:700_000]
+    bs = 65536
+    a = _lib.encode_blocks(data, bs)
+    b = _lib.encode_blocks_multi(data, bs, ngpu)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
+    assert kolm_gpu.compress_blocks_fixed(data, bs, devices=ngpu) == O.compress_blocks_fixed(data, bs, range(9))
