@@ -145,7 +145,7 @@ __global__ __launch_bounds__(WG) void k_tile_starts(TileGeom tg, const u8* flag,
 
 // Phase C': FS = last start <= p, FL = (next start > p, or block end) - FS.
 __global__ __launch_bounds__(WG) void k_fsfl(TileGeom tg, const u8* flag, const u32* cmax,
-                                             const u32* cmin, u64* FSL) {
+                                             const u32* cmin, u64* FSL, u8* FEd) {
     __shared__ u32 sh[WG / 64];
     u32 lo, hi, b;
     if (!tg.range(blockIdx.x, lo, hi, b)) return;
@@ -176,6 +176,7 @@ __global__ __launch_bounds__(WG) void k_fsfl(TileGeom tg, const u8* flag, const 
         if (i < hi) {
             const u32 end = fe == BIG ? bend : fe;
             FSL[i] = (u64)fsv[e] | ((u64)(end - fsv[e]) << 32);  // factor start | length << 32
+            FEd[i] = (u8)min(end - i, 255u);                      // distance to the factor end
         }
         if (f[e]) fe = i0 + e;
     }
@@ -418,12 +419,52 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
 
 // prevc[p] = the character preceding p cyclically inside its factor (streaming pass), so
 // the BBWT gather needs one random byte per slot instead of a factor lookup + a byte.
-__global__ void k_prevc(Geom geo, const u8* text, const u64* FSL, u8* prevc) {
+__global__ void k_prevc1(Geom geo, const u8* text, const u8* flag, const u64* FSL, u8* prevc) {
     for (u32 p = blockIdx.x * blockDim.x + threadIdx.x; p < geo.N; p += gridDim.x * blockDim.x) {
-        const u64 f = FSL[p];
-        const u32 fs = (u32)f;
-        prevc[p] = text[p == fs ? fs + (u32)(f >> 32) - 1 : p - 1];
+        u32 src = p - 1;
+        if (flag[p]) {  // factor start: its predecessor is the factor's last byte
+            const u64 f = FSL[p];
+            src = (u32)f + (u32)(f >> 32) - 1;
+        }
+        prevc[p] = text[src];
     }
+}
+
+// 16 positions per thread: flags and output as 16-byte words, text bytes p-1 .. p+14 from
+// aligned words (text 16-byte aligned; the launcher checks).
+__global__ __launch_bounds__(256) void k_prevc(Geom geo, const u8* text, const u8* flag, const u64* FSL, u8* prevc) {
+    const u32 p0 = (blockIdx.x * 256 + threadIdx.x) * 16;
+    const u32 N = (u32)geo.N;
+    if (p0 >= N) return;
+    if (p0 + 16 > N || p0 < 4) {
+        for (u32 p = p0; p < min(p0 + 16, N); ++p) {
+            u32 src = p - 1;
+            if (flag[p]) {
+                const u64 f = FSL[p];
+                src = (u32)f + (u32)(f >> 32) - 1;
+            }
+            prevc[p] = text[src];
+        }
+        return;
+    }
+    const uint4 fv = *reinterpret_cast<const uint4*>(flag + p0);
+    const u32 fw[4] = {fv.x, fv.y, fv.z, fv.w};
+    const u32* tw = reinterpret_cast<const u32*>(text + p0) - 1;  // bytes p0-4 .. p0+15
+    u32 w[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) w[i] = tw[i];
+    u32 o[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        // byte p0+e-1 = byte (e+3) of the 20-byte window starting at p0-4
+        u32 c = (w[(e + 3) >> 2] >> (8 * ((e + 3) & 3))) & 0xFF;
+        if ((fw[e >> 2] >> (8 * (e & 3))) & 0xFF) {  // factor start: the factor's last byte
+            const u64 f = FSL[p0 + e];
+            c = text[(u32)f + (u32)(f >> 32) - 1];
+        }
+        o[e >> 2] |= c << (8 * (e & 3));
+    }
+    *reinterpret_cast<uint4*>(prevc + p0) = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 // 4096 slots per workgroup, XCD-remapped so a block's slots (and its 1 MiB of prevc)
@@ -451,8 +492,8 @@ void launch_lyndon_isa(const Geom& geo, const u32* RK, u8* flag, u32* tile_tmp, 
 }
 
 // Lyndon factorisation of every block (parallel Duval + merge) -> per-position FSL.
-void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u32* fstart, u32* nfac, u32* stack,
-                   u32* tile_tmp, u32* tile_tmp2, hipStream_t s, KTimer* kt) {
+void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u8* FEd, u32* fstart, u32* nfac,
+                   u32* stack, u32* tile_tmp, u32* tile_tmp2, hipStream_t s, KTimer* kt) {
     if (!geo.N) return;
     TileGeom tg{geo, (geo.bs + TILE - 1) / TILE};
     const u32 nt = tg.tpb * geo.nb;
@@ -479,15 +520,18 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u32* fst
         k_tiles_scan<true, false><<<geo.nb, WG, 0, s>>>(C2, D, tg.tpb, BIG);
     }
     {
-        KScope k(kt, KT_LYNDON, "k_fsfl", 9 * N);  // flag 1 + FSL 8
-        k_fsfl<<<nt, WG, 0, s>>>(tg, flag, B, D, FSL);
+        KScope k(kt, KT_LYNDON, "k_fsfl", 10 * N);  // flag 1 + FSL 8 + FEd 1
+        k_fsfl<<<nt, WG, 0, s>>>(tg, flag, B, D, FSL, FEd);
     }
 }
 
-void launch_prevc(const Geom& geo, const u8* text, const u64* FSL, u8* prevc, hipStream_t s) {
+void launch_prevc(const Geom& geo, const u8* text, const u8* flag, const u64* FSL, u8* prevc, hipStream_t s) {
     if (!geo.N) return;
     const u32 grid = (u32)std::min<u64>((geo.N + 255) / 256, 65535);
-    k_prevc<<<grid, 256, 0, s>>>(geo, text, FSL, prevc);
+    if (((uintptr_t)text & 15) == 0)
+        k_prevc<<<(u32)((geo.N + 4095) / 4096), 256, 0, s>>>(geo, text, flag, FSL, prevc);
+    else  // caller's device buffer not 16-byte aligned
+        k_prevc1<<<grid, 256, 0, s>>>(geo, text, flag, FSL, prevc);
 }
 
 void launch_bbwt_gather(const Geom& geo, const u32* SA, const u8* prevc, u8* out, hipStream_t s) {

@@ -90,6 +90,8 @@ __device__ inline u32 make_key(const SortArgs& a, u32 p, u32 base, u32 end) {
             u32 c2 = p + 2 < end ? (u32)a.text[p + 2] + 1 : 0;
             return (c0 << 18) | (c1 << 9) | c2;
         }
+        if (a.FEd[p] > 3)  // the 4 rotation characters do not wrap
+            return ((u32)a.text[p] << 24) | ((u32)a.text[p + 1] << 16) | ((u32)a.text[p + 2] << 8) | a.text[p + 3];
         const u64 f = a.FSL[p];
         const u32 fs = (u32)f, m = (u32)(f >> 32);
         u32 t = p - fs, k = 0;
@@ -104,6 +106,7 @@ __device__ inline u32 make_key(const SortArgs& a, u32 p, u32 base, u32 end) {
         const u32 q = p + a.h;
         return q < end ? a.RK[q] - base + 1 : 0;
     }
+    if (a.h < a.FEd[p]) return a.RK[p + a.h] - base;  // no wrap: FSL not needed
     return a.RK[cyc_succ(a, p, a.h)] - base;
 }
 
@@ -115,6 +118,72 @@ __global__ __launch_bounds__(256) void k_keypos(SortArgs a, u32* KP) {
         const u32 b = a.geo.block_of(p);
         KP[p] = make_key(a, p, a.geo.base(b), a.geo.end(b));
     }
+}
+
+// Cyclic keys by position, 16 consecutive positions per thread with 16-byte loads/stores
+// (the grid-stride form above keeps one load per thread in flight).  Positions whose
+// rotation wraps inside the next h (round 0: 4) characters take the factor-record path.
+__global__ __launch_bounds__(256) void k_keypos_cyc(SortArgs a, u32* KP) {
+    a.KP = nullptr;
+    const u32 p0 = (blockIdx.x * 256 + threadIdx.x) * 16;
+    const u32 N = (u32)a.geo.N;
+    if (p0 >= N) return;
+    if (p0 + 16 > N) {  // ragged end of the batch
+        for (u32 p = p0; p < N; ++p) {
+            const u32 b = a.geo.block_of(p);
+            KP[p] = make_key(a, p, a.geo.base(b), a.geo.end(b));
+        }
+        return;
+    }
+    const uint4 dv = *reinterpret_cast<const uint4*>(a.FEd + p0);
+    const u32 dw[4] = {dv.x, dv.y, dv.z, dv.w};
+    u32 key[16];
+    if (a.initial) {
+        // bytes p0 .. p0+19 cover the 4-character windows of the 16 positions
+        const u32* tw = reinterpret_cast<const u32*>(a.text + p0);
+        u32 w[5];
+#pragma unroll
+        // a word that starts before N is inside the allocation (4-byte granular); bytes
+        // past N only feed positions that take the factor-record path (FEd <= 3)
+        for (int i = 0; i < 5; ++i) w[i] = (p0 + 4 * i < N) ? tw[i] : 0u;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const u32 lo = w[e >> 2], hi = w[(e >> 2) + 1];
+            const u32 v = __builtin_amdgcn_alignbyte(hi, lo, e & 3);  // bytes p..p+3, little-endian
+            key[e] = __builtin_bswap32(v);                            // first character most significant
+        }
+    } else {
+        if (p0 + a.h + 16 <= N) {
+            const uint4* rk = reinterpret_cast<const uint4*>(a.RK + p0 + a.h);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint4 r = rk[i];
+                key[4 * i] = r.x;
+                key[4 * i + 1] = r.y;
+                key[4 * i + 2] = r.z;
+                key[4 * i + 3] = r.w;
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) key[e] = p0 + e + a.h < N ? a.RK[p0 + e + a.h] : 0u;
+        }
+    }
+    const u32 b0 = a.geo.block_of(p0), base0 = a.geo.base(b0), end0 = a.geo.end(b0);
+    const u32 need = a.initial ? 3u : a.h;  // fast path iff need < FEd[p]
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const u32 p = p0 + e;
+        const u32 d = (dw[e >> 2] >> (8 * (e & 3))) & 0xFF;
+        if (need < d && p < end0) {
+            if (!a.initial) key[e] -= base0;
+        } else {
+            const u32 b = a.geo.block_of(p);
+            key[e] = make_key(a, p, a.geo.base(b), a.geo.end(b));
+        }
+    }
+    uint4* out = reinterpret_cast<uint4*>(KP + p0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = make_uint4(key[4 * i], key[4 * i + 1], key[4 * i + 2], key[4 * i + 3]);
 }
 
 // ------------------------------------------------------------------------------------
@@ -757,6 +826,10 @@ void launch_classify(const Seg* cur, u32 ncur, const SortArgs& a, const Lists& L
 }
 void launch_keypos(const SortArgs& a, u32* KP, hipStream_t s) {
     if (!a.geo.N) return;
+    if (a.cyclic && a.FEd && ((uintptr_t)a.text & 15) == 0) {
+        k_keypos_cyc<<<cdiv(a.geo.N, 4096), 256, 0, s>>>(a, KP);
+        return;
+    }
     const u32 grid = (u32)std::min<u64>((a.geo.N + 255) / 256, 8192);
     k_keypos<<<grid, 256, 0, s>>>(a, KP);
 }

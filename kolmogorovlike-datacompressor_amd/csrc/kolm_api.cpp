@@ -208,7 +208,7 @@ struct SortOut {
 };
 
 // Segmented prefix-doubling suffix sort of every block of the batch (k_sort.hip).
-SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, const u64* FSL) {
+SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, const u64* FSL, const u8* FEd) {
     hipStream_t s = c->active;
     const u64 N = geo.N;
     SortOut out;
@@ -221,6 +221,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
     a.SA2 = c->get<u32>("SA2", N);
     a.K22 = c->get<u32>("K22", N);
     a.FSL = FSL;
+    a.FEd = FEd;
     a.blk_split = c->get<u32>("blk_split", geo.nb);
     u32* blk_done = c->get<u32>("blk_done", geo.nb);
     a.blk_done = blk_done;
@@ -276,7 +277,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
             // round 0: 4 stable LSD passes over the 4-character keys, no host round trips
             u32* KP = c->get<u32>("KP", N);
             {
-                TScope t(c, KOLM_KT_KEYGEN, "k_keypos", N * 16);
+                TScope t(c, KOLM_KT_KEYGEN, "k_keypos", N * 9);  // FEd 1 + text 4 (overlapping) + KP 4
                 a.KP = nullptr;
                 launch_keypos(a, KP, s);
             }
@@ -315,8 +316,8 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
             a.KP = nullptr;
             if ((u64)h[C_ACTIVE] * 8 > N) {
                 u32* KP = c->get<u32>("KP", N);
-                // cyclic: FSL 8 + RK 4 (or text 4) + KP 4; linear: RK 4 (text 3) + KP 4
-                TScope t(c, KOLM_KT_KEYGEN, "k_keypos", N * (cyclic ? 16 : 8));
+                // cyclic: FEd 1 + RK 4 + KP 4 (FSL only within h of a factor end); linear: RK 4 + KP 4
+                TScope t(c, KOLM_KT_KEYGEN, "k_keypos", N * (cyclic ? 9 : 8));
                 launch_keypos(a, KP, s);
                 a.KP = KP;
             }
@@ -413,7 +414,8 @@ struct Pipeline {
         const u64 N = geo.N;
         const u64 ntiles = (u64)((geo.bs + TILE - 1) / TILE) * geo.nb + 16;
         const u64 nch = (geo.bs + 32767) / 32768 * (u64)geo.nb + 1;  // DUVAL_SPAN
-        launch_lyndon(geo, text, c->get<u8>("flag", N), c->get<u64>("FSL", N), c->get<u32>("lyn_fstart", N),
+        launch_lyndon(geo, text, c->get<u8>("flag", N), c->get<u64>("FSL", N), c->get<u8>("FEd", N),
+                      c->get<u32>("lyn_fstart", N),
                       c->get<u32>("lyn_nfac", nch), c->get<u32>("lyn_stack", N), c->get<u32>("lyn_t1", 2 * ntiles + 16),
                       c->get<u32>("lyn_t2", 2 * ntiles + 2 * geo.nb + 16), c->active, c->kt());
     }
@@ -432,12 +434,12 @@ struct Pipeline {
     u8* cyclic() {
         const u64 N = geo.N;
         u64* FSL = c->get<u64>("FSL", N);
-        SortOut cyc = sort_pass(c, geo, text, true, FSL);
+        SortOut cyc = sort_pass(c, geo, text, true, FSL, c->get<u8>("FEd", N));
         u8* out = c->get<u8>("bbwt", N);
         u8* prevc = c->get<u8>("prevc", N);
         {
-            TScope t(c, KOLM_KT_LYNDON, "k_prevc", N * 10);  // FSL 8 + text 1 + prevc 1 (streaming)
-            launch_prevc(geo, text, FSL, prevc, c->active);
+            TScope t(c, KOLM_KT_LYNDON, "k_prevc", N * 3);  // flag 1 + text 1 + prevc 1 (FSL at factor starts)
+            launch_prevc(geo, text, c->get<u8>("flag", N), FSL, prevc, c->active);
         }
         {
             TScope t(c, KOLM_KT_LYNDON, "k_bbwt_gather", N * 6);  // SA 4 + prevc 1 + out 1

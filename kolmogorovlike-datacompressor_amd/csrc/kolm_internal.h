@@ -158,6 +158,7 @@ struct SortArgs {
     u32* SA2;
     u32* K22;
     const u64* FSL;    // cyclic: start (low 32) | length (high 32) of each position's Lyndon factor
+    const u8* FEd;     // cyclic: min(distance to the factor end, 255): FSL is read only near the end
     u32* blk_split;    // [nb] set to 1 when a group of block b split this round
     const u32* blk_done;  // [nb] cyclic: block converged (no further splits possible)
     int cyclic;
@@ -212,10 +213,10 @@ void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists
 void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, hipStream_t s);
 
 // ---- k_blocks.hip: per-block scans, Lyndon factors, BBWT gather ----
-void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u32* fstart, u32* nfac, u32* stack,
-                   u32* tile_tmp, u32* tile_tmp2, hipStream_t s, KTimer* kt = nullptr);
+void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u8* FEd, u32* fstart, u32* nfac,
+                   u32* stack, u32* tile_tmp, u32* tile_tmp2, hipStream_t s, KTimer* kt = nullptr);
 void launch_lyndon_isa(const Geom& geo, const u32* RK, u8* flag, u32* tile_tmp, u32* tile_tmp2, hipStream_t s);
-void launch_prevc(const Geom& geo, const u8* text, const u64* FSL, u8* prevc, hipStream_t s);
+void launch_prevc(const Geom& geo, const u8* text, const u8* flag, const u64* FSL, u8* prevc, hipStream_t s);
 void launch_bbwt_gather(const Geom& geo, const u32* SA, const u8* prevc, u8* out, hipStream_t s);
 
 // ---- k_lsd.hip: per-block LSD radix passes: 3-gram index for LZ77, cyclic round 0 ----
