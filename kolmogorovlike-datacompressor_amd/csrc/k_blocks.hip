@@ -124,12 +124,22 @@ __global__ __launch_bounds__(WG) void k_tile_starts(TileGeom tg, const u8* flag,
     u32 lo, hi, b;
     const bool ok = tg.range(blockIdx.x, lo, hi, b);
     u32 mx = 0, mn = BIG;
-    if (ok)
-        for (u32 i = lo + threadIdx.x; i < hi; i += WG)
-            if (flag[i]) {
-                mx = max(mx, i);
-                mn = min(mn, i);
+    if (ok) {
+        const u32 i0 = lo + threadIdx.x * PER_THREAD;
+        if ((i0 & 7) == 0 && i0 + PER_THREAD <= hi) {
+            const u64 f8 = *reinterpret_cast<const u64*>(flag + i0);  // 8 flags (0/1 bytes)
+            if (f8) {
+                mn = i0 + ((u32)__ffsll((long long)f8) - 1) / 8;
+                mx = i0 + (63 - (u32)__clzll((long long)f8)) / 8;
             }
+        } else {
+            for (u32 i = i0; i < min(i0 + PER_THREAD, hi); ++i)
+                if (flag[i]) {
+                    mx = max(mx, i);
+                    mn = min(mn, i);
+                }
+        }
+    }
     mx = wave_reduce_max(mx);
     mn = wave_reduce_min(mn);
     if ((threadIdx.x & 63) == 0) {
@@ -151,12 +161,15 @@ __global__ __launch_bounds__(WG) void k_fsfl(TileGeom tg, const u8* flag, const 
     if (!tg.range(blockIdx.x, lo, hi, b)) return;
     const u32 bend = tg.geo.end(b);
     const u32 i0 = lo + threadIdx.x * PER_THREAD;
+    const bool full = (i0 & 7) == 0 && i0 + PER_THREAD <= hi;  // 8-byte flag load, 16-byte stores
+    u64 fl8 = 0;
+    if (full) fl8 = *reinterpret_cast<const u64*>(flag + i0);
     bool f[PER_THREAD];
     u32 lmax = 0, lmin = BIG;
 #pragma unroll
     for (int e = 0; e < PER_THREAD; ++e) {
         const u32 i = i0 + e;
-        f[e] = i < hi && flag[i];
+        f[e] = full ? ((fl8 >> (8 * e)) & 0xFF) != 0 : (i < hi && flag[i]);
         if (f[e]) {
             lmax = max(lmax, i);
             lmin = min(lmin, i);
@@ -170,15 +183,28 @@ __global__ __launch_bounds__(WG) void k_fsfl(TileGeom tg, const u8* flag, const 
         if (f[e]) fs = i0 + e;
         fsv[e] = fs;
     }
+    u64 fslv[PER_THREAD];
+    u64 fed8 = 0;
 #pragma unroll
     for (int e = PER_THREAD - 1; e >= 0; --e) {
         const u32 i = i0 + e;
-        if (i < hi) {
-            const u32 end = fe == BIG ? bend : fe;
-            FSL[i] = (u64)fsv[e] | ((u64)(end - fsv[e]) << 32);  // factor start | length << 32
-            FEd[i] = (u8)min(end - i, 255u);                      // distance to the factor end
+        const u32 end = fe == BIG ? bend : fe;
+        fslv[e] = (u64)fsv[e] | ((u64)(end - fsv[e]) << 32);  // factor start | length << 32
+        const u32 d = min(end - i, 255u);                       // distance to the factor end
+        fed8 |= (u64)d << (8 * e);
+        if (!full && i < hi) {
+            FSL[i] = fslv[e];
+            FEd[i] = (u8)d;
         }
         if (f[e]) fe = i0 + e;
+    }
+    if (full) {
+        uint4* o = reinterpret_cast<uint4*>(FSL + i0);
+#pragma unroll
+        for (int q = 0; q < PER_THREAD / 2; ++q)
+            o[q] = make_uint4((u32)fslv[2 * q], (u32)(fslv[2 * q] >> 32), (u32)fslv[2 * q + 1],
+                              (u32)(fslv[2 * q + 1] >> 32));
+        *reinterpret_cast<u64*>(FEd + i0) = fed8;
     }
 }
 

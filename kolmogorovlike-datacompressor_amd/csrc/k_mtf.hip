@@ -67,62 +67,126 @@ __global__ __launch_bounds__(256) void k_mtf_summary(ChunkGeom cg, const u8* in,
     scnt[c] = cnt;
 }
 
-// one wave (64 threads) per block
-__global__ __launch_bounds__(64) void k_mtf_compose(ChunkGeom cg, const u8* summary, const u16* scnt,
-                                                    u8* states) {
-    __shared__ u32 st[64];      // current state, 256 bytes
-    __shared__ u8 nst[256];     // next state
-    __shared__ u32 member[8];
-    const u32 b = blockIdx.x, lane = threadIdx.x;
-    st[lane] = (4 * lane) | ((4 * lane + 1) << 8) | ((4 * lane + 2) << 16) | ((4 * lane + 3) << 24);
-    __syncthreads();
-    const u64 lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    for (u32 k = 0; k < cg.cpb; ++k) {
+// One wave applies a recency summary (cnt symbols, most recent first) to a 256-entry
+// state held as 64 words in LDS: state' = summary ++ (state minus the summary's symbols),
+// a stable compaction by ballot counts.  All 64 lanes of the wave call it together.
+__device__ inline void mtf_apply(u32* st, u8* nst, u32* member, const u8* sm, u32 cnt) {
+    const u32 lane = threadIdx.x & 63;
+    if (lane < 8) member[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    u32 sv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const u32 i = 4 * lane + j;
+        sv[j] = i < cnt ? sm[i] : 0;
+        if (i < cnt) atomicOr(&member[sv[j] >> 5], 1u << (sv[j] & 31));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const u32 word = st[lane];
+    u32 keep = 0;
+    u8 e[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        e[j] = (word >> (8 * j)) & 0xFF;
+        const bool in_sum = (member[e[j] >> 5] >> (e[j] & 31)) & 1u;
+        keep |= (in_sum ? 0u : 1u) << j;
+    }
+    const u32 nk = __popc(keep);
+    u32 pos = cnt + wave_incl_scan(nk, OpAddU(), 0u) - nk;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const u32 i = 4 * lane + j;
+        if (i < cnt) nst[i] = (u8)sv[j];
+        if ((keep >> j) & 1u) nst[pos++] = e[j];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    st[lane] = reinterpret_cast<const u32*>(nst)[lane];
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Per block, CW waves split the chunks into CW ranges.  Phase 1: each wave composes its
+// range's summaries starting from the identity state; the first d entries of the result
+// (d = distinct symbols of the range) are the range's own recency summary.  Phase 2: wave
+// 0 chains the range summaries into each range's entry state.  Phase 3: each wave
+// re-walks its range from its entry state and publishes the state at every chunk start.
+constexpr int CW = 8;
+__global__ __launch_bounds__(64 * CW) void k_mtf_compose(ChunkGeom cg, const u8* summary, const u16* scnt,
+                                                         u8* states) {
+    __shared__ u32 st[CW][64];
+    __shared__ u8 nst[CW][256];
+    __shared__ u32 member[CW][8];
+    __shared__ u32 uni[CW][8];
+    __shared__ u32 entry[CW][64];
+    __shared__ u32 dist[CW];
+    const u32 b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const u32 ident = (4 * lane) | ((4 * lane + 1) << 8) | ((4 * lane + 2) << 16) | ((4 * lane + 3) << 24);
+    // chunks of this block that exist
+    u32 nch = 0;
+    {
+        const u32 lo0 = cg.geo.base(b), e = cg.geo.end(b);
+        nch = (e - lo0 + MTF_CHUNK - 1) / MTF_CHUNK;
+    }
+    const u32 per = (nch + CW - 1) / CW;
+    const u32 k0 = min(w * per, nch), k1 = min(k0 + per, nch);
+    // phase 1
+    st[w][lane] = ident;
+    if (lane < 8) uni[w][lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (u32 k = k0; k < k1; ++k) {
         const u32 c = b * cg.cpb + k;
-        u32 lo, hi;
-        if (!cg.range(c, lo, hi)) break;
-        // publish the state at chunk start
-        reinterpret_cast<u32*>(states + (u64)c * 256)[lane] = st[lane];
-        const u32 cnt = scnt[c];
-        if (lane < 8) member[lane] = 0;
-        __syncthreads();
         const u8* sm = summary + (u64)c * 256;
-        u32 sv[4];
+        const u32 cnt = scnt[c];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const u32 i = 4 * lane + j;
-            sv[j] = i < cnt ? sm[i] : 0;
-            if (i < cnt) atomicOr(&member[sv[j] >> 5], 1u << (sv[j] & 31));
+            if (i < cnt) atomicOr(&uni[w][sm[i] >> 5], 1u << (sm[i] & 31));
         }
-        __syncthreads();
-        const u32 word = st[lane];
-        u32 keep = 0;
-        u8 e[4];
+        mtf_apply(st[w], nst[w], member[w], sm, cnt);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+        u32 d = 0;
+        for (int q = 0; q < 8; ++q) d += __popc(uni[w][q]);
+        dist[w] = d;
+    }
+    __syncthreads();
+    // phase 2 (wave 0): entry[0] = identity, entry[v] = entry[v-1] after range v-1
+    if (w == 0) {
+        entry[0][lane] = ident;
+        __builtin_amdgcn_wave_barrier();
+        for (u32 v = 1; v < CW; ++v) {
+            // range v-1's summary = first dist[v-1] bytes of its phase-1 state
+            u8 tmp[4];
+            const u32 word = st[v - 1][lane];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            e[j] = (word >> (8 * j)) & 0xFF;
-            const bool in_sum = (member[e[j] >> 5] >> (e[j] & 31)) & 1u;
-            keep |= (in_sum ? 0u : 1u) << j;
+            for (int j = 0; j < 4; ++j) tmp[j] = (word >> (8 * j)) & 0xFF;
+            __builtin_amdgcn_wave_barrier();
+            // copy the summary out of st[v-1] before st[0] changes it (v-1 == 0 case)
+            u8* sumbuf = reinterpret_cast<u8*>(entry[v]);  // scratch: entry[v] is written below
+            for (int j = 0; j < 4; ++j) sumbuf[4 * lane + j] = tmp[j];
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (v == 1) st[0][lane] = ident;  // phase-1 state of range 0 consumed above
+            __builtin_amdgcn_wave_barrier();
+            mtf_apply(st[0], nst[0], member[0], sumbuf, dist[v - 1]);
+            entry[v][lane] = st[0][lane];
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
         }
-        // stable compaction: rank = kept entries before this lane + within lane
-        const u32 nk = __popc(keep);
-        // wave exclusive prefix of nk
-        u32 incl = nk;
-        for (u32 o = 1; o < 64; o <<= 1) {
-            const u32 t = __shfl_up(incl, o);
-            if (lane >= o) incl += t;
-        }
-        u32 pos = cnt + incl - nk;
-        (void)lt_mask;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const u32 i = 4 * lane + j;
-            if (i < cnt) nst[i] = (u8)sv[j];
-            if ((keep >> j) & 1u) nst[pos++] = e[j];
-        }
-        __syncthreads();
-        st[lane] = reinterpret_cast<const u32*>(nst)[lane];
-        __syncthreads();
+    }
+    __syncthreads();
+    // phase 3
+    st[w][lane] = entry[w][lane];
+    __builtin_amdgcn_wave_barrier();
+    for (u32 k = k0; k < k1; ++k) {
+        const u32 c = b * cg.cpb + k;
+        reinterpret_cast<u32*>(states + (u64)c * 256)[lane] = st[w][lane];
+        mtf_apply(st[w], nst[w], member[w], summary + (u64)c * 256, scnt[c]);
     }
 }
 
@@ -195,7 +259,7 @@ void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summar
     }
     {
         KScope k(kt, KT_MTF, "k_mtf_compose", (u64)nchunks * 512);
-        k_mtf_compose<<<geo.nb, 64, 0, s>>>(cg, summary, summary_cnt, states);
+        k_mtf_compose<<<geo.nb, 64 * CW, 0, s>>>(cg, summary, summary_cnt, states);
     }
     {
         KScope k(kt, KT_MTF, "k_mtf_replay", 2 * N + (u64)nchunks * 256);
