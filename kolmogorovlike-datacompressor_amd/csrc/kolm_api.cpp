@@ -673,7 +673,14 @@ int ctx_create(int device, kolm_ctx** out) {
         std::unique_ptr<kolm_ctx> c(new kolm_ctx);
         c->device = device;
         KOLM_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        KOLM_HIP_CHECK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+        {
+            // the sort chain (aux) is the critical path: give it the higher priority so its
+            // workgroups dispatch ahead of the 3-gram index / LZ77 stream (KOLM_PRIO=0: equal)
+            int lo = 0, hi = 0;
+            KOLM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            const bool prio = !getenv("KOLM_PRIO") || atoi(getenv("KOLM_PRIO")) != 0;
+            KOLM_HIP_CHECK(hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, prio ? hi : lo));
+        }
         c->active = c->stream;
         for (auto& e : c->evj) KOLM_HIP_CHECK(hipEventCreate(&e));
         KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_cnt, sizeof(u32) * C_N, hipHostMallocDefault));
