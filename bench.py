@@ -73,6 +73,15 @@ def cpu_baseline(data: bytes, bs: int, budget_s: float):
         _ = int(np.argmin(sizes))
         return len(blk)
 
+    # Re-Pair (id 9) per block, for the full-candidate comparison: the oracle's O(n log n)
+    # restatement (the reference's own O(n * rules) recount is far slower), 1 thread
+    t0 = time.time()
+    nr = 0
+    for i in range(2):
+        oracle.repair_fast(data[(i % nblk) * bs:(i % nblk + 1) * bs])
+        nr += 1
+    rp_s = (time.time() - t0) / nr
+
     # 1 thread
     t0 = time.time()
     n1 = b1 = 0
@@ -98,7 +107,11 @@ def cpu_baseline(data: bytes, bs: int, budget_s: float):
             "sample": f"{bt} x {bs >> 20} MiB blocks on {T} threads ({elt:.1f} s) and {b1} on 1 thread "
                       f"({el1:.1f} s) of the bench stream, candidates 0..8 (5x BBWT, list MTF, bit-serial "
                       f"Rice, exhaustive 4 KiB LZ77), Re-Pair (id 9) excluded as in the GPU path; {model}",
-            "single_thread": {"value": round(n1 / el1 / MB, 5), "cores": 1}}
+            "single_thread": {"value": round(n1 / el1 / MB, 5), "cores": 1},
+            "full_candidates": {
+                "value": round(1.0 / (el1 / max(b1, 1) + rp_s) * (bs / MB) * T, 5), "unit": "MB/s", "cores": T,
+                "sample": f"per-block time of ids 0..8 (1 thread, above) + Re-Pair by the O(n log n) oracle "
+                          f"({rp_s:.2f} s per {bs >> 20} MiB block, 2 blocks), scaled to {T} block-parallel threads"}}
 
 
 def main():
@@ -110,6 +123,8 @@ def main():
     ap.add_argument("--bs", type=int, default=1 << 20, help="block size")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of oracle CPU work (N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--full-steps", type=int, default=2,
+                    help="timed steps of the full candidate list 0..9 (Re-Pair included); 0 = skip")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -133,13 +148,13 @@ def main():
     cap = n + (4 << 20)
     arena = torch.empty(cap, dtype=torch.uint8, device="cuda")
     nb = (n + a.bs - 1) // a.bs
-    sizes = np.zeros((nb, 9), np.uint32)
+    sizes = np.zeros((nb, _lib.KOLM_NCAND), np.uint32)
     method = np.zeros(nb, np.uint32)
     off = np.zeros(nb + 1, np.uint64)
     torch.cuda.synchronize()
 
-    def step(st):
-        _lib.check(L.kolm_encode_blocks_device(ctx, d_in.data_ptr(), n, a.bs, 0x1FF, None, arena.data_ptr(), cap,
+    def step(st, mask=_lib.KOLM_HOTPATH_MASK):
+        _lib.check(L.kolm_encode_blocks_device(ctx, d_in.data_ptr(), n, a.bs, mask, None, arena.data_ptr(), cap,
                                                sizes.ctypes.data, method.ctypes.data, off.ctypes.data,
                                                ctypes.byref(st)))
         if world > 1:
@@ -202,6 +217,40 @@ def main():
             "achieved_GBs": round(alg_step / (ms_step * 1e-3) / 1e9, 2),
             "frac": round(alg_step / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
 
+    # The reference's FULL candidate list (ids 0..9: + exact Re-Pair, its own stream beside
+    # the hot path): same data, same timing discipline; reported beside the hot-path value.
+    full = None
+    if a.full_steps > 0:
+        method_hot = method.copy()
+        off_hot = off.copy()
+        step(_lib.Stats(), _lib.KOLM_DEFAULT_MASK)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fst = []
+        for _ in range(a.full_steps):
+            st = _lib.Stats()
+            step(st, _lib.KOLM_DEFAULT_MASK)
+            fst.append(st.as_dict())
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elf = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([elf], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elf = float(tt[0])
+        f0 = fst[-1]
+        full = {"value": round(world * n * a.full_steps / elf / MB, 2), "unit": "MB/s", "steps": a.full_steps,
+                "ms_per_step": round(elf / a.full_steps * 1e3, 2), "candidates": "0..9 (PY's full list)",
+                "ms_repair": round(f0["ms_repair"], 2), "ratio": round(float(off[-1]) / n, 4),
+                "methods": np.bincount(method, minlength=10).tolist(),
+                "repair_rules_per_block": round(f0["rp_rules"] / nb, 1),
+                "repair_batches_per_block": round(f0["rp_batches"] / nb, 1)}
+        method[:] = method_hot
+        off[:] = off_hot
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(data, a.bs, a.cpu_budget)
@@ -222,7 +271,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "detail": {"ratio": round(float(off[-1]) / n, 4),
-                       "methods": np.bincount(method, minlength=9).tolist(),
+                       "methods": np.bincount(method, minlength=10).tolist(),
+                       "full_candidates": full,
                        "device_ms": {k: round(s0[k], 2) for k in ("ms_total", "ms_sa", "ms_lz", "ms_entropy", "ms_emit")},
                        "rounds": [s0["lin_rounds"], s0["cyc_rounds"]],
                        "pipeline_roofline": pipe,

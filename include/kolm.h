@@ -8,8 +8,9 @@
  *   kolm_lz77_encode       <- encode_lz77(bytes)->(bytes, {})           PY:1686-1763
  *   kolm_bbwt_mtf_rice     <- encode_bbwt_mtf_rice(block, flags, k=2)   PY:2028-2073
  *   kolm_encode_blocks     <- the per-block MDL loop of compress_blocks_fixed
- *                             (candidates 0..8 of _select_encoders, argmin with
+ *                             (candidates 0..9 of _select_encoders, argmin with
  *                             ties -> lowest id)                        PY:2152-2178, 2332-2369
+ *                             candidate 9 = repair_compress            PY:1817-1911
  *   kolm_encode_blocks_device: same, input already resident in device memory
  *                             (bench / multi-GPU path; PY has no equivalent).
  *   kolm_encode_blocks_multi: same as kolm_encode_blocks over several devices of one
@@ -50,8 +51,11 @@ extern "C" {
 #define KOLM_M_BBWT_GRAY 6
 #define KOLM_M_LZ77 7
 #define KOLM_M_LFSR 8
-#define KOLM_NCAND 9           /* ids 0..8 are computed on the GPU */
-#define KOLM_DEFAULT_MASK 0x1FFu
+#define KOLM_M_REPAIR 9
+#define KOLM_NCAND 10          /* ids 0..9 are computed on the GPU (10 = v2_new raises in PY) */
+#define KOLM_DEFAULT_MASK 0x3FFu  /* the reference's full candidate set, ids 0..9 */
+#define KOLM_HOTPATH_MASK 0x1FFu  /* BBWT / MTF+Rice / LZ77 path of the north star, ids 0..8 */
+#define KOLM_REPAIR_MAX_BLOCK (1u << 22)  /* candidate 9 handles blocks up to 4 MiB */
 
 typedef struct kolm_ctx kolm_ctx;
 
@@ -66,7 +70,8 @@ typedef struct kolm_ctx kolm_ctx;
 #define KOLM_KT_SIZES 7      /* k_sizes, k_mdl, k_offsets */
 #define KOLM_KT_EMIT 8       /* emission kernels */
 #define KOLM_KT_LYNDON 9     /* k_duval_*, Lyndon scans, k_prevc, k_bbwt_gather */
-#define KOLM_NKT 10
+#define KOLM_KT_REPAIR 10    /* k_repair (one workgroup per block), k_rp_emit */
+#define KOLM_NKT 11
 
 typedef struct kolm_ktime {
     double ms;          /* summed launch durations (HIP events on the library stream) */
@@ -88,6 +93,10 @@ typedef struct kolm_stats {
     double ms_entropy;        /* of which: BBWT gather + MTF + Rice sizes */
     double ms_emit;           /* of which: MDL + payload emission */
     kolm_ktime kt[KOLM_NKT];  /* per kernel family, filled when timing is enabled */
+    double ms_repair;         /* Re-Pair (candidate 9) on its own stream, overlapping the rest */
+    uint64_t rp_rules;        /* Re-Pair rules over all blocks */
+    uint64_t rp_batches;      /* Re-Pair batches (sequential depth) summed over blocks */
+    uint64_t rp_final;        /* Re-Pair final sequence symbols over all blocks */
 } kolm_stats;
 
 /* ---- library / default context ------------------------------------------------ */
@@ -126,7 +135,7 @@ int kolm_encode_blocks(const uint8_t* data, const uint64_t* starts, const uint32
 /* kolm_encode_blocks over ngpu devices (0..ngpu-1, clamped to the device count and the
  * block count) of this process: fixed blocks of block_size over data[0, total), block i
  * of shard r lives on device r, shards are contiguous block ranges.  Outputs exactly as
- * kolm_encode_blocks (block order; sizes [nblocks*9], method [nblocks], payload_off
+ * kolm_encode_blocks (block order; sizes [nblocks*KOLM_NCAND], method [nblocks], payload_off
  * [nblocks+1]).  stats (optional) sums counts and takes the max of times over devices. */
 int kolm_encode_blocks_multi(int ngpu, const uint8_t* data, uint64_t total, uint32_t block_size,
                              uint32_t cand_mask, const int32_t* force_method, uint32_t* sizes,

@@ -75,7 +75,9 @@ struct kolm_ctx {
     hipStream_t stream = nullptr;  // main stream
     hipStream_t aux = nullptr;     // second stream: Lyndon + cyclic sort chain runs beside LZ77
     hipStream_t active = nullptr;  // stream used by launches / TScope / sync()
+    hipStream_t rp = nullptr;      // third stream: Re-Pair (candidate 9), one workgroup per block
     hipEvent_t evj[4] = {};        // join events
+    hipEvent_t evr[2] = {};        // Re-Pair start / done
     std::mutex mu;
     std::map<std::string, DevBuf> bufs;
     u32* h_cnt = nullptr;  // pinned mirror of the counters
@@ -549,6 +551,34 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
         ~Restore() { c->active = c->stream; }
     } restore{c};
     KOLM_HIP_CHECK(hipEventRecord(ev[0], ms));
+    // Re-Pair (candidate 9): persistent workgroups (one per block) on their own stream,
+    // launched first so they take their CUs while the sort / LZ77 chains queue beside them
+    const bool want_rp = (mask >> KOLM_M_REPAIR) & 1u;
+    RpArgs rpa{};
+    if (want_rp) {
+        if (bs > RP_MAX_N) {
+            set_err("Re-Pair (candidate 9) supports blocks up to 4 MiB (KOLM_REPAIR_MAX_BLOCK)");
+            return KOLM_EARG;
+        }
+        rpa.geo = geo;
+        rpa.text = d_text;
+        rpa.ws_stride = repair_ws_bytes(bs);
+        rpa.out_stride = 4ull * bs + 64;
+        rpa.out = c->get<u8>("rp_out", (u64)nb * rpa.out_stride);
+        rpa.result = c->get<u32>("rp_res", (u64)nb * RP_RS_N);
+        static const u64 budget = (getenv("KOLM_RP_WS_GB") ? (u64)atof(getenv("KOLM_RP_WS_GB")) : 64ull) << 30;
+        const u32 group = (u32)std::max<u64>(1, std::min<u64>(nb, budget / rpa.ws_stride));
+        rpa.ws = c->get<char>("rp_ws", (u64)group * rpa.ws_stride);
+        KOLM_HIP_CHECK(hipStreamWaitEvent(c->rp, ev[0], 0));
+        KOLM_HIP_CHECK(hipEventRecord(c->evr[1], c->rp));
+        c->active = c->rp;
+        for (u32 b0 = 0; b0 < nb; b0 += group) {
+            const u32 k = std::min(group, nb - b0);
+            TScope t(c, KOLM_KT_REPAIR, "k_repair", (u64)(geo.end(b0 + k - 1) - geo.base(b0)) * 9);
+            launch_repair(rpa, b0, k, c->rp);
+        }
+        KOLM_HIP_CHECK(hipEventRecord(c->evr[0], c->rp));
+    }
     KOLM_HIP_CHECK(hipStreamWaitEvent(s, ev[0], 0));
     c->active = s;
     P.lyndon();
@@ -598,14 +628,25 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
     KOLM_HIP_CHECK(hipEventRecord(ev[3], s));
     u32* cnt = c->get<u32>("counters", C_N);
     KOLM_HIP_CHECK(hipMemsetAsync(cnt + C_STATUS, 0, sizeof(u32), s));
+    if (want_rp) KOLM_HIP_CHECK(hipStreamWaitEvent(s, c->evr[0], 0));
     {
         TScope t(c, KOLM_KT_SIZES, "k_mdl+offsets", (u64)nb * 120);
-        launch_mdl(e, want_lz ? z.lz_size : nullptr, cnt + C_STATUS, s);
+        launch_mdl(e, want_lz ? z.lz_size : nullptr, want_rp ? rpa.result : nullptr, cnt + C_STATUS, s);
     }
     std::vector<u64> off(nb + 1);
+    std::vector<u32> rpres(want_rp ? (u64)nb * RP_RS_N : 0);
     KOLM_HIP_CHECK(hipMemcpyAsync(off.data(), e.off, sizeof(u64) * (nb + 1), hipMemcpyDeviceToHost, s));
     KOLM_HIP_CHECK(hipMemcpyAsync(c->h_cnt, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
+    if (want_rp)
+        KOLM_HIP_CHECK(hipMemcpyAsync(rpres.data(), rpa.result, sizeof(u32) * rpres.size(), hipMemcpyDeviceToHost, s));
     c->sync();
+    for (u32 b = 0; b < (want_rp ? nb : 0); ++b)
+        if (rpres[(u64)b * RP_RS_N + RP_RS_ERR]) {
+            char msg[128];
+            snprintf(msg, sizeof msg, "Re-Pair internal error %u in block %u", rpres[(u64)b * RP_RS_N + RP_RS_ERR], b);
+            set_err(msg);
+            return KOLM_EHIP;
+        }
     if (c->h_cnt[C_STATUS] || off[nb] + 4 > arena_cap) {
         set_err("payload arena too small");
         return KOLM_ECAP;
@@ -616,6 +657,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
         launch_emit_simple(e, s);
         launch_emit_rice(e, s);
         if (want_lz) launch_lz_emit(z, e.method, e.off, d_arena, s);
+        if (want_rp) launch_rp_emit(rpa, e.method, e.off, d_arena, s);
     }
     KOLM_HIP_CHECK(hipEventRecord(ev[4], s));
     if (h_sizes)
@@ -641,6 +683,14 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
         st.ms_lz = ev_ms(ej[2], ej[1]);
         st.ms_emit = ev_ms(ev[3], ev[4]);
         st.ms_total = ev_ms(ev[0], ev[4]);
+        if (want_rp) {
+            st.ms_repair = ev_ms(c->evr[1], c->evr[0]);
+            for (u32 b = 0; b < nb; ++b) {
+                st.rp_rules += rpres[(u64)b * RP_RS_N + RP_RS_RULES];
+                st.rp_batches += rpres[(u64)b * RP_RS_N + RP_RS_BATCHES];
+                st.rp_final += rpres[(u64)b * RP_RS_N + RP_RS_FINAL];
+            }
+        }
     }
     return KOLM_OK;
 }
@@ -681,8 +731,10 @@ int ctx_create(int device, kolm_ctx** out) {
             const bool prio = !getenv("KOLM_PRIO") || atoi(getenv("KOLM_PRIO")) != 0;
             KOLM_HIP_CHECK(hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, prio ? hi : lo));
         }
+        KOLM_HIP_CHECK(hipStreamCreateWithFlags(&c->rp, hipStreamNonBlocking));
         c->active = c->stream;
         for (auto& e : c->evj) KOLM_HIP_CHECK(hipEventCreate(&e));
+        for (auto& e : c->evr) KOLM_HIP_CHECK(hipEventCreate(&e));
         KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_cnt, sizeof(u32) * C_N, hipHostMallocDefault));
         for (auto& e : c->ev) KOLM_HIP_CHECK(hipEventCreate(&e));
         *out = c.release();
@@ -728,14 +780,17 @@ int kolm_ctx_destroy(kolm_ctx* c) {
         KOLM_HIP_CHECK(hipSetDevice(c->device));
         KOLM_HIP_CHECK(hipStreamSynchronize(c->stream));
         KOLM_HIP_CHECK(hipStreamSynchronize(c->aux));
+        KOLM_HIP_CHECK(hipStreamSynchronize(c->rp));
         for (auto& kv : c->bufs)
             if (kv.second.p) KOLM_HIP_CHECK(hipFree(kv.second.p));
         for (auto& e : c->ev) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evj) KOLM_HIP_CHECK(hipEventDestroy(e));
+        for (auto& e : c->evr) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evpool) KOLM_HIP_CHECK(hipEventDestroy(e));
         KOLM_HIP_CHECK(hipHostFree(c->h_cnt));
         KOLM_HIP_CHECK(hipStreamDestroy(c->stream));
         KOLM_HIP_CHECK(hipStreamDestroy(c->aux));
+        KOLM_HIP_CHECK(hipStreamDestroy(c->rp));
         delete c;
         return KOLM_OK;
     });
@@ -1015,6 +1070,10 @@ int kolm_encode_blocks_multi(int ngpu, const uint8_t* data, uint64_t total, uint
             agg.ms_lz = std::max(agg.ms_lz, s.ms_lz);
             agg.ms_entropy = std::max(agg.ms_entropy, s.ms_entropy);
             agg.ms_emit = std::max(agg.ms_emit, s.ms_emit);
+            agg.ms_repair = std::max(agg.ms_repair, s.ms_repair);
+            agg.rp_rules += s.rp_rules;
+            agg.rp_batches += s.rp_batches;
+            agg.rp_final += s.rp_final;
             for (int k = 0; k < KOLM_NKT; ++k) {
                 agg.kt[k].ms += s.kt[k].ms;
                 agg.kt[k].launches += s.kt[k].launches;
@@ -1140,7 +1199,7 @@ int kolm_bbwt_mtf_rice(const uint8_t* in, size_t n, int flags, int k, uint8_t* o
         const u64 dcap = 9 * n + 256;
         u8* arena = c->get<u8>("arena", dcap);
         std::vector<u64> off(2);
-        int r = encode_batch(c, d, n, (u32)n, KOLM_DEFAULT_MASK, &force, arena, dcap, nullptr, nullptr,
+        int r = encode_batch(c, d, n, (u32)n, 1u << force, &force, arena, dcap, nullptr, nullptr,
                              off.data(), nullptr);
         if (r) return r;
         if (out_len) *out_len = off[1];

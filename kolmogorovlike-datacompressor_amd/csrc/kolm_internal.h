@@ -25,7 +25,7 @@ constexpr int LZ_WINDOW = 4096;   // PY:1723 WINDOW_MAX
 constexpr int LZ_MIN = 3;         // PY:1724 MIN_MATCH
 constexpr int LZ_CAP = 32;        // per-lane capped compare; longer candidates are extended by the wave
 constexpr int MTF_CHUNK = 1024;   // bytes replayed per thread by the MTF kernel
-constexpr u32 NCAND = 9;          // candidate ids 0..8 computed on the device
+constexpr u32 NCAND = 10;         // candidate ids 0..9 computed on the device
 
 // Segment of the suffix array still to be refined: SA[start .. start+len).  Bit 31 of
 // len (SEG_FIRST) marks a segment that begins at the start of its round group, so its
@@ -253,7 +253,7 @@ struct EmitArgs {
     Geom geo;
     const u8* text;
     const u8* mtf;
-    u32* sizes;        // [nb * 9]
+    u32* sizes;        // [nb * NCAND]
     u64* bits;         // [nb * 8] scratch (bit counters)
     u32* method;       // [nb]
     const int32_t* force;  // [nb] or null
@@ -266,7 +266,7 @@ struct EmitArgs {
     int rice_k;
 };
 void launch_cheap_and_rice_sizes(const EmitArgs& e, hipStream_t s);
-void launch_mdl(const EmitArgs& e, const u32* lz_sizes, u32* status, hipStream_t s);
+void launch_mdl(const EmitArgs& e, const u32* lz_sizes, const u32* rp_result, u32* status, hipStream_t s);
 void launch_emit_simple(const EmitArgs& e, hipStream_t s);
 void launch_emit_rice(const EmitArgs& e, hipStream_t s);
 void launch_rice_only(const Geom& geo, const u8* in, int k, u8* out, u32* tile_tmp, u32* tile_tmp2,
@@ -307,6 +307,23 @@ struct LzArgs {
 };
 void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr);
 void launch_lz_emit(const LzArgs& z, const u32* method, const u64* off, u8* arena, hipStream_t s);
+
+// ---- k_repair.hip: exact Re-Pair (candidate 9), one workgroup per block ----
+constexpr u32 RP_RS_N = 6;       // result words per block (repair_core.h RS_*)
+constexpr u32 RP_RS_SIZE = 0, RP_RS_RULES = 1, RP_RS_FINAL = 2, RP_RS_BATCHES = 3, RP_RS_ERR = 4;
+constexpr u32 RP_MAX_N = 1u << 22;  // block length limit of the device Re-Pair
+struct RpArgs {
+    Geom geo;
+    const u8* text;
+    char* ws;          // workspace of the blocks of one launch group
+    u64 ws_stride;     // repair_ws_bytes(bs)
+    u8* out;           // [nb * out_stride] per-block payload
+    u64 out_stride;    // 4 * bs + 64
+    u32* result;       // [nb * RP_RS_N]
+};
+u64 repair_ws_bytes(u32 bs);
+void launch_repair(const RpArgs& a, u32 b0, u32 nblk, hipStream_t s);
+void launch_rp_emit(const RpArgs& a, const u32* method, const u64* off, u8* arena, hipStream_t s);
 
 }  // namespace kolm
 

@@ -1,0 +1,757 @@
+// Exact Re-Pair of one block by one workgroup (candidate 9, PY:1817-1911 repair_compress).
+//
+// Included by k_repair.hip (the device kernel, Exec = one HIP workgroup of NT threads)
+// and by tools/repair_emu.cpp (a host emulation that runs the same phases thread by
+// thread; test infrastructure for the batch logic only, never part of the product).
+// The includer defines RP_HD (function qualifiers) and provides the Exec policy:
+//   ex.par(f)            f(tid) for every tid in [0, NT), then a workgroup barrier
+//   ex.scan(a, &total)   in-place exclusive scan of a[0..NT) (LDS), total written by all
+//   ex.add/sub/min/max/cas  atomics (u32; cas64 on u64)
+//
+// Reference semantics (PY:1817-1911), restated exactly:
+//   freq(a,b) = number of overlapping adjacent positions holding (a,b); each round picks
+//   the max freq, ties -> lexicographically smallest (a,b); stop when freq < 2; replace
+//   left to right without overlap; stop (no rule) when that replaces fewer than 2.
+//
+// Device formulation (Larsson-Moffat style incremental counts, batched rounds):
+//   * live positions form a doubly linked list (nxt/prv); opair[p] = id of the pair that
+//     starts at live position p; cnt[id] is kept equal to a full recount at all times;
+//     every pair id owns a region of occpos (positions where it was created — it is only
+//     ever created once), validated lazily by opair[p] == id.
+//   * the maximum count never increases (old pairs only lose occurrences; a new pair has
+//     at most as many occurrences as the rule that created it), so rounds run by LEVEL f:
+//     the pairs with count f, sorted by (a,b), are the next rounds in order, except that a
+//     round can (i) lower the count of a later pair whose occurrences touch its own, and
+//     (ii) create a pair (x, X) with count f that sorts before later ones.
+//   * a BATCH is the longest prefix of the next W level pairs whose rounds commute with
+//     the rounds before them: no member's occurrence footprint {prv, i, nxt, nxt2} meets
+//     an earlier member's occurrence span {i, nxt}, no earlier member creates (x, X_k)
+//     with count f and x < a of the member, and no earlier member stops the run.  All
+//     rounds of a batch then execute in parallel with symbols X_k = next + k, which is
+//     the sequential result bit for bit.  Overlapping runs of (a,a) are resolved by
+//     pointer jumping (greedy left-to-right pairing = even distance from the run start).
+#pragma once
+#include <stdint.h>
+
+namespace kolm {
+namespace rp {
+
+using u8 = uint8_t;
+using u32 = uint32_t;
+using u64 = uint64_t;
+
+constexpr u32 NT = 1024;          // threads of the block's workgroup
+constexpr u32 W = 512;            // max rounds (members) per batch
+constexpr u32 CAPR = 1u << 16;    // occurrence-region entries per batch beyond its first member
+constexpr u32 SORT_LDS = 4096;    // level lists up to this size are sorted in LDS
+constexpr u32 NIL = 0xFFFFFFFFu;
+constexpr u32 DEAD = 0xFFFFFFFFu;
+constexpr u64 EMPTY = ~0ull;
+constexpr u32 BMAX = 1u << 22;    // owner tags (BMAX - batch) * W + member: batch < BMAX
+constexpr u32 NBASE = 65536;      // ids of the byte pairs: (a << 8) | b
+constexpr u32 MAX_N = 1u << 22;   // block length limit of the device Re-Pair
+
+enum : u32 { RS_SIZE = 0, RS_RULES, RS_FINAL, RS_BATCHES, RS_ERR, RS_LEVELS, RS_N };
+enum : u32 { RE_OK = 0, RE_CAP = 1, RE_LOOP = 2, RE_LEN = 3 };
+
+// Per-block workspace (all device pointers).  Sizes for a block of length n:
+//   n:      sym nxt prv opair oidx ctag owner  opos omem od0 od1 ot0 ot1 oidl oidr oj op oq
+//   3n+16:  occpos          PC = NBASE + 2n + 16: cnt poff plen pkey, lists (3 x key+id)
+//   HS = pow2 >= n + 64:     hkey hval;  n + 16: husd;  n/2 + 16: rules
+struct Block {
+    const u8* text;
+    u32 n;
+    u32 *sym, *nxt, *prv, *opair, *oidx, *ctag, *owner;
+    u32 *opos, *omem, *od0, *od1, *ot0, *ot1, *oidl, *oidr, *oj, *op, *oq;
+    u32* occpos;
+    u32 *cnt, *poff, *plen;
+    u64* pkey;
+    u64 *lkA, *lkB, *lkL;
+    u32 *liA, *liB, *liL;
+    u64* hkey;
+    u32* hval;
+    u32 hmask;
+    u32* husd;
+    u64* rules;
+    u8* out;
+    u64 out_cap;
+    u32* result;  // RS_N words
+};
+
+struct Shared {
+    u32 m_id[W], m_a[W], m_b[W], m_lpos[W], m_roff[W], m_rlen[W], m_pre[W + 1], m_repl[W], m_lmin[W], m_lmax[W];
+    u32 scan[NT];
+    u32 scan2[NT];
+    u32 wtot[NT / 64];
+    u32 chg[3];
+    u64 skey[SORT_LDS];
+    u32 sval[SORT_LDS];
+    u32 f, lp, lsize, M, V, T, tot, nocc, npairs, next_sym, nrules, pool, batch, hused, nlate;
+    u32 t1, t2, ts, any_aa, stop, maxc, err, total, levels;
+};
+
+// Carve a block's workspace out of `base` (nullptr: size query).  Returns the bytes
+// used; every array is 256-byte aligned.  out/out_cap/result/text/n are set by the caller.
+RP_HD inline u64 workspace_layout(char* base, u32 n, Block& B) {
+    u64 off = 0;
+    auto take = [&](u64 bytes) -> char* {
+        char* p = base ? base + off : nullptr;
+        off += (bytes + 255) & ~(u64)255;
+        return p;
+    };
+    const u64 N = (u64)n + 16, PC = NBASE + 2ull * n + 16;
+    u32 HS = 64;
+    while (HS < n + 64) HS <<= 1;
+    u32** n32[] = {&B.sym, &B.nxt, &B.prv, &B.opair, &B.oidx, &B.ctag, &B.owner, &B.opos, &B.omem, &B.od0,
+                   &B.od1, &B.ot0, &B.ot1, &B.oidl, &B.oidr, &B.oj, &B.op, &B.oq, &B.husd};
+    for (u32** p : n32) *p = (u32*)take(N * 4);
+    B.occpos = (u32*)take(3 * N * 4);
+    B.cnt = (u32*)take(PC * 4);
+    B.poff = (u32*)take(PC * 4);
+    B.plen = (u32*)take(PC * 4);
+    B.pkey = (u64*)take(PC * 8);
+    B.lkA = (u64*)take(PC * 8);
+    B.lkB = (u64*)take(PC * 8);
+    B.lkL = (u64*)take(PC * 8);
+    B.liA = (u32*)take(PC * 4);
+    B.liB = (u32*)take(PC * 4);
+    B.liL = (u32*)take(PC * 4);
+    B.hkey = (u64*)take((u64)HS * 8);
+    B.hval = (u32*)take((u64)HS * 4);
+    B.hmask = HS - 1;
+    B.rules = (u64*)take((N / 2 + 16) * 8);
+    return off;
+}
+
+RP_HD inline u64 pkey_of(u32 a, u32 b) { return ((u64)a << 32) | b; }
+
+RP_HD inline u32 hslot(u64 k, u32 mask) {
+    k ^= k >> 31;
+    k *= 0x9E3779B97F4A7C15ull;
+    k ^= k >> 29;
+    return (u32)k & mask;
+}
+
+RP_HD inline u32 uleb_len(u32 v) { return v < (1u << 7) ? 1 : v < (1u << 14) ? 2 : v < (1u << 21) ? 3 : v < (1u << 28) ? 4 : 5; }
+
+RP_HD inline u32 uleb_put(u8* o, u32 v) {
+    u32 k = 0;
+    for (;;) {
+        const u8 b = v & 0x7F;
+        v >>= 7;
+        if (v) {
+            o[k++] = b | 0x80;
+        } else {
+            o[k++] = b;
+            return k;
+        }
+    }
+}
+
+template <class E>
+RP_HD inline void hash_insert(E& ex, const Block& B, Shared& sh, u64 key) {
+    u32 s = hslot(key, B.hmask);
+    for (;;) {
+        const u64 cur = B.hkey[s];
+        if (cur == key) return;
+        if (cur == EMPTY) {
+            const u64 old = ex.cas64(&B.hkey[s], EMPTY, key);
+            if (old == EMPTY) {
+                const u32 u = ex.add(&sh.hused, 1u);
+                B.husd[u] = s;
+                return;
+            }
+            if (old == key) return;
+        }
+        s = (s + 1) & B.hmask;
+    }
+}
+
+RP_HD inline u32 hash_find(const Block& B, u64 key) {
+    u32 s = hslot(key, B.hmask);
+    while (B.hkey[s] != key) s = (s + 1) & B.hmask;
+    return B.hval[s];
+}
+
+// Sort key/id[0..n) ascending by key (keys unique); tk/ti is scratch of the same size.
+// Result is left in k/i.
+template <class E>
+RP_HD inline void sort_list(E& ex, Shared& sh, u64* k, u32* id, u64* tk, u32* ti, u32 n) {
+    // 1. runs of SORT_LDS sorted in LDS (bitonic)
+    for (u32 base = 0; base < n; base += SORT_LDS) {
+        const u32 len = n - base < SORT_LDS ? n - base : SORT_LDS;
+        u32 S = 2;
+        while (S < len) S <<= 1;
+        ex.par([&](u32 t) {
+            for (u32 e = t; e < S; e += NT) {
+                sh.skey[e] = e < len ? k[base + e] : EMPTY;
+                sh.sval[e] = e < len ? id[base + e] : NIL;
+            }
+        });
+        for (u32 kk = 2; kk <= S; kk <<= 1) {
+            for (u32 j = kk >> 1; j > 0; j >>= 1) {
+                ex.par([&](u32 t) {
+                    for (u32 e = t; e < S; e += NT) {
+                        const u32 l = e ^ j;
+                        if (l > e) {
+                            const bool asc = (e & kk) == 0;
+                            const u64 x = sh.skey[e], y = sh.skey[l];
+                            if (asc ? x > y : x < y) {
+                                sh.skey[e] = y;
+                                sh.skey[l] = x;
+                                const u32 v = sh.sval[e];
+                                sh.sval[e] = sh.sval[l];
+                                sh.sval[l] = v;
+                            }
+                        }
+                    }
+                });
+            }
+        }
+        ex.par([&](u32 t) {
+            for (u32 e = t; e < len; e += NT) {
+                k[base + e] = sh.skey[e];
+                id[base + e] = sh.sval[e];
+            }
+        });
+    }
+    // 2. merge passes (merge path by binary search; keys are unique)
+    u64* ka = k;
+    u32* ia = id;
+    u64* kb = tk;
+    u32* ib = ti;
+    for (u32 run = SORT_LDS; run < n; run <<= 1) {
+        ex.par([&](u32 t) {
+            for (u32 e = t; e < n; e += NT) {
+                const u32 pairbase = e / (2 * run) * (2 * run);
+                const u32 mid = pairbase + run < n ? pairbase + run : n;
+                const u32 end = pairbase + 2 * run < n ? pairbase + 2 * run : n;
+                const u64 key = ka[e];
+                u32 lo, hi;
+                if (e < mid) {
+                    lo = mid;
+                    hi = end;
+                } else {
+                    lo = pairbase;
+                    hi = mid;
+                }
+                const u32 s0 = lo;
+                while (lo < hi) {
+                    const u32 m = (lo + hi) >> 1;
+                    if (ka[m] < key) lo = m + 1; else hi = m;
+                }
+                const u32 rank = lo - s0;
+                const u32 dst = e < mid ? e + rank : pairbase + (e - mid) + rank;
+                kb[dst] = key;
+                ib[dst] = ia[e];
+            }
+        });
+        u64* tkk = ka; ka = kb; kb = tkk;
+        u32* tii = ia; ia = ib; ib = tii;
+    }
+    if (ka != k) {
+        ex.par([&](u32 t) {
+            for (u32 e = t; e < n; e += NT) {
+                k[e] = ka[e];
+                id[e] = ia[e];
+            }
+        });
+    }
+}
+
+template <class E>
+RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
+    const u32 n = B.n;
+    const u32 HS = B.hmask + 1;
+    // ---------------- init: linked list, byte-pair counts and regions ----------------
+    ex.par([&](u32 t) {
+        for (u32 i = t; i < NBASE; i += NT) {
+            B.cnt[i] = 0;
+            B.plen[i] = 0;
+            B.pkey[i] = pkey_of(i >> 8, i & 255);
+        }
+        for (u32 i = t; i < HS; i += NT) B.hkey[i] = EMPTY;
+        if (t == 0) {
+            sh.pool = 0; sh.npairs = NBASE; sh.next_sym = 256; sh.nrules = 0; sh.batch = 0;
+            sh.lp = 0; sh.lsize = 0; sh.f = 0; sh.hused = 0; sh.nlate = 0; sh.err = RE_OK; sh.levels = 0;
+            sh.stop = 0;
+        }
+    });
+    ex.par([&](u32 t) {
+        for (u32 i = t; i < n; i += NT) {
+            B.sym[i] = B.text[i];
+            B.nxt[i] = i + 1 < n ? i + 1 : NIL;
+            B.prv[i] = i ? i - 1 : NIL;
+            B.ctag[i] = NIL;
+            B.owner[i] = NIL;
+            if (i + 1 < n) {
+                const u32 code = ((u32)B.text[i] << 8) | B.text[i + 1];
+                B.opair[i] = code;
+                ex.add(&B.cnt[code], 1u);
+            } else {
+                B.opair[i] = NIL;
+            }
+        }
+    });
+    ex.par([&](u32 t) {
+        for (u32 c = t; c < NBASE; c += NT)
+            if (B.cnt[c]) B.poff[c] = ex.add(&sh.pool, B.cnt[c]);
+    });
+    ex.par([&](u32 t) {
+        for (u32 i = t; i + 1 < n; i += NT) {
+            const u32 code = B.opair[i];
+            B.occpos[B.poff[code] + ex.add(&B.plen[code], 1u)] = i;
+        }
+    });
+    u64* lk = B.lkA;
+    u32* li = B.liA;
+    u64* tk = B.lkB;
+    u32* ti = B.liB;
+    u32 guard = 0;
+    // ---------------- batches ----------------
+    for (;;) {
+        if (++guard > 4 * n + 64) {  // unreachable: every batch retires >= 1 round or 1 level entry
+            ex.par([&](u32 t) { if (t == 0) sh.err = RE_LOOP; });
+            break;
+        }
+        if (sh.lp >= sh.lsize) {
+            // new level: f = max count; the level list = pairs with count f, sorted
+            ex.par([&](u32 t) { if (t == 0) sh.maxc = 0; });
+            ex.par([&](u32 t) {
+                u32 m = 0;
+                for (u32 id = t; id < sh.npairs; id += NT) m = B.cnt[id] > m ? B.cnt[id] : m;
+                if (m) ex.max(&sh.maxc, m);
+            });
+            if (sh.maxc < 2) break;
+            ex.par([&](u32 t) {
+                if (t == 0) { sh.f = sh.maxc; sh.lsize = 0; sh.lp = 0; sh.levels++; }
+            });
+            ex.par([&](u32 t) {
+                for (u32 id = t; id < sh.npairs; id += NT)
+                    if (B.cnt[id] == sh.f) {
+                        const u32 k = ex.add(&sh.lsize, 1u);
+                        lk[k] = B.pkey[id];
+                        li[k] = id;
+                    }
+            });
+            sort_list(ex, sh, lk, li, tk, ti, sh.lsize);
+        }
+        const u32 f = sh.f;
+        const u32 batch = sh.batch;
+        // ---- window: the next valid level entries (count still f), in list order ----
+        ex.par([&](u32 t) {
+            const u32 idx = sh.lp + t;
+            sh.scan[t] = idx < sh.lsize && B.cnt[li[idx]] == f ? 1u : 0u;
+        });
+        ex.scan(sh.scan, &sh.V);
+        ex.par([&](u32 t) {
+            const u32 idx = sh.lp + t;
+            if (idx < sh.lsize && B.cnt[li[idx]] == f) {
+                const u32 r = sh.scan[t];
+                if (r < W) {
+                    const u32 id = li[idx];
+                    const u64 key = lk[idx];
+                    sh.m_id[r] = id;
+                    sh.m_a[r] = (u32)(key >> 32);
+                    sh.m_b[r] = (u32)key;
+                    sh.m_lpos[r] = idx;
+                    sh.m_roff[r] = B.poff[id];
+                    sh.m_rlen[r] = B.plen[id];
+                    sh.m_repl[r] = 0;
+                    sh.m_lmin[r] = NIL;
+                    sh.m_lmax[r] = 0;
+                }
+            }
+        });
+        if (sh.V == 0) {
+            ex.par([&](u32 t) {
+                if (t == 0) sh.lp = sh.lp + NT < sh.lsize ? sh.lp + NT : sh.lsize;
+            });
+            continue;
+        }
+        ex.par([&](u32 t) {
+            if (t == 0) {
+                u32 M = sh.V < W ? sh.V : W, pre = 0, aa = 0;
+                for (u32 m = 0; m < M; ++m) {
+                    if (m > 0 && pre + sh.m_rlen[m] > CAPR) {
+                        M = m;
+                        break;
+                    }
+                    sh.m_pre[m] = pre;
+                    pre += sh.m_rlen[m];
+                    aa |= sh.m_a[m] == sh.m_b[m] ? 1u : 0u;
+                }
+                sh.m_pre[M] = pre;
+                sh.M = M;
+                sh.tot = pre;
+                sh.any_aa = aa;
+                sh.nocc = 0;
+                sh.t1 = NIL;
+                sh.t2 = NIL;
+                sh.ts = NIL;
+                sh.hused = 0;
+                sh.nlate = 0;
+            }
+        });
+        const u32 M = sh.M;
+        // ---- gather the members' live occurrences ----
+        ex.par([&](u32 t) {
+            for (u32 e = t; e < sh.tot; e += NT) {
+                u32 lo = 0, hi = M;  // member m: m_pre[m] <= e < m_pre[m+1]
+                while (hi - lo > 1) {
+                    const u32 md = (lo + hi) >> 1;
+                    if (sh.m_pre[md] <= e) lo = md; else hi = md;
+                }
+                const u32 pos = B.occpos[sh.m_roff[lo] + (e - sh.m_pre[lo])];
+                if (B.opair[pos] == sh.m_id[lo]) {
+                    const u32 o = ex.add(&sh.nocc, 1u);
+                    B.opos[o] = pos;
+                    B.omem[o] = lo;
+                    B.oidx[pos] = o;
+                }
+            }
+        });
+        const u32 nocc = sh.nocc;
+        // ---- runs of (a,a): distance from the run start by pointer jumping ----
+        u32* dist = B.od0;
+        if (sh.any_aa) {
+            ex.par([&](u32 t) {
+                for (u32 o = t; o < nocc; o += NT) {
+                    const u32 m = B.omem[o], pos = B.opos[o];
+                    u32 pp = NIL;
+                    if (sh.m_a[m] == sh.m_b[m]) {
+                        const u32 p = B.prv[pos];
+                        if (p != NIL && B.opair[p] == sh.m_id[m]) pp = B.oidx[p];
+                    }
+                    B.ot0[o] = pp;
+                    B.od0[o] = pp != NIL ? 1u : 0u;
+                }
+            });
+            u32 *d0 = B.od0, *d1 = B.od1, *p0 = B.ot0, *p1 = B.ot1;
+            // three rotating flags: iteration k sets chg[k%3] and clears chg[(k+1)%3], which
+            // was last read two iterations ago (a barrier in between)
+            ex.par([&](u32 t) { if (t == 0) { sh.chg[0] = 0; sh.chg[1] = 0; sh.chg[2] = 0; } });
+            for (u32 it = 0;; ++it) {
+                const u32 c = it % 3;
+                ex.par([&](u32 t) {
+                    if (t == 0) sh.chg[(c + 1) % 3] = 0;
+                    bool any = false;
+                    for (u32 o = t; o < nocc; o += NT) {
+                        const u32 p = p0[o];
+                        if (p != NIL) {
+                            d1[o] = d0[o] + d0[p];
+                            p1[o] = p0[p];
+                            any = true;
+                        } else {
+                            d1[o] = d0[o];
+                            p1[o] = NIL;
+                        }
+                    }
+                    if (any) ex.max(&sh.chg[c], 1u);
+                });
+                u32* x = d0; d0 = d1; d1 = x;
+                x = p0; p0 = p1; p1 = x;
+                if (!sh.chg[c]) break;
+            }
+            dist = d0;
+        } else {
+            ex.par([&](u32 t) {
+                for (u32 o = t; o < nocc; o += NT) B.od0[o] = 0;
+            });
+        }
+        // ---- chosen occurrences: tags, replacement counts, span owners ----
+        const u32 ctag0 = batch * W;
+        const u32 otag0 = (BMAX - batch) * W;
+        ex.par([&](u32 t) {
+            for (u32 o = t; o < nocc; o += NT) {
+                if (dist[o] & 1u) continue;
+                const u32 m = B.omem[o], i = B.opos[o];
+                B.ctag[i] = ctag0 + m;
+                ex.add(&sh.m_repl[m], 1u);
+                ex.min(&B.owner[i], otag0 + m);
+                ex.min(&B.owner[B.nxt[i]], otag0 + m);
+            }
+        });
+        // ---- conflicts (footprint vs earlier spans), left-neighbour uniformity ----
+        ex.par([&](u32 t) {
+            for (u32 o = t; o < nocc; o += NT) {
+                if (dist[o] & 1u) continue;
+                const u32 m = B.omem[o], i = B.opos[o];
+                const u32 p = B.prv[i], j = B.nxt[i], q = B.nxt[j];
+                bool conf = false;
+                const u32 lo = otag0, hi = otag0 + m;  // owner in [lo, hi) = earlier member this batch
+                const u32 w0 = B.owner[i], w1 = B.owner[j];
+                conf |= w0 >= lo && w0 < hi;
+                conf |= w1 >= lo && w1 < hi;
+                if (p != NIL) {
+                    const u32 w = B.owner[p];
+                    conf |= w >= lo && w < hi;
+                }
+                if (q != NIL) {
+                    const u32 w = B.owner[q];
+                    conf |= w >= lo && w < hi;
+                }
+                if (conf) ex.min(&sh.t1, m);
+                const bool leftc = p != NIL && B.prv[p] != NIL && B.ctag[B.prv[p]] == ctag0 + m;
+                const u32 x = (p != NIL && !leftc) ? B.sym[p] : NIL;
+                ex.min(&sh.m_lmin[m], x);
+                ex.max(&sh.m_lmax[m], x);
+            }
+        });
+        ex.par([&](u32 t) {
+            for (u32 m = t; m < M; m += NT) {
+                if (sh.m_repl[m] < 2) ex.min(&sh.ts, m);
+                // (x, X_m) with count f sorts before every later member with a > x
+                if (sh.m_lmin[m] == sh.m_lmax[m] && sh.m_lmin[m] != NIL && sh.m_repl[m] == f) {
+                    const u32 x = sh.m_lmin[m];
+                    u32 lo = m + 1, hi = M;
+                    while (lo < hi) {
+                        const u32 md = (lo + hi) >> 1;
+                        if (sh.m_a[md] > x) hi = md; else lo = md + 1;
+                    }
+                    if (lo < M) ex.min(&sh.t2, lo);
+                }
+            }
+        });
+        ex.par([&](u32 t) {
+            if (t == 0) {
+                u32 T = M;
+                T = sh.t1 < T ? sh.t1 : T;
+                T = sh.t2 < T ? sh.t2 : T;
+                T = sh.ts < T ? sh.ts : T;
+                sh.T = T;
+                sh.stop = (sh.ts != NIL && sh.ts < sh.t1 && sh.ts < sh.t2) ? 1u : 0u;
+            }
+        });
+        const u32 T = sh.T;
+        if (T == 0) break;  // the next round replaces < 2 occurrences (PY:1879-1882)
+        const u32 X0 = sh.next_sym;
+        // ---- apply 1: destroy old pair occurrences, register the new pair keys ----
+        ex.par([&](u32 t) {
+            for (u32 o = t; o < nocc; o += NT) {
+                if (dist[o] & 1u) continue;
+                const u32 m = B.omem[o];
+                if (m >= T) continue;
+                const u32 i = B.opos[o], p = B.prv[i], j = B.nxt[i], q = B.nxt[j];
+                const bool leftc = p != NIL && B.prv[p] != NIL && B.ctag[B.prv[p]] == ctag0 + m;
+                const bool rightc = q != NIL && B.ctag[q] == ctag0 + m;
+                B.oj[o] = j;
+                B.op[o] = leftc ? NIL : p;
+                B.oq[o] = q;
+                ex.sub(&B.cnt[B.opair[i]], 1u);
+                if (q != NIL) ex.sub(&B.cnt[B.opair[j]], 1u);
+                if (p != NIL && !leftc) ex.sub(&B.cnt[B.opair[p]], 1u);
+                const u32 X = X0 + m;
+                if (q != NIL) {
+                    const u32 r = rightc ? X : B.sym[q];
+                    B.oidr[o] = r;  // right symbol (ids come after the barrier)
+                    hash_insert(ex, B, sh, pkey_of(X, r));
+                }
+                if (p != NIL && !leftc) {
+                    B.oidl[o] = B.sym[p];
+                    hash_insert(ex, B, sh, pkey_of(B.sym[p], X));
+                }
+            }
+        });
+        // ---- apply 2: ids for the new pairs ----
+        ex.par([&](u32 t) {
+            for (u32 u = t; u < sh.hused; u += NT) {
+                const u32 s = B.husd[u], id = sh.npairs + u;
+                B.hval[s] = id;
+                B.pkey[id] = B.hkey[s];
+                B.cnt[id] = 0;
+                B.plen[id] = 0;
+            }
+        });
+        // ---- apply 3: count the new pair occurrences ----
+        ex.par([&](u32 t) {
+            for (u32 o = t; o < nocc; o += NT) {
+                if (dist[o] & 1u) continue;
+                const u32 m = B.omem[o];
+                if (m >= T) continue;
+                const u32 X = X0 + m;
+                if (B.oq[o] != NIL) {
+                    const u32 id = hash_find(B, pkey_of(X, B.oidr[o]));
+                    B.oidr[o] = id;
+                    ex.add(&B.cnt[id], 1u);
+                }
+                if (B.op[o] != NIL) {
+                    const u32 id = hash_find(B, pkey_of(B.oidl[o], X));
+                    B.oidl[o] = id;
+                    ex.add(&B.cnt[id], 1u);
+                }
+            }
+        });
+        // ---- apply 4: rewrite the sequence ----
+        ex.par([&](u32 t) {
+            for (u32 o = t; o < nocc; o += NT) {
+                if (dist[o] & 1u) continue;
+                const u32 m = B.omem[o];
+                if (m >= T) continue;
+                const u32 i = B.opos[o], j = B.oj[o], q = B.oq[o], p = B.op[o];
+                B.sym[i] = X0 + m;
+                B.nxt[i] = q;
+                if (q != NIL) B.prv[q] = i;
+                B.sym[j] = DEAD;
+                B.opair[j] = NIL;
+                B.opair[i] = q != NIL ? B.oidr[o] : NIL;
+                if (p != NIL) B.opair[p] = B.oidl[o];
+            }
+            for (u32 u = t; u < sh.hused; u += NT) {
+                const u32 id = sh.npairs + u;
+                B.poff[id] = ex.add(&sh.pool, B.cnt[id]);
+                if (B.cnt[id] == f) {
+                    const u32 k = ex.add(&sh.nlate, 1u);
+                    B.lkL[k] = B.pkey[id];
+                    B.liL[k] = id;
+                }
+            }
+            for (u32 m = t; m < T; m += NT) B.rules[sh.nrules + m] = pkey_of(sh.m_a[m], sh.m_b[m]);
+        });
+        // ---- apply 5: occurrence regions of the new pairs ----
+        ex.par([&](u32 t) {
+            for (u32 o = t; o < nocc; o += NT) {
+                if (dist[o] & 1u) continue;
+                const u32 m = B.omem[o];
+                if (m >= T) continue;
+                if (B.oq[o] != NIL) {
+                    const u32 id = B.oidr[o];
+                    B.occpos[B.poff[id] + ex.add(&B.plen[id], 1u)] = B.opos[o];
+                }
+                if (B.op[o] != NIL) {
+                    const u32 id = B.oidl[o];
+                    B.occpos[B.poff[id] + ex.add(&B.plen[id], 1u)] = B.op[o];
+                }
+            }
+            for (u32 u = t; u < sh.hused; u += NT) B.hkey[B.husd[u]] = EMPTY;
+            if (t == 0) {
+                sh.lp = sh.m_lpos[T - 1] + 1;
+                sh.next_sym += T;
+                sh.nrules += T;
+                sh.npairs += sh.hused;
+                sh.batch += 1;
+            }
+        });
+        if (sh.nlate) {
+            // new pairs with count f join the level list at their key position
+            const u32 nl = sh.nlate;
+            sort_list(ex, sh, B.lkL, B.liL, tk, ti, nl);
+            const u32 r0 = sh.lp, rn = sh.lsize - sh.lp;
+            ex.par([&](u32 t) {
+                for (u32 e = t; e < rn + nl; e += NT) {
+                    u64 key;
+                    u32 idv, lo, hi, base;
+                    const u64* other;
+                    if (e < rn) {
+                        key = lk[r0 + e];
+                        idv = li[r0 + e];
+                        other = B.lkL;
+                        lo = 0;
+                        hi = nl;
+                        base = e;
+                    } else {
+                        key = B.lkL[e - rn];
+                        idv = B.liL[e - rn];
+                        other = lk + r0;
+                        lo = 0;
+                        hi = rn;
+                        base = e - rn;
+                    }
+                    while (lo < hi) {
+                        const u32 md = (lo + hi) >> 1;
+                        if (other[md] < key) lo = md + 1; else hi = md;
+                    }
+                    tk[base + lo] = key;
+                    ti[base + lo] = idv;
+                }
+                if (t == 0) {
+                    sh.lsize = rn + nl;
+                    sh.lp = 0;
+                    sh.nlate = 0;
+                }
+            });
+            u64* xk = lk; lk = tk; tk = xk;
+            u32* xi = li; li = ti; ti = xi;
+        }
+        if (sh.stop) break;
+        if (sh.next_sym - 256 > n) {  // impossible for a correct run (each rule removes >= 2 symbols)
+            ex.par([&](u32 t) { if (t == 0) sh.err = RE_LOOP; });
+            break;
+        }
+    }
+    // ---------------- serialise (PY:1889-1903): RP, 256, nrules, rules, len, seq ----------------
+    const u32 R = sh.nrules;
+    // final sequence length and ULEB bytes of the live symbols, per contiguous thread range
+    const u32 cp = (n + NT - 1) / NT;
+    ex.par([&](u32 t) {
+        u32 bytes = 0, live = 0;
+        const u32 e = (t + 1) * cp < n ? (t + 1) * cp : n;
+        for (u32 i = t * cp; i < e; ++i)
+            if (B.sym[i] != DEAD) {
+                bytes += uleb_len(B.sym[i]);
+                ++live;
+            }
+        sh.scan[t] = bytes;
+        sh.scan2[t] = live;
+    });
+    ex.scan(sh.scan, &sh.total);
+    const u32 seq_bytes = sh.total;
+    ex.par([&](u32 t) {
+        const u32 v = sh.scan[t];
+        sh.scan[t] = sh.scan2[t];
+        sh.scan2[t] = v;  // byte offset of thread t's symbols
+    });
+    ex.scan(sh.scan, &sh.total);
+    const u32 L = sh.total;
+    const u32 cr = (R + NT - 1) / NT;
+    ex.par([&](u32 t) {
+        u32 bytes = 0;
+        const u32 e = (t + 1) * cr < R ? (t + 1) * cr : R;
+        for (u32 r = t * cr; r < e; ++r) bytes += uleb_len((u32)(B.rules[r] >> 32)) + uleb_len((u32)B.rules[r]);
+        sh.scan[t] = bytes;
+    });
+    ex.scan(sh.scan, &sh.total);
+    const u32 rule_bytes = sh.total;
+    const u32 head = 2 + 2 + uleb_len(R);
+    const u64 size = (u64)head + rule_bytes + uleb_len(L) + seq_bytes;
+    const bool fits = size <= B.out_cap && sh.err == RE_OK;
+    if (fits) {
+        ex.par([&](u32 t) {
+            if (t == 0) {
+                u8* o = B.out;
+                o[0] = 'R';
+                o[1] = 'P';
+                u32 k = 2 + uleb_put(o + 2, 256);
+                uleb_put(o + k, R);
+                uleb_put(o + head + rule_bytes, L);
+            }
+            {
+                u8* o = B.out + head + sh.scan[t];
+                const u32 e = (t + 1) * cr < R ? (t + 1) * cr : R;
+                for (u32 r = t * cr; r < e; ++r) {
+                    o += uleb_put(o, (u32)(B.rules[r] >> 32));
+                    o += uleb_put(o, (u32)B.rules[r]);
+                }
+            }
+            {
+                u8* o = B.out + head + rule_bytes + uleb_len(L) + sh.scan2[t];
+                const u32 e = (t + 1) * cp < n ? (t + 1) * cp : n;
+                for (u32 i = t * cp; i < e; ++i)
+                    if (B.sym[i] != DEAD) o += uleb_put(o, B.sym[i]);
+            }
+        });
+    }
+    ex.par([&](u32 t) {
+        if (t == 0) {
+            B.result[RS_SIZE] = (u32)size;
+            B.result[RS_RULES] = R;
+            B.result[RS_FINAL] = L;
+            B.result[RS_BATCHES] = sh.batch;
+            B.result[RS_ERR] = sh.err != RE_OK ? sh.err : (fits ? RE_OK : RE_CAP);
+            B.result[RS_LEVELS] = sh.levels;
+        }
+    });
+}
+
+}  // namespace rp
+}  // namespace kolm

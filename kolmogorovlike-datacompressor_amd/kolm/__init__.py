@@ -9,7 +9,7 @@ Drop-in for the reference's block API (PY = final_researched/kolm_final_research
     encode_bbwt_mtf_rice, encode_raw, encode_xor,
     encode_lfsr_predict, fixed_boundaries, uleb128_encode      (same names / meaning)
 
-Every encode-side computation of candidates 0..8 runs as hand-written HIP kernels on
+Every encode-side computation of candidates 0..9 runs as hand-written HIP kernels on
 the GPU (libkolm_hip.so through ctypes, include/kolm.h); the per-block MDL loop of PY
 is one batched device call for all blocks.  There is no CPU fallback: without the
 library or a HIP device the encode functions raise ``KolmUnavailable``.
@@ -17,9 +17,11 @@ library or a HIP device the encode functions raise ``KolmUnavailable``.
 Candidate ids are the reference's (the list index is the on-disk method id):
 0 raw, 1 xor, 2 bbwt, 3 bbwt_bp, 4 bbwt_nib, 5 bbwt_br, 6 bbwt_gray, 7 lz77,
 8 lfsr_pred, 9 repair, 10 v2_new.  v2_new always raises in PY (NameError)
-and is never selected; repair (9) is not offloaded yet — its registry
-entry raises like a failing reference encoder, so the MDL argmin runs over ids 0..8 with
-ids unchanged (containers stay decodable by the reference).
+and is never selected, so the MDL argmin runs over ids 0..9 exactly as PY's does and
+compress_blocks_fixed() returns PY's container byte for byte.  Re-Pair (9) is the exact
+batched device Re-Pair of csrc/repair_core.h (blocks up to 4 MiB).  ``hot_path=True``
+restricts the candidates to ids 0..8 (the BBWT / MTF+Rice / LZ77 path of the north star;
+ids unchanged, containers still decodable by the reference).
 """
 from __future__ import annotations
 
@@ -35,13 +37,13 @@ from .decode import decode_block
 __all__ = [
     "compress_blocks_fixed", "decompress", "fixed_boundaries", "bbwt_forward", "mtf_encode",
     "rice_encode", "encode_lz77", "encode_bbwt_mtf_rice", "encode_raw", "encode_xor",
-    "encode_lfsr_predict", "uleb128_encode", "uleb128_decode_stream", "CANDIDATE_NAMES",
+    "encode_lfsr_predict", "repair_compress", "uleb128_encode", "uleb128_decode_stream", "CANDIDATE_NAMES",
     "KolmUnavailable", "KolmError", "last_stats",
 ]
 
 CANDIDATE_NAMES = ["raw", "xor", "bbwt", "bbwt_bp", "bbwt_nib", "bbwt_br", "bbwt_gray", "lz77",
                    "lfsr_pred", "repair", "v2_new"]
-GPU_CANDIDATES = 9
+GPU_CANDIDATES = 10
 
 # CLI-style switches of the reference (PY:92-96); ids stay stable (CPP:3750-3775 semantics)
 G_NO_LZ77: bool = False
@@ -119,7 +121,7 @@ def encode_bbwt_mtf_rice(block: bytes, use_bitplane: bool = False, use_lfsr: boo
 def _batched_single(block: bytes, mid: int) -> bytes:
     if not block:
         return b""
-    _, _, payloads, _ = _lib.encode_blocks(bytes(block), len(block), force=[mid])
+    _, _, payloads, _ = _lib.encode_blocks(bytes(block), len(block), cand_mask=1 << mid, force=[mid])
     return payloads[0]
 
 
@@ -135,8 +137,17 @@ def encode_lfsr_predict(block: bytes) -> Tuple[bytes, Dict[str, Any]]:  # PY:198
     return _batched_single(block, 8), {}
 
 
-def _not_offloaded(block: bytes):
-    raise NotImplementedError("repair (method 9) is not offloaded yet (SURVEY §8f row 1)")
+def repair_compress(block: bytes) -> Tuple[bytes, Dict[str, Any]]:
+    """Strict Re-Pair grammar, ULEB-serialised (PY:1841-1911), on the GPU.  The reference's
+    meta dict carries its rule table for introspection; here it carries the counts."""
+    block = bytes(block)
+    if not block:
+        from .container import uleb128_encode as _u
+        return b"RP" + _u(256) + _u(0) + _u(0), {"rules": {}, "final_len": 0}
+    if len(block) > _lib.KOLM_REPAIR_MAX_BLOCK:
+        raise ValueError("repair: blocks up to 4 MiB are supported on the device")
+    _, _, payloads, st = _lib.encode_blocks(block, len(block), cand_mask=1 << 9, force=[9])
+    return payloads[0], {"nrules": st.get("rp_rules"), "final_len": st.get("rp_final"), "terminals": 256}
 
 
 def _v2_new(block: bytes):
@@ -157,7 +168,7 @@ def _select_encoders() -> List[Tuple[Callable[[bytes], Tuple[bytes, Dict[str, An
         (lambda b: encode_bbwt_mtf_rice(b, False, False, False, False, True, rice_param=2), "bbwt_gray"),
         (encode_lz77, "lz77"),
         (encode_lfsr_predict, "lfsr_pred"),
-        (_not_offloaded, "repair"),
+        (repair_compress, "repair"),
         (_v2_new, "v2_new"),
     ]
     mask = candidate_mask()
@@ -174,8 +185,8 @@ def _select_decoders():
     return [(lambda payload, n, meta=None, _m=m: decode_block(_m, payload, n)) for m in range(10)]
 
 
-def candidate_mask() -> int:
-    mask = _lib.KOLM_DEFAULT_MASK
+def candidate_mask(hot_path: bool = False) -> int:
+    mask = _lib.KOLM_HOTPATH_MASK if hot_path else _lib.KOLM_DEFAULT_MASK
     if G_NO_LZ77:
         mask &= ~(1 << 7)
     if G_ONLY_METHOD is not None:
@@ -193,13 +204,14 @@ def candidate_mask() -> int:
 # block API
 # ---------------------------------------------------------------------------
 
-def encode_blocks(data: bytes, block_size: int, cand_mask: Optional[int] = None, devices: int = 1):
+def encode_blocks(data: bytes, block_size: int, cand_mask: Optional[int] = None, devices: int = 1,
+                  hot_path: bool = False):
     """Batched device MDL over fixed blocks: (method_ids, orig_lens, payloads, sizes).
     devices > 1 shards the blocks over that many GPUs of this process."""
     if block_size <= 0:
         raise ValueError("block_size must be positive")
     global _last_stats
-    mask = candidate_mask() if cand_mask is None else cand_mask
+    mask = candidate_mask(hot_path) if cand_mask is None else cand_mask
     n = len(data)
     if n == 0:
         return [], [], [], None
@@ -212,16 +224,17 @@ def encode_blocks(data: bytes, block_size: int, cand_mask: Optional[int] = None,
     return [int(m) for m in method], orig, payloads, sizes
 
 
-def compress_blocks_fixed(data: bytes, block_size: int = 8192, devices: int = 1) -> bytes:
+def compress_blocks_fixed(data: bytes, block_size: int = 8192, devices: int = 1, hot_path: bool = False) -> bytes:
     """Fixed-size chunking + per-block MDL selection + KOLR container (PY:2332-2445).
-    `devices` (not in PY) spreads the blocks over that many GPUs of this process."""
+    `devices` (not in PY) spreads the blocks over that many GPUs of this process;
+    `hot_path` (not in PY) restricts the candidates to ids 0..8."""
     if block_size <= 0:
         raise ValueError("block_size must be positive")
     n = len(data)
     nb = (n + block_size - 1) // block_size
     if nb > 0xFFFF:
         raise struct.error("'H' format requires 0 <= number <= 65535")
-    mids, orig, payloads, _ = encode_blocks(data, block_size, devices=devices)
+    mids, orig, payloads, _ = encode_blocks(data, block_size, devices=devices, hot_path=hot_path)
     return write_container(MODE_FIXED, block_size, n, mids, orig, payloads)
 
 

@@ -19,8 +19,10 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libkolm_hip.so")
 
-KOLM_NCAND = 9
-KOLM_DEFAULT_MASK = 0x1FF
+KOLM_NCAND = 10
+KOLM_DEFAULT_MASK = 0x3FF   # the reference's candidates 0..9 (kolm.h)
+KOLM_HOTPATH_MASK = 0x1FF  # BBWT / MTF+Rice / LZ77 path, ids 0..8
+KOLM_REPAIR_MAX_BLOCK = 1 << 22
 ERRORS = {-1: "bad argument", -2: "capacity too small", -3: "HIP error", -4: "collective error",
           -5: "not initialised"}
 
@@ -36,7 +38,7 @@ class KolmError(RuntimeError):
 
 
 KT_NAMES = ["classify", "keygen", "msd", "small_sort", "lsd", "lz_parse", "mtf", "sizes", "emit",
-            "lyndon_gather"]
+            "lyndon_gather", "repair"]
 
 
 class KTime(ctypes.Structure):
@@ -57,6 +59,10 @@ class Stats(ctypes.Structure):
         ("ms_entropy", ctypes.c_double),
         ("ms_emit", ctypes.c_double),
         ("kt", KTime * len(KT_NAMES)),
+        ("ms_repair", ctypes.c_double),
+        ("rp_rules", ctypes.c_uint64),
+        ("rp_batches", ctypes.c_uint64),
+        ("rp_final", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -210,7 +216,7 @@ def bbwt_mtf_rice(data: bytes, flags: int, k: int = 2) -> bytes:
 
 
 def encode_blocks(data: bytes, block_size: int, cand_mask: int = KOLM_DEFAULT_MASK, force=None):
-    """Batched MDL encode of fixed-size blocks.  Returns (sizes[nb,9], method[nb],
+    """Batched MDL encode of fixed-size blocks.  Returns (sizes[nb,KOLM_NCAND], method[nb],
     payloads list, stats dict)."""
     ensure_init()
     n = len(data)

@@ -49,6 +49,8 @@ def lib():
         L.oracle_bbwt_mtf_rice.restype = i64
         L.oracle_candidate.argtypes = [ctypes.c_int, P, i64, ctypes.c_void_p, i64]
         L.oracle_candidate.restype = i64
+        L.oracle_repair_fast.argtypes = [P, i64, ctypes.c_void_p, i64, ctypes.c_void_p]
+        L.oracle_repair_fast.restype = i64
         _lib = L
     return _lib
 
@@ -102,10 +104,26 @@ def repair_compress(block: bytes) -> bytes:
     return _call(lib().oracle_repair, block, 6 * len(block) + 64)
 
 
+def repair_fast(block: bytes, with_stats: bool = False):
+    """Exact Re-Pair (PY:1817-1911) in O(n log n) (repair_lm.cpp); same bytes as
+    repair_compress.  with_stats -> (payload, (nrules, final_len, freq2_rounds, max_freq))."""
+    cap = 6 * len(block) + 64
+    buf = ctypes.create_string_buffer(cap)
+    st = (ctypes.c_int64 * 4)()
+    r = lib().oracle_repair_fast(block, len(block), buf, cap, st)
+    if r < 0:
+        raise RuntimeError(f"oracle call failed ({r})")
+    return (buf.raw[:r], tuple(st)) if with_stats else buf.raw[:r]
+
+
 BBWT_FLAGS = (0, 1, 4, 8, 16)  # candidates 2..6 (PY:2156-2160)
 
 
 def candidate(mid: int, block: bytes) -> bytes:
+    """Payload of candidate `mid`; Re-Pair (9) through the O(n log n) restatement
+    (repair_lm.cpp, checked against the O(n*rules) one in tests/test_oracle.py)."""
+    if mid == 9:
+        return repair_fast(block)
     cap = 9 * len(block) + 64
     buf = ctypes.create_string_buffer(cap)
     r = lib().oracle_candidate(mid, block, len(block), buf, cap)

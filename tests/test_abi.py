@@ -41,8 +41,18 @@ def test_ctypes_signatures_cover_header():
 
 
 def test_stats_struct_size_matches_header():
-    # kolm_stats: 2 u32 + 4 u64 + 5 double + 10 x {double, u64, u64}
-    assert ctypes.sizeof(_lib.Stats) == 8 + 4 * 8 + 5 * 8 + 10 * 24
+    # kolm_stats: 2 u32 + 4 u64 + 5 double + KOLM_NKT(11) x {double, u64, u64} + double + 3 u64
+    nkt = int(re.search(r"#define KOLM_NKT (\d+)", open(HEADER).read()).group(1))
+    assert nkt == len(_lib.KT_NAMES) == 11
+    assert ctypes.sizeof(_lib.Stats) == 8 + 4 * 8 + 5 * 8 + nkt * 24 + 8 + 3 * 8
+
+
+def test_candidate_constants_match_header():
+    src = open(HEADER).read()
+    val = lambda name: int(re.search(rf"#define {name} (0x[0-9A-Fa-f]+|\d+)", src).group(1), 0)  # noqa: E731
+    assert val("KOLM_NCAND") == _lib.KOLM_NCAND == 10
+    assert val("KOLM_DEFAULT_MASK") == _lib.KOLM_DEFAULT_MASK
+    assert val("KOLM_HOTPATH_MASK") == _lib.KOLM_HOTPATH_MASK
 
 
 def test_gpu_entry_fails_loudly_without_device():

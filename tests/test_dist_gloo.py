@@ -36,7 +36,7 @@ def _worker(rank, world, port, data, bs, q):
         mids, pays = [], []
         for i in range(first, first + count):
             blk = data[i * bs:(i + 1) * bs]
-            cands = [O.candidate(m, blk) for m in range(9)]
+            cands = [O.candidate(m, blk) for m in range(10)]
             m = int(np.argmin([len(c) for c in cands]))
             mids.append(m)
             pays.append(cands[m])
@@ -75,4 +75,4 @@ def test_gloo_sharded_reassembly(world, bs, n):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert got == O.compress_blocks_fixed(data, bs, range(9))
+    assert got == O.compress_blocks_fixed(data, bs, range(10))

@@ -52,4 +52,4 @@ def test_distributed_gpu_encode_matches_single():
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert got == O.compress_blocks_fixed(data, bs, range(9))
+    assert got == O.compress_blocks_fixed(data, bs, range(10))

@@ -50,25 +50,37 @@ def test_lz77_golden(kolm_gpu, golden_kernels, name):
 
 @pytest.mark.parametrize("name", KNAMES)
 def test_batched_candidates_golden(kolm_gpu, golden_kernels, name):
-    """All 9 candidate payloads of one block through the batched entry (forced method)."""
+    """All 10 candidate payloads of one block (ids 0..9, Re-Pair included) through the
+    batched entry (forced method), against PY's own outputs."""
     inp = gk(golden_kernels, name, "input")
     if not inp:
         return
     from kolm import _lib
     want = {0: inp, 1: gk(golden_kernels, name, "xor"), 7: gk(golden_kernels, name, "lz77"),
-            8: gk(golden_kernels, name, "lfsr")}
+            8: gk(golden_kernels, name, "lfsr"), 9: gk(golden_kernels, name, "repair")}
     for mid, f in FLAG_OF_MID.items():
         want[mid] = gk(golden_kernels, name, f"rice{f}")
-    for mid in range(9):
+    for mid in range(10):
         sizes, method, payloads, _ = _lib.encode_blocks(inp, len(inp), force=[mid])
         assert int(method[0]) == mid
         assert payloads[0] == want[mid], f"candidate {mid}"
         assert int(sizes[0][mid]) == len(want[mid]), f"size of candidate {mid}"
     # un-forced: MDL winner = argmin, ties -> lowest id (PY:2359)
     sizes, method, payloads, _ = _lib.encode_blocks(inp, len(inp))
-    lens = [len(want[m]) for m in range(9)]
+    lens = [len(want[m]) for m in range(10)]
     assert list(map(int, sizes[0])) == lens
     assert int(method[0]) == int(np.argmin(lens))
+    # hot path (ids 0..8): candidate 9 disabled, argmin over the rest
+    sizes, method, payloads, _ = _lib.encode_blocks(inp, len(inp), cand_mask=_lib.KOLM_HOTPATH_MASK)
+    assert int(sizes[0][9]) == 0xFFFFFFFF
+    assert int(method[0]) == int(np.argmin(lens[:9]))
+
+
+@pytest.mark.parametrize("name", KNAMES)
+def test_repair_golden(kolm_gpu, golden_kernels, name):
+    """repair_compress (PY:1841-1911) on the GPU vs PY's payload."""
+    inp = gk(golden_kernels, name, "input")
+    assert kolm_gpu.repair_compress(inp)[0] == gk(golden_kernels, name, "repair")
 
 
 @pytest.mark.parametrize("name", ["text_hobbit", "rand4k", "enwik16k", "utf8_mixed", "zero16k"])
@@ -83,8 +95,10 @@ def test_container_golden(kolm_gpu, golden_containers, manifest, cname):
     inp = golden_containers[f"{cname}/input"].tobytes()
     bs = manifest["containers"][cname]["block_size"]
     got = kolm_gpu.compress_blocks_fixed(inp, bs)
-    assert got == golden_containers[f"{cname}/ids0_8"].tobytes()
+    assert got == golden_containers[f"{cname}/full"].tobytes()  # PY's container, byte for byte
     assert kolm_gpu.decompress(got) == inp
+    hot = kolm_gpu.compress_blocks_fixed(inp, bs, hot_path=True)
+    assert hot == golden_containers[f"{cname}/ids0_8"].tobytes()
 
 
 LARGE = {
@@ -117,7 +131,7 @@ def test_large_known_answers(kolm_gpu, large_known, case):
 
 
 def _oracle_all(block: bytes):
-    return [O.candidate(m, block) for m in range(9)]
+    return [O.candidate(m, block) for m in range(10)]
 
 
 @pytest.mark.parametrize("seed,bs,n", [(1, 65536, 4 * 65536 + 12345), (2, 4096, 65536 + 17), (3, 1000, 20011),
@@ -146,7 +160,8 @@ def test_container_vs_oracle_multiblock(kolm_gpu):
     data = D.mixed_corpus()[:300_000]
     bs = 65536
     got = kolm_gpu.compress_blocks_fixed(data, bs)
-    assert got == O.compress_blocks_fixed(data, bs, range(9))
+    assert got == O.compress_blocks_fixed(data, bs, range(10))
+    assert kolm_gpu.compress_blocks_fixed(data, bs, hot_path=True) == O.compress_blocks_fixed(data, bs, range(9))
 
 
 @pytest.mark.parametrize("seed", [11, 12])
@@ -178,7 +193,7 @@ def test_full_size_enwik_properties(kolm_gpu, seed):
 @pytest.mark.parametrize("data,bs", [(b"", 16), (b"\x00", 1), (b"ab", 1), (b"abc" * 5, 4), (bytes(range(256)) * 3, 100)])
 def test_edge_cases(kolm_gpu, data, bs):
     got = kolm_gpu.compress_blocks_fixed(data, bs)
-    assert got == O.compress_blocks_fixed(data, bs, range(9))
+    assert got == O.compress_blocks_fixed(data, bs, range(10))
     assert kolm_gpu.decompress(got) == data
 
 
@@ -254,4 +269,35 @@ def test_encode_blocks_multi(kolm_gpu, ngpu):
     a = _lib.encode_blocks(data, bs)
     b = _lib.encode_blocks_multi(data, bs, ngpu)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
-    assert kolm_gpu.compress_blocks_fixed(data, bs, devices=ngpu) == O.compress_blocks_fixed(data, bs, range(9))
+    assert kolm_gpu.compress_blocks_fixed(data, bs, devices=ngpu) == O.compress_blocks_fixed(data, bs, range(10))
+
+
+RP_LARGE = {
+    "enwik_1m": lambda: D.enwik_like(1 << 20, seed=5),
+    "gradient_1m": lambda: D.gradient_bmp()[: 1 << 20],
+    "random_1m": lambda: D.splitmix64_bytes(1 << 20),
+    "pattern_1m": lambda: D.pattern_blocks(),
+    "zeros_1m": lambda: bytes(1 << 20),
+}
+
+
+def test_repair_full_size_batch(kolm_gpu):
+    """Re-Pair on 1 MiB blocks (text: 18.9k rules in ~950 batches; gradient: 133k rules in
+    ~17k batches; random; runs of zeros; the pattern file), all in ONE batch of 5 blocks
+    run concurrently, vs the oracle's exact O(n log n) Re-Pair."""
+    from kolm import _lib
+    names = sorted(RP_LARGE)
+    blocks = [RP_LARGE[k]() for k in names]
+    data = b"".join(blocks)
+    sizes, method, payloads, st = _lib.encode_blocks(data, 1 << 20, cand_mask=1 << 9,
+                                                     force=[9] * len(blocks))
+    for name, blk, pay in zip(names, blocks, payloads):
+        assert pay == O.repair_fast(blk), name
+
+
+@pytest.mark.parametrize("kind", ADV)
+def test_adversarial_repair(kolm_gpu, kind):
+    """Re-Pair on the adversarial structures (long (a,a) runs, periodic text, two symbols):
+    one 200 KB block vs the oracle."""
+    data = _adversarial(kind, 200_000)
+    assert kolm_gpu.repair_compress(data)[0] == O.repair_fast(data)

@@ -87,13 +87,16 @@ def test_registry_ids_stable():
     assert len(kolm._select_decoders()) == 10
     kolm.G_NO_LZ77 = True
     try:
-        assert kolm.candidate_mask() == 0x1FF & ~(1 << 7)
+        assert kolm.candidate_mask() == 0x3FF & ~(1 << 7)
+        assert kolm.candidate_mask(hot_path=True) == 0x1FF & ~(1 << 7)
         assert [n for _, n in kolm._select_encoders()] == kolm.CANDIDATE_NAMES  # ids unchanged
     finally:
         kolm.G_NO_LZ77 = False
     kolm.G_ONLY_METHOD = "lz77"
     try:
         assert kolm.candidate_mask() == 1 << 7
+        kolm.G_ONLY_METHOD = "repair"
+        assert kolm.candidate_mask() == 1 << 9
     finally:
         kolm.G_ONLY_METHOD = None
     with pytest.raises(NameError):

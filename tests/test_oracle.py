@@ -35,6 +35,27 @@ def test_oracle_kernels_vs_py_goldens(golden_kernels, manifest):
     assert not bad, bad
 
 
+def test_repair_fast_vs_py_goldens(golden_kernels, manifest):
+    """The O(n log n) Re-Pair restatement (repair_lm.cpp) reproduces PY's payload on every
+    golden input (PY:1817-1911)."""
+    bad = [name for name in manifest["kernels"]
+           if O.repair_fast(golden_kernels[f"{name}/input"].tobytes()) != golden_kernels[f"{name}/repair"].tobytes()]
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("kind,n", [("enwik", 65536), ("gradient", 12288), ("random", 16384), ("zeros", 30000),
+                                    ("two", 20000), ("runs", 20000)])
+def test_repair_fast_vs_full_recount(kind, n):
+    """Incremental (fast) vs the reference's full-recount algorithm (slow restatement) on
+    inputs larger than the goldens: text, image rows, random, runs, two symbols."""
+    rng = np.random.default_rng(n)
+    data = {"enwik": lambda: D.enwik_like(n), "gradient": lambda: D.gradient_bmp()[1000:1000 + n],
+            "random": lambda: D.splitmix64_bytes(n), "zeros": lambda: bytes(n),
+            "two": lambda: rng.integers(0, 2, n).astype(np.uint8).tobytes(),
+            "runs": lambda: bytes(np.repeat(rng.integers(0, 3, n // 8), 8).astype(np.uint8))}[kind]()
+    assert O.repair_fast(data) == O.repair_compress(data)
+
+
 def test_oracle_containers_vs_py(golden_containers, manifest):
     for cname, e in manifest["containers"].items():
         inp = golden_containers[f"{cname}/input"].tobytes()
