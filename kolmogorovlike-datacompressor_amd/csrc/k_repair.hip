@@ -14,10 +14,24 @@
 
 namespace kolm {
 
+static_assert(RP_RS_N == rp::RS_N && RP_RS_SIZE == rp::RS_SIZE && RP_RS_ERR == rp::RS_ERR, "result layout");
+static_assert(RP_P_N == rp::P_N && RP_MAX_N == rp::MAX_N, "profile sections / block limit");
+
 namespace {
 
 struct DevExec {
     rp::Shared* sh;
+    u64* prof;      // [P_N] per block, or null
+    u64 last = 0;   // thread 0: time of the previous mark
+    u32 last_id = 0;
+    __device__ inline void mark(u32 id) {
+        if (prof && threadIdx.x == 0) {
+            const u64 now = wall_clock64();
+            if (last) prof[last_id] += now - last;
+            last = now;
+            last_id = id;
+        }
+    }
     template <class F>
     __device__ inline void par(F f) {
         f(threadIdx.x);
@@ -41,6 +55,17 @@ struct DevExec {
         if (t == 0) *total = tot;
         __syncthreads();
     }
+    // wave-aggregated append: one atomic per wave, slots in lane order among pred lanes
+    __device__ inline u32 append(u32* ctr, bool pred) {
+        const u64 m = __ballot(pred);
+        if (!m) return rp::NIL;
+        const u32 lane = __lane_id();
+        const u32 leader = (u32)__ffsll((unsigned long long)m) - 1;
+        u32 base = 0;
+        if (lane == leader) base = atomicAdd(ctr, (u32)__popcll(m));
+        base = (u32)__shfl((int)base, (int)leader);
+        return pred ? base + (u32)__popcll(m & ((1ull << lane) - 1ull)) : rp::NIL;
+    }
     __device__ inline u32 add(u32* p, u32 v) { return atomicAdd(p, v); }
     __device__ inline u32 sub(u32* p, u32 v) { return atomicSub(p, v); }
     __device__ inline u32 min(u32* p, u32 v) { return atomicMin(p, v); }
@@ -61,8 +86,9 @@ __global__ __launch_bounds__(rp::NT) void k_repair(RpArgs a, u32 b0) {
     B.out = a.out + (u64)b * a.out_stride;
     B.out_cap = a.out_stride;
     B.result = a.result + (u64)b * rp::RS_N;
-    DevExec ex{&sh};
+    DevExec ex{&sh, a.prof ? a.prof + (u64)b * rp::P_N : nullptr};
     rp::repair_block(ex, B, sh);
+    ex.mark(0);
 }
 
 // winners' Re-Pair payloads -> arena (one workgroup per block, 16-byte copies where aligned)

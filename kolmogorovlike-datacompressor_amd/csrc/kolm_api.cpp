@@ -566,6 +566,11 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
         rpa.out_stride = 4ull * bs + 64;
         rpa.out = c->get<u8>("rp_out", (u64)nb * rpa.out_stride);
         rpa.result = c->get<u32>("rp_res", (u64)nb * RP_RS_N);
+        static const bool rp_prof = getenv("KOLM_RP_PROF") && atoi(getenv("KOLM_RP_PROF")) != 0;
+        if (rp_prof) {
+            rpa.prof = c->get<u64>("rp_prof", (u64)nb * RP_P_N);
+            KOLM_HIP_CHECK(hipMemsetAsync(rpa.prof, 0, sizeof(u64) * nb * RP_P_N, c->rp));
+        }
         static const u64 budget = (getenv("KOLM_RP_WS_GB") ? (u64)atof(getenv("KOLM_RP_WS_GB")) : 64ull) << 30;
         const u32 group = (u32)std::max<u64>(1, std::min<u64>(nb, budget / rpa.ws_stride));
         rpa.ws = c->get<char>("rp_ws", (u64)group * rpa.ws_stride);
@@ -640,6 +645,20 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const i
     if (want_rp)
         KOLM_HIP_CHECK(hipMemcpyAsync(rpres.data(), rpa.result, sizeof(u32) * rpres.size(), hipMemcpyDeviceToHost, s));
     c->sync();
+    if (want_rp && rpa.prof) {
+        // per-section wall-clock of the Re-Pair kernel (100 MHz ticks), summed over blocks
+        std::vector<u64> pr((u64)nb * RP_P_N);
+        KOLM_HIP_CHECK(hipMemcpy(pr.data(), rpa.prof, sizeof(u64) * pr.size(), hipMemcpyDeviceToHost));
+        static const char* const nm[RP_P_N] = {"init", "lvscan", "lvsort", "window", "gather", "chains",
+                                               "select", "applyA", "applyB", "late", "serialise"};
+        fprintf(stderr, "[kolm] Re-Pair sections, ms per block (mean over %u blocks):", nb);
+        for (u32 k = 0; k < RP_P_N; ++k) {
+            u64 t = 0;
+            for (u32 b = 0; b < nb; ++b) t += pr[(u64)b * RP_P_N + k];
+            fprintf(stderr, " %s %.2f", nm[k], (double)t / nb / 1e5);
+        }
+        fprintf(stderr, "\n");
+    }
     for (u32 b = 0; b < (want_rp ? nb : 0); ++b)
         if (rpres[(u64)b * RP_RS_N + RP_RS_ERR]) {
             char msg[128];

@@ -320,7 +320,9 @@ struct RpArgs {
     u8* out;           // [nb * out_stride] per-block payload
     u64 out_stride;    // 4 * bs + 64
     u32* result;       // [nb * RP_RS_N]
+    u64* prof;         // [nb * RP_P_N] wall-clock ticks per section (KOLM_RP_PROF=1), or null
 };
+constexpr u32 RP_P_N = 11;
 u64 repair_ws_bytes(u32 bs);
 void launch_repair(const RpArgs& a, u32 b0, u32 nblk, hipStream_t s);
 void launch_rp_emit(const RpArgs& a, const u32* method, const u64* off, u8* arena, hipStream_t s);

@@ -7,6 +7,8 @@
 //   ex.par(f)            f(tid) for every tid in [0, NT), then a workgroup barrier
 //   ex.scan(a, &total)   in-place exclusive scan of a[0..NT) (LDS), total written by all
 //   ex.add/sub/min/max/cas  atomics (u32; cas64 on u64)
+//   ex.append(&n, pred)  index n++ for the threads with pred (wave-aggregated on the device), else NIL
+//   ex.mark(id)          profiling hook: time since the previous mark goes to the previous id
 //
 // Reference semantics (PY:1817-1911), restated exactly:
 //   freq(a,b) = number of overlapping adjacent positions holding (a,b); each round picks
@@ -52,6 +54,9 @@ constexpr u32 NBASE = 65536;      // ids of the byte pairs: (a << 8) | b
 constexpr u32 MAX_N = 1u << 22;   // block length limit of the device Re-Pair
 
 enum : u32 { RS_SIZE = 0, RS_RULES, RS_FINAL, RS_BATCHES, RS_ERR, RS_LEVELS, RS_N };
+// profile sections (ex.mark(id): time since the previous mark is charged to the previous id)
+enum : u32 { P_INIT = 0, P_LVSCAN, P_LVSORT, P_WINDOW, P_GATHER, P_CHAINS, P_SELECT, P_APPLY_A, P_APPLY_B, P_LATE,
+             P_SER, P_N };
 enum : u32 { RE_OK = 0, RE_CAP = 1, RE_LOOP = 2, RE_LEN = 3 };
 
 // Per-block workspace (all device pointers).  Sizes for a block of length n:
@@ -87,7 +92,7 @@ struct Shared {
     u64 skey[SORT_LDS];
     u32 sval[SORT_LDS];
     u32 f, lp, lsize, M, V, T, tot, nocc, npairs, next_sym, nrules, pool, batch, hused, nlate;
-    u32 t1, t2, ts, any_aa, stop, maxc, err, total, levels;
+    u32 t1, t2, ts, any_aa, cut, maxc, err, total, levels;
 };
 
 // Carve a block's workspace out of `base` (nullptr: size query).  Returns the bytes
@@ -148,29 +153,30 @@ RP_HD inline u32 uleb_put(u8* o, u32 v) {
     }
 }
 
+// Insert key into the batch's hash table; returns its slot.  The thread whose CAS wins
+// allocates the pair id (read back from hval[slot] after the next barrier).
 template <class E>
-RP_HD inline void hash_insert(E& ex, const Block& B, Shared& sh, u64 key) {
+RP_HD inline u32 hash_insert(E& ex, const Block& B, Shared& sh, u64 key) {
     u32 s = hslot(key, B.hmask);
     for (;;) {
         const u64 cur = B.hkey[s];
-        if (cur == key) return;
+        if (cur == key) return s;
         if (cur == EMPTY) {
             const u64 old = ex.cas64(&B.hkey[s], EMPTY, key);
             if (old == EMPTY) {
                 const u32 u = ex.add(&sh.hused, 1u);
+                const u32 id = sh.npairs + u;
                 B.husd[u] = s;
-                return;
+                B.hval[s] = id;
+                B.pkey[id] = key;
+                B.cnt[id] = 0;
+                B.plen[id] = 0;
+                return s;
             }
-            if (old == key) return;
+            if (old == key) return s;
         }
         s = (s + 1) & B.hmask;
     }
-}
-
-RP_HD inline u32 hash_find(const Block& B, u64 key) {
-    u32 s = hslot(key, B.hmask);
-    while (B.hkey[s] != key) s = (s + 1) & B.hmask;
-    return B.hval[s];
 }
 
 // Sort key/id[0..n) ascending by key (keys unique); tk/ti is scratch of the same size.
@@ -180,6 +186,25 @@ RP_HD inline void sort_list(E& ex, Shared& sh, u64* k, u32* id, u64* tk, u32* ti
     // 1. runs of SORT_LDS sorted in LDS (bitonic)
     for (u32 base = 0; base < n; base += SORT_LDS) {
         const u32 len = n - base < SORT_LDS ? n - base : SORT_LDS;
+        if (len <= NT) {
+            // rank sort: two barriers; each key's rank = number of smaller keys (broadcast LDS reads)
+            ex.par([&](u32 t) {
+                if (t < len) {
+                    sh.skey[t] = k[base + t];
+                    sh.sval[t] = id[base + t];
+                }
+            });
+            ex.par([&](u32 t) {
+                if (t < len) {
+                    const u64 key = sh.skey[t];
+                    u32 r = 0;
+                    for (u32 e = 0; e < len; ++e) r += sh.skey[e] < key ? 1u : 0u;
+                    k[base + r] = key;
+                    id[base + r] = sh.sval[t];
+                }
+            });
+            continue;
+        }
         u32 S = 2;
         while (S < len) S <<= 1;
         ex.par([&](u32 t) {
@@ -274,7 +299,6 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
         if (t == 0) {
             sh.pool = 0; sh.npairs = NBASE; sh.next_sym = 256; sh.nrules = 0; sh.batch = 0;
             sh.lp = 0; sh.lsize = 0; sh.f = 0; sh.hused = 0; sh.nlate = 0; sh.err = RE_OK; sh.levels = 0;
-            sh.stop = 0;
         }
     });
     ex.par([&](u32 t) {
@@ -303,6 +327,7 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
             B.occpos[B.poff[code] + ex.add(&B.plen[code], 1u)] = i;
         }
     });
+    ex.mark(P_INIT);
     u64* lk = B.lkA;
     u32* li = B.liA;
     u64* tk = B.lkB;
@@ -315,11 +340,20 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
             break;
         }
         if (sh.lp >= sh.lsize) {
+            ex.mark(P_LVSCAN);
             // new level: f = max count; the level list = pairs with count f, sorted
             ex.par([&](u32 t) { if (t == 0) sh.maxc = 0; });
             ex.par([&](u32 t) {
+                // 8 independent loads in flight per thread (a loop-carried max would wait on each)
                 u32 m = 0;
-                for (u32 id = t; id < sh.npairs; id += NT) m = B.cnt[id] > m ? B.cnt[id] : m;
+                const u32 np = sh.npairs;
+                for (u32 i0 = t; i0 < np; i0 += 8 * NT) {
+                    u32 v[8];
+#pragma unroll
+                    for (u32 k = 0; k < 8; ++k) v[k] = i0 + k * NT < np ? B.cnt[i0 + k * NT] : 0u;
+#pragma unroll
+                    for (u32 k = 0; k < 8; ++k) m = v[k] > m ? v[k] : m;
+                }
                 if (m) ex.max(&sh.maxc, m);
             });
             if (sh.maxc < 2) break;
@@ -327,40 +361,62 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
                 if (t == 0) { sh.f = sh.maxc; sh.lsize = 0; sh.lp = 0; sh.levels++; }
             });
             ex.par([&](u32 t) {
-                for (u32 id = t; id < sh.npairs; id += NT)
-                    if (B.cnt[id] == sh.f) {
-                        const u32 k = ex.add(&sh.lsize, 1u);
-                        lk[k] = B.pkey[id];
-                        li[k] = id;
+                const u32 np = sh.npairs, fl = sh.f;
+                for (u32 i0 = 0; i0 < np; i0 += 4 * NT) {
+                    u32 v[4];
+#pragma unroll
+                    for (u32 k = 0; k < 4; ++k) v[k] = i0 + k * NT + t < np ? B.cnt[i0 + k * NT + t] : 0u;
+#pragma unroll
+                    for (u32 k = 0; k < 4; ++k) {
+                        const u32 id = i0 + k * NT + t;
+                        const bool hit = v[k] == fl && id < np;
+                        const u32 slot = ex.append(&sh.lsize, hit);
+                        if (hit) {
+                            lk[slot] = B.pkey[id];
+                            li[slot] = id;
+                        }
                     }
+                }
             });
+            ex.mark(P_LVSORT);
             sort_list(ex, sh, lk, li, tk, ti, sh.lsize);
         }
+        ex.mark(P_WINDOW);
         const u32 f = sh.f;
         const u32 batch = sh.batch;
+        const u32 ctag0 = batch * W;
+        const u32 otag0 = (BMAX - batch) * W;
+        const u32 X0 = sh.next_sym;
         // ---- window: the next valid level entries (count still f), in list order ----
         ex.par([&](u32 t) {
             const u32 idx = sh.lp + t;
             sh.scan[t] = idx < sh.lsize && B.cnt[li[idx]] == f ? 1u : 0u;
+            sh.scan2[t] = 0;
+            if (t == 0) {
+                sh.cut = NIL; sh.any_aa = 0; sh.nocc = 0; sh.t1 = NIL; sh.t2 = NIL; sh.ts = NIL;
+                sh.hused = 0; sh.nlate = 0;
+            }
         });
         ex.scan(sh.scan, &sh.V);
         ex.par([&](u32 t) {
             const u32 idx = sh.lp + t;
-            if (idx < sh.lsize && B.cnt[li[idx]] == f) {
-                const u32 r = sh.scan[t];
-                if (r < W) {
-                    const u32 id = li[idx];
-                    const u64 key = lk[idx];
-                    sh.m_id[r] = id;
-                    sh.m_a[r] = (u32)(key >> 32);
-                    sh.m_b[r] = (u32)key;
-                    sh.m_lpos[r] = idx;
-                    sh.m_roff[r] = B.poff[id];
-                    sh.m_rlen[r] = B.plen[id];
-                    sh.m_repl[r] = 0;
-                    sh.m_lmin[r] = NIL;
-                    sh.m_lmax[r] = 0;
-                }
+            const u32 r = sh.scan[t];
+            const bool valid = (t + 1 < NT ? sh.scan[t + 1] : sh.V) != r;  // this entry's flag
+            if (valid && r < W) {
+                const u32 id = li[idx];
+                const u64 key = lk[idx];
+                const u32 a = (u32)(key >> 32), b = (u32)key, len = B.plen[id];
+                sh.m_id[r] = id;
+                sh.m_a[r] = a;
+                sh.m_b[r] = b;
+                sh.m_lpos[r] = idx;
+                sh.m_roff[r] = B.poff[id];
+                sh.m_rlen[r] = len;
+                sh.m_repl[r] = 0;
+                sh.m_lmin[r] = NIL;
+                sh.m_lmax[r] = 0;
+                sh.scan2[r] = len;
+                if (a == b) sh.any_aa = 1;
             }
         });
         if (sh.V == 0) {
@@ -369,52 +425,56 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
             });
             continue;
         }
+        const u32 Mw = sh.V < W ? sh.V : W;
+        ex.scan(sh.scan2, &sh.total);  // region prefix over the window's members
         ex.par([&](u32 t) {
-            if (t == 0) {
-                u32 M = sh.V < W ? sh.V : W, pre = 0, aa = 0;
-                for (u32 m = 0; m < M; ++m) {
-                    if (m > 0 && pre + sh.m_rlen[m] > CAPR) {
-                        M = m;
-                        break;
-                    }
-                    sh.m_pre[m] = pre;
-                    pre += sh.m_rlen[m];
-                    aa |= sh.m_a[m] == sh.m_b[m] ? 1u : 0u;
-                }
-                sh.m_pre[M] = pre;
-                sh.M = M;
-                sh.tot = pre;
-                sh.any_aa = aa;
-                sh.nocc = 0;
-                sh.t1 = NIL;
-                sh.t2 = NIL;
-                sh.ts = NIL;
-                sh.hused = 0;
-                sh.nlate = 0;
+            if (t < Mw) {
+                const u32 pre = sh.scan2[t];
+                sh.m_pre[t] = pre;
+                if (t > 0 && pre + sh.m_rlen[t] > CAPR) ex.min(&sh.cut, t);
             }
         });
-        const u32 M = sh.M;
-        // ---- gather the members' live occurrences ----
+        const u32 M = sh.cut < Mw ? sh.cut : Mw;
+        const u32 tot = sh.scan2[M];  // entries past Mw are 0: prefix at M
+        const bool aa = sh.any_aa != 0;
+        ex.mark(P_GATHER);
+        // ---- gather the members' live occurrences (+ chosen-occurrence marks when no
+        //      member is an (a,a) pair: then every live occurrence is replaced) ----
         ex.par([&](u32 t) {
-            for (u32 e = t; e < sh.tot; e += NT) {
-                u32 lo = 0, hi = M;  // member m: m_pre[m] <= e < m_pre[m+1]
-                while (hi - lo > 1) {
-                    const u32 md = (lo + hi) >> 1;
-                    if (sh.m_pre[md] <= e) lo = md; else hi = md;
+            for (u32 e0 = 0; e0 < tot; e0 += NT) {
+                const u32 e = e0 + t;
+                bool valid = false;
+                u32 pos = 0, lo = 0;
+                if (e < tot) {
+                    u32 hi = M;  // member lo: m_pre[lo] <= e < m_pre[lo+1]
+                    while (hi - lo > 1) {
+                        const u32 md = (lo + hi) >> 1;
+                        if (sh.m_pre[md] <= e) lo = md; else hi = md;
+                    }
+                    pos = B.occpos[sh.m_roff[lo] + (e - sh.m_pre[lo])];
+                    valid = B.opair[pos] == sh.m_id[lo];
                 }
-                const u32 pos = B.occpos[sh.m_roff[lo] + (e - sh.m_pre[lo])];
-                if (B.opair[pos] == sh.m_id[lo]) {
-                    const u32 o = ex.add(&sh.nocc, 1u);
+                const u32 o = ex.append(&sh.nocc, valid);
+                if (valid) {
                     B.opos[o] = pos;
                     B.omem[o] = lo;
-                    B.oidx[pos] = o;
+                    if (aa) {
+                        B.oidx[pos] = o;
+                    } else {
+                        B.ctag[pos] = ctag0 + lo;
+                        ex.add(&sh.m_repl[lo], 1u);
+                        ex.min(&B.owner[pos], otag0 + lo);
+                        ex.min(&B.owner[B.nxt[pos]], otag0 + lo);
+                    }
                 }
             }
         });
         const u32 nocc = sh.nocc;
-        // ---- runs of (a,a): distance from the run start by pointer jumping ----
+        ex.mark(P_CHAINS);
+        // ---- runs of (a,a): distance from the run start by pointer jumping; greedy
+        //      left-to-right pairing replaces the occurrences at even distance ----
         u32* dist = B.od0;
-        if (sh.any_aa) {
+        if (aa) {
             ex.par([&](u32 t) {
                 for (u32 o = t; o < nocc; o += NT) {
                     const u32 m = B.omem[o], pos = B.opos[o];
@@ -454,28 +514,24 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
                 if (!sh.chg[c]) break;
             }
             dist = d0;
-        } else {
+            // chosen occurrences: tags, replacement counts, span owners
             ex.par([&](u32 t) {
-                for (u32 o = t; o < nocc; o += NT) B.od0[o] = 0;
+                for (u32 o = t; o < nocc; o += NT) {
+                    if (dist[o] & 1u) continue;
+                    const u32 m = B.omem[o], i = B.opos[o];
+                    B.ctag[i] = ctag0 + m;
+                    ex.add(&sh.m_repl[m], 1u);
+                    ex.min(&B.owner[i], otag0 + m);
+                    ex.min(&B.owner[B.nxt[i]], otag0 + m);
+                }
             });
         }
-        // ---- chosen occurrences: tags, replacement counts, span owners ----
-        const u32 ctag0 = batch * W;
-        const u32 otag0 = (BMAX - batch) * W;
+        ex.mark(P_SELECT);
+        // ---- conflicts (footprint vs earlier spans), left-neighbour uniformity; the
+        //      neighbourhood of every chosen occurrence is kept for the apply phases ----
         ex.par([&](u32 t) {
             for (u32 o = t; o < nocc; o += NT) {
-                if (dist[o] & 1u) continue;
-                const u32 m = B.omem[o], i = B.opos[o];
-                B.ctag[i] = ctag0 + m;
-                ex.add(&sh.m_repl[m], 1u);
-                ex.min(&B.owner[i], otag0 + m);
-                ex.min(&B.owner[B.nxt[i]], otag0 + m);
-            }
-        });
-        // ---- conflicts (footprint vs earlier spans), left-neighbour uniformity ----
-        ex.par([&](u32 t) {
-            for (u32 o = t; o < nocc; o += NT) {
-                if (dist[o] & 1u) continue;
+                if (aa && (dist[o] & 1u)) continue;
                 const u32 m = B.omem[o], i = B.opos[o];
                 const u32 p = B.prv[i], j = B.nxt[i], q = B.nxt[j];
                 bool conf = false;
@@ -493,9 +549,15 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
                 }
                 if (conf) ex.min(&sh.t1, m);
                 const bool leftc = p != NIL && B.prv[p] != NIL && B.ctag[B.prv[p]] == ctag0 + m;
+                const bool rightc = q != NIL && B.ctag[q] == ctag0 + m;
                 const u32 x = (p != NIL && !leftc) ? B.sym[p] : NIL;
                 ex.min(&sh.m_lmin[m], x);
                 ex.max(&sh.m_lmax[m], x);
+                B.oj[o] = j;
+                B.op[o] = leftc ? NIL : p;
+                B.oq[o] = q;
+                B.oidl[o] = x;                                           // left symbol
+                B.oidr[o] = q == NIL ? NIL : rightc ? X0 + m : B.sym[q];  // right symbol
             }
         });
         ex.par([&](u32 t) {
@@ -513,90 +575,59 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
                 }
             }
         });
-        ex.par([&](u32 t) {
-            if (t == 0) {
-                u32 T = M;
-                T = sh.t1 < T ? sh.t1 : T;
-                T = sh.t2 < T ? sh.t2 : T;
-                T = sh.ts < T ? sh.ts : T;
-                sh.T = T;
-                sh.stop = (sh.ts != NIL && sh.ts < sh.t1 && sh.ts < sh.t2) ? 1u : 0u;
-            }
-        });
-        const u32 T = sh.T;
+        u32 T = M;
+        T = sh.t1 < T ? sh.t1 : T;
+        T = sh.t2 < T ? sh.t2 : T;
+        T = sh.ts < T ? sh.ts : T;
+        const bool stop = sh.ts != NIL && sh.ts < sh.t1 && sh.ts < sh.t2;
         if (T == 0) break;  // the next round replaces < 2 occurrences (PY:1879-1882)
-        const u32 X0 = sh.next_sym;
-        // ---- apply 1: destroy old pair occurrences, register the new pair keys ----
+        ex.mark(P_APPLY_A);
+        // ---- apply 1: destroy the old pair occurrences; register the new pair keys (the
+        //      inserting thread allocates the id) and keep each occurrence's hash slots ----
         ex.par([&](u32 t) {
             for (u32 o = t; o < nocc; o += NT) {
-                if (dist[o] & 1u) continue;
+                if (aa && (dist[o] & 1u)) continue;
                 const u32 m = B.omem[o];
                 if (m >= T) continue;
-                const u32 i = B.opos[o], p = B.prv[i], j = B.nxt[i], q = B.nxt[j];
-                const bool leftc = p != NIL && B.prv[p] != NIL && B.ctag[B.prv[p]] == ctag0 + m;
-                const bool rightc = q != NIL && B.ctag[q] == ctag0 + m;
-                B.oj[o] = j;
-                B.op[o] = leftc ? NIL : p;
-                B.oq[o] = q;
+                const u32 i = B.opos[o], p = B.op[o], j = B.oj[o], q = B.oq[o];
                 ex.sub(&B.cnt[B.opair[i]], 1u);
                 if (q != NIL) ex.sub(&B.cnt[B.opair[j]], 1u);
-                if (p != NIL && !leftc) ex.sub(&B.cnt[B.opair[p]], 1u);
+                if (p != NIL) ex.sub(&B.cnt[B.opair[p]], 1u);
                 const u32 X = X0 + m;
-                if (q != NIL) {
-                    const u32 r = rightc ? X : B.sym[q];
-                    B.oidr[o] = r;  // right symbol (ids come after the barrier)
-                    hash_insert(ex, B, sh, pkey_of(X, r));
-                }
-                if (p != NIL && !leftc) {
-                    B.oidl[o] = B.sym[p];
-                    hash_insert(ex, B, sh, pkey_of(B.sym[p], X));
-                }
+                if (q != NIL) B.oidr[o] = hash_insert(ex, B, sh, pkey_of(X, B.oidr[o]));
+                if (p != NIL) B.oidl[o] = hash_insert(ex, B, sh, pkey_of(B.oidl[o], X));
             }
         });
-        // ---- apply 2: ids for the new pairs ----
-        ex.par([&](u32 t) {
-            for (u32 u = t; u < sh.hused; u += NT) {
-                const u32 s = B.husd[u], id = sh.npairs + u;
-                B.hval[s] = id;
-                B.pkey[id] = B.hkey[s];
-                B.cnt[id] = 0;
-                B.plen[id] = 0;
-            }
-        });
-        // ---- apply 3: count the new pair occurrences ----
+        // ---- apply 2: count the new pair occurrences, rewrite the sequence ----
         ex.par([&](u32 t) {
             for (u32 o = t; o < nocc; o += NT) {
-                if (dist[o] & 1u) continue;
-                const u32 m = B.omem[o];
-                if (m >= T) continue;
-                const u32 X = X0 + m;
-                if (B.oq[o] != NIL) {
-                    const u32 id = hash_find(B, pkey_of(X, B.oidr[o]));
-                    B.oidr[o] = id;
-                    ex.add(&B.cnt[id], 1u);
-                }
-                if (B.op[o] != NIL) {
-                    const u32 id = hash_find(B, pkey_of(B.oidl[o], X));
-                    B.oidl[o] = id;
-                    ex.add(&B.cnt[id], 1u);
-                }
-            }
-        });
-        // ---- apply 4: rewrite the sequence ----
-        ex.par([&](u32 t) {
-            for (u32 o = t; o < nocc; o += NT) {
-                if (dist[o] & 1u) continue;
+                if (aa && (dist[o] & 1u)) continue;
                 const u32 m = B.omem[o];
                 if (m >= T) continue;
                 const u32 i = B.opos[o], j = B.oj[o], q = B.oq[o], p = B.op[o];
+                u32 idr = NIL;
+                if (q != NIL) {
+                    idr = B.hval[B.oidr[o]];
+                    B.oidr[o] = idr;
+                    ex.add(&B.cnt[idr], 1u);
+                }
+                if (p != NIL) {
+                    const u32 idl = B.hval[B.oidl[o]];
+                    B.oidl[o] = idl;
+                    ex.add(&B.cnt[idl], 1u);
+                    B.opair[p] = idl;
+                }
                 B.sym[i] = X0 + m;
                 B.nxt[i] = q;
                 if (q != NIL) B.prv[q] = i;
                 B.sym[j] = DEAD;
                 B.opair[j] = NIL;
-                B.opair[i] = q != NIL ? B.oidr[o] : NIL;
-                if (p != NIL) B.opair[p] = B.oidl[o];
+                B.opair[i] = idr;
             }
+        });
+        ex.mark(P_APPLY_B);
+        // ---- apply 3: regions of the new pairs; count-f pairs join the level late ----
+        ex.par([&](u32 t) {
             for (u32 u = t; u < sh.hused; u += NT) {
                 const u32 id = sh.npairs + u;
                 B.poff[id] = ex.add(&sh.pool, B.cnt[id]);
@@ -608,10 +639,10 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
             }
             for (u32 m = t; m < T; m += NT) B.rules[sh.nrules + m] = pkey_of(sh.m_a[m], sh.m_b[m]);
         });
-        // ---- apply 5: occurrence regions of the new pairs ----
+        // ---- apply 4: occurrence positions of the new pairs ----
         ex.par([&](u32 t) {
             for (u32 o = t; o < nocc; o += NT) {
-                if (dist[o] & 1u) continue;
+                if (aa && (dist[o] & 1u)) continue;
                 const u32 m = B.omem[o];
                 if (m >= T) continue;
                 if (B.oq[o] != NIL) {
@@ -632,10 +663,30 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
                 sh.batch += 1;
             }
         });
+        ex.mark(P_LATE);
         if (sh.nlate) {
-            // new pairs with count f join the level list at their key position
+            // new pairs with count f join the level list at their key position.  When they all
+            // start with a new symbol (X_m, y) they sort after every entry of the list (whose
+            // symbols all predate this batch): append; otherwise merge.
             const u32 nl = sh.nlate;
             sort_list(ex, sh, B.lkL, B.liL, tk, ti, nl);
+            if ((u32)(B.lkL[0] >> 32) >= X0) {
+                ex.par([&](u32 t) {
+                    const u32 base = sh.lsize;
+                    for (u32 e = t; e < nl; e += NT) {
+                        lk[base + e] = B.lkL[e];
+                        li[base + e] = B.liL[e];
+                    }
+                });
+                ex.par([&](u32 t) {
+                    if (t == 0) {
+                        sh.lsize += nl;
+                        sh.nlate = 0;
+                    }
+                });
+                if (stop) break;
+                continue;
+            }
             const u32 r0 = sh.lp, rn = sh.lsize - sh.lp;
             ex.par([&](u32 t) {
                 for (u32 e = t; e < rn + nl; e += NT) {
@@ -673,12 +724,13 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
             u64* xk = lk; lk = tk; tk = xk;
             u32* xi = li; li = ti; ti = xi;
         }
-        if (sh.stop) break;
+        if (stop) break;
         if (sh.next_sym - 256 > n) {  // impossible for a correct run (each rule removes >= 2 symbols)
             ex.par([&](u32 t) { if (t == 0) sh.err = RE_LOOP; });
             break;
         }
     }
+    ex.mark(P_SER);
     // ---------------- serialise (PY:1889-1903): RP, 256, nrules, rules, len, seq ----------------
     const u32 R = sh.nrules;
     // final sequence length and ULEB bytes of the live symbols, per contiguous thread range

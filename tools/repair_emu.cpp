@@ -44,6 +44,8 @@ struct HostExec {
     u32 min(u32* p, u32 v) { const u32 o = *p; if (v < o) *p = v; return o; }
     u32 max(u32* p, u32 v) { const u32 o = *p; if (v > o) *p = v; return o; }
     u64 cas64(u64* p, u64 cmp, u64 v) { const u64 o = *p; if (o == cmp) *p = v; return o; }
+    void mark(u32) {}
+    u32 append(u32* n, bool pred) { return pred ? (*n)++ : NIL; }
 };
 
 }  // namespace
