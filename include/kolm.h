@@ -71,7 +71,8 @@ typedef struct kolm_ctx kolm_ctx;
 #define KOLM_KT_EMIT 8       /* emission kernels */
 #define KOLM_KT_LYNDON 9     /* k_duval_*, Lyndon scans, k_prevc, k_bbwt_gather */
 #define KOLM_KT_REPAIR 10    /* k_repair (one workgroup per block), k_rp_emit */
-#define KOLM_NKT 11
+#define KOLM_KT_CDC 11       /* k_cdc_flags, k_cdc_spec, k_cdc_stitch, k_cdc_count/scan/emit */
+#define KOLM_NKT 12
 
 typedef struct kolm_ktime {
     double ms;          /* summed launch durations (HIP events on the library stream) */
@@ -119,9 +120,21 @@ int kolm_lz77_encode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size
 int kolm_bbwt_mtf_rice(const uint8_t* in, size_t n, int flags, int k, uint8_t* out, size_t cap,
                        size_t* out_len);
 
+/* ---- content-defined chunking (FastCDC) ------------------------------------------ */
+/* Chunk boundaries of data[0, n) exactly as cdc_fast_boundaries_strict (PY:210-309,
+ * replaces the loop at PY:247-298 + the orphan-tail merge PY:300-306): starts[0 ..
+ * *nchunks] receives the chunk starts followed by n (chunk i = [starts[i], starts[i+1])).
+ * cap = entries available in starts (n / min_size + 2 always suffices).  KOLM_EARG with
+ * PY's messages for the parameters it rejects (0 < min <= avg <= max, avg >= 64). */
+int kolm_cdc_boundaries(const uint8_t* data, uint64_t n, uint32_t min_size, uint32_t avg_size,
+                        uint32_t max_size, int merge_orphan_tail, uint64_t* starts, uint64_t cap,
+                        uint64_t* nchunks);
+
 /* ---- batched hot entry (host buffers, default context) ------------------------- */
 /* Encodes nblocks blocks of `data` (block i = data[starts[i] .. starts[i]+lens[i]);
- * fixed chunking: all lens equal except possibly the last, starts[i] = i*lens[0]).
+ * blocks contiguous and non-empty: fixed chunking when all lens are equal except a
+ * shorter last one, otherwise content-defined chunks, e.g. kolm_cdc_boundaries' output
+ * for compress_blocks_cdc, PY:2213-2326).
  * sizes[i*KOLM_NCAND + m] receives the payload size of candidate m (UINT32_MAX if the
  * candidate is disabled by cand_mask).  method[i] receives the MDL winner, or the
  * forced method when force_method != NULL and force_method[i] >= 0.  The winners'
@@ -168,6 +181,17 @@ int kolm_encode_blocks_device(kolm_ctx* ctx, const uint8_t* d_data, uint64_t tot
                               const int32_t* force_method, uint8_t* d_arena, uint64_t arena_cap,
                               uint32_t* h_sizes, uint32_t* h_method, uint64_t* h_off,
                               kolm_stats* stats);
+/* Content-defined blocks of d_data: block i = [h_bounds[i], h_bounds[i+1]), h_bounds[0] = 0,
+ * strictly increasing, nblocks + 1 entries (PY:2213-2326).  Outputs as
+ * kolm_encode_blocks_device. */
+int kolm_encode_blocks_device_var(kolm_ctx* ctx, const uint8_t* d_data, const uint32_t* h_bounds,
+                                  uint32_t nblocks, uint32_t cand_mask, const int32_t* force_method,
+                                  uint8_t* d_arena, uint64_t arena_cap, uint32_t* h_sizes,
+                                  uint32_t* h_method, uint64_t* h_off, kolm_stats* stats);
+/* kolm_cdc_boundaries over a device-resident buffer; h_starts are host u32 entries. */
+int kolm_cdc_boundaries_device(kolm_ctx* ctx, const uint8_t* d_data, uint64_t n, uint32_t min_size,
+                               uint32_t avg_size, uint32_t max_size, int merge_orphan_tail,
+                               uint32_t* h_starts, uint64_t cap, uint64_t* nchunks);
 
 #ifdef __cplusplus
 }

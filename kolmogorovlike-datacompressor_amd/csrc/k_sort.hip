@@ -905,4 +905,48 @@ void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, hipStream_t
     if (nb) k_update_done<<<cdiv(nb, 256), 256, 0, s>>>(blk_done, blk_split, nb);
 }
 
+// ------------------------------------------------------------------------------------
+// variable (content-defined) block geometry
+// ------------------------------------------------------------------------------------
+// vmap[k] = the block holding position k << vshift (last b with vb[b] <= k << vshift)
+__global__ void k_vmap(const u32* vb, u32 nb, u32* vmap, u32 ngran, u32 vshift) {
+    const u32 k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ngran) return;
+    const u32 g = k << vshift;
+    u32 lo = 0, hi = nb;
+    while (hi - lo > 1) {
+        const u32 m = (lo + hi) >> 1;
+        if (vb[m] <= g) lo = m; else hi = m;
+    }
+    vmap[k] = lo;
+}
+
+// granule 2^vshift <= the shortest block: block_of walks at most one boundary per lookup
+u32 geom_var_shift(const u32* hb, u32 nb) {
+    u32 mn = 0xFFFFFFFFu;
+    for (u32 b = 0; b < nb; ++b) mn = std::min(mn, hb[b + 1] - hb[b]);
+    u32 s = 0;
+    while (s < 16 && (2u << s) <= mn) ++s;
+    return s;
+}
+
+void geom_init_var(Geom& g, const u32* hb, u32 nb, u32* d_vb, u32* d_vmap, u32 vshift, hipStream_t s) {
+    g = Geom{};
+    g.N = hb[nb];
+    g.nb = nb;
+    u32 mx = 1;
+    for (u32 b = 0; b < nb; ++b) mx = std::max(mx, hb[b + 1] - hb[b]);
+    g.bs = mx;
+    g.magic = 0;
+    g.shift = 0;
+    g.vb = d_vb;
+    g.hvb = hb;
+    g.vmap = d_vmap;
+    g.vshift = vshift;
+    KOLM_HIP_CHECK(hipMemcpyAsync(d_vb, hb, sizeof(u32) * ((u64)nb + 1), hipMemcpyHostToDevice, s));
+    const u32 ngran = g.N ? (u32)((g.N - 1) >> vshift) + 1 : 0u;
+    if (ngran) k_vmap<<<cdiv(ngran, 256), 256, 0, s>>>(d_vb, nb, d_vmap, ngran, vshift);
+    KOLM_HIP_CHECK(hipStreamSynchronize(s));  // hb is pageable caller memory
+}
+
 }  // namespace kolm

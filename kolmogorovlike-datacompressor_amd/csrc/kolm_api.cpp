@@ -51,6 +51,7 @@ enum : int {
     C_CLSE = 24,     // 12 slots: elements per small class
     C_L0ELEM = 36,
     C_L1ELEM = 37,
+    C_CDC = 40,      // FastCDC cut count
     C_N = 48
 };
 
@@ -522,12 +523,42 @@ int check_geom(u64 N, u32 bs) {
     return KOLM_OK;
 }
 
-// Full batch: sizes of candidates 0..8, MDL, emission into d_arena.
-int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, u32 mask, const int32_t* h_force, u8* d_arena,
-                 u64 arena_cap, u32* h_sizes, u32* h_method, u64* h_off, kolm_stats* stats) {
-    if (int e = check_geom(N, bs)) return e;
+// Content-defined blocks: hb[0] = 0, strictly increasing, total < 2^31, blocks <= 32 MiB.
+int check_bounds(const u32* hb, u32 nb) {
+    if (hb[0] != 0) {
+        set_err("block bounds must start at 0");
+        return KOLM_EARG;
+    }
+    for (u32 b = 0; b < nb; ++b)
+        if (hb[b + 1] <= hb[b] || hb[b + 1] - hb[b] > (1u << 25)) {
+            set_err("blocks must be non-empty, contiguous and at most 32 MiB");
+            return KOLM_EARG;
+        }
+    if (hb[nb] >= (1u << 31)) {
+        set_err("batch larger than 2^31-1 bytes");
+        return KOLM_EARG;
+    }
+    return KOLM_OK;
+}
+
+// Full batch: sizes of candidates 0..9, MDL, emission into d_arena.  Fixed blocks of bs
+// bytes over [0, N), or (h_bounds != null) the nbv content-defined blocks
+// [h_bounds[i], h_bounds[i+1]) (PY:2213 compress_blocks_cdc).
+int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_bounds, u32 nbv, u32 mask,
+                 const int32_t* h_force, u8* d_arena, u64 arena_cap, u32* h_sizes, u32* h_method, u64* h_off,
+                 kolm_stats* stats) {
     Geom geo;
-    geom_init(geo, N, bs);
+    if (h_bounds) {
+        if (int e = check_bounds(h_bounds, nbv)) return e;
+        N = h_bounds[nbv];
+        const u32 vs = geom_var_shift(h_bounds, nbv);
+        geom_init_var(geo, h_bounds, nbv, c->get<u32>("vb", (u64)nbv + 1), c->get<u32>("vmap", (N >> vs) + 2), vs,
+                      c->stream);
+        bs = geo.bs;
+    } else {
+        if (int e = check_geom(N, bs)) return e;
+        geom_init(geo, N, bs);
+    }
     const u32 nb = geo.nb;
     if (nb == 0) {
         if (h_off) h_off[0] = 0;
@@ -933,8 +964,8 @@ int kolm_encode_blocks_device(kolm_ctx* c, const uint8_t* d_data, uint64_t total
     return guarded([&] {
         std::lock_guard<std::mutex> g(c->mu);
         KOLM_HIP_CHECK(hipSetDevice(c->device));
-        return encode_batch(c, d_data, total, block_size, cand_mask & KOLM_DEFAULT_MASK, force_method, d_arena,
-                            arena_cap, h_sizes, h_method, h_off, stats);
+        return encode_batch(c, d_data, total, block_size, nullptr, 0, cand_mask & KOLM_DEFAULT_MASK, force_method,
+                            d_arena, arena_cap, h_sizes, h_method, h_off, stats);
     });
 }
 
@@ -946,27 +977,41 @@ int kolm_encode_blocks(const uint8_t* data, const uint64_t* starts, const uint32
     if (nblocks && (!data || !starts || !lens)) return KOLM_EARG;
     if (!payload_off) return KOLM_EARG;
     if ((cand_mask & KOLM_DEFAULT_MASK) == 0) return KOLM_EARG;
-    // fixed chunking only: starts[i] = i*bs, lens[i] = bs except the last
+    // contiguous non-empty blocks; the fixed geometry when every block but a shorter last
+    // one has lens[0] bytes, the variable one otherwise (content-defined chunks)
     uint64_t total = 0;
     const uint32_t bs = nblocks ? lens[0] : 1;
+    bool fixed = true;
     for (uint32_t i = 0; i < nblocks; ++i) {
-        if (starts[i] != (uint64_t)i * bs || lens[i] == 0 || (i + 1 < nblocks && lens[i] != bs) || lens[i] > bs) {
-            set_err("kolm_encode_blocks: blocks must be fixed-size and contiguous");
+        if (lens[i] == 0 || starts[i] != starts[0] + total) {
+            set_err("kolm_encode_blocks: blocks must be contiguous and non-empty");
             return KOLM_EARG;
         }
+        if ((i + 1 < nblocks && lens[i] != bs) || lens[i] > bs) fixed = false;
         total += lens[i];
+    }
+    if (total >= (1ull << 31)) {
+        set_err("batch larger than 2^31-1 bytes");
+        return KOLM_EARG;
+    }
+    std::vector<u32> hb;
+    if (!fixed) {
+        hb.resize((size_t)nblocks + 1);
+        hb[0] = 0;
+        for (uint32_t i = 0; i < nblocks; ++i) hb[i + 1] = hb[i] + lens[i];
     }
     return guarded([&] {
         std::lock_guard<std::mutex> g(c->mu);
         KOLM_HIP_CHECK(hipSetDevice(c->device));
-        if (int e = check_geom(total, bs)) return e;
-        u8* d = upload(c, data, total);
+        if (fixed)
+            if (int e = check_geom(total, bs)) return e;
+        u8* d = upload(c, data + (nblocks ? starts[0] : 0), total);
         const bool has_raw = (cand_mask & 1u) && force_method == nullptr;
         const u64 dcap = (has_raw ? total : 9 * total) + 64 * (u64)nblocks + 256;
         u8* arena = c->get<u8>("arena", dcap);
         std::vector<u64> off(nblocks + 1);
-        int r = encode_batch(c, d, total, bs, cand_mask & KOLM_DEFAULT_MASK, force_method, arena, dcap, sizes,
-                             method, off.data(), stats);
+        int r = encode_batch(c, d, total, bs, fixed ? nullptr : hb.data(), nblocks, cand_mask & KOLM_DEFAULT_MASK,
+                             force_method, arena, dcap, sizes, method, off.data(), stats);
         if (r) return r;
         if (off[nblocks] > arena_cap) {
             set_err("payload_arena too small");
@@ -1039,7 +1084,7 @@ int kolm_encode_blocks_multi(int ngpu, const uint8_t* data, uint64_t total, uint
             const u64 dcap = (has_raw ? n : 9 * n) + 64 * (u64)nbr + 256;
             u8* arena = c->get<u8>("arena", dcap);
             P.off.assign(nbr + 1, 0);
-            int rc = encode_batch(c, d, n, block_size, cand_mask & KOLM_DEFAULT_MASK,
+            int rc = encode_batch(c, d, n, block_size, nullptr, 0, cand_mask & KOLM_DEFAULT_MASK,
                                   force_method ? force_method + b0[r] : nullptr, arena, dcap,
                                   sizes ? sizes + (u64)b0[r] * KOLM_NCAND : nullptr, method ? method + b0[r] : nullptr,
                                   P.off.data(), stats ? &P.st : nullptr);
@@ -1102,6 +1147,137 @@ int kolm_encode_blocks_multi(int ngpu, const uint8_t* data, uint64_t total, uint
         *stats = agg;
     }
     return KOLM_OK;
+}
+
+// FastCDC chunk starts of d_text[0, n) followed by n (PY:210-309): device kernels
+// (k_cdc.hip) for the cuts, then the orphan-tail merge (PY:300-306).  Parameter errors
+// carry PY's ValueError messages (PY:227-230).
+static int cdc_bounds(kolm_ctx* c, const u8* d_text, u64 n, u32 mn, u32 av, u32 mx, bool merge,
+                      std::vector<u32>& out) {
+    out.clear();
+    if (n == 0) return KOLM_OK;
+    if (!(mn > 0 && mn <= av && av <= mx)) {
+        set_err("Require 0 < min_size <= avg_size <= max_size");
+        return KOLM_EARG;
+    }
+    if (av < 64) {
+        set_err("avg_size too small; use >= 64");
+        return KOLM_EARG;
+    }
+    if (n >= (1ull << 31)) {
+        set_err("input larger than 2^31-1 bytes");
+        return KOLM_EARG;
+    }
+    int k = 31 - __builtin_clz(av);  // bit_length(avg) - 1, clamped to [6, 20] (PY:172-185)
+    k = k < 6 ? 6 : k > 20 ? 20 : k;
+    const int ks = k + 2 <= 20 ? k + 2 : 20, kl = k > 2 ? k - 2 : 1;  // PY:235-236
+    u32 gear[256];
+    u32 x = 0x243F6A88u;  // PY:152-165 (xorshift32, entries | 1)
+    for (int i = 0; i < 256; ++i) {
+        x ^= x << 13;
+        x ^= x >> 17;
+        x ^= x << 5;
+        gear[i] = x | 1u;
+    }
+    u32* dg = c->get<u32>("cdc_gear", 256);
+    KOLM_HIP_CHECK(hipMemcpyAsync(dg, gear, sizeof gear, hipMemcpyHostToDevice, c->stream));
+    const u64 seg = cdc_segment(av, mx);
+    const u64 nw = (n + 63) / 64, nseg = (n + seg - 1) / seg, nwg = (nw + 255) / 256;
+    const u64 maxcuts = n / mn + 2;
+    CdcParams p{d_text, (u32)n, mn, av, mx, (1u << ks) - 1u, (1u << kl) - 1u};
+    CdcBufs b{dg,
+              c->get<u64>("cdc_ws", nw),
+              c->get<u64>("cdc_wl", nw),
+              c->get<u64>("cdc_c", nw),
+              c->get<u64>("cdc_f", nw),
+              c->get<u32>("cdc_exit", nseg),
+              c->get<u32>("cdc_join", nseg),
+              c->get<u32>("cdc_wg", nwg),
+              c->get<u32>("cdc_cuts", maxcuts),
+              c->get<u32>("counters", C_N) + C_CDC};
+    launch_cdc(p, b, c->stream, c->kt());
+    KOLM_HIP_CHECK(hipMemcpyAsync(c->h_cnt + C_CDC, b.total, sizeof(u32), hipMemcpyDeviceToHost, c->stream));
+    c->sync();
+    const u32 total = c->h_cnt[C_CDC];
+    if (total > maxcuts) {
+        set_err("internal error: FastCDC cut count");
+        return KOLM_EHIP;
+    }
+    out.resize((size_t)total + 2);
+    out[0] = 0;
+    if (total) KOLM_HIP_CHECK(hipMemcpy(out.data() + 1, b.cuts, sizeof(u32) * total, hipMemcpyDeviceToHost));
+    out[total + 1] = (u32)n;
+    if (merge && out.size() >= 3 && out[out.size() - 1] - out[out.size() - 2] < mn) out.erase(out.end() - 2);
+    if (c->timing) {
+        kolm_stats tmp{};
+        c->timing_collect(&tmp);  // per-kernel totals (kolm_ctx_kernel_times)
+    }
+    return KOLM_OK;
+}
+
+int kolm_cdc_boundaries(const uint8_t* data, uint64_t n, uint32_t min_size, uint32_t avg_size, uint32_t max_size,
+                        int merge_orphan_tail, uint64_t* starts, uint64_t cap, uint64_t* nchunks) {
+    kolm_ctx* c = need_default();
+    if (!c) return KOLM_ENOINIT;
+    if ((n && (!data || !starts)) || !nchunks) return KOLM_EARG;
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        c->timing_reset();
+        const u8* d = (n && n < (1ull << 31)) ? upload(c, data, n) : nullptr;
+        std::vector<u32> v;
+        if (int e = cdc_bounds(c, d, n, min_size, avg_size, max_size, merge_orphan_tail != 0, v)) return e;
+        *nchunks = v.empty() ? 0 : v.size() - 1;
+        if (v.size() > cap) {
+            set_err("starts capacity too small");
+            return KOLM_ECAP;
+        }
+        for (size_t i = 0; i < v.size(); ++i) starts[i] = v[i];
+        return KOLM_OK;
+    });
+}
+
+int kolm_cdc_boundaries_device(kolm_ctx* c, const uint8_t* d_data, uint64_t n, uint32_t min_size, uint32_t avg_size,
+                               uint32_t max_size, int merge_orphan_tail, uint32_t* h_starts, uint64_t cap,
+                               uint64_t* nchunks) {
+    if (!c || (n && (!d_data || !h_starts)) || !nchunks) return KOLM_EARG;
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        c->timing_reset();
+        std::vector<u32> v;
+        if (int e = cdc_bounds(c, d_data, n, min_size, avg_size, max_size, merge_orphan_tail != 0, v)) return e;
+        *nchunks = v.empty() ? 0 : v.size() - 1;
+        if (v.size() > cap) {
+            set_err("starts capacity too small");
+            return KOLM_ECAP;
+        }
+        if (!v.empty()) std::memcpy(h_starts, v.data(), sizeof(u32) * v.size());
+        return KOLM_OK;
+    });
+}
+
+int kolm_encode_blocks_device_var(kolm_ctx* c, const uint8_t* d_data, const uint32_t* h_bounds, uint32_t nblocks,
+                                  uint32_t cand_mask, const int32_t* force_method, uint8_t* d_arena,
+                                  uint64_t arena_cap, uint32_t* h_sizes, uint32_t* h_method, uint64_t* h_off,
+                                  kolm_stats* stats) {
+    if (!c || !h_bounds || !d_arena || (nblocks && !d_data)) return KOLM_EARG;
+    if ((cand_mask & KOLM_DEFAULT_MASK) == 0) return KOLM_EARG;
+    if (reinterpret_cast<uintptr_t>(d_arena) & 3) {
+        set_err("device arena must be 4-byte aligned");
+        return KOLM_EARG;
+    }
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        if (nblocks == 0) {
+            if (h_off) h_off[0] = 0;
+            if (stats) *stats = kolm_stats{};
+            return KOLM_OK;
+        }
+        return encode_batch(c, d_data, 0, 0, h_bounds, nblocks, cand_mask & KOLM_DEFAULT_MASK, force_method, d_arena,
+                            arena_cap, h_sizes, h_method, h_off, stats);
+    });
 }
 
 int kolm_bbwt_forward(const uint8_t* in, size_t n, uint8_t* out) {
@@ -1218,7 +1394,7 @@ int kolm_bbwt_mtf_rice(const uint8_t* in, size_t n, int flags, int k, uint8_t* o
         const u64 dcap = 9 * n + 256;
         u8* arena = c->get<u8>("arena", dcap);
         std::vector<u64> off(2);
-        int r = encode_batch(c, d, n, (u32)n, 1u << force, &force, arena, dcap, nullptr, nullptr,
+        int r = encode_batch(c, d, n, (u32)n, nullptr, 0, 1u << force, &force, arena, dcap, nullptr, nullptr,
                              off.data(), nullptr);
         if (r) return r;
         if (out_len) *out_len = off[1];

@@ -49,24 +49,63 @@ struct LTile {
     u32 k;
 };
 
-// Fixed-size block geometry of a batch + a fast u32 division by bs.
+// Block geometry of a batch.  Fixed mode (vb == null): blocks of bs bytes (the last may be
+// short), block_of by a fast u32 division.  Variable mode (content-defined chunks, PY:2213):
+// block b = [vb[b], vb[b+1]), bs = the longest block (it sizes the per-block tile/chunk
+// counts; the tiles past a shorter block's end are empty), block_of by a granule map
+// (vmap[g >> vshift] = block of the granule's first position) plus a short forward walk.
+// Every kernel addresses blocks through base()/end()/block_of() only.
 struct Geom {
     u64 N;        // total bytes (< 2^31)
-    u32 bs;       // block size
+    u32 bs;       // block size (variable mode: longest block)
     u32 nb;       // number of blocks
     u64 magic;    // fastdiv: block_of(g) = g * magic >> shift, exact for g < 2^31
     u32 shift;
+    const u32* vb = nullptr;    // variable mode: device bounds [nb + 1]
+    const u32* hvb = nullptr;   // variable mode: the same bounds in host memory
+    const u32* vmap = nullptr;  // variable mode: device granule -> block map
+    u32 vshift = 0;
+    __host__ __device__ inline const u32* bounds() const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        return vb;
+#else
+        return hvb;
+#endif
+    }
     __host__ __device__ inline u32 block_of(u32 g) const {
+        if (const u32* v = bounds()) {
+#if defined(__HIP_DEVICE_COMPILE__)
+            u32 b = vmap[g >> vshift];
+#else
+            u32 lo = 0, hi = nb;  // host: binary search (no host copy of the map)
+            while (hi - lo > 1) {
+                const u32 m = (lo + hi) >> 1;
+                if (v[m] <= g) lo = m; else hi = m;
+            }
+            u32 b = lo;
+#endif
+            while (v[b + 1] <= g) ++b;
+            return b;
+        }
         return (u32)(((u64)g * magic) >> shift);
     }
-    __host__ __device__ inline u32 base(u32 b) const { return b * bs; }
+    __host__ __device__ inline u32 base(u32 b) const {
+        if (const u32* v = bounds()) return v[b];
+        return b * bs;
+    }
     __host__ __device__ inline u32 end(u32 b) const {
+        if (const u32* v = bounds()) return v[b + 1];
         u64 e = (u64)(b + 1) * bs;
         return (u32)(e < N ? e : N);
     }
 };
 
 void geom_init(Geom& g, u64 N, u32 bs);
+// Variable-mode geometry over host bounds hb[0..nb] (hb[0] = 0, strictly increasing,
+// hb[nb] = N < 2^31); d_vb / d_vmap hold nb + 1 and (N >> vshift) + 1 words.  Blocking
+// upload + map build on stream s; hb must outlive every host use of the geometry.
+void geom_init_var(Geom& g, const u32* hb, u32 nb, u32* d_vb, u32* d_vmap, u32 vshift, hipStream_t s);
+u32 geom_var_shift(const u32* hb, u32 nb);
 
 // ---- wave64 scans on DPP (gfx9 row shifts + row broadcasts): VALU only, no LDS permute
 // (__shfl_up/__shfl_xor compile to ds_bpermute + address math per step) ----
@@ -136,7 +175,8 @@ struct KScope {
         if (t) t->end();
     }
 };
-enum : int { KT_CLASSIFY = 0, KT_KEYGEN, KT_MSD, KT_SMALLSORT, KT_LSD, KT_LZPARSE, KT_MTF, KT_SIZES, KT_EMIT, KT_LYNDON };
+enum : int { KT_CLASSIFY = 0, KT_KEYGEN, KT_MSD, KT_SMALLSORT, KT_LSD, KT_LZPARSE, KT_MTF, KT_SIZES, KT_EMIT, KT_LYNDON,
+             KT_REPAIR, KT_CDC };
 
 // XCD-aware workgroup -> tile remap (speed only, never correctness): workgroups are dealt
 // round-robin over the 8 XCDs, so give each XCD a contiguous range of tiles — tiles of
@@ -326,6 +366,24 @@ constexpr u32 RP_P_N = 11;
 u64 repair_ws_bytes(u32 bs);
 void launch_repair(const RpArgs& a, u32 b0, u32 nblk, hipStream_t s);
 void launch_rp_emit(const RpArgs& a, const u32* method, const u64* off, u8* arena, hipStream_t s);
+
+// ---- k_cdc.hip: FastCDC chunk boundaries (PY:140-309) ----
+struct CdcParams {
+    const u8* d;     // device text
+    u32 n;           // bytes (< 2^31)
+    u32 mn, av, mx;  // min / avg / max chunk size (validated by the caller, PY:227-230)
+    u32 ms, ml;      // MaskS / MaskL (PY:233-240)
+};
+struct CdcBufs {
+    const u32* gear;       // [256] PY's GEAR table (PY:152-167)
+    u64 *WS, *WL, *C, *F;  // [nw = ceil(n / 64)] bitmaps
+    u32 *exitp, *join;     // [nseg = ceil(n / cdc_segment(avg, max))]
+    u32* wgcnt;            // [ceil(nw / 256)]
+    u32* cuts;             // [n / mn + 2] out: cut positions (chunk starts after 0), ascending
+    u32* total;            // [1] out: number of cuts
+};
+u32 cdc_segment(u32 avg, u32 mx);
+void launch_cdc(const CdcParams& p, const CdcBufs& b, hipStream_t s, KTimer* kt = nullptr);
 
 }  // namespace kolm
 

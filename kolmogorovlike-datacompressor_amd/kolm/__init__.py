@@ -3,6 +3,8 @@
 Drop-in for the reference's block API (PY = final_researched/kolm_final_researched_v2-2.py):
 
     compress_blocks_fixed(data, block_size=8192) -> bytes      PY:2332-2445
+    compress_blocks_cdc(data, min_size, avg_size, max_size)    PY:2213-2326
+    cdc_fast_boundaries_strict(data, min, avg, max, merge)     PY:210-309
     decompress(container) -> bytes                             PY:2451-2550
     _select_encoders() / _select_decoders()                    PY:2152-2207
     bbwt_forward, mtf_encode, rice_encode, encode_lz77,
@@ -35,7 +37,8 @@ from .container import (MODE_CDC, MODE_FIXED, read_container, uleb128_decode_str
 from .decode import decode_block
 
 __all__ = [
-    "compress_blocks_fixed", "decompress", "fixed_boundaries", "bbwt_forward", "mtf_encode",
+    "compress_blocks_fixed", "compress_blocks_cdc", "cdc_fast_boundaries_strict", "decompress",
+    "fixed_boundaries", "bbwt_forward", "mtf_encode",
     "rice_encode", "encode_lz77", "encode_bbwt_mtf_rice", "encode_raw", "encode_xor",
     "encode_lfsr_predict", "repair_compress", "uleb128_encode", "uleb128_decode_stream", "CANDIDATE_NAMES",
     "KolmUnavailable", "KolmError", "last_stats",
@@ -69,6 +72,30 @@ def fixed_boundaries(data: bytes, block_size: int = 8192) -> List[Tuple[int, int
     if block_size <= 0:
         raise ValueError("block_size must be positive")
     return [(i, min(n, i + block_size)) for i in range(0, n, block_size)]
+
+
+_U31 = 0x7FFFFFFF
+
+
+def cdc_fast_boundaries_strict(data: bytes, min_size: int = 4096, avg_size: int = 8192, max_size: int = 16384,
+                               merge_orphan_tail: bool = True) -> List[Tuple[int, int]]:
+    """FastCDC with normalized chunking (PY:210-309) on the GPU (k_cdc.hip), same chunks.
+
+    Note (parity): PY's GEAR entries are all odd (PY:164), so the rolled fingerprint is
+    always odd and no mask test ever passes: the reference cuts every chunk at
+    min(remaining, max_size) and only the tail rule varies.  The device path evaluates the
+    masks as the reference does and reproduces exactly that."""
+    n = len(data)
+    if n == 0:
+        return []
+    if not (min_size > 0 and min_size <= avg_size <= max_size):
+        raise ValueError("Require 0 < min_size <= avg_size <= max_size")
+    if avg_size < 64:
+        raise ValueError("avg_size too small; use >= 64")
+    # sizes past 2^31 act as 2^31 - 1 (n < 2^31; the mask bits clamp at 20 either way)
+    mn, av, mx = min(min_size, _U31), min(avg_size, _U31), min(max_size, _U31)
+    s = _lib.cdc_boundaries(bytes(data), mn, av, mx, merge_orphan_tail)
+    return [(int(s[i]), int(s[i + 1])) for i in range(len(s) - 1)]
 
 
 # ---------------------------------------------------------------------------
@@ -236,6 +263,25 @@ def compress_blocks_fixed(data: bytes, block_size: int = 8192, devices: int = 1,
         raise struct.error("'H' format requires 0 <= number <= 65535")
     mids, orig, payloads, _ = encode_blocks(data, block_size, devices=devices, hot_path=hot_path)
     return write_container(MODE_FIXED, block_size, n, mids, orig, payloads)
+
+
+def compress_blocks_cdc(data: bytes, min_size: int = 4096, avg_size: int = 8192, max_size: int = 16384,
+                        hot_path: bool = False) -> bytes:
+    """FastCDC chunking + per-block MDL selection + KOLR container in CDC mode
+    (PY:2213-2326): boundaries and every candidate on the GPU, one batched device call for
+    all chunks (variable block geometry), the TOC on the host.  `hot_path` (not in PY)
+    restricts the candidates to ids 0..8."""
+    global _last_stats
+    bounds = cdc_fast_boundaries_strict(data, min_size, avg_size, max_size)
+    if len(bounds) > 0xFFFF:  # PY packs the block count as '<H' before encoding (PY:2222)
+        raise struct.error("'H' format requires 0 <= number <= 65535")
+    n = len(data)
+    if n == 0:
+        return write_container(MODE_CDC, avg_size, 0, [], [], [])
+    edges = [s for s, _ in bounds] + [n]
+    _, method, payloads, st = _lib.encode_blocks_var(bytes(data), edges, candidate_mask(hot_path))
+    _last_stats = st
+    return write_container(MODE_CDC, avg_size, n, [int(m) for m in method], [e - s for s, e in bounds], payloads)
 
 
 def decompress(container: bytes) -> bytes:

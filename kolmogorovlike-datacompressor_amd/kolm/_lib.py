@@ -38,7 +38,7 @@ class KolmError(RuntimeError):
 
 
 KT_NAMES = ["classify", "keygen", "msd", "small_sort", "lsd", "lz_parse", "mtf", "sizes", "emit",
-            "lyndon_gather", "repair"]
+            "lyndon_gather", "repair", "cdc"]
 
 
 class KTime(ctypes.Structure):
@@ -107,6 +107,9 @@ SIGNATURES = [
     ("kolm_ctx_set_timing", I32, [P, I32]),
     ("kolm_ctx_kernel_times", I32, [P, P, SZ, ctypes.POINTER(SZ)]),
     ("kolm_encode_blocks_device", I32, [P, P, U64, U32, U32, P, P, U64, P, P, P, P]),
+    ("kolm_encode_blocks_device_var", I32, [P, P, P, U32, U32, P, P, U64, P, P, P, P]),
+    ("kolm_cdc_boundaries", I32, [U8P, U64, U32, U32, U32, I32, P, U64, ctypes.POINTER(U64)]),
+    ("kolm_cdc_boundaries_device", I32, [P, P, U64, U32, U32, U32, I32, P, U64, ctypes.POINTER(U64)]),
 ]
 
 
@@ -243,6 +246,50 @@ def encode_blocks(data: bytes, block_size: int, cand_mask: int = KOLM_DEFAULT_MA
         ctypes.byref(st)))
     payloads = [arena[int(off[i]):int(off[i + 1])].tobytes() for i in range(nb)]
     return sizes[:nb], method[:nb], payloads, st.as_dict()
+
+
+def encode_blocks_var(data: bytes, bounds, cand_mask: int = KOLM_DEFAULT_MASK, force=None):
+    """Batched MDL encode of content-defined blocks: block i = data[bounds[i]:bounds[i+1]]
+    (bounds[0] = 0, strictly increasing, bounds[-1] = len(data)).  Same return value as
+    encode_blocks."""
+    ensure_init()
+    b = np.ascontiguousarray(np.asarray(bounds, dtype=np.uint64))
+    nb = max(len(b) - 1, 0)
+    if nb and (b[0] != 0 or int(b[-1]) != len(data) or np.any(np.diff(b.astype(np.int64)) <= 0)):
+        raise ValueError("bounds must start at 0, increase strictly and end at len(data)")
+    starts = np.ascontiguousarray(b[:-1]) if nb else np.zeros(0, np.uint64)
+    lens = np.ascontiguousarray(np.diff(b).astype(np.uint32)) if nb else np.zeros(0, np.uint32)
+    n = len(data)
+    sizes = np.zeros((max(nb, 1), KOLM_NCAND), dtype=np.uint32)
+    method = np.zeros(max(nb, 1), dtype=np.uint32)
+    off = np.zeros(nb + 1, dtype=np.uint64)
+    cap = 9 * n + 64 * nb + 64
+    arena = np.zeros(cap, dtype=np.uint8)
+    fz = None
+    if force is not None:
+        fz = np.ascontiguousarray(np.asarray(force, dtype=np.int32))
+        if fz.shape != (nb,):
+            raise ValueError("force must have one entry per block")
+    st = Stats()
+    check(load().kolm_encode_blocks(
+        data, starts.ctypes.data, lens.ctypes.data, nb, cand_mask,
+        fz.ctypes.data if fz is not None else None,
+        sizes.ctypes.data, method.ctypes.data, arena.ctypes.data, cap, off.ctypes.data,
+        ctypes.byref(st)))
+    payloads = [arena[int(off[i]):int(off[i + 1])].tobytes() for i in range(nb)]
+    return sizes[:nb], method[:nb], payloads, st.as_dict()
+
+
+def cdc_boundaries(data: bytes, min_size: int, avg_size: int, max_size: int, merge_orphan_tail: bool = True):
+    """FastCDC chunk starts followed by len(data) (kolm_cdc_boundaries, PY:210-309)."""
+    ensure_init()
+    n = len(data)
+    cap = n // max(min_size, 1) + 3
+    starts = np.zeros(cap, dtype=np.uint64)
+    cnt = ctypes.c_uint64(0)
+    check(load().kolm_cdc_boundaries(data, n, min_size, avg_size, max_size, 1 if merge_orphan_tail else 0,
+                                     starts.ctypes.data, cap, ctypes.byref(cnt)))
+    return starts[:cnt.value + 1] if cnt.value else starts[:0]
 
 
 def encode_blocks_multi(data: bytes, block_size: int, ngpu: int, cand_mask: int = KOLM_DEFAULT_MASK):

@@ -51,6 +51,8 @@ def lib():
         L.oracle_candidate.restype = i64
         L.oracle_repair_fast.argtypes = [P, i64, ctypes.c_void_p, i64, ctypes.c_void_p]
         L.oracle_repair_fast.restype = i64
+        L.oracle_cdc.argtypes = [P, i64, i64, i64, i64, ctypes.c_int, ctypes.c_void_p, i64]
+        L.oracle_cdc.restype = i64
         _lib = L
     return _lib
 
@@ -114,6 +116,24 @@ def repair_fast(block: bytes, with_stats: bool = False):
     if r < 0:
         raise RuntimeError(f"oracle call failed ({r})")
     return (buf.raw[:r], tuple(st)) if with_stats else buf.raw[:r]
+
+
+def cdc_boundaries(data: bytes, min_size: int = 4096, avg_size: int = 8192, max_size: int = 16384,
+                   merge_orphan_tail: bool = True) -> List[Tuple[int, int]]:
+    """FastCDC chunks (PY:210-309) by cdc_oracle.cpp; PY's ValueErrors (PY:227-230)."""
+    n = len(data)
+    if n == 0:
+        return []
+    if not (min_size > 0 and min_size <= avg_size <= max_size):
+        raise ValueError("Require 0 < min_size <= avg_size <= max_size")
+    if avg_size < 64:
+        raise ValueError("avg_size too small; use >= 64")
+    cap = n // min_size + 2
+    arr = (ctypes.c_int64 * (2 * cap))()
+    r = lib().oracle_cdc(data, n, min_size, avg_size, max_size, 1 if merge_orphan_tail else 0, arr, cap)
+    if r < 0:
+        raise RuntimeError(f"oracle_cdc failed ({r})")
+    return [(arr[2 * i], arr[2 * i + 1]) for i in range(r)]
 
 
 BBWT_FLAGS = (0, 1, 4, 8, 16)  # candidates 2..6 (PY:2156-2160)
@@ -281,11 +301,16 @@ def rle_ids(ids):  # PY:1403-1410
     return syms, runs
 
 
+def zz_enc(x: int) -> int:  # PY:1261-1262
+    return (x << 1) if x >= 0 else ((-x) << 1) - 1
+
+
 def write_container_fixed(total_len: int, block_size: int, method_ids: Sequence[int],
-                          orig_lens: Sequence[int], payloads: Sequence[bytes]) -> bytes:
-    """PY:2332-2445 (FIXED mode) given the per-block MDL winners."""
+                          orig_lens: Sequence[int], payloads: Sequence[bytes], cdc: bool = False) -> bytes:
+    """PY:2332-2445 (FIXED mode) given the per-block MDL winners; cdc=True: PY:2213-2326
+    (CDC mode, block_size = avg_size: mode bit, ZigZag/Rice orig-length deltas)."""
     out = bytearray(b"KOLR")
-    out += struct.pack("<I", block_size & 0x7FFFFFFF)
+    out += struct.pack("<I", ((1 << 31) if cdc else 0) | (block_size & 0x7FFFFFFF))
     out += struct.pack("<I", total_len)
     out += struct.pack("<H", len(method_ids))
     payload_lens = [len(p) for p in payloads]
@@ -306,12 +331,26 @@ def write_container_fixed(total_len: int, block_size: int, method_ids: Sequence[
     for sym, L in sorted(lengths.items(), key=lambda kv: (kv[1], kv[0])):
         hdr += uleb128(sym) + uleb128(L)
     hdr += uleb128(best_k)
-    hdr += uleb128(orig_lens[-1] if orig_lens else 0)
+    deltas = None
+    if not cdc:
+        hdr += uleb128(orig_lens[-1] if orig_lens else 0)
+    else:
+        deltas = [zz_enc(ol - block_size) for ol in orig_lens]
+        best_k2, best_bits2 = 0, 1 << 60
+        for k in range(8):
+            bw = _Bits()
+            rice_write(bw, deltas, k)
+            _, bits = bw.value()
+            if bits < best_bits2:
+                best_bits2, best_k2 = bits, k
+        hdr += uleb128(best_k2)
     bw = _Bits()
     for s in run_syms:
         c, L = enc_tbl[s]
         bw.kbits(c, L)
     rice_write(bw, run_lens, best_k)
+    if deltas is not None:
+        rice_write(bw, deltas, best_k2)
     P, acc = [], 0
     for L in payload_lens:
         acc += L
@@ -342,6 +381,23 @@ def compress_blocks_fixed(data: bytes, block_size: int = 8192, ids: Sequence[int
         lens.append(len(block))
         pays.append(best[0])
     return write_container_fixed(n, block_size, mids, lens, pays)
+
+
+def compress_blocks_cdc(data: bytes, min_size: int = 4096, avg_size: int = 8192, max_size: int = 16384,
+                        ids: Sequence[int] = range(9)) -> bytes:
+    """Oracle compress in CDC mode (PY:2213-2326): FastCDC chunks, per-chunk MDL argmin."""
+    mids, lens, pays = [], [], []
+    for s, e in cdc_boundaries(data, min_size, avg_size, max_size):
+        block = data[s:e]
+        best = None
+        for mid in ids:
+            p = candidate(mid, block)
+            if best is None or len(p) < len(best[0]):
+                best = (p, mid)
+        mids.append(best[1])
+        lens.append(len(block))
+        pays.append(best[0])
+    return write_container_fixed(len(data), avg_size, mids, lens, pays, cdc=True)
 
 
 FNV_OFFSET = 0xCBF29CE484222325

@@ -41,9 +41,9 @@ def test_ctypes_signatures_cover_header():
 
 
 def test_stats_struct_size_matches_header():
-    # kolm_stats: 2 u32 + 4 u64 + 5 double + KOLM_NKT(11) x {double, u64, u64} + double + 3 u64
+    # kolm_stats: 2 u32 + 4 u64 + 5 double + KOLM_NKT(12) x {double, u64, u64} + double + 3 u64
     nkt = int(re.search(r"#define KOLM_NKT (\d+)", open(HEADER).read()).group(1))
-    assert nkt == len(_lib.KT_NAMES) == 11
+    assert nkt == len(_lib.KT_NAMES) == 12
     assert ctypes.sizeof(_lib.Stats) == 8 + 4 * 8 + 5 * 8 + nkt * 24 + 8 + 3 * 8
 
 
