@@ -125,6 +125,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--full-steps", type=int, default=2,
                     help="timed steps of the full candidate list 0..9 (Re-Pair included); 0 = skip")
+    ap.add_argument("--cdc-steps", type=int, default=2,
+                    help="timed steps of the content-defined (FastCDC) mode; 0 = skip")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -251,6 +253,51 @@ def main():
         method[:] = method_hot
         off[:] = off_hot
 
+    # Content-defined mode (compress_blocks_cdc, PY:2213-2326): FastCDC boundaries on the
+    # device (PY's default 4096/8192/16384) + candidates 0..8 over the variable-length
+    # chunks, same resident data, same timing discipline; reported beside the value.
+    cdc = None
+    if a.cdc_steps > 0:
+        ccap = n // 4096 + 3
+        hst = np.zeros(ccap, np.uint32)
+        nch = ctypes.c_uint64(0)
+        csz = np.zeros((ccap, _lib.KOLM_NCAND), np.uint32)
+        cmeth = np.zeros(ccap, np.uint32)
+        coff = np.zeros(ccap + 1, np.uint64)
+        cst = {}
+
+        def cdc_step():
+            t_b = time.perf_counter()
+            _lib.check(L.kolm_cdc_boundaries_device(ctx, d_in.data_ptr(), n, 4096, 8192, 16384, 1, hst.ctypes.data,
+                                                    ccap, ctypes.byref(nch)))
+            cst["ms_bounds"] = (time.perf_counter() - t_b) * 1e3
+            st = _lib.Stats()
+            _lib.check(L.kolm_encode_blocks_device_var(ctx, d_in.data_ptr(), hst.ctypes.data, int(nch.value),
+                                                       _lib.KOLM_HOTPATH_MASK, None, arena.data_ptr(), cap,
+                                                       csz.ctypes.data, cmeth.ctypes.data, coff.ctypes.data,
+                                                       ctypes.byref(st)))
+
+        cdc_step()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.cdc_steps):
+            cdc_step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elc = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([elc], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elc = float(tt[0])
+        nbc = int(nch.value)
+        cdc = {"value": round(world * n * a.cdc_steps / elc / MB, 2), "unit": "MB/s", "steps": a.cdc_steps,
+               "ms_per_step": round(elc / a.cdc_steps * 1e3, 2), "ms_boundaries": round(cst["ms_bounds"], 2),
+               "params": [4096, 8192, 16384], "chunks_per_gpu": nbc, "candidates": "0..8",
+               "ratio": round(float(coff[nbc]) / n, 4)}
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(data, a.bs, a.cpu_budget)
@@ -273,6 +320,7 @@ def main():
             "detail": {"ratio": round(float(off[-1]) / n, 4),
                        "methods": np.bincount(method, minlength=10).tolist(),
                        "full_candidates": full,
+                       "cdc_mode": cdc,
                        "device_ms": {k: round(s0[k], 2) for k in ("ms_total", "ms_sa", "ms_lz", "ms_entropy", "ms_emit")},
                        "rounds": [s0["lin_rounds"], s0["cyc_rounds"]],
                        "pipeline_roofline": pipe,
