@@ -220,6 +220,25 @@ __global__ __launch_bounds__(WG) void k_g3_tiles_scan(const u32* in, u32* out, u
     }
 }
 
+// the thread's 16 consecutive words X[i0 .. i0+15] (0 past hi): four 16-byte loads when
+// aligned and whole (the 16 scalar loads per array were 48 read instructions per wave)
+__device__ inline void load16(const u32* X, u32 i0, u32 hi, u32 (&v)[G3PT]) {
+    if ((i0 & 3) == 0 && i0 + G3PT <= hi) {
+        const uint4* p = reinterpret_cast<const uint4*>(X + i0);
+#pragma unroll
+        for (int q = 0; q < (int)G3PT / 4; ++q) {
+            const uint4 t = p[q];
+            v[4 * q] = t.x;
+            v[4 * q + 1] = t.y;
+            v[4 * q + 2] = t.z;
+            v[4 * q + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (u32 e = 0; e < G3PT; ++e) v[e] = i0 + e < hi ? X[i0 + e] : 0u;
+    }
+}
+
 // per slot: group start, inverse permutation; tail slots hold their own position
 __global__ __launch_bounds__(WG) void k_g3_final(G3Geom g, const u32* K, u32* SA3, const u32* tcarry, uint2* ig3) {
     __shared__ u32 sh[WG / 64];
@@ -228,12 +247,18 @@ __global__ __launch_bounds__(WG) void k_g3_final(G3Geom g, const u32* K, u32* SA
     const u32 base = g.geo.base(b), fe = g.fend(b);
     const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const u32 i0 = lo + threadIdx.x * G3PT;
+    u32 kv[G3PT], sv[G3PT];
+    load16(K, i0, hi, kv);
+    load16(SA3, i0, hi, sv);
+    u32 kprev = (i0 > base && i0 < hi) ? K[i0 - 1] : 0u;
     u32 hd[G3PT];
     u32 loc = 0;
 #pragma unroll
     for (u32 e = 0; e < G3PT; ++e) {
         const u32 i = i0 + e;
-        hd[e] = (i < hi && g3_head(g, K, i, base, fe)) ? 1u : 0u;
+        // g3_head: first slot of the block, a tail slot, or a new 3-gram
+        hd[e] = (i < hi && (i == base || i >= fe || kv[e] != kprev)) ? 1u : 0u;
+        kprev = kv[e];
         if (hd[e]) loc = max(loc, i);
     }
     const u32 incl = wave_incl_scan(loc, OpMaxU(), 0u);
@@ -252,7 +277,7 @@ __global__ __launch_bounds__(WG) void k_g3_final(G3Geom g, const u32* K, u32* SA
                 p = i;
                 SA3[i] = i;
             } else {
-                p = SA3[i];
+                p = sv[e];
             }
             ig3[p] = make_uint2(i, run);  // one 8-byte scattered store
         }
@@ -332,12 +357,17 @@ __global__ __launch_bounds__(WG) void k_r0_final(G3Geom g, const u32* K, const u
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid == 0) anysplit = 0;
     const u32 i0 = lo + tid * G3PT;
+    u32 kv[G3PT], sv[G3PT];
+    load16(K, i0, hi, kv);
+    load16(SA, i0, hi, sv);
+    u32 kprev = (i0 > base && i0 < hi) ? K[i0 - 1] : 0u;
     bool hd[G3PT];
     u32 lmax = 0, lmin = BIG;
 #pragma unroll
     for (u32 e = 0; e < G3PT; ++e) {
         const u32 i = i0 + e;
-        hd[e] = i < hi && r0_head(K, i, base);
+        hd[e] = i < hi && (i == base || kv[e] != kprev);  // r0_head
+        kprev = kv[e];
         if (hd[e]) {
             lmax = max(lmax, i);
             lmin = min(lmin, i);
@@ -365,7 +395,7 @@ __global__ __launch_bounds__(WG) void k_r0_final(G3Geom g, const u32* K, const u
                 run = i;
                 split |= i != base;
             }
-            RK[SA[i]] = run;
+            RK[sv[e]] = run;
         }
     }
     // group lengths (backwards) and next-round segments, one global atomic per workgroup
