@@ -46,6 +46,7 @@ constexpr u32 NT = 1024;          // threads of the block's workgroup
 constexpr u32 W = 512;            // max rounds (members) per batch
 constexpr u32 CAPR = 1u << 16;    // occurrence-region entries per batch beyond its first member
 constexpr u32 SORT_LDS = 4096;    // level lists up to this size are sorted in LDS
+constexpr u32 QLIM = 4096;        // level cache: the rescan picks flow so that Q holds <= QLIM pairs
 constexpr u32 NIL = 0xFFFFFFFFu;
 constexpr u32 DEAD = 0xFFFFFFFFu;
 constexpr u64 EMPTY = ~0ull;
@@ -78,6 +79,7 @@ struct Block {
     u32 hmask;
     u32* husd;
     u64* rules;
+    u32 *qa, *qb;  // level cache (PC entries each)
     u8* out;
     u64 out_cap;
     u32* result;  // RS_N words
@@ -93,6 +95,7 @@ struct Shared {
     u32 sval[SORT_LDS];
     u32 f, lp, lsize, M, V, T, tot, nocc, npairs, next_sym, nrules, pool, batch, hused, nlate;
     u32 t1, t2, ts, any_aa, cut, maxc, err, total, levels;
+    u32 flow, qn, qn2, qvalid;  // level cache: Q = every pair with count >= flow
 };
 
 // Carve a block's workspace out of `base` (nullptr: size query).  Returns the bytes
@@ -125,6 +128,8 @@ RP_HD inline u64 workspace_layout(char* base, u32 n, Block& B) {
     B.hval = (u32*)take((u64)HS * 4);
     B.hmask = HS - 1;
     B.rules = (u64*)take((N / 2 + 16) * 8);
+    B.qa = (u32*)take(PC * 4);
+    B.qb = (u32*)take(PC * 4);
     return off;
 }
 
@@ -153,21 +158,32 @@ RP_HD inline u32 uleb_put(u8* o, u32 v) {
     }
 }
 
+// The batch's table of new pair keys.  Every new pair contains a symbol created by this
+// batch, so no earlier batch can hold its key: the table only deduplicates within the
+// batch.  Small batches use the workgroup's LDS (the sort buffers, idle between the
+// window and the late merge); large ones the block's global table (cleared via husd).
+struct HTab {
+    u64* k;
+    u32* v;
+    u32 mask;
+    bool glob;
+};
+
 // Insert key into the batch's hash table; returns its slot.  The thread whose CAS wins
-// allocates the pair id (read back from hval[slot] after the next barrier).
+// allocates the pair id (read back from v[slot] after the next barrier).
 template <class E>
-RP_HD inline u32 hash_insert(E& ex, const Block& B, Shared& sh, u64 key) {
-    u32 s = hslot(key, B.hmask);
+RP_HD inline u32 hash_insert(E& ex, const Block& B, Shared& sh, const HTab& h, u64 key) {
+    u32 s = hslot(key, h.mask);
     for (;;) {
-        const u64 cur = B.hkey[s];
+        const u64 cur = h.k[s];
         if (cur == key) return s;
         if (cur == EMPTY) {
-            const u64 old = ex.cas64(&B.hkey[s], EMPTY, key);
+            const u64 old = ex.cas64(&h.k[s], EMPTY, key);
             if (old == EMPTY) {
                 const u32 u = ex.add(&sh.hused, 1u);
                 const u32 id = sh.npairs + u;
-                B.husd[u] = s;
-                B.hval[s] = id;
+                if (h.glob) B.husd[u] = s;
+                h.v[s] = id;
                 B.pkey[id] = key;
                 B.cnt[id] = 0;
                 B.plen[id] = 0;
@@ -175,7 +191,7 @@ RP_HD inline u32 hash_insert(E& ex, const Block& B, Shared& sh, u64 key) {
             }
             if (old == key) return s;
         }
-        s = (s + 1) & B.hmask;
+        s = (s + 1) & h.mask;
     }
 }
 
@@ -299,6 +315,7 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
         if (t == 0) {
             sh.pool = 0; sh.npairs = NBASE; sh.next_sym = 256; sh.nrules = 0; sh.batch = 0;
             sh.lp = 0; sh.lsize = 0; sh.f = 0; sh.hused = 0; sh.nlate = 0; sh.err = RE_OK; sh.levels = 0;
+            sh.qvalid = 0; sh.qn = 0; sh.flow = NIL;
         }
     });
     ex.par([&](u32 t) {
@@ -332,6 +349,8 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
     u32* li = B.liA;
     u64* tk = B.lkB;
     u32* ti = B.liB;
+    u32* qa = B.qa;  // level cache Q (and its compaction target)
+    u32* qb = B.qb;
     u32 guard = 0;
     // ---------------- batches ----------------
     for (;;) {
@@ -341,40 +360,113 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
         }
         if (sh.lp >= sh.lsize) {
             ex.mark(P_LVSCAN);
-            // new level: f = max count; the level list = pairs with count f, sorted
-            ex.par([&](u32 t) { if (t == 0) sh.maxc = 0; });
-            ex.par([&](u32 t) {
-                // 8 independent loads in flight per thread (a loop-carried max would wait on each)
-                u32 m = 0;
-                const u32 np = sh.npairs;
-                for (u32 i0 = t; i0 < np; i0 += 8 * NT) {
-                    u32 v[8];
+            // new level: f = max count; the level list = pairs with count f, sorted.  The
+            // candidates come from the level cache Q, which holds every pair whose count
+            // is >= flow: counts never rise except at creation, and created pairs with a
+            // count >= flow are appended (apply 3).  So while max(Q) >= flow it is the
+            // global maximum; when it drops below flow, all pairs are rescanned for a lower
+            // flow (chosen so that Q holds at most QLIM pairs).
+            bool done = false;
+            for (;;) {
+                if (!sh.qvalid) {
+                    u32* hist = reinterpret_cast<u32*>(sh.skey);  // 2048 count bins (LDS, idle here)
+                    ex.par([&](u32 t) {
+                        for (u32 i = t; i < 2048; i += NT) hist[i] = 0;
+                        if (t == 0) { sh.flow = NIL; sh.qn = 0; sh.maxc = 0; }
+                    });
+                    ex.par([&](u32 t) {
+                        const u32 np = sh.npairs;
+                        for (u32 i0 = 0; i0 < np; i0 += 4 * NT) {
+                            u32 v[4];
 #pragma unroll
-                    for (u32 k = 0; k < 8; ++k) v[k] = i0 + k * NT < np ? B.cnt[i0 + k * NT] : 0u;
+                            for (u32 k = 0; k < 4; ++k) v[k] = i0 + k * NT + t < np ? B.cnt[i0 + k * NT + t] : 0u;
 #pragma unroll
-                    for (u32 k = 0; k < 8; ++k) m = v[k] > m ? v[k] : m;
+                            for (u32 k = 0; k < 4; ++k)
+                                if (v[k] >= 2) ex.add(&hist[v[k] < 2047 ? v[k] : 2047u], 1u);
+                        }
+                    });
+                    // suffix sums over the bins, top down: thread t holds bins 2047-2t, 2046-2t
+                    ex.par([&](u32 t) { sh.scan[t] = hist[2047 - 2 * t] + hist[2046 - 2 * t]; });
+                    ex.scan(sh.scan, &sh.total);
+                    ex.par([&](u32 t) {
+                        const u32 bh = 2047 - 2 * t, bl = bh - 1;
+                        const u32 s_hi = sh.scan[t] + hist[bh], s_lo = s_hi + hist[bl];  // #(count >= bin)
+                        u32 cand = NIL;
+                        if (bh >= 2 && s_hi <= QLIM) cand = bh;
+                        if (bl >= 2 && s_lo <= QLIM) cand = bl;
+                        if (cand != NIL) ex.min(&sh.flow, cand);
+                        if (bh >= 2 && hist[bh]) ex.max(&sh.maxc, bh);  // the highest non-empty bin
+                        else if (bl >= 2 && hist[bl]) ex.max(&sh.maxc, bl);
+                    });
+                    ex.par([&](u32 t) {
+                        if (t == 0) {
+                            // flow <= the top count, so Q is never empty; all pairs in the top
+                            // bin are taken even when they are more than QLIM
+                            if (sh.total == 0) sh.flow = NIL;  // no pair occurs twice
+                            else if (sh.flow == NIL || sh.flow > sh.maxc) sh.flow = sh.maxc;
+                        }
+                    });
+                    if (sh.flow == NIL) {
+                        done = true;
+                        break;
+                    }
+                    ex.par([&](u32 t) {
+                        const u32 np = sh.npairs, fl = sh.flow;
+                        for (u32 i0 = 0; i0 < np; i0 += NT) {
+                            const u32 id = i0 + t;
+                            const bool keep = id < np && B.cnt[id] >= fl;
+                            const u32 slot = ex.append(&sh.qn, keep);
+                            if (keep) qa[slot] = id;
+                        }
+                        if (t == 0) sh.qvalid = 1;
+                    });
                 }
-                if (m) ex.max(&sh.maxc, m);
-            });
-            if (sh.maxc < 2) break;
+                // drop the entries below flow, and the maximum of the rest
+                ex.par([&](u32 t) { if (t == 0) { sh.maxc = 0; sh.qn2 = 0; } });
+                ex.par([&](u32 t) {
+                    u32 m = 0;
+                    const u32 qn = sh.qn, fl = sh.flow;
+                    for (u32 e0 = 0; e0 < qn; e0 += NT) {
+                        const u32 e = e0 + t;
+                        u32 id = 0, c = 0;
+                        if (e < qn) {
+                            id = qa[e];
+                            c = B.cnt[id];
+                        }
+                        const bool keep = e < qn && c >= fl;
+                        const u32 slot = ex.append(&sh.qn2, keep);
+                        if (keep) {
+                            qb[slot] = id;
+                            m = c > m ? c : m;
+                        }
+                    }
+                    if (m) ex.max(&sh.maxc, m);
+                });
+                {
+                    u32* x = qa; qa = qb; qb = x;
+                }
+                ex.par([&](u32 t) { if (t == 0) sh.qn = sh.qn2; });
+                if (sh.maxc >= sh.flow) break;
+                if (sh.flow <= 2) {  // every count is below 2: no further rule (PY:1879)
+                    done = true;
+                    break;
+                }
+                ex.par([&](u32 t) { if (t == 0) sh.qvalid = 0; });
+            }
+            if (done) break;
             ex.par([&](u32 t) {
                 if (t == 0) { sh.f = sh.maxc; sh.lsize = 0; sh.lp = 0; sh.levels++; }
             });
             ex.par([&](u32 t) {
-                const u32 np = sh.npairs, fl = sh.f;
-                for (u32 i0 = 0; i0 < np; i0 += 4 * NT) {
-                    u32 v[4];
-#pragma unroll
-                    for (u32 k = 0; k < 4; ++k) v[k] = i0 + k * NT + t < np ? B.cnt[i0 + k * NT + t] : 0u;
-#pragma unroll
-                    for (u32 k = 0; k < 4; ++k) {
-                        const u32 id = i0 + k * NT + t;
-                        const bool hit = v[k] == fl && id < np;
-                        const u32 slot = ex.append(&sh.lsize, hit);
-                        if (hit) {
-                            lk[slot] = B.pkey[id];
-                            li[slot] = id;
-                        }
+                const u32 qn = sh.qn, fl = sh.f;
+                for (u32 e0 = 0; e0 < qn; e0 += NT) {
+                    const u32 e = e0 + t;
+                    const u32 id = e < qn ? qa[e] : 0u;
+                    const bool hit = e < qn && B.cnt[id] == fl;
+                    const u32 slot = ex.append(&sh.lsize, hit);
+                    if (hit) {
+                        lk[slot] = B.pkey[id];
+                        li[slot] = id;
                     }
                 }
             });
@@ -392,6 +484,7 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
             const u32 idx = sh.lp + t;
             sh.scan[t] = idx < sh.lsize && B.cnt[li[idx]] == f ? 1u : 0u;
             sh.scan2[t] = 0;
+            for (u32 e = t; e < SORT_LDS; e += NT) sh.skey[e] = EMPTY;  // the LDS key table (HTab)
             if (t == 0) {
                 sh.cut = NIL; sh.any_aa = 0; sh.nocc = 0; sh.t1 = NIL; sh.t2 = NIL; sh.ts = NIL;
                 sh.hused = 0; sh.nlate = 0;
@@ -581,6 +674,10 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
         T = sh.ts < T ? sh.ts : T;
         const bool stop = sh.ts != NIL && sh.ts < sh.t1 && sh.ts < sh.t2;
         if (T == 0) break;  // the next round replaces < 2 occurrences (PY:1879-1882)
+        // at most 2 new keys per replaced occurrence: the LDS table while that keeps it at
+        // most half full
+        const bool hglob = nocc > SORT_LDS / 4;
+        const HTab ht = hglob ? HTab{B.hkey, B.hval, B.hmask, true} : HTab{sh.skey, sh.sval, SORT_LDS - 1, false};
         ex.mark(P_APPLY_A);
         // ---- apply 1: destroy the old pair occurrences; register the new pair keys (the
         //      inserting thread allocates the id) and keep each occurrence's hash slots ----
@@ -594,8 +691,8 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
                 if (q != NIL) ex.sub(&B.cnt[B.opair[j]], 1u);
                 if (p != NIL) ex.sub(&B.cnt[B.opair[p]], 1u);
                 const u32 X = X0 + m;
-                if (q != NIL) B.oidr[o] = hash_insert(ex, B, sh, pkey_of(X, B.oidr[o]));
-                if (p != NIL) B.oidl[o] = hash_insert(ex, B, sh, pkey_of(B.oidl[o], X));
+                if (q != NIL) B.oidr[o] = hash_insert(ex, B, sh, ht, pkey_of(X, B.oidr[o]));
+                if (p != NIL) B.oidl[o] = hash_insert(ex, B, sh, ht, pkey_of(B.oidl[o], X));
             }
         });
         // ---- apply 2: count the new pair occurrences, rewrite the sequence ----
@@ -607,12 +704,12 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
                 const u32 i = B.opos[o], j = B.oj[o], q = B.oq[o], p = B.op[o];
                 u32 idr = NIL;
                 if (q != NIL) {
-                    idr = B.hval[B.oidr[o]];
+                    idr = ht.v[B.oidr[o]];
                     B.oidr[o] = idr;
                     ex.add(&B.cnt[idr], 1u);
                 }
                 if (p != NIL) {
-                    const u32 idl = B.hval[B.oidl[o]];
+                    const u32 idl = ht.v[B.oidl[o]];
                     B.oidl[o] = idl;
                     ex.add(&B.cnt[idl], 1u);
                     B.opair[p] = idl;
@@ -630,12 +727,14 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
         ex.par([&](u32 t) {
             for (u32 u = t; u < sh.hused; u += NT) {
                 const u32 id = sh.npairs + u;
-                B.poff[id] = ex.add(&sh.pool, B.cnt[id]);
-                if (B.cnt[id] == f) {
+                const u32 c = B.cnt[id];
+                B.poff[id] = ex.add(&sh.pool, c);
+                if (c == f) {
                     const u32 k = ex.add(&sh.nlate, 1u);
                     B.lkL[k] = B.pkey[id];
                     B.liL[k] = id;
                 }
+                if (c >= sh.flow) qa[ex.add(&sh.qn, 1u)] = id;  // keeps Q complete (level cache)
             }
             for (u32 m = t; m < T; m += NT) B.rules[sh.nrules + m] = pkey_of(sh.m_a[m], sh.m_b[m]);
         });
@@ -654,7 +753,8 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
                     B.occpos[B.poff[id] + ex.add(&B.plen[id], 1u)] = B.op[o];
                 }
             }
-            for (u32 u = t; u < sh.hused; u += NT) B.hkey[B.husd[u]] = EMPTY;
+            if (hglob)
+                for (u32 u = t; u < sh.hused; u += NT) B.hkey[B.husd[u]] = EMPTY;
             if (t == 0) {
                 sh.lp = sh.m_lpos[T - 1] + 1;
                 sh.next_sym += T;

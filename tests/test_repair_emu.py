@@ -67,3 +67,14 @@ def test_emu_256k(emu, kind):
     got, res = emu(data, seed=3)
     assert got == O.repair_fast(data)
     assert res[3] <= res[1]  # batches <= rounds (rules)
+
+
+@pytest.mark.parametrize("kind", ["random", "gradient", "enwik"])
+def test_emu_1m_level_cache(emu, kind):
+    """1 MiB blocks: far more than QLIM pairs occur twice (random: ~65536 pairs sharing a few
+    top counts), so the level cache rescans with falling thresholds many times."""
+    n = 1 << 20
+    data = {"enwik": lambda: D.enwik_like(n, seed=5), "gradient": lambda: D.gradient_bmp()[-n:],
+            "random": lambda: D.splitmix64_bytes(n, seed=11)}[kind]()
+    got, res = emu(data)
+    assert got == O.repair_fast(data)
