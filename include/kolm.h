@@ -130,6 +130,16 @@ int kolm_cdc_boundaries(const uint8_t* data, uint64_t n, uint32_t min_size, uint
                         uint32_t max_size, int merge_orphan_tail, uint64_t* starts, uint64_t cap,
                         uint64_t* nchunks);
 
+/* ---- decode side (host buffers, default context) -------------------------------- */
+/* Decodes nblocks payloads of a container on the device (the decoder registry
+ * _select_decoders, PY:2194-2207): block i = payloads[payload_off[i], payload_off[i+1]),
+ * method id methods[i], original length orig_lens[i]; the blocks are written back to back
+ * into out (sum of orig_lens bytes, out_cap available).  Method ids outside
+ * KOLM_DECODE_MASK return KOLM_EARG; so do malformed payloads (message names the block). */
+#define KOLM_DECODE_MASK 0x183u  /* raw 0, xor 1, lz77 7, lfsr_pred 8 */
+int kolm_decode_blocks(const uint8_t* payloads, const uint64_t* payload_off, const uint32_t* methods,
+                       const uint32_t* orig_lens, uint32_t nblocks, uint8_t* out, uint64_t out_cap);
+
 /* ---- batched hot entry (host buffers, default context) ------------------------- */
 /* Encodes nblocks blocks of `data` (block i = data[starts[i] .. starts[i]+lens[i]);
  * blocks contiguous and non-empty: fixed chunking when all lens are equal except a

@@ -1280,6 +1280,91 @@ int kolm_encode_blocks_device_var(kolm_ctx* c, const uint8_t* d_data, const uint
     });
 }
 
+int kolm_decode_blocks(const uint8_t* payloads, const uint64_t* payload_off, const uint32_t* methods,
+                       const uint32_t* orig_lens, uint32_t nblocks, uint8_t* out, uint64_t out_cap) {
+    kolm_ctx* c = need_default();
+    if (!c) return KOLM_ENOINIT;
+    if (nblocks && (!payloads || !payload_off || !methods || !orig_lens || !out)) return KOLM_EARG;
+    u64 total = 0;
+    for (u32 i = 0; i < nblocks; ++i) {
+        if (methods[i] >= 32 || !((KOLM_DECODE_MASK >> methods[i]) & 1u)) {
+            char msg[96];
+            snprintf(msg, sizeof msg, "block %u: method %u is not decoded on the device", i, methods[i]);
+            set_err(msg);
+            return KOLM_EARG;
+        }
+        if (payload_off[i + 1] < payload_off[i]) return KOLM_EARG;
+        total += orig_lens[i];
+    }
+    if (total >= (1ull << 31)) {
+        set_err("decoded batch larger than 2^31-1 bytes");
+        return KOLM_EARG;
+    }
+    if (total > out_cap) {
+        set_err("output capacity too small");
+        return KOLM_ECAP;
+    }
+    if (nblocks == 0) return KOLM_OK;
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        hipStream_t s = c->stream;
+        const u32 nb = nblocks;
+        const u64 ptotal = payload_off[nb] - payload_off[0];
+        std::vector<u64> poff(nb + 1);
+        std::vector<u32> obase(nb + 1);
+        obase[0] = 0;
+        for (u32 i = 0; i <= nb; ++i) poff[i] = payload_off[i] - payload_off[0];
+        for (u32 i = 0; i < nb; ++i) obase[i + 1] = obase[i] + orig_lens[i];
+        // blocks per decoder
+        std::vector<u32> lists[KOLM_NCAND];
+        for (u32 i = 0; i < nb; ++i) lists[methods[i]].push_back(i);
+        std::vector<u32> flat;
+        u32 lstart[KOLM_NCAND + 1];
+        for (u32 m = 0; m < KOLM_NCAND; ++m) {
+            lstart[m] = (u32)flat.size();
+            flat.insert(flat.end(), lists[m].begin(), lists[m].end());
+        }
+        lstart[KOLM_NCAND] = (u32)flat.size();
+        u8* dpay = c->get<u8>("dec_pay", ptotal + 64);
+        u64* dpoff = c->get<u64>("dec_poff", nb + 1);
+        u32* dob = c->get<u32>("dec_obase", nb + 1);
+        u32* dlist = c->get<u32>("dec_list", nb);
+        u32* dst = c->get<u32>("dec_status", nb);
+        u8* dout = c->get<u8>("dec_out", total + 64);
+        if (ptotal)
+            KOLM_HIP_CHECK(hipMemcpyAsync(dpay, payloads + payload_off[0], ptotal, hipMemcpyHostToDevice, s));
+        KOLM_HIP_CHECK(hipMemcpyAsync(dpoff, poff.data(), sizeof(u64) * (nb + 1), hipMemcpyHostToDevice, s));
+        KOLM_HIP_CHECK(hipMemcpyAsync(dob, obase.data(), sizeof(u32) * (nb + 1), hipMemcpyHostToDevice, s));
+        KOLM_HIP_CHECK(hipMemcpyAsync(dlist, flat.data(), sizeof(u32) * nb, hipMemcpyHostToDevice, s));
+        KOLM_HIP_CHECK(hipMemsetAsync(dst, 0, sizeof(u32) * nb, s));
+        auto args = [&](u32 m) {
+            return DecArgs{dpay, dpoff, dob, dout, dst, dlist + lstart[m], lstart[m + 1] - lstart[m]};
+        };
+        launch_dec_raw(args(KOLM_M_RAW), s);
+        launch_dec_uleb(args(KOLM_M_XOR), false, s);
+        launch_dec_uleb(args(KOLM_M_LFSR), true, s);
+        if (!lists[KOLM_M_LZ77].empty()) {
+            const u64 T = total + 16;
+            launch_dec_lz77(args(KOLM_M_LZ77), c->get<u32>("dec_tpos", T), c->get<u32>("dec_tval", T),
+                            c->get<u32>("dec_ntok", nb), c->get<u32>("dec_mark", T), c->get<u32>("dec_src", T), s);
+        }
+        std::vector<u32> st(nb);
+        KOLM_HIP_CHECK(hipMemcpyAsync(st.data(), dst, sizeof(u32) * nb, hipMemcpyDeviceToHost, s));
+        c->sync();
+        for (u32 i = 0; i < nb; ++i)
+            if (st[i]) {
+                char msg[128];
+                snprintf(msg, sizeof msg, "block %u (method %u): %s", i, methods[i],
+                         st[i] == DEC_ELEN ? "decoded length mismatch" : "malformed payload");
+                set_err(msg);
+                return KOLM_EARG;
+            }
+        KOLM_HIP_CHECK(hipMemcpy(out, dout, total, hipMemcpyDeviceToHost));
+        return KOLM_OK;
+    });
+}
+
 int kolm_bbwt_forward(const uint8_t* in, size_t n, uint8_t* out) {
     kolm_ctx* c = need_default();
     if (!c) return KOLM_ENOINIT;

@@ -385,6 +385,22 @@ struct CdcBufs {
 u32 cdc_segment(u32 avg, u32 mx);
 void launch_cdc(const CdcParams& p, const CdcBufs& b, hipStream_t s, KTimer* kt = nullptr);
 
+// ---- k_decode.hip: block decoders (PY:2194-2207), one workgroup per block ----
+enum : u32 { DEC_OK = 0, DEC_ELEN = 1, DEC_EFORMAT = 2 };
+struct DecArgs {
+    const u8* pay;    // payload arena
+    const u64* poff;  // [nb + 1] payload offsets
+    const u32* obase; // [nb + 1] output offsets (prefix of the original lengths)
+    u8* out;          // decoded bytes
+    u32* status;      // [nb] DEC_* per block (zeroed by the caller)
+    const u32* list;  // blocks of this decoder
+    u32 nlist;
+};
+void launch_dec_raw(const DecArgs& a, hipStream_t s);
+void launch_dec_uleb(const DecArgs& a, bool lfsr, hipStream_t s);
+// scratch arrays tpos/tval/mark/src: one u32 per output byte; ntok: [nb]
+void launch_dec_lz77(const DecArgs& a, u32* tpos, u32* tval, u32* ntok, u32* mark, u32* src, hipStream_t s);
+
 }  // namespace kolm
 
 #define KOLM_HIP_CHECK(x)                                              \

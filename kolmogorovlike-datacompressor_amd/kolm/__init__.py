@@ -284,13 +284,29 @@ def compress_blocks_cdc(data: bytes, min_size: int = 4096, avg_size: int = 8192,
     return write_container(MODE_CDC, avg_size, n, [int(m) for m in method], [e - s for s, e in bounds], payloads)
 
 
-def decompress(container: bytes) -> bytes:
-    """Inverse of compress_blocks_fixed / the reference's containers (PY:2451-2550).
-    Host decoders (decode side is outside the offloaded hot path)."""
+def decompress(container: bytes, device: bool = True) -> bytes:
+    """Inverse of compress_blocks_fixed / compress_blocks_cdc / the reference's containers
+    (PY:2451-2550).  The TOC is parsed on the host; the blocks whose method the device
+    decodes (kolm_decode_blocks: raw, xor, lz77, lfsr_pred) are decoded on the GPU in one
+    batch, the others by the host decoders of kolm/decode.py (decode side: SURVEY §8f-4).
+    `device=False` (not in PY) decodes everything on the host."""
     mode, size_field, total_len, mids, orig, payloads = read_container(container)
+    parts: List[Optional[bytes]] = [None] * len(mids)
+    if device:
+        sel = [i for i, m in enumerate(mids) if (_lib.KOLM_DECODE_MASK >> m) & 1]
+        if sel:
+            try:
+                dec = _lib.decode_blocks([payloads[i] for i in sel], [mids[i] for i in sel],
+                                         [orig[i] for i in sel])
+            except _lib.KolmError as e:
+                raise ValueError(str(e)) from None
+            pos = 0
+            for i in sel:
+                parts[i] = dec[pos:pos + orig[i]]
+                pos += orig[i]
     out = bytearray()
-    for mid, n, p in zip(mids, orig, payloads):
-        out += decode_block(mid, p, n)
+    for i, (mid, n, p) in enumerate(zip(mids, orig, payloads)):
+        out += parts[i] if parts[i] is not None else decode_block(mid, p, n)
     if len(out) != total_len:
         raise ValueError(f"Length mismatch: got {len(out)}, expect {total_len}")
     return bytes(out)

@@ -110,7 +110,28 @@ SIGNATURES = [
     ("kolm_encode_blocks_device_var", I32, [P, P, P, U32, U32, P, P, U64, P, P, P, P]),
     ("kolm_cdc_boundaries", I32, [U8P, U64, U32, U32, U32, I32, P, U64, ctypes.POINTER(U64)]),
     ("kolm_cdc_boundaries_device", I32, [P, P, U64, U32, U32, U32, I32, P, U64, ctypes.POINTER(U64)]),
+    ("kolm_decode_blocks", I32, [P, P, P, P, U32, P, U64]),
 ]
+KOLM_DECODE_MASK = 0x183  # methods decoded on the device (kolm.h)
+
+
+def decode_blocks(payloads, methods, orig_lens) -> bytes:
+    """Decode the given blocks on the device (kolm_decode_blocks); every method must be in
+    KOLM_DECODE_MASK.  Returns the concatenated decoded bytes."""
+    ensure_init()
+    nb = len(payloads)
+    if nb == 0:
+        return b""
+    off = np.zeros(nb + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(p) for p in payloads])
+    arena = np.frombuffer(b"".join(payloads) + b"\0", dtype=np.uint8)
+    meth = np.ascontiguousarray(np.asarray(methods, dtype=np.uint32))
+    lens = np.ascontiguousarray(np.asarray(orig_lens, dtype=np.uint32))
+    total = int(lens.astype(np.uint64).sum())
+    out = np.zeros(max(total, 1), dtype=np.uint8)
+    check(load().kolm_decode_blocks(arena.ctypes.data, off.ctypes.data, meth.ctypes.data, lens.ctypes.data, nb,
+                                    out.ctypes.data, total))
+    return out[:total].tobytes()
 
 
 def load():

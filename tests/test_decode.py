@@ -1,0 +1,104 @@
+"""Decode side on the GPU (kolm_decode_blocks, the decoder registry PY:2194-2207): every
+PY golden container (fixed and CDC mode) decompresses to its input; device and host
+decoders agree block for block on seeded payloads of every device-decoded method;
+malformed payloads are rejected with the block named.  The host decoders (kolm/decode.py)
+are themselves pinned to PY by tests/test_host.py."""
+import os
+
+import numpy as np
+import pytest
+
+from kolm import datagen as D
+from kolm import decode as H
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_golden_containers_fixed(kolm_gpu, golden_containers, manifest):
+    for cname in manifest["containers"]:
+        inp = golden_containers[f"{cname}/input"].tobytes()
+        for kind in ("full", "ids0_8"):
+            blob = golden_containers[f"{cname}/{kind}"].tobytes()
+            assert kolm_gpu.decompress(blob) == inp, (cname, kind)
+
+
+def test_golden_containers_cdc(kolm_gpu):
+    import json
+    z = np.load(os.path.join(GOLDEN, "cdc.npz"))
+    with open(os.path.join(GOLDEN, "cdc.json")) as f:
+        man = json.load(f)
+    for name in man["containers"]:
+        inp = z[f"c_{name}/input"].tobytes()
+        for kind in ("full", "ids0_8"):
+            assert kolm_gpu.decompress(z[f"c_{name}/{kind}"].tobytes()) == inp, (name, kind)
+
+
+def _blocks():
+    yield D.enwik_like(200_000, seed=3)
+    yield D.splitmix64_bytes(70_001)
+    yield bytes(65_536)
+    yield D.gradient_bmp()[:100_000]
+    yield D.sine_wav()[:50_000]
+    yield b"a"
+    yield b"ab" * 3000 + b"c"
+    yield bytes(i & 0xFF for i in range(4099))
+
+
+@pytest.mark.parametrize("mid", [0, 1, 7, 8])
+def test_device_vs_host_per_method(kolm_gpu, mid):
+    """Payloads of method `mid` (forced through the batched encoder) for assorted blocks,
+    decoded in ONE device batch: equal to the inputs and to the host decoders."""
+    from kolm import _lib
+    blocks = list(_blocks())
+    pays = []
+    for blk in blocks:
+        _, _, p, _ = _lib.encode_blocks(blk, len(blk), cand_mask=1 << mid, force=[mid])
+        pays.append(p[0])
+        assert H.decode_block(mid, p[0], len(blk)) == blk
+    got = _lib.decode_blocks(pays, [mid] * len(blocks), [len(b) for b in blocks])
+    assert got == b"".join(blocks)
+
+
+def test_mixed_batch_large(kolm_gpu):
+    """64 MiB of 1 MiB blocks, hot-path candidates: the device batch decodes the LZ77 and
+    simple-model blocks, the rest go to the host decoders; round trip exact."""
+    data = D.enwik_like(24 << 20) + D.splitmix64_bytes(8 << 20) + bytes(4 << 20)
+    blob = kolm_gpu.compress_blocks_fixed(data, 1 << 20, hot_path=True)
+    assert kolm_gpu.decompress(blob) == data
+    assert kolm_gpu.decompress(blob, device=False) == data
+
+
+def test_lz77_long_overlaps(kolm_gpu):
+    """Copy chains through overlapping matches (dist 1..3 runs of 1 MiB) and the maximal
+    window distance: pointer jumping must resolve every chain."""
+    from kolm import _lib
+    blocks = [bytes(1 << 20), b"xyz" * 349_525, (b"q" + bytes(4095)) * 64, D.enwik_like(1 << 20, seed=9)]
+    pays = []
+    for blk in blocks:
+        _, _, p, _ = _lib.encode_blocks(blk, len(blk), cand_mask=1 << 7, force=[7])
+        pays.append(p[0])
+    assert _lib.decode_blocks(pays, [7] * len(blocks), [len(b) for b in blocks]) == b"".join(blocks)
+
+
+def test_malformed_payloads(kolm_gpu):
+    from kolm import _lib
+    cases = [
+        (0, b"abc", 4),                 # raw length mismatch
+        (1, b"\x05\x80", 2),            # truncated 2-byte ULEB value
+        (1, b"\x01\x02\x03", 2),        # too many values
+        (7, b"\x01\x03\x01", 3),        # first token a copy (distance > output)
+        (7, b"\x02\x41", 1),            # unknown flag
+        (7, b"\x00\x41", 2),            # short output
+        (8, b"\x01", 2),                # too few values
+    ]
+    for mid, pay, n in cases:
+        with pytest.raises(_lib.KolmError):
+            _lib.decode_blocks([pay], [mid], [n])
+    with pytest.raises(_lib.KolmError):  # method not decoded on the device
+        _lib.decode_blocks([b"x"], [2], [1])
+    # a bad block in a batch fails the batch and names the block
+    good = b"hello"
+    with pytest.raises(_lib.KolmError, match="block 1"):
+        _lib.decode_blocks([good, b"\x02"], [0, 7], [5, 1])

@@ -36,15 +36,15 @@ def test_container_roundtrip_goldens(golden_containers, manifest):
             inp = golden_containers[f"{cname}/input"].tobytes()
             mode, sz, tot, mids, orig, pays = container.read_container(blob)
             assert container.write_container(mode, sz, tot, mids, orig, pays) == blob
-            assert kolm.decompress(blob) == inp
+            assert kolm.decompress(blob, device=False) == inp
 
 
 def test_container_errors():
     with pytest.raises(ValueError):
-        kolm.decompress(b"NOPE" + bytes(20))
+        kolm.decompress(b"NOPE" + bytes(20), device=False)
     blob = container.write_container(container.MODE_FIXED, 4, 3, [0], [3], [b"abc"])
     with pytest.raises(ValueError):
-        kolm.decompress(blob + b"\x00")  # strict trailing-bytes check (PY:2545-2547)
+        kolm.decompress(blob + b"\x00", device=False)  # strict trailing-bytes check (PY:2545-2547)
     import struct
     with pytest.raises(struct.error):
         container.write_container(container.MODE_FIXED, 1, 70000, [0] * 70000, [1] * 70000, [b"a"] * 70000)
