@@ -1349,6 +1349,41 @@ int kolm_decode_blocks(const uint8_t* payloads, const uint64_t* payload_off, con
             launch_dec_lz77(args(KOLM_M_LZ77), c->get<u32>("dec_tpos", T), c->get<u32>("dec_tval", T),
                             c->get<u32>("dec_ntok", nb), c->get<u32>("dec_mark", T), c->get<u32>("dec_src", T), s);
         }
+        // BBWT family: one list over ids 2..6 (the flags come from each block's id)
+        std::vector<u32> bwl;
+        u32 maxn = 0;
+        for (u32 m = KOLM_M_BBWT; m <= KOLM_M_BBWT_GRAY; ++m)
+            for (u32 i : lists[m]) {
+                bwl.push_back(i);
+                maxn = std::max(maxn, orig_lens[i]);
+            }
+        if (!bwl.empty()) {
+            const u64 T = total + 16;
+            std::vector<u32> vb(nb + 1);
+            vb[0] = 0;
+            for (u32 i = 0; i < nb; ++i)
+                vb[i + 1] = vb[i] + (methods[i] == KOLM_M_BBWT_BP ? 8 * ((orig_lens[i] + 7) / 8) : 0u);
+            u32* dmeth = c->get<u32>("dec_meth", nb);
+            u32* dvb = c->get<u32>("dec_vbase", nb + 1);
+            u32* dbwl = c->get<u32>("dec_bwlist", bwl.size());
+            KOLM_HIP_CHECK(hipMemcpyAsync(dmeth, methods, sizeof(u32) * nb, hipMemcpyHostToDevice, s));
+            KOLM_HIP_CHECK(hipMemcpyAsync(dvb, vb.data(), sizeof(u32) * (nb + 1), hipMemcpyHostToDevice, s));
+            KOLM_HIP_CHECK(hipMemcpyAsync(dbwl, bwl.data(), sizeof(u32) * bwl.size(), hipMemcpyHostToDevice, s));
+            BwArgs a{};
+            a.d = DecArgs{dpay, dpoff, dob, dout, dst, dbwl, (u32)bwl.size()};
+            a.meth = dmeth;
+            a.vbase = dvb;
+            a.vals = c->get<u8>("dec_vals", (u64)vb[nb] + 16);
+            a.mi = c->get<u8>("dec_mi", T);
+            a.bw = c->get<u8>("dec_bw", T);
+            a.cpb = (maxn + MTF_CHUNK - 1) / MTF_CHUNK;
+            const u64 nch = (u64)bwl.size() * a.cpb;
+            a.summ = c->get<u8>("dec_summ", nch * 256 + 16);
+            a.states = c->get<u8>("dec_states", nch * 256 + 16);
+            static const char* const xn[8] = {"dec_x0", "dec_x1", "dec_x2", "dec_x3", "dec_x4", "dec_x5", "dec_x6", "dec_x7"};
+            for (int k = 0; k < 8; ++k) a.X[k] = c->get<u32>(xn[k], T);
+            launch_dec_bw(a, s);
+        }
         std::vector<u32> st(nb);
         KOLM_HIP_CHECK(hipMemcpyAsync(st.data(), dst, sizeof(u32) * nb, hipMemcpyDeviceToHost, s));
         c->sync();

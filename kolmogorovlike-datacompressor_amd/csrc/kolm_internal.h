@@ -400,6 +400,20 @@ void launch_dec_raw(const DecArgs& a, hipStream_t s);
 void launch_dec_uleb(const DecArgs& a, bool lfsr, hipStream_t s);
 // scratch arrays tpos/tval/mark/src: one u32 per output byte; ntok: [nb]
 void launch_dec_lz77(const DecArgs& a, u32* tpos, u32* tval, u32* ntok, u32* mark, u32* src, hipStream_t s);
+// BBWT family (ids 2..6): Rice -> inverse map -> MTF decode -> inverse BBWT
+struct BwArgs {
+    DecArgs d;         // list = the blocks with ids 2..6
+    const u32* meth;   // [nb] method ids
+    const u32* vbase;  // [nb + 1] Rice value offsets (bit-plane blocks: 8 * ceil(n / 8) values)
+    u8* vals;          // Rice values of bit-plane blocks
+    u8* mi;            // [N] MTF indices (at obase)
+    u8* bw;            // [N] BBWT string (at obase)
+    u8* summ;          // [nlist * cpb * 256] MTF chunk summaries
+    u8* states;        // [nlist * cpb * 256] MTF chunk entry tables
+    u32 cpb;           // MTF chunks per block slot (longest block / MTF_CHUNK)
+    u32* X[8];         // [N] u32 scratch of the inverse BBWT
+};
+void launch_dec_bw(const BwArgs& a, hipStream_t s);
 
 }  // namespace kolm
 

@@ -112,7 +112,7 @@ SIGNATURES = [
     ("kolm_cdc_boundaries_device", I32, [P, P, U64, U32, U32, U32, I32, P, U64, ctypes.POINTER(U64)]),
     ("kolm_decode_blocks", I32, [P, P, P, P, U32, P, U64]),
 ]
-KOLM_DECODE_MASK = 0x183  # methods decoded on the device (kolm.h)
+KOLM_DECODE_MASK = 0x1FF  # methods decoded on the device: 0..8 (kolm.h)
 
 
 def decode_blocks(payloads, methods, orig_lens) -> bytes:

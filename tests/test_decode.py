@@ -46,7 +46,7 @@ def _blocks():
     yield bytes(i & 0xFF for i in range(4099))
 
 
-@pytest.mark.parametrize("mid", [0, 1, 7, 8])
+@pytest.mark.parametrize("mid", list(range(9)))
 def test_device_vs_host_per_method(kolm_gpu, mid):
     """Payloads of method `mid` (forced through the batched encoder) for assorted blocks,
     decoded in ONE device batch: equal to the inputs and to the host decoders."""
@@ -68,6 +68,33 @@ def test_mixed_batch_large(kolm_gpu):
     blob = kolm_gpu.compress_blocks_fixed(data, 1 << 20, hot_path=True)
     assert kolm_gpu.decompress(blob) == data
     assert kolm_gpu.decompress(blob, device=False) == data
+
+
+def test_mixed_methods_one_batch(kolm_gpu):
+    """Every device-decoded id in ONE batch, blocks of different lengths interleaved (the
+    BBWT family shares one list; its MTF chunk grid is sized by the longest block)."""
+    from kolm import _lib
+    blocks = list(_blocks())
+    pays, mids = [], []
+    for j, blk in enumerate(blocks * 2):
+        mid = j % 9
+        _, _, p, _ = _lib.encode_blocks(blk, len(blk), cand_mask=1 << mid, force=[mid])
+        pays.append(p[0])
+        mids.append(mid)
+    got = _lib.decode_blocks(pays, mids, [len(b) for b in blocks * 2])
+    assert got == b"".join(blocks * 2)
+
+
+@pytest.mark.parametrize("mid", [2, 3, 5])
+def test_bbwt_family_large(kolm_gpu, mid):
+    """4 MiB blocks (4096 MTF chunks, multi-tile inverse BBWT, long Lyndon cycles)."""
+    from kolm import _lib
+    blocks = [D.enwik_like(4 << 20, seed=11), bytes(1 << 20) + b"x", b"ab" * (1 << 20)]
+    pays = []
+    for blk in blocks:
+        _, _, p, _ = _lib.encode_blocks(blk, len(blk), cand_mask=1 << mid, force=[mid])
+        pays.append(p[0])
+    assert _lib.decode_blocks(pays, [mid] * len(blocks), [len(b) for b in blocks]) == b"".join(blocks)
 
 
 def test_lz77_long_overlaps(kolm_gpu):
@@ -96,8 +123,13 @@ def test_malformed_payloads(kolm_gpu):
     for mid, pay, n in cases:
         with pytest.raises(_lib.KolmError):
             _lib.decode_blocks([pay], [mid], [n])
+    for mid in (2, 3, 6):
+        with pytest.raises(_lib.KolmError):   # Rice: unary run past 63 bits
+            _lib.decode_blocks([b"\xff" * 16], [mid], [4])
+        with pytest.raises(_lib.KolmError):   # Rice: too few values
+            _lib.decode_blocks([b"\x00"], [mid], [100])
     with pytest.raises(_lib.KolmError):  # method not decoded on the device
-        _lib.decode_blocks([b"x"], [2], [1])
+        _lib.decode_blocks([b"x"], [9], [1])
     # a bad block in a batch fails the batch and names the block
     good = b"hello"
     with pytest.raises(_lib.KolmError, match="block 1"):
