@@ -125,6 +125,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--full-steps", type=int, default=2,
                     help="timed steps of the full candidate list 0..9 (Re-Pair included); 0 = skip")
+    ap.add_argument("--decode-steps", type=int, default=3,
+                    help="timed device decode passes over the hot-path payloads (0: skip)")
     ap.add_argument("--cdc-steps", type=int, default=2,
                     help="timed steps of the content-defined (FastCDC) mode; 0 = skip")
     a = ap.parse_args()
@@ -218,6 +220,47 @@ def main():
     pipe = {"algorithmic_bytes_per_step": int(alg_step),
             "achieved_GBs": round(alg_step / (ms_step * 1e-3) / 1e9, 2),
             "frac": round(alg_step / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+
+    # Decode side (decompress, PY:2451-2550): the hot-path payloads still resident in the
+    # arena decoded back on the device (kolm_decode_blocks_device, every id 0..8); checked
+    # against the input once, then timed with the same discipline.
+    dec = None
+    if a.decode_steps > 0:
+        lens = np.full(nb, a.bs, np.uint32)
+        lens[-1] = n - a.bs * (nb - 1)
+        d_out = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        dms = ctypes.c_double(0.0)
+
+        def dstep():
+            _lib.check(L.kolm_decode_blocks_device(ctx, arena.data_ptr(), off.ctypes.data, method.ctypes.data,
+                                                   lens.ctypes.data, nb, d_out.data_ptr(), n + 64, ctypes.byref(dms)))
+
+        dstep()
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(d_out[:n], d_in[:n]))
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dk = 0.0
+        for _ in range(a.decode_steps):
+            dstep()
+            dk += dms.value
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        eld = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([eld], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            eld = float(tt[0])
+        dec = {"value": round(world * n * a.decode_steps / eld / MB, 2), "unit": "MB/s", "steps": a.decode_steps,
+               "ms_per_step": round(eld / a.decode_steps * 1e3, 2),
+               "kernel_ms_per_step": round(dk / a.decode_steps, 2), "round_trip_exact": ok,
+               "methods": np.bincount(method, minlength=10).tolist()}
+        del d_out
+        if not ok:
+            raise SystemExit("decode leg: device round trip differs from the input")
 
     # The reference's FULL candidate list (ids 0..9: + exact Re-Pair, its own stream beside
     # the hot path): same data, same timing discipline; reported beside the hot-path value.
@@ -319,6 +362,7 @@ def main():
             "cpu_baseline": cpu,
             "detail": {"ratio": round(float(off[-1]) / n, 4),
                        "methods": np.bincount(method, minlength=10).tolist(),
+                       "decode": dec,
                        "full_candidates": full,
                        "cdc_mode": cdc,
                        "device_ms": {k: round(s0[k], 2) for k in ("ms_total", "ms_sa", "ms_lz", "ms_entropy", "ms_emit")},

@@ -202,6 +202,13 @@ int kolm_encode_blocks_device_var(kolm_ctx* ctx, const uint8_t* d_data, const ui
 int kolm_cdc_boundaries_device(kolm_ctx* ctx, const uint8_t* d_data, uint64_t n, uint32_t min_size,
                                uint32_t avg_size, uint32_t max_size, int merge_orphan_tail,
                                uint32_t* h_starts, uint64_t cap, uint64_t* nchunks);
+/* kolm_decode_blocks over device-resident payloads (e.g. an encode arena): block i =
+ * d_payloads[payload_off[i], payload_off[i+1]) with payload_off / methods / orig_lens on
+ * the host; the blocks are written back to back into d_out (device, out_cap bytes).
+ * ms (optional) receives the device time of the decode kernels (HIP events). */
+int kolm_decode_blocks_device(kolm_ctx* ctx, const void* d_payloads, const uint64_t* payload_off,
+                              const uint32_t* methods, const uint32_t* orig_lens, uint32_t nblocks,
+                              void* d_out, uint64_t out_cap, double* ms);
 
 #ifdef __cplusplus
 }

@@ -1280,13 +1280,11 @@ int kolm_encode_blocks_device_var(kolm_ctx* c, const uint8_t* d_data, const uint
     });
 }
 
-int kolm_decode_blocks(const uint8_t* payloads, const uint64_t* payload_off, const uint32_t* methods,
-                       const uint32_t* orig_lens, uint32_t nblocks, uint8_t* out, uint64_t out_cap) {
-    kolm_ctx* c = need_default();
-    if (!c) return KOLM_ENOINIT;
-    if (nblocks && (!payloads || !payload_off || !methods || !orig_lens || !out)) return KOLM_EARG;
-    u64 total = 0;
-    for (u32 i = 0; i < nblocks; ++i) {
+// Checks a decode batch's method ids / offsets / lengths; total = decoded bytes.
+static int check_decode(const uint64_t* payload_off, const uint32_t* methods, const uint32_t* orig_lens, u32 nb,
+                        u64 out_cap, u64& total) {
+    total = 0;
+    for (u32 i = 0; i < nb; ++i) {
         if (methods[i] >= 32 || !((KOLM_DECODE_MASK >> methods[i]) & 1u)) {
             char msg[96];
             snprintf(msg, sizeof msg, "block %u: method %u is not decoded on the device", i, methods[i]);
@@ -1304,99 +1302,143 @@ int kolm_decode_blocks(const uint8_t* payloads, const uint64_t* payload_off, con
         set_err("output capacity too small");
         return KOLM_ECAP;
     }
+    return KOLM_OK;
+}
+
+// Decodes nb blocks whose payloads are resident at dpay (+ payload_off[i] - payload_off[0])
+// into dout (device).  Per-decoder block lists are built on the host; every kernel
+// runs on the context stream.  ms (optional) = device time of the decode kernels.
+static int decode_batch(kolm_ctx* c, const u8* dpay, const uint64_t* payload_off, const uint32_t* methods,
+                        const uint32_t* orig_lens, u32 nb, u64 total, u8* dout, double* ms) {
+    hipStream_t s = c->stream;
+    std::vector<u64> poff(nb + 1);
+    std::vector<u32> obase(nb + 1);
+    obase[0] = 0;
+    for (u32 i = 0; i <= nb; ++i) poff[i] = payload_off[i] - payload_off[0];
+    for (u32 i = 0; i < nb; ++i) obase[i + 1] = obase[i] + orig_lens[i];
+    // blocks per decoder
+    std::vector<u32> lists[KOLM_NCAND];
+    for (u32 i = 0; i < nb; ++i) lists[methods[i]].push_back(i);
+    std::vector<u32> flat;
+    u32 lstart[KOLM_NCAND + 1];
+    for (u32 m = 0; m < KOLM_NCAND; ++m) {
+        lstart[m] = (u32)flat.size();
+        flat.insert(flat.end(), lists[m].begin(), lists[m].end());
+    }
+    lstart[KOLM_NCAND] = (u32)flat.size();
+    // BBWT family: one list over ids 2..6 (the flags come from each block's id)
+    std::vector<u32> bwl;
+    u32 maxn = 0;
+    for (u32 m = KOLM_M_BBWT; m <= KOLM_M_BBWT_GRAY; ++m)
+        for (u32 i : lists[m]) {
+            bwl.push_back(i);
+            maxn = std::max(maxn, orig_lens[i]);
+        }
+    std::vector<u32> vb(nb + 1);
+    vb[0] = 0;
+    for (u32 i = 0; i < nb; ++i) vb[i + 1] = vb[i] + (methods[i] == KOLM_M_BBWT_BP ? 8 * ((orig_lens[i] + 7) / 8) : 0u);
+    u64* dpoff = c->get<u64>("dec_poff", nb + 1);
+    u32* dob = c->get<u32>("dec_obase", nb + 1);
+    u32* dlist = c->get<u32>("dec_list", nb);
+    u32* dst = c->get<u32>("dec_status", nb);
+    KOLM_HIP_CHECK(hipMemcpyAsync(dpoff, poff.data(), sizeof(u64) * (nb + 1), hipMemcpyHostToDevice, s));
+    KOLM_HIP_CHECK(hipMemcpyAsync(dob, obase.data(), sizeof(u32) * (nb + 1), hipMemcpyHostToDevice, s));
+    KOLM_HIP_CHECK(hipMemcpyAsync(dlist, flat.data(), sizeof(u32) * nb, hipMemcpyHostToDevice, s));
+    KOLM_HIP_CHECK(hipMemsetAsync(dst, 0, sizeof(u32) * nb, s));
+    BwArgs a{};
+    const u64 T = total + 16;
+    if (!bwl.empty()) {
+        u32* dmeth = c->get<u32>("dec_meth", nb);
+        u32* dvb = c->get<u32>("dec_vbase", nb + 1);
+        u32* dbwl = c->get<u32>("dec_bwlist", bwl.size());
+        KOLM_HIP_CHECK(hipMemcpyAsync(dmeth, methods, sizeof(u32) * nb, hipMemcpyHostToDevice, s));
+        KOLM_HIP_CHECK(hipMemcpyAsync(dvb, vb.data(), sizeof(u32) * (nb + 1), hipMemcpyHostToDevice, s));
+        KOLM_HIP_CHECK(hipMemcpyAsync(dbwl, bwl.data(), sizeof(u32) * bwl.size(), hipMemcpyHostToDevice, s));
+        a.d = DecArgs{dpay, dpoff, dob, dout, dst, dbwl, (u32)bwl.size()};
+        a.meth = dmeth;
+        a.vbase = dvb;
+        a.vals = c->get<u8>("dec_vals", (u64)vb[nb] + 16);
+        a.mi = c->get<u8>("dec_mi", T);
+        a.bw = c->get<u8>("dec_bw", T);
+        a.cpb = (maxn + MTF_CHUNK - 1) / MTF_CHUNK;
+        const u64 nch = (u64)bwl.size() * a.cpb;
+        a.summ = c->get<u8>("dec_summ", nch * 256 + 16);
+        a.states = c->get<u8>("dec_states", nch * 256 + 16);
+        static const char* const xn[8] = {"dec_x0", "dec_x1", "dec_x2", "dec_x3", "dec_x4", "dec_x5", "dec_x6", "dec_x7"};
+        for (int k = 0; k < 8; ++k) a.X[k] = c->get<u32>(xn[k], T);
+    }
+    u32 *tpos = nullptr, *tval = nullptr, *ntok = nullptr, *mark = nullptr, *src = nullptr;
+    if (!lists[KOLM_M_LZ77].empty()) {
+        tpos = c->get<u32>("dec_tpos", T);
+        tval = c->get<u32>("dec_tval", T);
+        ntok = c->get<u32>("dec_ntok", nb);
+        mark = c->get<u32>("dec_mark", T);
+        src = c->get<u32>("dec_src", T);
+    }
+    auto args = [&](u32 m) { return DecArgs{dpay, dpoff, dob, dout, dst, dlist + lstart[m], lstart[m + 1] - lstart[m]}; };
+    if (ms) KOLM_HIP_CHECK(hipEventRecord(c->ev[0], s));
+    launch_dec_raw(args(KOLM_M_RAW), s);
+    launch_dec_uleb(args(KOLM_M_XOR), false, s);
+    launch_dec_uleb(args(KOLM_M_LFSR), true, s);
+    if (!lists[KOLM_M_LZ77].empty()) launch_dec_lz77(args(KOLM_M_LZ77), tpos, tval, ntok, mark, src, s);
+    if (!bwl.empty()) launch_dec_bw(a, s);
+    if (ms) KOLM_HIP_CHECK(hipEventRecord(c->ev[1], s));
+    std::vector<u32> st(nb);
+    KOLM_HIP_CHECK(hipMemcpyAsync(st.data(), dst, sizeof(u32) * nb, hipMemcpyDeviceToHost, s));
+    c->sync();
+    if (ms) {
+        float f = 0.f;
+        KOLM_HIP_CHECK(hipEventElapsedTime(&f, c->ev[0], c->ev[1]));
+        *ms = f;
+    }
+    for (u32 i = 0; i < nb; ++i)
+        if (st[i]) {
+            char msg[128];
+            snprintf(msg, sizeof msg, "block %u (method %u): %s", i, methods[i],
+                     st[i] == DEC_ELEN ? "decoded length mismatch" : "malformed payload");
+            set_err(msg);
+            return KOLM_EARG;
+        }
+    return KOLM_OK;
+}
+
+int kolm_decode_blocks(const uint8_t* payloads, const uint64_t* payload_off, const uint32_t* methods,
+                       const uint32_t* orig_lens, uint32_t nblocks, uint8_t* out, uint64_t out_cap) {
+    kolm_ctx* c = need_default();
+    if (!c) return KOLM_ENOINIT;
+    if (nblocks && (!payloads || !payload_off || !methods || !orig_lens || !out)) return KOLM_EARG;
+    u64 total = 0;
+    if (int rc = check_decode(payload_off, methods, orig_lens, nblocks, out_cap, total)) return rc;
     if (nblocks == 0) return KOLM_OK;
     return guarded([&] {
         std::lock_guard<std::mutex> g(c->mu);
         KOLM_HIP_CHECK(hipSetDevice(c->device));
-        hipStream_t s = c->stream;
         const u32 nb = nblocks;
         const u64 ptotal = payload_off[nb] - payload_off[0];
-        std::vector<u64> poff(nb + 1);
-        std::vector<u32> obase(nb + 1);
-        obase[0] = 0;
-        for (u32 i = 0; i <= nb; ++i) poff[i] = payload_off[i] - payload_off[0];
-        for (u32 i = 0; i < nb; ++i) obase[i + 1] = obase[i] + orig_lens[i];
-        // blocks per decoder
-        std::vector<u32> lists[KOLM_NCAND];
-        for (u32 i = 0; i < nb; ++i) lists[methods[i]].push_back(i);
-        std::vector<u32> flat;
-        u32 lstart[KOLM_NCAND + 1];
-        for (u32 m = 0; m < KOLM_NCAND; ++m) {
-            lstart[m] = (u32)flat.size();
-            flat.insert(flat.end(), lists[m].begin(), lists[m].end());
-        }
-        lstart[KOLM_NCAND] = (u32)flat.size();
         u8* dpay = c->get<u8>("dec_pay", ptotal + 64);
-        u64* dpoff = c->get<u64>("dec_poff", nb + 1);
-        u32* dob = c->get<u32>("dec_obase", nb + 1);
-        u32* dlist = c->get<u32>("dec_list", nb);
-        u32* dst = c->get<u32>("dec_status", nb);
         u8* dout = c->get<u8>("dec_out", total + 64);
         if (ptotal)
-            KOLM_HIP_CHECK(hipMemcpyAsync(dpay, payloads + payload_off[0], ptotal, hipMemcpyHostToDevice, s));
-        KOLM_HIP_CHECK(hipMemcpyAsync(dpoff, poff.data(), sizeof(u64) * (nb + 1), hipMemcpyHostToDevice, s));
-        KOLM_HIP_CHECK(hipMemcpyAsync(dob, obase.data(), sizeof(u32) * (nb + 1), hipMemcpyHostToDevice, s));
-        KOLM_HIP_CHECK(hipMemcpyAsync(dlist, flat.data(), sizeof(u32) * nb, hipMemcpyHostToDevice, s));
-        KOLM_HIP_CHECK(hipMemsetAsync(dst, 0, sizeof(u32) * nb, s));
-        auto args = [&](u32 m) {
-            return DecArgs{dpay, dpoff, dob, dout, dst, dlist + lstart[m], lstart[m + 1] - lstart[m]};
-        };
-        launch_dec_raw(args(KOLM_M_RAW), s);
-        launch_dec_uleb(args(KOLM_M_XOR), false, s);
-        launch_dec_uleb(args(KOLM_M_LFSR), true, s);
-        if (!lists[KOLM_M_LZ77].empty()) {
-            const u64 T = total + 16;
-            launch_dec_lz77(args(KOLM_M_LZ77), c->get<u32>("dec_tpos", T), c->get<u32>("dec_tval", T),
-                            c->get<u32>("dec_ntok", nb), c->get<u32>("dec_mark", T), c->get<u32>("dec_src", T), s);
-        }
-        // BBWT family: one list over ids 2..6 (the flags come from each block's id)
-        std::vector<u32> bwl;
-        u32 maxn = 0;
-        for (u32 m = KOLM_M_BBWT; m <= KOLM_M_BBWT_GRAY; ++m)
-            for (u32 i : lists[m]) {
-                bwl.push_back(i);
-                maxn = std::max(maxn, orig_lens[i]);
-            }
-        if (!bwl.empty()) {
-            const u64 T = total + 16;
-            std::vector<u32> vb(nb + 1);
-            vb[0] = 0;
-            for (u32 i = 0; i < nb; ++i)
-                vb[i + 1] = vb[i] + (methods[i] == KOLM_M_BBWT_BP ? 8 * ((orig_lens[i] + 7) / 8) : 0u);
-            u32* dmeth = c->get<u32>("dec_meth", nb);
-            u32* dvb = c->get<u32>("dec_vbase", nb + 1);
-            u32* dbwl = c->get<u32>("dec_bwlist", bwl.size());
-            KOLM_HIP_CHECK(hipMemcpyAsync(dmeth, methods, sizeof(u32) * nb, hipMemcpyHostToDevice, s));
-            KOLM_HIP_CHECK(hipMemcpyAsync(dvb, vb.data(), sizeof(u32) * (nb + 1), hipMemcpyHostToDevice, s));
-            KOLM_HIP_CHECK(hipMemcpyAsync(dbwl, bwl.data(), sizeof(u32) * bwl.size(), hipMemcpyHostToDevice, s));
-            BwArgs a{};
-            a.d = DecArgs{dpay, dpoff, dob, dout, dst, dbwl, (u32)bwl.size()};
-            a.meth = dmeth;
-            a.vbase = dvb;
-            a.vals = c->get<u8>("dec_vals", (u64)vb[nb] + 16);
-            a.mi = c->get<u8>("dec_mi", T);
-            a.bw = c->get<u8>("dec_bw", T);
-            a.cpb = (maxn + MTF_CHUNK - 1) / MTF_CHUNK;
-            const u64 nch = (u64)bwl.size() * a.cpb;
-            a.summ = c->get<u8>("dec_summ", nch * 256 + 16);
-            a.states = c->get<u8>("dec_states", nch * 256 + 16);
-            static const char* const xn[8] = {"dec_x0", "dec_x1", "dec_x2", "dec_x3", "dec_x4", "dec_x5", "dec_x6", "dec_x7"};
-            for (int k = 0; k < 8; ++k) a.X[k] = c->get<u32>(xn[k], T);
-            launch_dec_bw(a, s);
-        }
-        std::vector<u32> st(nb);
-        KOLM_HIP_CHECK(hipMemcpyAsync(st.data(), dst, sizeof(u32) * nb, hipMemcpyDeviceToHost, s));
-        c->sync();
-        for (u32 i = 0; i < nb; ++i)
-            if (st[i]) {
-                char msg[128];
-                snprintf(msg, sizeof msg, "block %u (method %u): %s", i, methods[i],
-                         st[i] == DEC_ELEN ? "decoded length mismatch" : "malformed payload");
-                set_err(msg);
-                return KOLM_EARG;
-            }
+            KOLM_HIP_CHECK(hipMemcpyAsync(dpay, payloads + payload_off[0], ptotal, hipMemcpyHostToDevice, c->stream));
+        if (int rc = decode_batch(c, dpay, payload_off, methods, orig_lens, nb, total, dout, nullptr)) return rc;
         KOLM_HIP_CHECK(hipMemcpy(out, dout, total, hipMemcpyDeviceToHost));
         return KOLM_OK;
+    });
+}
+
+int kolm_decode_blocks_device(kolm_ctx* c, const void* d_payloads, const uint64_t* payload_off,
+                              const uint32_t* methods, const uint32_t* orig_lens, uint32_t nblocks, void* d_out,
+                              uint64_t out_cap, double* ms) {
+    if (!c) return KOLM_EARG;
+    if (nblocks && (!d_payloads || !payload_off || !methods || !orig_lens || !d_out)) return KOLM_EARG;
+    u64 total = 0;
+    if (int rc = check_decode(payload_off, methods, orig_lens, nblocks, out_cap, total)) return rc;
+    if (ms) *ms = 0.0;
+    if (nblocks == 0) return KOLM_OK;
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        return decode_batch(c, static_cast<const u8*>(d_payloads) + payload_off[0], payload_off, methods, orig_lens,
+                            nblocks, total, static_cast<u8*>(d_out), ms);
     });
 }
 

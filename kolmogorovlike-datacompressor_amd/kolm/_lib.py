@@ -111,6 +111,7 @@ SIGNATURES = [
     ("kolm_cdc_boundaries", I32, [U8P, U64, U32, U32, U32, I32, P, U64, ctypes.POINTER(U64)]),
     ("kolm_cdc_boundaries_device", I32, [P, P, U64, U32, U32, U32, I32, P, U64, ctypes.POINTER(U64)]),
     ("kolm_decode_blocks", I32, [P, P, P, P, U32, P, U64]),
+    ("kolm_decode_blocks_device", I32, [P, P, P, P, P, U32, P, U64, ctypes.POINTER(ctypes.c_double)]),
 ]
 KOLM_DECODE_MASK = 0x1FF  # methods decoded on the device: 0..8 (kolm.h)
 

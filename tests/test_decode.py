@@ -134,3 +134,45 @@ def test_malformed_payloads(kolm_gpu):
     good = b"hello"
     with pytest.raises(_lib.KolmError, match="block 1"):
         _lib.decode_blocks([good, b"\x02"], [0, 7], [5, 1])
+
+
+def test_decode_device_entry(kolm_gpu):
+    """kolm_decode_blocks_device: payloads resident in device memory (an encode arena),
+    output to device memory, kernel time reported; round trip exact."""
+    import ctypes
+    from kolm import _lib
+    L = _lib.load()
+    blocks = list(_blocks())
+    pays, mids = [], []
+    for j, blk in enumerate(blocks):
+        mid = (2, 7, 3, 0, 6, 1, 8, 4)[j % 8]
+        _, _, p, _ = _lib.encode_blocks(blk, len(blk), cand_mask=1 << mid, force=[mid])
+        pays.append(p[0])
+        mids.append(mid)
+    arena = b"".join(pays)
+    off = np.zeros(len(pays) + 1, np.uint64)
+    off[1:] = np.cumsum([len(p) for p in pays])
+    meth = np.asarray(mids, np.uint32)
+    lens = np.asarray([len(b) for b in blocks], np.uint32)
+    total = int(lens.sum())
+    ctx = ctypes.c_void_p()
+    _lib.check(L.kolm_ctx_create(0, ctypes.byref(ctx)))
+    try:
+        dp, do = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(L.kolm_dev_alloc(ctx, len(arena) + 64, ctypes.byref(dp)))
+        _lib.check(L.kolm_dev_alloc(ctx, total + 64, ctypes.byref(do)))
+        _lib.check(L.kolm_memcpy_h2d(ctx, dp, arena, len(arena)))
+        ms = ctypes.c_double(-1.0)
+        _lib.check(L.kolm_decode_blocks_device(ctx, dp, off.ctypes.data, meth.ctypes.data, lens.ctypes.data,
+                                               len(blocks), do, total, ctypes.byref(ms)))
+        out = ctypes.create_string_buffer(total)
+        _lib.check(L.kolm_memcpy_d2h(ctx, out, do, total))
+        assert out.raw == b"".join(blocks)
+        assert ms.value > 0.0
+        with pytest.raises(_lib.KolmError):  # capacity
+            _lib.check(L.kolm_decode_blocks_device(ctx, dp, off.ctypes.data, meth.ctypes.data, lens.ctypes.data,
+                                                   len(blocks), do, total - 1, None))
+        L.kolm_dev_free(ctx, dp)
+        L.kolm_dev_free(ctx, do)
+    finally:
+        L.kolm_ctx_destroy(ctx)
