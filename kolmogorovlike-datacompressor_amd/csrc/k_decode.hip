@@ -290,10 +290,11 @@ __device__ inline u32 rice_walk(u64 w, u32 nvalid, u32 st, u32& starts, F&& on_s
 __device__ inline u64 word_at(const u8* p, u32 plen, u32 wi) { return bits64(p, plen, wi * 64); }
 
 // One workgroup per block: per-thread word ranges -> phase functions -> sequential phase
-// chain over the 256 ranges -> values at every codeword start (index < L), inverse map,
+// chain over the DRC ranges -> values at every codeword start (index < L), inverse map,
 // bit-plane transpose for id 3.  Output: MTF indices at obase.
-__global__ __launch_bounds__(256) void k_dec_rice(BwArgs a) {
-    __shared__ u32 fex[256][4], fcnt[256][4], entry[256], sbase[256];
+constexpr u32 DRC = 1024;  // threads of the Rice parse (word ranges per block)
+__global__ __launch_bounds__(DRC) void k_dec_rice(BwArgs a) {
+    __shared__ u32 fex[DRC][4], fcnt[DRC][4], entry[DRC], sbase[DRC];
     __shared__ u32 total;
     const u32 b = a.d.list[blockIdx.x], tid = threadIdx.x;
     const u64 p0 = a.d.poff[b];
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(256) void k_dec_rice(BwArgs a) {
     const u32 L = (flags & 1) ? 8 * ((n + 7) / 8) : n;
     const u8* p = a.d.pay + p0;
     const u32 nbits = plen * 8, nw = (nbits + 63) / 64;
-    const u32 per = (nw + 255) / 256, w0 = min(tid * per, nw), w1 = min(w0 + per, nw);
+    const u32 per = (nw + DRC - 1) / DRC, w0 = min(tid * per, nw), w1 = min(w0 + per, nw);
     // phase function of the thread's words for each entry phase
     for (u32 e = 0; e < 4; ++e) {
         u32 st = e, cnt = 0;
@@ -315,7 +316,7 @@ __global__ __launch_bounds__(256) void k_dec_rice(BwArgs a) {
     __syncthreads();
     if (tid == 0) {
         u32 st = RS_S, base = 0;
-        for (u32 t = 0; t < 256; ++t) {
+        for (u32 t = 0; t < DRC; ++t) {
             entry[t] = st;
             sbase[t] = base;
             base += fcnt[t][st];
@@ -356,7 +357,7 @@ __global__ __launch_bounds__(256) void k_dec_rice(BwArgs a) {
         return;
     }
     if (flags & 1) {  // bit-plane deinterleave (PY:1122-1134): the 8x8 bit transpose is an involution
-        for (u32 gi = tid; gi < L / 8; gi += 256) {
+        for (u32 gi = tid; gi < L / 8; gi += DRC) {
             u32 in[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) in[i] = dst[8 * gi + i];
@@ -441,42 +442,96 @@ __global__ __launch_bounds__(DRT) void k_dec_mtf_replay(BwArgs a, u32 nch) {
     for (u32 i = lo; i < hi; ++i) a.bw[i] = (u8)mtf_pop_front(tab, t, a.mi[i]);
 }
 
-// Inverse BBWT (PY:425-454), one workgroup per block.  pi = stable sort of positions by
-// byte; every cycle of pi is one factor, read from its minimum c as L[pi(c)], L[pi^2(c)],
-// ..., L[c]; factors are emitted by decreasing minimum.  Here: cycle minima by doubling
-// (m <- min(m, m[P]), P <- P[P]), the steps s(x) from x to its minimum by list ranking,
-// cycle lengths d(c) = s(pi(c)) + 1, factor offsets by a reverse scan over the minima, and
-// x = pi^k(c) with k = d(c) - s(x) lands at offset(c) + k - 1.
-__global__ __launch_bounds__(1024) void k_dec_bwi(BwArgs a) {
-    __shared__ u32 hist[256], running[256];
-    __shared__ u32 wcnt[16][256];
-    __shared__ u32 sh[16];
-    __shared__ u32 carry_s;
-    const u32 b = a.d.list[blockIdx.x], tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const u32 o0 = a.d.obase[b], n = a.d.obase[b + 1] - o0;
-    if (a.d.status[b] != DEC_OK || n == 0) return;
-    const u8* L = a.bw + o0;
-    u32 *PI = a.X[0] + o0, *P0 = a.X[1] + o0, *P1 = a.X[2] + o0, *M0 = a.X[3] + o0, *M1 = a.X[4] + o0;
-    u32 *N0 = a.X[5] + o0, *N1 = a.X[6] + o0, *W0 = a.X[7] + o0;
-    // (a) stable counting sort by byte
-    for (u32 i = tid; i < 256; i += 1024) hist[i] = 0;
+// Inverse BBWT (PY:425-454), grid-wide.  PI = stable counting sort of the BBWT string L
+// (F-slot x -> L index); every cycle of PI is one Lyndon factor, read from its minimum
+// slot m as L[PI(m)], L[PI^2(m)], ..., L[m], and the factors appear in descending order
+// of m.  Cycle minima and distances come from a
+// ruling set instead of pointer jumping over all n elements (n log n random gathers):
+//   * splitters = slots that are multiples of S = 1 << sshift; one thread per splitter
+//     walks PI to the next splitter, tagging every slot with (segment, offset);
+//   * cycles that hold no splitter (e.g. the n one-slot cycles of a run) are settled by
+//     their own elements: a slot walks until it meets a smaller slot or returns (minimum);
+//   * the splitter graph (<= BWI_NODES per block) is solved in LDS by one workgroup:
+//     min doubling, then list ranking cut at the segment holding the cycle minimum.
+constexpr u32 FREE = 0x80000000u;  // SEG tag of a slot on a splitter-free cycle (| its minimum)
+
+struct BwiBlock {
+    u32 b, o0, n;
+    bool ok;
+};
+__device__ inline BwiBlock bwi_block(const BwArgs& a, u32 li) {
+    BwiBlock r;
+    r.b = a.d.list[li];
+    r.o0 = a.d.obase[r.b];
+    r.n = a.d.obase[r.b + 1] - r.o0;
+    r.ok = a.d.status[r.b] == DEC_OK;
+    return r;
+}
+
+// (1) byte histogram per BWI_TILE tile
+__global__ __launch_bounds__(256) void k_bwi_hist(BwArgs a) {
+    __shared__ u32 h[256];
+    const BwiBlock k = bwi_block(a, blockIdx.y);
+    const u32 lo = blockIdx.x * BWI_TILE;
+    h[threadIdx.x] = 0;
     __syncthreads();
-    for (u32 i = tid; i < n; i += 1024) atomicAdd(&hist[L[i]], 1u);
-    __syncthreads();
-    if (tid == 0) {
-        u32 acc = 0;
-        for (u32 d = 0; d < 256; ++d) {
-            running[d] = acc;
-            acc += hist[d];
-        }
+    if (k.ok && lo < k.n) {
+        const u32 hi = min(lo + BWI_TILE, k.n);
+        const u8* L = a.bw + k.o0;
+        for (u32 i = lo + threadIdx.x; i < hi; i += 256) atomicAdd(&h[L[i]], 1u);
     }
+    __syncthreads();
+    a.th[((u64)blockIdx.y * a.tpb + blockIdx.x) * 256 + threadIdx.x] = h[threadIdx.x];
+}
+
+// (2) per block: slot of each tile's first byte value d = digit base + earlier tiles
+__global__ __launch_bounds__(256) void k_bwi_scan(BwArgs a) {
+    __shared__ u32 ws[4];
+    const BwiBlock k = bwi_block(a, blockIdx.x);
+    if (!k.ok || k.n == 0) return;
+    const u32 d = threadIdx.x, nt = (k.n + BWI_TILE - 1) / BWI_TILE;
+    u32* th = a.th + (u64)blockIdx.x * a.tpb * 256;
+    u32 acc = 0;
+    for (u32 t = 0; t < nt; ++t) {
+        const u32 c = th[t * 256 + d];
+        th[t * 256 + d] = acc;
+        acc += c;
+    }
+    const u32 incl = wave_incl_scan(acc, OpAddU(), 0u);
+    if ((d & 63) == 63) ws[d >> 6] = incl;
+    __syncthreads();
+    u32 base = incl - acc;
+    for (u32 q = 0; q < (d >> 6); ++q) base += ws[q];
+    for (u32 t = 0; t < nt; ++t) th[t * 256 + d] += base;
+}
+
+// (3) stable scatter PI[slot] = i (ballot ranking per wave, LDS counts across waves);
+// also resets SEG (unvisited) and D (cycle lengths) of the tile
+__global__ __launch_bounds__(1024) void k_bwi_scatter(BwArgs a) {
+    __shared__ u32 running[256];
+    __shared__ u32 wcnt[16][256];
+    const BwiBlock k = bwi_block(a, blockIdx.y);
+    const u32 lo = blockIdx.x * BWI_TILE;
+    if (!k.ok || lo >= k.n) return;
+    const u32 hi = min(lo + BWI_TILE, k.n);
+    const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const u32* th = a.th + ((u64)blockIdx.y * a.tpb + blockIdx.x) * 256;
+    if (tid < 256) running[tid] = th[tid];
     for (u32 i = tid; i < 16 * 256; i += 1024) (&wcnt[0][0])[i] = 0;
     __syncthreads();
+    const u8* L = a.bw + k.o0;
+    u32* PI = a.X[0] + k.o0;
+    u32* SEG = a.X[1] + k.o0;
+    u32* D = a.X[3] + k.o0;
     const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    for (u32 t0 = 0; t0 < n; t0 += 1024) {
-        const u32 i = t0 + tid;
-        const bool valid = i < n;
+    for (u32 s0 = lo; s0 < hi; s0 += 1024) {
+        const u32 i = s0 + tid;
+        const bool valid = i < hi;
         const u32 d = valid ? L[i] : 0u;
+        if (valid) {
+            SEG[i] = NONE;
+            D[i] = 0;
+        }
         u64 m = __ballot(valid);
 #pragma unroll
         for (u32 bit = 0; bit < 8; ++bit) {
@@ -502,73 +557,221 @@ __global__ __launch_bounds__(1024) void k_dec_bwi(BwArgs a) {
         }
         __syncthreads();
     }
-    // (b) cycle minima: ceil(log2 n) doubling rounds cover every cycle
+}
+
+// node arrays of list entry li: next splitter node, segment length, segment minimum,
+// cycle minimum, rank (distance from the cycle's anchor splitter)
+__device__ inline u32* bwi_nodes(const BwArgs& a, u32 arr, u32 li) {
+    return a.nd + ((u64)arr * a.d.nlist + li) * a.nnmax;
+}
+
+// (4) one thread per splitter: walk to the next splitter
+__global__ __launch_bounds__(256) void k_bwi_walk(BwArgs a) {
+    const BwiBlock k = bwi_block(a, blockIdx.y);
+    const u32 j = blockIdx.x * 256 + threadIdx.x;
+    const u32 x0 = j << a.sshift;
+    if (!k.ok || x0 >= k.n) return;
+    const u32 msk = (1u << a.sshift) - 1;
+    const u32* PI = a.X[0] + k.o0;
+    u32* SEG = a.X[1] + k.o0;
+    u32* OFS = a.X[2] + k.o0;
+    u32 y = x0, len = 0, smin = x0;
+    do {
+        SEG[y] = j;
+        OFS[y] = len;
+        smin = min(smin, y);
+        ++len;
+        y = PI[y];
+    } while (y & msk);
+    bwi_nodes(a, 0, blockIdx.y)[j] = y >> a.sshift;
+    bwi_nodes(a, 1, blockIdx.y)[j] = len;
+    bwi_nodes(a, 2, blockIdx.y)[j] = smin;
+}
+
+// (5) one thread per slot on a splitter-free cycle: is it the cycle minimum?  The
+// minimum then tags its cycle with (FREE | minimum, distance) and stores the length.
+__global__ __launch_bounds__(256) void k_bwi_free(BwArgs a) {
+    const BwiBlock k = bwi_block(a, blockIdx.y);
+    const u32 x = blockIdx.x * 256 + threadIdx.x;
+    if (!k.ok || x >= k.n) return;
+    u32* SEG = a.X[1] + k.o0;
+    if (SEG[x] != NONE) return;
+    const u32* PI = a.X[0] + k.o0;
+    u32* OFS = a.X[2] + k.o0;
+    u32 z = PI[x], t = 1;
+    while (z > x) {
+        z = PI[z];
+        ++t;
+    }
+    if (z != x) return;
+    a.X[3][k.o0 + x] = t;
+    u32 y = x, d = 0;
+    do {
+        SEG[y] = FREE | x;
+        OFS[y] = d++;
+        y = PI[y];
+    } while (y != x);
+}
+
+// (6) per block, the splitter graph in LDS: cycle minimum by min doubling, then the
+// distance of every splitter from its cycle's anchor (the splitter whose segment holds
+// the minimum) by list ranking with the link into the anchor cut
+constexpr u32 BWI_NPT = BWI_NODES / 1024;
+__global__ __launch_bounds__(1024) void k_bwi_nodes(BwArgs a) {
+    __shared__ u32 J[BWI_NODES], V[BWI_NODES];
+    const BwiBlock k = bwi_block(a, blockIdx.x);
+    if (!k.ok || k.n == 0) return;
+    const u32 nn = (k.n + (1u << a.sshift) - 1) >> a.sshift, tid = threadIdx.x;
+    const u32* NX = bwi_nodes(a, 0, blockIdx.x);
+    const u32* NL = bwi_nodes(a, 1, blockIdx.x);
+    const u32* NS = bwi_nodes(a, 2, blockIdx.x);
+    u32* NM = bwi_nodes(a, 3, blockIdx.x);
+    u32* NP = bwi_nodes(a, 4, blockIdx.x);
+    const u32* SEG = a.X[1] + k.o0;
     u32 R = 0;
-    while ((1u << R) < n) ++R;
-    for (u32 x = tid; x < n; x += 1024) {
-        const u32 y = PI[x];
-        P0[x] = y;
-        M0[x] = min(x, y);
+    while ((1u << R) < nn) ++R;
+    for (u32 j = tid; j < nn; j += 1024) {
+        J[j] = NX[j];
+        V[j] = NS[j];
+    }
+    __syncthreads();
+    u32 rj[BWI_NPT], rv[BWI_NPT];
+    for (u32 r = 0; r < R; ++r) {
+#pragma unroll
+        for (u32 q = 0; q < BWI_NPT; ++q) {
+            const u32 j = tid + q * 1024;
+            if (j < nn) {
+                const u32 y = J[j];
+                rv[q] = min(V[j], V[y]);
+                rj[q] = J[y];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (u32 q = 0; q < BWI_NPT; ++q) {
+            const u32 j = tid + q * 1024;
+            if (j < nn) {
+                V[j] = rv[q];
+                J[j] = rj[q];
+            }
+        }
+        __syncthreads();
+    }
+    u32 anc[BWI_NPT], cm[BWI_NPT];
+#pragma unroll
+    for (u32 q = 0; q < BWI_NPT; ++q) {
+        const u32 j = tid + q * 1024;
+        if (j < nn) {
+            cm[q] = V[j];
+            anc[q] = SEG[cm[q]];
+            NM[j] = cm[q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (u32 q = 0; q < BWI_NPT; ++q) {
+        const u32 j = tid + q * 1024;
+        if (j < nn) {
+            const u32 y = NX[j];
+            J[j] = y == anc[q] ? NONE : y;
+            V[j] = NL[j];
+        }
     }
     __syncthreads();
     for (u32 r = 0; r < R; ++r) {
-        for (u32 x = tid; x < n; x += 1024) {
-            const u32 y = P0[x];
-            M1[x] = min(M0[x], M0[y]);
-            P1[x] = P0[y];
+#pragma unroll
+        for (u32 q = 0; q < BWI_NPT; ++q) {
+            const u32 j = tid + q * 1024;
+            if (j < nn) {
+                const u32 y = J[j];
+                rv[q] = V[j] + (y != NONE ? V[y] : 0u);
+                rj[q] = y != NONE ? J[y] : NONE;
+            }
         }
         __syncthreads();
-        u32* t = P0; P0 = P1; P1 = t;
-        t = M0; M0 = M1; M1 = t;
-    }
-    // (c) steps to the cycle minimum by list ranking (x -> pi(x) unless x is the minimum)
-    u32* Wa = W0;
-    u32* Wb = P1;  // free now
-    for (u32 x = tid; x < n; x += 1024) {
-        const bool head = M0[x] == x;
-        N0[x] = head ? NONE : PI[x];
-        Wa[x] = head ? 0u : 1u;
-    }
-    __syncthreads();
-    for (u32 r = 0; r < R; ++r) {
-        for (u32 x = tid; x < n; x += 1024) {
-            const u32 y = N0[x];
-            Wb[x] = Wa[x] + (y != NONE ? Wa[y] : 0u);
-            N1[x] = y != NONE ? N0[y] : NONE;
+#pragma unroll
+        for (u32 q = 0; q < BWI_NPT; ++q) {
+            const u32 j = tid + q * 1024;
+            if (j < nn) {
+                V[j] = rv[q];
+                J[j] = rj[q];
+            }
         }
         __syncthreads();
-        u32* t = N0; N0 = N1; N1 = t;
-        t = Wa; Wa = Wb; Wb = t;
     }
-    // (d) cycle lengths at the minima, offsets by a reverse exclusive scan over positions
-    u32* D = P0;    // d(c) at minima
-    u32* OFF = N0;  // offset(c) at minima
-    for (u32 x = tid; x < n; x += 1024)
-        if (M0[x] == x) D[x] = Wa[PI[x]] + 1;
+    // V[j] = slots from splitter j forward to the anchor's splitter (the whole cycle for the anchor)
+#pragma unroll
+    for (u32 q = 0; q < BWI_NPT; ++q) {
+        const u32 j = tid + q * 1024;
+        if (j < nn) {
+            const u32 len = V[anc[q]];
+            NP[j] = j == anc[q] ? 0u : len - V[j];
+            if (j == anc[q]) a.X[3][k.o0 + cm[q]] = len;
+        }
+    }
+}
+
+// (7) per block: OFF[m] = sum of the cycle lengths D[m'] over minima m' > m (the factors
+// are emitted in descending order of their minimum slot); 16 slots per thread
+__global__ __launch_bounds__(1024) void k_bwi_offsets(BwArgs a) {
+    __shared__ u32 sh[16];
+    __shared__ u32 carry_s;
+    const BwiBlock k = bwi_block(a, blockIdx.x);
+    if (!k.ok || k.n == 0) return;
+    const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const u32* D = a.X[3] + k.o0;
+    u32* OFF = a.X[4] + k.o0;
     if (tid == 0) carry_s = 0;
     __syncthreads();
-    for (u32 t1 = n; t1 > 0;) {
-        const u32 t0 = t1 > 1024 ? t1 - 1024 : 0;
-        const u32 x = t1 - 1 - tid;  // descending within the tile
-        const bool valid = tid < t1 - t0;
-        const u32 v = (valid && M0[x] == x) ? D[x] : 0u;
-        const u32 incl = wave_incl_scan(v, OpAddU(), 0u);
+    for (u32 r0 = 0; r0 < k.n; r0 += 16 * 1024) {
+        // reversed index r -> slot n-1-r; thread covers r in [r0 + 16 tid, +16)
+        const u32 rb = r0 + 16 * tid;
+        u32 v[16], sum = 0;
+#pragma unroll
+        for (u32 q = 0; q < 16; ++q) {
+            const u32 r = rb + q;
+            v[q] = r < k.n ? D[k.n - 1 - r] : 0u;
+            sum += v[q];
+        }
+        const u32 incl = wave_incl_scan(sum, OpAddU(), 0u);
         if (lane == 63) sh[wv] = incl;
         __syncthreads();
-        u32 pre = carry_s;
+        u32 pre = carry_s + incl - sum;
         for (u32 q = 0; q < wv; ++q) pre += sh[q];
-        if (valid && M0[x] == x) OFF[x] = pre + incl - v;
+#pragma unroll
+        for (u32 q = 0; q < 16; ++q) {
+            const u32 r = rb + q;
+            if (v[q]) OFF[k.n - 1 - r] = pre;
+            pre += v[q];
+        }
         __syncthreads();
-        if (tid == 1023) carry_s = pre + incl;
+        if (tid == 1023) carry_s = pre;
         __syncthreads();
-        t1 = t0;
     }
-    // (e) emit
-    for (u32 x = tid; x < n; x += 1024) {
-        const u32 c = M0[x];
-        const u32 k = D[c] - Wa[x];
-        a.d.out[o0 + OFF[c] + k - 1] = L[x];
+}
+
+// (8) one thread per slot x = PI^t(m) of the cycle with minimum m:
+// out[OFF[m] + (t - 1 mod D[m])] = L[x]
+__global__ __launch_bounds__(256) void k_bwi_emit(BwArgs a) {
+    const BwiBlock k = bwi_block(a, blockIdx.y);
+    const u32 x = blockIdx.x * 256 + threadIdx.x;
+    if (!k.ok || x >= k.n) return;
+    const u32* SEG = a.X[1] + k.o0;
+    const u32* OFS = a.X[2] + k.o0;
+    const u32 s = SEG[x], o = OFS[x];
+    u32 m, t, dm;
+    if (s & FREE) {
+        m = s & ~FREE;
+        t = o;
+        dm = a.X[3][k.o0 + m];
+    } else {
+        m = bwi_nodes(a, 3, blockIdx.y)[s];
+        dm = a.X[3][k.o0 + m];
+        t = bwi_nodes(a, 4, blockIdx.y)[s] + o + dm - OFS[m];
+        if (t >= dm) t -= dm;
     }
+    const u32 idx = a.X[4][k.o0 + m] + (t ? t - 1 : dm - 1);
+    a.d.out[k.o0 + idx] = a.bw[k.o0 + x];
 }
 
 }  // namespace
@@ -576,11 +779,20 @@ __global__ __launch_bounds__(1024) void k_dec_bwi(BwArgs a) {
 void launch_dec_bw(const BwArgs& a, hipStream_t s) {
     if (!a.d.nlist) return;
     const u32 nch = a.d.nlist * a.cpb;
-    k_dec_rice<<<a.d.nlist, 256, 0, s>>>(a);
+    k_dec_rice<<<a.d.nlist, DRC, 0, s>>>(a);
     k_dec_mtf_summary<<<(nch + DRT - 1) / DRT, DRT, 0, s>>>(a, nch);
     k_dec_mtf_compose<<<a.d.nlist, 256, 0, s>>>(a);
     k_dec_mtf_replay<<<(nch + DRT - 1) / DRT, DRT, 0, s>>>(a, nch);
-    k_dec_bwi<<<a.d.nlist, 1024, 0, s>>>(a);
+    const u32 nl = a.d.nlist;
+    const u32 mx = a.tpb * BWI_TILE;  // >= the longest block
+    k_bwi_hist<<<dim3(a.tpb, nl), 256, 0, s>>>(a);
+    k_bwi_scan<<<nl, 256, 0, s>>>(a);
+    k_bwi_scatter<<<dim3(a.tpb, nl), 1024, 0, s>>>(a);
+    k_bwi_walk<<<dim3((a.nnmax + 255) / 256, nl), 256, 0, s>>>(a);
+    k_bwi_free<<<dim3((mx + 255) / 256, nl), 256, 0, s>>>(a);
+    k_bwi_nodes<<<nl, 1024, 0, s>>>(a);
+    k_bwi_offsets<<<nl, 1024, 0, s>>>(a);
+    k_bwi_emit<<<dim3((mx + 255) / 256, nl), 256, 0, s>>>(a);
 }
 
 void launch_dec_raw(const DecArgs& a, hipStream_t s) {

@@ -1364,8 +1364,14 @@ static int decode_batch(kolm_ctx* c, const u8* dpay, const uint64_t* payload_off
         const u64 nch = (u64)bwl.size() * a.cpb;
         a.summ = c->get<u8>("dec_summ", nch * 256 + 16);
         a.states = c->get<u8>("dec_states", nch * 256 + 16);
-        static const char* const xn[8] = {"dec_x0", "dec_x1", "dec_x2", "dec_x3", "dec_x4", "dec_x5", "dec_x6", "dec_x7"};
-        for (int k = 0; k < 8; ++k) a.X[k] = c->get<u32>(xn[k], T);
+        static const char* const xn[5] = {"dec_x0", "dec_x1", "dec_x2", "dec_x3", "dec_x4"};
+        for (int k = 0; k < 5; ++k) a.X[k] = c->get<u32>(xn[k], T);
+        a.tpb = (maxn + BWI_TILE - 1) / BWI_TILE;
+        a.th = c->get<u32>("dec_th", (u64)bwl.size() * a.tpb * 256 + 16);
+        a.sshift = 6;
+        while (((u64)maxn + (1ull << a.sshift) - 1) >> a.sshift > BWI_NODES) ++a.sshift;
+        a.nnmax = (u32)(((u64)maxn + (1ull << a.sshift) - 1) >> a.sshift);
+        a.nd = c->get<u32>("dec_nodes", 5ull * bwl.size() * a.nnmax + 16);
     }
     u32 *tpos = nullptr, *tval = nullptr, *ntok = nullptr, *mark = nullptr, *src = nullptr;
     if (!lists[KOLM_M_LZ77].empty()) {

@@ -411,8 +411,15 @@ struct BwArgs {
     u8* summ;          // [nlist * cpb * 256] MTF chunk summaries
     u8* states;        // [nlist * cpb * 256] MTF chunk entry tables
     u32 cpb;           // MTF chunks per block slot (longest block / MTF_CHUNK)
-    u32* X[8];         // [N] u32 scratch of the inverse BBWT
+    u32* X[5];         // [N] u32 scratch of the inverse BBWT: PI, SEG, OFS, D, OFF
+    u32* th;           // [nlist * tpb * 256] counting-sort tile histograms / offsets
+    u32* nd;           // [5 * nlist * nnmax] ruling-set node arrays (next, length, min, cycle min, rank)
+    u32 tpb;           // counting-sort tiles per block slot
+    u32 sshift;        // splitters: elements whose local index is a multiple of 1 << sshift
+    u32 nnmax;         // nodes per block slot (<= BWI_NODES)
 };
+constexpr u32 BWI_TILE = 4096;    // counting-sort tile of the inverse BBWT
+constexpr u32 BWI_NODES = 16384;  // ruling-set nodes per block (LDS-resident in k_bwi_nodes)
 void launch_dec_bw(const BwArgs& a, hipStream_t s);
 
 }  // namespace kolm
