@@ -287,88 +287,168 @@ __device__ inline u32 rice_walk(u64 w, u32 nvalid, u32 st, u32& starts, F&& on_s
     return st;
 }
 
-__device__ inline u64 word_at(const u8* p, u32 plen, u32 wi) { return bits64(p, plen, wi * 64); }
+// 64 stream bits from bit g: two aligned 8-byte loads inside the payload (bytes near its
+// end one at a time, zero past plen)
+__device__ inline u64 bits64f(const u8* p, u32 plen, u32 g) {
+    const u32 B = g >> 3, s = g & 7;
+    if (B + 16 <= plen) {
+        const uintptr_t ad = (uintptr_t)(p + B);
+        const u64* q = reinterpret_cast<const u64*>(ad & ~(uintptr_t)7);
+        const u32 sh = (u32)(ad & 7) * 8;
+        const u64 lo = q[0], hi = q[1];
+        const u64 be = __builtin_bswap64(sh ? (lo >> sh) | (hi << (64 - sh)) : lo);
+        if (!s) return be;
+        return (be << s) | ((u32)((hi >> sh) & 0xFFu) >> (8 - s));
+    }
+    return bits64(p, plen, g);
+}
 
-// One workgroup per block: per-thread word ranges -> phase functions -> sequential phase
-// chain over the DRC ranges -> values at every codeword start (index < L), inverse map,
-// bit-plane transpose for id 3.  Output: MTF indices at obase.
-constexpr u32 DRC = 1024;  // threads of the Rice parse (word ranges per block)
-__global__ __launch_bounds__(DRC) void k_dec_rice(BwArgs a) {
+struct RiceBlk {
+    u32 b, plen, nbits, nw, o0, n, flags, L, wb;
+    const u8* p;
+};
+__device__ inline RiceBlk rice_blk(const BwArgs& a, u32 li) {
+    RiceBlk k;
+    k.b = a.d.list[li];
+    const u64 p0 = a.d.poff[k.b];
+    k.plen = (u32)(a.d.poff[k.b + 1] - p0);
+    k.p = a.d.pay + p0;
+    k.nbits = k.plen * 8;
+    k.nw = (k.nbits + 63) / 64;
+    k.o0 = a.d.obase[k.b];
+    k.n = a.d.obase[k.b + 1] - k.o0;
+    k.flags = bw_flags(a.meth[k.b]);
+    k.L = (k.flags & 1) ? 8 * ((k.n + 7) / 8) : k.n;
+    k.wb = a.wbase[li];
+    return k;
+}
+
+// Rice parse, three grid-wide steps over the 64-bit words of every payload:
+// (A) each word's phase function: exit phase + codeword starts for each entry phase
+__global__ __launch_bounds__(256) void k_rice_phase(BwArgs a) {
+    const RiceBlk k = rice_blk(a, blockIdx.y);
+    const u32 wi = blockIdx.x * 256 + threadIdx.x;
+    if (wi >= k.nw) return;
+    const u64 w = bits64f(k.p, k.plen, wi * 64);
+    const u32 nv = min(64u, k.nbits - wi * 64);
+    u32 f = 0;
+#pragma unroll
+    for (u32 e = 0; e < 4; ++e) {
+        u32 cnt = 0;  // <= 22 starts per word
+        const u32 ex = rice_walk(w, nv, e, cnt, [](u32) {});
+        f |= (ex | (cnt << 2)) << (8 * e);
+    }
+    a.fw[k.wb + wi] = f;
+}
+
+// (B) per block: compose the functions over per-thread word ranges, chain the ranges,
+// then every word's entry phase and first value index; too few values -> malformed
+constexpr u32 DRC = 1024;
+__global__ __launch_bounds__(DRC) void k_rice_chain(BwArgs a) {
     __shared__ u32 fex[DRC][4], fcnt[DRC][4], entry[DRC], sbase[DRC];
     __shared__ u32 total;
-    const u32 b = a.d.list[blockIdx.x], tid = threadIdx.x;
-    const u64 p0 = a.d.poff[b];
-    const u32 plen = (u32)(a.d.poff[b + 1] - p0);
-    const u32 o0 = a.d.obase[b], n = a.d.obase[b + 1] - o0;
-    const u32 flags = bw_flags(a.meth[b]);
-    const u32 L = (flags & 1) ? 8 * ((n + 7) / 8) : n;
-    const u8* p = a.d.pay + p0;
-    const u32 nbits = plen * 8, nw = (nbits + 63) / 64;
-    const u32 per = (nw + DRC - 1) / DRC, w0 = min(tid * per, nw), w1 = min(w0 + per, nw);
-    // phase function of the thread's words for each entry phase
+    const RiceBlk k = rice_blk(a, blockIdx.x);
+    const u32 tid = threadIdx.x;
+    const u32 per = (k.nw + DRC - 1) / DRC, w0 = min(tid * per, k.nw), w1 = min(w0 + per, k.nw);
+    const u32* fw = a.fw + k.wb;
+    u32 st[4] = {0, 1, 2, 3}, cnt[4] = {0, 0, 0, 0};
+    for (u32 wi = w0; wi < w1; ++wi) {
+        const u32 f = fw[wi];
+#pragma unroll
+        for (u32 e = 0; e < 4; ++e) {
+            const u32 by = f >> (8 * st[e]);
+            cnt[e] += (by >> 2) & 63u;
+            st[e] = by & 3u;
+        }
+    }
+#pragma unroll
     for (u32 e = 0; e < 4; ++e) {
-        u32 st = e, cnt = 0;
-        for (u32 wi = w0; wi < w1; ++wi)
-            st = rice_walk(word_at(p, plen, wi), min(64u, nbits - wi * 64), st, cnt, [](u32) {});
-        fex[tid][e] = st;
-        fcnt[tid][e] = cnt;
+        fex[tid][e] = st[e];
+        fcnt[tid][e] = cnt[e];
     }
     __syncthreads();
     if (tid == 0) {
-        u32 st = RS_S, base = 0;
+        u32 s = RS_S, base = 0;
         for (u32 t = 0; t < DRC; ++t) {
-            entry[t] = st;
+            entry[t] = s;
             sbase[t] = base;
-            base += fcnt[t][st];
-            st = fex[t][st];
+            base += fcnt[t][s];
+            s = fex[t][s];
         }
         total = base;
     }
     __syncthreads();
-    bool bad = total < L;
-    u8* dst = (flags & 1) ? a.vals + a.vbase[b] : a.mi + o0;
-    {
-        u32 st = entry[tid], cnt = 0;
-        const u32 vb0 = sbase[tid];
-        for (u32 wi = w0; wi < w1; ++wi) {
-            st = rice_walk(word_at(p, plen, wi), min(64u, nbits - wi * 64), st, cnt, [&](u32 pos) {
-                const u32 vi = vb0 + cnt;
-                if (vi >= L) return;
-                const u32 g = wi * 64 + pos;
-                const u64 v = bits64(p, plen, g);
-                const u32 q = (u32)__clzll((long long)~v);
-                if (q > 63 || g + q + 2 >= nbits) {
-                    bad = true;
-                    return;
-                }
-                const u32 r0 = (p[(g + q + 1) >> 3] >> (7 - ((g + q + 1) & 7))) & 1u;
-                const u32 r1 = (p[(g + q + 2) >> 3] >> (7 - ((g + q + 2) & 7))) & 1u;
-                const u32 val = (q << 2) | (r0 << 1) | r1;
-                if (val > 255) {
-                    bad = true;
-                    return;
-                }
-                dst[vi] = (u8)inv_map(val, flags);
-            });
-        }
-    }
-    if (__syncthreads_or(bad)) {
-        if (tid == 0) a.d.status[b] = DEC_EFORMAT;
+    if (total < k.L) {
+        if (tid == 0) a.d.status[k.b] = DEC_EFORMAT;
         return;
     }
-    if (flags & 1) {  // bit-plane deinterleave (PY:1122-1134): the 8x8 bit transpose is an involution
-        for (u32 gi = tid; gi < L / 8; gi += DRC) {
-            u32 in[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) in[i] = dst[8 * gi + i];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                u32 v = 0;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v |= ((in[j] >> (7 - i)) & 1u) << (7 - j);
-                if (8 * gi + i < n) a.mi[o0 + 8 * gi + i] = (u8)v;
-            }
+    u32 s = entry[tid], base = sbase[tid];
+    for (u32 wi = w0; wi < w1; ++wi) {
+        a.es[k.wb + wi] = (u8)s;
+        a.vbw[k.wb + wi] = base;
+        const u32 by = fw[wi] >> (8 * s);
+        base += (by >> 2) & 63u;
+        s = by & 3u;
+    }
+}
+
+// (C) each word from its entry phase: the values of the codewords starting in it
+// (index < L), inverse bitwise map, written at their index
+__global__ __launch_bounds__(256) void k_rice_vals(BwArgs a) {
+    const RiceBlk k = rice_blk(a, blockIdx.y);
+    const u32 wi = blockIdx.x * 256 + threadIdx.x;
+    if (wi >= k.nw || a.d.status[k.b] != DEC_OK) return;
+    const u32 vb0 = a.vbw[k.wb + wi];
+    if (vb0 >= k.L) return;
+    u8* dst = (k.flags & 1) ? a.vals + a.vbase[k.b] : a.mi + k.o0;
+    const u64 w = bits64f(k.p, k.plen, wi * 64);
+    const u32 nv = min(64u, k.nbits - wi * 64);
+    u32 cnt = 0;
+    bool bad = false;
+    rice_walk(w, nv, a.es[k.wb + wi], cnt, [&](u32 pos) {
+        const u32 vi = vb0 + cnt;
+        if (vi >= k.L) return;
+        const u32 g = wi * 64 + pos;
+        const u64 v = pos ? bits64f(k.p, k.plen, g) : w;
+        const u32 q = (u32)__clzll((long long)~v);
+        if (q > 63 || g + q + 2 >= k.nbits) {  // unary run past the stream, or a value > 255
+            bad = true;
+            return;
         }
+        u32 r;
+        if (q <= 61) {  // both remainder bits inside v
+            r = (u32)(v >> (61 - q)) & 3u;
+        } else {
+            const u32 r0 = (k.p[(g + q + 1) >> 3] >> (7 - ((g + q + 1) & 7))) & 1u;
+            const u32 r1 = (k.p[(g + q + 2) >> 3] >> (7 - ((g + q + 2) & 7))) & 1u;
+            r = (r0 << 1) | r1;
+        }
+        const u32 val = (q << 2) | r;
+        if (val > 255) {
+            bad = true;
+            return;
+        }
+        dst[vi] = (u8)inv_map(val, k.flags);
+    });
+    if (bad) a.d.status[k.b] = DEC_EFORMAT;
+}
+
+// (D) bit-plane blocks (id 3): deinterleave (PY:1122-1134); the 8x8 bit transpose is an
+// involution
+__global__ __launch_bounds__(256) void k_rice_bitplane(BwArgs a) {
+    const RiceBlk k = rice_blk(a, blockIdx.y);
+    const u32 gi = blockIdx.x * 256 + threadIdx.x;
+    if (!(k.flags & 1) || gi >= k.L / 8 || a.d.status[k.b] != DEC_OK) return;
+    const u8* src = a.vals + a.vbase[k.b];
+    u32 in[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) in[i] = src[8 * gi + i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        u32 v = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v |= ((in[j] >> (7 - i)) & 1u) << (7 - j);
+        if (8 * gi + i < k.n) a.mi[k.o0 + 8 * gi + i] = (u8)v;
     }
 }
 
@@ -779,7 +859,11 @@ __global__ __launch_bounds__(256) void k_bwi_emit(BwArgs a) {
 void launch_dec_bw(const BwArgs& a, hipStream_t s) {
     if (!a.d.nlist) return;
     const u32 nch = a.d.nlist * a.cpb;
-    k_dec_rice<<<a.d.nlist, DRC, 0, s>>>(a);
+    const u32 wg = (a.wmax + 255) / 256;
+    k_rice_phase<<<dim3(wg, a.d.nlist), 256, 0, s>>>(a);
+    k_rice_chain<<<a.d.nlist, DRC, 0, s>>>(a);
+    k_rice_vals<<<dim3(wg, a.d.nlist), 256, 0, s>>>(a);
+    k_rice_bitplane<<<dim3((a.tpb * BWI_TILE / 8 + 255) / 256, a.d.nlist), 256, 0, s>>>(a);
     k_dec_mtf_summary<<<(nch + DRT - 1) / DRT, DRT, 0, s>>>(a, nch);
     k_dec_mtf_compose<<<a.d.nlist, 256, 0, s>>>(a);
     k_dec_mtf_replay<<<(nch + DRT - 1) / DRT, DRT, 0, s>>>(a, nch);

@@ -1372,6 +1372,20 @@ static int decode_batch(kolm_ctx* c, const u8* dpay, const uint64_t* payload_off
         while (((u64)maxn + (1ull << a.sshift) - 1) >> a.sshift > BWI_NODES) ++a.sshift;
         a.nnmax = (u32)(((u64)maxn + (1ull << a.sshift) - 1) >> a.sshift);
         a.nd = c->get<u32>("dec_nodes", 5ull * bwl.size() * a.nnmax + 16);
+        std::vector<u32> wb(bwl.size() + 1);
+        wb[0] = 0;
+        a.wmax = 0;
+        for (size_t li = 0; li < bwl.size(); ++li) {
+            const u64 nw = (poff[bwl[li] + 1] - poff[bwl[li]] + 7) / 8;
+            a.wmax = std::max(a.wmax, (u32)nw);
+            wb[li + 1] = wb[li] + (u32)nw;
+        }
+        u32* dwb = c->get<u32>("dec_wbase", wb.size());
+        KOLM_HIP_CHECK(hipMemcpyAsync(dwb, wb.data(), sizeof(u32) * wb.size(), hipMemcpyHostToDevice, s));
+        a.wbase = dwb;
+        a.fw = c->get<u32>("dec_fw", (u64)wb.back() + 16);
+        a.es = c->get<u8>("dec_es", (u64)wb.back() + 16);
+        a.vbw = c->get<u32>("dec_vbw", (u64)wb.back() + 16);
     }
     u32 *tpos = nullptr, *tval = nullptr, *ntok = nullptr, *mark = nullptr, *src = nullptr;
     if (!lists[KOLM_M_LZ77].empty()) {

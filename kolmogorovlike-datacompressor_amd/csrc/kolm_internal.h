@@ -417,6 +417,11 @@ struct BwArgs {
     u32 tpb;           // counting-sort tiles per block slot
     u32 sshift;        // splitters: elements whose local index is a multiple of 1 << sshift
     u32 nnmax;         // nodes per block slot (<= BWI_NODES)
+    const u32* wbase;  // [nlist + 1] first 64-bit payload word of each listed block
+    u32 wmax;          // most words of one payload
+    u32* fw;           // [words] Rice phase function per word (8 bits per entry phase)
+    u8* es;            // [words] entry phase per word
+    u32* vbw;          // [words] index of the first value starting in the word
 };
 constexpr u32 BWI_TILE = 4096;    // counting-sort tile of the inverse BBWT
 constexpr u32 BWI_NODES = 16384;  // ruling-set nodes per block (LDS-resident in k_bwi_nodes)
