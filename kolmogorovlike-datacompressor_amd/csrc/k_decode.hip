@@ -533,7 +533,7 @@ __global__ __launch_bounds__(DRT) void k_dec_mtf_replay(BwArgs a, u32 nch) {
 //     their own elements: a slot walks until it meets a smaller slot or returns (minimum);
 //   * the splitter graph (<= BWI_NODES per block) is solved in LDS by one workgroup:
 //     min doubling, then list ranking cut at the segment holding the cycle minimum.
-constexpr u32 FREE = 0x80000000u;  // SEG tag of a slot on a splitter-free cycle (| its minimum)
+constexpr u32 FREE = 0x80000000u;  // segment tag of a slot on a splitter-free cycle (| its minimum)
 
 struct BwiBlock {
     u32 b, o0, n;
@@ -586,7 +586,7 @@ __global__ __launch_bounds__(256) void k_bwi_scan(BwArgs a) {
 }
 
 // (3) stable scatter PI[slot] = i (ballot ranking per wave, LDS counts across waves);
-// also resets SEG (unvisited) and D (cycle lengths) of the tile
+// also resets SO (unvisited) and D (cycle lengths) of the tile
 __global__ __launch_bounds__(1024) void k_bwi_scatter(BwArgs a) {
     __shared__ u32 running[256];
     __shared__ u32 wcnt[16][256];
@@ -601,7 +601,7 @@ __global__ __launch_bounds__(1024) void k_bwi_scatter(BwArgs a) {
     __syncthreads();
     const u8* L = a.bw + k.o0;
     u32* PI = a.X[0] + k.o0;
-    u32* SEG = a.X[1] + k.o0;
+    u64* SO = a.so + k.o0;
     u32* D = a.X[3] + k.o0;
     const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     for (u32 s0 = lo; s0 < hi; s0 += 1024) {
@@ -609,7 +609,7 @@ __global__ __launch_bounds__(1024) void k_bwi_scatter(BwArgs a) {
         const bool valid = i < hi;
         const u32 d = valid ? L[i] : 0u;
         if (valid) {
-            SEG[i] = NONE;
+            SO[i] = NONE;
             D[i] = 0;
         }
         u64 m = __ballot(valid);
@@ -653,12 +653,10 @@ __global__ __launch_bounds__(256) void k_bwi_walk(BwArgs a) {
     if (!k.ok || x0 >= k.n) return;
     const u32 msk = (1u << a.sshift) - 1;
     const u32* PI = a.X[0] + k.o0;
-    u32* SEG = a.X[1] + k.o0;
-    u32* OFS = a.X[2] + k.o0;
+    u64* SO = a.so + k.o0;
     u32 y = x0, len = 0, smin = x0;
     do {
-        SEG[y] = j;
-        OFS[y] = len;
+        SO[y] = (u64)j | ((u64)len << 32);
         smin = min(smin, y);
         ++len;
         y = PI[y];
@@ -674,10 +672,9 @@ __global__ __launch_bounds__(256) void k_bwi_free(BwArgs a) {
     const BwiBlock k = bwi_block(a, blockIdx.y);
     const u32 x = blockIdx.x * 256 + threadIdx.x;
     if (!k.ok || x >= k.n) return;
-    u32* SEG = a.X[1] + k.o0;
-    if (SEG[x] != NONE) return;
+    u64* SO = a.so + k.o0;
+    if ((u32)SO[x] != NONE) return;
     const u32* PI = a.X[0] + k.o0;
-    u32* OFS = a.X[2] + k.o0;
     u32 z = PI[x], t = 1;
     while (z > x) {
         z = PI[z];
@@ -687,8 +684,8 @@ __global__ __launch_bounds__(256) void k_bwi_free(BwArgs a) {
     a.X[3][k.o0 + x] = t;
     u32 y = x, d = 0;
     do {
-        SEG[y] = FREE | x;
-        OFS[y] = d++;
+        SO[y] = (u64)(FREE | x) | ((u64)d << 32);
+        ++d;
         y = PI[y];
     } while (y != x);
 }
@@ -707,7 +704,7 @@ __global__ __launch_bounds__(1024) void k_bwi_nodes(BwArgs a) {
     const u32* NS = bwi_nodes(a, 2, blockIdx.x);
     u32* NM = bwi_nodes(a, 3, blockIdx.x);
     u32* NP = bwi_nodes(a, 4, blockIdx.x);
-    const u32* SEG = a.X[1] + k.o0;
+    const u64* SO = a.so + k.o0;
     u32 R = 0;
     while ((1u << R) < nn) ++R;
     for (u32 j = tid; j < nn; j += 1024) {
@@ -743,7 +740,7 @@ __global__ __launch_bounds__(1024) void k_bwi_nodes(BwArgs a) {
         const u32 j = tid + q * 1024;
         if (j < nn) {
             cm[q] = V[j];
-            anc[q] = SEG[cm[q]];
+            anc[q] = (u32)SO[cm[q]];
             NM[j] = cm[q];
         }
     }
@@ -836,9 +833,9 @@ __global__ __launch_bounds__(256) void k_bwi_emit(BwArgs a) {
     const BwiBlock k = bwi_block(a, blockIdx.y);
     const u32 x = blockIdx.x * 256 + threadIdx.x;
     if (!k.ok || x >= k.n) return;
-    const u32* SEG = a.X[1] + k.o0;
-    const u32* OFS = a.X[2] + k.o0;
-    const u32 s = SEG[x], o = OFS[x];
+    const u64* SO = a.so + k.o0;
+    const u64 so = SO[x];
+    const u32 s = (u32)so, o = (u32)(so >> 32);
     u32 m, t, dm;
     if (s & FREE) {
         m = s & ~FREE;
@@ -847,7 +844,7 @@ __global__ __launch_bounds__(256) void k_bwi_emit(BwArgs a) {
     } else {
         m = bwi_nodes(a, 3, blockIdx.y)[s];
         dm = a.X[3][k.o0 + m];
-        t = bwi_nodes(a, 4, blockIdx.y)[s] + o + dm - OFS[m];
+        t = bwi_nodes(a, 4, blockIdx.y)[s] + o + dm - (u32)(SO[m] >> 32);
         if (t >= dm) t -= dm;
     }
     const u32 idx = a.X[4][k.o0 + m] + (t ? t - 1 : dm - 1);

@@ -1364,8 +1364,10 @@ static int decode_batch(kolm_ctx* c, const u8* dpay, const uint64_t* payload_off
         const u64 nch = (u64)bwl.size() * a.cpb;
         a.summ = c->get<u8>("dec_summ", nch * 256 + 16);
         a.states = c->get<u8>("dec_states", nch * 256 + 16);
-        static const char* const xn[5] = {"dec_x0", "dec_x1", "dec_x2", "dec_x3", "dec_x4"};
-        for (int k = 0; k < 5; ++k) a.X[k] = c->get<u32>(xn[k], T);
+        a.X[0] = c->get<u32>("dec_x0", T);
+        a.X[3] = c->get<u32>("dec_x3", T);
+        a.X[4] = c->get<u32>("dec_x4", T);
+        a.so = c->get<u64>("dec_so", T);
         a.tpb = (maxn + BWI_TILE - 1) / BWI_TILE;
         a.th = c->get<u32>("dec_th", (u64)bwl.size() * a.tpb * 256 + 16);
         a.sshift = 6;

@@ -411,7 +411,8 @@ struct BwArgs {
     u8* summ;          // [nlist * cpb * 256] MTF chunk summaries
     u8* states;        // [nlist * cpb * 256] MTF chunk entry tables
     u32 cpb;           // MTF chunks per block slot (longest block / MTF_CHUNK)
-    u32* X[5];         // [N] u32 scratch of the inverse BBWT: PI, SEG, OFS, D, OFF
+    u32* X[5];         // [N] u32 scratch of the inverse BBWT: PI, -, -, D (cycle lengths), OFF
+    u64* so;           // [N] segment | offset << 32 of every slot (inverse BBWT)
     u32* th;           // [nlist * tpb * 256] counting-sort tile histograms / offsets
     u32* nd;           // [5 * nlist * nnmax] ruling-set node arrays (next, length, min, cycle min, rank)
     u32 tpb;           // counting-sort tiles per block slot
