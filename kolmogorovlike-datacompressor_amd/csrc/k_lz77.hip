@@ -183,12 +183,13 @@ __device__ void best_match(const LzArgs& z, const T& t, u32 p, u32 end, u32 i, u
 
 // Speculative parse of one chunk per wave; the 4 waves of a workgroup take 4 consecutive
 // chunks and share one LDS copy of their text windows [first chunk - 4096, last chunk
-// end + 64) (20 KiB): with 32 waves per CU each on its own window in global memory the
-// windows overflow L2 and every candidate compare re-fetches its line.
-constexpr u32 LZ_LWIN = LZ_WINDOW + 4 * LZ_CHUNK + 64;
+// end) (20 KiB): with 32 waves per CU each on its own window in global memory the windows
+// overflow L2 and every candidate compare re-fetches its line.  8 waves per SIMD (<= 64
+// VGPRs, 8 x 20 KiB of LDS per CU): the parse chain is latency-bound, occupancy is speed.
+constexpr u32 LZ_LWIN = LZ_WINDOW + 4 * LZ_CHUNK;
 
 template <bool LDS>
-__global__ __launch_bounds__(256) void k_lz_spec(LzArgs z, u32 nchunks) {
+__global__ __launch_bounds__(256, 8) void k_lz_spec(LzArgs z, u32 nchunks) {
     __shared__ __align__(16) u8 win[LDS ? LZ_LWIN : 4];
     const u32 lane = threadIdx.x & 63;
     const u32 c = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -200,7 +201,7 @@ __global__ __launch_bounds__(256) void k_lz_spec(LzArgs z, u32 nchunks) {
         const u32 bb = z.geo.base(b0), be = z.geo.end(b0);
         const u32 s0 = bb + k0 * LZ_CHUNK;
         const u32 lo = s0 > bb + LZ_WINDOW ? s0 - LZ_WINDOW : bb;
-        const u32 hi = min(s0 + 4 * LZ_CHUNK + 64, be);
+        const u32 hi = min(s0 + 4 * LZ_CHUNK, be);
         if (lo < hi) {
             const u32 n = hi - lo;
             if ((lo & 3) == 0 && ((uintptr_t)z.text & 3) == 0) {
