@@ -644,7 +644,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         KOLM_HIP_CHECK(hipEventRecord(ej[1], ms));
     };
     u8* bw = nullptr;
-    if (overlap == 2 && !serial) {
+    if (overlap >= 2 && !serial) {
         // the LZ77 parse (latency-bound) waits for round 0 of the cyclic sort and then runs
         // beside the doubling rounds; the 3-gram index runs beside Lyndon + round 0
         c->active = s;
