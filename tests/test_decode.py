@@ -176,3 +176,47 @@ def test_decode_device_entry(kolm_gpu):
         L.kolm_dev_free(ctx, do)
     finally:
         L.kolm_ctx_destroy(ctx)
+
+
+def _payload_of_L(L: bytes) -> bytes:
+    """Candidate-2 payload whose MTF+Rice layer decodes to the BBWT string L (any L has
+    an inverse BBWT: the cycles of its stable sort permutation)."""
+    import oracle as O
+    return O.rice_encode(O.mtf_encode(L), 2)
+
+
+def _L_with_permutation(P):
+    """A string L whose stable counting sort is the permutation P (F-slot x -> index
+    P[x]): split x at the descents of P and give each run the next byte value."""
+    n = len(P)
+    L = bytearray(n)
+    g = 0
+    for x in range(n):
+        if x and P[x] < P[x - 1]:
+            g += 1
+        L[P[x]] = g
+    assert g < 256
+    return bytes(L)
+
+
+def test_inverse_bbwt_arbitrary_strings(kolm_gpu):
+    """Inverse BBWT of arbitrary BBWT strings (not produced by the encoder): random bytes,
+    sorted runs (n one-slot cycles), two symbols, and a permutation whose one long cycle
+    avoids every splitter slot (multiples of 64) — decoded by the splitter-free path —
+    against the host decoder (PY:425-454)."""
+    from kolm import _lib
+    rng = np.random.default_rng(5)
+    cases = [rng.integers(0, 256, 100_000, dtype=np.uint8).tobytes(),
+             bytes(sorted(rng.integers(0, 256, 50_000, dtype=np.uint8).tobytes())),
+             rng.integers(0, 2, 70_000, dtype=np.uint8).tobytes(),
+             bytes(range(256)) * 40, bytes(1)]
+    n = 4096
+    S = [x for x in range(n) if x % 64]
+    pos = {s: j for j, s in enumerate(S)}
+    P = [x if x % 64 == 0 else S[(pos[x] + 7) % len(S)] for x in range(n)]
+    cases.append(_L_with_permutation(P))
+    pays = [_payload_of_L(L) for L in cases]
+    lens = [len(L) for L in cases]
+    got = _lib.decode_blocks(pays, [2] * len(cases), lens)
+    want = b"".join(H.decode_block(2, p, m) for p, m in zip(pays, lens))
+    assert got == want
