@@ -136,7 +136,7 @@ int kolm_cdc_boundaries(const uint8_t* data, uint64_t n, uint32_t min_size, uint
  * method id methods[i], original length orig_lens[i]; the blocks are written back to back
  * into out (sum of orig_lens bytes, out_cap available).  Method ids outside
  * KOLM_DECODE_MASK return KOLM_EARG; so do malformed payloads (message names the block). */
-#define KOLM_DECODE_MASK 0x1FFu  /* raw 0, xor 1, bbwt family 2..6, lz77 7, lfsr_pred 8 */
+#define KOLM_DECODE_MASK 0x3FFu  /* every candidate id 0..9 (raw, xor, bbwt family 2..6, lz77, lfsr_pred, repair) */
 int kolm_decode_blocks(const uint8_t* payloads, const uint64_t* payload_off, const uint32_t* methods,
                        const uint32_t* orig_lens, uint32_t nblocks, uint8_t* out, uint64_t out_cap);
 

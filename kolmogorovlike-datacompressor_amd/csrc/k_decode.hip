@@ -851,6 +851,208 @@ __global__ __launch_bounds__(256) void k_bwi_emit(BwArgs a) {
     a.d.out[k.o0 + idx] = a.bw[k.o0 + x];
 }
 
+// ---------------------------------------------------------------- Re-Pair (id 9)
+// PY:1913-1978 repair_decompress: "RP" ULEB(256) ULEB(nrules) nrules x (ULEB a, ULEB b)
+// ULEB(seq_len) seq_len x ULEB(sym); rule r defines symbol 256 + r; the output is the
+// expansion of the final sequence.  Device: (1) every ULEB value of the stream by start
+// flags + scan; (2) per block the rule lengths (rules only reference earlier symbols in
+// encoder output; a forward reference is rejected as malformed) and the final sequence's
+// output offsets; (3) breadth-first expansion: (symbol, offset) entries split into their
+// two children until only terminals remain (work = grammar tree nodes, depth iterations).
+constexpr u32 RP_INVALID = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(256) void k_rp_values(DecArgs a, u32* vals, u32* nval) {
+    __shared__ u32 sh[4];
+    const u32 b = a.list[blockIdx.x], tid = threadIdx.x;
+    const u64 p0 = a.poff[b];
+    const u32 plen = (u32)(a.poff[b + 1] - p0);
+    const u8* pay = a.pay + p0;
+    u32* V = vals + p0;
+    if (plen < 2 || pay[0] != 'R' || pay[1] != 'P') {
+        if (tid == 0) a.status[b] = DEC_EFORMAT;
+        return;
+    }
+    u32 vcount = 0;
+    for (u32 s0 = 2; s0 < plen; s0 += 2048) {
+        const u32 j0 = s0 + tid * 8;
+        u32 v[8];
+        u32 nv = 0;
+#pragma unroll
+        for (u32 e = 0; e < 8; ++e) {
+            const u32 j = j0 + e;
+            v[e] = RP_INVALID;
+            if (j < plen && (j == 2 || pay[j - 1] < 128)) {
+                u32 x = 0, q = j;
+                bool ok = false;
+                for (u32 shf = 0; shf < 35 && q < plen; shf += 7) {
+                    const u32 by = pay[q++];
+                    if (shf == 28 && (by & 0x70u)) break;  // >= 2^32
+                    x |= (by & 0x7Fu) << shf;
+                    if (!(by & 0x80u)) {
+                        ok = true;
+                        break;
+                    }
+                }
+                v[e] = ok && x != RP_INVALID ? x : RP_INVALID - 1;  // truncated / oversized -> marker
+                ++nv;
+            }
+        }
+        u32 tot = 0;
+        u32 vi = vcount + wg_excl_sum(nv, sh, &tot);
+#pragma unroll
+        for (u32 e = 0; e < 8; ++e)
+            if (v[e] != RP_INVALID) V[vi++] = v[e];
+        vcount += tot;
+    }
+    if (tid == 0) nval[b] = vcount;
+}
+
+constexpr u32 RP_LDS_RULES = 32768;  // rule lengths kept in LDS (longer grammars: global)
+constexpr u32 RP_CH = 2048;          // rules staged per chunk
+
+// One workgroup per block: header checks, rule lengths (sequential in rule order, lengths
+// in LDS, saturated above n), final-sequence offsets by a workgroup scan, first BFS level.
+__global__ __launch_bounds__(1024) void k_rp_rules(DecArgs a, const u32* vals, const u32* nval, u32* rlen,
+                                                   u64* ea, u32* ecount) {
+    __shared__ u32 L[RP_LDS_RULES];
+    __shared__ uint2 ch[RP_CH];
+    __shared__ u32 sh[16];
+    __shared__ u32 s_bad, s_carry;
+    const u32 b = a.list[blockIdx.x], tid = threadIdx.x;
+    if (a.status[b] != DEC_OK) return;
+    const u64 p0 = a.poff[b];
+    const u32* V = vals + p0;
+    u32* RL = rlen + p0;
+    const u32 nv = nval[b];
+    const u32 o0 = a.obase[b], n = a.obase[b + 1] - o0;
+    const u32 cap = n + 1;  // saturation: any expansion longer than the block is an error
+    // header: 256, nrules, 2 nrules symbols, seq_len, seq_len symbols
+    bool bad = nv < 3 || V[0] != 256u;
+    const u32 nr = bad ? 0u : V[1];
+    bad = bad || nr > (nv - 3) / 2;
+    const u32 sl = bad ? 0u : V[2 + 2 * nr];
+    bad = bad || sl > nv - 3 - 2 * nr || sl > n;
+    if (bad) {
+        if (tid == 0) a.status[b] = DEC_EFORMAT;
+        return;
+    }
+    if (tid == 0) s_bad = 0;
+    // rule lengths, in rule order
+    for (u32 c0 = 0; c0 < nr; c0 += RP_CH) {
+        const u32 m = min(RP_CH, nr - c0);
+        __syncthreads();
+        for (u32 i = tid; i < m; i += 1024) ch[i] = make_uint2(V[2 + 2 * (c0 + i)], V[3 + 2 * (c0 + i)]);
+        __syncthreads();
+        if (tid == 0) {
+            bool bb = false;
+            for (u32 i = 0; i < m; ++i) {
+                const u32 r = c0 + i, x = ch[i].x, y = ch[i].y;
+                if (x >= 256 + r || y >= 256 + r) {  // forward / self reference (or marker)
+                    bb = true;
+                    break;
+                }
+                const u32 lx = x < 256 ? 1u : (x - 256 < RP_LDS_RULES ? L[x - 256] : RL[x - 256]);
+                const u32 ly = y < 256 ? 1u : (y - 256 < RP_LDS_RULES ? L[y - 256] : RL[y - 256]);
+                const u32 l = min(lx + ly, cap);
+                if (r < RP_LDS_RULES)
+                    L[r] = l;
+                else
+                    RL[r] = l;
+            }
+            if (bb) s_bad = 1;
+        }
+    }
+    __syncthreads();
+    if (s_bad) {
+        if (tid == 0) a.status[b] = DEC_EFORMAT;
+        return;
+    }
+    for (u32 r = tid; r < min(nr, RP_LDS_RULES); r += 1024) RL[r] = L[r];
+    // final sequence: lengths, offsets, first level of entries
+    const u32* S = V + 3 + 2 * nr;
+    if (tid == 0) s_carry = 0;
+    __syncthreads();
+    bool sbad = false;
+    for (u32 j0 = 0; j0 < sl; j0 += 1024) {
+        const u32 j = j0 + tid;
+        u32 sym = 0, l = 0;
+        if (j < sl) {
+            sym = S[j];
+            if (sym >= 256 + nr) {
+                sbad = true;
+            } else {
+                l = sym < 256 ? 1u : (sym - 256 < RP_LDS_RULES ? L[sym - 256] : RL[sym - 256]);
+            }
+        }
+        u32 tot = 0;
+        const u32 off = s_carry + wg_excl_sum(l, sh, &tot);
+        if (j < sl && off + l <= n) ea[o0 + j] = (u64)sym | ((u64)off << 32);
+        if (j < sl && off + l > n) sbad = true;
+        __syncthreads();
+        if (tid == 0) s_carry = min(s_carry + tot, cap);  // totals past n are errors
+        __syncthreads();
+    }
+    const bool anyb = __syncthreads_or(sbad);
+    if (tid == 0) {
+        if (anyb || s_carry != n) a.status[b] = anyb && s_carry <= n ? DEC_EFORMAT : DEC_ELEN;
+        ecount[blockIdx.x] = sl;
+    }
+}
+
+// Breadth-first expansion, one workgroup per block: terminals write their byte, rule
+// entries append their two children (wave-aggregated LDS counter), until none remain.
+__global__ __launch_bounds__(1024) void k_rp_expand(DecArgs a, const u32* vals, const u32* rlen, u64* ea, u64* eb,
+                                                    const u32* ecount) {
+    __shared__ u32 s_next;
+    const u32 b = a.list[blockIdx.x], tid = threadIdx.x, lane = tid & 63;
+    if (a.status[b] != DEC_OK) return;
+    const u64 p0 = a.poff[b];
+    const u32* V = vals + p0;
+    const u32* RL = rlen + p0;
+    const u32 o0 = a.obase[b];
+    u8* out = a.out + o0;
+    u64* A = ea + o0;
+    u64* B = eb + o0;
+    u32 cnt = ecount[blockIdx.x];
+    while (cnt) {
+        if (tid == 0) s_next = 0;
+        __syncthreads();
+        for (u32 i0 = 0; i0 < cnt; i0 += 1024) {
+            const u32 i = i0 + tid;
+            const bool valid = i < cnt;
+            u64 e = valid ? A[i] : 0ull;
+            const u32 sym = (u32)e, off = (u32)(e >> 32);
+            const bool nt = valid && sym >= 256;
+            if (valid && !nt) out[off] = (u8)sym;
+            u32 x = 0, y = 0, lx = 0;
+            if (nt) {
+                const u32 r = sym - 256;
+                x = V[2 + 2 * r];
+                y = V[3 + 2 * r];
+                lx = x < 256 ? 1u : RL[x - 256];
+            }
+            const u64 m = __ballot(nt);
+            u32 base = 0;
+            if (m) {
+                const u32 leader = __ffsll((long long)m) - 1;
+                if (lane == leader) base = atomicAdd(&s_next, 2u * (u32)__popcll(m));
+                base = __shfl(base, leader);
+            }
+            if (nt) {
+                const u32 k = base + 2u * (u32)__popcll(m & ((1ull << lane) - 1ull));
+                B[k] = (u64)x | ((u64)off << 32);
+                B[k + 1] = (u64)y | ((u64)(off + lx) << 32);
+            }
+        }
+        __syncthreads();
+        cnt = s_next;
+        u64* t = A;
+        A = B;
+        B = t;
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 void launch_dec_bw(const BwArgs& a, hipStream_t s) {
@@ -886,6 +1088,14 @@ void launch_dec_uleb(const DecArgs& a, bool lfsr, hipStream_t s) {
         k_dec_uleb<true><<<a.nlist, 256, 0, s>>>(a);
     else
         k_dec_uleb<false><<<a.nlist, 256, 0, s>>>(a);
+}
+
+void launch_dec_repair(const DecArgs& a, u32* vals, u32* nval, u32* ecount, u32* rlen, u64* ea, u64* eb,
+                       hipStream_t s) {
+    if (!a.nlist) return;
+    k_rp_values<<<a.nlist, 256, 0, s>>>(a, vals, nval);
+    k_rp_rules<<<a.nlist, 1024, 0, s>>>(a, vals, nval, rlen, ea, ecount);
+    k_rp_expand<<<a.nlist, 1024, 0, s>>>(a, vals, rlen, ea, eb, ecount);
 }
 
 void launch_dec_lz77(const DecArgs& a, u32* tpos, u32* tval, u32* ntok, u32* mark, u32* src, hipStream_t s) {

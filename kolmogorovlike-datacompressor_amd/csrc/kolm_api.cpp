@@ -1423,6 +1423,17 @@ static int decode_batch(kolm_ctx* c, const u8* dpay, const uint64_t* payload_off
         mark = c->get<u32>("dec_mark", T);
         src = c->get<u32>("dec_src", T);
     }
+    u32 *rvals = nullptr, *rnval = nullptr, *recnt = nullptr, *rlen = nullptr;
+    u64 *rea = nullptr, *reb = nullptr;
+    if (!lists[KOLM_M_REPAIR].empty()) {
+        const u64 P = poff[nb] + 16;
+        rvals = c->get<u32>("dec_rvals", P);
+        rlen = c->get<u32>("dec_rlen", P);
+        rnval = c->get<u32>("dec_rnval", nb);
+        recnt = c->get<u32>("dec_recnt", lists[KOLM_M_REPAIR].size());
+        rea = c->get<u64>("dec_rea", T);
+        reb = c->get<u64>("dec_reb", T);
+    }
     auto args = [&](u32 m) { return DecArgs{dpay, dpoff, dob, dout, dst, dlist + lstart[m], lstart[m + 1] - lstart[m]}; };
     if (ms) KOLM_HIP_CHECK(hipEventRecord(c->ev[0], s));
     launch_dec_raw(args(KOLM_M_RAW), s);
@@ -1430,6 +1441,7 @@ static int decode_batch(kolm_ctx* c, const u8* dpay, const uint64_t* payload_off
     launch_dec_uleb(args(KOLM_M_LFSR), true, s);
     if (!lists[KOLM_M_LZ77].empty()) launch_dec_lz77(args(KOLM_M_LZ77), tpos, tval, ntok, mark, src, s);
     if (!bwl.empty()) launch_dec_bw(a, s);
+    if (rvals) launch_dec_repair(args(KOLM_M_REPAIR), rvals, rnval, recnt, rlen, rea, reb, s);
     if (ms) KOLM_HIP_CHECK(hipEventRecord(c->ev[1], s));
     std::vector<u32> st(nb);
     KOLM_HIP_CHECK(hipMemcpyAsync(st.data(), dst, sizeof(u32) * nb, hipMemcpyDeviceToHost, s));

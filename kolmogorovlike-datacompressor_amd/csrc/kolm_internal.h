@@ -400,6 +400,10 @@ void launch_dec_raw(const DecArgs& a, hipStream_t s);
 void launch_dec_uleb(const DecArgs& a, bool lfsr, hipStream_t s);
 // scratch arrays tpos/tval/mark/src: one u32 per output byte; ntok: [nb]
 void launch_dec_lz77(const DecArgs& a, u32* tpos, u32* tval, u32* ntok, u32* mark, u32* src, hipStream_t s);
+// Re-Pair (id 9): vals / rlen one u32 per payload byte (at the payload offset), ea / eb one
+// u64 per output byte, nval [nb], ecount [nlist]
+void launch_dec_repair(const DecArgs& a, u32* vals, u32* nval, u32* ecount, u32* rlen, u64* ea, u64* eb,
+                       hipStream_t s);
 // BBWT family (ids 2..6): Rice -> inverse map -> MTF decode -> inverse BBWT
 struct BwArgs {
     DecArgs d;         // list = the blocks with ids 2..6

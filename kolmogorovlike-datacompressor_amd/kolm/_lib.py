@@ -113,7 +113,7 @@ SIGNATURES = [
     ("kolm_decode_blocks", I32, [P, P, P, P, U32, P, U64]),
     ("kolm_decode_blocks_device", I32, [P, P, P, P, P, U32, P, U64, ctypes.POINTER(ctypes.c_double)]),
 ]
-KOLM_DECODE_MASK = 0x1FF  # methods decoded on the device: 0..8 (kolm.h)
+KOLM_DECODE_MASK = 0x3FF  # methods decoded on the device: every id 0..9 (kolm.h)
 
 
 def decode_blocks(payloads, methods, orig_lens) -> bytes:

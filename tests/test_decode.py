@@ -46,7 +46,7 @@ def _blocks():
     yield bytes(i & 0xFF for i in range(4099))
 
 
-@pytest.mark.parametrize("mid", list(range(9)))
+@pytest.mark.parametrize("mid", list(range(10)))
 def test_device_vs_host_per_method(kolm_gpu, mid):
     """Payloads of method `mid` (forced through the batched encoder) for assorted blocks,
     decoded in ONE device batch: equal to the inputs and to the host decoders."""
@@ -62,8 +62,7 @@ def test_device_vs_host_per_method(kolm_gpu, mid):
 
 
 def test_mixed_batch_large(kolm_gpu):
-    """64 MiB of 1 MiB blocks, hot-path candidates: the device batch decodes the LZ77 and
-    simple-model blocks, the rest go to the host decoders; round trip exact."""
+    """64 MiB of 1 MiB blocks, hot-path candidates, one device batch; round trip exact."""
     data = D.enwik_like(24 << 20) + D.splitmix64_bytes(8 << 20) + bytes(4 << 20)
     blob = kolm_gpu.compress_blocks_fixed(data, 1 << 20, hot_path=True)
     assert kolm_gpu.decompress(blob) == data
@@ -77,7 +76,7 @@ def test_mixed_methods_one_batch(kolm_gpu):
     blocks = list(_blocks())
     pays, mids = [], []
     for j, blk in enumerate(blocks * 2):
-        mid = j % 9
+        mid = j % 10
         _, _, p, _ = _lib.encode_blocks(blk, len(blk), cand_mask=1 << mid, force=[mid])
         pays.append(p[0])
         mids.append(mid)
@@ -128,8 +127,29 @@ def test_malformed_payloads(kolm_gpu):
             _lib.decode_blocks([b"\xff" * 16], [mid], [4])
         with pytest.raises(_lib.KolmError):   # Rice: too few values
             _lib.decode_blocks([b"\x00"], [mid], [100])
-    with pytest.raises(_lib.KolmError):  # method not decoded on the device
-        _lib.decode_blocks([b"x"], [9], [1])
+    def u(v):
+        out = bytearray()
+        while True:
+            out.append((v & 0x7F) | (0x80 if v >= 128 else 0))
+            v >>= 7
+            if not v:
+                return bytes(out)
+    rp = [
+        (b"XP" + u(256) + u(0) + u(1) + u(65), 1),                     # magic
+        (b"RP" + u(255) + u(0) + u(1) + u(65), 1),                     # terminal alphabet
+        (b"RP" + u(256) + u(5), 4),                                    # truncated rules
+        (b"RP" + u(256) + u(1) + u(256) + u(65) + u(1) + u(256), 2),   # self-referencing rule
+        (b"RP" + u(256) + u(1) + u(65) + u(66) + u(1) + u(257), 2),    # undefined symbol
+        (b"RP" + u(256) + u(0) + u(2) + u(65) + u(66), 3),             # length mismatch
+        (b"RP" + u(256) + u(0) + u(2) + u(65) + b"\x80", 2),           # truncated value
+    ]
+    for pay, n in rp:
+        with pytest.raises(_lib.KolmError):
+            _lib.decode_blocks([pay], [9], [n])
+    ok = b"RP" + u(256) + u(1) + u(65) + u(66) + u(3) + u(256) + u(67) + u(256)
+    assert _lib.decode_blocks([ok], [9], [5]) == b"ABCAB" == H.decode_block(9, ok, 5)
+    with pytest.raises(_lib.KolmError):  # method id outside the decoder registry
+        _lib.decode_blocks([b"x"], [10], [1])
     # a bad block in a batch fails the batch and names the block
     good = b"hello"
     with pytest.raises(_lib.KolmError, match="block 1"):
@@ -145,7 +165,7 @@ def test_decode_device_entry(kolm_gpu):
     blocks = list(_blocks())
     pays, mids = [], []
     for j, blk in enumerate(blocks):
-        mid = (2, 7, 3, 0, 6, 1, 8, 4)[j % 8]
+        mid = (2, 7, 3, 0, 6, 1, 8, 9)[j % 8]
         _, _, p, _ = _lib.encode_blocks(blk, len(blk), cand_mask=1 << mid, force=[mid])
         pays.append(p[0])
         mids.append(mid)
@@ -220,3 +240,11 @@ def test_inverse_bbwt_arbitrary_strings(kolm_gpu):
     got = _lib.decode_blocks(pays, [2] * len(cases), lens)
     want = b"".join(H.decode_block(2, p, m) for p, m in zip(pays, lens))
     assert got == want
+
+
+def test_repair_containers_large(kolm_gpu):
+    """Full candidate list (Re-Pair wins on text): 8 x 1 MiB text blocks + zeros + a
+    period-3 pattern decoded on the device (deep and wide grammars) == input == host."""
+    data = D.enwik_like(8 << 20, seed=21) + bytes(1 << 20) + b"abc" * 349_525
+    blob = kolm_gpu.compress_blocks_fixed(data, 1 << 20)
+    assert kolm_gpu.decompress(blob) == data
