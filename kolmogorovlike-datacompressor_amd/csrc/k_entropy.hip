@@ -6,8 +6,8 @@
 //   * bbwt family (PY:2028-2073, candidates 2..6 = flags 0, 1, 4, 8, 16): Rice k=2 of the
 //     MTF of the BBWT, optionally after bit-plane interleave (8-byte groups, zero padded,
 //     PY:1100-1120), nibble swap, bit reverse or Gray code (PY:1650-1662).
-// One read of (text, mtf) per block produces all sizes (5 Rice variants + xor + lfsr);
-// only the MDL winner (PY:2350-2369: smallest payload, ties -> lowest id) is emitted.
+// The 5 Rice sizes are counted by the MTF replay as it produces the indices (k_mtf.hip),
+// xor / lfsr from one text pass on the index stream; only the MDL winner (PY:2350-2369: smallest payload, ties -> lowest id) is emitted.
 // Rice emission is a two-pass scan: per-tile bit counts -> per-block exclusive scan over
 // tiles -> each thread writes its symbols' bits (MSB-first, PY:1231-1254) into an LDS
 // big-endian word buffer, flushed with plain stores (interior words) and atomicOr
@@ -83,49 +83,32 @@ __device__ inline u32 wg_excl_add(u32 v, u32* sh) {
     return carry + incl - v;
 }
 
-// counters per block in `bits`: 0 b0, 1 bp, 2 nib, 3 br, 4 gray, 5 xor extra, 6 lfsr extra
-__global__ __launch_bounds__(WG) void k_sizes(TileG tg, const u8* text, const u8* mtf, u64* bits, int k) {
+// counters per block in `bits`: 0 b0, 1 bp, 2 nib, 3 br, 4 gray (added by the MTF replay,
+// k_mtf.hip), 5 xor extra, 6 lfsr extra (k_cheap_sizes)
+// xor / lfsr_pred counters only (5, 6): text bytes, 8 per thread
+__global__ __launch_bounds__(WG) void k_cheap_sizes(TileG tg, const u8* text, u64* bits) {
     __shared__ u64 sh[WG / 64];
     u32 lo, hi, b;
     if (!tg.range(blockIdx.x, lo, hi, b)) return;
     const u32 base = tg.geo.base(b);
     const u32 g0 = lo + threadIdx.x * 8;
-    u32 v[8], tb[8];
-    u32 nvalid = 0;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const bool ok = g0 + e < hi;
-        v[e] = ok ? mtf[g0 + e] : 0;
-        tb[e] = ok ? text[g0 + e] : 0;
-        nvalid += ok;
-    }
-    u64 c[7] = {0, 0, 0, 0, 0, 0, 0};
-    if (nvalid) {
+    u32 c5 = 0, c6 = 0;
+    if (g0 < hi) {
         u32 prev = (g0 == base) ? 0u : (u32)text[g0 - 1];
-        u32 li = g0 - base;
-        u32 ph = li % 255u;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            if ((u32)e < nvalid) {
-                c[0] += rice_bits(v[e], k);
-                c[2] += rice_bits(variant_sym(v[e], 4), k);
-                c[3] += rice_bits(variant_sym(v[e], 8), k);
-                c[4] += rice_bits(variant_sym(v[e], 16), k);
-                c[5] += ((tb[e] - prev) & 0xFFu) >= 128u;
-                c[6] += ((tb[e] - (u32)c_lfsr[ph]) & 0xFFu) >= 128u;
-                prev = tb[e];
-                if (++ph == 255u) ph = 0;
-            }
+        u32 ph = (g0 - base) % 255u;
+        const u32 m = min(8u, hi - g0);
+        for (u32 e = 0; e < m; ++e) {
+            const u32 t = text[g0 + e];
+            c5 += ((t - prev) & 0xFFu) >= 128u;
+            c6 += ((t - (u32)c_lfsr[ph]) & 0xFFu) >= 128u;
+            prev = t;
+            if (++ph == 255u) ph = 0;
         }
-        u32 o[8];
-        bitplane8(v, o);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) c[1] += rice_bits(o[e], k);
     }
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-        const u64 t = wg_sum<u64>(c[i], sh);
-        if (threadIdx.x == 0 && t) atomicAdd((unsigned long long*)&bits[(u64)b * 8 + i], (unsigned long long)t);
+    const u64 t5 = wg_sum<u64>(c5, sh), t6 = wg_sum<u64>(c6, sh);
+    if (threadIdx.x == 0) {
+        if (t5) atomicAdd((unsigned long long*)&bits[(u64)b * 8 + 5], (unsigned long long)t5);
+        if (t6) atomicAdd((unsigned long long*)&bits[(u64)b * 8 + 6], (unsigned long long)t6);
     }
 }
 
@@ -412,12 +395,11 @@ static void lfsr_init_once() {
     done[dev] = true;
 }
 
-void launch_cheap_and_rice_sizes(const EmitArgs& e, hipStream_t s) {
+void launch_cheap_sizes(const EmitArgs& e, hipStream_t s) {
     lfsr_init_once();
     if (!e.geo.N) return;
     TileG tg{e.geo, cdiv32(e.geo.bs, TILE)};
-    KOLM_HIP_CHECK(hipMemsetAsync(e.bits, 0, sizeof(u64) * 8 * e.geo.nb, s));
-    k_sizes<<<tg.tpb * e.geo.nb, WG, 0, s>>>(tg, e.text, e.mtf, e.bits, e.rice_k);
+    k_cheap_sizes<<<tg.tpb * e.geo.nb, WG, 0, s>>>(tg, e.text, e.bits);
 }
 
 void launch_mdl(const EmitArgs& e, const u32* lz_sizes, const u32* rp_result, u32* status, hipStream_t s) {

@@ -192,8 +192,33 @@ __global__ __launch_bounds__(64 * CW) void k_mtf_compose(ChunkGeom cg, const u8*
 
 constexpr int RT = 128;  // threads per workgroup in the replay kernel
 
+// Rice-k bit lengths of the 5 BBWT candidates (PY:2028-2073: flags 0, bit-plane, nibble,
+// bit reverse, Gray) accumulated while the MTF indices are produced (counter order of
+// k_entropy.hip: 0 plain, 1 bit-plane, 2 nibble, 3 bit reverse, 4 Gray).
+struct RiceAcc {
+    u32 c[5] = {0, 0, 0, 0, 0};
+    int k;
+    __device__ inline u32 rb(u32 v) const { return (v >> k) + 1 + k; }
+    __device__ inline void add(u32 v) {
+        c[0] += rb(v);
+        c[2] += rb(((v & 0x0Fu) << 4) | (v >> 4));
+        c[3] += rb(__brev(v) >> 24);
+        c[4] += rb(v ^ (v >> 1));
+    }
+    // one 8-byte bit-plane group (PY:1100-1120), bytes little-endian in lo / hi
+    __device__ inline void group(u32 lo, u32 hi) {
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+            u32 v = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v |= (((i < 4 ? lo >> (8 * i) : hi >> (8 * (i - 4))) >> (7 - bit)) & 1u) << (7 - i);
+            c[1] += rb(v);
+        }
+    }
+};
+
 __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, const u8* states, u8* out,
-                                                   u32 nchunks) {
+                                                   u32 nchunks, u64* bits, int rice_k) {
     __shared__ u32 tab[64 * RT];  // word w of thread t at tab[w * RT + t]
     const u32 t = threadIdx.x;
     const u32 c = blockIdx.x * RT + t;
@@ -225,8 +250,11 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
         tab[w * RT + t] = (x & highmask) | ((x & lowmask) << 8) | carry;
         return 4 * w + j;
     };
+    RiceAcc acc;
+    acc.k = rice_k;
     if (((lo | hi) & 15) == 0) {
-        // 16 bytes in / 16 bytes out per global access (threads are 1 KiB apart)
+        // 16 bytes in / 16 bytes out per global access (threads are 1 KiB apart); chunk
+        // starts are multiples of 1 KiB from the block start, so 8-byte groups align
         for (u32 i = lo; i < hi; i += 16) {
             const uint4 v = *reinterpret_cast<const uint4*>(in + i);
             const u32 wv[4] = {v.x, v.y, v.z, v.w};
@@ -235,20 +263,48 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
             for (int q = 0; q < 4; ++q) {
                 u32 o = 0;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) o |= step((wv[q] >> (8 * j)) & 0xFF) << (8 * j);
+                for (int j = 0; j < 4; ++j) {
+                    const u32 m = step((wv[q] >> (8 * j)) & 0xFF);
+                    if (bits) acc.add(m);
+                    o |= m << (8 * j);
+                }
                 ov[q] = o;
             }
             *reinterpret_cast<uint4*>(out + i) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+            if (bits) {
+                acc.group(ov[0], ov[1]);
+                acc.group(ov[2], ov[3]);
+            }
         }
     } else {
-        for (u32 i = lo; i < hi; ++i) out[i] = (u8)step(in[i]);
+        u32 g[2] = {0, 0}, gi = 0;
+        for (u32 i = lo; i < hi; ++i) {
+            const u32 m = step(in[i]);
+            out[i] = (u8)m;
+            if (bits) {
+                acc.add(m);
+                g[gi >> 2] |= m << (8 * (gi & 3));
+                if (++gi == 8) {
+                    acc.group(g[0], g[1]);
+                    g[0] = g[1] = 0;
+                    gi = 0;
+                }
+            }
+        }
+        if (bits && gi) acc.group(g[0], g[1]);  // zero-padded last group of the block
+    }
+    if (bits) {
+        u64* dst = bits + (u64)(c / cg.cpb) * 8;
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+            if (acc.c[q]) atomicAdd((unsigned long long*)&dst[q], (unsigned long long)acc.c[q]);
     }
 }
 
 }  // namespace
 
 void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summary_cnt, u8* states,
-                hipStream_t s, KTimer* kt) {
+                hipStream_t s, KTimer* kt, u64* bits, int rice_k) {
     if (!geo.N) return;
     ChunkGeom cg{geo, (geo.bs + MTF_CHUNK - 1) / MTF_CHUNK};
     const u32 nchunks = cg.cpb * geo.nb;
@@ -263,7 +319,7 @@ void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summar
     }
     {
         KScope k(kt, KT_MTF, "k_mtf_replay", 2 * N + (u64)nchunks * 256);
-        k_mtf_replay<<<(nchunks + RT - 1) / RT, RT, 0, s>>>(cg, in, states, out, nchunks);
+        k_mtf_replay<<<(nchunks + RT - 1) / RT, RT, 0, s>>>(cg, in, states, out, nchunks, bits, rice_k);
     }
 }
 

@@ -466,12 +466,12 @@ struct Pipeline {
         return cyclic();
     }
 
-    u8* mtf(const u8* in) {
+    u8* mtf(const u8* in, u64* bits = nullptr) {
         const u64 N = geo.N;
         const u64 nch = (u64)((geo.bs + MTF_CHUNK - 1) / MTF_CHUNK) * geo.nb + 1;
         u8* out = c->get<u8>("mtf", N);
         launch_mtf(geo, in, out, c->get<u8>("mtf_sum", nch * 256), c->get<u16>("mtf_cnt", nch),
-                   c->get<u8>("mtf_states", nch * 256), c->active, c->kt());
+                   c->get<u8>("mtf_states", nch * 256), c->active, c->kt(), bits, 2);
         return out;
     }
 
@@ -591,6 +591,10 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         kolm_ctx* c;
         ~Restore() { c->active = c->stream; }
     } restore{c};
+    // per-block size counters: xor / lfsr from the text on the index stream, the Rice
+    // candidates from the MTF replay on the sort stream
+    u64* d_bits = c->get<u64>("bits", (u64)nb * 8);
+    KOLM_HIP_CHECK(hipMemsetAsync(d_bits, 0, sizeof(u64) * 8 * nb, ms));
     KOLM_HIP_CHECK(hipEventRecord(ev[0], ms));
     // Re-Pair (candidate 9): persistent workgroups (one per block) on their own stream,
     // launched first so they take their CUs while the sort / LZ77 chains queue beside them
@@ -634,6 +638,14 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     }
     c->active = ms;
     P.linear3();
+    {
+        EmitArgs ce{};
+        ce.geo = geo;
+        ce.text = d_text;
+        ce.bits = d_bits;
+        TScope t(c, KOLM_KT_SIZES, "k_cheap_sizes", N);
+        launch_cheap_sizes(ce, ms);
+    }
     KOLM_HIP_CHECK(hipEventRecord(ej[0], ms));
     LzArgs z = P.lz_args();
     const bool want_lz = (mask >> KOLM_M_LZ77) & 1u || (h_force != nullptr);
@@ -659,13 +671,13 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         bw = P.cyclic();
     }
     KOLM_HIP_CHECK(hipEventRecord(ev[1], s));
-    u8* mt = P.mtf(bw);
+    u8* mt = P.mtf(bw, d_bits);
     EmitArgs e{};
     e.geo = geo;
     e.text = d_text;
     e.mtf = mt;
     e.sizes = c->get<u32>("sizes", (u64)nb * KOLM_NCAND);
-    e.bits = c->get<u64>("bits", (u64)nb * 8);
+    e.bits = d_bits;
     e.method = c->get<u32>("method", nb);
     int32_t* d_force = nullptr;
     if (h_force) {
@@ -681,10 +693,6 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     e.tile_tmp = c->get<u32>("tile_tmp", 2 * ntiles + 16);
     e.tile_tmp2 = c->get<u32>("tile_tmp2", 2 * ntiles + 2 * nb + 16);
     e.rice_k = 2;
-    {
-        TScope t(c, KOLM_KT_SIZES, "k_sizes", 2 * N);  // text + mtf once
-        launch_cheap_and_rice_sizes(e, s);
-    }
     KOLM_HIP_CHECK(hipEventRecord(ev[2], s));
     KOLM_HIP_CHECK(hipStreamWaitEvent(s, ej[1], 0));
     KOLM_HIP_CHECK(hipEventRecord(ev[3], s));

@@ -285,8 +285,10 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
                    KTimer* kt = nullptr);
 
 // ---- k_mtf.hip ----
+// bits (optional, [nb * 8], zeroed by the caller): the replay also adds each block's Rice-k
+// bit counts of the 5 BBWT candidates (counters 0..4, see k_entropy.hip) — no extra pass
 void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summary_cnt, u8* states,
-                hipStream_t s, KTimer* kt = nullptr);
+                hipStream_t s, KTimer* kt = nullptr, u64* bits = nullptr, int rice_k = 2);
 
 // ---- k_entropy.hip: cheap sizes, Rice sizes / emission, MDL, emission of simple models ----
 struct EmitArgs {
@@ -305,7 +307,8 @@ struct EmitArgs {
     u32* tile_tmp2;
     int rice_k;
 };
-void launch_cheap_and_rice_sizes(const EmitArgs& e, hipStream_t s);
+// xor / lfsr_pred size counters (5, 6) only, from the text: runs on the index stream
+void launch_cheap_sizes(const EmitArgs& e, hipStream_t s);
 void launch_mdl(const EmitArgs& e, const u32* lz_sizes, const u32* rp_result, u32* status, hipStream_t s);
 void launch_emit_simple(const EmitArgs& e, hipStream_t s);
 void launch_emit_rice(const EmitArgs& e, hipStream_t s);
