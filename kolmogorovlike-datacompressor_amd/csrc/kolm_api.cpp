@@ -442,16 +442,23 @@ struct Pipeline {
         st.lin_active = N;
     }
     // omega-order of all rotations of the Lyndon factors + BBWT gather -> "bbwt"
+    // cyclic predecessor byte of every position (needs the Lyndon factors only)
+    hipEvent_t prevc_ready = nullptr;  // set when prevc() ran on another stream
+    void prevc() {
+        const u64 N = geo.N;
+        TScope t(c, KOLM_KT_LYNDON, "k_prevc", N * 3);  // flag 1 + text 1 + prevc 1 (FSL at factor starts)
+        launch_prevc(geo, text, c->get<u8>("flag", N), c->get<u64>("FSL", N), c->get<u8>("prevc", N), c->active);
+    }
     u8* cyclic(const std::function<void()>& after_round0 = {}) {
         const u64 N = geo.N;
         u64* FSL = c->get<u64>("FSL", N);
         SortOut cyc = sort_pass(c, geo, text, true, FSL, c->get<u8>("FEd", N), after_round0);
         u8* out = c->get<u8>("bbwt", N);
         u8* prevc = c->get<u8>("prevc", N);
-        {
-            TScope t(c, KOLM_KT_LYNDON, "k_prevc", N * 3);  // flag 1 + text 1 + prevc 1 (FSL at factor starts)
-            launch_prevc(geo, text, c->get<u8>("flag", N), FSL, prevc, c->active);
-        }
+        if (prevc_ready)
+            KOLM_HIP_CHECK(hipStreamWaitEvent(c->active, prevc_ready, 0));
+        else
+            this->prevc();
         {
             TScope t(c, KOLM_KT_LYNDON, "k_bbwt_gather", N * 6);  // SA 4 + prevc 1 + out 1
             launch_bbwt_gather(geo, c->get<u32>("SA", N), prevc, out, c->active);
@@ -632,6 +639,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     KOLM_HIP_CHECK(hipStreamWaitEvent(s, ev[0], 0));
     c->active = s;
     P.lyndon();
+    KOLM_HIP_CHECK(hipEventRecord(ev[5], s));
     if (overlap == 1) {
         KOLM_HIP_CHECK(hipEventRecord(ej[3], s));
         KOLM_HIP_CHECK(hipStreamWaitEvent(ms, ej[3], 0));
@@ -645,6 +653,13 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         ce.bits = d_bits;
         TScope t(c, KOLM_KT_SIZES, "k_cheap_sizes", N);
         launch_cheap_sizes(ce, ms);
+    }
+    if (!serial) {
+        // the BBWT gather's predecessor bytes on the index stream, off the sort chain
+        KOLM_HIP_CHECK(hipStreamWaitEvent(ms, ev[5], 0));
+        P.prevc();
+        KOLM_HIP_CHECK(hipEventRecord(ev[6], ms));
+        P.prevc_ready = ev[6];
     }
     KOLM_HIP_CHECK(hipEventRecord(ej[0], ms));
     LzArgs z = P.lz_args();
