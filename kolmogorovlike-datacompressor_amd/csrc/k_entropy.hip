@@ -85,24 +85,40 @@ __device__ inline u32 wg_excl_add(u32 v, u32* sh) {
 
 // counters per block in `bits`: 0 b0, 1 bp, 2 nib, 3 br, 4 gray (added by the MTF replay,
 // k_mtf.hip), 5 xor extra, 6 lfsr extra (k_cheap_sizes)
-// xor / lfsr_pred counters only (5, 6): text bytes, 8 per thread
-__global__ __launch_bounds__(WG) void k_cheap_sizes(TileG tg, const u8* text, u64* bits) {
+// xor / lfsr_pred counters only (5, 6): 16 text bytes per thread (one 16-byte load when
+// aligned), LFSR table in LDS (per-lane indices would serialise on the constant cache)
+constexpr u32 CHEAP_T = 4096;  // bytes per workgroup
+__global__ __launch_bounds__(WG) void k_cheap_sizes(Geom geo, u32 tpb, const u8* text, u64* bits) {
     __shared__ u64 sh[WG / 64];
-    u32 lo, hi, b;
-    if (!tg.range(blockIdx.x, lo, hi, b)) return;
-    const u32 base = tg.geo.base(b);
-    const u32 g0 = lo + threadIdx.x * 8;
+    __shared__ u8 lf[256];
+    lf[threadIdx.x] = c_lfsr[threadIdx.x];
+    __syncthreads();
+    const u32 b = blockIdx.x / tpb, k = blockIdx.x - b * tpb;
+    const u32 base = geo.base(b), e = geo.end(b);
+    const u32 g0 = base + k * CHEAP_T + threadIdx.x * 16;
     u32 c5 = 0, c6 = 0;
-    if (g0 < hi) {
+    if (g0 < e) {
+        u32 t[16];
+        const u32 m = min(16u, e - g0);
+        if (m == 16 && ((uintptr_t)(text + g0) & 15) == 0) {
+            const uint4 v = *reinterpret_cast<const uint4*>(text + g0);
+            const u32 w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 16; ++q) t[q] = (w[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) t[q] = (u32)q < m ? text[g0 + q] : 0u;
+        }
         u32 prev = (g0 == base) ? 0u : (u32)text[g0 - 1];
         u32 ph = (g0 - base) % 255u;
-        const u32 m = min(8u, hi - g0);
-        for (u32 e = 0; e < m; ++e) {
-            const u32 t = text[g0 + e];
-            c5 += ((t - prev) & 0xFFu) >= 128u;
-            c6 += ((t - (u32)c_lfsr[ph]) & 0xFFu) >= 128u;
-            prev = t;
-            if (++ph == 255u) ph = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            if ((u32)q < m) {
+                c5 += ((t[q] - prev) & 0xFFu) >= 128u;
+                c6 += ((t[q] - (u32)lf[ph]) & 0xFFu) >= 128u;
+                prev = t[q];
+                ph = ph == 254u ? 0u : ph + 1;
+            }
         }
     }
     const u64 t5 = wg_sum<u64>(c5, sh), t6 = wg_sum<u64>(c6, sh);
@@ -398,8 +414,8 @@ static void lfsr_init_once() {
 void launch_cheap_sizes(const EmitArgs& e, hipStream_t s) {
     lfsr_init_once();
     if (!e.geo.N) return;
-    TileG tg{e.geo, cdiv32(e.geo.bs, TILE)};
-    k_cheap_sizes<<<tg.tpb * e.geo.nb, WG, 0, s>>>(tg, e.text, e.bits);
+    const u32 tpb = cdiv32(e.geo.bs, CHEAP_T);
+    k_cheap_sizes<<<tpb * e.geo.nb, WG, 0, s>>>(e.geo, tpb, e.text, e.bits);
 }
 
 void launch_mdl(const EmitArgs& e, const u32* lz_sizes, const u32* rp_result, u32* status, hipStream_t s) {

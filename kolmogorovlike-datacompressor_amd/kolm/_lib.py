@@ -17,7 +17,7 @@ import threading
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libkolm_hip.so")
+LIB_PATH = os.environ.get("KOLM_LIB") or os.path.join(HERE, "libkolm_hip.so")  # KOLM_LIB: A/B builds
 
 KOLM_NCAND = 10
 KOLM_DEFAULT_MASK = 0x3FF   # the reference's candidates 0..9 (kolm.h)
