@@ -387,16 +387,41 @@ __global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8*
     }
 }
 
-// x = s[a0, a1) < y = s[a1, b1) lexicographically (proper prefix smaller); wave-uniform
-__device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1) {
+// 8 bytes at s + x (any alignment) from three aligned dwords, little-endian
+__device__ inline u64 load8u(const u8* s, u32 x) {
+    const uintptr_t a = (uintptr_t)(s + x);
+    const u32* w = reinterpret_cast<const u32*>(a & ~(uintptr_t)3);
+    const u32 sh = (u32)(a & 3);
+    const u32 w0 = w[0], w1 = w[1], w2 = w[2];
+    return ((u64)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
+}
+
+// x = s[a0, a1) < y = s[a1, b1) lexicographically (proper prefix smaller); wave-uniform.
+// 8 bytes per lane per step (512 per wave) while the loads stay inside s[0, N).
+__device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N) {
     const u32 lane = threadIdx.x & 63;
     const u32 la = a1 - a0, lb = b1 - a1, m = min(la, lb);
-    for (u32 o = 0; o < m; o += 64) {
-        const u32 t = o + lane;
-        const bool diff = t < m && s[a0 + t] != s[a1 + t];
-        const u64 bal = __ballot(diff);
+    for (u32 o = 0; o < m; o += 512) {
+        const u32 t = o + 8 * lane;
+        u32 dpos = 0xFFFFFFFFu;
+        if ((u64)a1 + o + 512 + 12 <= N) {
+            if (t < m) {
+                u64 d = load8u(s, a0 + t) ^ load8u(s, a1 + t);
+                if (t + 8 > m) d &= (1ull << (8 * (m - t))) - 1ull;
+                if (d) dpos = t + (u32)(__ffsll((long long)d) - 1) / 8;
+            }
+        } else {
+            for (u32 e = 0; e < 8; ++e) {
+                const u32 tt = t + e;
+                if (tt < m && s[a0 + tt] != s[a1 + tt]) {
+                    dpos = tt;
+                    break;
+                }
+            }
+        }
+        const u64 bal = __ballot(dpos != 0xFFFFFFFFu);
         if (bal) {
-            const u32 d = o + (__ffsll((long long)bal) - 1);
+            const u32 d = __builtin_amdgcn_readlane(dpos, __ffsll((long long)bal) - 1);
             return s[a0 + d] < s[a1 + d];
         }
     }
@@ -425,7 +450,7 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
             bool merged = false;
             while (sp >= 2) {
                 const u32 a0 = stk[sp - 2], a1 = stk[sp - 1];
-                if (!lyn_less(s, a0, a1, frontier)) break;
+                if (!lyn_less(s, a0, a1, frontier, (u32)geo.N)) break;
                 --sp;  // stack[-2] absorbs the top factor
                 merged = true;
             }
