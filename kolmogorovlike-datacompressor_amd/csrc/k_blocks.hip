@@ -428,11 +428,20 @@ __device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N) {
     return la < lb;
 }
 
+constexpr u32 MERGE_LDS = 8192;  // factor stack entries kept in LDS (more: the global stack)
 __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8* s, const u32* fstart,
                                                     const u32* nfac, u32* stack, u8* flag) {
+    __shared__ u32 lstk[MERGE_LDS];
     const u32 b = blockIdx.x, lane = threadIdx.x;
     const u32 base = geo.base(b), end = geo.end(b);
-    volatile u32* stk = stack + base;  // written by lane 0, re-read uniformly: bypass the scalar cache
+    // the stack never holds more entries than the span factorisations together: in LDS
+    // when they fit (text: a few dozen), else in global memory (e.g. a run: n factors)
+    u32 tot = 0;
+    for (u32 k = lane; k < cpb; k += 64)
+        if (base + k * DUVAL_SPAN < end) tot += nfac[b * cpb + k];
+    tot = wave_reduce(tot, OpAddU(), 0u);
+    // written by lane 0, re-read uniformly: volatile keeps the reads off the scalar cache
+    volatile u32* stk = tot <= MERGE_LDS ? lstk : stack + base;
     u32 sp = 0;
     for (u32 k = 0; k < cpb; ++k) {
         const u32 c = b * cpb + k;
