@@ -38,6 +38,13 @@ from kolm import _lib, datagen  # noqa: E402
 from kolm.parallel import gather_payloads  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# kernels whose limiter is not HBM bandwidth (measured)
+LIMITER = {
+    "k_lz_spec<true>": "latency: the dependent greedy-parse chain (one wave per 4 KiB chunk; each token's "
+                       "candidate search starts where the previous token ended)",
+    "k_lz_spec<false>": "latency: the dependent greedy-parse chain",
+    "k_repair": "latency: one workgroup per block, barrier-separated batches of dependent global accesses",
+}
 MB = 1e6
 
 
@@ -210,8 +217,11 @@ def main():
             tr = json.load(f).get("kernels", {}).get(name)
         if tr and tr.get("hbm_bytes_per_launch"):
             traffic = int(tr["hbm_bytes_per_launch"])
+    # "bound"/"peak": the roof the kernel is priced against (integer/byte work: HBM);
+    # "limiter": what actually stops it short of that roof
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": name,
+            "limiter": LIMITER.get(name, "hbm"),
             "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": int(bytes_per_launch),
             "launches_per_step": k["launches"] // a.steps}
     # whole pipeline: every kernel's algorithmic bytes per step / wall time per step (the two

@@ -855,11 +855,14 @@ __global__ __launch_bounds__(256) void k_bwi_emit(BwArgs a) {
 // PY:1913-1978 repair_decompress: "RP" ULEB(256) ULEB(nrules) nrules x (ULEB a, ULEB b)
 // ULEB(seq_len) seq_len x ULEB(sym); rule r defines symbol 256 + r; the output is the
 // expansion of the final sequence.  Device: (1) every ULEB value of the stream by start
-// flags + scan; (2) per block the rule lengths (rules only reference earlier symbols in
-// encoder output; a forward reference is rejected as malformed) and the final sequence's
-// output offsets; (3) breadth-first expansion: (symbol, offset) entries split into their
+// flags + scan; (2) per block the rule lengths (in rule order: the encoder's rules only
+// reference earlier symbols; a hand-made grammar with forward references takes a
+// depth-first pass instead, and only a USED rule that does not resolve is an error, as
+// in PY) and the final sequence's output offsets; (3) breadth-first expansion: (symbol, offset) entries split into their
 // two children until only terminals remain (work = grammar tree nodes, depth iterations).
 constexpr u32 RP_INVALID = 0xFFFFFFFFu;
+constexpr u32 RP_INPROG = 0xFFFFFFFFu;  // rule length marks of k_rp_rules' general pass
+constexpr u32 RP_BADLEN = 0xFFFFFFFEu;
 
 __global__ __launch_bounds__(256) void k_rp_values(DecArgs a, u32* vals, u32* nval) {
     __shared__ u32 sh[4];
@@ -936,19 +939,18 @@ __global__ __launch_bounds__(1024) void k_rp_rules(DecArgs a, const u32* vals, c
         if (tid == 0) a.status[b] = DEC_EFORMAT;
         return;
     }
-    if (tid == 0) s_bad = 0;
-    // rule lengths, in rule order
-    for (u32 c0 = 0; c0 < nr; c0 += RP_CH) {
+    if (tid == 0) s_bad = NONE;
+    __syncthreads();
+    // rule lengths, in rule order (the encoder's rules only reference earlier symbols)
+    for (u32 c0 = 0; c0 < nr && s_bad == NONE; c0 += RP_CH) {
         const u32 m = min(RP_CH, nr - c0);
-        __syncthreads();
         for (u32 i = tid; i < m; i += 1024) ch[i] = make_uint2(V[2 + 2 * (c0 + i)], V[3 + 2 * (c0 + i)]);
         __syncthreads();
         if (tid == 0) {
-            bool bb = false;
             for (u32 i = 0; i < m; ++i) {
                 const u32 r = c0 + i, x = ch[i].x, y = ch[i].y;
-                if (x >= 256 + r || y >= 256 + r) {  // forward / self reference (or marker)
-                    bb = true;
+                if (x >= 256 + r || y >= 256 + r) {  // forward / self reference: general pass below
+                    s_bad = r;
                     break;
                 }
                 const u32 lx = x < 256 ? 1u : (x - 256 < RP_LDS_RULES ? L[x - 256] : RL[x - 256]);
@@ -959,13 +961,56 @@ __global__ __launch_bounds__(1024) void k_rp_rules(DecArgs a, const u32* vals, c
                 else
                     RL[r] = l;
             }
-            if (bb) s_bad = 1;
         }
+        __syncthreads();
     }
     __syncthreads();
-    if (s_bad) {
-        if (tid == 0) a.status[b] = DEC_EFORMAT;
-        return;
+    if (s_bad != NONE) {
+        // A hand-made grammar may reference later rules; PY (PY:1945-1970) accepts it as
+        // long as every symbol it expands resolves, and never looks at unused rules.
+        // Rules from r0 on get their lengths by an iterative depth-first pass (thread 0,
+        // explicit stack in RL[nr, 2nr): 2nr + 3 <= values <= payload bytes).  Marks:
+        // 0 unknown, RP_INPROG on the stack (a child on the stack = a cycle), RP_BADLEN for
+        // a rule that does not resolve (cycle / undefined symbol): an error only if used.
+        const u32 r0 = s_bad;
+        for (u32 r = r0 + tid; r < nr; r += 1024) {
+            if (r < RP_LDS_RULES)
+                L[r] = 0;
+            else
+                RL[r] = 0;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            auto get = [&](u32 s) -> u32 {
+                return s < 256 ? 1u : s - 256 >= nr ? RP_BADLEN : s - 256 < RP_LDS_RULES ? L[s - 256] : RL[s - 256];
+            };
+            auto put = [&](u32 r, u32 v) {
+                if (r < RP_LDS_RULES)
+                    L[r] = v;
+                else
+                    RL[r] = v;
+            };
+            u32* stk = RL + nr;
+            for (u32 r = r0; r < nr; ++r) {
+                if (get(256 + r)) continue;
+                u32 sp = 0;
+                stk[sp++] = r;
+                put(r, RP_INPROG);
+                while (sp) {
+                    const u32 t = stk[sp - 1], x = V[2 + 2 * t], y = V[3 + 2 * t];
+                    const u32 lx = get(x), ly = get(y);
+                    if (!lx || !ly) {
+                        const u32 c = (!lx ? x : y) - 256;
+                        put(c, RP_INPROG);
+                        stk[sp++] = c;
+                        continue;
+                    }
+                    put(t, lx >= RP_BADLEN || ly >= RP_BADLEN ? RP_BADLEN : min(lx + ly, cap));
+                    --sp;
+                }
+            }
+        }
+        __syncthreads();
     }
     for (u32 r = tid; r < min(nr, RP_LDS_RULES); r += 1024) RL[r] = L[r];
     // final sequence: lengths, offsets, first level of entries
@@ -982,6 +1027,10 @@ __global__ __launch_bounds__(1024) void k_rp_rules(DecArgs a, const u32* vals, c
                 sbad = true;
             } else {
                 l = sym < 256 ? 1u : (sym - 256 < RP_LDS_RULES ? L[sym - 256] : RL[sym - 256]);
+                if (l >= RP_BADLEN) {  // an unresolvable rule (cycle / undefined symbol) is used
+                    sbad = true;
+                    l = 0;
+                }
             }
         }
         u32 tot = 0;

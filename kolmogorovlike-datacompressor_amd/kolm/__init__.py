@@ -286,10 +286,11 @@ def compress_blocks_cdc(data: bytes, min_size: int = 4096, avg_size: int = 8192,
 
 def decompress(container: bytes, device: bool = True) -> bytes:
     """Inverse of compress_blocks_fixed / compress_blocks_cdc / the reference's containers
-    (PY:2451-2550).  The TOC is parsed on the host; the blocks whose method the device
-    decodes (kolm_decode_blocks: raw, xor, lz77, lfsr_pred) are decoded on the GPU in one
-    batch, the others by the host decoders of kolm/decode.py (decode side: SURVEY §8f-4).
-    `device=False` (not in PY) decodes everything on the host."""
+    (PY:2451-2550).  The TOC is parsed on the host; every block (ids 0..9: raw, xor, the
+    BBWT family, lz77, lfsr_pred and Re-Pair — KOLM_DECODE_MASK) is decoded on the GPU in
+    one kolm_decode_blocks batch (decode side: SURVEY §8f-4).  Only an id outside the
+    device mask would fall to the host decoders of kolm/decode.py; `device=False` (not in
+    PY) decodes everything on the host."""
     mode, size_field, total_len, mids, orig, payloads = read_container(container)
     parts: List[Optional[bytes]] = [None] * len(mids)
     if device:

@@ -148,6 +148,30 @@ def test_malformed_payloads(kolm_gpu):
             _lib.decode_blocks([pay], [9], [n])
     ok = b"RP" + u(256) + u(1) + u(65) + u(66) + u(3) + u(256) + u(67) + u(256)
     assert _lib.decode_blocks([ok], [9], [5]) == b"ABCAB" == H.decode_block(9, ok, 5)
+    # hand-made grammars PY (PY:1945-1970) accepts although the encoder never writes them:
+    # forward references, and unused rules that do not resolve (undefined symbol, cycle)
+    def rp_pay(rules, seq):
+        body = b"".join(u(x) + u(y) for x, y in rules)
+        return b"RP" + u(256) + u(len(rules)) + body + u(len(seq)) + b"".join(u(s) for s in seq)
+    accepted = [
+        (rp_pay([(257, 67), (65, 66)], [256, 257]), b"ABCAB"),                    # forward reference
+        (rp_pay([(258, 257), (65, 66), (259, 67), (68, 69)], [256, 257]), b"DECABAB"),  # forward chain
+        (rp_pay([(65, 66), (999, 65)], [256]), b"AB"),                           # unused, undefined symbol
+        (rp_pay([(65, 66), (258, 65), (257, 66)], [256, 256]), b"ABAB"),          # unused cycle
+    ]
+    for pay, want in accepted:
+        assert H.decode_block(9, pay, len(want)) == want
+        assert _lib.decode_blocks([pay], [9], [len(want)]) == want
+    # the same chains beside 40000 backward rules (the forward pass starts mid-grammar, past
+    # the rule lengths kept in LDS)
+    big = [(65, 66)] + [(256 + r - 1, 67) for r in range(1, 40000)]
+    tail = len(big)
+    big += [(256 + tail + 1, 68), (69, 256 + tail + 2), (70, 71)]
+    pay = rp_pay(big, [256 + tail, 256 + 5])
+    want = b"EFGD" + b"AB" + b"C" * 5
+    assert _lib.decode_blocks([pay], [9], [len(want)]) == want == H.decode_block(9, pay, len(want))
+    with pytest.raises(_lib.KolmError):  # a USED cycle (PY would not terminate on it)
+        _lib.decode_blocks([rp_pay([(257, 65), (256, 66)], [256])], [9], [4])
     with pytest.raises(_lib.KolmError):  # method id outside the decoder registry
         _lib.decode_blocks([b"x"], [10], [1])
     # a bad block in a batch fails the batch and names the block

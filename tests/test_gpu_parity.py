@@ -259,6 +259,33 @@ def test_adversarial_batched(kolm_gpu, kind):
         assert payloads[i] == cand[int(method[i])], f"block {i}"
 
 
+def _merge_stack_block(z: int, swap: bool) -> bytes:
+    """A 65536-byte block whose two 32 KiB Duval spans factorise into exactly z + 2 span
+    factors: span 0 = "\\x01" + text (one Lyndon word: its minimum byte occurs once, at
+    the front), span 1 = "\\x01" + text + z zero bytes (one word + z factors "\\x00").  The
+    two words merge across the spans when the first is smaller (swap picks the order)."""
+    t0 = D.enwik_like(32767, seed=31)
+    t1 = D.enwik_like(32767 - z, seed=32)
+    if swap:
+        t0, t1 = D.enwik_like(32767, seed=32), D.enwik_like(32767 - z, seed=31)
+    blk = b"\x01" + t0 + b"\x01" + t1 + bytes(z)
+    assert len(blk) == 65536
+    return blk
+
+
+def test_lyndon_merge_stack_boundary(kolm_gpu):
+    """k_duval_merge keeps its factor stack in LDS while the span factorisations total at
+    most MERGE_LDS (8192) entries and in global memory past that: blocks at 8191, 8192 and
+    8193 span factors, with and without the cross-span merge, in ONE batch, vs the oracle."""
+    from kolm import _lib
+    blocks = [_merge_stack_block(z, sw) for z in (8189, 8190, 8191) for sw in (False, True)]
+    data = b"".join(blocks)
+    _, method, payloads, _ = _lib.encode_blocks(data, 65536, force=[2] * len(blocks))
+    for i, blk in enumerate(blocks):
+        assert payloads[i] == O.candidate(2, blk), f"block {i}"
+    assert kolm_gpu.bbwt_forward(blocks[3]) == O.bbwt_forward(blocks[3])
+
+
 @pytest.mark.parametrize("ngpu", [1, 2])
 def test_encode_blocks_multi(kolm_gpu, ngpu):
     """Single-process multi-device entry (kolm_encode_blocks_multi): same outputs as the
