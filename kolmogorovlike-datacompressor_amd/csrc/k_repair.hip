@@ -22,15 +22,28 @@ namespace {
 struct DevExec {
     rp::Shared* sh;
     u64* prof;      // [P_N] per block, or null
+    u32* trace;     // per-batch records (block 0 only), or null
+    u32* rec = nullptr;
     u64 last = 0;   // thread 0: time of the previous mark
     u32 last_id = 0;
     __device__ inline void mark(u32 id) {
-        if (prof && threadIdx.x == 0) {
+        if ((prof || trace) && threadIdx.x == 0) {
             const u64 now = wall_clock64();
-            if (last) prof[last_id] += now - last;
+            if (last) {
+                if (prof) prof[last_id] += now - last;
+                if (rec) rec[8 + last_id] += (u32)(now - last);
+            }
             last = now;
             last_id = id;
         }
+    }
+    // debug trace: it = loop iteration (a record per iteration), then the batch's fields
+    __device__ inline void begin(u32 it) {
+        if (trace && threadIdx.x == 0) rec = it < RP_TR_CAP ? trace + (u64)it * RP_TR_W : nullptr;
+    }
+    __device__ inline void record(const u32 (&f)[8]) {
+        if (rec && threadIdx.x == 0)
+            for (u32 k = 0; k < 8; ++k) rec[k] = f[k];
     }
     template <class F>
     __device__ inline void par(F f) {
@@ -66,6 +79,60 @@ struct DevExec {
         base = (u32)__shfl((int)base, (int)leader);
         return pred ? base + (u32)__popcll(m & ((1ull << lane) - 1ull)) : rp::NIL;
     }
+    // Lanes grouped by equal key (the active lanes only): this lane's group as a lane mask
+    // (0 when inactive).  One iteration per distinct key in the wave.
+    __device__ inline u64 peers(u64 key, bool act) {
+        u64 rem = __ballot(act);
+        u64 mine = 0;
+        while (rem) {
+            const u32 l = (u32)__ffsll((unsigned long long)rem) - 1;
+            const u64 kl = ((u64)(u32)__builtin_amdgcn_readlane((int)(key >> 32), l) << 32) |
+                           (u32)__builtin_amdgcn_readlane((int)(u32)key, l);
+            const bool eq = act && key == kl;
+            const u64 m = __ballot(eq);
+            if (eq) mine = m;
+            rem &= ~m;
+        }
+        return mine;
+    }
+    // wave-aggregated atomics (agg, wave-uniform): lanes hitting the same word combine into
+    // one atomic by the group's first lane (text has a few hot pairs per big batch:
+    // thousands of +-1 on one word); without agg every lane does its own
+    __device__ inline void add_agg(u32* p, bool act, bool agg) {
+        if (!agg) {
+            if (act) atomicAdd(p, 1u);
+            return;
+        }
+        const u64 m = peers((u64)(uintptr_t)p, act);
+        if (act && __lane_id() == (u32)__ffsll((unsigned long long)m) - 1) atomicAdd(p, (u32)__popcll(m));
+    }
+    __device__ inline void sub_agg(u32* p, bool act, bool agg) {
+        if (!agg) {
+            if (act) atomicSub(p, 1u);
+            return;
+        }
+        const u64 m = peers((u64)(uintptr_t)p, act);
+        if (act && __lane_id() == (u32)__ffsll((unsigned long long)m) - 1) atomicSub(p, (u32)__popcll(m));
+    }
+    // slot = old value + this lane's rank among the group (as if every lane did atomicAdd(p, 1))
+    __device__ inline u32 slot_agg(u32* p, bool act, bool agg) {
+        if (!agg) return act ? atomicAdd(p, 1u) : 0u;
+        const u32 lane = __lane_id();
+        const u64 m = peers((u64)(uintptr_t)p, act);
+        const u32 ld = act ? (u32)__ffsll((unsigned long long)m) - 1 : lane;
+        u32 base = 0;
+        if (act && lane == ld) base = atomicAdd(p, (u32)__popcll(m));
+        base = (u32)__shfl((int)base, (int)ld);
+        return base + (u32)__popcll(m & ((1ull << lane) - 1ull));
+    }
+    // one representative lane per distinct key: leader lane of this lane's group
+    __device__ inline u32 leader(u64 key, bool act, bool agg) {
+        if (!agg) return __lane_id();
+        const u64 m = peers(key, act);
+        return act ? (u32)__ffsll((unsigned long long)m) - 1 : __lane_id();
+    }
+    __device__ inline bool is_leader(u32 ld) const { return __lane_id() == ld; }
+    __device__ inline u32 from_leader(u32 v, u32 ld) const { return (u32)__shfl((int)v, (int)ld); }
     __device__ inline u32 add(u32* p, u32 v) { return atomicAdd(p, v); }
     __device__ inline u32 sub(u32* p, u32 v) { return atomicSub(p, v); }
     __device__ inline u32 min(u32* p, u32 v) { return atomicMin(p, v); }
@@ -86,7 +153,7 @@ __global__ __launch_bounds__(rp::NT) void k_repair(RpArgs a, u32 b0) {
     B.out = a.out + (u64)b * a.out_stride;
     B.out_cap = a.out_stride;
     B.result = a.result + (u64)b * rp::RS_N;
-    DevExec ex{&sh, a.prof ? a.prof + (u64)b * rp::P_N : nullptr};
+    DevExec ex{&sh, a.prof ? a.prof + (u64)b * rp::P_N : nullptr, b == 0 ? a.trace : nullptr};
     rp::repair_block(ex, B, sh);
     ex.mark(0);
 }

@@ -170,6 +170,10 @@ struct kolm_ctx {
     T* get(const char* name, size_t count) {
         return static_cast<T*>(raw(name, count * sizeof(T)));
     }
+    u64 bytes_held(const char* name) const {
+        const auto it = bufs.find(name);
+        return it == bufs.end() ? 0 : it->second.cap;
+    }
     void sync() { KOLM_HIP_CHECK(hipStreamSynchronize(active)); }
 };
 
@@ -623,7 +627,23 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
             rpa.prof = c->get<u64>("rp_prof", (u64)nb * RP_P_N);
             KOLM_HIP_CHECK(hipMemsetAsync(rpa.prof, 0, sizeof(u64) * nb * RP_P_N, c->rp));
         }
-        static const u64 budget = (getenv("KOLM_RP_WS_GB") ? (u64)atof(getenv("KOLM_RP_WS_GB")) : 64ull) << 30;
+        static const char* rp_trace = getenv("KOLM_RP_TRACE");
+        if (rp_trace && *rp_trace) {
+            rpa.trace = c->get<u32>("rp_trace", (u64)RP_TR_CAP * RP_TR_W);
+            KOLM_HIP_CHECK(hipMemsetAsync(rpa.trace, 0, sizeof(u32) * RP_TR_CAP * RP_TR_W, c->rp));
+        }
+        // Blocks run in groups whose workspaces fit the budget (~258 MB per 1 MiB block);
+        // a second group serialises behind the first, so the default budget is most of the
+        // device memory still free (KOLM_RP_WS_GB overrides), not a fixed figure.
+        u64 budget;
+        if (getenv("KOLM_RP_WS_GB")) {
+            budget = (u64)(atof(getenv("KOLM_RP_WS_GB")) * (double)(1ull << 30));
+        } else {
+            size_t fr = 0, total = 0;
+            KOLM_HIP_CHECK(hipMemGetInfo(&fr, &total));
+            const u64 held = c->bytes_held("rp_ws");  // reused below: counts as free
+            budget = std::max<u64>((u64)((fr + held) * 0.75), 8ull << 30);
+        }
         const u32 group = (u32)std::max<u64>(1, std::min<u64>(nb, budget / rpa.ws_stride));
         rpa.ws = c->get<char>("rp_ws", (u64)group * rpa.ws_stride);
         KOLM_HIP_CHECK(hipStreamWaitEvent(c->rp, ev[0], 0));
@@ -738,6 +758,15 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
             fprintf(stderr, " %s %.2f", nm[k], (double)t / nb / 1e5);
         }
         fprintf(stderr, "\n");
+    }
+    if (want_rp && rpa.trace) {
+        // per-batch records of block 0 (debug): raw u32 words, RP_TR_W per loop iteration
+        std::vector<u32> tr((u64)RP_TR_CAP * RP_TR_W);
+        KOLM_HIP_CHECK(hipMemcpy(tr.data(), rpa.trace, sizeof(u32) * tr.size(), hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(getenv("KOLM_RP_TRACE"), "wb")) {
+            fwrite(tr.data(), sizeof(u32), tr.size(), f);
+            fclose(f);
+        }
     }
     for (u32 b = 0; b < (want_rp ? nb : 0); ++b)
         if (rpres[(u64)b * RP_RS_N + RP_RS_ERR]) {

@@ -364,8 +364,11 @@ struct RpArgs {
     u64 out_stride;    // 4 * bs + 64
     u32* result;       // [nb * RP_RS_N]
     u64* prof;         // [nb * RP_P_N] wall-clock ticks per section (KOLM_RP_PROF=1), or null
+    u32* trace;        // [RP_TR_CAP * RP_TR_W] per-batch records of block 0 (KOLM_RP_TRACE=file), or null
 };
 constexpr u32 RP_P_N = 11;
+constexpr u32 RP_TR_W = 20;        // trace record: 8 batch fields + per-section ticks
+constexpr u32 RP_TR_CAP = 1u << 16;
 u64 repair_ws_bytes(u32 bs);
 void launch_repair(const RpArgs& a, u32 b0, u32 nblk, hipStream_t s);
 void launch_rp_emit(const RpArgs& a, const u32* method, const u64* off, u8* arena, hipStream_t s);

@@ -8,6 +8,11 @@
 //   ex.scan(a, &total)   in-place exclusive scan of a[0..NT) (LDS), total written by all
 //   ex.add/sub/min/max/cas  atomics (u32; cas64 on u64)
 //   ex.append(&n, pred)  index n++ for the threads with pred (wave-aggregated on the device), else NIL
+//   ex.add_agg/sub_agg(p, act)  *p += / -= 1 for the threads with act; ex.slot_agg(p, act) the
+//                        same returning the old value (a unique slot); on the device the lanes of
+//                        a wave that hit the same word combine into one atomic
+//   ex.leader(key, act), ex.is_leader(ld), ex.from_leader(v, ld)  one representative thread per
+//                        distinct key (device: per wave; host: every thread represents itself)
 //   ex.mark(id)          profiling hook: time since the previous mark goes to the previous id
 //
 // Reference semantics (PY:1817-1911), restated exactly:
@@ -42,8 +47,9 @@ using u8 = uint8_t;
 using u32 = uint32_t;
 using u64 = uint64_t;
 
-constexpr u32 NT = 1024;          // threads of the block's workgroup
-constexpr u32 W = 512;            // max rounds (members) per batch
+constexpr u32 NT = 1024;          // threads of the block's workgroup (512 measured: the hot-path
+                                  // streams then run beside it, but Re-Pair itself is 30 % slower)
+constexpr u32 W = 512;            // max rounds (members) per batch (<= NT: one window of NT entries)
 constexpr u32 CAPR = 1u << 16;    // occurrence-region entries per batch beyond its first member
 constexpr u32 SORT_LDS = 4096;    // level lists up to this size are sorted in LDS
 constexpr u32 QLIM = 4096;        // level cache: the rescan picks flow so that Q holds <= QLIM pairs
@@ -53,6 +59,8 @@ constexpr u64 EMPTY = ~0ull;
 constexpr u32 BMAX = 1u << 22;    // owner tags (BMAX - batch) * W + member: batch < BMAX
 constexpr u32 NBASE = 65536;      // ids of the byte pairs: (a << 8) | b
 constexpr u32 MAX_N = 1u << 22;   // block length limit of the device Re-Pair
+constexpr u32 RK = 4;             // occurrences per thread per step in the occurrence loops
+constexpr u32 AGG_MIN = 2048;     // batches with at least this many occurrences aggregate atomics
 
 enum : u32 { RS_SIZE = 0, RS_RULES, RS_FINAL, RS_BATCHES, RS_ERR, RS_LEVELS, RS_N };
 // profile sections (ex.mark(id): time since the previous mark is charged to the previous id)
@@ -60,14 +68,27 @@ enum : u32 { P_INIT = 0, P_LVSCAN, P_LVSORT, P_WINDOW, P_GATHER, P_CHAINS, P_SEL
              P_SER, P_N };
 enum : u32 { RE_OK = 0, RE_CAP = 1, RE_LOOP = 2, RE_LEN = 3 };
 
+// Per position, one 32-byte record (AoS): an occurrence's neighbourhood (prev, next and
+// their marks) is a few cache lines instead of a line per field.
+//   sym    symbol (DEAD once merged into its left neighbour)
+//   nxt/prv  the live doubly linked list
+//   opair  id of the pair starting here (NIL: none)
+//   ctag   batch*W + member of a chosen occurrence;  owner: min span owner tag this batch
+//   oidx   occurrence index in this batch ((a,a) chains)
+// Field order: the pairs read together are adjacent (nxt+opair in the gather; the 16-byte
+// halves in the conflict scan).
+struct alignas(32) Node {
+    u32 nxt, opair, prv, sym, owner, ctag, oidx, pad;
+};
+
 // Per-block workspace (all device pointers).  Sizes for a block of length n:
-//   n:      sym nxt prv opair oidx ctag owner  opos omem od0 od1 ot0 ot1 oidl oidr oj op oq
+//   n:      nd (32 B each);  opos omem od0 od1 ot0 ot1 oidl oidr oj op oq
 //   3n+16:  occpos          PC = NBASE + 2n + 16: cnt poff plen pkey, lists (3 x key+id)
 //   HS = pow2 >= n + 64:     hkey hval;  n + 16: husd;  n/2 + 16: rules
 struct Block {
     const u8* text;
     u32 n;
-    u32 *sym, *nxt, *prv, *opair, *oidx, *ctag, *owner;
+    Node* nd;  // per position: the live sequence and its per-batch marks
     u32 *opos, *omem, *od0, *od1, *ot0, *ot1, *oidl, *oidr, *oj, *op, *oq;
     u32* occpos;
     u32 *cnt, *poff, *plen;
@@ -110,8 +131,8 @@ RP_HD inline u64 workspace_layout(char* base, u32 n, Block& B) {
     const u64 N = (u64)n + 16, PC = NBASE + 2ull * n + 16;
     u32 HS = 64;
     while (HS < n + 64) HS <<= 1;
-    u32** n32[] = {&B.sym, &B.nxt, &B.prv, &B.opair, &B.oidx, &B.ctag, &B.owner, &B.opos, &B.omem, &B.od0,
-                   &B.od1, &B.ot0, &B.ot1, &B.oidl, &B.oidr, &B.oj, &B.op, &B.oq, &B.husd};
+    B.nd = (Node*)take(N * sizeof(Node));
+    u32** n32[] = {&B.opos, &B.omem, &B.od0, &B.od1, &B.ot0, &B.ot1, &B.oidl, &B.oidr, &B.oj, &B.op, &B.oq, &B.husd};
     for (u32** p : n32) *p = (u32*)take(N * 4);
     B.occpos = (u32*)take(3 * N * 4);
     B.cnt = (u32*)take(PC * 4);
@@ -193,6 +214,16 @@ RP_HD inline u32 hash_insert(E& ex, const Block& B, Shared& sh, const HTab& h, u
         }
         s = (s + 1) & h.mask;
     }
+}
+
+// hash_insert by one representative thread per distinct key (device: per wave); every
+// thread with act gets the key's slot.
+template <class E>
+RP_HD inline u32 hash_insert_wave(E& ex, const Block& B, Shared& sh, const HTab& h, u64 key, bool act, bool agg) {
+    const u32 ld = ex.leader(key, act, agg);
+    u32 s = 0;
+    if (act && ex.is_leader(ld)) s = hash_insert(ex, B, sh, h, key);
+    return ex.from_leader(s, ld);
 }
 
 // Sort key/id[0..n) ascending by key (keys unique); tk/ti is scratch of the same size.
@@ -300,8 +331,9 @@ RP_HD inline void sort_list(E& ex, Shared& sh, u64* k, u32* id, u64* tk, u32* ti
     }
 }
 
+// always_inline: as a called function its register budget and the call ABI spill to scratch
 template <class E>
-RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
+RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block& B, Shared& sh) {
     const u32 n = B.n;
     const u32 HS = B.hmask + 1;
     // ---------------- init: linked list, byte-pair counts and regions ----------------
@@ -320,17 +352,17 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
     });
     ex.par([&](u32 t) {
         for (u32 i = t; i < n; i += NT) {
-            B.sym[i] = B.text[i];
-            B.nxt[i] = i + 1 < n ? i + 1 : NIL;
-            B.prv[i] = i ? i - 1 : NIL;
-            B.ctag[i] = NIL;
-            B.owner[i] = NIL;
+            B.nd[i].sym = B.text[i];
+            B.nd[i].nxt = i + 1 < n ? i + 1 : NIL;
+            B.nd[i].prv = i ? i - 1 : NIL;
+            B.nd[i].ctag = NIL;
+            B.nd[i].owner = NIL;
             if (i + 1 < n) {
                 const u32 code = ((u32)B.text[i] << 8) | B.text[i + 1];
-                B.opair[i] = code;
+                B.nd[i].opair = code;
                 ex.add(&B.cnt[code], 1u);
             } else {
-                B.opair[i] = NIL;
+                B.nd[i].opair = NIL;
             }
         }
     });
@@ -340,7 +372,7 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
     });
     ex.par([&](u32 t) {
         for (u32 i = t; i + 1 < n; i += NT) {
-            const u32 code = B.opair[i];
+            const u32 code = B.nd[i].opair;
             B.occpos[B.poff[code] + ex.add(&B.plen[code], 1u)] = i;
         }
     });
@@ -354,6 +386,7 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
     u32 guard = 0;
     // ---------------- batches ----------------
     for (;;) {
+        ex.begin(guard);
         if (++guard > 4 * n + 64) {  // unreachable: every batch retires >= 1 round or 1 level entry
             ex.par([&](u32 t) { if (t == 0) sh.err = RE_LOOP; });
             break;
@@ -385,18 +418,28 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
                                 if (v[k] >= 2) ex.add(&hist[v[k] < 2047 ? v[k] : 2047u], 1u);
                         }
                     });
-                    // suffix sums over the bins, top down: thread t holds bins 2047-2t, 2046-2t
-                    ex.par([&](u32 t) { sh.scan[t] = hist[2047 - 2 * t] + hist[2046 - 2 * t]; });
+                    // suffix sums over the bins, top down: thread t holds the HB bins
+                    // 2047 - HB*t - k, k < HB (descending)
+                    constexpr u32 HB = 2048 / NT;
+                    ex.par([&](u32 t) {
+                        u32 v = 0;
+                        for (u32 k = 0; k < HB; ++k) v += hist[2047 - HB * t - k];
+                        sh.scan[t] = v;
+                    });
                     ex.scan(sh.scan, &sh.total);
                     ex.par([&](u32 t) {
-                        const u32 bh = 2047 - 2 * t, bl = bh - 1;
-                        const u32 s_hi = sh.scan[t] + hist[bh], s_lo = s_hi + hist[bl];  // #(count >= bin)
-                        u32 cand = NIL;
-                        if (bh >= 2 && s_hi <= QLIM) cand = bh;
-                        if (bl >= 2 && s_lo <= QLIM) cand = bl;
+                        u32 run = sh.scan[t], cand = NIL;
+                        bool top = false;
+                        for (u32 k = 0; k < HB; ++k) {
+                            const u32 bin = 2047 - HB * t - k;
+                            run += hist[bin];  // #(count >= bin)
+                            if (bin >= 2 && run <= QLIM) cand = bin;
+                            if (bin >= 2 && hist[bin] && !top) {  // the highest non-empty bin
+                                ex.max(&sh.maxc, bin);
+                                top = true;
+                            }
+                        }
                         if (cand != NIL) ex.min(&sh.flow, cand);
-                        if (bh >= 2 && hist[bh]) ex.max(&sh.maxc, bh);  // the highest non-empty bin
-                        else if (bl >= 2 && hist[bl]) ex.max(&sh.maxc, bl);
                     });
                     ex.par([&](u32 t) {
                         if (t == 0) {
@@ -528,41 +571,63 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
             }
         });
         const u32 M = sh.cut < Mw ? sh.cut : Mw;
-        const u32 tot = sh.scan2[M];  // entries past Mw are 0: prefix at M
+        const u32 tot = M < NT ? sh.scan2[M] : sh.total;  // entries past Mw are 0: prefix at M
         const bool aa = sh.any_aa != 0;
         ex.mark(P_GATHER);
+        // Occurrence loops below take RK occurrences per thread per step, their dependent
+        // loads staged level by level (every load of a level issued before any is used): the
+        // phases are latency-bound, so RK chains are in flight per thread instead of one.
+        // Wave-aggregated atomics pay off only when a batch has many occurrences (few hot
+        // words then take thousands of +-1); below AGG_MIN they cost more than they save.
+        const bool agg_g = tot >= AGG_MIN;
         // ---- gather the members' live occurrences (+ chosen-occurrence marks when no
         //      member is an (a,a) pair: then every live occurrence is replaced) ----
         ex.par([&](u32 t) {
-            for (u32 e0 = 0; e0 < tot; e0 += NT) {
-                const u32 e = e0 + t;
-                bool valid = false;
-                u32 pos = 0, lo = 0;
-                if (e < tot) {
-                    u32 hi = M;  // member lo: m_pre[lo] <= e < m_pre[lo+1]
-                    while (hi - lo > 1) {
-                        const u32 md = (lo + hi) >> 1;
-                        if (sh.m_pre[md] <= e) lo = md; else hi = md;
+            for (u32 e0 = 0; e0 < tot; e0 += RK * NT) {
+                u32 pos[RK], lo[RK], nx[RK];
+                bool valid[RK];
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    const u32 e = e0 + k * NT + t;
+                    u32 l = 0;
+                    pos[k] = 0;
+                    if (e < tot) {
+                        u32 hi = M;  // member l: m_pre[l] <= e < m_pre[l+1]
+                        while (hi - l > 1) {
+                            const u32 md = (l + hi) >> 1;
+                            if (sh.m_pre[md] <= e) l = md; else hi = md;
+                        }
+                        pos[k] = B.occpos[sh.m_roff[l] + (e - sh.m_pre[l])];
                     }
-                    pos = B.occpos[sh.m_roff[lo] + (e - sh.m_pre[lo])];
-                    valid = B.opair[pos] == sh.m_id[lo];
+                    lo[k] = l;
                 }
-                const u32 o = ex.append(&sh.nocc, valid);
-                if (valid) {
-                    B.opos[o] = pos;
-                    B.omem[o] = lo;
-                    if (aa) {
-                        B.oidx[pos] = o;
-                    } else {
-                        B.ctag[pos] = ctag0 + lo;
-                        ex.add(&sh.m_repl[lo], 1u);
-                        ex.min(&B.owner[pos], otag0 + lo);
-                        ex.min(&B.owner[B.nxt[pos]], otag0 + lo);
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    const bool in = e0 + k * NT + t < tot;
+                    const u32 op = in ? B.nd[pos[k]].opair : NIL;  // nxt + opair: one 8-byte load
+                    nx[k] = in ? B.nd[pos[k]].nxt : 0u;
+                    valid[k] = in && op == sh.m_id[lo[k]];
+                }
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    const u32 o = ex.append(&sh.nocc, valid[k]);
+                    if (valid[k]) {
+                        B.opos[o] = pos[k];
+                        B.omem[o] = lo[k];
+                        if (aa) {
+                            B.nd[pos[k]].oidx = o;
+                        } else {
+                            B.nd[pos[k]].ctag = ctag0 + lo[k];
+                            ex.min(&B.nd[pos[k]].owner, otag0 + lo[k]);
+                            ex.min(&B.nd[nx[k]].owner, otag0 + lo[k]);
+                        }
                     }
+                    if (!aa) ex.add_agg(&sh.m_repl[lo[k]], valid[k], agg_g);
                 }
             }
         });
         const u32 nocc = sh.nocc;
+        const bool agg = nocc >= AGG_MIN;
         ex.mark(P_CHAINS);
         // ---- runs of (a,a): distance from the run start by pointer jumping; greedy
         //      left-to-right pairing replaces the occurrences at even distance ----
@@ -573,8 +638,8 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
                     const u32 m = B.omem[o], pos = B.opos[o];
                     u32 pp = NIL;
                     if (sh.m_a[m] == sh.m_b[m]) {
-                        const u32 p = B.prv[pos];
-                        if (p != NIL && B.opair[p] == sh.m_id[m]) pp = B.oidx[p];
+                        const u32 p = B.nd[pos].prv;
+                        if (p != NIL && B.nd[p].opair == sh.m_id[m]) pp = B.nd[p].oidx;
                     }
                     B.ot0[o] = pp;
                     B.od0[o] = pp != NIL ? 1u : 0u;
@@ -610,12 +675,14 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
             // chosen occurrences: tags, replacement counts, span owners
             ex.par([&](u32 t) {
                 for (u32 o = t; o < nocc; o += NT) {
-                    if (dist[o] & 1u) continue;
+                    const bool ch = !(dist[o] & 1u);
                     const u32 m = B.omem[o], i = B.opos[o];
-                    B.ctag[i] = ctag0 + m;
-                    ex.add(&sh.m_repl[m], 1u);
-                    ex.min(&B.owner[i], otag0 + m);
-                    ex.min(&B.owner[B.nxt[i]], otag0 + m);
+                    if (ch) {
+                        B.nd[i].ctag = ctag0 + m;
+                        ex.min(&B.nd[i].owner, otag0 + m);
+                        ex.min(&B.nd[B.nd[i].nxt].owner, otag0 + m);
+                    }
+                    ex.add_agg(&sh.m_repl[m], ch, agg);
                 }
             });
         }
@@ -623,34 +690,61 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
         // ---- conflicts (footprint vs earlier spans), left-neighbour uniformity; the
         //      neighbourhood of every chosen occurrence is kept for the apply phases ----
         ex.par([&](u32 t) {
-            for (u32 o = t; o < nocc; o += NT) {
-                if (aa && (dist[o] & 1u)) continue;
-                const u32 m = B.omem[o], i = B.opos[o];
-                const u32 p = B.prv[i], j = B.nxt[i], q = B.nxt[j];
-                bool conf = false;
-                const u32 lo = otag0, hi = otag0 + m;  // owner in [lo, hi) = earlier member this batch
-                const u32 w0 = B.owner[i], w1 = B.owner[j];
-                conf |= w0 >= lo && w0 < hi;
-                conf |= w1 >= lo && w1 < hi;
-                if (p != NIL) {
-                    const u32 w = B.owner[p];
-                    conf |= w >= lo && w < hi;
+            for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
+                bool act[RK], conf[RK];
+                u32 m[RK], i[RK], p[RK], j[RK], q[RK], pp[RK], sp[RK], sq[RK], cq[RK], cpp[RK];
+                // owner in [otag0, otag0 + m) = an earlier member of this batch
+                auto early = [&](u32 w, u32 mm) { return w >= otag0 && w < otag0 + mm; };
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    const u32 o = o0 + k * NT;
+                    act[k] = o < nocc && !(aa && (dist[o] & 1u));
+                    m[k] = act[k] ? B.omem[o] : 0u;
+                    i[k] = act[k] ? B.opos[o] : 0u;
                 }
-                if (q != NIL) {
-                    const u32 w = B.owner[q];
-                    conf |= w >= lo && w < hi;
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    const Node x = B.nd[act[k] ? i[k] : 0u];
+                    p[k] = act[k] ? x.prv : NIL;
+                    j[k] = act[k] ? x.nxt : 0u;
+                    conf[k] = act[k] && early(x.owner, m[k]);
                 }
-                if (conf) ex.min(&sh.t1, m);
-                const bool leftc = p != NIL && B.prv[p] != NIL && B.ctag[B.prv[p]] == ctag0 + m;
-                const bool rightc = q != NIL && B.ctag[q] == ctag0 + m;
-                const u32 x = (p != NIL && !leftc) ? B.sym[p] : NIL;
-                ex.min(&sh.m_lmin[m], x);
-                ex.max(&sh.m_lmax[m], x);
-                B.oj[o] = j;
-                B.op[o] = leftc ? NIL : p;
-                B.oq[o] = q;
-                B.oidl[o] = x;                                           // left symbol
-                B.oidr[o] = q == NIL ? NIL : rightc ? X0 + m : B.sym[q];  // right symbol
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    const Node y = B.nd[act[k] ? j[k] : 0u];
+                    q[k] = act[k] ? y.nxt : NIL;
+                    conf[k] = conf[k] || (act[k] && early(y.owner, m[k]));
+                    const bool hp = p[k] != NIL;
+                    const Node z = B.nd[hp ? p[k] : 0u];
+                    conf[k] = conf[k] || (hp && early(z.owner, m[k]));
+                    pp[k] = hp ? z.prv : NIL;
+                    sp[k] = hp ? z.sym : NIL;
+                }
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    const bool hq = q[k] != NIL;
+                    const Node w = B.nd[hq ? q[k] : 0u];
+                    conf[k] = conf[k] || (hq && early(w.owner, m[k]));
+                    cq[k] = hq ? w.ctag : NIL;
+                    sq[k] = hq ? w.sym : NIL;
+                    cpp[k] = pp[k] != NIL ? B.nd[pp[k]].ctag : NIL;
+                }
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    if (!act[k]) continue;
+                    const u32 o = o0 + k * NT;
+                    if (conf[k]) ex.min(&sh.t1, m[k]);
+                    const bool leftc = pp[k] != NIL && cpp[k] == ctag0 + m[k];
+                    const bool rightc = q[k] != NIL && cq[k] == ctag0 + m[k];
+                    const u32 x = (p[k] != NIL && !leftc) ? sp[k] : NIL;
+                    ex.min(&sh.m_lmin[m[k]], x);
+                    ex.max(&sh.m_lmax[m[k]], x);
+                    B.oj[o] = j[k];
+                    B.op[o] = leftc ? NIL : p[k];
+                    B.oq[o] = q[k];
+                    B.oidl[o] = x;                                                  // left symbol
+                    B.oidr[o] = q[k] == NIL ? NIL : rightc ? X0 + m[k] : sq[k];  // right symbol
+                }
             }
         });
         ex.par([&](u32 t) {
@@ -682,44 +776,83 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
         // ---- apply 1: destroy the old pair occurrences; register the new pair keys (the
         //      inserting thread allocates the id) and keep each occurrence's hash slots ----
         ex.par([&](u32 t) {
-            for (u32 o = t; o < nocc; o += NT) {
-                if (aa && (dist[o] & 1u)) continue;
-                const u32 m = B.omem[o];
-                if (m >= T) continue;
-                const u32 i = B.opos[o], p = B.op[o], j = B.oj[o], q = B.oq[o];
-                ex.sub(&B.cnt[B.opair[i]], 1u);
-                if (q != NIL) ex.sub(&B.cnt[B.opair[j]], 1u);
-                if (p != NIL) ex.sub(&B.cnt[B.opair[p]], 1u);
-                const u32 X = X0 + m;
-                if (q != NIL) B.oidr[o] = hash_insert(ex, B, sh, ht, pkey_of(X, B.oidr[o]));
-                if (p != NIL) B.oidl[o] = hash_insert(ex, B, sh, ht, pkey_of(B.oidl[o], X));
+            for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
+                bool act[RK];
+                u32 m[RK], p[RK], j[RK], q[RK], xl[RK], yr[RK], pj[RK], pp[RK];
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    const u32 o = o0 + k * NT;
+                    act[k] = o < nocc && !(aa && (dist[o] & 1u));
+                    m[k] = act[k] ? B.omem[o] : 0u;
+                    act[k] = act[k] && m[k] < T;
+                    p[k] = act[k] ? B.op[o] : NIL;
+                    j[k] = act[k] ? B.oj[o] : 0u;
+                    q[k] = act[k] ? B.oq[o] : NIL;
+                    xl[k] = act[k] ? B.oidl[o] : 0u;
+                    yr[k] = act[k] ? B.oidr[o] : 0u;
+                }
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    pj[k] = q[k] != NIL ? B.nd[j[k]].opair : 0u;
+                    pp[k] = p[k] != NIL ? B.nd[p[k]].opair : 0u;
+                }
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    // the member's own pair loses m_repl[m] occurrences: subtracted once in apply 3
+                    const bool hq = q[k] != NIL, hp = p[k] != NIL;
+                    ex.sub_agg(&B.cnt[pj[k]], hq, agg);
+                    ex.sub_agg(&B.cnt[pp[k]], hp, agg);
+                    const u32 X = X0 + m[k];
+                    const u32 sr = hash_insert_wave(ex, B, sh, ht, pkey_of(X, yr[k]), hq, agg);
+                    const u32 sl = hash_insert_wave(ex, B, sh, ht, pkey_of(xl[k], X), hp, agg);
+                    const u32 o = o0 + k * NT;
+                    if (hq) B.oidr[o] = sr;
+                    if (hp) B.oidl[o] = sl;
+                }
             }
         });
         // ---- apply 2: count the new pair occurrences, rewrite the sequence ----
         ex.par([&](u32 t) {
-            for (u32 o = t; o < nocc; o += NT) {
-                if (aa && (dist[o] & 1u)) continue;
-                const u32 m = B.omem[o];
-                if (m >= T) continue;
-                const u32 i = B.opos[o], j = B.oj[o], q = B.oq[o], p = B.op[o];
-                u32 idr = NIL;
-                if (q != NIL) {
-                    idr = ht.v[B.oidr[o]];
-                    B.oidr[o] = idr;
-                    ex.add(&B.cnt[idr], 1u);
+            for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
+                bool act[RK];
+                u32 m[RK], i[RK], j[RK], q[RK], p[RK], idr[RK], idl[RK];
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    const u32 o = o0 + k * NT;
+                    act[k] = o < nocc && !(aa && (dist[o] & 1u));
+                    m[k] = act[k] ? B.omem[o] : 0u;
+                    act[k] = act[k] && m[k] < T;
+                    i[k] = act[k] ? B.opos[o] : 0u;
+                    j[k] = act[k] ? B.oj[o] : 0u;
+                    q[k] = act[k] ? B.oq[o] : NIL;
+                    p[k] = act[k] ? B.op[o] : NIL;
+                    idr[k] = q[k] != NIL ? B.oidr[o] : 0u;  // hash slots (apply 1)
+                    idl[k] = p[k] != NIL ? B.oidl[o] : 0u;
                 }
-                if (p != NIL) {
-                    const u32 idl = ht.v[B.oidl[o]];
-                    B.oidl[o] = idl;
-                    ex.add(&B.cnt[idl], 1u);
-                    B.opair[p] = idl;
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    idr[k] = q[k] != NIL ? ht.v[idr[k]] : NIL;
+                    idl[k] = p[k] != NIL ? ht.v[idl[k]] : NIL;
                 }
-                B.sym[i] = X0 + m;
-                B.nxt[i] = q;
-                if (q != NIL) B.prv[q] = i;
-                B.sym[j] = DEAD;
-                B.opair[j] = NIL;
-                B.opair[i] = idr;
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    const bool hq = q[k] != NIL, hp = p[k] != NIL;
+                    ex.add_agg(&B.cnt[hq ? idr[k] : 0u], hq, agg);
+                    ex.add_agg(&B.cnt[hp ? idl[k] : 0u], hp, agg);
+                    if (!act[k]) continue;
+                    const u32 o = o0 + k * NT;
+                    if (hq) B.oidr[o] = idr[k];
+                    if (hp) {
+                        B.oidl[o] = idl[k];
+                        B.nd[p[k]].opair = idl[k];
+                    }
+                    B.nd[i[k]].sym = X0 + m[k];
+                    B.nd[i[k]].nxt = q[k];
+                    if (hq) B.nd[q[k]].prv = i[k];
+                    B.nd[j[k]].sym = DEAD;
+                    B.nd[j[k]].opair = NIL;
+                    B.nd[i[k]].opair = idr[k];
+                }
             }
         });
         ex.mark(P_APPLY_B);
@@ -736,21 +869,39 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
                 }
                 if (c >= sh.flow) qa[ex.add(&sh.qn, 1u)] = id;  // keeps Q complete (level cache)
             }
-            for (u32 m = t; m < T; m += NT) B.rules[sh.nrules + m] = pkey_of(sh.m_a[m], sh.m_b[m]);
+            for (u32 m = t; m < T; m += NT) {
+                B.rules[sh.nrules + m] = pkey_of(sh.m_a[m], sh.m_b[m]);
+                ex.sub(&B.cnt[sh.m_id[m]], sh.m_repl[m]);  // its replaced occurrences (apply 1)
+            }
         });
         // ---- apply 4: occurrence positions of the new pairs ----
         ex.par([&](u32 t) {
-            for (u32 o = t; o < nocc; o += NT) {
-                if (aa && (dist[o] & 1u)) continue;
-                const u32 m = B.omem[o];
-                if (m >= T) continue;
-                if (B.oq[o] != NIL) {
-                    const u32 id = B.oidr[o];
-                    B.occpos[B.poff[id] + ex.add(&B.plen[id], 1u)] = B.opos[o];
+            for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
+                bool act[RK];
+                u32 p[RK], q[RK], i[RK], idr[RK], idl[RK], br[RK], bl[RK];
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    const u32 o = o0 + k * NT;
+                    act[k] = o < nocc && !(aa && (dist[o] & 1u));
+                    act[k] = act[k] && B.omem[o] < T;
+                    q[k] = act[k] ? B.oq[o] : NIL;
+                    p[k] = act[k] ? B.op[o] : NIL;
+                    i[k] = act[k] ? B.opos[o] : 0u;
+                    idr[k] = q[k] != NIL ? B.oidr[o] : 0u;
+                    idl[k] = p[k] != NIL ? B.oidl[o] : 0u;
                 }
-                if (B.op[o] != NIL) {
-                    const u32 id = B.oidl[o];
-                    B.occpos[B.poff[id] + ex.add(&B.plen[id], 1u)] = B.op[o];
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    br[k] = q[k] != NIL ? B.poff[idr[k]] : 0u;
+                    bl[k] = p[k] != NIL ? B.poff[idl[k]] : 0u;
+                }
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    const bool hq = q[k] != NIL, hp = p[k] != NIL;
+                    const u32 sr = ex.slot_agg(&B.plen[idr[k]], hq, agg);
+                    const u32 sl = ex.slot_agg(&B.plen[idl[k]], hp, agg);
+                    if (hq) B.occpos[br[k] + sr] = i[k];
+                    if (hp) B.occpos[bl[k] + sl] = p[k];
                 }
             }
             if (hglob)
@@ -763,6 +914,10 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
                 sh.batch += 1;
             }
         });
+        {
+            const u32 fr[8] = {f, M, T, nocc, sh.hused, sh.nlate, aa ? 1u : 0u, sh.lsize};
+            ex.record(fr);
+        }
         ex.mark(P_LATE);
         if (sh.nlate) {
             // new pairs with count f join the level list at their key position.  When they all
@@ -839,8 +994,8 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
         u32 bytes = 0, live = 0;
         const u32 e = (t + 1) * cp < n ? (t + 1) * cp : n;
         for (u32 i = t * cp; i < e; ++i)
-            if (B.sym[i] != DEAD) {
-                bytes += uleb_len(B.sym[i]);
+            if (B.nd[i].sym != DEAD) {
+                bytes += uleb_len(B.nd[i].sym);
                 ++live;
             }
         sh.scan[t] = bytes;
@@ -889,7 +1044,7 @@ RP_HD void repair_block(E& ex, const Block& B, Shared& sh) {
                 u8* o = B.out + head + rule_bytes + uleb_len(L) + sh.scan2[t];
                 const u32 e = (t + 1) * cp < n ? (t + 1) * cp : n;
                 for (u32 i = t * cp; i < e; ++i)
-                    if (B.sym[i] != DEAD) o += uleb_put(o, B.sym[i]);
+                    if (B.nd[i].sym != DEAD) o += uleb_put(o, B.nd[i].sym);
             }
         });
     }

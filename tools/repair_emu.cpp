@@ -44,7 +44,15 @@ struct HostExec {
     u32 min(u32* p, u32 v) { const u32 o = *p; if (v < o) *p = v; return o; }
     u32 max(u32* p, u32 v) { const u32 o = *p; if (v > o) *p = v; return o; }
     u64 cas64(u64* p, u64 cmp, u64 v) { const u64 o = *p; if (o == cmp) *p = v; return o; }
+    void add_agg(u32* p, bool act, bool) { if (act) ++*p; }
+    void sub_agg(u32* p, bool act, bool) { if (act) --*p; }
+    u32 slot_agg(u32* p, bool act, bool) { return act ? (*p)++ : 0; }
+    u32 leader(u64, bool, bool) { return 0; }
+    bool is_leader(u32) const { return true; }
+    u32 from_leader(u32 v, u32) const { return v; }
     void mark(u32) {}
+    void begin(u32) {}
+    void record(const u32 (&)[8]) {}
     u32 append(u32* n, bool pred) { return pred ? (*n)++ : NIL; }
 };
 

@@ -1,0 +1,70 @@
+"""Per-batch trace of the device Re-Pair (debug): runs block 0 of a batch with
+KOLM_RP_TRACE set and summarises where the kernel's time goes by batch class.
+
+  on the GPU box:  python tools/rp_trace.py run <out_dir> [nblocks] [kind]
+  anywhere:        python tools/rp_trace.py show <trace file>
+
+Record (u32 x RP_TR_W per loop iteration): f, M (window members), T (rounds executed),
+nocc, hused, nlate, aa, lsize, then 100 MHz ticks per section (repair_core.h P_*)."""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+W = 20
+SEC = ["init", "lvscan", "lvsort", "window", "gather", "chains", "select", "applyA", "applyB", "late", "ser"]
+
+
+def run(out_dir, nblocks, kind):
+    os.makedirs(out_dir, exist_ok=True)
+    path = os.path.join(out_dir, f"trace_{kind}_{nblocks}.bin")
+    os.environ["KOLM_RP_TRACE"] = path
+    sys.path[:0] = [os.path.join(REPO, "kolmogorovlike-datacompressor_amd")]
+    from kolm import _lib, datagen as D
+    _lib.ensure_init(0)
+    MB = 1 << 20
+    gen = {"enwik": lambda s: D.enwik_like(MB, seed=s), "gradient": lambda s: D.gradient_bmp()[:MB],
+           "random": lambda s: D.splitmix64_bytes(MB, seed=s)}[kind]
+    data = b"".join(gen(5 + i) for i in range(nblocks))
+    _, _, _, st = _lib.encode_blocks(data, MB, cand_mask=1 << 9, force=[9] * nblocks)
+    print(f"{kind} x{nblocks}: ms_repair={st['ms_repair']:.1f} rules={st['rp_rules']} batches={st['rp_batches']}",
+          flush=True)
+    show(path)
+
+
+def show(path):
+    t = np.fromfile(path, np.uint32).reshape(-1, W).astype(np.int64)
+    ticks = t[:, 8:8 + len(SEC)]
+    used = np.nonzero(ticks.sum(1))[0]
+    t, ticks = t[: used[-1] + 1], ticks[: used[-1] + 1]
+    f, M, T, nocc, hused, nlate, aa, lsize = (t[:, k] for k in range(8))
+    ms = ticks / 1e5
+    tot = ms.sum()
+    print(f"iterations {len(t)}  batches {int((T > 0).sum())}  total {tot:.2f} ms  rounds {int(T.sum())}")
+    print("section ms: " + " ".join(f"{s} {ms[:, k].sum():.2f}" for k, s in enumerate(SEC)))
+    per = ms.sum(1)
+    # by occurrence count class
+    cls = np.where(T > 0, np.minimum(np.log2(np.maximum(nocc, 1)).astype(int), 16), -1)
+    print("nocc class   iters   ms    us/iter  rounds  occ")
+    for c in sorted(set(cls.tolist())):
+        m = cls == c
+        print(f"{'empty' if c < 0 else f'2^{c}':>10} {int(m.sum()):7d} {per[m].sum():7.2f} {per[m].mean() * 1e3:8.1f} "
+              f"{int(T[m].sum()):7d} {int(nocc[m].sum()):8d}")
+    # by count level f
+    print("f class      iters   ms    rounds")
+    fc = np.minimum(np.log2(np.maximum(f, 1)).astype(int), 20)
+    for c in sorted(set(fc.tolist())):
+        m = fc == c
+        print(f"{f'2^{c}':>10} {int(m.sum()):7d} {per[m].sum():7.2f} {int(T[m].sum()):7d}")
+    lim = np.bincount(np.minimum(T, 600) // 50, minlength=13)
+    print("rounds per batch histogram (bins of 50):", lim.tolist())
+    print("mean us per section per iteration: " + " ".join(f"{s} {ms[:, k].mean() * 1e3:.1f}"
+                                                           for k, s in enumerate(SEC)))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "run":
+        run(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 1, sys.argv[4] if len(sys.argv) > 4 else "enwik")
+    else:
+        show(sys.argv[2])
