@@ -43,6 +43,7 @@ LIMITER = {
     "k_lz_spec<true>": "latency: the dependent greedy-parse chain (one wave per 4 KiB chunk; each token's "
                        "candidate search starts where the previous token ended)",
     "k_lz_spec<false>": "latency: the dependent greedy-parse chain",
+    "k_lz_spec2": "latency: the dependent greedy-parse chains (two 2 KiB chunks per wave, one per half)",
     "k_repair": "latency: one workgroup per block, barrier-separated batches of dependent global accesses",
 }
 MB = 1e6

@@ -10,6 +10,9 @@
 //
 // BBWT gather (PY:417: out.append(w[(i - 1) % m])): out[r] = text[prev(SA[r])] where
 // prev steps back cyclically inside the factor.
+#include <cstdio>
+#include <cstdlib>
+
 #include "kolm_internal.h"
 
 namespace kolm {
@@ -224,6 +227,8 @@ __global__ __launch_bounds__(WG) void k_fsfl(TileGeom tg, const u8* flag, const 
 constexpr u32 DUVAL_CH = 128;                 // bytes per thread
 constexpr u32 DUVAL_SPAN = DUVAL_CH * 256;    // bytes per workgroup (32 KiB)
 constexpr u32 DUVAL_PAD = 4;                  // LDS pad per chunk (bank spread)
+constexpr u32 DUVAL_WAVE_W = 4096;            // tree levels merged by whole waves (<= 4 merges)
+constexpr u32 DUVAL_PF = 64;                  // factors per span with a cached 32-byte prefix
 
 __device__ inline u32 lds_addr(u32 q) { return q + (q / DUVAL_CH) * DUVAL_PAD; }
 
@@ -233,6 +238,21 @@ __device__ inline bool span_less(const u8* t, u32 x0, u32 x1, u32 y1) {
     for (u32 i = 0; i < m; ++i) {
         const u8 a = t[lds_addr(x0 + i)], b = t[lds_addr(x1 + i)];
         if (a != b) return a < b;
+    }
+    return la < lb;
+}
+
+// the same comparison by a whole wave, 64 bytes per step (uniform result)
+__device__ inline bool span_less_wave(const u8* t, u32 x0, u32 x1, u32 y1, u32 lane) {
+    const u32 la = x1 - x0, lb = y1 - x1, m = min(la, lb);
+    for (u32 o = 0; o < m; o += 64) {
+        const u32 i = o + lane;
+        const bool diff = i < m && t[lds_addr(x0 + i)] != t[lds_addr(x1 + i)];
+        const u64 bal = __ballot(diff);
+        if (bal) {
+            const u32 d = o + (u32)__ffsll((unsigned long long)bal) - 1;
+            return t[lds_addr(x0 + d)] < t[lds_addr(x1 + d)];
+        }
     }
     return la < lb;
 }
@@ -276,7 +296,17 @@ __device__ inline u32 bm_next(const u32* bm, const u32* sm, u32 q, u32 hi) {
     return r < hi ? r : hi;
 }
 
-__global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8* s, u32* fstart, u32* nfac) {
+// prof (debug, KOLM_DUVAL_PROF): wall-clock ticks per phase summed over workgroups
+__device__ inline void dprof(u64* prof, u32 k, u64& last) {
+    if (prof && threadIdx.x == 0) {
+        const u64 now = wall_clock64();
+        atomicAdd((unsigned long long*)&prof[k], (unsigned long long)(now - last));
+        last = now;
+    }
+}
+__global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8* s, u32* fstart, uint4* fpre,
+                                                    u32* nfac, u64* prof) {
+    u64 tlast = prof ? wall_clock64() : 0;
     __shared__ __align__(16) u8 t[DUVAL_SPAN + 256 * DUVAL_PAD];
     __shared__ u32 bm[DUVAL_SPAN / 32];
     __shared__ u32 sm[DUVAL_SPAN / 1024];
@@ -284,7 +314,7 @@ __global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8*
     const u32 sp = blockIdx.x, tid = threadIdx.x;
     const u32 b = sp / spb, k = sp - b * spb;
     const u32 lo = geo.base(b) + k * DUVAL_SPAN;
-    const u32 e = geo.end(b);
+    const u32 e = geo.end(b), e_blk = e;
     if (lo >= e) {
         if (tid == 0) nfac[sp] = 0;
         return;
@@ -306,6 +336,7 @@ __global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8*
     }
     for (u32 i = tid; i < DUVAL_SPAN / 32; i += 256) bm[i] = 0;
     __syncthreads();
+    dprof(prof, 0, tlast);
     // Duval on the thread's chunk; factor starts -> bitmap (bits of one chunk are 4 words
     // owned by this thread only)
     {
@@ -327,14 +358,44 @@ __global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8*
         }
     }
     __syncthreads();
+    dprof(prof, 1, tlast);
     if (tid < DUVAL_SPAN / 1024) {
         u32 v = 0;
         for (u32 q = 0; q < 32; ++q) v |= (bm[tid * 32 + q] != 0) << q;
         sm[tid] = v;
     }
     __syncthreads();
-    // tree merge of adjacent factorizations
+    // tree merge of adjacent factorizations: a thread per merge on the low levels, a wave
+    // per merge (64-lane factor comparisons) from DUVAL_WAVE_W up, where few merges remain
+    // and adjacent factors of text share long prefixes
     for (u32 w = DUVAL_CH; w < DUVAL_SPAN; w <<= 1) {
+        if (w >= DUVAL_WAVE_W) {
+            const u32 lane = tid & 63, wv = tid >> 6;
+            for (u32 a0 = wv * 2 * w; a0 + w < n; a0 += 2 * w * (256 / 64)) {
+                const u32 m = a0 + w, hi = min(m + w, n);
+                u32 r = m;
+                while (r < hi) {
+                    const u32 re = bm_next(bm, sm, r + 1, hi);
+                    u32 ts = r;
+                    bool merged = false;
+                    while (ts > a0) {
+                        const u32 ps = bm_prev(bm, sm, ts - 1);
+                        if (!span_less_wave(t, ps, ts, re, lane)) break;
+                        // every lane writes the same value: each then reads its own write
+                        const u32 nw = bm[ts >> 5] & ~(1u << (ts & 31));
+                        bm[ts >> 5] = nw;
+                        if (!nw) atomicAnd(&sm[ts >> 10], ~(1u << ((ts >> 5) & 31)));
+                        ts = ps;
+                        merged = true;
+                    }
+                    if (!merged) break;
+                    r = re;
+                }
+            }
+            __syncthreads();
+            dprof(prof, 2 + (31 - __clz(w)) - 7, tlast);
+            continue;
+        }
         const u32 a0 = tid * 2 * w, m = a0 + w;
         if (m < n) {
             const u32 hi = min(m + w, n);
@@ -357,6 +418,7 @@ __global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8*
             }
         }
         __syncthreads();
+        dprof(prof, 2 + (31 - __clz(w)) - 7, tlast);  // levels w = 128 .. 16384 -> 2 .. 9
     }
     // compact the factor starts of the span into fstart[lo ...]
     u32 cnt = 0;
@@ -382,9 +444,29 @@ __global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8*
         while (v) {
             const u32 bit = __ffs(v) - 1;
             v &= v - 1;
-            fstart[lo + o++] = lo + tid * DUVAL_CH + q * 32 + bit;
+            const u32 x = tid * DUVAL_CH + q * 32 + bit;  // span-local start
+            if (o < DUVAL_PF) {
+                // its first 32 bytes, big-endian words (k_duval_merge compares these first)
+                u32 w[8];
+#pragma unroll
+                for (u32 k = 0; k < 8; ++k) {
+                    u32 v4 = 0;
+#pragma unroll
+                    for (u32 e = 0; e < 4; ++e) {
+                        const u32 y = x + 4 * k + e;
+                        const u8 ch = y < n ? t[lds_addr(y)] : (lo + y < e_blk ? s[lo + y] : (u8)0);
+                        v4 = (v4 << 8) | ch;
+                    }
+                    w[k] = v4;
+                }
+                fpre[((u64)sp * DUVAL_PF + o) * 2] = make_uint4(w[0], w[1], w[2], w[3]);
+                fpre[((u64)sp * DUVAL_PF + o) * 2 + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+            }
+            fstart[lo + o++] = lo + x;
         }
     }
+    __syncthreads();
+    dprof(prof, 10, tlast);
 }
 
 // 8 bytes at s + x (any alignment) from three aligned dwords, little-endian
@@ -398,10 +480,11 @@ __device__ inline u64 load8u(const u8* s, u32 x) {
 
 // x = s[a0, a1) < y = s[a1, b1) lexicographically (proper prefix smaller); wave-uniform.
 // 8 bytes per lane per step (512 per wave) while the loads stay inside s[0, N).
-__device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N) {
+__device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N, u32* nsteps = nullptr, u32 o0 = 0) {
     const u32 lane = threadIdx.x & 63;
     const u32 la = a1 - a0, lb = b1 - a1, m = min(la, lb);
-    for (u32 o = 0; o < m; o += 512) {
+    for (u32 o = o0; o < m; o += 512) {
+        if (nsteps) ++*nsteps;
         const u32 t = o + 8 * lane;
         u32 dpos = 0xFFFFFFFFu;
         if ((u64)a1 + o + 512 + 12 <= N) {
@@ -429,9 +512,54 @@ __device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N) {
 }
 
 constexpr u32 MERGE_LDS = 8192;  // factor stack entries kept in LDS (more: the global stack)
+constexpr u32 PRE_LDS = 512;     // stack entries with their 32-byte prefix in LDS
+
+struct Pre {  // a factor's first 32 bytes as big-endian words
+    uint4 a, b;
+};
+
+// Order of x, y on their first min(m, 32) bytes: -1, 1, or 0 (equal so far).
+__device__ inline int pre_cmp(const Pre& x, const Pre& y, u32 m) {
+    const u32 xs[8] = {x.a.x, x.a.y, x.a.z, x.a.w, x.b.x, x.b.y, x.b.z, x.b.w};
+    const u32 ys[8] = {y.a.x, y.a.y, y.a.z, y.a.w, y.b.x, y.b.y, y.b.z, y.b.w};
+    const u32 mm = min(m, 32u);
+#pragma unroll
+    for (u32 k = 0; k < 8; ++k) {
+        if (4 * k >= mm) break;
+        const u32 valid = mm - 4 * k;
+        const u32 mask = valid >= 4 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (8 * valid));
+        const u32 a = xs[k] & mask, b = ys[k] & mask;
+        if (a != b) return a < b ? -1 : 1;
+    }
+    return 0;
+}
+
+__device__ inline u32 rdl(u32 v, u32 l) { return (u32)__builtin_amdgcn_readlane((int)v, l); }
+__device__ inline Pre rdl(const Pre& p, u32 l) {
+    return Pre{make_uint4(rdl(p.a.x, l), rdl(p.a.y, l), rdl(p.a.z, l), rdl(p.a.w, l)),
+               make_uint4(rdl(p.b.x, l), rdl(p.b.y, l), rdl(p.b.z, l), rdl(p.b.w, l))};
+}
+__device__ inline u32 shf(u32 v, u32 l) { return (u32)__shfl((int)v, (int)l); }
+__device__ inline Pre shf(const Pre& p, u32 l) {
+    return Pre{make_uint4(shf(p.a.x, l), shf(p.a.y, l), shf(p.a.z, l), shf(p.a.w, l)),
+               make_uint4(shf(p.b.x, l), shf(p.b.y, l), shf(p.b.z, l), shf(p.b.w, l))};
+}
+
+// One wave per block merges the span factorisations left to right (stack rule of
+// k_duval_span).  A span's first DUVAL_PF factor starts and 32-byte prefixes arrive in
+// one vector load; the two stack entries under comparison are held in registers (the
+// one below them is re-read from LDS only after a merge) and every entry keeps its
+// prefix in LDS, so nearly all comparisons are decided in registers.  Only factors that
+// agree on 32 bytes compare the text in global memory: the chain of ~800 dependent
+// comparisons per 1 MiB text block cost ~0.7 us of load latency each.
 __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8* s, const u32* fstart,
-                                                    const u32* nfac, u32* stack, u8* flag) {
+                                                    const uint4* fpre, const u32* nfac, u32* stack, u8* flag,
+                                                    u64* prof) {
     __shared__ u32 lstk[MERGE_LDS];
+    __shared__ Pre lpre[PRE_LDS];
+    __shared__ u32 lok[PRE_LDS];
+    const u64 t0 = prof ? wall_clock64() : 0;
+    u32 ncmp = 0, nstep = 0;
     const u32 b = blockIdx.x, lane = threadIdx.x;
     const u32 base = geo.base(b), end = geo.end(b);
     // the stack never holds more entries than the span factorisations together: in LDS
@@ -443,38 +571,105 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
     // written by lane 0, re-read uniformly: volatile keeps the reads off the scalar cache
     volatile u32* stk = tot <= MERGE_LDS ? lstk : stack + base;
     u32 sp = 0;
+    // the stack's top entry (valid when sp > 0): start, prefix, prefix valid
+    u32 top = 0, tok = 0;
+    Pre tpre{};
     for (u32 k = 0; k < cpb; ++k) {
         const u32 c = b * cpb + k;
         const u32 lo = base + k * DUVAL_SPAN;
         if (lo >= end) break;
         const u32 hi = min(lo + DUVAL_SPAN, end);
         const u32 nf = nfac[c];
+        // the span's first 64 factor starts and prefixes, one per lane
+        const u32 vst = lane < nf ? fstart[lo + lane] : hi;
+        Pre vpr{};
+        if (lane < nf) {
+            vpr.a = fpre[((u64)c * DUVAL_PF + lane) * 2];
+            vpr.b = fpre[((u64)c * DUVAL_PF + lane) * 2 + 1];
+        }
         u32 t = 0;
         while (t < nf) {
-            const u32 r = fstart[lo + t];
-            const u32 frontier = (t + 1 < nf) ? fstart[lo + t + 1] : hi;
-            if (lane == 0) stk[sp] = r;
-            __builtin_amdgcn_s_waitcnt(0);
+            const u32 cached = t < DUVAL_PF ? 1u : 0u;
+            const u32 r = cached ? rdl(vst, t) : fstart[lo + t];
+            const u32 frontier = t + 1 >= nf ? hi : t + 1 < DUVAL_PF ? rdl(vst, t + 1) : fstart[lo + t + 1];
+            const Pre rp = cached ? rdl(vpr, t) : Pre{};
+            if (lane == 0) {
+                stk[sp] = r;
+                if (sp < PRE_LDS) {
+                    lok[sp] = cached;
+                    lpre[sp] = rp;
+                }
+            }
             ++sp;
+            // y = the top (r, or what r merged into), x = the entry below it
+            u32 ys = r, yok = cached;
+            Pre yp = rp;
+            u32 xs = top, xok = tok;
+            Pre xp = tpre;
             bool merged = false;
             while (sp >= 2) {
-                const u32 a0 = stk[sp - 2], a1 = stk[sp - 1];
-                if (!lyn_less(s, a0, a1, frontier, (u32)geo.N)) break;
-                --sp;  // stack[-2] absorbs the top factor
+                ++ncmp;
+                const u32 la = ys - xs, lb = frontier - ys, m = min(la, lb);
+                bool less;
+                int cr = 0;
+                if (xok && yok) cr = pre_cmp(xp, yp, m);
+                if (cr)
+                    less = cr < 0;
+                else if (xok && yok && m <= 32)
+                    less = la < lb;
+                else
+                    less = lyn_less(s, xs, ys, frontier, (u32)geo.N, prof ? &nstep : nullptr, xok && yok ? 32u : 0u);
+                if (!less) break;
+                --sp;  // x absorbs y: the merged factor keeps x's start and prefix
+                ys = xs;
+                yok = xok;
+                yp = xp;
                 merged = true;
+                if (sp >= 2) {
+                    __builtin_amdgcn_s_waitcnt(0);
+                    xs = stk[sp - 2];
+                    xok = sp - 2 < PRE_LDS ? lok[sp - 2] : 0u;
+                    if (xok) xp = lpre[sp - 2];
+                }
             }
+            top = ys;
+            tok = yok;
+            tpre = yp;
             ++t;
             if (!merged) break;
         }
         // remaining right factors cannot merge: append in bulk
         for (u32 o = t; o < nf; o += 64) {
             const u32 idx = o + lane;
-            if (idx < nf) stk[sp + (idx - t)] = fstart[lo + idx];
+            // shuffles with every lane active (a source lane may be past nf)
+            const Pre pv = shf(vpr, idx & 63);
+            const u32 sv = shf(vst, idx & 63);
+            if (idx < nf) {
+                const u32 d = sp + (idx - t);
+                stk[d] = idx < DUVAL_PF ? sv : fstart[lo + idx];
+                if (d < PRE_LDS) {
+                    lok[d] = idx < DUVAL_PF ? 1u : 0u;
+                    lpre[d] = pv;
+                }
+            }
         }
-        if (t < nf) sp += nf - t;
+        if (t < nf) {
+            sp += nf - t;
+            const u32 l = nf - 1;  // the new top
+            top = l < DUVAL_PF ? rdl(vst, l) : fstart[lo + l];
+            tok = l < DUVAL_PF ? 1u : 0u;
+            if (tok) tpre = rdl(vpr, l);
+        }
         __builtin_amdgcn_s_waitcnt(0);
     }
     for (u32 i = lane; i < sp; i += 64) flag[stk[i]] = 1;
+    if (prof && lane == 0) {
+        atomicAdd((unsigned long long*)&prof[11], (unsigned long long)(wall_clock64() - t0));
+        atomicMax((unsigned long long*)&prof[12], (unsigned long long)(wall_clock64() - t0));
+        atomicAdd((unsigned long long*)&prof[13], (unsigned long long)ncmp);
+        atomicAdd((unsigned long long*)&prof[14], (unsigned long long)nstep);
+        atomicAdd((unsigned long long*)&prof[15], (unsigned long long)tot);
+    }
 }
 
 // prevc[p] = the character preceding p cyclically inside its factor (streaming pass), so
@@ -551,8 +746,19 @@ void launch_lyndon_isa(const Geom& geo, const u32* RK, u8* flag, u32* tile_tmp, 
     k_lyn_flags<<<nt, WG, 0, s>>>(tg, RK, tile_tmp + nt, flag);
 }
 
+// KOLM_DUVAL_PROF=1 (debug): per-phase wall-clock of k_duval_span and k_duval_merge
+u64* dprof_buf() {
+    static u64* prof = nullptr;
+    static const bool dp = getenv("KOLM_DUVAL_PROF") && atoi(getenv("KOLM_DUVAL_PROF"));
+    if (dp && !prof) {
+        KOLM_HIP_CHECK(hipMalloc(&prof, 16 * sizeof(u64)));
+        KOLM_HIP_CHECK(hipMemset(prof, 0, 16 * sizeof(u64)));
+    }
+    return prof;
+}
+
 // Lyndon factorisation of every block (parallel Duval + merge) -> per-position FSL.
-void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u8* FEd, u32* fstart, u32* nfac,
+void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u8* FEd, u32* fstart, uint4* fpre, u32* nfac,
                    u32* stack, u32* tile_tmp, u32* tile_tmp2, hipStream_t s, KTimer* kt) {
     if (!geo.N) return;
     TileGeom tg{geo, (geo.bs + TILE - 1) / TILE};
@@ -567,11 +773,22 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u8* FEd,
     KOLM_HIP_CHECK(hipMemsetAsync(flag, 0, geo.N, s));
     {
         KScope k(kt, KT_LYNDON, "k_duval_span", N);  // text once (+ 4 B per factor start)
-        k_duval_span<<<nch, 256, 0, s>>>(geo, cpb, text, fstart, nfac);
+        k_duval_span<<<nch, 256, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, dprof_buf());
     }
     {
         KScope k(kt, KT_LYNDON, "k_duval_merge", (u64)nch * 8);
-        k_duval_merge<<<geo.nb, 64, 0, s>>>(geo, cpb, text, fstart, nfac, stack, flag);
+        k_duval_merge<<<geo.nb, 64, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, stack, flag, dprof_buf());
+    }
+    if (u64* prof = dprof_buf()) {
+        u64 h[16];
+        KOLM_HIP_CHECK(hipStreamSynchronize(s));
+        KOLM_HIP_CHECK(hipMemcpy(h, prof, sizeof h, hipMemcpyDeviceToHost));
+        KOLM_HIP_CHECK(hipMemset(prof, 0, 16 * sizeof(u64)));
+        fprintf(stderr, "[kolm] duval_span us per workgroup:");
+        for (int k = 0; k < 11; ++k) fprintf(stderr, " %d:%.1f", k, (double)h[k] / nch / 100.0);
+        fprintf(stderr, " | merge us per block mean %.1f max %.1f, compares/block %.1f, 512-B steps/block %.1f, "
+                "span factors/block %.1f\n", (double)h[11] / geo.nb / 100.0, (double)h[12] / 100.0,
+                (double)h[13] / geo.nb, (double)h[14] / geo.nb, (double)h[15] / geo.nb);
     }
     {
         KScope k(kt, KT_LYNDON, "k_tile_starts", N);

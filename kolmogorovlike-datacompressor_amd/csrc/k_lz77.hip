@@ -295,6 +295,213 @@ __global__ __launch_bounds__(256, 8) void k_lz_spec(LzArgs z, u32 nchunks) {
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Two parse chains per wave.  The parse is a dependent chain of candidate loads (one
+// global round trip per token) and k_lz_spec runs one chain per wave: 32 chains per CU,
+// the LDS window being the limit.  Here the wave's halves parse two chunks: lanes 0-31
+// score 32 candidates of chain A's position, lanes 32-63 those of chain B, so both
+// chains' loads are in flight together (64 chains per CU with 2 KiB chunks in the same
+// 20 KiB of LDS per workgroup).  Every ballot is masked to the lane's half; per-half
+// values (position, best length) live in each lane of the half.
+// ---------------------------------------------------------------------------------
+__device__ inline u64 half_mask(u32 lane) { return (lane & 32) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull; }
+
+// Longest match at p for this lane's half (act: the half has a position to score).
+template <class T>
+__device__ void best_match_h(const LzArgs& z, const T& t, bool act, u32 p, u32 end, u32 i, u32 gs, u32& out_len,
+                             u32& out_dist, u32& nlong) {
+    const u32 lane = threadIdx.x & 63, hl = lane & 31;
+    const u64 HM = half_mask(lane);
+    u32 best = 0, bd = 0;
+    bool go = act && p + (u32)LZ_MIN <= end && i > gs;
+    const u32 maxl = go ? end - p : 0u;
+    const u32 capl = min((u32)LZ_CAP, maxl);
+    bool wide = false;
+    if constexpr (IsLds<T>::value) wide = go && p >= t.lo && p + capl + 11 <= t.hi;
+    u32 k0 = i;  // candidates this batch: slots k0-1-hl
+    while (__ballot(go)) {
+        bool valid = go && k0 > gs + hl;
+        const u32 q = valid ? z.SA3[k0 - 1 - hl] : 0u;
+        valid = valid && (p - q <= (u32)LZ_WINDOW);
+        const u64 inwin = __ballot(valid) & HM;
+        u32 l = 0;
+        if (valid) {
+            // a later candidate wins only if strictly longer: it must match at `best`
+            const bool can = best == 0 || (best < maxl && t[p + best] == t[q + best]);
+            if (can) {
+                l = LZ_MIN;  // the 3-gram is shared by the group
+                bool done = false;
+                if constexpr (IsLds<T>::value) {
+                    if (wide) {
+#pragma unroll
+                        for (int k = 0; k < LZ_CAP / 8; ++k) {
+                            if (l >= capl) break;
+                            const u64 d = lds8(t.l, p - t.lo + 3 + 8 * k) ^ lds8(t.l, q - t.lo + 3 + 8 * k);
+                            if (d) {
+                                l += (u32)(__ffsll((long long)d) - 1) >> 3;
+                                break;
+                            }
+                            l += 8;
+                        }
+                        l = min(l, capl);
+                        done = true;
+                    }
+                }
+                if (!done)
+                    while (l < capl && t[p + l] == t[q + l]) ++l;
+            }
+        }
+        // capped candidates extended exactly, one at a time by the whole wave
+        u64 longm = __ballot(valid && l >= capl && capl < maxl);
+        while (longm) {
+            const u32 j = (u32)__ffsll((long long)longm) - 1;
+            const u32 pj = __builtin_amdgcn_readlane(p, j), qj = __builtin_amdgcn_readlane(q, j);
+            const u32 cj = __builtin_amdgcn_readlane(capl, j), mj = __builtin_amdgcn_readlane(maxl, j);
+            const u32 lj = wave_lcp(t, pj, qj, cj, mj);
+            if (lane == j) l = lj;
+            longm &= longm - 1;
+            ++nlong;
+        }
+        // max length, ties -> smallest lane of the half (= smallest distance)
+        const u32 lv = valid ? l : 0u;
+        u64 cand = __ballot(lv > best) & HM;
+        if (__ballot(lv >= 64u)) {
+            u32 lm = lv;
+#pragma unroll
+            for (int o = 16; o >= 1; o >>= 1) lm = max(lm, (u32)__shfl_xor(lm, o));
+            const u64 eq = __ballot(lv == lm) & HM;
+            cand = cand ? eq : 0ull;
+        } else {
+#pragma unroll
+            for (int b = 5; b >= 0; --b) {
+                const u64 tb = __ballot((lv >> b) & 1u) & cand;
+                if (tb) cand = tb;
+            }
+        }
+        const u32 wl = cand ? (u32)__ffsll((long long)cand) - 1 : lane;
+        const u32 nl = (u32)__shfl((int)lv, (int)wl), nq = (u32)__shfl((int)q, (int)wl);
+        if (cand) {
+            best = nl;
+            bd = p - nq;
+        }
+        if (best >= maxl || inwin != HM) go = false;
+        k0 -= 32;
+    }
+    if (best < (u32)LZ_MIN) {
+        best = 0;
+        bd = 0;
+    }
+    out_len = best;
+    out_dist = bd;
+}
+
+constexpr u32 LZ_CPW = 8;                               // chunks per workgroup (2 per wave)
+constexpr u32 LZ_LWIN2 = LZ_WINDOW + LZ_CPW * LZ_CHUNK;  // 20 KiB with 2 KiB chunks
+
+__global__ __launch_bounds__(256, 8) void k_lz_spec2(LzArgs z, u32 nchunks) {
+    __shared__ __align__(16) u8 win[LZ_LWIN2];
+    const u32 lane = threadIdx.x & 63, hl = lane & 31;
+    const u32 c = blockIdx.x * LZ_CPW + (threadIdx.x >> 6) * 2 + (lane >> 5);
+    LText t{z.text, win, 0u, 0u};
+    {
+        // the workgroup's window, from its first chunk's block
+        const u32 c0 = blockIdx.x * LZ_CPW;
+        const u32 b0 = c0 / z.cpb, k0 = c0 - b0 * z.cpb;
+        const u32 bb = z.geo.base(b0), be = z.geo.end(b0);
+        const u32 s0 = bb + k0 * LZ_CHUNK;
+        const u32 lo = s0 > bb + LZ_WINDOW ? s0 - LZ_WINDOW : bb;
+        const u32 hi = min(s0 + LZ_CPW * LZ_CHUNK, be);
+        if (lo < hi) {
+            const u32 n = hi - lo;
+            if ((lo & 3) == 0 && ((uintptr_t)z.text & 3) == 0) {
+                const u32* src = reinterpret_cast<const u32*>(z.text + lo);
+                u32* dst = reinterpret_cast<u32*>(win);
+                for (u32 i = threadIdx.x; i < n / 4; i += 256) dst[i] = src[i];
+                for (u32 i = (n & ~3u) + threadIdx.x; i < n; i += 256) win[i] = z.text[lo + i];
+            } else {
+                for (u32 i = threadIdx.x; i < n; i += 256) win[i] = z.text[lo + i];
+            }
+            t.lo = lo;
+            t.hi = hi;
+        }
+        __syncthreads();
+    }
+    // this half's chunk (a half past the last chunk, or a chunk past its block end, parses nothing)
+    const bool has = c < nchunks;
+    const u32 b = has ? c / z.cpb : 0u, k = has ? c - b * z.cpb : 0u;
+    const u32 bend = has ? z.geo.end(b) : 0u;
+    const u32 s = has ? z.geo.base(b) + k * LZ_CHUNK : 0u;
+    const u32 e = (has && s < bend) ? min(s + (u32)LZ_CHUNK, bend) : s;
+    // 32-position windows of (idx3, gs3) per half, the next one prefetched
+    u32 wbase = s;
+    u32 P = wbase + hl;
+    uint2 v = P < bend ? z.ig3[P] : make_uint2(0u, 0u);
+    u32 Iw = v.x, Gw = v.y;
+    P += 32;
+    v = P < bend ? z.ig3[P] : make_uint2(0u, 0u);
+    u32 In = v.x, Gn = v.y;
+    u32 q = s, ntok = 0, off = 0, nlong = 0, nbuf = 0;
+    u32 bpos = 0, blen = 0, bdist = 0, boff = 0;
+    const u32 hbase = lane & 32;
+    while (__ballot(q < e)) {
+        const bool act = q < e;
+        if (act && q >= wbase + 32) {
+            if (q < wbase + 64) {
+                Iw = In;
+                Gw = Gn;
+                wbase += 32;
+            } else {
+                wbase = q;
+                const u32 P0 = wbase + hl;
+                const uint2 w0 = P0 < bend ? z.ig3[P0] : make_uint2(0u, 0u);
+                Iw = w0.x;
+                Gw = w0.y;
+            }
+            const u32 P1 = wbase + 32 + hl;
+            const uint2 w1 = P1 < bend ? z.ig3[P1] : make_uint2(0u, 0u);
+            In = w1.x;
+            Gn = w1.y;
+        }
+        const u32 cur = act ? q - wbase : 0u;
+        const u32 iq = (u32)__shfl((int)Iw, (int)(hbase + cur)), gq = (u32)__shfl((int)Gw, (int)(hbase + cur));
+        u32 len, dist;
+        best_match_h(z, t, act, q, bend, iq, gq, len, dist, nlong);
+        if (act) {
+            if (hl == nbuf) {
+                bpos = q;
+                blen = len;
+                bdist = dist;
+                boff = off;
+            }
+            if (++nbuf == 32) {
+                const u32 slot = s + ntok + 1 - 32 + hl;
+                z.tok_pos[slot] = bpos;
+                z.tok_len[slot] = blen;
+                z.tok_dist[slot] = bdist;
+                z.tok_off[slot] = boff;
+                nbuf = 0;
+            }
+            ++ntok;
+            off += tok_bytes(len, dist);
+            q += len ? len : 1;
+        }
+    }
+    if (has && hl < nbuf) {
+        const u32 slot = s + ntok - nbuf + hl;
+        z.tok_pos[slot] = bpos;
+        z.tok_len[slot] = blen;
+        z.tok_dist[slot] = bdist;
+        z.tok_off[slot] = boff;
+    }
+    if (has && hl == 0) {
+        z.c_ntok[c] = ntok;
+        z.c_exit[c] = q;
+        z.c_bytes[c] = off;
+    }
+    nlong = wave_reduce(nlong, OpAddU(), 0u);
+    if (lane == 0 && nlong) atomicAdd(z.nlong, nlong);
+}
+
 // Per block (one wave): real chunk entries, fix-up tokens, chunk output offsets, size.
 __global__ __launch_bounds__(64) void k_lz_stitch(LzArgs z) {
     const u32 b = blockIdx.x;
@@ -409,6 +616,12 @@ __global__ __launch_bounds__(256) void k_lz_emit(LzArgs z, const u32* method, co
 
 }  // namespace
 
+const char* lz_spec_name() {
+    static const bool lds = !getenv("KOLM_LZ_LDS") || atoi(getenv("KOLM_LZ_LDS")) != 0;
+    static const bool dual = !getenv("KOLM_LZ_DUAL") || atoi(getenv("KOLM_LZ_DUAL")) != 0;
+    return dual ? "k_lz_spec2" : lds ? "k_lz_spec<true>" : "k_lz_spec<false>";
+}
+
 void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
     if (!z.geo.nb) return;
     const u32 nchunks = z.cpb * z.geo.nb;
@@ -416,8 +629,11 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
         // (slot, group start) windows 8 B + text 1 B per position (+16 B per token, added
         // by the caller once the token count is known)
         static const bool lds = !getenv("KOLM_LZ_LDS") || atoi(getenv("KOLM_LZ_LDS")) != 0;
-        KScope k(kt, KT_LZPARSE, lds ? "k_lz_spec<true>" : "k_lz_spec<false>", z.geo.N * 9);
-        if (lds)
+        static const bool dual = !getenv("KOLM_LZ_DUAL") || atoi(getenv("KOLM_LZ_DUAL")) != 0;
+        KScope k(kt, KT_LZPARSE, lz_spec_name(), z.geo.N * 9);
+        if (dual)
+            k_lz_spec2<<<(nchunks + LZ_CPW - 1) / LZ_CPW, 256, 0, s>>>(z, nchunks);
+        else if (lds)
             k_lz_spec<true><<<(nchunks + 3) / 4, 256, 0, s>>>(z, nchunks);
         else
             k_lz_spec<false><<<(nchunks + 3) / 4, 256, 0, s>>>(z, nchunks);

@@ -174,7 +174,19 @@ struct kolm_ctx {
         const auto it = bufs.find(name);
         return it == bufs.end() ? 0 : it->second.cap;
     }
-    void sync() { KOLM_HIP_CHECK(hipStreamSynchronize(active)); }
+    // Host round trips (per-round counters) spin on the stream instead of sleeping in
+    // hipStreamSynchronize: the sort stream idles for the host's wake-up otherwise.
+    void sync() {
+        static const bool block = getenv("KOLM_SYNC_BLOCK") && atoi(getenv("KOLM_SYNC_BLOCK"));
+        if (block) {
+            KOLM_HIP_CHECK(hipStreamSynchronize(active));
+            return;
+        }
+        hipError_t e;
+        while ((e = hipStreamQuery(active)) == hipErrorNotReady) {
+        }
+        KOLM_HIP_CHECK(e);
+    }
 };
 
 namespace {
@@ -430,7 +442,7 @@ struct Pipeline {
         const u64 ntiles = (u64)((geo.bs + TILE - 1) / TILE) * geo.nb + 16;
         const u64 nch = (geo.bs + 32767) / 32768 * (u64)geo.nb + 1;  // DUVAL_SPAN
         launch_lyndon(geo, text, c->get<u8>("flag", N), c->get<u64>("FSL", N), c->get<u8>("FEd", N),
-                      c->get<u32>("lyn_fstart", N),
+                      c->get<u32>("lyn_fstart", N), c->get<uint4>("lyn_fpre", nch * 128),
                       c->get<u32>("lyn_nfac", nch), c->get<u32>("lyn_stack", N), c->get<u32>("lyn_t1", 2 * ntiles + 16),
                       c->get<u32>("lyn_t2", 2 * ntiles + 2 * geo.nb + 16), c->active, c->kt());
     }
@@ -804,7 +816,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         st.lz_tokens = tokens;
         c->timing_collect(&st);
         st.kt[KOLM_KT_LZPARSE].bytes += tokens * 16;
-        if (c->timing && want_lz) c->kacc[getenv("KOLM_LZ_LDS") && !atoi(getenv("KOLM_LZ_LDS")) ? "k_lz_spec<false>" : "k_lz_spec<true>"].bytes += tokens * 16;  // token records
+        if (c->timing && want_lz) c->kacc[lz_spec_name()].bytes += tokens * 16;  // token records
         st.lz_long = c->h_cnt[C_NLONG];
         st.ms_sa = ev_ms(ev[0], ev[1]);
         st.ms_entropy = ev_ms(ev[1], ev[2]);

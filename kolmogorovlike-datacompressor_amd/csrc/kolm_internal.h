@@ -253,7 +253,7 @@ void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists
 void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, hipStream_t s);
 
 // ---- k_blocks.hip: per-block scans, Lyndon factors, BBWT gather ----
-void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u8* FEd, u32* fstart, u32* nfac,
+void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u8* FEd, u32* fstart, uint4* fpre, u32* nfac,
                    u32* stack, u32* tile_tmp, u32* tile_tmp2, hipStream_t s, KTimer* kt = nullptr);
 void launch_lyndon_isa(const Geom& geo, const u32* RK, u8* flag, u32* tile_tmp, u32* tile_tmp2, hipStream_t s);
 void launch_prevc(const Geom& geo, const u8* text, const u8* flag, const u64* FSL, u8* prevc, hipStream_t s);
@@ -316,7 +316,7 @@ void launch_rice_only(const Geom& geo, const u8* in, int k, u8* out, u32* tile_t
                       u32* out_size, hipStream_t s);
 
 // ---- k_lz77.hip ----
-constexpr int LZ_CHUNK = 4096;  // speculative-parse chunk (one wave each)
+constexpr int LZ_CHUNK = 2048;  // speculative-parse chunk (one half-wave chain each, k_lz_spec2)
 
 struct LzArgs {
     Geom geo;
@@ -349,6 +349,7 @@ struct LzArgs {
     u32 cpb;           // chunks per block
 };
 void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr);
+const char* lz_spec_name();  // the speculative-parse kernel in use (timing / roofline)
 void launch_lz_emit(const LzArgs& z, const u32* method, const u64* off, u8* arena, hipStream_t s);
 
 // ---- k_repair.hip: exact Re-Pair (candidate 9), one workgroup per block ----

@@ -44,7 +44,7 @@ def main():
     arena = ctypes.c_void_p()
     _lib.check(L.kolm_dev_alloc(ctx, cap, ctypes.byref(arena)))
     nb = (n + a.bs - 1) // a.bs
-    sizes = np.zeros((nb, 9), np.uint32)
+    sizes = np.zeros((nb, _lib.KOLM_NCAND), np.uint32)
     method = np.zeros(nb, np.uint32)
     off = np.zeros(nb + 1, np.uint64)
     for it in range(a.iters):
