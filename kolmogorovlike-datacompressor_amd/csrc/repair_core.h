@@ -61,6 +61,7 @@ constexpr u32 NBASE = 65536;      // ids of the byte pairs: (a << 8) | b
 constexpr u32 MAX_N = 1u << 22;   // block length limit of the device Re-Pair
 constexpr u32 RK = 4;             // occurrences per thread per step in the occurrence loops
 constexpr u32 AGG_MIN = 2048;     // batches with at least this many occurrences aggregate atomics
+constexpr u32 WIN_MIN = 32;       // smallest adaptive window (members per batch)
 
 enum : u32 { RS_SIZE = 0, RS_RULES, RS_FINAL, RS_BATCHES, RS_ERR, RS_LEVELS, RS_N };
 // profile sections (ex.mark(id): time since the previous mark is charged to the previous id)
@@ -117,6 +118,7 @@ struct Shared {
     u32 f, lp, lsize, M, V, T, tot, nocc, npairs, next_sym, nrules, pool, batch, hused, nlate;
     u32 t1, t2, ts, any_aa, cut, maxc, err, total, levels;
     u32 flow, qn, qn2, qvalid;  // level cache: Q = every pair with count >= flow
+    u32 mcap;                   // adaptive window: members gathered per batch (<= W)
 };
 
 // Carve a block's workspace out of `base` (nullptr: size query).  Returns the bytes
@@ -155,6 +157,8 @@ RP_HD inline u64 workspace_layout(char* base, u32 n, Block& B) {
 }
 
 RP_HD inline u64 pkey_of(u32 a, u32 b) { return ((u64)a << 32) | b; }
+RP_HD inline u32 umin(u32 a, u32 b) { return a < b ? a : b; }
+RP_HD inline u32 umax(u32 a, u32 b) { return a > b ? a : b; }
 
 RP_HD inline u32 hslot(u64 k, u32 mask) {
     k ^= k >> 31;
@@ -347,7 +351,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
         if (t == 0) {
             sh.pool = 0; sh.npairs = NBASE; sh.next_sym = 256; sh.nrules = 0; sh.batch = 0;
             sh.lp = 0; sh.lsize = 0; sh.f = 0; sh.hused = 0; sh.nlate = 0; sh.err = RE_OK; sh.levels = 0;
-            sh.qvalid = 0; sh.qn = 0; sh.flow = NIL;
+            sh.qvalid = 0; sh.qn = 0; sh.flow = NIL; sh.mcap = W;
         }
     });
     ex.par([&](u32 t) {
@@ -498,7 +502,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
             }
             if (done) break;
             ex.par([&](u32 t) {
-                if (t == 0) { sh.f = sh.maxc; sh.lsize = 0; sh.lp = 0; sh.levels++; }
+                if (t == 0) { sh.f = sh.maxc; sh.lsize = 0; sh.lp = 0; sh.levels++; sh.mcap = W; }
             });
             ex.par([&](u32 t) {
                 const u32 qn = sh.qn, fl = sh.f;
@@ -561,7 +565,9 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
             });
             continue;
         }
-        const u32 Mw = sh.V < W ? sh.V : W;
+        // members beyond T are gathered and scanned for nothing (re-gathered by the next
+        // batch): the window follows the previous batch's T (doubling when it was not cut)
+        const u32 Mw = umin(sh.V, umin(W, sh.mcap));
         ex.scan(sh.scan2, &sh.total);  // region prefix over the window's members
         ex.par([&](u32 t) {
             if (t < Mw) {
@@ -912,6 +918,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                 sh.nrules += T;
                 sh.npairs += sh.hused;
                 sh.batch += 1;
+                sh.mcap = T < M ? umax(WIN_MIN, umin(W, 2 * T + 16)) : umin(W, 2 * M);
             }
         });
         {
