@@ -101,7 +101,7 @@ struct Block {
     u32 hmask;
     u32* husd;
     u64* rules;
-    u32 *qa, *qb;  // level cache (PC entries each)
+    u64 *qa, *qb;  // level cache (PC entries each): (count when last read) << 32 | pair id
     u8* out;
     u64 out_cap;
     u32* result;  // RS_N words
@@ -151,8 +151,8 @@ RP_HD inline u64 workspace_layout(char* base, u32 n, Block& B) {
     B.hval = (u32*)take((u64)HS * 4);
     B.hmask = HS - 1;
     B.rules = (u64*)take((N / 2 + 16) * 8);
-    B.qa = (u32*)take(PC * 4);
-    B.qb = (u32*)take(PC * 4);
+    B.qa = (u64*)take(PC * 8);
+    B.qb = (u64*)take(PC * 8);
     return off;
 }
 
@@ -385,8 +385,8 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
     u32* li = B.liA;
     u64* tk = B.lkB;
     u32* ti = B.liB;
-    u32* qa = B.qa;  // level cache Q (and its compaction target)
-    u32* qb = B.qb;
+    u64* qa = B.qa;  // level cache Q (and its compaction target)
+    u64* qb = B.qb;
     u32 guard = 0;
     // ---------------- batches ----------------
     for (;;) {
@@ -459,11 +459,17 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                     }
                     ex.par([&](u32 t) {
                         const u32 np = sh.npairs, fl = sh.flow;
-                        for (u32 i0 = 0; i0 < np; i0 += NT) {
-                            const u32 id = i0 + t;
-                            const bool keep = id < np && B.cnt[id] >= fl;
-                            const u32 slot = ex.append(&sh.qn, keep);
-                            if (keep) qa[slot] = id;
+                        for (u32 i0 = 0; i0 < np; i0 += RK * NT) {
+                            u32 c[RK];
+#pragma unroll
+                            for (u32 k = 0; k < RK; ++k) c[k] = i0 + k * NT + t < np ? B.cnt[i0 + k * NT + t] : 0u;
+#pragma unroll
+                            for (u32 k = 0; k < RK; ++k) {
+                                const u32 id = i0 + k * NT + t;
+                                const bool keep = id < np && c[k] >= fl;
+                                const u32 slot = ex.append(&sh.qn, keep);
+                                if (keep) qa[slot] = ((u64)c[k] << 32) | id;
+                            }
                         }
                         if (t == 0) sh.qvalid = 1;
                     });
@@ -471,26 +477,30 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                 // drop the entries below flow, and the maximum of the rest
                 ex.par([&](u32 t) { if (t == 0) { sh.maxc = 0; sh.qn2 = 0; } });
                 ex.par([&](u32 t) {
+                    // current counts (they only fall between levels); the survivors keep
+                    // theirs, so the level list below needs no second count load
                     u32 m = 0;
                     const u32 qn = sh.qn, fl = sh.flow;
-                    for (u32 e0 = 0; e0 < qn; e0 += NT) {
-                        const u32 e = e0 + t;
-                        u32 id = 0, c = 0;
-                        if (e < qn) {
-                            id = qa[e];
-                            c = B.cnt[id];
-                        }
-                        const bool keep = e < qn && c >= fl;
-                        const u32 slot = ex.append(&sh.qn2, keep);
-                        if (keep) {
-                            qb[slot] = id;
-                            m = c > m ? c : m;
+                    for (u32 e0 = 0; e0 < qn; e0 += RK * NT) {
+                        u32 id[RK], c[RK];
+#pragma unroll
+                        for (u32 k = 0; k < RK; ++k) id[k] = e0 + k * NT + t < qn ? (u32)qa[e0 + k * NT + t] : 0u;
+#pragma unroll
+                        for (u32 k = 0; k < RK; ++k) c[k] = e0 + k * NT + t < qn ? B.cnt[id[k]] : 0u;
+#pragma unroll
+                        for (u32 k = 0; k < RK; ++k) {
+                            const bool keep = e0 + k * NT + t < qn && c[k] >= fl;
+                            const u32 slot = ex.append(&sh.qn2, keep);
+                            if (keep) {
+                                qb[slot] = ((u64)c[k] << 32) | id[k];
+                                m = c[k] > m ? c[k] : m;
+                            }
                         }
                     }
                     if (m) ex.max(&sh.maxc, m);
                 });
                 {
-                    u32* x = qa; qa = qb; qb = x;
+                    u64* x = qa; qa = qb; qb = x;
                 }
                 ex.par([&](u32 t) { if (t == 0) sh.qn = sh.qn2; });
                 if (sh.maxc >= sh.flow) break;
@@ -505,15 +515,20 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                 if (t == 0) { sh.f = sh.maxc; sh.lsize = 0; sh.lp = 0; sh.levels++; sh.mcap = W; }
             });
             ex.par([&](u32 t) {
+                // Q was just filtered: its entries carry their current counts
                 const u32 qn = sh.qn, fl = sh.f;
-                for (u32 e0 = 0; e0 < qn; e0 += NT) {
-                    const u32 e = e0 + t;
-                    const u32 id = e < qn ? qa[e] : 0u;
-                    const bool hit = e < qn && B.cnt[id] == fl;
-                    const u32 slot = ex.append(&sh.lsize, hit);
-                    if (hit) {
-                        lk[slot] = B.pkey[id];
-                        li[slot] = id;
+                for (u32 e0 = 0; e0 < qn; e0 += RK * NT) {
+                    u64 q[RK];
+#pragma unroll
+                    for (u32 k = 0; k < RK; ++k) q[k] = e0 + k * NT + t < qn ? qa[e0 + k * NT + t] : 0ull;
+#pragma unroll
+                    for (u32 k = 0; k < RK; ++k) {
+                        const bool hit = e0 + k * NT + t < qn && (u32)(q[k] >> 32) == fl;
+                        const u32 slot = ex.append(&sh.lsize, hit);
+                        if (hit) {
+                            lk[slot] = B.pkey[(u32)q[k]];
+                            li[slot] = (u32)q[k];
+                        }
                     }
                 }
             });
@@ -873,7 +888,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                     B.lkL[k] = B.pkey[id];
                     B.liL[k] = id;
                 }
-                if (c >= sh.flow) qa[ex.add(&sh.qn, 1u)] = id;  // keeps Q complete (level cache)
+                if (c >= sh.flow) qa[ex.add(&sh.qn, 1u)] = ((u64)c << 32) | id;  // keeps Q complete (level cache)
             }
             for (u32 m = t; m < T; m += NT) {
                 B.rules[sh.nrules + m] = pkey_of(sh.m_a[m], sh.m_b[m]);
