@@ -762,7 +762,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         std::vector<u64> pr((u64)nb * RP_P_N);
         KOLM_HIP_CHECK(hipMemcpy(pr.data(), rpa.prof, sizeof(u64) * pr.size(), hipMemcpyDeviceToHost));
         static const char* const nm[RP_P_N] = {"init", "lvscan", "lvsort", "window", "gather", "chains",
-                                               "select", "applyA", "applyB", "late", "serialise"};
+                                               "select", "applyA", "applyB", "late", "serialise", "applyA2"};
         fprintf(stderr, "[kolm] Re-Pair sections, ms per block (mean over %u blocks):", nb);
         for (u32 k = 0; k < RP_P_N; ++k) {
             u64 t = 0;

@@ -367,7 +367,7 @@ struct RpArgs {
     u64* prof;         // [nb * RP_P_N] wall-clock ticks per section (KOLM_RP_PROF=1), or null
     u32* trace;        // [RP_TR_CAP * RP_TR_W] per-batch records of block 0 (KOLM_RP_TRACE=file), or null
 };
-constexpr u32 RP_P_N = 11;
+constexpr u32 RP_P_N = 12;
 constexpr u32 RP_TR_W = 20;        // trace record: 8 batch fields + per-section ticks
 constexpr u32 RP_TR_CAP = 1u << 16;
 u64 repair_ws_bytes(u32 bs);

@@ -62,11 +62,12 @@ constexpr u32 MAX_N = 1u << 22;   // block length limit of the device Re-Pair
 constexpr u32 RK = 4;             // occurrences per thread per step in the occurrence loops
 constexpr u32 AGG_MIN = 2048;     // batches with at least this many occurrences aggregate atomics
 constexpr u32 WIN_MIN = 32;       // smallest adaptive window (members per batch)
+constexpr u32 NCNT = 2048;        // batches creating at most this many pairs count them in LDS
 
 enum : u32 { RS_SIZE = 0, RS_RULES, RS_FINAL, RS_BATCHES, RS_ERR, RS_LEVELS, RS_N };
 // profile sections (ex.mark(id): time since the previous mark is charged to the previous id)
 enum : u32 { P_INIT = 0, P_LVSCAN, P_LVSORT, P_WINDOW, P_GATHER, P_CHAINS, P_SELECT, P_APPLY_A, P_APPLY_B, P_LATE,
-             P_SER, P_N };
+             P_SER, P_APPLY_A2, P_N };
 enum : u32 { RE_OK = 0, RE_CAP = 1, RE_LOOP = 2, RE_LEN = 3 };
 
 // Per position, one 32-byte record (AoS): an occurrence's neighbourhood (prev, next and
@@ -119,6 +120,8 @@ struct Shared {
     u32 t1, t2, ts, any_aa, cut, maxc, err, total, levels;
     u32 flow, qn, qn2, qvalid;  // level cache: Q = every pair with count >= flow
     u32 mcap;                   // adaptive window: members gathered per batch (<= W)
+    u32 ncnt[NCNT];             // new pairs of a batch (id - npairs < NCNT): counts, then fill counters
+    u32 npoff[NCNT];            //   and region offsets, in LDS instead of global atomics
 };
 
 // Carve a block's workspace out of `base` (nullptr: size query).  Returns the bytes
@@ -547,6 +550,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
             sh.scan[t] = idx < sh.lsize && B.cnt[li[idx]] == f ? 1u : 0u;
             sh.scan2[t] = 0;
             for (u32 e = t; e < SORT_LDS; e += NT) sh.skey[e] = EMPTY;  // the LDS key table (HTab)
+            for (u32 e = t; e < NCNT; e += NT) sh.ncnt[e] = 0;
             if (t == 0) {
                 sh.cut = NIL; sh.any_aa = 0; sh.nocc = 0; sh.t1 = NIL; sh.t2 = NIL; sh.ts = NIL;
                 sh.hused = 0; sh.nlate = 0;
@@ -832,7 +836,10 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                 }
             }
         });
+        ex.mark(P_APPLY_A2);
         // ---- apply 2: count the new pair occurrences, rewrite the sequence ----
+        const bool lcnt = sh.hused <= NCNT;  // new-pair counters in LDS
+        const u32 np0 = sh.npairs;
         ex.par([&](u32 t) {
             for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
                 bool act[RK];
@@ -858,8 +865,13 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
                     const bool hq = q[k] != NIL, hp = p[k] != NIL;
-                    ex.add_agg(&B.cnt[hq ? idr[k] : 0u], hq, agg);
-                    ex.add_agg(&B.cnt[hp ? idl[k] : 0u], hp, agg);
+                    if (lcnt) {
+                        if (hq) ex.add(&sh.ncnt[idr[k] - np0], 1u);
+                        if (hp) ex.add(&sh.ncnt[idl[k] - np0], 1u);
+                    } else {
+                        ex.add_agg(&B.cnt[hq ? idr[k] : 0u], hq, agg);
+                        ex.add_agg(&B.cnt[hp ? idl[k] : 0u], hp, agg);
+                    }
                     if (!act[k]) continue;
                     const u32 o = o0 + k * NT;
                     if (hq) B.oidr[o] = idr[k];
@@ -881,8 +893,15 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
         ex.par([&](u32 t) {
             for (u32 u = t; u < sh.hused; u += NT) {
                 const u32 id = sh.npairs + u;
-                const u32 c = B.cnt[id];
-                B.poff[id] = ex.add(&sh.pool, c);
+                const u32 c = lcnt ? sh.ncnt[u] : B.cnt[id];
+                const u32 po = ex.add(&sh.pool, c);
+                B.poff[id] = po;
+                if (lcnt) {
+                    B.cnt[id] = c;
+                    B.plen[id] = c;  // apply 4 fills all c slots of the region
+                    sh.npoff[u] = po;
+                    sh.ncnt[u] = 0;  // now the region's fill counter
+                }
                 if (c == f) {
                     const u32 k = ex.add(&sh.nlate, 1u);
                     B.lkL[k] = B.pkey[id];
@@ -910,6 +929,20 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                     i[k] = act[k] ? B.opos[o] : 0u;
                     idr[k] = q[k] != NIL ? B.oidr[o] : 0u;
                     idl[k] = p[k] != NIL ? B.oidl[o] : 0u;
+                }
+                if (lcnt) {
+#pragma unroll
+                    for (u32 k = 0; k < RK; ++k) {
+                        if (q[k] != NIL) {
+                            const u32 u = idr[k] - np0;
+                            B.occpos[sh.npoff[u] + ex.add(&sh.ncnt[u], 1u)] = i[k];
+                        }
+                        if (p[k] != NIL) {
+                            const u32 u = idl[k] - np0;
+                            B.occpos[sh.npoff[u] + ex.add(&sh.ncnt[u], 1u)] = p[k];
+                        }
+                    }
+                    continue;
                 }
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {

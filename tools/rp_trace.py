@@ -13,7 +13,7 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 W = 20
-SEC = ["init", "lvscan", "lvsort", "window", "gather", "chains", "select", "applyA", "applyB", "late", "ser"]
+SEC = ["init", "lvscan", "lvsort", "window", "gather", "chains", "select", "applyA", "applyB", "late", "ser", "applyA2"]
 
 
 def run(out_dir, nblocks, kind):
