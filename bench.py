@@ -383,6 +383,8 @@ def main():
                        "cdc_mode": cdc,
                        "device_ms": {k: round(s0[k], 2) for k in ("ms_total", "ms_sa", "ms_lz", "ms_entropy", "ms_emit")},
                        "rounds": [s0["lin_rounds"], s0["cyc_rounds"]],
+                       "lz77": {"tokens": s0["lz_tokens"], "stitch_fixups": s0["lz_fix"],
+                                "long_extensions": s0["lz_long"]},
                        "pipeline_roofline": pipe,
                        "families_ms_per_step": {kk: round(v["ms"] / a.steps, 2) for kk, v in
                                                 sorted(kern.items(), key=lambda kv: -kv[1]["ms"])},

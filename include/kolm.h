@@ -98,6 +98,7 @@ typedef struct kolm_stats {
     uint64_t rp_rules;        /* Re-Pair rules over all blocks */
     uint64_t rp_batches;      /* Re-Pair batches (sequential depth) summed over blocks */
     uint64_t rp_final;        /* Re-Pair final sequence symbols over all blocks */
+    uint64_t lz_fix;          /* LZ77 tokens the stitch computed off the speculative paths */
 } kolm_stats;
 
 /* ---- library / default context ------------------------------------------------ */

@@ -568,6 +568,497 @@ __global__ __launch_bounds__(64) void k_lz_stitch(LzArgs z) {
     }
 }
 
+// =====================================================================================
+// Workgroup-local path (default, KOLM_LZ_LOCAL=1): no global 3-gram index.
+//
+// A workgroup owns the LZL_HOME home positions [hs, he) of one block.  Every candidate of
+// a home position p lies in [p - 4096, p), so the window W = [hs - 4096 - LZL_LEAD, he)
+// (clipped to the block) holds them all.  The workgroup copies W's text into LDS, sorts
+// W's 3-gram positions by (3-gram, position) with three stable LSD byte passes in LDS
+// (u16 window offsets; no global traffic), and keeps the slot of every home position
+// (islot) and a group-head bitmap: p's candidates are the slots islot(p)-1, islot(p)-2, ...
+// down to p's group start, in ascending distance — the same contiguous-slot walk as the
+// global index, with every load an LDS load.
+//
+// The home is parsed by 16 speculative chains (16 lanes each, 4 per wave) over 256-byte
+// chunks.  A chain starts LZL_LEAD bytes before its chunk (a lead-in whose tokens are not
+// recorded) so that its path has usually re-synchronised with the true greedy path by the
+// chunk start.  Matches are compared (exactly, in LDS) up to LZL_CAPX bytes past the chunk
+// end; a token that reaches that cap ends the chunk with its length unresolved (LZ_UNRES).
+//
+// k_lz_stitch_l then walks each block's true path over the chunk summaries (64 chunks
+// per wave load): a chunk whose first recorded token starts at the true entry is taken
+// as it is; otherwise the true path is followed token by token with an exact brute-force
+// search of the 4096-byte window (LDS copy) until it lands on a recorded token; an
+// unresolved last token on the path is recomputed exactly.
+// =====================================================================================
+constexpr u32 LZL_NW = LZL_HOME + LZ_WINDOW + LZL_LEAD;  // window positions indexed (8256)
+constexpr u32 LZL_TXT = LZL_NW + LZL_CAPX + 32;         // text window + alignment + compare slack
+constexpr u32 LZL_ISL = LZL_HOME + LZL_LEAD;            // islot entries [hs - LEAD, he)
+constexpr u32 LZL_NCHAIN = LZL_HOME / LZL_CHUNK;        // 16 chains, 4 per wave
+static_assert(LZL_NCHAIN == 16, "4 chains of 16 lanes per wave, 4 waves");
+static_assert(LZL_ISL * 2 + ((LZL_NW + 63) / 64) * 8 <= LZL_NW * 2, "islot + head bitmap fit the sort scratch");
+
+// LDS text without bounds checks (every access is inside the loaded window by construction)
+struct WinText {
+    const u8* l;
+    u32 tlo;
+    __device__ inline u8 operator[](u32 x) const { return l[x - tlo]; }
+};
+
+__device__ inline u32 key3(const u8* t, u32 x) { return ((u32)t[x] << 16) | ((u32)t[x + 1] << 8) | t[x + 2]; }
+
+// One stable LSD pass over the nw window positions by the byte t[x + DOFF] (t = window text
+// at window offset 0): src (null = identity) -> dst.  Wave w owns the contiguous element
+// range [w*Q, (w+1)*Q): per-wave digit counts (LDS atomics), digit-major / wave-minor
+// offsets, then each wave places its elements 64 at a time in order (ballot match-any
+// ranking; the leader advances the wave's digit offset — a wave's LDS operations retire in
+// program order, so no barrier is needed between its steps).
+template <int DOFF>
+__device__ void lzl_pass(const u8* t, const u16* src, u16* dst, u32 nw, u32 (*hist)[256], u32* sh) {
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) hist[i][tid] = 0;
+    __syncthreads();
+    const u32 Q = (nw + 3) / 4;
+    const u32 b0 = min(w * Q, nw), b1 = min(b0 + Q, nw);
+    for (u32 e = b0 + lane; e < b1; e += 64) {
+        const u32 x = src ? (u32)src[e] : e;
+        atomicAdd(&hist[w][t[x + DOFF]], 1u);
+    }
+    __syncthreads();
+    {
+        const u32 h0 = hist[0][tid], h1 = hist[1][tid], h2 = hist[2][tid], h3 = hist[3][tid];
+        const u32 tot = h0 + h1 + h2 + h3;
+        const u32 incl = wave_incl_scan(tot, OpAddU(), 0u);
+        if (lane == 63) sh[w] = incl;
+        __syncthreads();
+        u32 ex = incl - tot;
+        for (u32 i = 0; i < w; ++i) ex += sh[i];
+        hist[0][tid] = ex;
+        hist[1][tid] = ex + h0;
+        hist[2][tid] = ex + h0 + h1;
+        hist[3][tid] = ex + h0 + h1 + h2;
+    }
+    __syncthreads();
+    const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (u32 e0 = b0; e0 < b1; e0 += 64) {
+        const u32 e = e0 + lane;
+        const bool valid = e < b1;
+        const u32 x = valid ? (src ? (u32)src[e] : e) : 0u;
+        const u32 dg = valid ? (u32)t[x + DOFF] : 0u;
+        u64 m = __ballot(valid);
+#pragma unroll
+        for (u32 bit = 0; bit < 8; ++bit) {
+            const u64 bal = __ballot((dg >> bit) & 1u);
+            m &= ((dg >> bit) & 1u) ? bal : ~bal;
+        }
+        const u32 rank = (u32)__popcll(m & lt);
+        const u32 o = valid ? hist[w][dg] : 0u;
+        if (valid) dst[o + rank] = (u16)x;
+        if (valid && rank == 0) hist[w][dg] = o + (u32)__popcll(m);
+    }
+    __syncthreads();
+}
+
+// first slot of slot k's 3-gram group (slot 0 is always a head)
+__device__ inline u32 lzl_gs(const u64* bm, u32 k) {
+    u32 wi = k >> 6;
+    u64 m = bm[wi] & (~0ull >> (63 - (k & 63)));
+    while (!m) m = bm[--wi];
+    return wi * 64 + 63 - (u32)__clzll(m);
+}
+
+__device__ inline u64 grp_mask(u32 lane) { return 0xFFFFull << (lane & 48); }
+
+// Longest match at p for this lane's 16-lane chain (act: the chain has a position to
+// score).  Exact up to lim = min(block end, chunk end + LZL_CAPX) - p: unres when the best
+// candidate reaches lim short of the block end.
+__device__ void lzl_best(const u8* txt, u32 tlo, const u16* A, const u64* bm, const u16* isl, u32 lo, u32 ilo,
+                         bool act, u32 p, u32 lim, u32 end, u32& out_len, u32& out_dist, bool& unres, u32& nlong) {
+    const u32 lane = threadIdx.x & 63, hl = lane & 15;
+    const u64 GM = grp_mask(lane);
+    const WinText T{txt, tlo};
+    u32 best = 0, bd = 0;
+    bool go = act && p + (u32)LZ_MIN <= end;
+    u32 k0 = 0, gs = 0;
+    if (go) {
+        k0 = isl[p - ilo];
+        gs = lzl_gs(bm, k0);
+        go = k0 > gs;
+    }
+    const u32 capl = min((u32)LZ_CAP, lim);
+    const u32 pr = p - tlo;
+    while (__ballot(go)) {
+        bool valid = go && k0 > gs + hl;
+        const u32 q = valid ? lo + (u32)A[k0 - 1 - hl] : 0u;
+        valid = valid && (p - q <= (u32)LZ_WINDOW);
+        const u64 inwin = __ballot(valid) & GM;
+        u32 l = 0;
+        if (valid) {
+            // a later candidate wins only if strictly longer: it must match at `best`
+            const bool can = best == 0 || (best < lim && T[p + best] == T[q + best]);
+            if (can) {
+                l = LZ_MIN;  // the 3-gram is shared by the group
+                const u32 qr = q - tlo;
+#pragma unroll
+                for (int k = 0; k < LZ_CAP / 8; ++k) {
+                    if (l >= capl) break;
+                    const u64 d = lds8(txt, pr + 3 + 8 * k) ^ lds8(txt, qr + 3 + 8 * k);
+                    if (d) {
+                        l += (u32)(__ffsll((long long)d) - 1) >> 3;
+                        break;
+                    }
+                    l += 8;
+                }
+                l = min(l, capl);
+            }
+        }
+        // capped candidates extended exactly (up to lim), one at a time by the whole wave
+        u64 longm = __ballot(valid && l >= capl && capl < lim);
+        while (longm) {
+            const u32 j = (u32)__ffsll((long long)longm) - 1;
+            const u32 pj = __builtin_amdgcn_readlane(p, j), qj = __builtin_amdgcn_readlane(q, j);
+            const u32 cj = __builtin_amdgcn_readlane(capl, j), mj = __builtin_amdgcn_readlane(lim, j);
+            const u32 lj = wave_lcp(T, pj, qj, cj, mj);
+            if (lane == j) l = lj;
+            longm &= longm - 1;
+            ++nlong;
+        }
+        // max length, ties -> smallest lane of the chain (= smallest distance)
+        const u32 lv = valid ? l : 0u;
+        u64 cand = __ballot(lv > best) & GM;
+        if (__ballot(lv >= 64u)) {
+            u32 lm = lv;
+#pragma unroll
+            for (int o = 8; o >= 1; o >>= 1) lm = max(lm, (u32)__shfl_xor(lm, o));
+            const u64 eq = __ballot(lv == lm) & GM;
+            cand = cand ? eq : 0ull;
+        } else {
+#pragma unroll
+            for (int b = 5; b >= 0; --b) {
+                const u64 tb = __ballot((lv >> b) & 1u) & cand;
+                if (tb) cand = tb;
+            }
+        }
+        const u32 wl = cand ? (u32)__ffsll((long long)cand) - 1 : lane;
+        const u32 nl = (u32)__shfl((int)lv, (int)wl), nq = (u32)__shfl((int)q, (int)wl);
+        if (cand) {
+            best = nl;
+            bd = p - nq;
+        }
+        if (best >= lim || inwin != GM) go = false;
+        k0 -= 16;
+    }
+    unres = false;
+    if (best < (u32)LZ_MIN) {
+        best = 0;
+        bd = 0;
+    } else {
+        unres = best >= lim && lim < end - p;
+    }
+    out_len = best;
+    out_dist = bd;
+}
+
+__global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb) {
+    __shared__ __align__(16) u8 txt[LZL_TXT];
+    __shared__ __align__(16) u16 A[LZL_NW];
+    __shared__ __align__(16) u16 B[LZL_NW];
+    __shared__ u32 hist[4][256];
+    __shared__ u32 sh[4];
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u32 b = blockIdx.x / hpb, h = blockIdx.x - b * hpb;
+    const u32 base = z.geo.base(b), end = z.geo.end(b);
+    const u32 hs = base + h * LZL_HOME;
+    if (hs >= end) return;
+    const u32 he = min(hs + (u32)LZL_HOME, end);
+    const u32 lo = hs - base > (u32)(LZ_WINDOW + LZL_LEAD) ? hs - LZ_WINDOW - LZL_LEAD : base;
+    const u32 ilo = hs - base > (u32)LZL_LEAD ? hs - LZL_LEAD : base;
+    const u32 hi = min(end, he + (u32)LZL_CAPX);
+    const u32 tlo = lo & ~3u;  // LDS origin (dword aligned)
+    {
+        const u32 n = hi - tlo;
+        if (((uintptr_t)z.text & 3) == 0) {
+            const u32* src = reinterpret_cast<const u32*>(z.text + tlo);
+            u32* dst = reinterpret_cast<u32*>(txt);
+            for (u32 i = tid; i < n / 4; i += 256) dst[i] = src[i];
+            for (u32 i = (n & ~3u) + tid; i < n; i += 256) txt[i] = z.text[tlo + i];
+        } else {
+            for (u32 i = tid; i < n; i += 256) txt[i] = z.text[tlo + i];
+        }
+    }
+    __syncthreads();
+    // 3-gram positions of the window: [lo, min(he, end - 2))
+    const u32 lim3 = end - base >= 3 ? end - 2 : base;
+    const u32 top = min(he, lim3);
+    const u32 nw = top > lo ? top - lo : 0u;
+    const u8* tw = txt + (lo - tlo);  // window text at window offset 0
+    if (nw) {
+        lzl_pass<2>(tw, nullptr, A, nw, hist, sh);
+        lzl_pass<1>(tw, A, B, nw, hist, sh);
+        lzl_pass<0>(tw, B, A, nw, hist, sh);
+    }
+    // islot of [ilo, he) and the group-head bitmap, in the sort scratch B
+    u16* isl = B;
+    u64* bm = reinterpret_cast<u64*>(B + LZL_ISL);
+    for (u32 j0 = 0; j0 < nw; j0 += 256) {
+        const u32 j = j0 + tid;
+        bool head = false;
+        if (j < nw) {
+            const u32 x = A[j];
+            if (lo + x >= ilo) isl[lo + x - ilo] = (u16)j;
+            head = j == 0 || key3(tw, x) != key3(tw, A[j - 1]);
+        }
+        const u64 bal = __ballot(head);
+        if (lane == 0 && j0 + w * 64 < nw) bm[(j0 >> 6) + w] = bal;
+    }
+    __syncthreads();
+    // 16 chains: chain g of wave w parses chunk cid = 4w + g
+    const u32 hl = lane & 15;
+    const u32 cid = w * 4 + (lane >> 4);
+    const u32 s = hs + cid * LZL_CHUNK;
+    const bool has = s < end;
+    const u32 e = has ? min(s + (u32)LZL_CHUNK, end) : 0u;
+    const u32 c = b * z.cpb + h * LZL_NCHAIN + cid;
+    const u32 lend = has ? min(end, e + (u32)LZL_CAPX) : 0u;
+    u32 q = has ? ((cid == 0 && hs == base) ? s : s - LZL_LEAD) : 0u;
+    u32 ntok = 0, off = 0, nlong = 0, nbuf = 0;
+    u32 bpos = 0, blen = 0, bdist = 0, boff = 0;
+    bool un = false;
+    while (__ballot(has && q < e)) {
+        const bool act = has && q < e;
+        u32 len, dist;
+        bool unres;
+        lzl_best(txt, tlo, A, bm, isl, lo, ilo, act, q, act ? lend - q : 0u, end, len, dist, unres, nlong);
+        if (act) {
+            if (q >= s) {
+                if (hl == nbuf) {
+                    bpos = q;
+                    blen = len;
+                    bdist = dist;
+                    boff = off;
+                }
+                if (++nbuf == 16) {
+                    const u32 slot = s + ntok + 1 - 16 + hl;
+                    z.tok_pos[slot] = bpos;
+                    z.tok_len[slot] = blen;
+                    z.tok_dist[slot] = bdist;
+                    z.tok_off[slot] = boff;
+                    nbuf = 0;
+                }
+                ++ntok;
+                off += tok_bytes(len, dist);
+            }
+            un = un || unres;
+            q += len ? len : 1;
+        }
+    }
+    if (has && hl < nbuf) {
+        const u32 slot = s + ntok - nbuf + hl;
+        z.tok_pos[slot] = bpos;
+        z.tok_len[slot] = blen;
+        z.tok_dist[slot] = bdist;
+        z.tok_off[slot] = boff;
+    }
+    if (has && hl == 0) {
+        z.c_ntok[c] = ntok;
+        z.c_exit[c] = q | (un ? LZ_UNRES : 0u);
+        z.c_bytes[c] = off;
+    }
+    nlong = wave_reduce(nlong, OpAddU(), 0u);
+    if (lane == 0 && nlong) atomicAdd(z.nlong, nlong);
+}
+
+// Exact longest match at q (PY:1686-1708 semantics: ascending distance, strictly longer
+// wins, unbounded length) by brute force over the window, from an LDS copy of the text
+// [wlo, whi) refreshed when q's window is not inside it.  One wave.
+constexpr u32 BF_WIN = LZ_WINDOW + 1024;
+
+__device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u32 base, u32 end, u32& out_len,
+                         u32& out_dist, u32& nlong) {
+    const u32 lane = threadIdx.x & 63;
+    out_len = 0;
+    out_dist = 0;
+    if (q + (u32)LZ_MIN > end) return;
+    const u32 dmax = min(q - base, (u32)LZ_WINDOW);
+    if (!dmax) return;
+    const u32 need = q - dmax;
+    if (!(wlo <= need && wlo <= whi && (q + 256 <= whi || whi == end))) {
+        wlo = need;
+        const u32 tlo = need & ~3u;
+        whi = min(end, tlo + BF_WIN);
+        const u32 n = whi - tlo;
+        __syncthreads();
+        if (((uintptr_t)z.text & 3) == 0) {
+            const u32* src = reinterpret_cast<const u32*>(z.text + tlo);
+            u32* dst = reinterpret_cast<u32*>(win);
+            for (u32 i = lane; i < n / 4; i += 64) dst[i] = src[i];
+            for (u32 i = (n & ~3u) + lane; i < n; i += 64) win[i] = z.text[tlo + i];
+        } else {
+            for (u32 i = lane; i < n; i += 64) win[i] = z.text[tlo + i];
+        }
+        __syncthreads();
+    }
+    const LText t{z.text, win, wlo & ~3u, whi};
+    const u32 maxl = end - q;
+    const u32 capl = min((u32)LZ_CAP, maxl);
+    const u8 c0 = t[q], c1 = t[q + 1], c2 = t[q + 2];
+    u32 best = 0, bd = 0;
+    for (u32 d0 = 1; d0 <= dmax; d0 += 64) {
+        const u32 d = d0 + lane;
+        const u32 x = q - d;
+        bool ok = d <= dmax && t[x] == c0 && t[x + 1] == c1 && t[x + 2] == c2;
+        if (ok && best) ok = best < maxl && t[x + best] == t[q + best];
+        u32 l = 0;
+        if (ok) {
+            l = LZ_MIN;
+            while (l < capl && t[x + l] == t[q + l]) ++l;
+        }
+        u64 longm = __ballot(ok && l >= capl && capl < maxl);
+        while (longm) {
+            const u32 j = (u32)__ffsll((long long)longm) - 1;
+            const u32 xj = __builtin_amdgcn_readlane(x, j);
+            const u32 lj = wave_lcp(t, q, xj, capl, maxl);
+            if (lane == j) l = lj;
+            longm &= longm - 1;
+            ++nlong;
+        }
+        const u32 lv = ok ? l : 0u;
+        const u32 lm = wave_reduce(lv, OpMaxU(), 0u);
+        if (lm > best) {
+            const u64 eq = __ballot(lv == lm);
+            best = lm;
+            bd = d0 + (u32)__ffsll((long long)eq) - 1;
+        }
+        if (best >= maxl) break;
+    }
+    if (best >= (u32)LZ_MIN) {
+        out_len = best;
+        out_dist = bd;
+    }
+}
+
+// Per block (one wave): the true path over the chunk summaries of k_lz_local.
+__global__ __launch_bounds__(64) void k_lz_stitch_l(LzArgs z) {
+    __shared__ __align__(16) u8 win[BF_WIN + 16];
+    const u32 b = blockIdx.x, lane = threadIdx.x;
+    const u32 base = z.geo.base(b), bend = z.geo.end(b);
+    const u32 CH = 1u << z.cshift;
+    const u32 nck = (bend - base + CH - 1) >> z.cshift;
+    u32 wlo = 1, whi = 0;  // no window loaded
+    u32 entry = base, boff = 0, ntot = 0, fi = 0, nlong = 0, nfix_all = 0;
+    for (u32 kb = 0; kb < nck; kb += 64) {
+        const u32 k = kb + lane;
+        const bool have = k < nck;
+        const u32 c = b * z.cpb + k;
+        const u32 sl = base + (k << z.cshift);
+        const u32 nt_l = have ? z.c_ntok[c] : 0u;
+        const u32 ex_l = have ? z.c_exit[c] : 0u;
+        const u32 by_l = have ? z.c_bytes[c] : 0u;
+        const u32 fp_l = (have && nt_l) ? z.tok_pos[sl] : NONE;
+        u32 o_first = 0, o_fix0 = 0, o_nfix = 0, o_fixb = 0, o_off = 0;
+        const u32 kn = min(64u, nck - kb);
+        for (u32 j = 0; j < kn; ++j) {
+            const u32 s = base + ((kb + j) << z.cshift);
+            const u32 e = min(s + CH, bend);
+            const u32 nt = __builtin_amdgcn_readlane(nt_l, j), ex = __builtin_amdgcn_readlane(ex_l, j);
+            const u32 by = __builtin_amdgcn_readlane(by_l, j), fp = __builtin_amdgcn_readlane(fp_l, j);
+            const u32 fix0 = base + fi;
+            u32 first, nfix = 0, fixb = 0, spec = 0, next;
+            if (entry >= e) {
+                first = nt;
+                next = entry;
+            } else if (fp == entry && !(ex & LZ_UNRES)) {
+                first = 0;
+                spec = by;
+                next = ex;
+            } else {
+                u32 q = entry, jt = 0;
+                bool conv = false;
+                while (q < e) {
+                    // first recorded token at or after q (tokens ascend; jt only grows)
+                    u32 tq = NONE;
+                    for (;;) {
+                        const u32 i = jt + lane;
+                        const u32 tp = i < nt ? z.tok_pos[s + i] : NONE;
+                        const u64 ge = __ballot(tp >= q);
+                        if (ge) {
+                            const u32 f = (u32)__ffsll((long long)ge) - 1;
+                            jt += f;
+                            tq = (u32)__shfl((int)tp, (int)f);
+                            break;
+                        }
+                        jt += 64;
+                    }
+                    if (jt < nt && tq == q) {
+                        conv = true;
+                        break;
+                    }
+                    u32 len, dist;
+                    bf_match(z, win, wlo, whi, q, base, bend, len, dist, nlong);
+                    if (lane == 0) {
+                        z.fix_pos[base + fi] = q;
+                        z.fix_len[base + fi] = len;
+                        z.fix_dist[base + fi] = dist;
+                        z.fix_off[base + fi] = boff + fixb;
+                    }
+                    ++fi;
+                    ++nfix;
+                    fixb += tok_bytes(len, dist);
+                    q += len ? len : 1;
+                }
+                if (conv) {
+                    first = jt;
+                    spec = by - z.tok_off[s + jt];
+                    next = ex & ~LZ_UNRES;
+                    if (ex & LZ_UNRES) {
+                        // the last recorded token reached the speculative cap: exact length
+                        const u32 li = s + nt - 1;
+                        const u32 pp = z.tok_pos[li], ol = z.tok_len[li], od = z.tok_dist[li];
+                        u32 nl, nd;
+                        bf_match(z, win, wlo, whi, pp, base, bend, nl, nd, nlong);
+                        spec = spec + tok_bytes(nl, nd) - tok_bytes(ol, od);
+                        if (lane == 0) {
+                            z.tok_len[li] = nl;
+                            z.tok_dist[li] = nd;
+                        }
+                        next = pp + (nl ? nl : 1u);
+                    }
+                } else {
+                    first = nt;
+                    next = q;
+                }
+                nfix_all += nfix;
+            }
+            if (lane == j) {
+                o_first = first;
+                o_fix0 = fix0;
+                o_nfix = nfix;
+                o_fixb = fixb;
+                o_off = boff;
+            }
+            boff += fixb + spec;
+            ntot += nfix + (nt - first);
+            entry = next;
+        }
+        if (have) {
+            z.c_first[c] = o_first;
+            z.c_fix0[c] = o_fix0;
+            z.c_nfix[c] = o_nfix;
+            z.c_fixbytes[c] = o_fixb;
+            z.c_off[c] = o_off;
+        }
+    }
+    if (lane == 0) {
+        z.lz_size[b] = boff;
+        z.ntok[b] = ntot;
+        z.b_nfix[b] = fi;
+        if (nlong) atomicAdd(z.nlong, nlong);
+        if (nfix_all && z.nfix) atomicAdd(z.nfix, nfix_all);
+    }
+}
+
 __device__ inline u32 put_uleb(u8* d, u32 v) {
     u32 n = 0;
     for (;;) {
@@ -602,9 +1093,9 @@ __global__ __launch_bounds__(256) void k_lz_emit(LzArgs z, const u32* method, co
     if (!force_all && method[b] != 7u) return;
     const u32 base = z.geo.base(b);
     u8* dst = arena + off[b];
-    const u32 k = (g - base) / LZ_CHUNK;
+    const u32 k = (g - base) >> z.cshift;
     const u32 c = b * z.cpb + k;
-    const u32 s = base + k * LZ_CHUNK;
+    const u32 s = base + (k << z.cshift);
     const u32 i = g - s;
     const u32 first = z.c_first[c];
     if (i >= first && i < z.c_ntok[c]) {
@@ -616,14 +1107,34 @@ __global__ __launch_bounds__(256) void k_lz_emit(LzArgs z, const u32* method, co
 
 }  // namespace
 
+bool lz_local() {
+    static const bool v = !getenv("KOLM_LZ_LOCAL") || atoi(getenv("KOLM_LZ_LOCAL")) != 0;
+    return v;
+}
+
 const char* lz_spec_name() {
     static const bool lds = !getenv("KOLM_LZ_LDS") || atoi(getenv("KOLM_LZ_LDS")) != 0;
     static const bool dual = !getenv("KOLM_LZ_DUAL") || atoi(getenv("KOLM_LZ_DUAL")) != 0;
+    if (lz_local()) return "k_lz_local";
     return dual ? "k_lz_spec2" : lds ? "k_lz_spec<true>" : "k_lz_spec<false>";
 }
 
 void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
     if (!z.geo.nb) return;
+    if (lz_local()) {
+        const u32 hpb = (z.geo.bs + LZL_HOME - 1) / LZL_HOME;
+        {
+            // text window (LZL_NW + LZL_CAPX bytes per 4 KiB home: ~2.1 B per position) +
+            // 16 B per token (added by the caller once the token count is known)
+            KScope k(kt, KT_LZPARSE, "k_lz_local", z.geo.N * 2);
+            k_lz_local<<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb);
+        }
+        {
+            KScope k(kt, KT_LZPARSE, "k_lz_stitch", (u64)z.cpb * z.geo.nb * 16);
+            k_lz_stitch_l<<<z.geo.nb, 64, 0, s>>>(z);
+        }
+        return;
+    }
     const u32 nchunks = z.cpb * z.geo.nb;
     {
         // (slot, group start) windows 8 B + text 1 B per position (+16 B per token, added

@@ -49,6 +49,7 @@ enum : int {
     C_STATUS = 20,
     C_NLONG = 21,
     C_RICE = 22,
+    C_NFIX = 23,     // LZ77 stitch fix-up tokens (statistics)
     C_CLSE = 24,     // 12 slots: elements per small class
     C_L0ELEM = 36,
     C_L1ELEM = 37,
@@ -484,7 +485,6 @@ struct Pipeline {
         return out;
     }
     u8* bbwt() {
-        linear3();
         lyndon();
         return cyclic();
     }
@@ -503,8 +503,10 @@ struct Pipeline {
         LzArgs z{};
         z.geo = geo;
         z.text = text;
-        z.SA3 = c->get<u32>("SA3", N);
-        z.ig3 = c->get<uint2>("ig3", N);
+        if (!lz_local()) {
+            z.SA3 = c->get<u32>("SA3", N);
+            z.ig3 = c->get<uint2>("ig3", N);
+        }
         z.tok_pos = c->get<u32>("tok_pos", N);
         z.tok_len = c->get<u32>("tok_len", N);
         z.tok_dist = c->get<u32>("tok_dist", N);
@@ -513,7 +515,9 @@ struct Pipeline {
         z.fix_len = c->get<u32>("fix_len", N);
         z.fix_dist = c->get<u32>("fix_dist", N);
         z.fix_off = c->get<u32>("fix_off", N);
-        z.cpb = (geo.bs + LZ_CHUNK - 1) / LZ_CHUNK;
+        z.cshift = lz_local() ? 8 : 11;
+        static_assert(LZL_CHUNK == 256 && LZ_CHUNK == 2048, "chunk shifts");
+        z.cpb = (geo.bs + (1u << z.cshift) - 1) >> z.cshift;
         const u64 nch = (u64)z.cpb * geo.nb + 1;
         z.c_ntok = c->get<u32>("c_ntok", nch);
         z.c_exit = c->get<u32>("c_exit", nch);
@@ -527,11 +531,13 @@ struct Pipeline {
         z.ntok = c->get<u32>("ntok", geo.nb);
         z.lz_size = c->get<u32>("lz_size", geo.nb);
         z.nlong = c->get<u32>("counters", C_N) + C_NLONG;
+        z.nfix = c->get<u32>("counters", C_N) + C_NFIX;
         return z;
     }
 
     void lz(const LzArgs& z) {
         KOLM_HIP_CHECK(hipMemsetAsync(z.nlong, 0, sizeof(u32), c->active));
+        KOLM_HIP_CHECK(hipMemsetAsync(z.nfix, 0, sizeof(u32), c->active));
         launch_lz_parse(z, c->active, c->kt());
     }
 };
@@ -677,7 +683,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         KOLM_HIP_CHECK(hipStreamWaitEvent(ms, ej[3], 0));
     }
     c->active = ms;
-    P.linear3();
+    if (!lz_local()) P.linear3();  // the global 3-gram index of the KOLM_LZ_LOCAL=0 path
     {
         EmitArgs ce{};
         ce.geo = geo;
@@ -818,6 +824,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         st.kt[KOLM_KT_LZPARSE].bytes += tokens * 16;
         if (c->timing && want_lz) c->kacc[lz_spec_name()].bytes += tokens * 16;  // token records
         st.lz_long = c->h_cnt[C_NLONG];
+        st.lz_fix = c->h_cnt[C_NFIX];
         st.ms_sa = ev_ms(ev[0], ev[1]);
         st.ms_entropy = ev_ms(ev[1], ev[2]);
         st.ms_lz = ev_ms(ej[2], ej[1]);
@@ -1219,6 +1226,7 @@ int kolm_encode_blocks_multi(int ngpu, const uint8_t* data, uint64_t total, uint
             agg.cyc_active += s.cyc_active;
             agg.lz_tokens += s.lz_tokens;
             agg.lz_long += s.lz_long;
+            agg.lz_fix += s.lz_fix;
             agg.ms_total = std::max(agg.ms_total, s.ms_total);
             agg.ms_sa = std::max(agg.ms_sa, s.ms_sa);
             agg.ms_lz = std::max(agg.ms_lz, s.ms_lz);
@@ -1710,7 +1718,7 @@ int kolm_lz77_encode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size
         geom_init(geo, n, (u32)n);
         u8* d = upload(c, in, n);
         Pipeline P{c, geo, d};
-        P.linear3();
+        if (!lz_local()) P.linear3();
         LzArgs z = P.lz_args();
         P.lz(z);
         u32 sz = 0;

@@ -316,7 +316,15 @@ void launch_rice_only(const Geom& geo, const u8* in, int k, u8* out, u32* tile_t
                       u32* out_size, hipStream_t s);
 
 // ---- k_lz77.hip ----
-constexpr int LZ_CHUNK = 2048;  // speculative-parse chunk (one half-wave chain each, k_lz_spec2)
+constexpr int LZ_CHUNK = 2048;  // speculative-parse chunk of the global-index path (k_lz_spec2, KOLM_LZ_LOCAL=0)
+// Workgroup-local path (k_lz_local, default): a workgroup owns LZL_HOME consecutive positions
+// of one block, indexes its window [home - 4096 - LZL_LEAD, home end) in LDS, and parses the
+// home with LZL_HOME / LZL_CHUNK chains of 16 lanes (4 per wave)
+constexpr int LZL_HOME = 4096;
+constexpr int LZL_CHUNK = 256;
+constexpr int LZL_LEAD = 64;    // speculative lead-in parsed before a chain's chunk start
+constexpr int LZL_CAPX = 256;   // speculative matches are compared up to this far past the chunk end
+constexpr u32 LZ_UNRES = 0x80000000u;  // c_exit flag: the chunk's last token reached LZL_CAPX (length unresolved)
 
 struct LzArgs {
     Geom geo;
@@ -347,7 +355,10 @@ struct LzArgs {
     u32* lz_size;      // [nb] stream size
     u32* nlong;        // [1]
     u32 cpb;           // chunks per block
+    u32 cshift;        // chunk = 1 << cshift bytes (LZ_CHUNK or LZL_CHUNK)
+    u32* nfix;         // [1] fix-up tokens computed by the stitch (statistics)
 };
+bool lz_local();       // KOLM_LZ_LOCAL (default 1): workgroup-local index path
 void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr);
 const char* lz_spec_name();  // the speculative-parse kernel in use (timing / roofline)
 void launch_lz_emit(const LzArgs& z, const u32* method, const u64* off, u8* arena, hipStream_t s);

@@ -63,6 +63,7 @@ class Stats(ctypes.Structure):
         ("rp_rules", ctypes.c_uint64),
         ("rp_batches", ctypes.c_uint64),
         ("rp_final", ctypes.c_uint64),
+        ("lz_fix", ctypes.c_uint64),
     ]
 
     def as_dict(self):
