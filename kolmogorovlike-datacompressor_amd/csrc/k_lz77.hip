@@ -23,6 +23,7 @@
 //     chunk's speculative path (a token depends on its position only, so both parses
 //     coincide from there); greedy parses re-synchronise within a few tokens;
 //   * k_lz_emit: one thread per token slot writes its bytes at its final offset.
+#include <algorithm>
 #include <cstdlib>
 
 #include "kolm_internal.h"
@@ -606,26 +607,39 @@ struct WinText {
     __device__ inline u8 operator[](u32 x) const { return l[x - tlo]; }
 };
 
-__device__ inline u32 key3(const u8* t, u32 x) { return ((u32)t[x] << 16) | ((u32)t[x + 1] << 8) | t[x + 2]; }
+// 16-bit hash of the 3-gram at window offset x: the LDS index groups positions by hash
+// (ascending position inside a group); a candidate whose 3-gram differs is rejected by
+// the byte compare, so hash collisions only cost a wasted lane.
+__device__ inline u32 hash3(const u8* t, u32 x) {
+    const u32 k = ((u32)t[x] << 16) | ((u32)t[x + 1] << 8) | t[x + 2];
+    return (k * 0x9E3779B1u) >> 16;
+}
 
-// One stable LSD pass over the nw window positions by the byte t[x + DOFF] (t = window text
-// at window offset 0): src (null = identity) -> dst.  Wave w owns the contiguous element
-// range [w*Q, (w+1)*Q): per-wave digit counts (LDS atomics), digit-major / wave-minor
+constexpr u32 LZL_PER = (LZL_NW + 255) / 256;  // window elements per lane in a sort pass (33)
+
+// One stable LSD pass over the nw window positions by hash byte DG, in place in A (identity
+// order for the first pass).  Wave w owns the contiguous element range [w*Q, (w+1)*Q),
+// staged in registers: per-wave digit counts (LDS atomics), digit-major / wave-minor
 // offsets, then each wave places its elements 64 at a time in order (ballot match-any
 // ranking; the leader advances the wave's digit offset — a wave's LDS operations retire in
 // program order, so no barrier is needed between its steps).
-template <int DOFF>
-__device__ void lzl_pass(const u8* t, const u16* src, u16* dst, u32 nw, u32 (*hist)[256], u32* sh) {
+template <int DG, bool IOTA>
+__device__ void lzl_pass(const u8* t, u16* A, u32 nw, u32 (*hist)[256], u32* sh) {
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u32 Q = (nw + 3) / 4;
+    const u32 b0 = min(w * Q, nw), b1 = min(b0 + Q, nw);
+    u32 xv[LZL_PER];
+#pragma unroll
+    for (u32 k = 0; k < LZL_PER; ++k) {
+        const u32 e = b0 + k * 64 + lane;
+        xv[k] = e < b1 ? (IOTA ? e : (u32)A[e]) : 0u;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) hist[i][tid] = 0;
     __syncthreads();
-    const u32 Q = (nw + 3) / 4;
-    const u32 b0 = min(w * Q, nw), b1 = min(b0 + Q, nw);
-    for (u32 e = b0 + lane; e < b1; e += 64) {
-        const u32 x = src ? (u32)src[e] : e;
-        atomicAdd(&hist[w][t[x + DOFF]], 1u);
-    }
+#pragma unroll
+    for (u32 k = 0; k < LZL_PER; ++k)
+        if (b0 + k * 64 + lane < b1) atomicAdd(&hist[w][(hash3(t, xv[k]) >> (8 * DG)) & 255u], 1u);
     __syncthreads();
     {
         const u32 h0 = hist[0][tid], h1 = hist[1][tid], h2 = hist[2][tid], h3 = hist[3][tid];
@@ -642,11 +656,12 @@ __device__ void lzl_pass(const u8* t, const u16* src, u16* dst, u32 nw, u32 (*hi
     }
     __syncthreads();
     const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    for (u32 e0 = b0; e0 < b1; e0 += 64) {
-        const u32 e = e0 + lane;
-        const bool valid = e < b1;
-        const u32 x = valid ? (src ? (u32)src[e] : e) : 0u;
-        const u32 dg = valid ? (u32)t[x + DOFF] : 0u;
+#pragma unroll
+    for (u32 k = 0; k < LZL_PER; ++k) {
+        if (b0 + k * 64 >= b1) break;  // wave-uniform
+        const bool valid = b0 + k * 64 + lane < b1;
+        const u32 x = xv[k];
+        const u32 dg = valid ? (hash3(t, x) >> (8 * DG)) & 255u : 0u;
         u64 m = __ballot(valid);
 #pragma unroll
         for (u32 bit = 0; bit < 8; ++bit) {
@@ -655,13 +670,13 @@ __device__ void lzl_pass(const u8* t, const u16* src, u16* dst, u32 nw, u32 (*hi
         }
         const u32 rank = (u32)__popcll(m & lt);
         const u32 o = valid ? hist[w][dg] : 0u;
-        if (valid) dst[o + rank] = (u16)x;
+        if (valid) A[o + rank] = (u16)x;
         if (valid && rank == 0) hist[w][dg] = o + (u32)__popcll(m);
     }
     __syncthreads();
 }
 
-// first slot of slot k's 3-gram group (slot 0 is always a head)
+// first slot of slot k's hash group (slot 0 is always a head)
 __device__ inline u32 lzl_gs(const u64* bm, u32 k) {
     u32 wi = k >> 6;
     u64 m = bm[wi] & (~0ull >> (63 - (k & 63)));
@@ -671,51 +686,68 @@ __device__ inline u32 lzl_gs(const u64* bm, u32 k) {
 
 __device__ inline u64 grp_mask(u32 lane) { return 0xFFFFull << (lane & 48); }
 
+// max over the 16 lanes of a DPP row, in every lane of the row (quad butterflies + row rotates)
+__device__ inline u32 row_max16(u32 v) {
+    v = max(v, KOLM_DPP(0u, v, 0xB1, 0xF));   // quad_perm [1,0,3,2]
+    v = max(v, KOLM_DPP(0u, v, 0x4E, 0xF));   // quad_perm [2,3,0,1]
+    v = max(v, KOLM_DPP(0u, v, 0x124, 0xF));  // row_ror:4
+    v = max(v, KOLM_DPP(0u, v, 0x128, 0xF));  // row_ror:8
+    return v;
+}
+
 // Longest match at p for this lane's 16-lane chain (act: the chain has a position to
-// score).  Exact up to lim = min(block end, chunk end + LZL_CAPX) - p: unres when the best
-// candidate reaches lim short of the block end.
+// score).  Exact up to lim = min(block end, chunk end + LZL_CAPX) - p (<= 576): unres when
+// the best candidate reaches lim short of the block end.
 __device__ void lzl_best(const u8* txt, u32 tlo, const u16* A, const u64* bm, const u16* isl, u32 lo, u32 ilo,
-                         bool act, u32 p, u32 lim, u32 end, u32& out_len, u32& out_dist, bool& unres, u32& nlong) {
+                         bool act, u32 p, u32 lim, u32 end, u32& out_len, u32& out_dist, bool& unres, u32& nlong,
+                         u32& nbatch) {
     const u32 lane = threadIdx.x & 63, hl = lane & 15;
     const u64 GM = grp_mask(lane);
     const WinText T{txt, tlo};
     u32 best = 0, bd = 0;
     bool go = act && p + (u32)LZ_MIN <= end;
-    u32 k0 = 0, gs = 0;
+    u32 k0 = 0, gs = 0, qa = 0;
     if (go) {
         k0 = isl[p - ilo];
+        qa = k0 > hl ? (u32)A[k0 - 1 - hl] : 0u;  // first batch, issued beside the bitmap load
         gs = lzl_gs(bm, k0);
         go = k0 > gs;
     }
     const u32 capl = min((u32)LZ_CAP, lim);
     const u32 pr = p - tlo;
     while (__ballot(go)) {
+        ++nbatch;
+        const u32 qn = (go && k0 > 16 + hl) ? (u32)A[k0 - 17 - hl] : 0u;  // next batch
         bool valid = go && k0 > gs + hl;
-        const u32 q = valid ? lo + (u32)A[k0 - 1 - hl] : 0u;
+        const u32 q = lo + qa;
         valid = valid && (p - q <= (u32)LZ_WINDOW);
         const u64 inwin = __ballot(valid) & GM;
         u32 l = 0;
         if (valid) {
-            // a later candidate wins only if strictly longer: it must match at `best`
-            const bool can = best == 0 || (best < lim && T[p + best] == T[q + best]);
-            if (can) {
-                l = LZ_MIN;  // the 3-gram is shared by the group
-                const u32 qr = q - tlo;
+            const u32 qr = q - tlo;
+            const u64 d0 = lds8(txt, pr) ^ lds8(txt, qr);
+            if ((d0 & 0xFFFFFFull) == 0) {  // same 3-gram (not just the same hash)
+                if (d0) {
+                    l = (u32)(__ffsll((long long)d0) - 1) >> 3;
+                } else if (best < 8 || (best < lim && T[p + best] == T[q + best])) {
+                    // a longer candidate must match at `best`
+                    l = 8;
 #pragma unroll
-                for (int k = 0; k < LZ_CAP / 8; ++k) {
-                    if (l >= capl) break;
-                    const u64 d = lds8(txt, pr + 3 + 8 * k) ^ lds8(txt, qr + 3 + 8 * k);
-                    if (d) {
-                        l += (u32)(__ffsll((long long)d) - 1) >> 3;
-                        break;
+                    for (int k = 1; k < LZ_CAP / 8; ++k) {
+                        if (l >= capl) break;
+                        const u64 d = lds8(txt, pr + 8 * k) ^ lds8(txt, qr + 8 * k);
+                        if (d) {
+                            l += (u32)(__ffsll((long long)d) - 1) >> 3;
+                            break;
+                        }
+                        l += 8;
                     }
-                    l += 8;
                 }
                 l = min(l, capl);
             }
         }
         // capped candidates extended exactly (up to lim), one at a time by the whole wave
-        u64 longm = __ballot(valid && l >= capl && capl < lim);
+        u64 longm = __ballot(l >= capl && capl < lim);
         while (longm) {
             const u32 j = (u32)__ffsll((long long)longm) - 1;
             const u32 pj = __builtin_amdgcn_readlane(p, j), qj = __builtin_amdgcn_readlane(q, j);
@@ -725,29 +757,15 @@ __device__ void lzl_best(const u8* txt, u32 tlo, const u16* A, const u64* bm, co
             longm &= longm - 1;
             ++nlong;
         }
-        // max length, ties -> smallest lane of the chain (= smallest distance)
-        const u32 lv = valid ? l : 0u;
-        u64 cand = __ballot(lv > best) & GM;
-        if (__ballot(lv >= 64u)) {
-            u32 lm = lv;
-#pragma unroll
-            for (int o = 8; o >= 1; o >>= 1) lm = max(lm, (u32)__shfl_xor(lm, o));
-            const u64 eq = __ballot(lv == lm) & GM;
-            cand = cand ? eq : 0ull;
-        } else {
-#pragma unroll
-            for (int b = 5; b >= 0; --b) {
-                const u64 tb = __ballot((lv >> b) & 1u) & cand;
-                if (tb) cand = tb;
-            }
-        }
-        const u32 wl = cand ? (u32)__ffsll((long long)cand) - 1 : lane;
-        const u32 nl = (u32)__shfl((int)lv, (int)wl), nq = (u32)__shfl((int)q, (int)wl);
-        if (cand) {
-            best = nl;
-            bd = p - nq;
+        // max length, ties -> largest position (= smallest distance): one 28-bit key per
+        // lane (length <= 576 < 2^14, window offset < 2^14), maximised over the DPP row
+        const u32 key = row_max16(l >= (u32)LZ_MIN ? (l << 14) | (q - lo) : 0u);
+        if ((key >> 14) > best) {
+            best = key >> 14;
+            bd = p - (lo + (key & 0x3FFFu));
         }
         if (best >= lim || inwin != GM) go = false;
+        qa = qn;
         k0 -= 16;
     }
     unres = false;
@@ -761,12 +779,14 @@ __device__ void lzl_best(const u8* txt, u32 tlo, const u16* A, const u64* bm, co
     out_dist = bd;
 }
 
-__global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb) {
+__global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
     __shared__ __align__(16) u8 txt[LZL_TXT];
     __shared__ __align__(16) u16 A[LZL_NW];
-    __shared__ __align__(16) u16 B[LZL_NW];
-    __shared__ u32 hist[4][256];
+    // islot of [ilo, he) + head bitmap; the sort's histograms live here before them
+    __shared__ __align__(16) u16 B[LZL_ISL + 4 * ((LZL_NW + 63) / 64)];
     __shared__ u32 sh[4];
+    u32(*hist)[256] = reinterpret_cast<u32(*)[256]>(B);
+    static_assert(sizeof(u32) * 4 * 256 <= sizeof(u16) * LZL_ISL, "histograms alias the islot array");
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const u32 b = blockIdx.x / hpb, h = blockIdx.x - b * hpb;
     const u32 base = z.geo.base(b), end = z.geo.end(b);
@@ -777,6 +797,8 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb) {
     const u32 ilo = hs - base > (u32)LZL_LEAD ? hs - LZL_LEAD : base;
     const u32 hi = min(end, he + (u32)LZL_CAPX);
     const u32 tlo = lo & ~3u;  // LDS origin (dword aligned)
+    u64 t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+    if (z.prof) t0 = wall_clock64();
     {
         const u32 n = hi - tlo;
         if (((uintptr_t)z.text & 3) == 0) {
@@ -794,12 +816,12 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb) {
     const u32 top = min(he, lim3);
     const u32 nw = top > lo ? top - lo : 0u;
     const u8* tw = txt + (lo - tlo);  // window text at window offset 0
+    if (z.prof) t1 = wall_clock64();
     if (nw) {
-        lzl_pass<2>(tw, nullptr, A, nw, hist, sh);
-        lzl_pass<1>(tw, A, B, nw, hist, sh);
-        lzl_pass<0>(tw, B, A, nw, hist, sh);
+        lzl_pass<0, true>(tw, A, nw, hist, sh);
+        lzl_pass<1, false>(tw, A, nw, hist, sh);
     }
-    // islot of [ilo, he) and the group-head bitmap, in the sort scratch B
+    // islot of [ilo, he) and the group-head bitmap
     u16* isl = B;
     u64* bm = reinterpret_cast<u64*>(B + LZL_ISL);
     for (u32 j0 = 0; j0 < nw; j0 += 256) {
@@ -808,12 +830,14 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb) {
         if (j < nw) {
             const u32 x = A[j];
             if (lo + x >= ilo) isl[lo + x - ilo] = (u16)j;
-            head = j == 0 || key3(tw, x) != key3(tw, A[j - 1]);
+            head = j == 0 || hash3(tw, x) != hash3(tw, A[j - 1]);
         }
         const u64 bal = __ballot(head);
         if (lane == 0 && j0 + w * 64 < nw) bm[(j0 >> 6) + w] = bal;
     }
+    if (z.prof) t2 = wall_clock64();
     __syncthreads();
+    if (z.prof) t3 = wall_clock64();
     // 16 chains: chain g of wave w parses chunk cid = 4w + g
     const u32 hl = lane & 15;
     const u32 cid = w * 4 + (lane >> 4);
@@ -822,15 +846,16 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb) {
     const u32 e = has ? min(s + (u32)LZL_CHUNK, end) : 0u;
     const u32 c = b * z.cpb + h * LZL_NCHAIN + cid;
     const u32 lend = has ? min(end, e + (u32)LZL_CAPX) : 0u;
-    u32 q = has ? ((cid == 0 && hs == base) ? s : s - LZL_LEAD) : 0u;
-    u32 ntok = 0, off = 0, nlong = 0, nbuf = 0;
+    u32 q = has ? ((cid == 0 && hs == base) ? s : s - lead) : 0u;
+    u32 ntok = 0, off = 0, nlong = 0, nbuf = 0, nstep = 0, nbatch = 0;
     u32 bpos = 0, blen = 0, bdist = 0, boff = 0;
     bool un = false;
     while (__ballot(has && q < e)) {
+        ++nstep;
         const bool act = has && q < e;
         u32 len, dist;
         bool unres;
-        lzl_best(txt, tlo, A, bm, isl, lo, ilo, act, q, act ? lend - q : 0u, end, len, dist, unres, nlong);
+        lzl_best(txt, tlo, A, bm, isl, lo, ilo, act, q, act ? lend - q : 0u, end, len, dist, unres, nlong, nbatch);
         if (act) {
             if (q >= s) {
                 if (hl == nbuf) {
@@ -868,6 +893,22 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb) {
     }
     nlong = wave_reduce(nlong, OpAddU(), 0u);
     if (lane == 0 && nlong) atomicAdd(z.nlong, nlong);
+    if (z.prof) {
+        // per-phase wall clock (100 MHz) summed over workgroups; wave loop trip counts
+        if (lane == 0) {
+            atomicAdd(z.prof + 4, (u64)nstep);
+            atomicAdd(z.prof + 5, (u64)nbatch);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const u64 t4 = wall_clock64();
+            atomicAdd(z.prof + 0, t1 - t0);
+            atomicAdd(z.prof + 1, t2 - t1);
+            atomicAdd(z.prof + 2, t3 - t2);
+            atomicAdd(z.prof + 3, t4 - t3);
+            atomicAdd(z.prof + 6, (u64)1);
+        }
+    }
 }
 
 // Exact longest match at q (PY:1686-1708 semantics: ascending distance, strictly longer
@@ -1127,7 +1168,8 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
             // text window (LZL_NW + LZL_CAPX bytes per 4 KiB home: ~2.1 B per position) +
             // 16 B per token (added by the caller once the token count is known)
             KScope k(kt, KT_LZPARSE, "k_lz_local", z.geo.N * 2);
-            k_lz_local<<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb);
+            static const u32 lead = getenv("KOLM_LZ_LEAD") ? std::min<u32>(atoi(getenv("KOLM_LZ_LEAD")), LZL_LEAD) : LZL_LEAD;
+            k_lz_local<<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb, lead);
         }
         {
             KScope k(kt, KT_LZPARSE, "k_lz_stitch", (u64)z.cpb * z.geo.nb * 16);

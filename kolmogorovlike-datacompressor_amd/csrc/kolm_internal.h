@@ -357,6 +357,7 @@ struct LzArgs {
     u32 cpb;           // chunks per block
     u32 cshift;        // chunk = 1 << cshift bytes (LZ_CHUNK or LZL_CHUNK)
     u32* nfix;         // [1] fix-up tokens computed by the stitch (statistics)
+    u64* prof;         // [8] optional k_lz_local phase clocks (KOLM_LZ_PROF=1), null = off
 };
 bool lz_local();       // KOLM_LZ_LOCAL (default 1): workgroup-local index path
 void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr);
