@@ -44,6 +44,9 @@ LIMITER = {
                        "candidate search starts where the previous token ended)",
     "k_lz_spec<false>": "latency: the dependent greedy-parse chain",
     "k_lz_spec2": "latency: the dependent greedy-parse chains (two 2 KiB chunks per wave, one per half)",
+    "k_lz_local": "LDS latency / issue: in-LDS 3-gram index + 16 dependent greedy-parse chains per workgroup "
+                  "(4 waves/SIMD, LDS-limited); HBM traffic is only the text window and the token records; "
+                  "it runs beside the sort stream at lower priority, so its overlapped duration is inflated",
     "k_repair": "latency: one workgroup per block, barrier-separated batches of dependent global accesses",
 }
 MB = 1e6
