@@ -385,7 +385,7 @@ def main():
                        "full_candidates": full,
                        "cdc_mode": cdc,
                        "device_ms": {k: round(s0[k], 2) for k in ("ms_total", "ms_sa", "ms_lz", "ms_entropy", "ms_emit")},
-                       "rounds": [s0["lin_rounds"], s0["cyc_rounds"]],
+                       "cyclic_rounds": s0["cyc_rounds"],
                        "lz77": {"tokens": s0["lz_tokens"], "stitch_fixups": s0["lz_fix"],
                                 "long_extensions": s0["lz_long"]},
                        "pipeline_roofline": pipe,

@@ -64,8 +64,8 @@ typedef struct kolm_ctx kolm_ctx;
 #define KOLM_KT_KEYGEN 1     /* k_keypos, k_keygen_small, k_keygen_large */
 #define KOLM_KT_MSD 2        /* k_msd_hist, k_msd_scan, k_msd_scatter, k_copy_back */
 #define KOLM_KT_SMALLSORT 3  /* k_small_sort<1..11>, k_single, k_finalize_eq */
-#define KOLM_KT_LSD 4        /* per-block LSD radix passes: k_g3_* (3-gram index), k_r0_* (round 0) */
-#define KOLM_KT_LZPARSE 5    /* k_lz_spec, k_lz_stitch */
+#define KOLM_KT_LSD 4        /* per-block LSD radix passes of the cyclic round 0: k_lsd_*, k_r0_* */
+#define KOLM_KT_LZPARSE 5    /* k_lz_local (LDS 3-gram index + speculative parse), k_lz_stitch */
 #define KOLM_KT_MTF 6        /* k_mtf_summary, k_mtf_compose, k_mtf_replay */
 #define KOLM_KT_SIZES 7      /* k_sizes, k_mdl, k_offsets */
 #define KOLM_KT_EMIT 8       /* emission kernels */
@@ -82,9 +82,9 @@ typedef struct kolm_ktime {
 
 /* Per-batch statistics reported by the encode entry points. */
 typedef struct kolm_stats {
-    uint32_t lin_rounds;      /* prefix-doubling rounds, linear suffix order (max over blocks) */
+    uint32_t lin_rounds;      /* linear suffix-order rounds: 0 (Lyndon factors by Duval, LZ77 index in LDS) */
     uint32_t cyc_rounds;      /* prefix-doubling rounds, cyclic omega-order (max over blocks) */
-    uint64_t lin_active;      /* sum over rounds of active (unsorted) positions, linear */
+    uint64_t lin_active;      /* 0 (kept for ABI stability) */
     uint64_t cyc_active;      /* same, cyclic */
     uint64_t lz_tokens;       /* LZ77 tokens over all blocks */
     uint64_t lz_long;         /* LZ77 parse positions that needed exact long-match resolution */

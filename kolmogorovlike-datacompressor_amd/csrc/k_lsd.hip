@@ -1,67 +1,40 @@
-// Per-block stable LSD radix passes (gfx950) and their two users:
-//   * the 3-gram candidate index for LZ77 (launch_gram3);
-//   * round 0 of the cyclic suffix sort (launch_round0): positions grouped by the first
-//     4 characters of their rotation, ranks + next-round segments (k_sort.hip).
-//
-// 3-gram index: every block's positions grouped by their 3-byte prefix, positions
-// ascending inside a group.
-//
-// The reference's LZ77 (PY:1711-1763) finds, for each position, the longest earlier
-// match inside the 4096-byte window by walking previous occurrences of the current
-// 3-byte prefix (hash chain, nearest first).  Here the chain is materialised as a sorted
-// array: SA3 = the block's positions stably sorted by their 24-bit 3-gram, so the
-// candidates of p are the contiguous slots idx3[p]-1, idx3[p]-2, ... down to the group
-// start gs3[p] (ascending distance).  Positions with fewer than 3 bytes left in the
-// block (the last two) cannot start a match and become singleton groups in the block's
-// last two slots.  Group ORDER is irrelevant to LZ77; only the grouping and the
-// position order inside a group are used.
-//
-// Three stable LSD passes of 8 bits (c2, c1, c0) per block with 4096-element tiles:
-//   hist (per-wave LDS histograms) -> per-block scan over (digit, tile) -> stable scatter
-// (wave ballot ranking), then group starts by a per-block max-scan of group heads.
-// No host synchronisation: the whole index is a fixed sequence of launches that runs on
-// its own stream beside the Lyndon factorisation and the cyclic suffix sort.
+// Round 0 of the cyclic suffix sort (gfx950): every block's positions stably sorted by the
+// first 4 characters of their rotation (4 LSD passes of 8 bits, 4096-element tiles:
+// per-wave LDS histograms -> per-block scan over (digit, tile) -> stable scatter with wave
+// ballot ranking), then group starts, ranks and the next round's segments (k_sort.hip).
+// No host synchronisation: a fixed sequence of launches on the sort stream.
 #include "kolm_internal.h"
 
 namespace kolm {
 
 namespace {
 
-constexpr u32 G3T = 4096;          // elements per tile
-constexpr u32 G3PT = G3T / WG;     // 16 per thread
+constexpr u32 LSD_T = 4096;          // elements per tile
+constexpr u32 LSD_PT = LSD_T / WG;     // 16 per thread
 
-struct G3Geom {
+struct LsdGeom {
     Geom geo;
-    u32 tpb;    // tiles per block
-    bool full;  // tiles cover [base, end) (slots) instead of the full-3-gram region
-    __device__ inline u32 fend(u32 b) const {
-        const u32 s = geo.base(b), e = geo.end(b);
-        return e - s >= 2 ? e - 2 : s;
-    }
+    u32 tpb;  // tiles per block
     __device__ inline bool range(u32 t, u32& lo, u32& hi, u32& b) const {
         b = t / tpb;
         const u32 k = t - b * tpb;
-        lo = geo.base(b) + k * G3T;
-        const u32 e = full ? geo.end(b) : fend(b);
-        hi = min(lo + G3T, e);
+        lo = geo.base(b) + k * LSD_T;
+        const u32 e = geo.end(b);
+        hi = min(lo + LSD_T, e);
         return lo < e;
     }
 };
-
-__device__ inline u32 key24(const u8* t, u32 p) {
-    return ((u32)t[p] << 16) | ((u32)t[p + 1] << 8) | (u32)t[p + 2];
-}
 
 template <int P>
 __device__ inline u32 digit(u32 key) {
     return (key >> (8 * P)) & 255u;
 }
 
-// where a pass reads its (key, position) pairs
-enum Src { SRC_TEXT3 = 0, SRC_KP = 1, SRC_PAIR = 2 };
+// where a pass reads its (key, position) pairs: keys by position (first pass) or pairs
+enum Src { SRC_KP = 1, SRC_PAIR = 2 };
 
 template <int P, int SRC>
-__global__ __launch_bounds__(WG) void k_g3_hist(G3Geom g, const u8* text, const u32* K, u32* hist) {
+__global__ __launch_bounds__(WG) void k_lsd_hist(LsdGeom g, const u32* K, u32* hist) {
     __shared__ u32 h[WG / 64][256];
     const u32 tid = threadIdx.x, w = tid >> 6;
 #pragma unroll
@@ -71,7 +44,7 @@ __global__ __launch_bounds__(WG) void k_g3_hist(G3Geom g, const u8* text, const 
     if (g.range(xcd_tile(), lo, hi, b)) {
 #pragma unroll 4
         for (u32 i = lo + tid; i < hi; i += WG) {
-            const u32 d = SRC == SRC_TEXT3 ? (u32)text[i + 2 - P] : digit<P>(K[i]);
+            const u32 d = digit<P>(K[i]);
             atomicAdd(&h[w][d], 1u);
         }
     }
@@ -80,7 +53,7 @@ __global__ __launch_bounds__(WG) void k_g3_hist(G3Geom g, const u8* text, const 
 }
 
 // hist[t][d] -> absolute destination of the first element of digit d in tile t.
-__global__ __launch_bounds__(WG) void k_g3_scan(G3Geom g, u32* hist) {
+__global__ __launch_bounds__(WG) void k_lsd_scan(LsdGeom g, u32* hist) {
     __shared__ u32 sh[WG / 64];
     const u32 b = blockIdx.x, d = threadIdx.x, lane = d & 63, w = d >> 6;
     const u64 t0 = (u64)b * g.tpb;
@@ -115,9 +88,9 @@ __global__ __launch_bounds__(WG) void k_g3_scan(G3Geom g, u32* hist) {
 
 // Stable scatter of one tile by digit P: element order e = j*WG + tid; each wave ranks
 // its 64 elements per digit with ballots, per-wave counts are combined in (j, wave)
-// order.  P == 0 reads positions in order and builds the keys from the text.
+// order.  SRC_KP reads the keys by position (positions implicit).
 template <int P, int SRC>
-__global__ __launch_bounds__(WG) void k_g3_scatter(G3Geom g, const u8* text, const u32* Kin, const u32* Pin,
+__global__ __launch_bounds__(WG) void k_lsd_scatter(LsdGeom g, const u32* Kin, const u32* Pin,
                                                    u32* Kout, u32* Pout, const u32* hist) {
     __shared__ u32 wcnt[WG / 64][256];
     __shared__ u32 running[256];
@@ -129,15 +102,12 @@ __global__ __launch_bounds__(WG) void k_g3_scatter(G3Geom g, const u8* text, con
     for (int i = 0; i < WG / 64; ++i) wcnt[i][tid] = 0;
     __syncthreads();
     const u64 lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (u32 j = 0; j < G3PT; ++j) {
+    for (u32 j = 0; j < LSD_PT; ++j) {
         const u32 i = lo + j * WG + tid;
         const bool valid = i < hi;
         u32 key = 0, pos = 0, dg = 0;
         if (valid) {
-            if (SRC == SRC_TEXT3) {
-                key = key24(text, i);
-                pos = i;
-            } else if (SRC == SRC_KP) {
+            if (SRC == SRC_KP) {
                 key = Kin[i];
                 pos = i;
             } else {
@@ -176,29 +146,8 @@ __global__ __launch_bounds__(WG) void k_g3_scatter(G3Geom g, const u8* text, con
 
 __device__ inline u32 wave_max(u32 v) { return wave_reduce(v, OpMaxU(), 0u); }
 
-// slot g starts a group: first slot of the block, a tail slot, or a new 3-gram
-__device__ inline bool g3_head(const G3Geom& g, const u32* K, u32 slot, u32 base, u32 fe) {
-    return slot == base || slot >= fe || K[slot] != K[slot - 1];
-}
-
-// per slot tile: last group head (0 if none)
-__global__ __launch_bounds__(WG) void k_g3_tile_heads(G3Geom g, const u32* K, u32* tmax) {
-    __shared__ u32 sh[WG / 64];
-    u32 lo, hi, b;
-    u32 mx = 0;
-    if (g.range(xcd_tile(), lo, hi, b)) {
-        const u32 base = g.geo.base(b), fe = g.fend(b);
-        for (u32 i = lo + threadIdx.x; i < hi; i += WG)
-            if (g3_head(g, K, i, base, fe)) mx = max(mx, i);
-    }
-    mx = wave_max(mx);
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = mx;
-    __syncthreads();
-    if (threadIdx.x == 0) tmax[xcd_tile()] = max(max(sh[0], sh[1]), max(sh[2], sh[3]));
-}
-
 // per block: exclusive max over its tiles (one workgroup per block)
-__global__ __launch_bounds__(WG) void k_g3_tiles_scan(const u32* in, u32* out, u32 tpb) {
+__global__ __launch_bounds__(WG) void k_tiles_max_scan(const u32* in, u32* out, u32 tpb) {
     __shared__ u32 sh[WG / 64];
     __shared__ u32 edge;
     const u32 b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -222,11 +171,11 @@ __global__ __launch_bounds__(WG) void k_g3_tiles_scan(const u32* in, u32* out, u
 
 // the thread's 16 consecutive words X[i0 .. i0+15] (0 past hi): four 16-byte loads when
 // aligned and whole (the 16 scalar loads per array were 48 read instructions per wave)
-__device__ inline void load16(const u32* X, u32 i0, u32 hi, u32 (&v)[G3PT]) {
-    if ((i0 & 3) == 0 && i0 + G3PT <= hi) {
+__device__ inline void load16(const u32* X, u32 i0, u32 hi, u32 (&v)[LSD_PT]) {
+    if ((i0 & 3) == 0 && i0 + LSD_PT <= hi) {
         const uint4* p = reinterpret_cast<const uint4*>(X + i0);
 #pragma unroll
-        for (int q = 0; q < (int)G3PT / 4; ++q) {
+        for (int q = 0; q < (int)LSD_PT / 4; ++q) {
             const uint4 t = p[q];
             v[4 * q] = t.x;
             v[4 * q + 1] = t.y;
@@ -235,52 +184,7 @@ __device__ inline void load16(const u32* X, u32 i0, u32 hi, u32 (&v)[G3PT]) {
         }
     } else {
 #pragma unroll
-        for (u32 e = 0; e < G3PT; ++e) v[e] = i0 + e < hi ? X[i0 + e] : 0u;
-    }
-}
-
-// per slot: group start, inverse permutation; tail slots hold their own position
-__global__ __launch_bounds__(WG) void k_g3_final(G3Geom g, const u32* K, u32* SA3, const u32* tcarry, uint2* ig3) {
-    __shared__ u32 sh[WG / 64];
-    u32 lo, hi, b;
-    if (!g.range(blockIdx.x, lo, hi, b)) return;
-    const u32 base = g.geo.base(b), fe = g.fend(b);
-    const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const u32 i0 = lo + threadIdx.x * G3PT;
-    u32 kv[G3PT], sv[G3PT];
-    load16(K, i0, hi, kv);
-    load16(SA3, i0, hi, sv);
-    u32 kprev = (i0 > base && i0 < hi) ? K[i0 - 1] : 0u;
-    u32 hd[G3PT];
-    u32 loc = 0;
-#pragma unroll
-    for (u32 e = 0; e < G3PT; ++e) {
-        const u32 i = i0 + e;
-        // g3_head: first slot of the block, a tail slot, or a new 3-gram
-        hd[e] = (i < hi && (i == base || i >= fe || kv[e] != kprev)) ? 1u : 0u;
-        kprev = kv[e];
-        if (hd[e]) loc = max(loc, i);
-    }
-    const u32 incl = wave_incl_scan(loc, OpMaxU(), 0u);
-    const u32 ex = KOLM_DPP(0u, incl, DPP_WAVE_SHR1, 0xF);
-    if (lane == 63) sh[w] = incl;
-    __syncthreads();
-    u32 run = max(tcarry[blockIdx.x], ex);
-    for (u32 i = 0; i < w; ++i) run = max(run, sh[i]);
-#pragma unroll
-    for (u32 e = 0; e < G3PT; ++e) {
-        const u32 i = i0 + e;
-        if (i < hi) {
-            if (hd[e]) run = i;
-            u32 p;
-            if (i >= fe) {
-                p = i;
-                SA3[i] = i;
-            } else {
-                p = sv[e];
-            }
-            ig3[p] = make_uint2(i, run);  // one 8-byte scattered store
-        }
+        for (u32 e = 0; e < LSD_PT; ++e) v[e] = i0 + e < hi ? X[i0 + e] : 0u;
     }
 }
 
@@ -297,7 +201,7 @@ __device__ inline bool r0_head(const u32* K, u32 g, u32 base) { return g == base
 
 __device__ inline u32 wave_min(u32 v) { return wave_reduce(v, OpMinU(), BIG); }
 
-__global__ __launch_bounds__(WG) void k_r0_tile_heads(G3Geom g, const u32* K, u32* tmax, u32* tmin) {
+__global__ __launch_bounds__(WG) void k_r0_tile_heads(LsdGeom g, const u32* K, u32* tmax, u32* tmin) {
     __shared__ u32 s1[WG / 64], s2[WG / 64];
     u32 lo, hi, b;
     u32 mx = 0, mn = BIG;
@@ -346,7 +250,7 @@ __global__ __launch_bounds__(WG) void k_r0_tiles_rscan(const u32* in, u32* out, 
     }
 }
 
-__global__ __launch_bounds__(WG) void k_r0_final(G3Geom g, const u32* K, const u32* SA, const u32* cmax,
+__global__ __launch_bounds__(WG) void k_r0_final(LsdGeom g, const u32* K, const u32* SA, const u32* cmax,
                                                  const u32* cmin, u32* RK, Seg* next, u32* next_cnt,
                                                  u32* blk_split) {
     __shared__ u32 sh[WG / 64], sh2[WG / 64], sh3[WG / 64];
@@ -356,15 +260,15 @@ __global__ __launch_bounds__(WG) void k_r0_final(G3Geom g, const u32* K, const u
     const u32 base = g.geo.base(b), bend = g.geo.end(b);
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid == 0) anysplit = 0;
-    const u32 i0 = lo + tid * G3PT;
-    u32 kv[G3PT], sv[G3PT];
+    const u32 i0 = lo + tid * LSD_PT;
+    u32 kv[LSD_PT], sv[LSD_PT];
     load16(K, i0, hi, kv);
     load16(SA, i0, hi, sv);
     u32 kprev = (i0 > base && i0 < hi) ? K[i0 - 1] : 0u;
-    bool hd[G3PT];
+    bool hd[LSD_PT];
     u32 lmax = 0, lmin = BIG;
 #pragma unroll
-    for (u32 e = 0; e < G3PT; ++e) {
+    for (u32 e = 0; e < LSD_PT; ++e) {
         const u32 i = i0 + e;
         hd[e] = i < hi && (i == base || kv[e] != kprev);  // r0_head
         kprev = kv[e];
@@ -388,7 +292,7 @@ __global__ __launch_bounds__(WG) void k_r0_final(G3Geom g, const u32* K, const u
     // ranks
     bool split = false;
 #pragma unroll
-    for (u32 e = 0; e < G3PT; ++e) {
+    for (u32 e = 0; e < LSD_PT; ++e) {
         const u32 i = i0 + e;
         if (i < hi) {
             if (hd[e]) {
@@ -399,10 +303,10 @@ __global__ __launch_bounds__(WG) void k_r0_final(G3Geom g, const u32* K, const u
         }
     }
     // group lengths (backwards) and next-round segments, one global atomic per workgroup
-    u32 len[G3PT];
+    u32 len[LSD_PT];
     u32 nseg = 0;
 #pragma unroll
-    for (int e = G3PT - 1; e >= 0; --e) {
+    for (int e = LSD_PT - 1; e >= 0; --e) {
         const u32 i = i0 + e;
         len[e] = 0;
         if (hd[e]) {
@@ -425,125 +329,68 @@ __global__ __launch_bounds__(WG) void k_r0_final(G3Geom g, const u32* K, const u
     __syncthreads();
     off += wbase;
 #pragma unroll
-    for (u32 e = 0; e < G3PT; ++e)
+    for (u32 e = 0; e < LSD_PT; ++e)
         if (len[e] >= 2) next[off++] = Seg{i0 + e, len[e]};
 }
 
 }  // namespace
 
-u32 lsd_tiles(const Geom& geo) { return (geo.bs + G3T - 1) / G3T * geo.nb; }
+u32 lsd_tiles(const Geom& geo) { return (geo.bs + LSD_T - 1) / LSD_T * geo.nb; }
 
 // Round 0 of the cyclic sort.  KP = 4-character keys by position (k_keypos).
 // Passes: (KP, p) -> (K2, SA) -> (K22, SA2) -> (KP, RK) -> (K2, SA); then ranks/segments.
 void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s,
                    KTimer* kt) {
     if (!geo.N) return;
-    G3Geom g{geo, (geo.bs + G3T - 1) / G3T, true};
+    LsdGeom g{geo, (geo.bs + LSD_T - 1) / LSD_T};
     const u32 nt = g.tpb * geo.nb;
     const u64 N = geo.N, H = (u64)nt * 1024;  // H: per-tile histogram bytes
     {
-        KScope k(kt, KT_LSD, "k_g3_hist<0, 1>", 4 * N + H);
-        k_g3_hist<0, SRC_KP><<<nt, WG, 0, s>>>(g, nullptr, t.KP, t.hist);
+        KScope k(kt, KT_LSD, "k_lsd_hist<0, 1>", 4 * N + H);
+        k_lsd_hist<0, SRC_KP><<<nt, WG, 0, s>>>(g, t.KP, t.hist);
     }
     {
-        KScope k(kt, KT_LSD, "k_g3_scan", 3 * H);
-        k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
+        KScope k(kt, KT_LSD, "k_lsd_scan", 3 * H);
+        k_lsd_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
     }
     {
-        KScope k(kt, KT_LSD, "k_g3_scatter<0, 1>", 12 * N + H);
-        k_g3_scatter<0, SRC_KP><<<nt, WG, 0, s>>>(g, nullptr, t.KP, nullptr, t.K2, t.SA, t.hist);
+        KScope k(kt, KT_LSD, "k_lsd_scatter<0, 1>", 12 * N + H);
+        k_lsd_scatter<0, SRC_KP><<<nt, WG, 0, s>>>(g, t.KP, nullptr, t.K2, t.SA, t.hist);
     }
     u32* kin[3] = {t.K2, t.K22, t.KP};
     u32* pin[3] = {t.SA, t.SA2, t.RK};
     u32* kout[3] = {t.K22, t.KP, t.K2};
     u32* pout[3] = {t.SA2, t.RK, t.SA};
-    static const char* const hn[3] = {"k_g3_hist<1, 2>", "k_g3_hist<2, 2>", "k_g3_hist<3, 2>"};
-    static const char* const sn[3] = {"k_g3_scatter<1, 2>", "k_g3_scatter<2, 2>", "k_g3_scatter<3, 2>"};
+    static const char* const hn[3] = {"k_lsd_hist<1, 2>", "k_lsd_hist<2, 2>", "k_lsd_hist<3, 2>"};
+    static const char* const sn[3] = {"k_lsd_scatter<1, 2>", "k_lsd_scatter<2, 2>", "k_lsd_scatter<3, 2>"};
     for (int q = 0; q < 3; ++q) {
         {
             KScope k(kt, KT_LSD, hn[q], 4 * N + H);
-            if (q == 0) k_g3_hist<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, kin[q], t.hist);
-            if (q == 1) k_g3_hist<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, kin[q], t.hist);
-            if (q == 2) k_g3_hist<3, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, kin[q], t.hist);
+            if (q == 0) k_lsd_hist<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, kin[q], t.hist);
+            if (q == 1) k_lsd_hist<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, kin[q], t.hist);
+            if (q == 2) k_lsd_hist<3, SRC_PAIR><<<nt, WG, 0, s>>>(g, kin[q], t.hist);
         }
         {
-            KScope k(kt, KT_LSD, "k_g3_scan", 3 * H);
-            k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
+            KScope k(kt, KT_LSD, "k_lsd_scan", 3 * H);
+            k_lsd_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
         }
         {
             KScope k(kt, KT_LSD, sn[q], 16 * N + H);
-            if (q == 0) k_g3_scatter<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, kin[q], pin[q], kout[q], pout[q], t.hist);
-            if (q == 1) k_g3_scatter<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, kin[q], pin[q], kout[q], pout[q], t.hist);
-            if (q == 2) k_g3_scatter<3, SRC_PAIR><<<nt, WG, 0, s>>>(g, nullptr, kin[q], pin[q], kout[q], pout[q], t.hist);
+            if (q == 0) k_lsd_scatter<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, kin[q], pin[q], kout[q], pout[q], t.hist);
+            if (q == 1) k_lsd_scatter<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, kin[q], pin[q], kout[q], pout[q], t.hist);
+            if (q == 2) k_lsd_scatter<3, SRC_PAIR><<<nt, WG, 0, s>>>(g, kin[q], pin[q], kout[q], pout[q], t.hist);
         }
     }
     {
         KScope k(kt, KT_LSD, "k_r0_tile_heads", 4 * N);
         k_r0_tile_heads<<<nt, WG, 0, s>>>(g, t.K2, t.tmax, t.tmin);
-        k_g3_tiles_scan<<<geo.nb, WG, 0, s>>>(t.tmax, t.cmax, g.tpb);
+        k_tiles_max_scan<<<geo.nb, WG, 0, s>>>(t.tmax, t.cmax, g.tpb);
         k_r0_tiles_rscan<<<geo.nb, WG, 0, s>>>(t.tmin, t.cmin, g.tpb);
     }
     {
         // K 4 + SA 4 read, RK 4 scattered (+ 8 B per new segment)
         KScope k(kt, KT_LSD, "k_r0_final", 12 * N);
         k_r0_final<<<nt, WG, 0, s>>>(g, t.K2, t.SA, t.cmax, t.cmin, t.RK, next, next_cnt, blk_split);
-    }
-}
-
-void launch_gram3(const Geom& geo, const u8* text, const G3Bufs& t, hipStream_t s, KTimer* kt) {
-    if (!geo.N) return;
-    G3Geom g{geo, (geo.bs + G3T - 1) / G3T, false};
-    const u32 nt = g.tpb * geo.nb;
-    const u64 N = geo.N, H = (u64)nt * 1024;
-    // pass c2: text -> (Ka, Pa); c1: -> (Kb, Pb); c0: -> (Ka, SA3); Pa/Pb live in ig3 (free until final)
-    u32* Pa = reinterpret_cast<u32*>(t.ig3);
-    u32* Pb = Pa + geo.N;
-    {
-        KScope k(kt, KT_LSD, "k_g3_hist<0, 0>", N + H);
-        k_g3_hist<0, SRC_TEXT3><<<nt, WG, 0, s>>>(g, text, nullptr, t.hist);
-    }
-    {
-        KScope k(kt, KT_LSD, "k_g3_scan", 3 * H);
-        k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
-    }
-    {
-        KScope k(kt, KT_LSD, "k_g3_scatter<0, 0>", 9 * N + H);  // text 1 + (key, pos) 8
-        k_g3_scatter<0, SRC_TEXT3><<<nt, WG, 0, s>>>(g, text, nullptr, nullptr, t.Ka, Pa, t.hist);
-    }
-    {
-        KScope k(kt, KT_LSD, "k_g3_hist<1, 2>", 4 * N + H);
-        k_g3_hist<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Ka, t.hist);
-    }
-    {
-        KScope k(kt, KT_LSD, "k_g3_scan", 3 * H);
-        k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
-    }
-    {
-        KScope k(kt, KT_LSD, "k_g3_scatter<1, 2>", 16 * N + H);
-        k_g3_scatter<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Ka, Pa, t.Kb, Pb, t.hist);
-    }
-    {
-        KScope k(kt, KT_LSD, "k_g3_hist<2, 2>", 4 * N + H);
-        k_g3_hist<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Kb, t.hist);
-    }
-    {
-        KScope k(kt, KT_LSD, "k_g3_scan", 3 * H);
-        k_g3_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
-    }
-    {
-        KScope k(kt, KT_LSD, "k_g3_scatter<2, 2>", 16 * N + H);
-        k_g3_scatter<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, text, t.Kb, Pb, t.Ka, t.SA3, t.hist);
-    }
-    G3Geom gs{geo, g.tpb, true};
-    {
-        KScope k(kt, KT_LSD, "k_g3_tile_heads", 4 * N);
-        k_g3_tile_heads<<<nt, WG, 0, s>>>(gs, t.Ka, t.tmax);
-        k_g3_tiles_scan<<<geo.nb, WG, 0, s>>>(t.tmax, t.tcarry, g.tpb);
-    }
-    {
-        // K 4 + SA3 4 read, (slot, group start) 8 scattered
-        KScope k(kt, KT_LSD, "k_g3_final", 16 * N);
-        k_g3_final<<<nt, WG, 0, s>>>(gs, t.Ka, t.SA3, t.tcarry, t.ig3);
     }
 }
 

@@ -6,22 +6,18 @@
 // block[pos-d:] (unbounded); a strictly longer match wins (ties -> smallest d);
 // best >= 3 emits [1][ULEB len][ULEB dist], otherwise [0][byte].
 //
-// GPU formulation (bit-exact):
-//   * any match >= 3 starts with an equal 3-gram, so the candidates of p are exactly the
-//     earlier members of p's 3-gram group inside the window.  Round 0 of the linear
-//     suffix sort (k_sort.hip) sorts positions by (3-gram, position): in that array SA3
-//     p's candidates are the CONTIGUOUS slots idx3[p]-1, idx3[p]-2, ... down to the group
-//     start gs3[p], in ascending distance — no pointer chasing;
-//   * matches are computed lazily, only at positions on the parse path, by a whole wave:
-//     64 lanes score 64 candidates at once (capped byte compare; later batches first
-//     test whether a candidate can beat the current best at offset `best`); the
-//     winner is a wave max-reduction of (length, -distance).  Candidates reaching the
-//     cap are extended exactly with 64-lane compares (no length limit, as PY);
-//   * the greedy parse is parallel by speculation: k_lz_spec parses every LZ_CHUNK-byte
-//     chunk with its own wave from the chunk start; k_lz_stitch walks, per block, the
-//     TRUE path from each chunk's real entry only until it lands on a position of that
-//     chunk's speculative path (a token depends on its position only, so both parses
-//     coincide from there); greedy parses re-synchronise within a few tokens;
+// GPU formulation (bit-exact), three kernels:
+//   * k_lz_local: one workgroup per 4 KiB "home" of a block.  Any match >= 3 starts with
+//     an equal 3-gram, so p's candidates are the earlier positions of its 3-gram inside
+//     [p - 4096, p).  The workgroup copies the window [home - 4096 - lead-in, home end)
+//     to LDS, buckets its positions by a 9-bit 3-gram hash with one stable counting-sort
+//     pass in LDS, and parses the home with 16 speculative chains (16 lanes = 16
+//     candidates at a time, nearest first; max length, ties -> nearest);
+//   * k_lz_stitch_l: per block, the TRUE path over the chunk summaries: a chunk whose
+//     first recorded token is the true entry is taken whole; otherwise exact tokens by a
+//     brute-force window search until the true path lands on a recorded token (greedy
+//     parses re-synchronise within a few tokens; the lead-in makes that happen before
+//     the chunk start: 54 off-path tokens per 56 M on 256 MiB of text);
 //   * k_lz_emit: one thread per token slot writes its bytes at its final offset.
 #include <algorithm>
 #include <cstdlib>
@@ -43,11 +39,7 @@ __device__ inline u32 uleb_len(u32 v) {
 
 __device__ inline u32 tok_bytes(u32 len, u32 dist) { return len ? 1 + uleb_len(len) + uleb_len(dist) : 2; }
 
-// Text accessors: global memory, or an LDS copy of [lo, hi) with global fallback outside.
-struct GText {
-    const u8* g;
-    __device__ inline u8 operator[](u32 x) const { return g[x]; }
-};
+// Text accessor: an LDS copy of [lo, hi) with global memory outside it.
 struct LText {
     const u8* g;
     const u8* l;
@@ -82,495 +74,8 @@ __device__ inline u64 lds8(const u8* l, u32 x) {
     return ((u64)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
 }
 
-template <class T>
-struct IsLds {
-    static constexpr bool value = false;
-};
-template <>
-struct IsLds<LText> {
-    static constexpr bool value = true;
-};
-
-// Longest match at p (uniform across the wave).  i = idx3[p], gs = gs3[p].
-template <class T>
-__device__ void best_match(const LzArgs& z, const T& t, u32 p, u32 end, u32 i, u32 gs, u32& out_len,
-                           u32& out_dist, u32& nlong) {
-    const u32 lane = threadIdx.x & 63;
-    u32 best = 0, bd = 0;
-    if (p + (u32)LZ_MIN <= end && i > gs) {
-        const u32 maxl = end - p;
-        const u32 capl = min((u32)LZ_CAP, maxl);
-        // LDS window: capped compares 8 bytes at a time with p's bytes hoisted
-        bool wide = false;
-        if constexpr (IsLds<T>::value) wide = p >= t.lo && p + capl + 11 <= t.hi;
-        u32 k0 = i;  // candidates this batch: slots k0-1-lane
-        for (;;) {
-            bool valid = k0 > gs + lane;
-            const u32 q = valid ? z.SA3[k0 - 1 - lane] : 0u;
-            valid = valid && (p - q <= (u32)LZ_WINDOW);
-            const u64 inwin = __ballot(valid);
-            if (!inwin) break;
-            u32 l = 0;
-            if (valid) {
-                // a later candidate wins only if strictly longer: it must match at `best`
-                const bool can = best == 0 || (best < maxl && t[p + best] == t[q + best]);
-                if (can) {
-                    l = LZ_MIN;  // the 3-gram is shared by the group
-                    bool done = false;
-                    if constexpr (IsLds<T>::value) {
-                        if (wide) {
-                            // q >= window start (candidates lie inside the window), q < p
-#pragma unroll
-                            for (int k = 0; k < LZ_CAP / 8; ++k) {
-                                if (l >= capl) break;
-                                // p's bytes loaded lazily: most candidates differ in the first 8
-                                const u64 d = lds8(t.l, p - t.lo + 3 + 8 * k) ^ lds8(t.l, q - t.lo + 3 + 8 * k);
-                                if (d) {
-                                    l += (u32)(__ffsll((long long)d) - 1) >> 3;
-                                    break;
-                                }
-                                l += 8;
-                            }
-                            l = min(l, capl);
-                            done = true;
-                        }
-                    }
-                    if (!done)
-                        while (l < capl && t[p + l] == t[q + l]) ++l;
-                }
-            }
-            u64 longm = __ballot(valid && l >= capl && capl < maxl);
-            while (longm) {
-                const u32 j = __ffsll((long long)longm) - 1;
-                const u32 qj = __builtin_amdgcn_readlane(q, j);
-                const u32 lj = wave_lcp(t, p, qj, capl, maxl);
-                if (lane == j) l = lj;
-                longm &= longm - 1;
-                ++nlong;
-            }
-            // max length, ties -> smallest lane (= smallest distance).  Lengths below 64
-            // (all but extended matches): bit-serial over ballots, no cross-lane data
-            // movement (__shfl_xor is an LDS permute + address math per step)
-            const u32 lv = valid ? l : 0u;
-            u64 cand = __ballot(lv > best);
-            if (cand) {
-                if (__ballot(lv >= 64u)) {
-                    u32 lm = lv;
-#pragma unroll
-                    for (int o = 32; o >= 1; o >>= 1) lm = max(lm, (u32)__shfl_xor(lm, o));
-                    cand = __ballot(lv == lm);
-                } else {
-#pragma unroll
-                    for (int b = 5; b >= 0; --b) {
-                        const u64 tb = __ballot((lv >> b) & 1u) & cand;
-                        if (tb) cand = tb;
-                    }
-                }
-                const u32 wl = (u32)__ffsll((long long)cand) - 1;
-                best = __builtin_amdgcn_readlane(lv, wl);
-                bd = p - __builtin_amdgcn_readlane(q, wl);
-            }
-            if (best >= maxl || inwin != ~0ull) break;
-            k0 -= 64;
-        }
-    }
-    if (best < (u32)LZ_MIN) {
-        best = 0;
-        bd = 0;
-    }
-    out_len = best;
-    out_dist = bd;
-}
-
-// Speculative parse of one chunk per wave; the 4 waves of a workgroup take 4 consecutive
-// chunks and share one LDS copy of their text windows [first chunk - 4096, last chunk
-// end) (20 KiB): with 32 waves per CU each on its own window in global memory the windows
-// overflow L2 and every candidate compare re-fetches its line.  8 waves per SIMD (<= 64
-// VGPRs, 8 x 20 KiB of LDS per CU): the parse chain is latency-bound, occupancy is speed.
-constexpr u32 LZ_LWIN = LZ_WINDOW + 4 * LZ_CHUNK;
-
-template <bool LDS>
-__global__ __launch_bounds__(256, 8) void k_lz_spec(LzArgs z, u32 nchunks) {
-    __shared__ __align__(16) u8 win[LDS ? LZ_LWIN : 4];
-    const u32 lane = threadIdx.x & 63;
-    const u32 c = blockIdx.x * 4 + (threadIdx.x >> 6);
-    LText t{z.text, win, 0u, 0u};
-    if (LDS) {
-        // the workgroup's window, from its first chunk's block
-        const u32 c0 = blockIdx.x * 4;
-        const u32 b0 = c0 / z.cpb, k0 = c0 - b0 * z.cpb;
-        const u32 bb = z.geo.base(b0), be = z.geo.end(b0);
-        const u32 s0 = bb + k0 * LZ_CHUNK;
-        const u32 lo = s0 > bb + LZ_WINDOW ? s0 - LZ_WINDOW : bb;
-        const u32 hi = min(s0 + 4 * LZ_CHUNK, be);
-        if (lo < hi) {
-            const u32 n = hi - lo;
-            if ((lo & 3) == 0 && ((uintptr_t)z.text & 3) == 0) {
-                const u32* src = reinterpret_cast<const u32*>(z.text + lo);
-                u32* dst = reinterpret_cast<u32*>(win);
-                for (u32 i = threadIdx.x; i < n / 4; i += 256) dst[i] = src[i];
-                for (u32 i = (n & ~3u) + threadIdx.x; i < n; i += 256) win[i] = z.text[lo + i];
-            } else {
-                for (u32 i = threadIdx.x; i < n; i += 256) win[i] = z.text[lo + i];
-            }
-            t.lo = lo;
-            t.hi = hi;
-        }
-        __syncthreads();
-    }
-    if (c >= nchunks) return;
-    const u32 b = c / z.cpb, k = c - b * z.cpb;
-    const u32 bend = z.geo.end(b);
-    const u32 s = z.geo.base(b) + k * LZ_CHUNK;
-    if (s >= bend) {
-        if (lane == 0) {
-            z.c_ntok[c] = 0;
-            z.c_exit[c] = s;
-            z.c_bytes[c] = 0;
-        }
-        return;
-    }
-    const u32 e = min(s + (u32)LZ_CHUNK, bend);
-    // 64-position windows of (idx3, gs3), the next one prefetched
-    u32 wbase = s;
-    u32 P = wbase + lane;
-    uint2 v = P < bend ? z.ig3[P] : make_uint2(0u, 0u);
-    u32 Iw = v.x, Gw = v.y;
-    P += 64;
-    v = P < bend ? z.ig3[P] : make_uint2(0u, 0u);
-    u32 In = v.x, Gn = v.y;
-    u32 q = s, ntok = 0, off = 0, nlong = 0, nbuf = 0;
-    u32 bpos = 0, blen = 0, bdist = 0, boff = 0;
-    while (q < e) {
-        if (q >= wbase + 64) {
-            if (q < wbase + 128) {
-                Iw = In;
-                Gw = Gn;
-                wbase += 64;
-            } else {
-                wbase = q;
-                const u32 P0 = wbase + lane;
-                const uint2 w0 = P0 < bend ? z.ig3[P0] : make_uint2(0u, 0u);
-                Iw = w0.x;
-                Gw = w0.y;
-            }
-            const u32 P1 = wbase + 64 + lane;
-            const uint2 w1 = P1 < bend ? z.ig3[P1] : make_uint2(0u, 0u);
-            In = w1.x;
-            Gn = w1.y;
-        }
-        const u32 cur = q - wbase;
-        u32 len, dist;
-        best_match(z, t, q, bend, __builtin_amdgcn_readlane(Iw, cur), __builtin_amdgcn_readlane(Gw, cur), len,
-                   dist, nlong);
-        if (lane == nbuf) {
-            bpos = q;
-            blen = len;
-            bdist = dist;
-            boff = off;
-        }
-        if (++nbuf == 64) {
-            const u32 slot = s + ntok + 1 - 64 + lane;
-            z.tok_pos[slot] = bpos;
-            z.tok_len[slot] = blen;
-            z.tok_dist[slot] = bdist;
-            z.tok_off[slot] = boff;
-            nbuf = 0;
-        }
-        ++ntok;
-        off += tok_bytes(len, dist);
-        q += len ? len : 1;
-    }
-    if (lane < nbuf) {
-        const u32 slot = s + ntok - nbuf + lane;
-        z.tok_pos[slot] = bpos;
-        z.tok_len[slot] = blen;
-        z.tok_dist[slot] = bdist;
-        z.tok_off[slot] = boff;
-    }
-    if (lane == 0) {
-        z.c_ntok[c] = ntok;
-        z.c_exit[c] = q;
-        z.c_bytes[c] = off;
-        if (nlong) atomicAdd(z.nlong, nlong);
-    }
-}
-
-// ---------------------------------------------------------------------------------
-// Two parse chains per wave.  The parse is a dependent chain of candidate loads (one
-// global round trip per token) and k_lz_spec runs one chain per wave: 32 chains per CU,
-// the LDS window being the limit.  Here the wave's halves parse two chunks: lanes 0-31
-// score 32 candidates of chain A's position, lanes 32-63 those of chain B, so both
-// chains' loads are in flight together (64 chains per CU with 2 KiB chunks in the same
-// 20 KiB of LDS per workgroup).  Every ballot is masked to the lane's half; per-half
-// values (position, best length) live in each lane of the half.
-// ---------------------------------------------------------------------------------
-__device__ inline u64 half_mask(u32 lane) { return (lane & 32) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull; }
-
-// Longest match at p for this lane's half (act: the half has a position to score).
-template <class T>
-__device__ void best_match_h(const LzArgs& z, const T& t, bool act, u32 p, u32 end, u32 i, u32 gs, u32& out_len,
-                             u32& out_dist, u32& nlong) {
-    const u32 lane = threadIdx.x & 63, hl = lane & 31;
-    const u64 HM = half_mask(lane);
-    u32 best = 0, bd = 0;
-    bool go = act && p + (u32)LZ_MIN <= end && i > gs;
-    const u32 maxl = go ? end - p : 0u;
-    const u32 capl = min((u32)LZ_CAP, maxl);
-    bool wide = false;
-    if constexpr (IsLds<T>::value) wide = go && p >= t.lo && p + capl + 11 <= t.hi;
-    u32 k0 = i;  // candidates this batch: slots k0-1-hl
-    while (__ballot(go)) {
-        bool valid = go && k0 > gs + hl;
-        const u32 q = valid ? z.SA3[k0 - 1 - hl] : 0u;
-        valid = valid && (p - q <= (u32)LZ_WINDOW);
-        const u64 inwin = __ballot(valid) & HM;
-        u32 l = 0;
-        if (valid) {
-            // a later candidate wins only if strictly longer: it must match at `best`
-            const bool can = best == 0 || (best < maxl && t[p + best] == t[q + best]);
-            if (can) {
-                l = LZ_MIN;  // the 3-gram is shared by the group
-                bool done = false;
-                if constexpr (IsLds<T>::value) {
-                    if (wide) {
-#pragma unroll
-                        for (int k = 0; k < LZ_CAP / 8; ++k) {
-                            if (l >= capl) break;
-                            const u64 d = lds8(t.l, p - t.lo + 3 + 8 * k) ^ lds8(t.l, q - t.lo + 3 + 8 * k);
-                            if (d) {
-                                l += (u32)(__ffsll((long long)d) - 1) >> 3;
-                                break;
-                            }
-                            l += 8;
-                        }
-                        l = min(l, capl);
-                        done = true;
-                    }
-                }
-                if (!done)
-                    while (l < capl && t[p + l] == t[q + l]) ++l;
-            }
-        }
-        // capped candidates extended exactly, one at a time by the whole wave
-        u64 longm = __ballot(valid && l >= capl && capl < maxl);
-        while (longm) {
-            const u32 j = (u32)__ffsll((long long)longm) - 1;
-            const u32 pj = __builtin_amdgcn_readlane(p, j), qj = __builtin_amdgcn_readlane(q, j);
-            const u32 cj = __builtin_amdgcn_readlane(capl, j), mj = __builtin_amdgcn_readlane(maxl, j);
-            const u32 lj = wave_lcp(t, pj, qj, cj, mj);
-            if (lane == j) l = lj;
-            longm &= longm - 1;
-            ++nlong;
-        }
-        // max length, ties -> smallest lane of the half (= smallest distance)
-        const u32 lv = valid ? l : 0u;
-        u64 cand = __ballot(lv > best) & HM;
-        if (__ballot(lv >= 64u)) {
-            u32 lm = lv;
-#pragma unroll
-            for (int o = 16; o >= 1; o >>= 1) lm = max(lm, (u32)__shfl_xor(lm, o));
-            const u64 eq = __ballot(lv == lm) & HM;
-            cand = cand ? eq : 0ull;
-        } else {
-#pragma unroll
-            for (int b = 5; b >= 0; --b) {
-                const u64 tb = __ballot((lv >> b) & 1u) & cand;
-                if (tb) cand = tb;
-            }
-        }
-        const u32 wl = cand ? (u32)__ffsll((long long)cand) - 1 : lane;
-        const u32 nl = (u32)__shfl((int)lv, (int)wl), nq = (u32)__shfl((int)q, (int)wl);
-        if (cand) {
-            best = nl;
-            bd = p - nq;
-        }
-        if (best >= maxl || inwin != HM) go = false;
-        k0 -= 32;
-    }
-    if (best < (u32)LZ_MIN) {
-        best = 0;
-        bd = 0;
-    }
-    out_len = best;
-    out_dist = bd;
-}
-
-constexpr u32 LZ_CPW = 8;                               // chunks per workgroup (2 per wave)
-constexpr u32 LZ_LWIN2 = LZ_WINDOW + LZ_CPW * LZ_CHUNK;  // 20 KiB with 2 KiB chunks
-
-__global__ __launch_bounds__(256, 8) void k_lz_spec2(LzArgs z, u32 nchunks) {
-    __shared__ __align__(16) u8 win[LZ_LWIN2];
-    const u32 lane = threadIdx.x & 63, hl = lane & 31;
-    const u32 c = blockIdx.x * LZ_CPW + (threadIdx.x >> 6) * 2 + (lane >> 5);
-    LText t{z.text, win, 0u, 0u};
-    {
-        // the workgroup's window, from its first chunk's block
-        const u32 c0 = blockIdx.x * LZ_CPW;
-        const u32 b0 = c0 / z.cpb, k0 = c0 - b0 * z.cpb;
-        const u32 bb = z.geo.base(b0), be = z.geo.end(b0);
-        const u32 s0 = bb + k0 * LZ_CHUNK;
-        const u32 lo = s0 > bb + LZ_WINDOW ? s0 - LZ_WINDOW : bb;
-        const u32 hi = min(s0 + LZ_CPW * LZ_CHUNK, be);
-        if (lo < hi) {
-            const u32 n = hi - lo;
-            if ((lo & 3) == 0 && ((uintptr_t)z.text & 3) == 0) {
-                const u32* src = reinterpret_cast<const u32*>(z.text + lo);
-                u32* dst = reinterpret_cast<u32*>(win);
-                for (u32 i = threadIdx.x; i < n / 4; i += 256) dst[i] = src[i];
-                for (u32 i = (n & ~3u) + threadIdx.x; i < n; i += 256) win[i] = z.text[lo + i];
-            } else {
-                for (u32 i = threadIdx.x; i < n; i += 256) win[i] = z.text[lo + i];
-            }
-            t.lo = lo;
-            t.hi = hi;
-        }
-        __syncthreads();
-    }
-    // this half's chunk (a half past the last chunk, or a chunk past its block end, parses nothing)
-    const bool has = c < nchunks;
-    const u32 b = has ? c / z.cpb : 0u, k = has ? c - b * z.cpb : 0u;
-    const u32 bend = has ? z.geo.end(b) : 0u;
-    const u32 s = has ? z.geo.base(b) + k * LZ_CHUNK : 0u;
-    const u32 e = (has && s < bend) ? min(s + (u32)LZ_CHUNK, bend) : s;
-    // 32-position windows of (idx3, gs3) per half, the next one prefetched
-    u32 wbase = s;
-    u32 P = wbase + hl;
-    uint2 v = P < bend ? z.ig3[P] : make_uint2(0u, 0u);
-    u32 Iw = v.x, Gw = v.y;
-    P += 32;
-    v = P < bend ? z.ig3[P] : make_uint2(0u, 0u);
-    u32 In = v.x, Gn = v.y;
-    u32 q = s, ntok = 0, off = 0, nlong = 0, nbuf = 0;
-    u32 bpos = 0, blen = 0, bdist = 0, boff = 0;
-    const u32 hbase = lane & 32;
-    while (__ballot(q < e)) {
-        const bool act = q < e;
-        if (act && q >= wbase + 32) {
-            if (q < wbase + 64) {
-                Iw = In;
-                Gw = Gn;
-                wbase += 32;
-            } else {
-                wbase = q;
-                const u32 P0 = wbase + hl;
-                const uint2 w0 = P0 < bend ? z.ig3[P0] : make_uint2(0u, 0u);
-                Iw = w0.x;
-                Gw = w0.y;
-            }
-            const u32 P1 = wbase + 32 + hl;
-            const uint2 w1 = P1 < bend ? z.ig3[P1] : make_uint2(0u, 0u);
-            In = w1.x;
-            Gn = w1.y;
-        }
-        const u32 cur = act ? q - wbase : 0u;
-        const u32 iq = (u32)__shfl((int)Iw, (int)(hbase + cur)), gq = (u32)__shfl((int)Gw, (int)(hbase + cur));
-        u32 len, dist;
-        best_match_h(z, t, act, q, bend, iq, gq, len, dist, nlong);
-        if (act) {
-            if (hl == nbuf) {
-                bpos = q;
-                blen = len;
-                bdist = dist;
-                boff = off;
-            }
-            if (++nbuf == 32) {
-                const u32 slot = s + ntok + 1 - 32 + hl;
-                z.tok_pos[slot] = bpos;
-                z.tok_len[slot] = blen;
-                z.tok_dist[slot] = bdist;
-                z.tok_off[slot] = boff;
-                nbuf = 0;
-            }
-            ++ntok;
-            off += tok_bytes(len, dist);
-            q += len ? len : 1;
-        }
-    }
-    if (has && hl < nbuf) {
-        const u32 slot = s + ntok - nbuf + hl;
-        z.tok_pos[slot] = bpos;
-        z.tok_len[slot] = blen;
-        z.tok_dist[slot] = bdist;
-        z.tok_off[slot] = boff;
-    }
-    if (has && hl == 0) {
-        z.c_ntok[c] = ntok;
-        z.c_exit[c] = q;
-        z.c_bytes[c] = off;
-    }
-    nlong = wave_reduce(nlong, OpAddU(), 0u);
-    if (lane == 0 && nlong) atomicAdd(z.nlong, nlong);
-}
-
-// Per block (one wave): real chunk entries, fix-up tokens, chunk output offsets, size.
-__global__ __launch_bounds__(64) void k_lz_stitch(LzArgs z) {
-    const u32 b = blockIdx.x;
-    const u32 lane = threadIdx.x;
-    const u32 base = z.geo.base(b), bend = z.geo.end(b);
-    u32 entry = base, boff = 0, ntot = 0, fi = 0, nlong = 0;
-    for (u32 k = 0; k < z.cpb; ++k) {
-        const u32 c = b * z.cpb + k;
-        const u32 s = base + k * LZ_CHUNK;
-        if (s >= bend) break;
-        const u32 e = min(s + (u32)LZ_CHUNK, bend);
-        const u32 nt = z.c_ntok[c];
-        u32 first, nfix = 0, fixbytes = 0, next;
-        const u32 fix0 = base + fi;
-        if (entry == s) {
-            first = 0;
-            next = z.c_exit[c];
-        } else if (entry >= e) {
-            first = nt;
-            next = entry;
-        } else {
-            u32 q = entry, j = 0;
-            bool conv = false;
-            while (q < e) {
-                while (j < nt && z.tok_pos[s + j] < q) ++j;
-                if (j < nt && z.tok_pos[s + j] == q) {
-                    conv = true;
-                    break;
-                }
-                u32 len, dist;
-                const uint2 ig = z.ig3[q];
-                best_match(z, GText{z.text}, q, bend, ig.x, ig.y, len, dist, nlong);
-                if (lane == 0) {
-                    z.fix_pos[base + fi] = q;
-                    z.fix_len[base + fi] = len;
-                    z.fix_dist[base + fi] = dist;
-                    z.fix_off[base + fi] = boff + fixbytes;
-                }
-                ++fi;
-                ++nfix;
-                fixbytes += tok_bytes(len, dist);
-                q += len ? len : 1;
-            }
-            first = conv ? j : nt;
-            next = conv ? z.c_exit[c] : q;
-        }
-        const u32 spec_bytes = first < nt ? z.c_bytes[c] - z.tok_off[s + first] : 0u;
-        if (lane == 0) {
-            z.c_first[c] = first;
-            z.c_fix0[c] = fix0;
-            z.c_nfix[c] = nfix;
-            z.c_fixbytes[c] = fixbytes;
-            z.c_off[c] = boff;
-        }
-        boff += fixbytes + spec_bytes;
-        ntot += nfix + (nt - first);
-        entry = next;
-    }
-    if (lane == 0) {
-        z.lz_size[b] = boff;
-        z.ntok[b] = ntot;
-        z.b_nfix[b] = fi;
-        if (nlong) atomicAdd(z.nlong, nlong);
-    }
-}
-
 // =====================================================================================
-// Workgroup-local path (default, KOLM_LZ_LOCAL=1): no global 3-gram index.
+// Workgroup-local 3-gram index and speculative parse.
 //
 // A workgroup owns the LZL_HOME home positions [hs, he) of one block.  Every candidate of
 // a home position p lies in [p - 4096, p), so the window W = [hs - 4096 - LZL_LEAD, he)
@@ -607,76 +112,87 @@ struct WinText {
     __device__ inline u8 operator[](u32 x) const { return l[x - tlo]; }
 };
 
-// 16-bit hash of the 3-gram at window offset x: the LDS index groups positions by hash
-// (ascending position inside a group); a candidate whose 3-gram differs is rejected by
-// the byte compare, so hash collisions only cost a wasted lane.
+// LZL_HB-bit hash of the 3-gram at window offset x: the LDS index buckets the window's
+// positions by hash (ascending position inside a bucket); a candidate whose 3-gram differs
+// is rejected by the first byte compare, so other 3-grams sharing the bucket only cost
+// lanes (about 4096 / 2^LZL_HB of them per token).
+constexpr u32 LZL_HB = 9;
+constexpr u32 LZL_NBK = 1u << LZL_HB;
 __device__ inline u32 hash3(const u8* t, u32 x) {
     const u32 k = ((u32)t[x] << 16) | ((u32)t[x + 1] << 8) | t[x + 2];
-    return (k * 0x9E3779B1u) >> 16;
+    return (k * 0x9E3779B1u) >> (32 - LZL_HB);
 }
 
-constexpr u32 LZL_PER = (LZL_NW + 255) / 256;  // window elements per lane in a sort pass (33)
+constexpr u32 LZL_PER = (LZL_NW + 255) / 256;  // window elements per lane (33)
 
-// One stable LSD pass over the nw window positions by hash byte DG, in place in A (identity
-// order for the first pass).  Wave w owns the contiguous element range [w*Q, (w+1)*Q),
-// staged in registers: per-wave digit counts (LDS atomics), digit-major / wave-minor
-// offsets, then each wave places its elements 64 at a time in order (ballot match-any
-// ranking; the leader advances the wave's digit offset — a wave's LDS operations retire in
-// program order, so no barrier is needed between its steps).
-template <int DG, bool IOTA>
-__device__ void lzl_pass(const u8* t, u16* A, u32 nw, u32 (*hist)[256], u32* sh) {
+// Stable counting sort of the nw window positions by hash into A (one pass).  Wave w owns
+// the contiguous position range [w*Q, (w+1)*Q): per-wave bucket counts (LDS atomics),
+// bucket-major / wave-minor offsets, then each wave places its positions 64 at a time in
+// order (ballot match-any ranking over the LZL_HB hash bits; the leader advances the
+// wave's bucket offset — a wave's LDS operations retire in program order, so no barrier
+// is needed between its steps).
+__device__ void lzl_bucket(const u8* t, u16* A, u32 nw, u32* hist /*[4][LZL_NBK]*/, u32* sh) {
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr u32 R = LZL_NBK / 256;  // buckets per thread in the scan
     const u32 Q = (nw + 3) / 4;
     const u32 b0 = min(w * Q, nw), b1 = min(b0 + Q, nw);
-    u32 xv[LZL_PER];
+    u32 hv[LZL_PER];
 #pragma unroll
     for (u32 k = 0; k < LZL_PER; ++k) {
         const u32 e = b0 + k * 64 + lane;
-        xv[k] = e < b1 ? (IOTA ? e : (u32)A[e]) : 0u;
+        hv[k] = e < b1 ? hash3(t, e) : 0u;
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) hist[i][tid] = 0;
+    for (u32 i = tid; i < 4 * LZL_NBK; i += 256) hist[i] = 0;
     __syncthreads();
 #pragma unroll
     for (u32 k = 0; k < LZL_PER; ++k)
-        if (b0 + k * 64 + lane < b1) atomicAdd(&hist[w][(hash3(t, xv[k]) >> (8 * DG)) & 255u], 1u);
+        if (b0 + k * 64 + lane < b1) atomicAdd(&hist[w * LZL_NBK + hv[k]], 1u);
     __syncthreads();
     {
-        const u32 h0 = hist[0][tid], h1 = hist[1][tid], h2 = hist[2][tid], h3 = hist[3][tid];
-        const u32 tot = h0 + h1 + h2 + h3;
+        u32 h[4][R], tot = 0;
+#pragma unroll
+        for (u32 r = 0; r < R; ++r)
+#pragma unroll
+            for (u32 q = 0; q < 4; ++q) {
+                h[q][r] = hist[q * LZL_NBK + tid * R + r];
+                tot += h[q][r];
+            }
         const u32 incl = wave_incl_scan(tot, OpAddU(), 0u);
         if (lane == 63) sh[w] = incl;
         __syncthreads();
         u32 ex = incl - tot;
         for (u32 i = 0; i < w; ++i) ex += sh[i];
-        hist[0][tid] = ex;
-        hist[1][tid] = ex + h0;
-        hist[2][tid] = ex + h0 + h1;
-        hist[3][tid] = ex + h0 + h1 + h2;
+#pragma unroll
+        for (u32 r = 0; r < R; ++r)
+#pragma unroll
+            for (u32 q = 0; q < 4; ++q) {
+                hist[q * LZL_NBK + tid * R + r] = ex;
+                ex += h[q][r];
+            }
     }
     __syncthreads();
     const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
 #pragma unroll
     for (u32 k = 0; k < LZL_PER; ++k) {
         if (b0 + k * 64 >= b1) break;  // wave-uniform
-        const bool valid = b0 + k * 64 + lane < b1;
-        const u32 x = xv[k];
-        const u32 dg = valid ? (hash3(t, x) >> (8 * DG)) & 255u : 0u;
+        const u32 e = b0 + k * 64 + lane;
+        const bool valid = e < b1;
+        const u32 dg = hv[k];
         u64 m = __ballot(valid);
 #pragma unroll
-        for (u32 bit = 0; bit < 8; ++bit) {
+        for (u32 bit = 0; bit < LZL_HB; ++bit) {
             const u64 bal = __ballot((dg >> bit) & 1u);
             m &= ((dg >> bit) & 1u) ? bal : ~bal;
         }
         const u32 rank = (u32)__popcll(m & lt);
-        const u32 o = valid ? hist[w][dg] : 0u;
-        if (valid) A[o + rank] = (u16)x;
-        if (valid && rank == 0) hist[w][dg] = o + (u32)__popcll(m);
+        const u32 o = valid ? hist[w * LZL_NBK + dg] : 0u;
+        if (valid) A[o + rank] = (u16)e;
+        if (valid && rank == 0) hist[w * LZL_NBK + dg] = o + (u32)__popcll(m);
     }
     __syncthreads();
 }
 
-// first slot of slot k's hash group (slot 0 is always a head)
+// first slot of slot k's hash bucket (slot 0 is always a head)
 __device__ inline u32 lzl_gs(const u64* bm, u32 k) {
     u32 wi = k >> 6;
     u64 m = bm[wi] & (~0ull >> (63 - (k & 63)));
@@ -785,8 +301,8 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
     // islot of [ilo, he) + head bitmap; the sort's histograms live here before them
     __shared__ __align__(16) u16 B[LZL_ISL + 4 * ((LZL_NW + 63) / 64)];
     __shared__ u32 sh[4];
-    u32(*hist)[256] = reinterpret_cast<u32(*)[256]>(B);
-    static_assert(sizeof(u32) * 4 * 256 <= sizeof(u16) * LZL_ISL, "histograms alias the islot array");
+    u32* hist = reinterpret_cast<u32*>(B);
+    static_assert(sizeof(u32) * 4 * LZL_NBK <= sizeof(B), "histograms alias the islot array + bitmap");
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const u32 b = blockIdx.x / hpb, h = blockIdx.x - b * hpb;
     const u32 base = z.geo.base(b), end = z.geo.end(b);
@@ -818,8 +334,7 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
     const u8* tw = txt + (lo - tlo);  // window text at window offset 0
     if (z.prof) t1 = wall_clock64();
     if (nw) {
-        lzl_pass<0, true>(tw, A, nw, hist, sh);
-        lzl_pass<1, false>(tw, A, nw, hist, sh);
+        lzl_bucket(tw, A, nw, hist, sh);
     }
     // islot of [ilo, he) and the group-head bitmap
     u16* isl = B;
@@ -1148,52 +663,22 @@ __global__ __launch_bounds__(256) void k_lz_emit(LzArgs z, const u32* method, co
 
 }  // namespace
 
-bool lz_local() {
-    static const bool v = !getenv("KOLM_LZ_LOCAL") || atoi(getenv("KOLM_LZ_LOCAL")) != 0;
-    return v;
-}
-
-const char* lz_spec_name() {
-    static const bool lds = !getenv("KOLM_LZ_LDS") || atoi(getenv("KOLM_LZ_LDS")) != 0;
-    static const bool dual = !getenv("KOLM_LZ_DUAL") || atoi(getenv("KOLM_LZ_DUAL")) != 0;
-    if (lz_local()) return "k_lz_local";
-    return dual ? "k_lz_spec2" : lds ? "k_lz_spec<true>" : "k_lz_spec<false>";
-}
+const char* lz_spec_name() { return "k_lz_local"; }
 
 void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
     if (!z.geo.nb) return;
-    if (lz_local()) {
-        const u32 hpb = (z.geo.bs + LZL_HOME - 1) / LZL_HOME;
-        {
-            // text window (LZL_NW + LZL_CAPX bytes per 4 KiB home: ~2.1 B per position) +
-            // 16 B per token (added by the caller once the token count is known)
-            KScope k(kt, KT_LZPARSE, "k_lz_local", z.geo.N * 2);
-            static const u32 lead = getenv("KOLM_LZ_LEAD") ? std::min<u32>(atoi(getenv("KOLM_LZ_LEAD")), LZL_LEAD) : LZL_LEAD;
-            k_lz_local<<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb, lead);
-        }
-        {
-            KScope k(kt, KT_LZPARSE, "k_lz_stitch", (u64)z.cpb * z.geo.nb * 16);
-            k_lz_stitch_l<<<z.geo.nb, 64, 0, s>>>(z);
-        }
-        return;
-    }
-    const u32 nchunks = z.cpb * z.geo.nb;
+    const u32 hpb = (z.geo.bs + LZL_HOME - 1) / LZL_HOME;
     {
-        // (slot, group start) windows 8 B + text 1 B per position (+16 B per token, added
-        // by the caller once the token count is known)
-        static const bool lds = !getenv("KOLM_LZ_LDS") || atoi(getenv("KOLM_LZ_LDS")) != 0;
-        static const bool dual = !getenv("KOLM_LZ_DUAL") || atoi(getenv("KOLM_LZ_DUAL")) != 0;
-        KScope k(kt, KT_LZPARSE, lz_spec_name(), z.geo.N * 9);
-        if (dual)
-            k_lz_spec2<<<(nchunks + LZ_CPW - 1) / LZ_CPW, 256, 0, s>>>(z, nchunks);
-        else if (lds)
-            k_lz_spec<true><<<(nchunks + 3) / 4, 256, 0, s>>>(z, nchunks);
-        else
-            k_lz_spec<false><<<(nchunks + 3) / 4, 256, 0, s>>>(z, nchunks);
+        // text window (LZL_NW + LZL_CAPX bytes per 4 KiB home: ~2.1 B per position) +
+        // 16 B per token (added by the caller once the token count is known)
+        static const u32 lead =
+            getenv("KOLM_LZ_LEAD") ? std::min<u32>(atoi(getenv("KOLM_LZ_LEAD")), LZL_LEAD) : LZL_LEAD;
+        KScope k(kt, KT_LZPARSE, "k_lz_local", z.geo.N * 2);
+        k_lz_local<<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb, lead);
     }
     {
-        KScope k(kt, KT_LZPARSE, "k_lz_stitch", (u64)nchunks * 32);
-        k_lz_stitch<<<z.geo.nb, 64, 0, s>>>(z);
+        KScope k(kt, KT_LZPARSE, "k_lz_stitch", (u64)z.cpb * z.geo.nb * 16);
+        k_lz_stitch_l<<<z.geo.nb, 64, 0, s>>>(z);
     }
 }
 

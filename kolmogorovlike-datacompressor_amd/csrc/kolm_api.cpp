@@ -447,17 +447,6 @@ struct Pipeline {
                       c->get<u32>("lyn_nfac", nch), c->get<u32>("lyn_stack", N), c->get<u32>("lyn_t1", 2 * ntiles + 16),
                       c->get<u32>("lyn_t2", 2 * ntiles + 2 * geo.nb + 16), c->active, c->kt());
     }
-    // linear suffix order at 3 characters only: LZ77 candidate groups (SA3, idx3, GS3)
-    void linear3() {
-        const u64 N = geo.N;
-        const u64 nt = lsd_tiles(geo) + 1;
-        G3Bufs t{c->get<u32>("g3Ka", N), c->get<u32>("g3Kb", N), c->get<u32>("g3hist", nt * 256),
-                 c->get<u32>("g3tmax", nt), c->get<u32>("g3tcarry", nt), c->get<u32>("SA3", N),
-                 c->get<uint2>("ig3", N)};
-        launch_gram3(geo, text, t, c->active, c->kt());
-        st.lin_rounds = 1;
-        st.lin_active = N;
-    }
     // omega-order of all rotations of the Lyndon factors + BBWT gather -> "bbwt"
     // cyclic predecessor byte of every position (needs the Lyndon factors only)
     hipEvent_t prevc_ready = nullptr;  // set when prevc() ran on another stream
@@ -503,10 +492,6 @@ struct Pipeline {
         LzArgs z{};
         z.geo = geo;
         z.text = text;
-        if (!lz_local()) {
-            z.SA3 = c->get<u32>("SA3", N);
-            z.ig3 = c->get<uint2>("ig3", N);
-        }
         z.tok_pos = c->get<u32>("tok_pos", N);
         z.tok_len = c->get<u32>("tok_len", N);
         z.tok_dist = c->get<u32>("tok_dist", N);
@@ -515,8 +500,8 @@ struct Pipeline {
         z.fix_len = c->get<u32>("fix_len", N);
         z.fix_dist = c->get<u32>("fix_dist", N);
         z.fix_off = c->get<u32>("fix_off", N);
-        z.cshift = lz_local() ? 8 : 11;
-        static_assert(LZL_CHUNK == 256 && LZ_CHUNK == 2048, "chunk shifts");
+        z.cshift = 8;
+        static_assert(LZL_CHUNK == 256, "chunk shift");
         z.cpb = (geo.bs + (1u << z.cshift) - 1) >> z.cshift;
         const u64 nch = (u64)z.cpb * geo.nb + 1;
         z.c_ntok = c->get<u32>("c_ntok", nch);
@@ -605,13 +590,13 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         if (stats) *stats = kolm_stats{};
         return KOLM_OK;
     }
-    // Two streams: main runs the 3-gram linear sort and then the LZ77 parse; aux runs the
-    // Lyndon factorisation (beside the linear sort), then the cyclic sort, BBWT, MTF and
-    // the size kernels (beside LZ77), joins LZ77 and finishes MDL + emission.
-    // KOLM_SERIAL=1 runs everything on one stream (profiling); KOLM_OVERLAP selects when the
-    // 3-gram index + LZ77 start: 0 at once, 1 after the Lyndon factorisation, 2 (default)
-    // the index at once and LZ77 after round 0 of the cyclic sort (measured 73.1 -> 71.0 ms
-    // per 256 MiB: the latency-bound parse fills the CUs the doubling rounds leave idle).
+    // Two streams: the index stream (main) runs the xor/lfsr size counters, the BBWT
+    // predecessor bytes and the LZ77 parse (k_lz_local + stitch); the sort stream (aux,
+    // higher priority: the critical path) runs the Lyndon factorisation, the cyclic sort,
+    // BBWT, MTF and the Rice sizes, joins LZ77 and finishes MDL + emission.
+    // KOLM_SERIAL=1 runs everything on one stream (profiling); KOLM_OVERLAP selects when
+    // LZ77 starts: 0 at once, 1 after the Lyndon factorisation, 2 (default) after round 0
+    // of the cyclic sort (measured 58.5-59.0 ms per 256 MiB vs 59.1-59.7 for 0 and 1).
     static const bool serial = getenv("KOLM_SERIAL") && atoi(getenv("KOLM_SERIAL")) != 0;
     static const int overlap = getenv("KOLM_OVERLAP") ? atoi(getenv("KOLM_OVERLAP")) : 2;
     hipStream_t ms = c->stream, s = serial ? c->stream : c->aux;
@@ -686,7 +671,6 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         KOLM_HIP_CHECK(hipStreamWaitEvent(ms, ej[3], 0));
     }
     c->active = ms;
-    if (!lz_local()) P.linear3();  // the global 3-gram index of the KOLM_LZ_LOCAL=0 path
     {
         EmitArgs ce{};
         ce.geo = geo;
@@ -1730,7 +1714,6 @@ int kolm_lz77_encode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size
         geom_init(geo, n, (u32)n);
         u8* d = upload(c, in, n);
         Pipeline P{c, geo, d};
-        if (!lz_local()) P.linear3();
         LzArgs z = P.lz_args();
         P.lz(z);
         u32 sz = 0;

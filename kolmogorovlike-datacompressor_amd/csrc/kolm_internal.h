@@ -259,18 +259,8 @@ void launch_lyndon_isa(const Geom& geo, const u32* RK, u8* flag, u32* tile_tmp, 
 void launch_prevc(const Geom& geo, const u8* text, const u8* flag, const u64* FSL, u8* prevc, hipStream_t s);
 void launch_bbwt_gather(const Geom& geo, const u32* SA, const u8* prevc, u8* out, hipStream_t s);
 
-// ---- k_lsd.hip: per-block LSD radix passes: 3-gram index for LZ77, cyclic round 0 ----
-struct G3Bufs {
-    u32* Ka;      // [N] key ping
-    u32* Kb;      // [N] key pong
-    u32* hist;    // [gram3_tiles * 256]
-    u32* tmax;    // [gram3_tiles]
-    u32* tcarry;  // [gram3_tiles]
-    u32* SA3;     // [N] out: positions grouped by 3-gram, ascending inside a group
-    uint2* ig3;   // [N] out: (slot, first slot of the group) of each position
-};
+// ---- k_lsd.hip: per-block LSD radix passes: round 0 of the cyclic sort ----
 u32 lsd_tiles(const Geom& geo);
-void launch_gram3(const Geom& geo, const u8* text, const G3Bufs& t, hipStream_t s, KTimer* kt = nullptr);
 struct R0Bufs {
     u32* KP;   // [N] in: 4-character keys by position; scratch afterwards
     u32* K2;   // [N] out: sorted keys (scratch)
@@ -316,8 +306,7 @@ void launch_rice_only(const Geom& geo, const u8* in, int k, u8* out, u32* tile_t
                       u32* out_size, hipStream_t s);
 
 // ---- k_lz77.hip ----
-constexpr int LZ_CHUNK = 2048;  // speculative-parse chunk of the global-index path (k_lz_spec2, KOLM_LZ_LOCAL=0)
-// Workgroup-local path (k_lz_local, default): a workgroup owns LZL_HOME consecutive positions
+// k_lz_local: a workgroup owns LZL_HOME consecutive positions
 // of one block, indexes its window [home - 4096 - LZL_LEAD, home end) in LDS, and parses the
 // home with LZL_HOME / LZL_CHUNK chains of 16 lanes (4 per wave)
 constexpr int LZL_HOME = 4096;
@@ -329,9 +318,6 @@ constexpr u32 LZ_UNRES = 0x80000000u;  // c_exit flag: the chunk's last token re
 struct LzArgs {
     Geom geo;
     const u8* text;
-    // 3-gram candidate structure captured after round 0 of the linear suffix sort:
-    const u32* SA3;    // [N] positions sorted by (3-gram key, position)
-    const uint2* ig3;  // [N] (idx3[p] = slot of p in SA3, gs3[p] = first slot of p's group)
     // speculative tokens of chunk c live in slots [chunk start, chunk start + ntok[c])
     u32* tok_pos;      // [N] token start position
     u32* tok_len;      // [N] match length (0 = literal)
@@ -355,11 +341,10 @@ struct LzArgs {
     u32* lz_size;      // [nb] stream size
     u32* nlong;        // [1]
     u32 cpb;           // chunks per block
-    u32 cshift;        // chunk = 1 << cshift bytes (LZ_CHUNK or LZL_CHUNK)
+    u32 cshift;        // chunk = 1 << cshift bytes (LZL_CHUNK)
     u32* nfix;         // [1] fix-up tokens computed by the stitch (statistics)
     u64* prof;         // [8] optional k_lz_local phase clocks (KOLM_LZ_PROF=1), null = off
 };
-bool lz_local();       // KOLM_LZ_LOCAL (default 1): workgroup-local index path
 void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr);
 const char* lz_spec_name();  // the speculative-parse kernel in use (timing / roofline)
 void launch_lz_emit(const LzArgs& z, const u32* method, const u64* off, u8* arena, hipStream_t s);

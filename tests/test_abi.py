@@ -40,11 +40,22 @@ def test_ctypes_signatures_cover_header():
     assert set(declared_functions()) == bound
 
 
-def test_stats_struct_size_matches_header():
-    # kolm_stats: 2 u32 + 4 u64 + 5 double + KOLM_NKT(12) x {double, u64, u64} + double + 3 u64
+def test_stats_struct_size_matches_header(tmp_path):
+    # kolm_stats: 2 u32 + 4 u64 + 5 double + KOLM_NKT(12) x {double, u64, u64} + double + 4 u64
     nkt = int(re.search(r"#define KOLM_NKT (\d+)", open(HEADER).read()).group(1))
     assert nkt == len(_lib.KT_NAMES) == 12
-    assert ctypes.sizeof(_lib.Stats) == 8 + 4 * 8 + 5 * 8 + nkt * 24 + 8 + 3 * 8
+    assert ctypes.sizeof(_lib.Stats) == 8 + 4 * 8 + 5 * 8 + nkt * 24 + 8 + 4 * 8
+    # the C compiler's layout of the header struct: size and every field offset
+    src = tmp_path / "sz.c"
+    fields = [f for f, _ in _lib.Stats._fields_]
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "kolm.h"\nint main(void){printf("%zu'
+                   + "".join(" %zu" for _ in fields) + '\\n", sizeof(kolm_stats)'
+                   + "".join(f", offsetof(kolm_stats, {f})" for f in fields) + ");return 0;}\n")
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got[0] == ctypes.sizeof(_lib.Stats)
+    assert got[1:] == [getattr(_lib.Stats, f).offset for f in fields]
 
 
 def test_candidate_constants_match_header():

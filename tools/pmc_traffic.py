@@ -25,7 +25,7 @@ from collections import defaultdict
 FAMILY = [
     ("k_classify", "classify"), ("k_keygen", "keygen"), ("k_msd_", "msd"), ("k_copy_back", "msd"),
     ("k_small_sort", "small_sort"), ("k_single", "small_sort"), ("k_finalize_eq", "small_sort"),
-    ("k_g3_", "lsd"), ("k_r0_", "lsd"), ("k_lz_spec", "lz_parse"), ("k_lz_stitch", "lz_parse"),
+    ("k_lsd_", "lsd"), ("k_r0_", "lsd"), ("k_lz_local", "lz_parse"), ("k_lz_stitch", "lz_parse"),
     ("k_duval", "lyndon_gather"), ("k_prevc", "lyndon_gather"), ("k_keypos", "keygen"),
     ("k_mtf", "mtf"), ("k_sizes", "sizes"), ("k_mdl", "sizes"), ("k_offsets", "sizes"),
     ("k_emit", "emit"), ("k_rice", "emit"), ("k_simple", "emit"), ("k_lz_emit", "emit"),

@@ -57,7 +57,7 @@ def main():
               f" last-end {(max(r[1] for r in rs) - t0) / 1e6:.2f} ms")
     # phases on each stream, split where one of the marker kernels starts
     print("\nper-stream phases:")
-    marks = ("k_iota", "k_duval_span", "k_lz_spec", "k_prevc", "k_mtf_summary", "k_sizes")
+    marks = ("k_iota", "k_duval_span", "k_lz_local", "k_prevc", "k_mtf_summary", "k_sizes")
     for sid, rs in sorted(by_stream.items()):
         phases = []
         for r in rs:
