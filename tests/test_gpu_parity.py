@@ -328,3 +328,52 @@ def test_adversarial_repair(kolm_gpu, kind):
     one 200 KB block vs the oracle."""
     data = _adversarial(kind, 200_000)
     assert kolm_gpu.repair_compress(data)[0] == O.repair_fast(data)
+
+
+def _lz_edge(kind: str) -> bytes:
+    """Inputs aimed at the workgroup-local LZ77 path (k_lz77.hip): 4 KiB homes, 256-byte
+    chunks with 64-byte lead-ins, matches resolved exactly only 256 bytes past a chunk."""
+    rng = np.random.default_rng(7 + len(kind))
+    if kind == "long_copies":     # copies of 300..5000 bytes with sparse mutations: matches
+        out = bytearray(rng.integers(0, 256, 6000).astype(np.uint8).tobytes())  # past the cap
+        while len(out) < 150_000:
+            L = int(rng.integers(300, 5000))
+            d = int(rng.integers(L, min(len(out), 4096) + 1)) if L <= 4096 else len(out) - 1
+            seg = bytearray(out[len(out) - d:len(out) - d + L])
+            for _ in range(int(rng.integers(0, 3))):
+                seg[int(rng.integers(0, L))] ^= 0x5A
+            out += seg + rng.integers(0, 256, int(rng.integers(1, 40))).astype(np.uint8).tobytes()
+        return bytes(out)
+    if kind in ("period4096", "period4097"):  # a match only at exactly the window edge (or none)
+        per = int(kind[6:])
+        unit = rng.integers(0, 256, per).astype(np.uint8).tobytes()
+        return (unit * (150_000 // per + 1))[:150_000]
+    if kind == "text_zero_runs":  # tokens spanning many chunks and homes, then text again
+        parts = []
+        for i, z in enumerate((9000, 300, 70_000, 4096, 257)):
+            parts += [D.enwik_like(6000 + 1000 * i, seed=40 + i), bytes(z)]
+        return b"".join(parts)
+    if kind == "random":          # all literals: every chain trivially in sync
+        return rng.integers(0, 256, 120_000).astype(np.uint8).tobytes()
+    if kind == "text":
+        return D.enwik_like(200_000, seed=99)
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["long_copies", "period4096", "period4097", "text_zero_runs", "random", "text"])
+def test_lz77_local_edges(kolm_gpu, kind):
+    data = _lz_edge(kind)
+    assert kolm_gpu.encode_lz77(data)[0] == O.encode_lz77(data)
+
+
+@pytest.mark.parametrize("bs", [255, 256, 257, 4095, 4096, 4097, 4096 + 256 + 63, 12288 + 5])
+def test_lz77_local_block_geometry(kolm_gpu, bs):
+    """Block sizes around the chunk (256) and home (4096) sizes in one batch: the last
+    chunk / home of every block is partial; candidates must never cross a block."""
+    from kolm import _lib
+    data = (D.enwik_like(30_000, seed=5) + bytes(700) + D.enwik_like(20_000, seed=6))
+    nb = (len(data) + bs - 1) // bs
+    _, method, payloads, st = _lib.encode_blocks(data, bs, force=[7] * nb)
+    for i in range(nb):
+        blk = data[i * bs:(i + 1) * bs]
+        assert payloads[i] == O.encode_lz77(blk), f"block {i}"
