@@ -161,7 +161,12 @@ def main():
     d_in = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     d_in[:n].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
     cap = n + (4 << 20)
-    arena = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    # payload arenas: N > 1 double-buffers them, so the RCCL gather of step k (over xGMI,
+    # on the NCCL stream) overlaps step k+1's encoding instead of serialising behind it
+    arenas = [torch.empty(cap, dtype=torch.uint8, device="cuda") for _ in range(2 if world > 1 else 1)]
+    pending = [None] * len(arenas)
+    nstep = [0]
+    arena = arenas[0]
     nb = (n + a.bs - 1) // a.bs
     sizes = np.zeros((nb, _lib.KOLM_NCAND), np.uint32)
     method = np.zeros(nb, np.uint32)
@@ -169,15 +174,31 @@ def main():
     torch.cuda.synchronize()
 
     def step(st, mask=_lib.KOLM_HOTPATH_MASK):
-        _lib.check(L.kolm_encode_blocks_device(ctx, d_in.data_ptr(), n, a.bs, mask, None, arena.data_ptr(), cap,
+        j = nstep[0] % len(arenas)
+        nstep[0] += 1
+        buf = arenas[j]
+        if pending[j] is not None:  # the gather of two steps ago still reads this buffer
+            pending[j].wait()
+            pending[j] = None
+        _lib.check(L.kolm_encode_blocks_device(ctx, d_in.data_ptr(), n, a.bs, mask, None, buf.data_ptr(), cap,
                                                sizes.ctypes.data, method.ctypes.data, off.ctypes.data,
                                                ctypes.byref(st)))
         if world > 1:
             ids = torch.from_numpy(method.astype(np.int32)).cuda()
-            gather_payloads(arena, int(off[-1]), ids, dst=0)
+            pending[j] = gather_payloads(buf, int(off[-1]), ids, dst=0, async_op=True)
+        return buf
+
+    def drain():
+        """every gather in flight completed (inside the timed region for timed steps)"""
+        for j, w in enumerate(pending):
+            if w is not None:
+                w.wait()
+                pending[j] = None
+        torch.cuda.synchronize()
 
     for _ in range(a.warmup):
         step(_lib.Stats())
+    drain()
     _lib.check(L.kolm_ctx_set_timing(ctx, 1))
     kern = {}
     stats = []
@@ -187,14 +208,14 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         st = _lib.Stats()
-        step(st)
+        arena = step(st)
         d = st.as_dict()
         stats.append(d)
         for k, v in d["kernels"].items():
             e = kern.setdefault(k, {"ms": 0.0, "launches": 0, "bytes": 0})
             for f in ("ms", "launches", "bytes"):
                 e[f] += v[f]
-    torch.cuda.synchronize()
+    drain()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -228,6 +249,31 @@ def main():
             "limiter": LIMITER.get(name, "hbm"),
             "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": int(bytes_per_launch),
             "launches_per_step": k["launches"] // a.steps}
+    # the critical path's own roofline: the sort stream's largest kernel (the LZ77 parse runs
+    # beside it), algorithmic bytes and PMC-measured HBM traffic per launch / launch time
+    sort_fams = ("keygen", "small_sort", "lsd", "msd", "classify", "lyndon_gather", "mtf")
+    crit = None
+    cands = {k: v for k, v in singles.items() if _lib.KT_NAMES[v.get("family", 0)] in sort_fams}
+    if cands:
+        cname, cv = max(cands.items(), key=lambda kv: kv[1]["ms"])
+        cavg = cv["ms"] / cv["launches"]
+        ctraffic = craw = None
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                tr = json.load(f).get("kernels", {}).get(cname)
+            if tr and tr.get("hbm_bytes_per_launch"):
+                ctraffic = tr["hbm_bytes_per_launch"]
+                # FETCH_SIZE x2 is the guide's correction for wide streaming reads; for 4-byte
+                # gathers the uncorrected figure is the plausible one, so both are reported
+                craw = tr.get("fetch_bytes_raw", 0) + tr.get("write_bytes", 0)
+        cach = cv["bytes"] / cv["launches"] / (cavg * 1e-3) / 1e9
+        crit = {"kernel": cname, "avg_launch_ms": round(cavg, 4), "launches_per_step": cv["launches"] // a.steps,
+                "achieved_algorithmic_GBs": round(cach, 2), "frac_algorithmic": round(cach / HBM_PEAK_GBS, 5),
+                "traffic_per_launch": int(ctraffic) if ctraffic else None,
+                "achieved_traffic_GBs": round(ctraffic / (cavg * 1e-3) / 1e9, 2) if ctraffic else None,
+                "frac_traffic": round(ctraffic / (cavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if ctraffic else None,
+                "achieved_traffic_uncorrected_GBs": round(craw / (cavg * 1e-3) / 1e9, 2) if craw else None,
+                "limiter": "random 4-byte gathers / scatters (one 32-64 B HBM request each)"}
     # whole pipeline: every kernel's algorithmic bytes per step / wall time per step (the two
     # streams overlap, so this is the chip-level rate the path sustains)
     alg_step = sum(v["bytes"] for v in ktimes.values()) / a.steps
@@ -284,7 +330,9 @@ def main():
     if a.full_steps > 0:
         method_hot = method.copy()
         off_hot = off.copy()
+        arena_hot = arena
         step(_lib.Stats(), _lib.KOLM_DEFAULT_MASK)
+        drain()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -292,9 +340,9 @@ def main():
         fst = []
         for _ in range(a.full_steps):
             st = _lib.Stats()
-            step(st, _lib.KOLM_DEFAULT_MASK)
+            arena = step(st, _lib.KOLM_DEFAULT_MASK)
             fst.append(st.as_dict())
-        torch.cuda.synchronize()
+        drain()
         if world > 1:
             dist.barrier()
         elf = time.perf_counter() - t0
@@ -314,6 +362,7 @@ def main():
             full["decode"] = decode_leg()
         method[:] = method_hot
         off[:] = off_hot
+        arena = arena_hot
 
     # Content-defined mode (compress_blocks_cdc, PY:2213-2326): FastCDC boundaries on the
     # device (PY's default 4096/8192/16384) + candidates 0..8 over the variable-length
@@ -389,6 +438,7 @@ def main():
                        "lz77": {"tokens": s0["lz_tokens"], "stitch_fixups": s0["lz_fix"],
                                 "long_extensions": s0["lz_long"]},
                        "pipeline_roofline": pipe,
+                       "critical_path_roofline": crit,
                        "families_ms_per_step": {kk: round(v["ms"] / a.steps, 2) for kk, v in
                                                 sorted(kern.items(), key=lambda kv: -kv[1]["ms"])},
                        "kernels_ms_per_step": {kk: round(v["ms"] / a.steps, 3) for kk, v in

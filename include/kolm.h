@@ -181,8 +181,8 @@ int kolm_ctx_sync(kolm_ctx* ctx);
 /* Enable (1) / disable (0) per-launch HIP-event timing of the kernel families. */
 int kolm_ctx_set_timing(kolm_ctx* ctx, int enable);
 /* Per-kernel timing accumulated since timing was enabled, as JSON text
- * {"k_name": {"ms": .., "launches": .., "bytes": ..}, ...} (bytes = algorithmic HBM
- * bytes).  *len receives the length; buf may be NULL to query it. */
+ * {"k_name": {"ms": .., "launches": .., "bytes": .., "family": KOLM_KT_*}, ...} (bytes =
+ * algorithmic HBM bytes).  *len receives the length; buf may be NULL to query it. */
 int kolm_ctx_kernel_times(kolm_ctx* ctx, char* buf, size_t cap, size_t* len);
 /* Fixed-size blocks of d_data (device pointer, total bytes, block_size).  Payloads go
  * to the device arena d_arena (cap bytes); h_sizes / h_method / h_off are host arrays

@@ -99,6 +99,7 @@ struct kolm_ctx {
     struct Acc {
         double ms = 0;
         u64 launches = 0, bytes = 0;
+        int fam = 0;  // KOLM_KT_* family of the kernel
     };
     std::map<std::string, Acc> kacc;  // per kernel, accumulated while timing is enabled
     // KTimer for multi-kernel launchers: events on the active stream, nested scopes allowed
@@ -148,6 +149,7 @@ struct kolm_ctx {
             st->kt[p.fam].launches += 1;
             st->kt[p.fam].bytes += p.bytes;
             Acc& a = kacc[p.name];
+            a.fam = p.fam;
             a.ms += ms;
             a.launches += 1;
             a.bytes += p.bytes;
@@ -1022,10 +1024,10 @@ int kolm_ctx_kernel_times(kolm_ctx* c, char* buf, size_t cap, size_t* len) {
     std::string js = "{";
     bool first = true;
     for (auto& kv : c->kacc) {
-        char tmp[256];
-        snprintf(tmp, sizeof tmp, "%s\"%s\": {\"ms\": %.6f, \"launches\": %llu, \"bytes\": %llu}", first ? "" : ", ",
-                 kv.first.c_str(), kv.second.ms, (unsigned long long)kv.second.launches,
-                 (unsigned long long)kv.second.bytes);
+        char tmp[320];
+        snprintf(tmp, sizeof tmp, "%s\"%s\": {\"ms\": %.6f, \"launches\": %llu, \"bytes\": %llu, \"family\": %d}",
+                 first ? "" : ", ", kv.first.c_str(), kv.second.ms, (unsigned long long)kv.second.launches,
+                 (unsigned long long)kv.second.bytes, kv.second.fam);
         js += tmp;
         first = false;
     }

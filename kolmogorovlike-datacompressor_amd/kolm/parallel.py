@@ -25,7 +25,29 @@ def shard_blocks(nblocks: int, rank: int, world: int) -> Tuple[int, int]:
     return first, base + (1 if rank < extra else 0)
 
 
-def gather_payloads(arena, nbytes: int, method_ids, dst: int = 0, group=None):
+class PendingGather:
+    """An in-flight gather_payloads(async_op=True): wait() blocks the host until the
+    collectives are done (the arena may be reused after that); result() waits, then
+    returns what the synchronous call would."""
+
+    def __init__(self, works, result):
+        self._works = works
+        self._result = result
+
+    def wait(self):
+        import torch
+        for w in self._works:
+            w.wait()
+        self._works = []
+        if torch.cuda.is_available():
+            torch.cuda.current_stream().synchronize()
+
+    def result(self):
+        self.wait()
+        return self._result
+
+
+def gather_payloads(arena, nbytes: int, method_ids, dst: int = 0, group=None, async_op: bool = False):
     """Gather every rank's payload arena prefix and method ids onto `dst`.
 
     arena: 1-D uint8 tensor (device for nccl, host for gloo) holding this rank's payloads
@@ -33,6 +55,10 @@ def gather_payloads(arena, nbytes: int, method_ids, dst: int = 0, group=None):
     method_ids: 1-D int32 tensor of this rank's per-block winners (same device).
     Returns on dst: (list of per-rank uint8 tensors trimmed to their nbytes,
     list of per-rank int32 method-id tensors); on other ranks (None, None).
+    async_op: the small size exchange completes here, the payload and id gathers are left
+    in flight and a PendingGather is returned (the caller must not overwrite `arena`
+    before its wait()) — bench.py double-buffers the arena so the gather of step k runs
+    over xGMI while step k+1 computes.
     """
     import torch
     import torch.distributed as dist
@@ -55,12 +81,13 @@ def gather_payloads(arena, nbytes: int, method_ids, dst: int = 0, group=None):
         id_list = [torch.empty(maxc, dtype=torch.int32, device=dev) for _ in range(world)]
     else:
         pay_list = id_list = None
-    dist.gather(arena[:maxb].contiguous(), pay_list, dst=dst, group=group)
-    dist.gather(ids, id_list, dst=dst, group=group)
-    if rank != dst:
-        return None, None
-    return ([p[: sizes[r]] for r, p in enumerate(pay_list)],
-            [i[: counts[r]] for r, i in enumerate(id_list)])
+    w1 = dist.gather(arena[:maxb].contiguous(), pay_list, dst=dst, group=group, async_op=async_op)
+    w2 = dist.gather(ids, id_list, dst=dst, group=group, async_op=async_op)
+    res = (None, None) if rank != dst else ([p[: sizes[r]] for r, p in enumerate(pay_list)],
+                                            [i[: counts[r]] for r, i in enumerate(id_list)])
+    if async_op:
+        return PendingGather([w for w in (w1, w2) if w is not None], res)
+    return res
 
 
 def assemble_container(block_size: int, total_len: int, per_rank_ids: Sequence[Sequence[int]],

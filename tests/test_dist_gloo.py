@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, data, bs, q):
+def _worker(rank, world, port, data, bs, q, use_async=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
@@ -47,7 +47,11 @@ def _worker(rank, world, port, data, bs, q):
         arena = torch.zeros(max(int(mx[0]), 1), dtype=torch.uint8)
         if blob:
             arena[: len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
-        got_p, got_i = gather_payloads(arena, len(blob), torch.tensor(mids, dtype=torch.int32), dst=0)
+        ids = torch.tensor(mids, dtype=torch.int32)
+        if use_async:  # bench.py's double-buffered form: the gather completes at wait()/result()
+            got_p, got_i = gather_payloads(arena, len(blob), ids, dst=0, async_op=True).result()
+        else:
+            got_p, got_i = gather_payloads(arena, len(blob), ids, dst=0)
         all_offs = [None] * world
         dist.all_gather_object(all_offs, offs)
         if rank == 0:
@@ -60,15 +64,16 @@ def _worker(rank, world, port, data, bs, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,bs,n", [(2, 4096, 4096 * 5 + 123), (2, 1000, 999), (3, 2048, 2048 * 4)])
-def test_gloo_sharded_reassembly(world, bs, n):
+@pytest.mark.parametrize("world,bs,n,use_async", [(2, 4096, 4096 * 5 + 123, False), (2, 1000, 999, False),
+                                                 (3, 2048, 2048 * 4, False), (2, 4096, 4096 * 3 + 7, True)])
+def test_gloo_sharded_reassembly(world, bs, n, use_async):
     import oracle as O
     from kolm import datagen as D
     data = (D.enwik_like(n // 2, seed=5) + bytes(n // 4) + D.splitmix64_bytes(n, seed=9))[:n]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, data, bs, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, data, bs, q, use_async)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)
