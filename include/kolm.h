@@ -52,8 +52,10 @@ extern "C" {
 #define KOLM_M_LZ77 7
 #define KOLM_M_LFSR 8
 #define KOLM_M_REPAIR 9
-#define KOLM_NCAND 10          /* ids 0..9 are computed on the GPU (10 = v2_new raises in PY) */
-#define KOLM_DEFAULT_MASK 0x3FFu  /* the reference's full candidate set, ids 0..9 */
+#define KOLM_M_V2NEW 10
+#define KOLM_NCAND 11          /* ids 0..10 are computed on the GPU */
+#define KOLM_DEFAULT_MASK 0x3FFu  /* the reference's candidate set as shipped, ids 0..9 (v2_new raises in PY) */
+#define KOLM_FULL_MASK 0x7FFu     /* + v2_new (id 10) with the automaton evaluated serially (opt-in) */
 #define KOLM_HOTPATH_MASK 0x1FFu  /* BBWT / MTF+Rice / LZ77 path of the north star, ids 0..8 */
 #define KOLM_REPAIR_MAX_BLOCK (1u << 22)  /* candidate 9 handles blocks up to 4 MiB */
 

@@ -128,8 +128,8 @@ __global__ __launch_bounds__(WG) void k_cheap_sizes(Geom geo, u32 tpb, const u8*
     }
 }
 
-__global__ void k_mdl(Geom geo, const u64* bits, const u32* lz_size, const u32* rp_result, u32* sizes,
-                      u32* method, const int32_t* force, u32 mask, u64* wsize) {
+__global__ void k_mdl(Geom geo, const u64* bits, const u32* lz_size, const u32* rp_result, const u32* v2_size,
+                      u32* sizes, u32* method, const int32_t* force, u32 mask, u64* wsize) {
     const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= geo.nb) return;
     const u32 n = geo.end(b) - geo.base(b);
@@ -145,6 +145,7 @@ __global__ void k_mdl(Geom geo, const u64* bits, const u32* lz_size, const u32* 
     sz[7] = lz_size ? lz_size[b] : 0xFFFFFFFFull;
     sz[8] = n + c[6];
     sz[9] = rp_result ? rp_result[(u64)b * RP_RS_N + RP_RS_SIZE] : 0xFFFFFFFFull;
+    sz[10] = v2_size ? v2_size[b] : 0xFFFFFFFFull;
     u32 best = 0;
     u64 bsz = ~0ull;
     for (u32 m = 0; m < NCAND; ++m) {
@@ -418,10 +419,11 @@ void launch_cheap_sizes(const EmitArgs& e, hipStream_t s) {
     k_cheap_sizes<<<tpb * e.geo.nb, WG, 0, s>>>(e.geo, tpb, e.text, e.bits);
 }
 
-void launch_mdl(const EmitArgs& e, const u32* lz_sizes, const u32* rp_result, u32* status, hipStream_t s) {
+void launch_mdl(const EmitArgs& e, const u32* lz_sizes, const u32* rp_result, const u32* v2_size, u32* status,
+                hipStream_t s) {
     if (!e.geo.nb) return;
     u64* wsize = reinterpret_cast<u64*>(e.tile_tmp2);  // nb u64 scratch
-    k_mdl<<<cdiv32(e.geo.nb, 256), 256, 0, s>>>(e.geo, e.bits, lz_sizes, rp_result, e.sizes, e.method, e.force,
+    k_mdl<<<cdiv32(e.geo.nb, 256), 256, 0, s>>>(e.geo, e.bits, lz_sizes, rp_result, v2_size, e.sizes, e.method, e.force,
                                                 e.cand_mask, wsize);
     k_offsets<<<1, WG, 0, s>>>(wsize, e.geo.nb, e.off, e.arena_cap, status);
 }

@@ -457,11 +457,11 @@ struct Pipeline {
         TScope t(c, KOLM_KT_LYNDON, "k_prevc", N * 3);  // flag 1 + text 1 + prevc 1 (FSL at factor starts)
         launch_prevc(geo, text, c->get<u8>("flag", N), c->get<u64>("FSL", N), c->get<u8>("prevc", N), c->active);
     }
-    u8* cyclic(const std::function<void()>& after_round0 = {}) {
+    u8* cyclic(const std::function<void()>& after_round0 = {}, u8* out = nullptr) {
         const u64 N = geo.N;
         u64* FSL = c->get<u64>("FSL", N);
         SortOut cyc = sort_pass(c, geo, text, true, FSL, c->get<u8>("FEd", N), after_round0);
-        u8* out = c->get<u8>("bbwt", N);
+        if (!out) out = c->get<u8>("bbwt", N);
         u8* prevc = c->get<u8>("prevc", N);
         if (prevc_ready)
             KOLM_HIP_CHECK(hipStreamWaitEvent(c->active, prevc_ready, 0));
@@ -568,7 +568,62 @@ int check_bounds(const u32* hb, u32 nb) {
     return KOLM_OK;
 }
 
-// Full batch: sizes of candidates 0..9, MDL, emission into d_arena.  Fixed blocks of bs
+// Candidate 10 (k_v2.hip): sizes of every block; U / L (planes and their BBWTs) stay
+// resident for the emission.
+struct V2State {
+    u8* U = nullptr;    // [8N] bit planes, plane block (b, j) at 8*base(b) + j*len(b)
+    u8* L = nullptr;    // [8N] their BBWTs
+    u32* pb = nullptr;  // [8nb + 1] plane block bounds (device)
+    u32* meta = nullptr;
+    u32* size = nullptr;
+};
+
+bool v2_stage(kolm_ctx* c, const Geom& geo, const u8* d_text, hipStream_t s, V2State& v) {
+    const u64 N = geo.N;
+    const u32 nb = geo.nb;
+    if (8 * N >= (1ull << 32)) {
+        set_err("v2_new (candidate 10): batches up to 512 MiB");
+        return false;
+    }
+    v.U = c->get<u8>("v2U", 8 * N + 64);
+    v.L = c->get<u8>("v2L", 8 * N + 64);
+    u32* sel = c->get<u32>("v2sel", nb);
+    launch_v2_sizes(geo, d_text, c->get<u32>("v2hist", (u64)nb * 13 * 256), sel, v.U, s, c->kt());
+    // plane block bounds
+    std::vector<u32> hb(8 * (u64)nb + 1);
+    for (u32 b = 0; b < nb; ++b) {
+        const u32 base = geo.base(b), len = geo.end(b) - base;
+        for (u32 j = 0; j < 8; ++j) hb[8 * (u64)b + j] = 8 * base + j * len;
+    }
+    hb[8 * (u64)nb] = (u32)(8 * N);
+    v.pb = c->get<u32>("v2pb", 8 * (u64)nb + 1);
+    KOLM_HIP_CHECK(hipMemcpyAsync(v.pb, hb.data(), sizeof(u32) * hb.size(), hipMemcpyHostToDevice, s));
+    // BBWT of the planes in groups of blocks (< 2^28 plane positions per group)
+    for (u32 b0 = 0; b0 < nb;) {
+        u32 b1 = b0 + 1;
+        while (b1 < nb && (u64)hb[8 * (u64)(b1 + 1)] - hb[8 * (u64)b0] <= (1ull << 28)) ++b1;
+        const u32 nq = 8 * (b1 - b0);
+        std::vector<u32> gb(nq + 1);
+        for (u32 i = 0; i <= nq; ++i) gb[i] = hb[8 * (u64)b0 + i] - hb[8 * (u64)b0];
+        Geom pg;
+        const u32 vs = geom_var_shift(gb.data(), nq);
+        geom_init_var(pg, gb.data(), nq, c->get<u32>("v2vb", (u64)nq + 1), c->get<u32>("v2vmap", (gb[nq] >> vs) + 2), vs, s);
+        Pipeline P{c, pg, v.U + hb[8 * (u64)b0]};
+        c->active = s;
+        P.lyndon();
+        P.cyclic({}, v.L + hb[8 * (u64)b0]);
+        b0 = b1;
+    }
+    u64* rbits = c->get<u64>("v2rbits", 8 * (u64)nb * 16);
+    u32* b1v = c->get<u32>("v2b1", 8 * (u64)nb);
+    launch_v2_runs(8 * nb, v.pb, v.L, rbits, b1v, s, c->kt(), 8 * N);
+    v.meta = c->get<u32>("v2meta", (u64)nb * V2_META);
+    v.size = c->get<u32>("v2size", nb);
+    launch_v2_size(geo, sel, rbits, b1v, v.meta, v.size, s);
+    return true;
+}
+
+// Full batch: sizes of candidates 0..10, MDL, emission into d_arena.  Fixed blocks of bs
 // bytes over [0, N), or (h_bounds != null) the nbv content-defined blocks
 // [h_bounds[i], h_bounds[i+1]) (PY:2213 compress_blocks_cdc).
 int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_bounds, u32 nbv, u32 mask,
@@ -735,6 +790,14 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     e.tile_tmp = c->get<u32>("tile_tmp", 2 * ntiles + 16);
     e.tile_tmp2 = c->get<u32>("tile_tmp2", 2 * ntiles + 2 * nb + 16);
     e.rice_k = 2;
+    // candidate 10 (v2_new, opt-in): automaton + bit planes, the BBWT of every plane by the
+    // same pipeline (groups of blocks whose 8 planes stay below 2^28 positions), runs and
+    // Rice sizes; the plane BBWTs reuse the sort scratch (the blocks' own sort is done)
+    const bool want_v2 = (mask >> KOLM_M_V2NEW) & 1u;
+    V2State v2{};
+    if (want_v2) {
+        if (!v2_stage(c, geo, d_text, s, v2)) return KOLM_EARG;
+    }
     KOLM_HIP_CHECK(hipEventRecord(ev[2], s));
     KOLM_HIP_CHECK(hipStreamWaitEvent(s, ej[1], 0));
     KOLM_HIP_CHECK(hipEventRecord(ev[3], s));
@@ -743,7 +806,8 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     if (want_rp) KOLM_HIP_CHECK(hipStreamWaitEvent(s, c->evr[0], 0));
     {
         TScope t(c, KOLM_KT_SIZES, "k_mdl+offsets", (u64)nb * 120);
-        launch_mdl(e, want_lz ? z.lz_size : nullptr, want_rp ? rpa.result : nullptr, cnt + C_STATUS, s);
+        launch_mdl(e, want_lz ? z.lz_size : nullptr, want_rp ? rpa.result : nullptr, want_v2 ? v2.size : nullptr,
+                   cnt + C_STATUS, s);
     }
     std::vector<u64> off(nb + 1);
     std::vector<u32> rpres(want_rp ? (u64)nb * RP_RS_N : 0);
@@ -793,6 +857,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         launch_emit_rice(e, s);
         if (want_lz) launch_lz_emit(z, e.method, e.off, d_arena, s);
         if (want_rp) launch_rp_emit(rpa, e.method, e.off, d_arena, s);
+        if (want_v2) launch_v2_emit(geo, v2.pb, v2.meta, e.method, e.off, v2.U, v2.L, d_arena, s);
     }
     KOLM_HIP_CHECK(hipEventRecord(ev[4], s));
     if (h_sizes)
@@ -1051,7 +1116,7 @@ int kolm_encode_blocks_device(kolm_ctx* c, const uint8_t* d_data, uint64_t total
                               uint64_t arena_cap, uint32_t* h_sizes, uint32_t* h_method, uint64_t* h_off,
                               kolm_stats* stats) {
     if (!c || (!d_data && total) || !d_arena) return KOLM_EARG;
-    if ((cand_mask & KOLM_DEFAULT_MASK) == 0) return KOLM_EARG;
+    if ((cand_mask & KOLM_FULL_MASK) == 0) return KOLM_EARG;
     if (reinterpret_cast<uintptr_t>(d_arena) & 3) {
         set_err("device arena must be 4-byte aligned");
         return KOLM_EARG;
@@ -1059,7 +1124,7 @@ int kolm_encode_blocks_device(kolm_ctx* c, const uint8_t* d_data, uint64_t total
     return guarded([&] {
         std::lock_guard<std::mutex> g(c->mu);
         KOLM_HIP_CHECK(hipSetDevice(c->device));
-        return encode_batch(c, d_data, total, block_size, nullptr, 0, cand_mask & KOLM_DEFAULT_MASK, force_method,
+        return encode_batch(c, d_data, total, block_size, nullptr, 0, cand_mask & KOLM_FULL_MASK, force_method,
                             d_arena, arena_cap, h_sizes, h_method, h_off, stats);
     });
 }
@@ -1071,7 +1136,7 @@ int kolm_encode_blocks(const uint8_t* data, const uint64_t* starts, const uint32
     if (!c) return KOLM_ENOINIT;
     if (nblocks && (!data || !starts || !lens)) return KOLM_EARG;
     if (!payload_off) return KOLM_EARG;
-    if ((cand_mask & KOLM_DEFAULT_MASK) == 0) return KOLM_EARG;
+    if ((cand_mask & KOLM_FULL_MASK) == 0) return KOLM_EARG;
     // contiguous non-empty blocks; the fixed geometry when every block but a shorter last
     // one has lens[0] bytes, the variable one otherwise (content-defined chunks)
     uint64_t total = 0;
@@ -1105,7 +1170,7 @@ int kolm_encode_blocks(const uint8_t* data, const uint64_t* starts, const uint32
         const u64 dcap = (has_raw ? total : 9 * total) + 64 * (u64)nblocks + 256;
         u8* arena = c->get<u8>("arena", dcap);
         std::vector<u64> off(nblocks + 1);
-        int r = encode_batch(c, d, total, bs, fixed ? nullptr : hb.data(), nblocks, cand_mask & KOLM_DEFAULT_MASK,
+        int r = encode_batch(c, d, total, bs, fixed ? nullptr : hb.data(), nblocks, cand_mask & KOLM_FULL_MASK,
                              force_method, arena, dcap, sizes, method, off.data(), stats);
         if (r) return r;
         if (off[nblocks] > arena_cap) {
@@ -1125,7 +1190,7 @@ int kolm_encode_blocks_multi(int ngpu, const uint8_t* data, uint64_t total, uint
                              uint32_t cand_mask, const int32_t* force_method, uint32_t* sizes, uint32_t* method,
                              uint8_t* payload_arena, uint64_t arena_cap, uint64_t* payload_off, kolm_stats* stats) {
     if (ngpu < 1 || (total && !data) || !payload_off || block_size == 0) return KOLM_EARG;
-    if ((cand_mask & KOLM_DEFAULT_MASK) == 0) return KOLM_EARG;
+    if ((cand_mask & KOLM_FULL_MASK) == 0) return KOLM_EARG;
     const u64 nb64 = (total + block_size - 1) / block_size;
     if (nb64 > 0xFFFFFFFFull) return KOLM_EARG;
     const u32 nb = (u32)nb64;
@@ -1179,7 +1244,7 @@ int kolm_encode_blocks_multi(int ngpu, const uint8_t* data, uint64_t total, uint
             const u64 dcap = (has_raw ? n : 9 * n) + 64 * (u64)nbr + 256;
             u8* arena = c->get<u8>("arena", dcap);
             P.off.assign(nbr + 1, 0);
-            int rc = encode_batch(c, d, n, block_size, nullptr, 0, cand_mask & KOLM_DEFAULT_MASK,
+            int rc = encode_batch(c, d, n, block_size, nullptr, 0, cand_mask & KOLM_FULL_MASK,
                                   force_method ? force_method + b0[r] : nullptr, arena, dcap,
                                   sizes ? sizes + (u64)b0[r] * KOLM_NCAND : nullptr, method ? method + b0[r] : nullptr,
                                   P.off.data(), stats ? &P.st : nullptr);
@@ -1358,7 +1423,7 @@ int kolm_encode_blocks_device_var(kolm_ctx* c, const uint8_t* d_data, const uint
                                   uint64_t arena_cap, uint32_t* h_sizes, uint32_t* h_method, uint64_t* h_off,
                                   kolm_stats* stats) {
     if (!c || !h_bounds || !d_arena || (nblocks && !d_data)) return KOLM_EARG;
-    if ((cand_mask & KOLM_DEFAULT_MASK) == 0) return KOLM_EARG;
+    if ((cand_mask & KOLM_FULL_MASK) == 0) return KOLM_EARG;
     if (reinterpret_cast<uintptr_t>(d_arena) & 3) {
         set_err("device arena must be 4-byte aligned");
         return KOLM_EARG;
@@ -1371,7 +1436,7 @@ int kolm_encode_blocks_device_var(kolm_ctx* c, const uint8_t* d_data, const uint
             if (stats) *stats = kolm_stats{};
             return KOLM_OK;
         }
-        return encode_batch(c, d_data, 0, 0, h_bounds, nblocks, cand_mask & KOLM_DEFAULT_MASK, force_method, d_arena,
+        return encode_batch(c, d_data, 0, 0, h_bounds, nblocks, cand_mask & KOLM_FULL_MASK, force_method, d_arena,
                             arena_cap, h_sizes, h_method, h_off, stats);
     });
 }

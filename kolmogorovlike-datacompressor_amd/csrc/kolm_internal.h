@@ -25,7 +25,7 @@ constexpr int LZ_WINDOW = 4096;   // PY:1723 WINDOW_MAX
 constexpr int LZ_MIN = 3;         // PY:1724 MIN_MATCH
 constexpr int LZ_CAP = 32;        // per-lane capped compare; longer candidates are extended by the wave
 constexpr int MTF_CHUNK = 1024;   // bytes replayed per thread by the MTF kernel
-constexpr u32 NCAND = 10;         // candidate ids 0..9 computed on the device
+constexpr u32 NCAND = 11;         // candidate ids 0..10 computed on the device (10 = v2_new, opt-in)
 
 // Segment of the suffix array still to be refined: SA[start .. start+len).  Bit 31 of
 // len (SEG_FIRST) marks a segment that begins at the start of its round group, so its
@@ -299,11 +299,26 @@ struct EmitArgs {
 };
 // xor / lfsr_pred size counters (5, 6) only, from the text: runs on the index stream
 void launch_cheap_sizes(const EmitArgs& e, hipStream_t s);
-void launch_mdl(const EmitArgs& e, const u32* lz_sizes, const u32* rp_result, u32* status, hipStream_t s);
+void launch_mdl(const EmitArgs& e, const u32* lz_sizes, const u32* rp_result, const u32* v2_size, u32* status,
+                hipStream_t s);
 void launch_emit_simple(const EmitArgs& e, hipStream_t s);
 void launch_emit_rice(const EmitArgs& e, hipStream_t s);
 void launch_rice_only(const Geom& geo, const u8* in, int k, u8* out, u32* tile_tmp, u32* tile_tmp2,
                       u32* out_size, hipStream_t s);
+
+// ---- k_v2.hip: candidate 10 (v2_new, opt-in: the reference raises NameError) ----
+constexpr u32 V2_META = 11;  // per-block plane decisions (k_v2_size)
+// automaton histograms + choice per block, mapped bytes as 8 plane blocks per block in U
+void launch_v2_sizes(const Geom& geo, const u8* text, u32* hist, u32* sel, u8* U, hipStream_t s,
+                     KTimer* kt = nullptr);
+// per plane block (bounds d_pb[nplanes + 1], absolute in L): Rice bits of the runs for k 0..15, first bit
+void launch_v2_runs(u32 nplanes, const u32* d_pb, const u8* L, u64* rbits, u32* b1, hipStream_t s, KTimer* kt,
+                    u64 bytes);
+void launch_v2_size(const Geom& geo, const u32* sel, const u64* rbits, const u32* b1, u32* meta, u32* size,
+                    hipStream_t s);
+// payloads of the blocks whose method is 10 (method == null: every block)
+void launch_v2_emit(const Geom& geo, const u32* d_pb, const u32* meta, const u32* method, const u64* off,
+                    const u8* U, const u8* L, u8* arena, hipStream_t s);
 
 // ---- k_lz77.hip ----
 // k_lz_local: a workgroup owns LZL_HOME consecutive positions

@@ -19,8 +19,11 @@ library or a HIP device the encode functions raise ``KolmUnavailable``.
 Candidate ids are the reference's (the list index is the on-disk method id):
 0 raw, 1 xor, 2 bbwt, 3 bbwt_bp, 4 bbwt_nib, 5 bbwt_br, 6 bbwt_gray, 7 lz77,
 8 lfsr_pred, 9 repair, 10 v2_new.  v2_new always raises in PY (NameError)
-and is never selected, so the MDL argmin runs over ids 0..9 exactly as PY's does and
-compress_blocks_fixed() returns PY's container byte for byte.  Re-Pair (9) is the exact
+and is never selected, so by default the MDL argmin runs over ids 0..9 exactly as PY's
+does and compress_blocks_fixed() returns PY's container byte for byte.  ``G_V2_NEW =
+True`` (or ``v2_new=True``) enables id 10 as the pipeline defines it with its automaton
+evaluated serially (PY:1033-1035): encode_new_pipeline on the GPU
+(csrc/k_v2.hip), bit-exact against PY run that way.  Re-Pair (9) is the exact
 batched device Re-Pair of csrc/repair_core.h (blocks up to 4 MiB).  ``hot_path=True``
 restricts the candidates to ids 0..8 (the BBWT / MTF+Rice / LZ77 path of the north star;
 ids unchanged, containers still decodable by the reference).
@@ -40,17 +43,19 @@ __all__ = [
     "compress_blocks_fixed", "compress_blocks_cdc", "cdc_fast_boundaries_strict", "decompress",
     "fixed_boundaries", "bbwt_forward", "mtf_encode",
     "rice_encode", "encode_lz77", "encode_bbwt_mtf_rice", "encode_raw", "encode_xor",
-    "encode_lfsr_predict", "repair_compress", "uleb128_encode", "uleb128_decode_stream", "CANDIDATE_NAMES",
+    "encode_lfsr_predict", "repair_compress", "encode_new_pipeline", "uleb128_encode", "uleb128_decode_stream", "CANDIDATE_NAMES",
     "KolmUnavailable", "KolmError", "last_stats",
 ]
 
 CANDIDATE_NAMES = ["raw", "xor", "bbwt", "bbwt_bp", "bbwt_nib", "bbwt_br", "bbwt_gray", "lz77",
                    "lfsr_pred", "repair", "v2_new"]
-GPU_CANDIDATES = 10
+GPU_CANDIDATES = 11
 
 # CLI-style switches of the reference (PY:92-96); ids stay stable (CPP:3750-3775 semantics)
 G_NO_LZ77: bool = False
 G_ONLY_METHOD: Optional[str] = None
+# candidate 10 (v2_new) with its automaton evaluated serially; PY as shipped raises instead
+G_V2_NEW: bool = False
 
 _last_stats: Dict[str, Any] = {}
 
@@ -177,8 +182,15 @@ def repair_compress(block: bytes) -> Tuple[bytes, Dict[str, Any]]:
     return payloads[0], {"nrules": st.get("rp_rules"), "final_len": st.get("rp_final"), "terminals": 256}
 
 
+def encode_new_pipeline(block: bytes) -> bytes:
+    """v2_new (PY:1498-1576) with the automaton evaluated serially, on the GPU."""
+    return _batched_single(bytes(block), 10)
+
+
 def _v2_new(block: bytes):
-    raise NameError("v2_new raises in the reference (PY:1037-1043); never selected")
+    if not G_V2_NEW:
+        raise NameError("v2_new raises in the reference (PY:1037-1043); never selected")
+    return encode_new_pipeline(block), {}
 
 
 def _select_encoders() -> List[Tuple[Callable[[bytes], Tuple[bytes, Dict[str, Any]]], str]]:
@@ -203,17 +215,18 @@ def _select_encoders() -> List[Tuple[Callable[[bytes], Tuple[bytes, Dict[str, An
     def disabled(_b):
         raise RuntimeError("candidate disabled")
 
-    return [(e if (i < GPU_CANDIDATES and (mask >> i) & 1) or i >= GPU_CANDIDATES else disabled, n)
-            for i, (e, n) in enumerate(encs)]
+    return [(e if (mask >> i) & 1 or (i == 10 and not G_V2_NEW) else disabled, n) for i, (e, n) in enumerate(encs)]
 
 
 def _select_decoders():
     """Decoder registry aligned with the encoder ids (PY:2194-2207)."""
-    return [(lambda payload, n, meta=None, _m=m: decode_block(_m, payload, n)) for m in range(10)]
+    return [(lambda payload, n, meta=None, _m=m: decode_block(_m, payload, n)) for m in range(11)]
 
 
-def candidate_mask(hot_path: bool = False) -> int:
+def candidate_mask(hot_path: bool = False, v2_new: Optional[bool] = None) -> int:
     mask = _lib.KOLM_HOTPATH_MASK if hot_path else _lib.KOLM_DEFAULT_MASK
+    if (G_V2_NEW if v2_new is None else v2_new) and not hot_path:
+        mask |= 1 << 10
     if G_NO_LZ77:
         mask &= ~(1 << 7)
     if G_ONLY_METHOD is not None:
@@ -232,13 +245,13 @@ def candidate_mask(hot_path: bool = False) -> int:
 # ---------------------------------------------------------------------------
 
 def encode_blocks(data: bytes, block_size: int, cand_mask: Optional[int] = None, devices: int = 1,
-                  hot_path: bool = False):
+                  hot_path: bool = False, v2_new: Optional[bool] = None):
     """Batched device MDL over fixed blocks: (method_ids, orig_lens, payloads, sizes).
     devices > 1 shards the blocks over that many GPUs of this process."""
     if block_size <= 0:
         raise ValueError("block_size must be positive")
     global _last_stats
-    mask = candidate_mask(hot_path) if cand_mask is None else cand_mask
+    mask = candidate_mask(hot_path, v2_new) if cand_mask is None else cand_mask
     n = len(data)
     if n == 0:
         return [], [], [], None
@@ -251,22 +264,24 @@ def encode_blocks(data: bytes, block_size: int, cand_mask: Optional[int] = None,
     return [int(m) for m in method], orig, payloads, sizes
 
 
-def compress_blocks_fixed(data: bytes, block_size: int = 8192, devices: int = 1, hot_path: bool = False) -> bytes:
+def compress_blocks_fixed(data: bytes, block_size: int = 8192, devices: int = 1, hot_path: bool = False,
+                          v2_new: Optional[bool] = None) -> bytes:
     """Fixed-size chunking + per-block MDL selection + KOLR container (PY:2332-2445).
     `devices` (not in PY) spreads the blocks over that many GPUs of this process;
-    `hot_path` (not in PY) restricts the candidates to ids 0..8."""
+    `hot_path` (not in PY) restricts the candidates to ids 0..8; `v2_new` (default
+    G_V2_NEW) adds candidate 10 (see the module docstring)."""
     if block_size <= 0:
         raise ValueError("block_size must be positive")
     n = len(data)
     nb = (n + block_size - 1) // block_size
     if nb > 0xFFFF:
         raise struct.error("'H' format requires 0 <= number <= 65535")
-    mids, orig, payloads, _ = encode_blocks(data, block_size, devices=devices, hot_path=hot_path)
+    mids, orig, payloads, _ = encode_blocks(data, block_size, devices=devices, hot_path=hot_path, v2_new=v2_new)
     return write_container(MODE_FIXED, block_size, n, mids, orig, payloads)
 
 
 def compress_blocks_cdc(data: bytes, min_size: int = 4096, avg_size: int = 8192, max_size: int = 16384,
-                        hot_path: bool = False) -> bytes:
+                        hot_path: bool = False, v2_new: Optional[bool] = None) -> bytes:
     """FastCDC chunking + per-block MDL selection + KOLR container in CDC mode
     (PY:2213-2326): boundaries and every candidate on the GPU, one batched device call for
     all chunks (variable block geometry), the TOC on the host.  `hot_path` (not in PY)
@@ -279,7 +294,7 @@ def compress_blocks_cdc(data: bytes, min_size: int = 4096, avg_size: int = 8192,
     if n == 0:
         return write_container(MODE_CDC, avg_size, 0, [], [], [])
     edges = [s for s, _ in bounds] + [n]
-    _, method, payloads, st = _lib.encode_blocks_var(bytes(data), edges, candidate_mask(hot_path))
+    _, method, payloads, st = _lib.encode_blocks_var(bytes(data), edges, candidate_mask(hot_path, v2_new))
     _last_stats = st
     return write_container(MODE_CDC, avg_size, n, [int(m) for m in method], [e - s for s, e in bounds], payloads)
 

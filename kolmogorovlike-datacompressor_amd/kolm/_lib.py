@@ -19,8 +19,9 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KOLM_LIB") or os.path.join(HERE, "libkolm_hip.so")  # KOLM_LIB: A/B builds
 
-KOLM_NCAND = 10
-KOLM_DEFAULT_MASK = 0x3FF   # the reference's candidates 0..9 (kolm.h)
+KOLM_NCAND = 11
+KOLM_DEFAULT_MASK = 0x3FF   # the reference's candidates 0..9 as shipped (kolm.h)
+KOLM_FULL_MASK = 0x7FF      # + v2_new (id 10), automaton evaluated serially (opt-in)
 KOLM_HOTPATH_MASK = 0x1FF  # BBWT / MTF+Rice / LZ77 path, ids 0..8
 KOLM_REPAIR_MAX_BLOCK = 1 << 22
 ERRORS = {-1: "bad argument", -2: "capacity too small", -3: "HIP error", -4: "collective error",

@@ -226,6 +226,133 @@ def repair_decompress(data: bytes, orig_len: int) -> bytes:  # PY:1913-1978
 BBWT_FLAGS = {2: 0, 3: 1, 4: 4, 5: 8, 6: 16}
 
 
+# ---- v2_new (id 10): decode_new_pipeline PY:1578-1648 + circuit_map_automaton_inverse
+# PY:1056-1092.  Every model predicts byte i from the decoded bytes before it, so the
+# inverse is a sequential recurrence (PY's own backward loops).
+def _dil(x: int) -> int:
+    return ((((x << 1) & 0xFE) | x) | (((x >> 1) & 0x7F) | x)) & 0xFF
+
+
+def _ero(x: int) -> int:
+    return ~_dil(~x & 0xFF) & 0xFF
+
+
+def _v2_inverse(y: bytes, mode: int, param: int) -> bytes:
+    n = len(y)
+    if mode == 0 or mode > 5 or n == 0 or (mode == 1 and param == 0):
+        return bytes(y)
+    r = bytearray(n)
+    for i in range(n):
+        if mode == 1:    # Delta-k PY:679-690
+            p = 0 if i < param else r[i - param]
+        elif mode in (2, 3):  # Gray family PY:727-752, nibble interleave PY:805-826
+            if i == 0:
+                p = 0
+            elif i == 1:
+                p = r[0]
+            else:
+                a, b = r[i - 1], r[i - 2]
+                if mode == 3:
+                    p = (a & 0xF0) | (b & 0x0F)  # mux(select, cross, run) == cross for every a, b
+                else:
+                    v = param & 3
+                    x = a if v == 0 else b if v == 1 else (a ^ b) if v == 2 else (a | b)
+                    p = x ^ (x >> 1)
+        elif mode == 4:  # Majority-of-3 PY:849-866
+            if i == 0:
+                p = 0
+            elif i < 3:
+                p = r[i - 1]
+            else:
+                a, b, c = r[i - 1], r[i - 2], r[i - 3]
+                p = (a & b) | (a & c) | (b & c)
+        else:            # Morpho-Predict PY:887-900
+            if i == 0:
+                p = 0
+            else:
+                d = r[i - 1]
+                m = _ero(_dil(d)) if (param & 1) == 0 else _dil(_ero(d))
+                e = _dil(d) ^ _ero(d)
+                p = (m & e) | (d & ~e & 0xFF)
+        r[i] = y[i] ^ p
+    return bytes(r)
+
+
+def _rice_runs_until(bits: np.ndarray, pos: int, k: int, target: int) -> Tuple[List[int], int]:
+    """PY:1462-1487 _rice_decode_until_len over an unpacked bit array from bit `pos`."""
+    runs: List[int] = []
+    total = 0
+    nb = bits.size
+    zeros = np.flatnonzero(bits[pos:] == 0) + pos
+    zi = 0
+    while total < target:
+        zi = int(np.searchsorted(zeros, pos, side="left"))
+        if zi >= zeros.size:
+            raise ValueError("BitReader: out of data")
+        z = int(zeros[zi])
+        q = z - pos
+        pos = z + 1
+        r = 0
+        if k:
+            if pos + k > nb:
+                raise ValueError("BitReader: out of data")
+            for t in range(k):
+                r = (r << 1) | int(bits[pos + t])
+            pos += k
+        val = (q << k) | r
+        if val <= 0:
+            raise ValueError("Invalid Rice value (non-positive)")
+        runs.append(val)
+        total += val
+        if total > target:
+            raise ValueError("RLE overrun: sum(runs) > target_len")
+    return runs, pos
+
+
+def decode_new_pipeline(payload: bytes, n: int) -> bytes:  # PY:1578-1648
+    if n == 0:
+        return b""
+    if len(payload) < 3:
+        raise ValueError("V2 slim header truncated")
+    h0 = payload[0]
+    mode, plen = (h0 >> 5) & 7, h0 & 7
+    if plen > 4:
+        raise ValueError("V2 slim header invalid param_len (>4)")
+    if len(payload) < 1 + plen + 2:
+        raise ValueError("V2 slim header truncated (param/raw/b1)")
+    param = int.from_bytes(payload[1:1 + plen], "little")
+    pos = 1 + plen
+    raw_mask, b1_mask = payload[pos], payload[pos + 1]
+    pos += 2
+    nenc = 8 - bin(raw_mask).count("1")
+    if pos + nenc > len(payload):
+        raise ValueError("V2 slim header k_list truncated")
+    ks = list(payload[pos:pos + nenc])
+    data = payload[pos + nenc:]
+    bits = np.unpackbits(np.frombuffer(data, dtype=np.uint8)) if data else np.zeros(0, np.uint8)
+    dpos = 0  # byte position in data
+    planes = np.zeros((8, n), dtype=np.uint8)
+    ki = 0
+    for j in range(8):
+        if (raw_mask >> j) & 1:
+            need = (n + 7) // 8
+            if dpos + need > len(data):
+                raise ValueError("V2 payload truncated in RAW plane")
+            planes[j] = np.unpackbits(np.frombuffer(data[dpos:dpos + need], dtype=np.uint8))[:n]
+            dpos += need
+        else:
+            k = ks[ki]
+            ki += 1
+            runs, bitpos = _rice_runs_until(bits, 8 * dpos, k, n)
+            dpos = (bitpos + 7) // 8
+            b = (b1_mask >> j) & 1
+            lbits = np.repeat((np.arange(len(runs)) + b) & 1, runs).astype(np.uint8)
+            u = np.frombuffer(bbwt_inverse(lbits.tobytes()), dtype=np.uint8)
+            planes[j, :min(n, u.size)] = u[:n]
+    mapped = np.packbits(planes.T, axis=1).ravel().tobytes()
+    return _v2_inverse(mapped, mode, param)
+
+
 def decode_block(mid: int, payload: bytes, n: int) -> bytes:
     """Decoder registry aligned with the encoder ids (PY:2194-2207)."""
     if mid == 0:
@@ -240,4 +367,6 @@ def decode_block(mid: int, payload: bytes, n: int) -> bytes:
         return decode_lfsr(payload, n)
     if mid == 9:
         return repair_decompress(payload, n)
+    if mid == 10:
+        return decode_new_pipeline(payload, n)
     raise ValueError(f"Unknown method_id {mid}")

@@ -14,6 +14,7 @@
 // C ABI (ctypes): all outputs caller-allocated; functions return the number of bytes
 // written, or -1 when the capacity is too small.
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -312,6 +313,163 @@ Bytes repair_compress(const u8* blk, int64_t n) {
     return out;
 }
 
+// ---------------------------------------------------------------------------------
+// v2_new (candidate 10): encode_new_pipeline PY:1498-1576 with the automaton evaluated
+// serially (circuit_map_automaton_forward(parallel=False), PY:1013-1054; as shipped, PY
+// calls it with parallel=True and raises NameError, SURVEY §0.3, so PY itself never
+// emits id 10 — this is the pipeline's defined result).
+// ---------------------------------------------------------------------------------
+// gates on bytes (PY:550-626): xor/or/not reduce to the plain bit operations
+inline u8 gray8(u8 v) { return (u8)(v ^ (v >> 1)); }                       // PY:596
+inline u8 maj3(u8 a, u8 b, u8 c) { return (u8)((a & b) | (a & c) | (b & c)); }  // PY:599-604
+inline u8 mux8(u8 m, u8 a, u8 b) { return (u8)((a & m) | (b & (u8)~m)); }       // PY:592-594
+inline u8 dilate1(u8 x) { return (u8)((((x << 1) & 0xFE) | x) | (((x >> 1) & 0x7F) | x)); }  // PY:608-615
+inline u8 erode1(u8 x) { return (u8)(~dilate1((u8)~x) & 0xFF); }                 // PY:617-618
+inline u8 edge1(u8 x) { return (u8)(dilate1(x) ^ erode1(x)); }                   // PY:626-627
+inline u8 nib_hi_eq(u8 a, u8 b) { return ((a ^ b) & 0xF0) ? 0x00 : 0xF0; }      // PY:754-767
+inline u8 nib_lo_eq(u8 a, u8 b) { return ((a ^ b) & 0x0F) ? 0x00 : 0x0F; }      // PY:769-778
+
+// predictor of byte i from the raw bytes before it (every model is out[i] = raw[i] ^ pred)
+inline u8 v2_pred(int code, int param, const u8* r, int64_t i) {
+    switch (code) {
+        case 1:  // Delta-k PY:664-690
+            return i < param ? 0 : r[i - param];
+        case 2: {  // Gray family PY:698-752
+            if (i == 0) return 0;
+            if (i == 1) return r[0];
+            const u8 p1 = r[i - 1], p2 = r[i - 2];
+            switch (param & 3) {
+                case 0: return gray8(p1);
+                case 1: return gray8(p2);
+                case 2: return gray8((u8)(p1 ^ p2));
+                default: return gray8((u8)(p1 | p2));
+            }
+        }
+        case 3: {  // Nibble-MUX interleave PY:780-826
+            if (i == 0) return 0;
+            if (i == 1) return r[0];
+            const u8 a = r[i - 1], b = r[i - 2];
+            const u8 cross = (u8)((a & 0xF0) | (b & 0x0F));
+            const u8 sel = (u8)((((u8)~nib_hi_eq(a, b)) & 0xF0) | (((u8)~nib_lo_eq(a, b)) & 0x0F));
+            return mux8(sel, cross, a);
+        }
+        case 4:  // Majority-of-3 PY:828-866
+            if (i == 0) return 0;
+            if (i < 3) return r[i - 1];
+            return maj3(r[i - 1], r[i - 2], r[i - 3]);
+        case 5: {  // Morpho-Predict PY:868-900 (param 0: close1, 1: open1)
+            if (i == 0) return 0;
+            const u8 d = r[i - 1];
+            const u8 m = (param & 1) == 0 ? erode1(dilate1(d)) : dilate1(erode1(d));
+            return mux8(edge1(d), m, d);
+        }
+        default:
+            return 0;
+    }
+}
+
+Bytes v2_forward(const u8* r, int64_t n, int code, int param) {
+    Bytes out(n);
+    for (int64_t i = 0; i < n; ++i) out[i] = (u8)(r[i] ^ v2_pred(code, param, r, i));
+    return out;
+}
+
+// PY:631-643 zero_order_entropy_bits_per_byte (same summation order, C log2 as CPython)
+double h0_bits(const Bytes& d) {
+    if (d.empty()) return 0.0;
+    int64_t f[256] = {0};
+    for (u8 v : d) f[v]++;
+    const double n = (double)d.size();
+    double H = 0.0;
+    for (int i = 0; i < 256; ++i)
+        if (f[i]) {
+            const double p = (double)f[i] / n;
+            H -= p * std::log2(p);
+        }
+    return H;
+}
+
+// PY:1013-1054 (parallel=False) + PY:936-1011: candidates in `kinds` order, folded by
+// _pick_better (H0 lower by more than 1e-12 wins; within 1e-12 the smaller (code, param))
+void v2_automaton(const u8* r, int64_t n, int& code, int& param, Bytes& mapped) {
+    static const int K[13][2] = {{0, 0}, {1, 1}, {1, 2}, {1, 3}, {1, 4}, {2, 0}, {2, 1},
+                                 {2, 2}, {2, 3}, {3, 0}, {4, 0}, {5, 0}, {5, 1}};
+    double bh = 0;
+    for (int c = 0; c < 13; ++c) {
+        Bytes y = v2_forward(r, n, K[c][0], K[c][1]);
+        if (K[c][0] == 0) y.assign(r, r + n);
+        const double h = h0_bits(y);
+        bool take = c == 0;
+        if (!take) {
+            if (h < bh - 1e-12) take = true;
+            else if (std::fabs(h - bh) <= 1e-12 &&
+                     (K[c][0] < code || (K[c][0] == code && K[c][1] < param))) take = true;
+        }
+        if (take) { bh = h; code = K[c][0]; param = K[c][1]; mapped.swap(y); }
+    }
+}
+
+// PY:1413-1421 rice_encode over arbitrary non-negative integers
+Bytes rice_encode_u(const std::vector<uint64_t>& seq, int k) {
+    BitWriter bw;
+    for (uint64_t v : seq) {
+        const uint64_t q = v >> k, r = v & ((1ull << k) - 1);
+        for (uint64_t i = 0; i < q; ++i) bw.bit(1);
+        bw.bit(0);
+        for (int i = k - 1; i >= 0; --i) bw.bit((int)((r >> i) & 1));
+    }
+    bw.pad();
+    return bw.buf;
+}
+
+Bytes encode_new_pipeline(const u8* blk, int64_t n) {
+    if (n == 0) return Bytes();
+    int code = 0, param = 0;
+    Bytes mapped;
+    v2_automaton(blk, n, code, param, mapped);
+    const uint32_t mp = (uint32_t)param;
+    const int plen = mp == 0 ? 0 : mp <= 0xFF ? 1 : mp <= 0xFFFF ? 2 : mp <= 0xFFFFFF ? 3 : 4;
+    int raw_mask = 0, b1_mask = 0;
+    std::vector<int> ks;
+    Bytes payload;
+    for (int j = 0; j < 8; ++j) {
+        Bytes U(n);
+        for (int64_t t = 0; t < n; ++t) U[t] = (mapped[t] >> (7 - j)) & 1;  // PY:1137-1155
+        Bytes raw((n + 7) / 8, 0);                                           // PY:1191-1195
+        for (int64_t t = 0; t < n; ++t) if (U[t]) raw[t >> 3] |= (u8)(1 << (7 - (t & 7)));
+        Bytes L = bbwt_forward(U.data(), n);
+        std::vector<uint64_t> runs;                                          // PY:1177-1183
+        uint64_t cur = 1;
+        for (int64_t i = 1; i < n; ++i) {
+            if (L[i] == L[i - 1]) ++cur;
+            else { runs.push_back(cur); cur = 1; }
+        }
+        runs.push_back(cur);
+        int bk = 0;
+        Bytes best;
+        for (int k = 0; k < 16; ++k) {                                       // PY:1489-1496
+            Bytes b = rice_encode_u(runs, k);
+            if (k == 0 || b.size() < best.size()) { bk = k; best.swap(b); }
+        }
+        if (raw.size() <= best.size() + 1) {
+            raw_mask |= 1 << j;
+            payload.insert(payload.end(), raw.begin(), raw.end());
+        } else {
+            if (L[0] & 1) b1_mask |= 1 << j;
+            ks.push_back(bk & 0xFF);
+            payload.insert(payload.end(), best.begin(), best.end());
+        }
+    }
+    Bytes out;
+    out.push_back((u8)(((code & 7) << 5) | (plen & 7)));
+    for (int i = 0; i < plen; ++i) out.push_back((u8)((mp >> (8 * i)) & 0xFF));
+    out.push_back((u8)raw_mask);
+    out.push_back((u8)b1_mask);
+    for (int k : ks) out.push_back((u8)k);
+    out.insert(out.end(), payload.begin(), payload.end());
+    return out;
+}
+
 int64_t emit(const Bytes& b, uint8_t* out, int64_t cap) {
     if ((int64_t)b.size() > cap) return -1;
     if (!b.empty()) std::memcpy(out, b.data(), b.size());
@@ -361,7 +519,18 @@ int64_t oracle_repair(const uint8_t* s, int64_t n, uint8_t* out, int64_t cap) {
     return emit(repair_compress(s, n), out, cap);
 }
 
-// Candidate payload of method id `mid` (PY:2152-2178 order, ids 0..9).
+// v2_new automaton choice: (code, param) of the winning transform, and its H0
+int64_t oracle_v2_automaton(const uint8_t* s, int64_t n, int32_t* code_param, double* h0) {
+    int code = 0, param = 0;
+    Bytes mapped;
+    v2_automaton(s, n, code, param, mapped);
+    code_param[0] = code;
+    code_param[1] = param;
+    if (h0) *h0 = h0_bits(mapped);
+    return 0;
+}
+
+// Candidate payload of method id `mid` (PY:2152-2178 order, ids 0..10).
 int64_t oracle_candidate(int mid, const uint8_t* s, int64_t n, uint8_t* out, int64_t cap) {
     static const int bbwt_flags[5] = {0, 1, 4, 8, 16};
     switch (mid) {
@@ -372,7 +541,8 @@ int64_t oracle_candidate(int mid, const uint8_t* s, int64_t n, uint8_t* out, int
         case 7: return oracle_lz77(s, n, out, cap);
         case 8: return oracle_lfsr(s, n, out, cap);
         case 9: return oracle_repair(s, n, out, cap);
-        default: return -2;  // v2_new (10) raises in PY
+        case 10: return emit(encode_new_pipeline(s, n), out, cap);  // serial automaton (see above)
+        default: return -2;
     }
 }
 

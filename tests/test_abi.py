@@ -61,7 +61,8 @@ def test_stats_struct_size_matches_header(tmp_path):
 def test_candidate_constants_match_header():
     src = open(HEADER).read()
     val = lambda name: int(re.search(rf"#define {name} (0x[0-9A-Fa-f]+|\d+)", src).group(1), 0)  # noqa: E731
-    assert val("KOLM_NCAND") == _lib.KOLM_NCAND == 10
+    assert val("KOLM_NCAND") == _lib.KOLM_NCAND == 11
+    assert val("KOLM_FULL_MASK") == _lib.KOLM_FULL_MASK == 0x7FF
     assert val("KOLM_DEFAULT_MASK") == _lib.KOLM_DEFAULT_MASK
     assert val("KOLM_HOTPATH_MASK") == _lib.KOLM_HOTPATH_MASK
 

@@ -377,3 +377,57 @@ def test_lz77_local_block_geometry(kolm_gpu, bs):
     for i in range(nb):
         blk = data[i * bs:(i + 1) * bs]
         assert payloads[i] == O.encode_lz77(blk), f"block {i}"
+
+
+# ---- candidate 10 (v2_new, opt-in; PY:1498-1576 with the automaton evaluated serially) ----
+
+def _v2_golden():
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    return np.load(os.path.join(here, "v2new.npz")), json.load(open(os.path.join(here, "v2new.json")))
+
+
+def test_v2new_golden_payloads(kolm_gpu):
+    """Every PY v2_new payload (85 inputs: every automaton model selected somewhere) through
+    the batched device entry, candidate 10 forced."""
+    from kolm import _lib
+    z, m = _v2_golden()
+    bad = []
+    for n in m["kernels"]:
+        inp = z[f"{n}/input"].tobytes()
+        if not inp:
+            continue
+        _, _, payloads, _ = _lib.encode_blocks(inp, len(inp), cand_mask=1 << 10, force=[10])
+        if payloads[0] != z[f"{n}/v2new"].tobytes():
+            bad.append(n)
+    assert not bad, bad
+
+
+def test_v2new_golden_containers(kolm_gpu):
+    """PY's containers with its full candidate list 0..10 (v2_new enabled) — v2_new wins
+    blocks there — byte for byte, and decoded back."""
+    z, m = _v2_golden()
+    for c, e in m["containers"].items():
+        data = z[f"C/{c}/input"].tobytes()
+        got = kolm_gpu.compress_blocks_fixed(data, e["block_size"], v2_new=True)
+        assert got == z[f"C/{c}/full10"].tobytes(), c
+        assert kolm_gpu.decompress(got) == data
+
+
+@pytest.mark.parametrize("bs", [16384, 5000])
+def test_v2new_multiblock_vs_oracle(kolm_gpu, bs):
+    """Several blocks (text, image rows, audio, zeros, random, ramp) in one batch, each
+    block's candidate-10 payload and the MDL winner over ids 0..10 vs the oracle."""
+    from kolm import _lib
+    data = (D.enwik_like(bs + 77, seed=3) + D.gradient_bmp()[54:54 + bs] + D.sine_wav()[44:44 + bs]
+            + bytes(bs // 2) + D.splitmix64_bytes(bs, seed=4) + bytes(i & 0xFF for i in range(bs)))
+    nb = (len(data) + bs - 1) // bs
+    sizes, method, payloads, _ = _lib.encode_blocks(data, bs, cand_mask=_lib.KOLM_FULL_MASK)
+    for i in range(nb):
+        blk = data[i * bs:(i + 1) * bs]
+        want10 = O.candidate(10, blk)
+        assert int(sizes[i][10]) == len(want10), f"block {i}"
+        if int(method[i]) == 10:
+            assert payloads[i] == want10, f"block {i}"
+    _, _, forced, _ = _lib.encode_blocks(data, bs, cand_mask=1 << 10, force=[10] * nb)
+    for i in range(nb):
+        assert forced[i] == O.candidate(10, data[i * bs:(i + 1) * bs]), f"block {i}"

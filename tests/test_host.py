@@ -84,7 +84,7 @@ def test_fixed_boundaries_matches_reference_semantics():
 def test_registry_ids_stable():
     names = [n for _, n in kolm._select_encoders()]
     assert names == kolm.CANDIDATE_NAMES
-    assert len(kolm._select_decoders()) == 10
+    assert len(kolm._select_decoders()) == 11
     kolm.G_NO_LZ77 = True
     try:
         assert kolm.candidate_mask() == 0x3FF & ~(1 << 7)
@@ -101,6 +101,12 @@ def test_registry_ids_stable():
         kolm.G_ONLY_METHOD = None
     with pytest.raises(NameError):
         kolm._select_encoders()[10][0](b"x")  # v2_new raises as in PY
+    kolm.G_V2_NEW = True
+    try:
+        assert kolm.candidate_mask() == 0x7FF
+        assert kolm.candidate_mask(hot_path=True) == 0x1FF
+    finally:
+        kolm.G_V2_NEW = False
 
 
 @pytest.mark.parametrize("nb,world", [(0, 2), (1, 2), (7, 2), (256, 8), (5, 8), (1000, 3)])
@@ -120,3 +126,19 @@ def test_uleb128():
         assert kolm.uleb128_decode_stream(b, 0) == (v, len(b))
     with pytest.raises(ValueError):
         kolm.uleb128_encode(-1)
+
+
+def test_host_v2new_decoder_goldens():
+    """decode_new_pipeline (PY:1578-1648) + automaton inverse (PY:1056-1092) on the host
+    inverts every PY v2_new payload, and decompress(device=False) PY's id-10 containers."""
+    import json
+    import os
+    from kolm.decode import decode_new_pipeline
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    z = np.load(os.path.join(here, "v2new.npz"))
+    m = json.load(open(os.path.join(here, "v2new.json")))
+    for n in m["kernels"]:
+        data = z[f"{n}/input"].tobytes()
+        assert decode_new_pipeline(z[f"{n}/v2new"].tobytes(), len(data)) == data, n
+    for c in m["containers"]:
+        assert kolm.decompress(z[f"C/{c}/full10"].tobytes(), device=False) == z[f"C/{c}/input"].tobytes(), c

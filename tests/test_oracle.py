@@ -102,3 +102,21 @@ def test_oracle_rice_params_small():
         out = O.rice_encode(seq, k)
         bits = sum((v >> k) + 1 + k for v in seq)
         assert len(out) == (bits + 7) // 8
+
+
+def test_oracle_v2new_vs_py_goldens():
+    """Candidate 10 (v2_new, PY:1498-1576 with the automaton evaluated serially, SURVEY §8f
+    row 3): the oracle reproduces PY's payload on every golden input (tests/golden/v2new.npz,
+    made by tests/golden/make_golden_v2.py) and PY's full-list containers (ids 0..10)."""
+    import json
+    import os
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    z = np.load(os.path.join(here, "v2new.npz"))
+    m = json.load(open(os.path.join(here, "v2new.json")))
+    bad = [n for n in m["kernels"] if O.candidate(10, z[f"{n}/input"].tobytes()) != z[f"{n}/v2new"].tobytes()]
+    assert not bad, bad
+    modes = {(e["mode"], e["param"]) for e in m["kernels"].values()}
+    assert len(modes) >= 8  # identity, delta-k, Gray, interleave, BM3, morpho close/open exercised
+    for c, e in m["containers"].items():
+        data = z[f"C/{c}/input"].tobytes()
+        assert O.compress_blocks_fixed(data, e["block_size"], range(11)) == z[f"C/{c}/full10"].tobytes(), c
