@@ -160,7 +160,7 @@ def test_gpu_variable_blocks_vs_oracle(kolm_gpu, seed):
     for i in range(len(edges) - 1):
         blk = data[edges[i]:edges[i + 1]]
         want = [len(O.candidate(m, blk)) for m in range(10)]
-        assert list(map(int, sizes[i])) == want, (i, len(blk))
+        assert list(map(int, sizes[i][:10])) == want, (i, len(blk))
         assert int(method[i]) == int(np.argmin(want))
         assert payloads[i] == O.candidate(int(method[i]), blk)
 

@@ -68,7 +68,7 @@ def test_batched_candidates_golden(kolm_gpu, golden_kernels, name):
     # un-forced: MDL winner = argmin, ties -> lowest id (PY:2359)
     sizes, method, payloads, _ = _lib.encode_blocks(inp, len(inp))
     lens = [len(want[m]) for m in range(10)]
-    assert list(map(int, sizes[0])) == lens
+    assert list(map(int, sizes[0][:10])) == lens
     assert int(method[0]) == int(np.argmin(lens))
     # hot path (ids 0..8): candidate 9 disabled, argmin over the rest
     sizes, method, payloads, _ = _lib.encode_blocks(inp, len(inp), cand_mask=_lib.KOLM_HOTPATH_MASK)
@@ -150,7 +150,7 @@ def test_multiblock_vs_oracle(kolm_gpu, seed, bs, n):
         blk = data[i * bs:(i + 1) * bs]
         cand = _oracle_all(blk)
         lens = [len(c) for c in cand]
-        assert list(map(int, sizes[i])) == lens, f"block {i}"
+        assert list(map(int, sizes[i][:10])) == lens, f"block {i}"
         m = int(np.argmin(lens))
         assert int(method[i]) == m, f"block {i}"
         assert payloads[i] == cand[m], f"block {i} payload"
@@ -176,7 +176,7 @@ def test_full_size_enwik_properties(kolm_gpu, seed):
     assert len(payloads) == 16
     blk = data[:bs]
     cand = _oracle_all(blk)
-    assert list(map(int, sizes[0])) == [len(c) for c in cand]
+    assert list(map(int, sizes[0][:10])) == [len(c) for c in cand]
     assert payloads[0] == cand[int(method[0])]
     for i in range(16):
         assert int(sizes[i][int(method[i])]) == len(payloads[i])
@@ -255,7 +255,7 @@ def test_adversarial_batched(kolm_gpu, kind):
     for i in range((len(data) + bs - 1) // bs):
         blk = data[i * bs:(i + 1) * bs]
         cand = _oracle_all(blk)
-        assert list(map(int, sizes[i])) == [len(c) for c in cand], f"block {i}"
+        assert list(map(int, sizes[i][:10])) == [len(c) for c in cand], f"block {i}"
         assert payloads[i] == cand[int(method[i])], f"block {i}"
 
 
