@@ -5,6 +5,8 @@
 // No host synchronisation: a fixed sequence of launches on the sort stream.
 #include "kolm_internal.h"
 
+#include <string>
+
 namespace kolm {
 
 namespace {
@@ -89,9 +91,11 @@ __global__ __launch_bounds__(WG) void k_lsd_scan(LsdGeom g, u32* hist) {
 // Stable scatter of one tile by digit P: element order e = j*WG + tid; each wave ranks
 // its 64 elements per digit with ballots, per-wave counts are combined in (j, wave)
 // order.  SRC_KP reads the keys by position (positions implicit).
-template <int P, int SRC>
+// G: the pass writes Kg[position] as the key (the next digit set, gathered by position)
+// instead of the key it sorted by — the last pass of the 8-character sort's first half.
+template <int P, int SRC, int G>
 __global__ __launch_bounds__(WG) void k_lsd_scatter(LsdGeom g, const u32* Kin, const u32* Pin,
-                                                   u32* Kout, u32* Pout, const u32* hist) {
+                                                   u32* Kout, u32* Pout, const u32* Kg, const u32* hist) {
     __shared__ u32 wcnt[WG / 64][256];
     __shared__ u32 running[256];
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -129,7 +133,7 @@ __global__ __launch_bounds__(WG) void k_lsd_scatter(LsdGeom g, const u32* Kin, c
             u32 pre = running[dg];
             for (u32 q = 0; q < w; ++q) pre += wcnt[q][dg];
             const u32 dst = pre + rank;
-            Kout[dst] = key;
+            Kout[dst] = G ? Kg[pos] : key;
             Pout[dst] = pos;
         }
         __syncthreads();
@@ -197,21 +201,49 @@ __device__ inline void load16(const u32* X, u32 i0, u32 hi, u32 (&v)[LSD_PT]) {
 // ---------------------------------------------------------------------------------
 constexpr u32 BIG = 0xFFFFFFFFu;
 
-__device__ inline bool r0_head(const u32* K, u32 g, u32 base) { return g == base || K[g] != K[g - 1]; }
-
 __device__ inline u32 wave_min(u32 v) { return wave_reduce(v, OpMinU(), BIG); }
 
-__global__ __launch_bounds__(WG) void k_r0_tile_heads(LsdGeom g, const u32* K, u32* tmax, u32* tmin) {
+// Group heads of every tile: bit e of HF[t * WG + tid] = slot lo + 16 tid + e starts a group
+// (the block's first slot, or its key differs from the previous slot's; with KA — the
+// 8-character round 0, K = characters 0..3 — also when characters 4..7, KA[SA[slot]],
+// differ).  tmax / tmin = the tile's last / first head.
+__global__ __launch_bounds__(WG) void k_r0_tile_heads(LsdGeom g, const u32* K, const u32* SA, const u32* KA, u32* HF,
+                                                      u32* tmax, u32* tmin) {
     __shared__ u32 s1[WG / 64], s2[WG / 64];
+    const u32 t = xcd_tile();
     u32 lo, hi, b;
     u32 mx = 0, mn = BIG;
-    if (g.range(xcd_tile(), lo, hi, b)) {
+    if (g.range(t, lo, hi, b)) {
         const u32 base = g.geo.base(b);
-        for (u32 i = lo + threadIdx.x; i < hi; i += WG)
-            if (r0_head(K, i, base)) {
-                mx = max(mx, i);
-                mn = min(mn, i);
+        const u32 i0 = lo + threadIdx.x * LSD_PT;
+        u32 hm = 0;
+        if (i0 < hi) {
+            u32 kv[LSD_PT], av[LSD_PT];
+            load16(K, i0, hi, kv);
+            u32 kprev = i0 > base ? K[i0 - 1] : 0u, aprev = 0;
+            if (KA) {
+                u32 sv[LSD_PT];
+                load16(SA, i0, hi, sv);
+#pragma unroll
+                for (u32 e = 0; e < LSD_PT; ++e) av[e] = i0 + e < hi ? KA[sv[e]] : 0u;
+                aprev = i0 > base ? KA[SA[i0 - 1]] : 0u;
+            } else {
+#pragma unroll
+                for (u32 e = 0; e < LSD_PT; ++e) av[e] = 0;
             }
+#pragma unroll
+            for (u32 e = 0; e < LSD_PT; ++e) {
+                const u32 i = i0 + e;
+                if (i < hi && (i == base || kv[e] != kprev || av[e] != aprev)) {
+                    hm |= 1u << e;
+                    mx = max(mx, i);
+                    mn = min(mn, i);
+                }
+                kprev = kv[e];
+                aprev = av[e];
+            }
+        }
+        HF[(u64)t * WG + threadIdx.x] = hm;
     }
     mx = wave_max(mx);
     mn = wave_min(mn);
@@ -221,8 +253,8 @@ __global__ __launch_bounds__(WG) void k_r0_tile_heads(LsdGeom g, const u32* K, u
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        tmax[xcd_tile()] = max(max(s1[0], s1[1]), max(s1[2], s1[3]));
-        tmin[xcd_tile()] = min(min(s2[0], s2[1]), min(s2[2], s2[3]));
+        tmax[t] = max(max(s1[0], s1[1]), max(s1[2], s1[3]));
+        tmin[t] = min(min(s2[0], s2[1]), min(s2[2], s2[3]));
     }
 }
 
@@ -250,7 +282,7 @@ __global__ __launch_bounds__(WG) void k_r0_tiles_rscan(const u32* in, u32* out, 
     }
 }
 
-__global__ __launch_bounds__(WG) void k_r0_final(LsdGeom g, const u32* K, const u32* SA, const u32* cmax,
+__global__ __launch_bounds__(WG) void k_r0_final(LsdGeom g, const u32* HF, const u32* SA, const u32* cmax,
                                                  const u32* cmin, u32* RK, Seg* next, u32* next_cnt,
                                                  u32* blk_split) {
     __shared__ u32 sh[WG / 64], sh2[WG / 64], sh3[WG / 64];
@@ -261,17 +293,15 @@ __global__ __launch_bounds__(WG) void k_r0_final(LsdGeom g, const u32* K, const 
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid == 0) anysplit = 0;
     const u32 i0 = lo + tid * LSD_PT;
-    u32 kv[LSD_PT], sv[LSD_PT];
-    load16(K, i0, hi, kv);
+    u32 sv[LSD_PT];
     load16(SA, i0, hi, sv);
-    u32 kprev = (i0 > base && i0 < hi) ? K[i0 - 1] : 0u;
+    const u32 hm = HF[(u64)blockIdx.x * WG + tid];
     bool hd[LSD_PT];
     u32 lmax = 0, lmin = BIG;
 #pragma unroll
     for (u32 e = 0; e < LSD_PT; ++e) {
         const u32 i = i0 + e;
-        hd[e] = i < hi && (i == base || kv[e] != kprev);  // r0_head
-        kprev = kv[e];
+        hd[e] = (hm >> e) & 1u;
         if (hd[e]) {
             lmax = max(lmax, i);
             lmin = min(lmin, i);
@@ -333,64 +363,71 @@ __global__ __launch_bounds__(WG) void k_r0_final(LsdGeom g, const u32* K, const 
         if (len[e] >= 2) next[off++] = Seg{i0 + e, len[e]};
 }
 
+template <int P, int SRC, int G>
+void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kout, u32* pout, const u32* kg,
+              u32* hist, hipStream_t s, KTimer* kt) {
+    static const std::string hn = "k_lsd_hist<" + std::to_string(P) + ", " + std::to_string(SRC) + ">";
+    static const std::string sn =
+        "k_lsd_scatter<" + std::to_string(P) + ", " + std::to_string(SRC) + ", " + std::to_string(G) + ">";
+    const u64 N = g.geo.N, H = (u64)nt * 1024;  // H: per-tile histogram bytes
+    {
+        KScope k(kt, KT_LSD, hn.c_str(), 4 * N + H);
+        k_lsd_hist<P, SRC><<<nt, WG, 0, s>>>(g, kin, hist);
+    }
+    {
+        KScope k(kt, KT_LSD, "k_lsd_scan", 3 * H);
+        k_lsd_scan<<<g.geo.nb, WG, 0, s>>>(g, hist);
+    }
+    {
+        // key + position in (the first pass reads the key by position only) and out; G: + the gather
+        KScope k(kt, KT_LSD, sn.c_str(), (SRC == SRC_KP ? 12 : 16) * N + (G ? 4 * N : 0) + H);
+        k_lsd_scatter<P, SRC, G><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
+    }
+}
+
 }  // namespace
 
 u32 lsd_tiles(const Geom& geo) { return (geo.bs + LSD_T - 1) / LSD_T * geo.nb; }
 
-// Round 0 of the cyclic sort.  KP = 4-character keys by position (k_keypos).
-// Passes: (KP, p) -> (K2, SA) -> (K22, SA2) -> (KP, RK) -> (K2, SA); then ranks/segments.
+// Round 0 of the cyclic sort: a stable sort of every block's positions by the first 4 or 8
+// rotation characters (KP = characters 0..3 by position; 8 characters: RK holds characters
+// 4..7 by position on entry).  4 characters: (KP, p) -> (K2, SA) -> (K22, SA2) -> (KP, RK) ->
+// (K2, SA).  8 characters: 4 passes over characters 4..7 (RK, p) -> (K22, SA2) -> (K2, SA)
+// -> (K22, SA2) -> (K2 = KP[SA], SA), then 4 over characters 0..3 ending in (K2, SA).  Then
+// group heads (HF), ranks and next-round segments.
 void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s,
                    KTimer* kt) {
     if (!geo.N) return;
     LsdGeom g{geo, (geo.bs + LSD_T - 1) / LSD_T};
     const u32 nt = g.tpb * geo.nb;
-    const u64 N = geo.N, H = (u64)nt * 1024;  // H: per-tile histogram bytes
-    {
-        KScope k(kt, KT_LSD, "k_lsd_hist<0, 1>", 4 * N + H);
-        k_lsd_hist<0, SRC_KP><<<nt, WG, 0, s>>>(g, t.KP, t.hist);
+    const u64 N = geo.N;
+    const bool c8 = t.chars == 8;
+    if (!c8) {
+        lsd_pass<0, SRC_KP, 0>(g, nt, t.KP, nullptr, t.K2, t.SA, nullptr, t.hist, s, kt);
+        lsd_pass<1, SRC_PAIR, 0>(g, nt, t.K2, t.SA, t.K22, t.SA2, nullptr, t.hist, s, kt);
+        lsd_pass<2, SRC_PAIR, 0>(g, nt, t.K22, t.SA2, t.KP, t.RK, nullptr, t.hist, s, kt);
+        lsd_pass<3, SRC_PAIR, 0>(g, nt, t.KP, t.RK, t.K2, t.SA, nullptr, t.hist, s, kt);
+    } else {
+        lsd_pass<0, SRC_KP, 0>(g, nt, t.RK, nullptr, t.K22, t.SA2, nullptr, t.hist, s, kt);
+        lsd_pass<1, SRC_PAIR, 0>(g, nt, t.K22, t.SA2, t.K2, t.SA, nullptr, t.hist, s, kt);
+        lsd_pass<2, SRC_PAIR, 0>(g, nt, t.K2, t.SA, t.K22, t.SA2, nullptr, t.hist, s, kt);
+        lsd_pass<3, SRC_PAIR, 1>(g, nt, t.K22, t.SA2, t.K2, t.SA, t.KP, t.hist, s, kt);
+        lsd_pass<0, SRC_PAIR, 0>(g, nt, t.K2, t.SA, t.K22, t.SA2, nullptr, t.hist, s, kt);
+        lsd_pass<1, SRC_PAIR, 0>(g, nt, t.K22, t.SA2, t.K2, t.SA, nullptr, t.hist, s, kt);
+        lsd_pass<2, SRC_PAIR, 0>(g, nt, t.K2, t.SA, t.K22, t.SA2, nullptr, t.hist, s, kt);
+        lsd_pass<3, SRC_PAIR, 0>(g, nt, t.K22, t.SA2, t.K2, t.SA, nullptr, t.hist, s, kt);
     }
     {
-        KScope k(kt, KT_LSD, "k_lsd_scan", 3 * H);
-        k_lsd_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
-    }
-    {
-        KScope k(kt, KT_LSD, "k_lsd_scatter<0, 1>", 12 * N + H);
-        k_lsd_scatter<0, SRC_KP><<<nt, WG, 0, s>>>(g, t.KP, nullptr, t.K2, t.SA, t.hist);
-    }
-    u32* kin[3] = {t.K2, t.K22, t.KP};
-    u32* pin[3] = {t.SA, t.SA2, t.RK};
-    u32* kout[3] = {t.K22, t.KP, t.K2};
-    u32* pout[3] = {t.SA2, t.RK, t.SA};
-    static const char* const hn[3] = {"k_lsd_hist<1, 2>", "k_lsd_hist<2, 2>", "k_lsd_hist<3, 2>"};
-    static const char* const sn[3] = {"k_lsd_scatter<1, 2>", "k_lsd_scatter<2, 2>", "k_lsd_scatter<3, 2>"};
-    for (int q = 0; q < 3; ++q) {
-        {
-            KScope k(kt, KT_LSD, hn[q], 4 * N + H);
-            if (q == 0) k_lsd_hist<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, kin[q], t.hist);
-            if (q == 1) k_lsd_hist<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, kin[q], t.hist);
-            if (q == 2) k_lsd_hist<3, SRC_PAIR><<<nt, WG, 0, s>>>(g, kin[q], t.hist);
-        }
-        {
-            KScope k(kt, KT_LSD, "k_lsd_scan", 3 * H);
-            k_lsd_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
-        }
-        {
-            KScope k(kt, KT_LSD, sn[q], 16 * N + H);
-            if (q == 0) k_lsd_scatter<1, SRC_PAIR><<<nt, WG, 0, s>>>(g, kin[q], pin[q], kout[q], pout[q], t.hist);
-            if (q == 1) k_lsd_scatter<2, SRC_PAIR><<<nt, WG, 0, s>>>(g, kin[q], pin[q], kout[q], pout[q], t.hist);
-            if (q == 2) k_lsd_scatter<3, SRC_PAIR><<<nt, WG, 0, s>>>(g, kin[q], pin[q], kout[q], pout[q], t.hist);
-        }
-    }
-    {
-        KScope k(kt, KT_LSD, "k_r0_tile_heads", 4 * N);
-        k_r0_tile_heads<<<nt, WG, 0, s>>>(g, t.K2, t.tmax, t.tmin);
+        // K 4 (+ SA 4 + the KA gather 4) read, head masks written
+        KScope k(kt, KT_LSD, "k_r0_tile_heads", (c8 ? 12 : 4) * N);
+        k_r0_tile_heads<<<nt, WG, 0, s>>>(g, t.K2, t.SA, c8 ? t.RK : nullptr, t.HF, t.tmax, t.tmin);
         k_tiles_max_scan<<<geo.nb, WG, 0, s>>>(t.tmax, t.cmax, g.tpb);
         k_r0_tiles_rscan<<<geo.nb, WG, 0, s>>>(t.tmin, t.cmin, g.tpb);
     }
     {
-        // K 4 + SA 4 read, RK 4 scattered (+ 8 B per new segment)
-        KScope k(kt, KT_LSD, "k_r0_final", 12 * N);
-        k_r0_final<<<nt, WG, 0, s>>>(g, t.K2, t.SA, t.cmax, t.cmin, t.RK, next, next_cnt, blk_split);
+        // SA 4 read, RK 4 scattered (+ head masks, 8 B per new segment)
+        KScope k(kt, KT_LSD, "k_r0_final", 8 * N);
+        k_r0_final<<<nt, WG, 0, s>>>(g, t.HF, t.SA, t.cmax, t.cmin, t.RK, next, next_cnt, blk_split);
     }
 }
 

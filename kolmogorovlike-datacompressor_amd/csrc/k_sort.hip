@@ -81,6 +81,25 @@ __device__ inline u32 cyc_succ(const SortArgs& a, u32 p, u32 h) {
     return fs + t;
 }
 
+// characters off .. off+3 of the rotation starting at p (cyclic inside p's Lyndon factor),
+// the first most significant
+__device__ inline u32 cyc_chars(const SortArgs& a, u32 p, u32 off) {
+    if (a.FEd[p] > off + 3) {  // the 4 characters do not wrap
+        const u8* t = a.text + p + off;
+        return ((u32)t[0] << 24) | ((u32)t[1] << 16) | ((u32)t[2] << 8) | t[3];
+    }
+    const u64 f = a.FSL[p];
+    const u32 fs = (u32)f, m = (u32)(f >> 32);
+    u32 t = (p - fs) + off % m, k = 0;
+    if (t >= m) t -= m;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        k = (k << 8) | a.text[fs + t];
+        if (++t == m) t = 0;
+    }
+    return k;
+}
+
 __device__ inline u32 make_key(const SortArgs& a, u32 p, u32 base, u32 end) {
     if (a.KP) return a.KP[p];
     if (a.initial) {
@@ -90,17 +109,7 @@ __device__ inline u32 make_key(const SortArgs& a, u32 p, u32 base, u32 end) {
             u32 c2 = p + 2 < end ? (u32)a.text[p + 2] + 1 : 0;
             return (c0 << 18) | (c1 << 9) | c2;
         }
-        if (a.FEd[p] > 3)  // the 4 rotation characters do not wrap
-            return ((u32)a.text[p] << 24) | ((u32)a.text[p + 1] << 16) | ((u32)a.text[p + 2] << 8) | a.text[p + 3];
-        const u64 f = a.FSL[p];
-        const u32 fs = (u32)f, m = (u32)(f >> 32);
-        u32 t = p - fs, k = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            k = (k << 8) | a.text[fs + t];
-            if (++t == m) t = 0;
-        }
-        return k;
+        return cyc_chars(a, p, 0);
     }
     if (!a.cyclic) {
         const u32 q = p + a.h;
@@ -117,6 +126,7 @@ __global__ __launch_bounds__(256) void k_keypos(SortArgs a, u32* KP) {
     for (u32 p = blockIdx.x * blockDim.x + threadIdx.x; p < a.geo.N; p += gridDim.x * blockDim.x) {
         const u32 b = a.geo.block_of(p);
         KP[p] = make_key(a, p, a.geo.base(b), a.geo.end(b));
+        if (a.initial && a.KA) a.KA[p] = cyc_chars(a, p, 4);
     }
 }
 
@@ -132,25 +142,26 @@ __global__ __launch_bounds__(256) void k_keypos_cyc(SortArgs a, u32* KP) {
         for (u32 p = p0; p < N; ++p) {
             const u32 b = a.geo.block_of(p);
             KP[p] = make_key(a, p, a.geo.base(b), a.geo.end(b));
+            if (a.initial && a.KA) a.KA[p] = cyc_chars(a, p, 4);
         }
         return;
     }
     const uint4 dv = *reinterpret_cast<const uint4*>(a.FEd + p0);
     const u32 dw[4] = {dv.x, dv.y, dv.z, dv.w};
-    u32 key[16];
+    u32 key[16], ka[16];
     if (a.initial) {
-        // bytes p0 .. p0+19 cover the 4-character windows of the 16 positions
+        // bytes p0 .. p0+23 cover the 8-character windows of the 16 positions
         const u32* tw = reinterpret_cast<const u32*>(a.text + p0);
-        u32 w[5];
+        u32 w[6];
 #pragma unroll
         // a word that starts before N is inside the allocation (4-byte granular); bytes
-        // past N only feed positions that take the factor-record path (FEd <= 3)
-        for (int i = 0; i < 5; ++i) w[i] = (p0 + 4 * i < N) ? tw[i] : 0u;
+        // past N only feed positions that take the factor-record path (FEd <= 3 / 7)
+        for (int i = 0; i < 6; ++i) w[i] = (p0 + 4 * i < N) ? tw[i] : 0u;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-            const u32 lo = w[e >> 2], hi = w[(e >> 2) + 1];
-            const u32 v = __builtin_amdgcn_alignbyte(hi, lo, e & 3);  // bytes p..p+3, little-endian
-            key[e] = __builtin_bswap32(v);                            // first character most significant
+            const u32 lo = w[e >> 2], mid = w[(e >> 2) + 1], hi = w[(e >> 2) + 2];
+            key[e] = __builtin_bswap32(__builtin_amdgcn_alignbyte(mid, lo, e & 3));  // bytes p..p+3, first most significant
+            ka[e] = __builtin_bswap32(__builtin_amdgcn_alignbyte(hi, mid, e & 3));   // bytes p+4..p+7
         }
     } else {
         if (p0 + a.h + 16 <= N) {
@@ -184,6 +195,16 @@ __global__ __launch_bounds__(256) void k_keypos_cyc(SortArgs a, u32* KP) {
     uint4* out = reinterpret_cast<uint4*>(KP + p0);
 #pragma unroll
     for (int i = 0; i < 4; ++i) out[i] = make_uint4(key[4 * i], key[4 * i + 1], key[4 * i + 2], key[4 * i + 3]);
+    if (a.initial && a.KA) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const u32 d = (dw[e >> 2] >> (8 * (e & 3))) & 0xFF;
+            if (d <= 7) ka[e] = cyc_chars(a, p0 + e, 4);
+        }
+        uint4* oa = reinterpret_cast<uint4*>(a.KA + p0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) oa[i] = make_uint4(ka[4 * i], ka[4 * i + 1], ka[4 * i + 2], ka[4 * i + 3]);
+    }
 }
 
 // ------------------------------------------------------------------------------------

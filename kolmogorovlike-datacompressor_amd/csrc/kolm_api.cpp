@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -287,9 +288,21 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
     Seg* cur = segA;
     Seg* nxt = segB;
     u32 ncur = geo.nb;
-    const u32 h0 = cyclic ? 4 : 3;
+    // cyclic round 0 sorts by 8 rotation characters (KOLM_R0_CHARS=4: by 4, one more doubling round)
+    static const int r0_chars = getenv("KOLM_R0_CHARS") && atoi(getenv("KOLM_R0_CHARS")) == 4 ? 4 : 8;
+    const u32 h0 = cyclic ? (u32)r0_chars : 3;
     const u32 kb_rank = bitlen(geo.bs) ? bitlen(geo.bs) : 1;
     u32* h = c->h_cnt;
+    static const bool dbg = getenv("KOLM_DEBUG_ROUNDS") != nullptr;
+    // KOLM_DEBUG_ROUNDS: per-round class counts and wall time (the round ends at a host sync)
+    auto t_round = std::chrono::steady_clock::now();
+    auto round_done = [&](u32 r) {
+        if (!dbg) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[kolm] %s round %u: %.3f ms\n", cyclic ? "cyc" : "lin", r,
+                std::chrono::duration<double, std::milli>(now - t_round).count());
+        t_round = now;
+    };
     for (u32 round = 0; round < 64 && ncur; ++round) {
         a.initial = round == 0 ? 1 : 0;
         a.h = round == 0 ? 0u : (h0 << (round - 1));
@@ -300,16 +313,20 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
         KOLM_HIP_CHECK(hipMemsetAsync(cnt + C_CLSE, 0, sizeof(u32) * (C_N - C_CLSE), s));
         KOLM_HIP_CHECK(hipMemsetAsync(a.blk_split, 0, sizeof(u32) * geo.nb, s));
         if (round == 0 && cyclic) {
-            // round 0: 4 stable LSD passes over the 4-character keys, no host round trips
+            // round 0: stable LSD passes over the 8 (4) rotation characters, no host round trips
             u32* KP = c->get<u32>("KP", N);
             {
-                TScope t(c, KOLM_KT_KEYGEN, "k_keypos", N * 9);  // FEd 1 + text 4 (overlapping) + KP 4
+                // FEd 1 + text 4 (overlapping) + KP 4 (+ characters 4..7 into RK: 4)
+                TScope t(c, KOLM_KT_KEYGEN, "k_keypos", N * (r0_chars == 8 ? 13 : 9));
                 a.KP = nullptr;
+                a.KA = r0_chars == 8 ? a.RK : nullptr;
                 launch_keypos(a, KP, s);
+                a.KA = nullptr;
             }
             const u64 nt = lsd_tiles(geo) + 1;
             R0Bufs r{KP, a.K2, a.SA, a.K22, a.SA2, a.RK, c->get<u32>("r0hist", nt * 256), c->get<u32>("r0tmax", nt),
-                     c->get<u32>("r0tmin", nt), c->get<u32>("r0cmax", nt), c->get<u32>("r0cmin", nt)};
+                     c->get<u32>("r0tmin", nt), c->get<u32>("r0cmax", nt), c->get<u32>("r0cmin", nt),
+                     c->get<u32>("r0hf", nt * WG), r0_chars};
             launch_round0(geo, r, nxt, L.next_cnt, a.blk_split, s, c->kt());
             out.active += N;
             out.rounds = 1;
@@ -320,6 +337,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
                 c->active = s;
             }
             c->sync();
+            round_done(round);
             ncur = h[C_NEXT];
             std::swap(cur, nxt);
             continue;
@@ -333,7 +351,6 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
         if (h[C_ACTIVE] == 0) break;
         out.active += h[C_ACTIVE];
         out.rounds = round + 1;
-        static const bool dbg = getenv("KOLM_DEBUG_ROUNDS") != nullptr;
         if (dbg) {
             fprintf(stderr, "[kolm] round %u h=%u active=%u large: segs %u elems %u | class segs/elems:", round, a.h,
                     h[C_ACTIVE], h[C_L0SEG], h[C_L0ELEM]);
@@ -426,6 +443,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
         if (cyclic) launch_update_done(blk_done, a.blk_split, geo.nb, s);
         KOLM_HIP_CHECK(hipMemcpyAsync(h + C_NEXT, cnt + C_NEXT, sizeof(u32), hipMemcpyDeviceToHost, s));
         c->sync();
+        round_done(round);
         ncur = h[C_NEXT];
         std::swap(cur, nxt);
     }
@@ -652,10 +670,11 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     // higher priority: the critical path) runs the Lyndon factorisation, the cyclic sort,
     // BBWT, MTF and the Rice sizes, joins LZ77 and finishes MDL + emission.
     // KOLM_SERIAL=1 runs everything on one stream (profiling); KOLM_OVERLAP selects when
-    // LZ77 starts: 0 at once, 1 after the Lyndon factorisation, 2 (default) after round 0
-    // of the cyclic sort (measured 58.5-59.0 ms per 256 MiB vs 59.1-59.7 for 0 and 1).
+    // LZ77 starts: 0 (default) at once, 1 after the Lyndon factorisation, 2 after round 0 of
+    // the cyclic sort.  With the 8-character round 0 (eight streaming LSD passes beside the
+    // LDS-bound parse): 53.8-54.2 ms per 256 MiB for 0, 54.1-54.2 for 1, 55.4-56.2 for 2.
     static const bool serial = getenv("KOLM_SERIAL") && atoi(getenv("KOLM_SERIAL")) != 0;
-    static const int overlap = getenv("KOLM_OVERLAP") ? atoi(getenv("KOLM_OVERLAP")) : 2;
+    static const int overlap = getenv("KOLM_OVERLAP") ? atoi(getenv("KOLM_OVERLAP")) : 0;
     hipStream_t ms = c->stream, s = serial ? c->stream : c->aux;
     Pipeline P{c, geo, d_text};
     hipEvent_t* ev = c->ev;

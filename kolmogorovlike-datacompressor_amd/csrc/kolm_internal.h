@@ -206,6 +206,7 @@ struct SortArgs {
     u32 h;             // doubling offset of this round (round >= 1)
     const u32* KP;     // [N] this round's key by position (k_keypos), or null: keys gathered directly
     u32 key_bits;      // keys of this round are < 2^key_bits (small sort packs key|index in 32 bits)
+    u32* KA;           // cyclic round 0 with 8 characters: k_keypos also writes characters 4..7 here
 };
 
 // Append-only lists written by the classify / MSD / small-sort kernels.
@@ -262,14 +263,17 @@ void launch_bbwt_gather(const Geom& geo, const u32* SA, const u8* prevc, u8* out
 // ---- k_lsd.hip: per-block LSD radix passes: round 0 of the cyclic sort ----
 u32 lsd_tiles(const Geom& geo);
 struct R0Bufs {
-    u32* KP;   // [N] in: 4-character keys by position; scratch afterwards
+    u32* KP;   // [N] in: keys by position (characters 0..3 of the rotation); scratch afterwards
     u32* K2;   // [N] out: sorted keys (scratch)
     u32* SA;   // [N] out: positions in 4-character order (ties by position)
     u32* K22;  // [N] scratch
     u32* SA2;  // [N] scratch
-    u32* RK;   // [N] out: group start slot of every position
+    u32* RK;   // [N] out: group start slot of every position.  8-character round 0: in,
+               // characters 4..7 of the rotation by position (read before RK is written)
     u32* hist;                    // [lsd_tiles * 256]
     u32 *tmax, *tmin, *cmax, *cmin;  // [lsd_tiles]
+    u32* HF;   // [lsd_tiles * WG] group-head masks (16 slots per thread)
+    int chars; // 4 or 8 rotation characters
 };
 void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s,
                    KTimer* kt = nullptr);

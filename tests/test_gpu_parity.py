@@ -227,10 +227,19 @@ def _adversarial(kind: str, n: int) -> bytes:
         return bytes(n)
     if kind == "two_symbols":
         return rng.integers(0, 2, n).astype(np.uint8).tobytes()
+    if kind == "short_words":     # Lyndon factors of 1..10 bytes: the 8 round-0 characters wrap
+        out = bytearray()         # inside the factor at every offset
+        c = 250
+        while len(out) < n:
+            ln = int(rng.integers(1, 11))
+            out.append(c)
+            out += rng.integers(c + 1, 256, ln - 1).astype(np.uint8).tobytes()
+            c = c - 1 if c > 1 else 250
+        return bytes(out[:n])
     raise ValueError(kind)
 
 
-ADV = ["decreasing", "fibonacci", "thue_morse", "period7", "runs", "zeros", "two_symbols"]
+ADV = ["decreasing", "fibonacci", "thue_morse", "period7", "runs", "zeros", "two_symbols", "short_words"]
 
 
 @pytest.mark.parametrize("kind", ADV)
@@ -245,7 +254,7 @@ def test_adversarial_bbwt_lz77(kolm_gpu, kind):
     assert kolm_gpu.encode_lz77(data)[0] == O.encode_lz77(data), "lz77"
 
 
-@pytest.mark.parametrize("kind", ["decreasing", "period7", "runs", "two_symbols"])
+@pytest.mark.parametrize("kind", ["decreasing", "period7", "runs", "two_symbols", "short_words"])
 def test_adversarial_batched(kolm_gpu, kind):
     """Same structures through the batched entry: 4 blocks of 65536 + a ragged tail."""
     from kolm import _lib
