@@ -140,6 +140,9 @@ def main():
                     help="timed device decode passes over the hot-path payloads (0: skip)")
     ap.add_argument("--cdc-steps", type=int, default=2,
                     help="timed steps of the content-defined (FastCDC) mode; 0 = skip")
+    ap.add_argument("--v2-steps", type=int, default=1,
+                    help="timed steps of the candidate list 0..10 (+ v2_new, opt-in) on --v2-mib MiB; 0 = skip")
+    ap.add_argument("--v2-mib", type=int, default=32, help="input MiB of the v2_new leg")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -409,6 +412,44 @@ def main():
                "params": [4096, 8192, 16384], "chunks_per_gpu": nbc, "candidates": "0..8",
                "ratio": round(float(coff[nbc]) / n, 4)}
 
+    # Candidate 10 (v2_new, opt-in: PY as shipped raises before computing it) on a prefix of
+    # the resident input: the automaton + 8 bit planes, the BBWT of every plane (8x the
+    # positions of the hot path, binary alphabet), run-length Rice; ids 0..10 + MDL.
+    v2 = None
+    if a.v2_steps > 0:
+        n2 = min(n, a.v2_mib << 20)
+        nb2 = (n2 + a.bs - 1) // a.bs
+        sz2 = np.zeros((nb2, _lib.KOLM_NCAND), np.uint32)
+        m2 = np.zeros(nb2, np.uint32)
+        o2 = np.zeros(nb2 + 1, np.uint64)
+
+        def v2_step():
+            st = _lib.Stats()
+            _lib.check(L.kolm_encode_blocks_device(ctx, d_in.data_ptr(), n2, a.bs, _lib.KOLM_FULL_MASK, None,
+                                                   arena.data_ptr(), cap, sz2.ctypes.data, m2.ctypes.data,
+                                                   o2.ctypes.data, ctypes.byref(st)))
+
+        v2_step()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.v2_steps):
+            v2_step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el2 = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([el2], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el2 = float(tt[0])
+        v2 = {"value": round(world * n2 * a.v2_steps / el2 / MB, 2), "unit": "MB/s", "steps": a.v2_steps,
+              "ms_per_step": round(el2 / a.v2_steps * 1e3, 2), "mib_per_gpu": n2 >> 20,
+              "candidates": "0..10 (v2_new opt-in)", "ratio": round(float(o2[-1]) / n2, 4),
+              "methods": np.bincount(m2, minlength=11).tolist(),
+              "v2_new_size_ratio": round(float(sz2[:, 10].astype(np.float64).sum()) / n2, 4)}
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(data, a.bs, a.cpu_budget)
@@ -433,6 +474,7 @@ def main():
                        "decode": dec,
                        "full_candidates": full,
                        "cdc_mode": cdc,
+                       "v2_new": v2,
                        "device_ms": {k: round(s0[k], 2) for k in ("ms_total", "ms_sa", "ms_lz", "ms_entropy", "ms_emit")},
                        "cyclic_rounds": s0["cyc_rounds"],
                        "lz77": {"tokens": s0["lz_tokens"], "stitch_fixups": s0["lz_fix"],

@@ -44,10 +44,22 @@ __global__ __launch_bounds__(WG) void k_lsd_hist(LsdGeom g, const u32* K, u32* h
     __syncthreads();
     u32 lo, hi, b;
     if (g.range(xcd_tile(), lo, hi, b)) {
-#pragma unroll 4
-        for (u32 i = lo + tid; i < hi; i += WG) {
-            const u32 d = digit<P>(K[i]);
-            atomicAdd(&h[w][d], 1u);
+        // 16 consecutive keys per thread, four 16-byte loads when aligned (order is irrelevant)
+        const u32 i0 = lo + tid * LSD_PT;
+        if ((i0 & 3) == 0 && i0 + LSD_PT <= hi) {
+            const uint4* p = reinterpret_cast<const uint4*>(K + i0);
+            uint4 v[LSD_PT / 4];
+#pragma unroll
+            for (u32 q = 0; q < LSD_PT / 4; ++q) v[q] = p[q];
+#pragma unroll
+            for (u32 q = 0; q < LSD_PT / 4; ++q) {
+                atomicAdd(&h[w][digit<P>(v[q].x)], 1u);
+                atomicAdd(&h[w][digit<P>(v[q].y)], 1u);
+                atomicAdd(&h[w][digit<P>(v[q].z)], 1u);
+                atomicAdd(&h[w][digit<P>(v[q].w)], 1u);
+            }
+        } else {
+            for (u32 i = i0; i < min(i0 + LSD_PT, hi); ++i) atomicAdd(&h[w][digit<P>(K[i])], 1u);
         }
     }
     __syncthreads();

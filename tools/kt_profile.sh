@@ -1,7 +1,7 @@
 #!/bin/bash
 # Kernel-trace profile of the bench workload (rocprofv3 --kernel-trace --stats only) + per-stream timeline.
 OUT=${1:-gpurun_out/kt}
-ARGS=${2:-"--steps 2 --warmup 1 --no-cpu-baseline --full-steps 0 --decode-steps 0 --cdc-steps 0"}
+ARGS=${2:-"--steps 2 --warmup 1 --no-cpu-baseline --full-steps 0 --decode-steps 0 --cdc-steps 0 --v2-steps 0"}
 mkdir -p $OUT
 export TMPDIR=/tmp
 ( for i in $(seq 1 40); do sleep 20; echo "tick $i" >> $OUT/ticks.txt; done ) &

@@ -5,7 +5,7 @@ timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -1 gpurun_out/t_lz.log
 run() {  # name env...
   local n=$1; shift
-  env "$@" timeout -k 10 200 python bench.py --steps 6 --warmup 2 --no-cpu-baseline --full-steps 0 --decode-steps 0 --cdc-steps 0 > gpurun_out/b_$n.json 2>gpurun_out/b_$n.err || return 1
+  env "$@" timeout -k 10 200 python bench.py --steps 6 --warmup 2 --no-cpu-baseline --full-steps 0 --decode-steps 0 --cdc-steps 0 --v2-steps 0 > gpurun_out/b_$n.json 2>gpurun_out/b_$n.err || return 1
   python -c "
 import json;d=json.load(open('gpurun_out/b_$n.json'));x=d['detail'];print('$n', d['value'], d['ms_per_step'], x['lz77'], x['device_ms']['ms_lz'], list(x['kernels_ms_per_step'].items())[:4])"
   grep "k_lz_local us" gpurun_out/b_$n.err | tail -1
