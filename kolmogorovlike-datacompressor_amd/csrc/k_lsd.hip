@@ -5,18 +5,27 @@
 // No host synchronisation: a fixed sequence of launches on the sort stream.
 #include "kolm_internal.h"
 
+#include <algorithm>
 #include <string>
+#include <vector>
 
 namespace kolm {
 
 namespace {
 
-constexpr u32 LSD_T = 4096;          // elements per tile
-constexpr u32 LSD_PT = LSD_T / WG;     // 16 per thread
+#ifndef KOLM_LSD_T
+#define KOLM_LSD_T 4096
+#endif
+constexpr u32 LSD_T = KOLM_LSD_T;    // elements per tile
+constexpr u32 LSD_PT = LSD_T / WG;   // 16 per thread
+static_assert(LSD_PT % 4 == 0 && LSD_PT <= 32, "head masks hold 32 slots per thread");
 
 struct LsdGeom {
     Geom geo;
     u32 tpb;  // tiles per block
+    const u8* text;
+    const u8* FEd;    // min(distance to the factor end, 255)
+    const u64* FSL;   // factor start | length << 32
     __device__ inline bool range(u32 t, u32& lo, u32& hi, u32& b) const {
         b = t / tpb;
         const u32 k = t - b * tpb;
@@ -375,6 +384,110 @@ __global__ __launch_bounds__(WG) void k_r0_final(LsdGeom g, const u32* HF, const
         if (len[e] >= 2) next[off++] = Seg{i0 + e, len[e]};
 }
 
+// ---------------------------------------------------------------------------------
+// Alphabet compaction.  Rotation comparisons inside a block depend only on the ORDER of
+// its byte values, so every byte is replaced by its rank among the block's distinct bytes
+// (code < sigma_b) and a round-0 key packs C = min(32, 64 / w) characters of w = the
+// batch's max ceil(log2 sigma_b) bits each into 64 bits (enwik-style text: 50 distinct
+// bytes -> w = 6, C = 10 characters in the same 8 LSD passes that held 8 raw bytes; bit
+// planes: w = 1, C = 32 in 4 passes).  Fewer positions stay active after round 0
+// (text: 60 % instead of 79 %) and the doubling rounds start at h = C.
+// ---------------------------------------------------------------------------------
+constexpr u32 AL_PER = 65536;  // bytes per workgroup of k_alpha_present
+
+// pres[b * 8 + (c >> 5)] bit (c & 31): byte value c occurs in block b
+__global__ __launch_bounds__(WG) void k_alpha_present(Geom geo, const u8* text, u32 parts, u32* pres) {
+    __shared__ u32 f[256];
+    f[threadIdx.x] = 0;
+    __syncthreads();
+    const u32 b = blockIdx.x / parts, part = blockIdx.x - b * parts;
+    const u32 lo = geo.base(b) + part * AL_PER, hi = min(lo + AL_PER, geo.end(b));
+    for (u32 i = lo + threadIdx.x; i < hi; i += WG) f[text[i]] = 1u;  // benign same-value races
+    __syncthreads();
+    const u64 m = __ballot(f[threadIdx.x] != 0);
+    if ((threadIdx.x & 31) == 0) {
+        const u32 word = (u32)(m >> (threadIdx.x & 32));
+        if (word) atomicOr(&pres[(u64)b * 8 + (threadIdx.x >> 5)], word);
+    }
+}
+
+// code[b * 256 + c] = rank of byte c among block b's byte values; wmax = max bits per code
+__global__ __launch_bounds__(WG) void k_alpha_codes(const u32* pres, u8* code, u32* wmax) {
+    __shared__ u32 pw[8];
+    const u32 b = blockIdx.x, c = threadIdx.x;
+    if (c < 8) pw[c] = pres[(u64)b * 8 + c];
+    __syncthreads();
+    u32 r = 0;
+    for (u32 k = 0; k < (c >> 5); ++k) r += __popc(pw[k]);
+    r += __popc(pw[c >> 5] & ((1u << (c & 31)) - 1u));
+    code[(u64)b * 256 + c] = (u8)r;
+    if (c == 255) {
+        const u32 sigma = r + ((pw[7] >> 31) & 1u);
+        const u32 w = sigma > 1 ? 32 - __clz(sigma - 1) : 1u;
+        atomicMax(wmax, w);
+    }
+}
+
+// Round-0 keys by position: KA = the low 32 bits, KB = the high bits of the packed codes of
+// the first C rotation characters (first character most significant).  A workgroup owns
+// one LSD tile (one block's positions): text [lo, hi + C) and the block's code table in
+// LDS, 16 consecutive positions per thread with a rolling key (drop the oldest character,
+// append the next); positions whose C characters wrap inside their Lyndon factor (FEd <
+// C) are rebuilt from the factor record.
+__global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32 C, u32 w, u32* KA, u32* KB) {
+    __shared__ u8 tx[LSD_T + 64];
+    __shared__ u8 cd[256];
+    u32 lo, hi, b;
+    if (!g.range(xcd_tile(), lo, hi, b)) return;
+    const u32 N = (u32)g.geo.N;
+    cd[threadIdx.x] = code[(u64)b * 256 + threadIdx.x];
+    const u32 n = min(hi + C, N) - lo;
+    for (u32 i = threadIdx.x; i < n; i += WG) tx[i] = g.text[lo + i];
+    __syncthreads();
+    const u32 i0 = threadIdx.x * LSD_PT;
+    if (lo + i0 >= hi) return;
+    const u64 mask = C * w >= 64 ? ~0ull : ((1ull << (C * w)) - 1);
+    u64 key = 0;
+    for (u32 k = 0; k < C; ++k) key = (key << w) | (i0 + k < n ? cd[tx[i0 + k]] : 0u);
+    u32 ka[LSD_PT], kb[LSD_PT];
+#pragma unroll
+    for (u32 e = 0; e < LSD_PT; ++e) {
+        ka[e] = (u32)key;
+        kb[e] = (u32)(key >> 32);
+        const u32 x = i0 + e + C;
+        key = ((key << w) | (x < n ? cd[tx[x]] : 0u)) & mask;
+    }
+#pragma unroll
+    for (u32 e = 0; e < LSD_PT; ++e) {
+        const u32 p = lo + i0 + e;
+        if (p < hi && g.FEd[p] < C) {  // the C characters wrap inside the factor
+            const u64 f = g.FSL[p];
+            const u32 fs = (u32)f, m = (u32)(f >> 32);
+            u32 t = p - fs;
+            u64 k2 = 0;
+            for (u32 k = 0; k < C; ++k) {
+                k2 = (k2 << w) | cd[g.text[fs + t]];
+                if (++t == m) t = 0;
+            }
+            ka[e] = (u32)k2;
+            kb[e] = (u32)(k2 >> 32);
+        }
+    }
+    const u32 p0 = lo + i0;
+    if ((p0 & 3) == 0 && p0 + LSD_PT <= hi) {
+#pragma unroll
+        for (u32 q = 0; q < LSD_PT / 4; ++q) {
+            reinterpret_cast<uint4*>(KA + p0)[q] = make_uint4(ka[4 * q], ka[4 * q + 1], ka[4 * q + 2], ka[4 * q + 3]);
+            if (KB) reinterpret_cast<uint4*>(KB + p0)[q] = make_uint4(kb[4 * q], kb[4 * q + 1], kb[4 * q + 2], kb[4 * q + 3]);
+        }
+    } else {
+        for (u32 e = 0; e < LSD_PT && p0 + e < hi; ++e) {
+            KA[p0 + e] = ka[e];
+            if (KB) KB[p0 + e] = kb[e];
+        }
+    }
+}
+
 template <int P, int SRC, int G>
 void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kout, u32* pout, const u32* kg,
               u32* hist, hipStream_t s, KTimer* kt) {
@@ -397,42 +510,87 @@ void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kou
     }
 }
 
+using PassFn = void (*)(const LsdGeom&, u32, const u32*, const u32*, u32*, u32*, const u32*, u32*, hipStream_t,
+                        KTimer*);
+template <int P>
+constexpr PassFn pass_of(int src_kp, int gat) {
+    return src_kp ? (gat ? lsd_pass<P, SRC_KP, 1> : lsd_pass<P, SRC_KP, 0>)
+                  : (gat ? lsd_pass<P, SRC_PAIR, 1> : lsd_pass<P, SRC_PAIR, 0>);
+}
+void run_pass(int P, bool src_kp, bool gat, const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kout,
+              u32* pout, const u32* kg, u32* hist, hipStream_t s, KTimer* kt) {
+    const int a = src_kp ? 1 : 0, c = gat ? 1 : 0;
+    const PassFn f = P == 0 ? pass_of<0>(a, c) : P == 1 ? pass_of<1>(a, c) : P == 2 ? pass_of<2>(a, c) : pass_of<3>(a, c);
+    f(g, nt, kin, pin, kout, pout, kg, hist, s, kt);
+}
+
 }  // namespace
 
 u32 lsd_tiles(const Geom& geo) { return (geo.bs + LSD_T - 1) / LSD_T * geo.nb; }
 
-// Round 0 of the cyclic sort: a stable sort of every block's positions by the first 4 or 8
-// rotation characters (KP = characters 0..3 by position; 8 characters: RK holds characters
-// 4..7 by position on entry).  4 characters: (KP, p) -> (K2, SA) -> (K22, SA2) -> (KP, RK) ->
-// (K2, SA).  8 characters: 4 passes over characters 4..7 (RK, p) -> (K22, SA2) -> (K2, SA)
-// -> (K22, SA2) -> (K2 = KP[SA], SA), then 4 over characters 0..3 ending in (K2, SA).  Then
-// group heads (HF), ranks and next-round segments.
+// Per-block code tables (alphabet compaction); returns the max code width w of the batch
+// (one host round trip).  compact = false: identity codes, w = 8.
+u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w, u32* h_w, bool compact,
+                 hipStream_t s, KTimer* kt) {
+    if (!geo.N) return 8;
+    if (!compact) {
+        std::vector<u8> id(256 * (size_t)geo.nb);
+        for (size_t i = 0; i < id.size(); ++i) id[i] = (u8)i;
+        KOLM_HIP_CHECK(hipMemcpyAsync(code, id.data(), id.size(), hipMemcpyHostToDevice, s));
+        KOLM_HIP_CHECK(hipStreamSynchronize(s));
+        return 8;
+    }
+    const u32 parts = (geo.bs + AL_PER - 1) / AL_PER;
+    KOLM_HIP_CHECK(hipMemsetAsync(pres, 0, sizeof(u32) * 8 * geo.nb, s));
+    KOLM_HIP_CHECK(hipMemsetAsync(d_w, 0, sizeof(u32), s));
+    {
+        KScope k(kt, KT_LSD, "k_alpha_present", geo.N);
+        k_alpha_present<<<parts * geo.nb, WG, 0, s>>>(geo, text, parts, pres);
+        k_alpha_codes<<<geo.nb, WG, 0, s>>>(pres, code, d_w);
+    }
+    KOLM_HIP_CHECK(hipMemcpyAsync(h_w, d_w, sizeof(u32), hipMemcpyDeviceToHost, s));
+    KOLM_HIP_CHECK(hipStreamSynchronize(s));
+    return std::max<u32>(1, std::min<u32>(8, *h_w));
+}
+
+// Round 0 of the cyclic sort: a stable sort of every block's positions by the packed codes
+// of their first C rotation characters (k_keypos_r0: KA = low 32 bits -> RK, KB = high bits
+// -> KP, by position).  LSD passes over the digits of KA (text order -> ... ), the last of
+// them writing KB[SA] as the next key when KB has digits, then over the digits of KB; the
+// passes alternate (K2, SA) / (K22, SA2) and end in (K2, SA).  A slot heads a group when K2
+// differs from the previous slot's or (two halves) KA[SA[slot]] does: head masks (HF), then
+// ranks and next-round segments.
 void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s,
                    KTimer* kt) {
     if (!geo.N) return;
-    LsdGeom g{geo, (geo.bs + LSD_T - 1) / LSD_T};
+    LsdGeom g{geo, (geo.bs + LSD_T - 1) / LSD_T, t.text, t.FEd, t.FSL};
     const u32 nt = g.tpb * geo.nb;
     const u64 N = geo.N;
-    const bool c8 = t.chars == 8;
-    if (!c8) {
-        lsd_pass<0, SRC_KP, 0>(g, nt, t.KP, nullptr, t.K2, t.SA, nullptr, t.hist, s, kt);
-        lsd_pass<1, SRC_PAIR, 0>(g, nt, t.K2, t.SA, t.K22, t.SA2, nullptr, t.hist, s, kt);
-        lsd_pass<2, SRC_PAIR, 0>(g, nt, t.K22, t.SA2, t.KP, t.RK, nullptr, t.hist, s, kt);
-        lsd_pass<3, SRC_PAIR, 0>(g, nt, t.KP, t.RK, t.K2, t.SA, nullptr, t.hist, s, kt);
-    } else {
-        lsd_pass<0, SRC_KP, 0>(g, nt, t.RK, nullptr, t.K22, t.SA2, nullptr, t.hist, s, kt);
-        lsd_pass<1, SRC_PAIR, 0>(g, nt, t.K22, t.SA2, t.K2, t.SA, nullptr, t.hist, s, kt);
-        lsd_pass<2, SRC_PAIR, 0>(g, nt, t.K2, t.SA, t.K22, t.SA2, nullptr, t.hist, s, kt);
-        lsd_pass<3, SRC_PAIR, 1>(g, nt, t.K22, t.SA2, t.K2, t.SA, t.KP, t.hist, s, kt);
-        lsd_pass<0, SRC_PAIR, 0>(g, nt, t.K2, t.SA, t.K22, t.SA2, nullptr, t.hist, s, kt);
-        lsd_pass<1, SRC_PAIR, 0>(g, nt, t.K22, t.SA2, t.K2, t.SA, nullptr, t.hist, s, kt);
-        lsd_pass<2, SRC_PAIR, 0>(g, nt, t.K2, t.SA, t.K22, t.SA2, nullptr, t.hist, s, kt);
-        lsd_pass<3, SRC_PAIR, 0>(g, nt, t.K22, t.SA2, t.K2, t.SA, nullptr, t.hist, s, kt);
+    const u32 bits = t.chars * t.w;
+    const u32 pa = std::min<u32>(4, (bits + 7) / 8), pb = bits > 32 ? (bits - 32 + 7) / 8 : 0u;
+    {
+        // text + FEd 2 (+ FSL near factor ends), KA 4 (+ KB 4)
+        KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6));
+        k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, t.RK, pb ? t.KP : nullptr);
+    }
+    u32* K[2] = {t.K2, t.K22};
+    u32* S[2] = {t.SA, t.SA2};
+    const u32 T = pa + pb;
+    int o = (T & 1) ? 0 : 1;  // output pair of the first pass: the last one lands in (K2, SA)
+    for (u32 q = 0; q < pa; ++q) {
+        const bool first = q == 0, gat = q + 1 == pa && pb > 0;
+        run_pass((int)q, first, gat, g, nt, first ? t.RK : K[o ^ 1], first ? nullptr : S[o ^ 1], K[o], S[o],
+                 gat ? t.KP : nullptr, t.hist, s, kt);
+        o ^= 1;
+    }
+    for (u32 q = 0; q < pb; ++q) {
+        run_pass((int)q, false, false, g, nt, K[o ^ 1], S[o ^ 1], K[o], S[o], nullptr, t.hist, s, kt);
+        o ^= 1;
     }
     {
         // K 4 (+ SA 4 + the KA gather 4) read, head masks written
-        KScope k(kt, KT_LSD, "k_r0_tile_heads", (c8 ? 12 : 4) * N);
-        k_r0_tile_heads<<<nt, WG, 0, s>>>(g, t.K2, t.SA, c8 ? t.RK : nullptr, t.HF, t.tmax, t.tmin);
+        KScope k(kt, KT_LSD, "k_r0_tile_heads", (pb ? 12 : 4) * N);
+        k_r0_tile_heads<<<nt, WG, 0, s>>>(g, t.K2, t.SA, pb ? t.RK : nullptr, t.HF, t.tmax, t.tmin);
         k_tiles_max_scan<<<geo.nb, WG, 0, s>>>(t.tmax, t.cmax, g.tpb);
         k_r0_tiles_rscan<<<geo.nb, WG, 0, s>>>(t.tmin, t.cmin, g.tpb);
     }

@@ -43,6 +43,7 @@ enum : int {
     C_NEXT = 12,
     C_EQ = 13,
     C_ACTIVE = 14,
+    C_ALPHA = 15,    // round 0: max code width of the batch
     C_L0SEG = 16,
     C_L0TILE = 17,
     C_L1SEG = 18,
@@ -229,6 +230,7 @@ const char* const kSmallSortName[2][NCLASS] = {
 struct SortOut {
     u32 rounds = 0;
     u64 active = 0;
+    u32 r0_chars = 0;  // cyclic: rotation characters of round 0
 };
 
 // Segmented prefix-doubling suffix sort of every block of the batch (k_sort.hip).
@@ -288,9 +290,9 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
     Seg* cur = segA;
     Seg* nxt = segB;
     u32 ncur = geo.nb;
-    // cyclic round 0 sorts by 8 rotation characters (KOLM_R0_CHARS=4: by 4, one more doubling round)
-    static const int r0_chars = getenv("KOLM_R0_CHARS") && atoi(getenv("KOLM_R0_CHARS")) == 4 ? 4 : 8;
-    const u32 h0 = cyclic ? (u32)r0_chars : 3;
+    // cyclic: round 0 sorts by C rotation characters (alphabet-compacted codes, launch_alpha),
+    // the doubling rounds continue at h = C
+    u32 h0 = cyclic ? 8 : 3;
     const u32 kb_rank = bitlen(geo.bs) ? bitlen(geo.bs) : 1;
     u32* h = c->h_cnt;
     static const bool dbg = getenv("KOLM_DEBUG_ROUNDS") != nullptr;
@@ -313,20 +315,21 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
         KOLM_HIP_CHECK(hipMemsetAsync(cnt + C_CLSE, 0, sizeof(u32) * (C_N - C_CLSE), s));
         KOLM_HIP_CHECK(hipMemsetAsync(a.blk_split, 0, sizeof(u32) * geo.nb, s));
         if (round == 0 && cyclic) {
-            // round 0: stable LSD passes over the 8 (4) rotation characters, no host round trips
-            u32* KP = c->get<u32>("KP", N);
-            {
-                // FEd 1 + text 4 (overlapping) + KP 4 (+ characters 4..7 into RK: 4)
-                TScope t(c, KOLM_KT_KEYGEN, "k_keypos", N * (r0_chars == 8 ? 13 : 9));
-                a.KP = nullptr;
-                a.KA = r0_chars == 8 ? a.RK : nullptr;
-                launch_keypos(a, KP, s);
-                a.KA = nullptr;
-            }
+            // round 0: stable LSD passes over the packed codes of the first C rotation
+            // characters (KOLM_R0_ALPHA=0: raw bytes, C = 8), no host round trips but one
+            static const bool compact = !(getenv("KOLM_R0_ALPHA") && atoi(getenv("KOLM_R0_ALPHA")) == 0);
             const u64 nt = lsd_tiles(geo) + 1;
-            R0Bufs r{KP, a.K2, a.SA, a.K22, a.SA2, a.RK, c->get<u32>("r0hist", nt * 256), c->get<u32>("r0tmax", nt),
-                     c->get<u32>("r0tmin", nt), c->get<u32>("r0cmax", nt), c->get<u32>("r0cmin", nt),
-                     c->get<u32>("r0hf", nt * WG), r0_chars};
+            u8* code = c->get<u8>("r0code", (u64)geo.nb * 256);
+            const u32 w = launch_alpha(geo, text, c->get<u32>("r0pres", (u64)geo.nb * 8), code, cnt + C_ALPHA,
+                                       h + C_ALPHA, compact, s, c->kt());
+            static const u32 cmax = getenv("KOLM_R0_CMAX") ? (u32)atoi(getenv("KOLM_R0_CMAX")) : 32u;  // A/B
+            const u32 C = std::max<u32>(1, std::min<u32>(std::min<u32>(32, cmax), 64 / w));
+            h0 = C;
+            R0Bufs r{text, FEd, FSL, code, C, w, c->get<u32>("KP", N), a.K2, a.SA, a.K22, a.SA2, a.RK,
+                     c->get<u32>("r0hist", nt * 256), c->get<u32>("r0tmax", nt), c->get<u32>("r0tmin", nt),
+                     c->get<u32>("r0cmax", nt), c->get<u32>("r0cmin", nt), c->get<u32>("r0hf", nt * WG)};
+            out.r0_chars = C;
+            if (dbg) fprintf(stderr, "[kolm] round 0: %u characters of %u bits\n", C, w);
             launch_round0(geo, r, nxt, L.next_cnt, a.blk_split, s, c->kt());
             out.active += N;
             out.rounds = 1;
@@ -951,14 +954,14 @@ int ctx_create(int device, kolm_ctx** out) {
         KOLM_HIP_CHECK(hipSetDevice(device));
         std::unique_ptr<kolm_ctx> c(new kolm_ctx);
         c->device = device;
-        KOLM_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         {
             // the sort chain (aux) is the critical path: give it the higher priority so its
-            // workgroups dispatch ahead of the 3-gram index / LZ77 stream (KOLM_PRIO=0: equal)
+            // workgroups dispatch ahead of the LZ77 stream (KOLM_PRIO=0: equal, 2: LZ77 higher)
             int lo = 0, hi = 0;
             KOLM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            const bool prio = !getenv("KOLM_PRIO") || atoi(getenv("KOLM_PRIO")) != 0;
-            KOLM_HIP_CHECK(hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, prio ? hi : lo));
+            const int prio = getenv("KOLM_PRIO") ? atoi(getenv("KOLM_PRIO")) : 1;
+            KOLM_HIP_CHECK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio == 2 ? hi : lo));
+            KOLM_HIP_CHECK(hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, prio == 1 ? hi : lo));
         }
         KOLM_HIP_CHECK(hipStreamCreateWithFlags(&c->rp, hipStreamNonBlocking));
         c->active = c->stream;

@@ -263,18 +263,25 @@ void launch_bbwt_gather(const Geom& geo, const u32* SA, const u8* prevc, u8* out
 // ---- k_lsd.hip: per-block LSD radix passes: round 0 of the cyclic sort ----
 u32 lsd_tiles(const Geom& geo);
 struct R0Bufs {
-    u32* KP;   // [N] in: keys by position (characters 0..3 of the rotation); scratch afterwards
+    const u8* text;
+    const u8* FEd;    // min(distance to the factor end, 255)
+    const u64* FSL;   // factor start | length << 32 (read only where the C characters wrap)
+    const u8* code;   // [nb * 256] per-block byte -> code (launch_alpha)
+    u32 chars;        // C rotation characters per key
+    u32 w;            // bits per code
+    u32* KP;   // [N] scratch: high key bits by position (KB)
     u32* K2;   // [N] out: sorted keys (scratch)
-    u32* SA;   // [N] out: positions in 4-character order (ties by position)
+    u32* SA;   // [N] out: positions in C-character order (ties by position)
     u32* K22;  // [N] scratch
     u32* SA2;  // [N] scratch
-    u32* RK;   // [N] out: group start slot of every position.  8-character round 0: in,
-               // characters 4..7 of the rotation by position (read before RK is written)
+    u32* RK;   // [N] out: group start slot of every position (low key bits KA by position first)
     u32* hist;                    // [lsd_tiles * 256]
     u32 *tmax, *tmin, *cmax, *cmin;  // [lsd_tiles]
-    u32* HF;   // [lsd_tiles * WG] group-head masks (16 slots per thread)
-    int chars; // 4 or 8 rotation characters
+    u32* HF;   // [lsd_tiles * WG] group-head masks (LSD_T / WG slots per thread)
 };
+// per-block code tables for round 0 (alphabet compaction), max code width of the batch
+u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w, u32* h_w, bool compact,
+                 hipStream_t s, KTimer* kt = nullptr);
 void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s,
                    KTimer* kt = nullptr);
 

@@ -440,3 +440,33 @@ def test_v2new_multiblock_vs_oracle(kolm_gpu, bs):
     _, _, forced, _ = _lib.encode_blocks(data, bs, cand_mask=1 << 10, force=[10] * nb)
     for i in range(nb):
         assert forced[i] == O.candidate(10, data[i * bs:(i + 1) * bs]), f"block {i}"
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sigma", [1, 2, 3, 5, 16, 17, 33, 64, 65, 129, 256])
+def test_round0_alphabet_widths(kolm_gpu, sigma):
+    """Round 0 packs C = min(32, 64 / w) alphabet-compacted characters (w = bits of the
+    block's distinct-byte count): every code width 1..8 and its boundaries, on random text
+    over sigma scattered byte values (short Lyndon factors: the C characters wrap)."""
+    rng = np.random.default_rng(sigma)
+    vals = rng.choice(256, sigma, replace=False).astype(np.uint8)
+    data = vals[rng.integers(0, sigma, 30000)].tobytes()
+    assert kolm_gpu.bbwt_forward(data) == O.bbwt_forward(data)
+
+
+@pytest.mark.gpu
+def test_round0_alphabet_mixed_batch(kolm_gpu):
+    """One batch whose blocks have different alphabets (1, 3, 17, 50, 256 distinct bytes):
+    the batch's code width is the widest block's, every block keeps its own code table."""
+    from kolm import _lib
+    rng = np.random.default_rng(7)
+    bs = 8192
+    parts = [bytes(bs), rng.choice([7, 99, 200], bs).astype(np.uint8).tobytes(),
+             rng.choice(np.arange(40, 57), bs).astype(np.uint8).tobytes(), D.enwik_like(bs, seed=5),
+             rng.integers(0, 256, bs).astype(np.uint8).tobytes(), b"ab" * 1000]
+    data = b"".join(parts)
+    sizes, method, payloads, _ = _lib.encode_blocks(data, bs)
+    for i in range((len(data) + bs - 1) // bs):
+        blk = data[i * bs:(i + 1) * bs]
+        cand = _oracle_all(blk)
+        assert list(map(int, sizes[i][:10])) == [len(c) for c in cand], f"block {i}"
+        assert payloads[i] == cand[int(method[i])], f"block {i}"
