@@ -80,11 +80,10 @@ __device__ inline u64 lds8(const u8* l, u32 x) {
 // A workgroup owns the LZL_HOME home positions [hs, he) of one block.  Every candidate of
 // a home position p lies in [p - 4096, p), so the window W = [hs - 4096 - LZL_LEAD, he)
 // (clipped to the block) holds them all.  The workgroup copies W's text into LDS, sorts
-// W's 3-gram positions by (3-gram, position) with three stable LSD byte passes in LDS
-// (u16 window offsets; no global traffic), and keeps the slot of every home position
-// (islot) and a group-head bitmap: p's candidates are the slots islot(p)-1, islot(p)-2, ...
-// down to p's group start, in ascending distance — the same contiguous-slot walk as the
-// global index, with every load an LDS load.
+// W's 3-gram positions by (hash of the 3-gram, position) with one stable counting-sort pass
+// in LDS (u16 window offsets; no global traffic), and keeps the slot of every home position
+// (islot) and a bucket-head bitmap: p's candidates are the slots islot(p)-1, islot(p)-2, ...
+// down to p's bucket start, in ascending distance, every load an LDS load.
 //
 // The home is parsed by 16 speculative chains (16 lanes each, 4 per wave) over 256-byte
 // chunks.  A chain starts LZL_LEAD bytes before its chunk (a lead-in whose tokens are not
@@ -333,22 +332,23 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
     const u32 nw = top > lo ? top - lo : 0u;
     const u8* tw = txt + (lo - tlo);  // window text at window offset 0
     if (z.prof) t1 = wall_clock64();
+    u16* isl = B;
+    u64* bm = reinterpret_cast<u64*>(B + LZL_ISL);  // disjoint from the sort's histograms
+    for (u32 i = tid; i < (nw + 63) / 64; i += 256) bm[i] = 0;
     if (nw) {
         lzl_bucket(tw, A, nw, hist, sh);
-    }
-    // islot of [ilo, he) and the group-head bitmap
-    u16* isl = B;
-    u64* bm = reinterpret_cast<u64*>(B + LZL_ISL);
-    for (u32 j0 = 0; j0 < nw; j0 += 256) {
-        const u32 j = j0 + tid;
-        bool head = false;
-        if (j < nw) {
-            const u32 x = A[j];
-            if (lo + x >= ilo) isl[lo + x - ilo] = (u16)j;
-            head = j == 0 || hash3(tw, x) != hash3(tw, A[j - 1]);
+        // group-head bitmap = the starts of the non-empty buckets: after the placement, wave
+        // 3's offset of bucket d is the bucket's end (bucket-major / wave-minor layout)
+        for (u32 d = tid; d < LZL_NBK; d += 256) {
+            const u32 e = hist[3 * LZL_NBK + d], st = d ? hist[3 * LZL_NBK + d - 1] : 0u;
+            if (e > st) atomicOr(&bm[st >> 6], 1ull << (st & 63));
         }
-        const u64 bal = __ballot(head);
-        if (lane == 0 && j0 + w * 64 < nw) bm[(j0 >> 6) + w] = bal;
+        __syncthreads();  // the islot writes below overwrite the histograms
+    }
+    // islot of [ilo, he)
+    for (u32 j = tid; j < nw; j += 256) {
+        const u32 x = A[j];
+        if (lo + x >= ilo) isl[lo + x - ilo] = (u16)j;
     }
     if (z.prof) t2 = wall_clock64();
     __syncthreads();
