@@ -434,33 +434,53 @@ __global__ __launch_bounds__(WG) void k_alpha_codes(const u32* pres, u8* code, u
 // LDS, 16 consecutive positions per thread with a rolling key (drop the oldest character,
 // append the next); positions whose C characters wrap inside their Lyndon factor (FEd <
 // C) are rebuilt from the factor record.
-__global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32 C, u32 w, u32* KA, u32* KB) {
-    __shared__ u8 tx[LSD_T + 64];
+__global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32 C, u32 w, u32 sh, u32* KA, u32* KB) {
+    __shared__ __align__(16) u8 tx[LSD_T + 64];
     __shared__ u8 cd[256];
     u32 lo, hi, b;
     if (!g.range(xcd_tile(), lo, hi, b)) return;
     const u32 N = (u32)g.geo.N;
     cd[threadIdx.x] = code[(u64)b * 256 + threadIdx.x];
     const u32 n = min(hi + C, N) - lo;
-    for (u32 i = threadIdx.x; i < n; i += WG) tx[i] = g.text[lo + i];
+    if ((((uintptr_t)g.text + lo) & 3) == 0) {  // dword copies (a dword that starts before N is allocated)
+        const u32* src = reinterpret_cast<const u32*>(g.text + lo);
+        u32* dst = reinterpret_cast<u32*>(tx);
+        for (u32 i = threadIdx.x; i < (n + 3) / 4; i += WG) dst[i] = src[i];
+    } else {
+        for (u32 i = threadIdx.x; i < n; i += WG) tx[i] = g.text[lo + i];
+    }
     __syncthreads();
     const u32 i0 = threadIdx.x * LSD_PT;
     if (lo + i0 >= hi) return;
+    // the 16 distances to the factor end (one 16-byte load when aligned and whole)
+    u8 fed[LSD_PT];
+    if (((lo + i0) & 15) == 0 && lo + i0 + LSD_PT <= hi) {
+#pragma unroll
+        for (u32 q = 0; q < LSD_PT / 16; ++q) {
+            const uint4 v = reinterpret_cast<const uint4*>(g.FEd + lo + i0)[q];
+            const u32 wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (u32 e = 0; e < 16; ++e) fed[16 * q + e] = (u8)(wd[e >> 2] >> (8 * (e & 3)));
+        }
+    } else {
+#pragma unroll
+        for (u32 e = 0; e < LSD_PT; ++e) fed[e] = lo + i0 + e < hi ? g.FEd[lo + i0 + e] : (u8)255;
+    }
     const u64 mask = C * w >= 64 ? ~0ull : ((1ull << (C * w)) - 1);
     u64 key = 0;
     for (u32 k = 0; k < C; ++k) key = (key << w) | (i0 + k < n ? cd[tx[i0 + k]] : 0u);
     u32 ka[LSD_PT], kb[LSD_PT];
 #pragma unroll
     for (u32 e = 0; e < LSD_PT; ++e) {
-        ka[e] = (u32)key;
-        kb[e] = (u32)(key >> 32);
+        ka[e] = (u32)(key << sh);
+        kb[e] = (u32)((key << sh) >> 32);
         const u32 x = i0 + e + C;
         key = ((key << w) | (x < n ? cd[tx[x]] : 0u)) & mask;
     }
 #pragma unroll
     for (u32 e = 0; e < LSD_PT; ++e) {
         const u32 p = lo + i0 + e;
-        if (p < hi && g.FEd[p] < C) {  // the C characters wrap inside the factor
+        if (p < hi && fed[e] < C) {  // the C characters wrap inside the factor
             const u64 f = g.FSL[p];
             const u32 fs = (u32)f, m = (u32)(f >> 32);
             u32 t = p - fs;
@@ -469,8 +489,8 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
                 k2 = (k2 << w) | cd[g.text[fs + t]];
                 if (++t == m) t = 0;
             }
-            ka[e] = (u32)k2;
-            kb[e] = (u32)(k2 >> 32);
+            ka[e] = (u32)(k2 << sh);
+            kb[e] = (u32)((k2 << sh) >> 32);
         }
     }
     const u32 p0 = lo + i0;
@@ -566,12 +586,14 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
     LsdGeom g{geo, (geo.bs + LSD_T - 1) / LSD_T, t.text, t.FEd, t.FSL};
     const u32 nt = g.tpb * geo.nb;
     const u64 N = geo.N;
-    const u32 bits = t.chars * t.w;
-    const u32 pa = std::min<u32>(4, (bits + 7) / 8), pb = bits > 32 ? (bits - 32 + 7) / 8 : 0u;
+    // D byte digits; the packed codes are left-aligned in them, so the 8 D - C w padding bits
+    // fall into the first pass's digit (its few distinct values keep that scatter's runs long)
+    const u32 bits = t.chars * t.w, D = (bits + 7) / 8, sh = 8 * D - bits;
+    const u32 pa = std::min<u32>(4, D), pb = D - pa;
     {
         // text + FEd 2 (+ FSL near factor ends), KA 4 (+ KB 4)
         KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6));
-        k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, t.RK, pb ? t.KP : nullptr);
+        k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr);
     }
     u32* K[2] = {t.K2, t.K22};
     u32* S[2] = {t.SA, t.SA2};
