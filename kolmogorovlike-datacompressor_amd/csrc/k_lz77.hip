@@ -115,7 +115,7 @@ struct WinText {
 // positions by hash (ascending position inside a bucket); a candidate whose 3-gram differs
 // is rejected by the first byte compare, so other 3-grams sharing the bucket only cost
 // lanes (about 4096 / 2^LZL_HB of them per token).
-constexpr u32 LZL_HB = 9;
+constexpr u32 LZL_HB = 10;
 constexpr u32 LZL_NBK = 1u << LZL_HB;
 __device__ inline u32 hash3(const u8* t, u32 x) {
     const u32 k = ((u32)t[x] << 16) | ((u32)t[x + 1] << 8) | t[x + 2];
@@ -130,7 +130,9 @@ constexpr u32 LZL_PER = (LZL_NW + 255) / 256;  // window elements per lane (33)
 // order (ballot match-any ranking over the LZL_HB hash bits; the leader advances the
 // wave's bucket offset — a wave's LDS operations retire in program order, so no barrier
 // is needed between its steps).
-__device__ void lzl_bucket(const u8* t, u16* A, u32 nw, u32* hist /*[4][LZL_NBK]*/, u32* sh) {
+// hist: [4][LZL_NBK] 16-bit counters / offsets (window positions < 2^16; a count is added
+// to its dword with the half's shift, plain 16-bit stores otherwise)
+__device__ void lzl_bucket(const u8* t, u16* A, u32 nw, u16* hist, u32* sh) {
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     constexpr u32 R = LZL_NBK / 256;  // buckets per thread in the scan
     const u32 Q = (nw + 3) / 4;
@@ -141,11 +143,12 @@ __device__ void lzl_bucket(const u8* t, u16* A, u32 nw, u32* hist /*[4][LZL_NBK]
         const u32 e = b0 + k * 64 + lane;
         hv[k] = e < b1 ? hash3(t, e) : 0u;
     }
-    for (u32 i = tid; i < 4 * LZL_NBK; i += 256) hist[i] = 0;
+    for (u32 i = tid; i < 2 * LZL_NBK; i += 256) reinterpret_cast<u32*>(hist)[i] = 0;
     __syncthreads();
 #pragma unroll
     for (u32 k = 0; k < LZL_PER; ++k)
-        if (b0 + k * 64 + lane < b1) atomicAdd(&hist[w * LZL_NBK + hv[k]], 1u);
+        if (b0 + k * 64 + lane < b1)
+            atomicAdd(reinterpret_cast<u32*>(hist) + ((w * LZL_NBK + hv[k]) >> 1), 1u << (16 * (hv[k] & 1)));
     __syncthreads();
     {
         u32 h[4][R], tot = 0;
@@ -165,7 +168,7 @@ __device__ void lzl_bucket(const u8* t, u16* A, u32 nw, u32* hist /*[4][LZL_NBK]
         for (u32 r = 0; r < R; ++r)
 #pragma unroll
             for (u32 q = 0; q < 4; ++q) {
-                hist[q * LZL_NBK + tid * R + r] = ex;
+                hist[q * LZL_NBK + tid * R + r] = (u16)ex;
                 ex += h[q][r];
             }
     }
@@ -186,7 +189,7 @@ __device__ void lzl_bucket(const u8* t, u16* A, u32 nw, u32* hist /*[4][LZL_NBK]
         const u32 rank = (u32)__popcll(m & lt);
         const u32 o = valid ? hist[w * LZL_NBK + dg] : 0u;
         if (valid) A[o + rank] = (u16)e;
-        if (valid && rank == 0) hist[w * LZL_NBK + dg] = o + (u32)__popcll(m);
+        if (valid && rank == 0) hist[w * LZL_NBK + dg] = (u16)(o + (u32)__popcll(m));
     }
     __syncthreads();
 }
@@ -300,8 +303,8 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
     // islot of [ilo, he) + head bitmap; the sort's histograms live here before them
     __shared__ __align__(16) u16 B[LZL_ISL + 4 * ((LZL_NW + 63) / 64)];
     __shared__ u32 sh[4];
-    u32* hist = reinterpret_cast<u32*>(B);
-    static_assert(sizeof(u32) * 4 * LZL_NBK <= sizeof(B), "histograms alias the islot array + bitmap");
+    u16* hist = B;  // the counting sort's 16-bit histograms (dead once the islot array is written)
+    static_assert(sizeof(u16) * 4 * LZL_NBK <= sizeof(B), "histograms alias the islot array + bitmap");
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const u32 b = blockIdx.x / hpb, h = blockIdx.x - b * hpb;
     const u32 base = z.geo.base(b), end = z.geo.end(b);
