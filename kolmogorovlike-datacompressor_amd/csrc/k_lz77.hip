@@ -10,7 +10,7 @@
 //   * k_lz_local: one workgroup per 4 KiB "home" of a block.  Any match >= 3 starts with
 //     an equal 3-gram, so p's candidates are the earlier positions of its 3-gram inside
 //     [p - 4096, p).  The workgroup copies the window [home - 4096 - lead-in, home end)
-//     to LDS, buckets its positions by a 9-bit 3-gram hash with one stable counting-sort
+//     to LDS, buckets its positions by a 10-bit 3-gram hash with one stable counting-sort
 //     pass in LDS, and parses the home with 16 speculative chains (16 lanes = 16
 //     candidates at a time, nearest first; max length, ties -> nearest);
 //   * k_lz_stitch_l: per block, the TRUE path over the chunk summaries: a chunk whose
