@@ -322,8 +322,8 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
             u8* code = c->get<u8>("r0code", (u64)geo.nb * 256);
             const u32 w = launch_alpha(geo, text, c->get<u32>("r0pres", (u64)geo.nb * 8), code, cnt + C_ALPHA,
                                        h + C_ALPHA, compact, s, c->kt());
-            static const u32 cmax = getenv("KOLM_R0_CMAX") ? (u32)atoi(getenv("KOLM_R0_CMAX")) : 32u;  // A/B
-            const u32 C = std::max<u32>(1, std::min<u32>(std::min<u32>(32, cmax), 64 / w));
+            static const u32 cmax = getenv("KOLM_R0_CMAX") ? (u32)atoi(getenv("KOLM_R0_CMAX")) : 32u;  // A/B (<= 64)
+            const u32 C = std::max<u32>(1, std::min<u32>(std::min<u32>(64, cmax), 64 / w));
             h0 = C;
             R0Bufs r{text, FEd, FSL, code, C, w, c->get<u32>("KP", N), a.K2, a.SA, a.K22, a.SA2, a.RK,
                      c->get<u32>("r0hist", nt * 256), c->get<u32>("r0tmax", nt), c->get<u32>("r0tmin", nt),
