@@ -233,6 +233,7 @@ __device__ void lzl_best(const u8* txt, u32 tlo, const u16* A, const u64* bm, co
     }
     const u32 capl = min((u32)LZ_CAP, lim);
     const u32 pr = p - tlo;
+    const u64 pv = go ? lds8(txt, pr) : 0ull;  // p's first 8 bytes, once per token
     while (__ballot(go)) {
         ++nbatch;
         const u32 qn = (go && k0 > 16 + hl) ? (u32)A[k0 - 17 - hl] : 0u;  // next batch
@@ -243,7 +244,7 @@ __device__ void lzl_best(const u8* txt, u32 tlo, const u16* A, const u64* bm, co
         u32 l = 0;
         if (valid) {
             const u32 qr = q - tlo;
-            const u64 d0 = lds8(txt, pr) ^ lds8(txt, qr);
+            const u64 d0 = pv ^ lds8(txt, qr);
             if ((d0 & 0xFFFFFFull) == 0) {  // same 3-gram (not just the same hash)
                 if (d0) {
                     l = (u32)(__ffsll((long long)d0) - 1) >> 3;
