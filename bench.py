@@ -486,6 +486,8 @@ def main():
                        "kernels_ms_per_step": {kk: round(v["ms"] / a.steps, 3) for kk, v in
                                                sorted(ktimes.items(), key=lambda kv: -kv[1]["ms"])[:12]}},
         }
+        if os.environ.get("KOLM_BENCH_ALLK"):  # A/B tooling (tools/kab.sh): every kernel
+            out["detail"]["kernels_all_ms_per_step"] = {kk: round(v["ms"] / a.steps, 3) for kk, v in ktimes.items()}
         if cpu:
             out["detail"]["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         print(json.dumps(out), flush=True)
