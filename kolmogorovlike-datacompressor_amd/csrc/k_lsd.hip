@@ -6,6 +6,7 @@
 #include "kolm_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -73,6 +74,57 @@ __global__ __launch_bounds__(WG) void k_lsd_hist(LsdGeom g, const u32* K, u32* h
     }
     __syncthreads();
     hist[(u64)xcd_tile() * 256 + tid] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+}
+
+// The same histograms, TPW tiles per workgroup: every tile's keys are loaded up front (TPW x
+// 64 B per thread in flight instead of 64 B), then counted into per-tile LDS histograms.
+template <int P, int TPW>
+__global__ __launch_bounds__(WG) void k_lsd_hist_m(LsdGeom g, const u32* K, u32* hist, u32 nt) {
+    __shared__ u32 h[TPW][WG / 64][256];
+    const u32 tid = threadIdx.x, w = tid >> 6;
+#pragma unroll
+    for (int k = 0; k < TPW; ++k)
+#pragma unroll
+        for (int i = 0; i < WG / 64; ++i) h[k][i][tid] = 0;
+    const u32 t0 = xcd_tile() * TPW;
+    uint4 v[TPW][LSD_PT / 4];
+    bool whole[TPW];
+    u32 lo[TPW], hi[TPW];
+#pragma unroll
+    for (int k = 0; k < TPW; ++k) {
+        u32 b;
+        whole[k] = false;
+        lo[k] = hi[k] = 0;
+        if (t0 + k < nt && g.range(t0 + k, lo[k], hi[k], b)) {
+            const u32 i0 = lo[k] + tid * LSD_PT;
+            whole[k] = (i0 & 3) == 0 && i0 + LSD_PT <= hi[k];
+            if (whole[k]) {
+                const uint4* p = reinterpret_cast<const uint4*>(K + i0);
+#pragma unroll
+                for (u32 q = 0; q < LSD_PT / 4; ++q) v[k][q] = p[q];
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < TPW; ++k) {
+        if (whole[k]) {
+#pragma unroll
+            for (u32 q = 0; q < LSD_PT / 4; ++q) {
+                atomicAdd(&h[k][w][digit<P>(v[k][q].x)], 1u);
+                atomicAdd(&h[k][w][digit<P>(v[k][q].y)], 1u);
+                atomicAdd(&h[k][w][digit<P>(v[k][q].z)], 1u);
+                atomicAdd(&h[k][w][digit<P>(v[k][q].w)], 1u);
+            }
+        } else {
+            const u32 i0 = lo[k] + tid * LSD_PT;
+            for (u32 i = i0; i < min(i0 + LSD_PT, hi[k]); ++i) atomicAdd(&h[k][w][digit<P>(K[i])], 1u);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < TPW; ++k)
+        if (t0 + k < nt) hist[(u64)(t0 + k) * 256 + tid] = h[k][0][tid] + h[k][1][tid] + h[k][2][tid] + h[k][3][tid];
 }
 
 // hist[t][d] -> absolute destination of the first element of digit d in tile t.
@@ -166,6 +218,87 @@ __global__ __launch_bounds__(WG) void k_lsd_scatter(LsdGeom g, const u32* Kin, c
         }
         running[tid] += add;
         __syncthreads();
+    }
+}
+
+// The same stable scatter with three barriers per tile instead of three per 256 elements:
+// wave w owns the contiguous quarter [lo + 1024 w, lo + 1024 (w + 1)) of the tile (64
+// elements per step, 16 steps, all held in registers).  Pass 1: every element's offset
+// among its wave's equal digits (ballot match; the digit's leader advances the wave's LDS
+// counter — a wave's LDS operations retire in order, so no barrier between steps).  Then
+// per digit the waves' counts become bases (tile base + counts of the lower waves), and
+// pass 2 writes every element to base + offset.  Same order as k_lsd_scatter: (wave, step,
+// lane) is tile order.
+template <int P, int SRC, int G>
+__global__ __launch_bounds__(WG) void k_lsd_scatter_w(LsdGeom g, const u32* Kin, const u32* Pin, u32* Kout,
+                                                     u32* Pout, const u32* Kg, const u32* hist) {
+    // few registers on purpose (keys and positions, offsets in LDS): the pass runs beside
+    // the LZ77 parse, which holds 4 waves per SIMD, and a 108-VGPR version of this kernel
+    // was starved for the parse's whole duration (one pass 1.7 -> 11 ms)
+    __shared__ u32 wc[WG / 64][256];
+    __shared__ u16 loc[LSD_T];
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    u32 lo, hi, b;
+    const u32 t = xcd_tile();
+    if (!g.range(t, lo, hi, b)) return;
+#pragma unroll
+    for (int i = 0; i < WG / 64; ++i) wc[i][tid] = 0;
+    const u32 tb = hist[(u64)t * 256 + tid];
+    u32 key[LSD_PT], pos[LSD_PT];
+    const u32 q0 = lo + w * (LSD_T / 4);
+#pragma unroll
+    for (u32 j = 0; j < LSD_PT; ++j) {
+        const u32 i = q0 + j * 64 + lane;
+        key[j] = 0;
+        pos[j] = 0;
+        if (i < hi) {
+            key[j] = Kin[i];
+            pos[j] = SRC == SRC_KP ? i : Pin[i];
+        }
+    }
+    // G: the next key gathered by position up front (its latency under the ranking; at
+    // write time it measured 2.5 -> 3.4 ms per step)
+    u32 kg[G ? LSD_PT : 1];
+    if (G) {
+#pragma unroll
+        for (u32 j = 0; j < LSD_PT; ++j) kg[j] = q0 + j * 64 + lane < hi ? Kg[pos[j]] : 0u;
+    }
+    __syncthreads();
+    const u64 lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    u16* lw = loc + w * (LSD_T / 4) + lane;
+#pragma unroll
+    for (u32 j = 0; j < LSD_PT; ++j) {
+        const bool valid = q0 + j * 64 + lane < hi;
+        const u32 dg = digit<P>(key[j]);
+        u64 m = __ballot(valid);
+#pragma unroll
+        for (u32 bit = 0; bit < 8; ++bit) {
+            const u64 bal = __ballot((dg >> bit) & 1u);
+            m &= ((dg >> bit) & 1u) ? bal : ~bal;
+        }
+        const u32 rank = __popcll(m & lt_mask);
+        const u32 pre = valid ? wc[w][dg] : 0u;
+        lw[j * 64] = (u16)(pre + rank);
+        if (valid && rank == 0) wc[w][dg] = pre + (u32)__popcll(m);
+    }
+    __syncthreads();
+    {
+        u32 acc = tb;
+#pragma unroll
+        for (int q = 0; q < WG / 64; ++q) {
+            const u32 c = wc[q][tid];
+            wc[q][tid] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (u32 j = 0; j < LSD_PT; ++j) {
+        if (q0 + j * 64 + lane < hi) {
+            const u32 dst = wc[w][digit<P>(key[j])] + lw[j * 64];
+            Kout[dst] = G ? kg[G ? j : 0] : key[j];
+            Pout[dst] = pos[j];
+        }
     }
 }
 
@@ -303,20 +436,25 @@ __global__ __launch_bounds__(WG) void k_r0_tiles_rscan(const u32* in, u32* out, 
     }
 }
 
+// RK is scattered for the positions p with p - base in [plo, phi) only (several launches
+// over disjoint position windows keep one XCD's concurrent scatters inside a part of the
+// block's RK that its L2 holds, so partial lines combine before write-back); `segs`: this
+// launch also writes the next-round segments and split flags; `xcd`: XCD-contiguous tiles.
 __global__ __launch_bounds__(WG) void k_r0_final(LsdGeom g, const u32* HF, const u32* SA, const u32* cmax,
                                                  const u32* cmin, u32* RK, Seg* next, u32* next_cnt,
-                                                 u32* blk_split) {
+                                                 u32* blk_split, u32 plo, u32 phi, u32 segs, u32 xcd) {
     __shared__ u32 sh[WG / 64], sh2[WG / 64], sh3[WG / 64];
     __shared__ u32 wbase, anysplit;
     u32 lo, hi, b;
-    if (!g.range(blockIdx.x, lo, hi, b)) return;
+    const u32 t = xcd ? xcd_tile() : blockIdx.x;
+    if (!g.range(t, lo, hi, b)) return;
     const u32 base = g.geo.base(b), bend = g.geo.end(b);
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid == 0) anysplit = 0;
     const u32 i0 = lo + tid * LSD_PT;
     u32 sv[LSD_PT];
     load16(SA, i0, hi, sv);
-    const u32 hm = HF[(u64)blockIdx.x * WG + tid];
+    const u32 hm = HF[(u64)t * WG + tid];
     bool hd[LSD_PT];
     u32 lmax = 0, lmin = BIG;
 #pragma unroll
@@ -335,9 +473,9 @@ __global__ __launch_bounds__(WG) void k_r0_final(LsdGeom g, const u32* HF, const
     if (lane == 63) sh[w] = fi;
     if (lane == 0) sh2[w] = ri;
     __syncthreads();
-    u32 run = max(cmax[blockIdx.x], fex);
+    u32 run = max(cmax[t], fex);
     for (u32 q = 0; q < w; ++q) run = max(run, sh[q]);
-    u32 nh = min(cmin[blockIdx.x], rex);
+    u32 nh = min(cmin[t], rex);
     for (u32 q = w + 1; q < WG / 64; ++q) nh = min(nh, sh2[q]);
     if (nh == BIG) nh = bend;
     // ranks
@@ -350,9 +488,10 @@ __global__ __launch_bounds__(WG) void k_r0_final(LsdGeom g, const u32* HF, const
                 run = i;
                 split |= i != base;
             }
-            RK[sv[e]] = run;
+            if (sv[e] - base - plo < phi - plo) RK[sv[e]] = run;
         }
     }
+    if (!segs) return;
     // group lengths (backwards) and next-round segments, one global atomic per workgroup
     u32 len[LSD_PT];
     u32 nseg = 0;
@@ -517,7 +656,14 @@ void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kou
     const u64 N = g.geo.N, H = (u64)nt * 1024;  // H: per-tile histogram bytes
     {
         KScope k(kt, KT_LSD, hn.c_str(), 4 * N + H);
-        k_lsd_hist<P, SRC><<<nt, WG, 0, s>>>(g, kin, hist);
+        // A/B switch KOLM_LSD_HT: tiles per histogram workgroup (1, 2 or 4)
+        static const int ht = getenv("KOLM_LSD_HT") ? atoi(getenv("KOLM_LSD_HT")) : 1;
+        if (ht == 4)
+            k_lsd_hist_m<P, 4><<<(nt + 3) / 4, WG, 0, s>>>(g, kin, hist, nt);
+        else if (ht == 2)
+            k_lsd_hist_m<P, 2><<<(nt + 1) / 2, WG, 0, s>>>(g, kin, hist, nt);
+        else
+            k_lsd_hist<P, SRC><<<nt, WG, 0, s>>>(g, kin, hist);
     }
     {
         KScope k(kt, KT_LSD, "k_lsd_scan", 3 * H);
@@ -526,7 +672,14 @@ void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kou
     {
         // key + position in (the first pass reads the key by position only) and out; G: + the gather
         KScope k(kt, KT_LSD, sn.c_str(), (SRC == SRC_KP ? 12 : 16) * N + (G ? 4 * N : 0) + H);
-        k_lsd_scatter<P, SRC, G><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
+        // k_lsd_scatter_w (three barriers per tile; 256 MiB text, overlapped: 1.5-1.7 -> 0.9-1.0
+        // ms per pass).  A/B switch KOLM_LSD_SW: 0 = k_lsd_scatter everywhere, 1 = except the
+        // first pass (keys by position), 2 = everywhere (default)
+        static const int sw = getenv("KOLM_LSD_SW") ? atoi(getenv("KOLM_LSD_SW")) : 2;
+        if (sw == 2 || (sw == 1 && SRC == SRC_PAIR))
+            k_lsd_scatter_w<P, SRC, G><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
+        else
+            k_lsd_scatter<P, SRC, G><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
     }
 }
 
@@ -619,7 +772,14 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
     {
         // SA 4 read, RK 4 scattered (+ head masks, 8 B per new segment)
         KScope k(kt, KT_LSD, "k_r0_final", 8 * N);
-        k_r0_final<<<nt, WG, 0, s>>>(g, t.HF, t.SA, t.cmax, t.cmin, t.RK, next, next_cnt, blk_split);
+        // A/B switches: KOLM_R0F_PARTS position windows per block, KOLM_R0F_XCD tile mapping
+        // (default: two windows on XCD-contiguous tiles, 256 MiB text 3.24 -> 2.42 ms per step)
+        static const u32 parts = getenv("KOLM_R0F_PARTS") ? std::max(1, atoi(getenv("KOLM_R0F_PARTS"))) : 2u;
+        static const u32 xcd = getenv("KOLM_R0F_XCD") ? (u32)atoi(getenv("KOLM_R0F_XCD")) : 1u;
+        const u32 step = (geo.bs + parts - 1) / parts;
+        for (u32 q = 0; q < parts; ++q)
+            k_r0_final<<<nt, WG, 0, s>>>(g, t.HF, t.SA, t.cmax, t.cmin, t.RK, next, next_cnt, blk_split, q * step,
+                                         q + 1 == parts ? 0xFFFFFFFFu : (q + 1) * step, q == 0, xcd);
     }
 }
 

@@ -305,6 +305,11 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
                 std::chrono::duration<double, std::milli>(now - t_round).count());
         t_round = now;
     };
+    // classes 1..tiny_c: one thread per segment (k_tiny_sort); larger: LDS sorts.  Class 5
+    // (17-32 elements) goes to the LDS sort: k_tiny_sort<5> holds 32 64-bit words in 144
+    // VGPRs and was starved beside the LZ77 parse (1.0 ms alone, 3.0 overlapped; step 45.7
+    // -> 44.0 ms).  A/B switch KOLM_TINY_C (1..TINY_C)
+    static const int tiny_c = getenv("KOLM_TINY_C") ? std::max(1, std::min(TINY_C, atoi(getenv("KOLM_TINY_C")))) : 4;
     for (u32 round = 0; round < 64 && ncur; ++round) {
         a.initial = round == 0 ? 1 : 0;
         a.h = round == 0 ? 0u : (h0 << (round - 1));
@@ -375,7 +380,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
             const u64 per = a.KP ? 12 : a.initial ? (cyclic ? 20 : 11) : (cyclic ? 20 : 12);
             for (int k = 1; k < NCLASS; ++k) {
                 if (!h[C_CLS + k]) continue;
-                if (a.KP && k <= TINY_C) continue;  // k_tiny_sort gathers KP itself
+                if (a.KP && k <= tiny_c) continue;  // k_tiny_sort gathers KP itself
                 TScope t(c, KOLM_KT_KEYGEN, "k_keygen_small", (u64)h[C_CLSE + k] * per);
                 launch_keygen_small(k, L.cls[k], h[C_CLS + k], a, s);
             }
@@ -427,7 +432,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
         // per element: K2 + SA read, SA + RK write (16 B); per segment record 8 B
         for (int k = 0; k < NCLASS; ++k) {
             if (!h[C_CLS + k]) continue;
-            if (k >= 1 && k <= TINY_C) {
+            if (k >= 1 && k <= tiny_c) {
                 static const char* const tn[6] = {"",          "k_tiny_sort<1>", "k_tiny_sort<2>",
                                                   "k_tiny_sort<3>", "k_tiny_sort<4>", "k_tiny_sort<5>"};
                 // SA + key (KP gather or K2) read, SA + RK write per element; 8 B per segment
