@@ -42,6 +42,25 @@ __device__ inline u32 digit(u32 key) {
     return (key >> (8 * P)) & 255u;
 }
 
+// the thread's 16 consecutive words X[i0 .. i0+15] (0 past hi): four 16-byte loads when
+// aligned and whole (the 16 scalar loads per array were 48 read instructions per wave)
+__device__ inline void load16(const u32* X, u32 i0, u32 hi, u32 (&v)[LSD_PT]) {
+    if ((i0 & 3) == 0 && i0 + LSD_PT <= hi) {
+        const uint4* p = reinterpret_cast<const uint4*>(X + i0);
+#pragma unroll
+        for (int q = 0; q < (int)LSD_PT / 4; ++q) {
+            const uint4 t = p[q];
+            v[4 * q] = t.x;
+            v[4 * q + 1] = t.y;
+            v[4 * q + 2] = t.z;
+            v[4 * q + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (u32 e = 0; e < LSD_PT; ++e) v[e] = i0 + e < hi ? X[i0 + e] : 0u;
+    }
+}
+
 // where a pass reads its (key, position) pairs: keys by position (first pass) or pairs
 enum Src { SRC_KP = 1, SRC_PAIR = 2 };
 
@@ -74,57 +93,6 @@ __global__ __launch_bounds__(WG) void k_lsd_hist(LsdGeom g, const u32* K, u32* h
     }
     __syncthreads();
     hist[(u64)xcd_tile() * 256 + tid] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
-}
-
-// The same histograms, TPW tiles per workgroup: every tile's keys are loaded up front (TPW x
-// 64 B per thread in flight instead of 64 B), then counted into per-tile LDS histograms.
-template <int P, int TPW>
-__global__ __launch_bounds__(WG) void k_lsd_hist_m(LsdGeom g, const u32* K, u32* hist, u32 nt) {
-    __shared__ u32 h[TPW][WG / 64][256];
-    const u32 tid = threadIdx.x, w = tid >> 6;
-#pragma unroll
-    for (int k = 0; k < TPW; ++k)
-#pragma unroll
-        for (int i = 0; i < WG / 64; ++i) h[k][i][tid] = 0;
-    const u32 t0 = xcd_tile() * TPW;
-    uint4 v[TPW][LSD_PT / 4];
-    bool whole[TPW];
-    u32 lo[TPW], hi[TPW];
-#pragma unroll
-    for (int k = 0; k < TPW; ++k) {
-        u32 b;
-        whole[k] = false;
-        lo[k] = hi[k] = 0;
-        if (t0 + k < nt && g.range(t0 + k, lo[k], hi[k], b)) {
-            const u32 i0 = lo[k] + tid * LSD_PT;
-            whole[k] = (i0 & 3) == 0 && i0 + LSD_PT <= hi[k];
-            if (whole[k]) {
-                const uint4* p = reinterpret_cast<const uint4*>(K + i0);
-#pragma unroll
-                for (u32 q = 0; q < LSD_PT / 4; ++q) v[k][q] = p[q];
-            }
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < TPW; ++k) {
-        if (whole[k]) {
-#pragma unroll
-            for (u32 q = 0; q < LSD_PT / 4; ++q) {
-                atomicAdd(&h[k][w][digit<P>(v[k][q].x)], 1u);
-                atomicAdd(&h[k][w][digit<P>(v[k][q].y)], 1u);
-                atomicAdd(&h[k][w][digit<P>(v[k][q].z)], 1u);
-                atomicAdd(&h[k][w][digit<P>(v[k][q].w)], 1u);
-            }
-        } else {
-            const u32 i0 = lo[k] + tid * LSD_PT;
-            for (u32 i = i0; i < min(i0 + LSD_PT, hi[k]); ++i) atomicAdd(&h[k][w][digit<P>(K[i])], 1u);
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < TPW; ++k)
-        if (t0 + k < nt) hist[(u64)(t0 + k) * 256 + tid] = h[k][0][tid] + h[k][1][tid] + h[k][2][tid] + h[k][3][tid];
 }
 
 // hist[t][d] -> absolute destination of the first element of digit d in tile t.
@@ -327,24 +295,6 @@ __global__ __launch_bounds__(WG) void k_tiles_max_scan(const u32* in, u32* out, 
     }
 }
 
-// the thread's 16 consecutive words X[i0 .. i0+15] (0 past hi): four 16-byte loads when
-// aligned and whole (the 16 scalar loads per array were 48 read instructions per wave)
-__device__ inline void load16(const u32* X, u32 i0, u32 hi, u32 (&v)[LSD_PT]) {
-    if ((i0 & 3) == 0 && i0 + LSD_PT <= hi) {
-        const uint4* p = reinterpret_cast<const uint4*>(X + i0);
-#pragma unroll
-        for (int q = 0; q < (int)LSD_PT / 4; ++q) {
-            const uint4 t = p[q];
-            v[4 * q] = t.x;
-            v[4 * q + 1] = t.y;
-            v[4 * q + 2] = t.z;
-            v[4 * q + 3] = t.w;
-        }
-    } else {
-#pragma unroll
-        for (u32 e = 0; e < LSD_PT; ++e) v[e] = i0 + e < hi ? X[i0 + e] : 0u;
-    }
-}
 
 // ---------------------------------------------------------------------------------
 // Round 0 of the cyclic suffix sort: after 4 LSD passes over the 4-character rotation
@@ -656,14 +606,7 @@ void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kou
     const u64 N = g.geo.N, H = (u64)nt * 1024;  // H: per-tile histogram bytes
     {
         KScope k(kt, KT_LSD, hn.c_str(), 4 * N + H);
-        // A/B switch KOLM_LSD_HT: tiles per histogram workgroup (1, 2 or 4)
-        static const int ht = getenv("KOLM_LSD_HT") ? atoi(getenv("KOLM_LSD_HT")) : 1;
-        if (ht == 4)
-            k_lsd_hist_m<P, 4><<<(nt + 3) / 4, WG, 0, s>>>(g, kin, hist, nt);
-        else if (ht == 2)
-            k_lsd_hist_m<P, 2><<<(nt + 1) / 2, WG, 0, s>>>(g, kin, hist, nt);
-        else
-            k_lsd_hist<P, SRC><<<nt, WG, 0, s>>>(g, kin, hist);
+        k_lsd_hist<P, SRC><<<nt, WG, 0, s>>>(g, kin, hist);
     }
     {
         KScope k(kt, KT_LSD, "k_lsd_scan", 3 * H);

@@ -318,6 +318,31 @@ __global__ __launch_bounds__(WG) void k_keygen_small(const Seg* segs, u32 count,
     const u32 spt = TILE >> c;
     const u32 first = blockIdx.x * spt;
     const u32 mask = (1u << c) - 1;
+    if (a.KP) {
+        // dense rounds: K2[g] = KP[SA[g]].  All loads staged before the first store (the
+        // stores may alias the loads for the compiler, which otherwise serialises every
+        // element's segment -> SA -> KP chain)
+        u32 g[PER_THREAD], v[PER_THREAD];
+#pragma unroll
+        for (int j = 0; j < PER_THREAD; ++j) {
+            const u32 slot = j * WG + threadIdx.x;
+            const u32 si = first + (slot >> c);
+            g[j] = ~0u;
+            if (si < count) {
+                const Seg s = segs[si];
+                const u32 k = slot & mask;
+                if (k < (s.len & SEG_LEN)) g[j] = s.start + k;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < PER_THREAD; ++j) v[j] = g[j] != ~0u ? a.SA[g[j]] : 0u;
+#pragma unroll
+        for (int j = 0; j < PER_THREAD; ++j) v[j] = g[j] != ~0u ? a.KP[v[j]] : 0u;
+#pragma unroll
+        for (int j = 0; j < PER_THREAD; ++j)
+            if (g[j] != ~0u) a.K2[g[j]] = v[j];
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < PER_THREAD; ++j) {
         const u32 slot = j * WG + threadIdx.x;
