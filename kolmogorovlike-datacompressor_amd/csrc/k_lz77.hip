@@ -677,11 +677,8 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
         // 16 B per token (added by the caller once the token count is known)
         static const u32 lead =
             getenv("KOLM_LZ_LEAD") ? std::min<u32>(atoi(getenv("KOLM_LZ_LEAD")), LZL_LEAD) : LZL_LEAD;
-        // A/B switch KOLM_LZ_LDSPAD: extra (unused) LDS bytes per workgroup, to cap the parse
-        // at fewer workgroups per CU beside the sort stream (7000: 3 instead of 4)
-        static const u32 ldspad = getenv("KOLM_LZ_LDSPAD") ? (u32)atoi(getenv("KOLM_LZ_LDSPAD")) : 0u;
         KScope k(kt, KT_LZPARSE, "k_lz_local", z.geo.N * 2);
-        k_lz_local<<<z.geo.nb * hpb, 256, ldspad, s>>>(z, hpb, lead);
+        k_lz_local<<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb, lead);
     }
     {
         KScope k(kt, KT_LZPARSE, "k_lz_stitch", (u64)z.cpb * z.geo.nb * 16);
