@@ -233,7 +233,11 @@ __device__ inline int seg_class(const SortArgs& a, const Seg* cur, u32 ncur, u32
     return s.len > (u32)TILE ? NCLASS : size_class(s.len);
 }
 
-__global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur, SortArgs a, Lists L, Level lv) {
+// MODE 0: all segments placed by per-workgroup reservations (list order arbitrary).
+// MODE 1: counts as MODE 0 plus per-(class, bin) counts; only the large segments are written.
+// MODE 2: small segments placed at their bin's offset (after k_bin_scan).
+template <int MODE>
+__global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur, SortArgs a, Lists L, Level lv, Bins bn) {
     __shared__ u32 lcnt[NCLASS + 1], lbase[NCLASS + 1], lel[NCLASS + 1], lcur[NCLASS + 1];
     __shared__ u32 lact, ltiles, ltb;
     const u32 tid = threadIdx.x, lane = tid & 63;
@@ -249,10 +253,42 @@ __global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur, Sort
     __syncthreads();
     const u32 stride = gridDim.x * 256;
     const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    if (MODE == 2) {
+        for (u32 i0 = blockIdx.x * 256; i0 < ncur; i0 += stride) {
+            Seg s;
+            const int c = seg_class(a, cur, ncur, i0 + tid, s);
+            const u32 key = (c >= 0 && c < NCLASS) ? (u32)c * CLS_NBIN + (s.start >> bn.bsh) : ~0u;
+            u64 pend = __ballot(key != ~0u);
+            u32 dst = 0;
+            while (pend) {
+                const u32 f = (u32)__ffsll((long long)pend) - 1;
+                const u32 kk = __builtin_amdgcn_readlane(key, f);
+                const u64 m = __ballot(key == kk);
+                u32 base = 0;
+                if (lane == f) base = bn.cnt[kk] + atomicAdd(&bn.fill[kk], (u32)__popcll(m));
+                base = __builtin_amdgcn_readlane(base, f);
+                if (key == kk) dst = base + (u32)__popcll(m & lt);
+                pend &= ~m;
+            }
+            if (key != ~0u) L.cls[c][dst] = Seg{s.start, s.len | SEG_FIRST};
+        }
+        return;
+    }
     // pass 1: counts
     for (u32 i0 = blockIdx.x * 256; i0 < ncur; i0 += stride) {
         Seg s;
         const int c = seg_class(a, cur, ncur, i0 + tid, s);
+        if (MODE == 1) {
+            const u32 key = (c >= 0 && c < NCLASS) ? (u32)c * CLS_NBIN + (s.start >> bn.bsh) : ~0u;
+            u64 bp = __ballot(key != ~0u);
+            while (bp) {
+                const u32 f = (u32)__ffsll((long long)bp) - 1;
+                const u32 kk = __builtin_amdgcn_readlane(key, f);
+                const u64 m = __ballot(key == kk);
+                if (lane == f) atomicAdd(&bn.cnt[kk], (u32)__popcll(m));
+                bp &= ~m;
+            }
+        }
         u64 pend = __ballot(c >= 0);
         u32 nt = c == NCLASS ? (s.len + TILE - 1) / TILE : 0u;
         nt = wave_reduce(nt, OpAddU(), 0u);
@@ -283,11 +319,12 @@ __global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur, Sort
     }
     if (tid == NCLASS + 1 && lact) atomicAdd(&L.misc[0], lact);
     __syncthreads();
+    if (MODE == 1 && lcnt[NCLASS] == 0) return;  // small segments are placed by MODE 2
     // pass 2: writes
     for (u32 i0 = blockIdx.x * 256; i0 < ncur; i0 += stride) {
         Seg s;
         const int c = seg_class(a, cur, ncur, i0 + tid, s);
-        u64 pend = __ballot(c >= 0);
+        u64 pend = __ballot(MODE == 1 ? c == NCLASS : c >= 0);
         u32 li = 0;
         while (pend) {
             const u32 f = (u32)__ffsll((long long)pend) - 1;
@@ -305,9 +342,33 @@ __global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur, Sort
             const u32 tb = ltb + atomicAdd(&ltiles, nt);
             lv.segs[si] = LSeg{s.start, s.len | SEG_FIRST, tb, nt};
             for (u32 k = 0; k < nt; ++k) lv.tiles[tb + k] = LTile{si, k};
-        } else if (c >= 0) {
+        } else if (MODE == 0 && c >= 0) {
             L.cls[c][lbase[c] + li] = Seg{s.start, s.len | SEG_FIRST};
         }
+    }
+}
+
+// per class: exclusive scan of the bin counts -> class-local bin offsets (one workgroup per class)
+__global__ __launch_bounds__(256) void k_bin_scan(Bins bn) {
+    constexpr u32 R = CLS_NBIN / 256;
+    __shared__ u32 sh[4];
+    u32* c = bn.cnt + blockIdx.x * CLS_NBIN;
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    u32 v[R], tot = 0;
+#pragma unroll
+    for (u32 r = 0; r < R; ++r) {
+        v[r] = c[tid * R + r];
+        tot += v[r];
+    }
+    const u32 incl = wave_incl_scan(tot, OpAddU(), 0u);
+    if (lane == 63) sh[w] = incl;
+    __syncthreads();
+    u32 ex = incl - tot;
+    for (u32 i = 0; i < w; ++i) ex += sh[i];
+#pragma unroll
+    for (u32 r = 0; r < R; ++r) {
+        c[tid * R + r] = ex;
+        ex += v[r];
     }
 }
 
@@ -316,7 +377,7 @@ __global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur, Sort
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(WG) void k_keygen_small(const Seg* segs, u32 count, int c, SortArgs a) {
     const u32 spt = TILE >> c;
-    const u32 first = blockIdx.x * spt;
+    const u32 first = (a.xcd ? xcd_tile() : blockIdx.x) * spt;
     const u32 mask = (1u << c) - 1;
     if (a.KP) {
         // dense rounds: K2[g] = KP[SA[g]].  All loads staged before the first store (the
@@ -582,7 +643,7 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
     __shared__ u32 last_hi[WG];
     __shared__ u8 ssplit[SPT];  // sub-array split by this round's key
     const u32 tid = threadIdx.x;
-    const u32 first = blockIdx.x * SPT;
+    const u32 first = (a.xcd ? xcd_tile() : blockIdx.x) * SPT;
     const u32 nthis = min(SPT, count - first);
     for (u32 i = tid; i < SPT; i += WG) {
         ss[i] = i < nthis ? segs[first + i] : Seg{0, 0};
@@ -732,7 +793,7 @@ __global__ __launch_bounds__(256) void k_tiny_sort(const Seg* segs, u32 count, S
     constexpr u32 S = 1u << C;
     __shared__ u32 sh[WG / 64], wtot;
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const u32 i = blockIdx.x * WG + tid;
+    const u32 i = (a.xcd ? xcd_tile() : blockIdx.x) * WG + tid;
     Seg sg{0, 0};
     u32 len = 0;
     if (i < count) {
@@ -868,7 +929,17 @@ void launch_block_segs(Seg* segs, const Geom& geo, hipStream_t s) {
 }
 void launch_classify(const Seg* cur, u32 ncur, const SortArgs& a, const Lists& L, const Level& lv0,
                      hipStream_t s) {
-    if (ncur) k_classify<<<std::min<u32>(cdiv(ncur, 256), 2048u), 256, 0, s>>>(cur, ncur, a, L, lv0);
+    if (ncur) k_classify<0><<<std::min<u32>(cdiv(ncur, 256), 2048u), 256, 0, s>>>(cur, ncur, a, L, lv0, Bins{});
+}
+void launch_classify_bins(const Seg* cur, u32 ncur, const SortArgs& a, const Lists& L, const Level& lv0,
+                          const Bins& bn, hipStream_t s) {
+    if (!ncur) return;
+    const u32 grid = std::min<u32>(cdiv(ncur, 256), 2048u);
+    KOLM_HIP_CHECK(hipMemsetAsync(bn.cnt, 0, sizeof(u32) * NCLASS * CLS_NBIN, s));
+    KOLM_HIP_CHECK(hipMemsetAsync(bn.fill, 0, sizeof(u32) * NCLASS * CLS_NBIN, s));
+    k_classify<1><<<grid, 256, 0, s>>>(cur, ncur, a, L, lv0, bn);
+    k_bin_scan<<<NCLASS, 256, 0, s>>>(bn);
+    k_classify<2><<<grid, 256, 0, s>>>(cur, ncur, a, L, lv0, bn);
 }
 void launch_keypos(const SortArgs& a, u32* KP, hipStream_t s) {
     if (!a.geo.N) return;

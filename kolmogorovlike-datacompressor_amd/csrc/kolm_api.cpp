@@ -351,8 +351,19 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
             continue;
         }
         {
-            TScope t(c, KOLM_KT_CLASSIFY, "k_classify", (u64)ncur * 16);
-            launch_classify(cur, ncur, a, L, lv[0], s);
+            // position-ordered class lists (default; A/B switch KOLM_CLS_BIN=0: arbitrary order)
+            static const bool bin = !(getenv("KOLM_CLS_BIN") && atoi(getenv("KOLM_CLS_BIN")) == 0);
+            TScope t(c, KOLM_KT_CLASSIFY, "k_classify", (u64)ncur * (bin ? 24 : 16));
+            if (bin) {
+                const u32 nbits = bitlen((u32)(N - 1));
+                const Bins bn{c->get<u32>("cls_bins", NCLASS * CLS_NBIN), c->get<u32>("cls_fill", NCLASS * CLS_NBIN),
+                              nbits > 10 ? nbits - 10 : 0u};
+                launch_classify_bins(cur, ncur, a, L, lv[0], bn, s);
+                a.xcd = 1;
+            } else {
+                launch_classify(cur, ncur, a, L, lv[0], s);
+                a.xcd = 0;
+            }
         }
         KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
         c->sync();

@@ -207,6 +207,19 @@ struct SortArgs {
     const u32* KP;     // [N] this round's key by position (k_keypos), or null: keys gathered directly
     u32 key_bits;      // keys of this round are < 2^key_bits (small sort packs key|index in 32 bits)
     u32* KA;           // cyclic round 0 with 8 characters: k_keypos also writes characters 4..7 here
+    u32 xcd;           // class lists are position-ordered: per-class kernels map workgroups to
+                       // XCD-contiguous list ranges (k_classify_bins)
+};
+
+// Position-ordered class lists: k_classify bins every small segment by start >> bsh (at most
+// CLS_NBIN bins per class), so a class list is in (coarse) position order and the per-class
+// kernels' KP gathers / RK scatters of concurrent workgroups on one XCD stay inside a few
+// blocks (L2 locality).
+constexpr u32 CLS_NBIN = 1024;
+struct Bins {
+    u32* cnt;   // [NCLASS][CLS_NBIN] counts, then class-local offsets
+    u32* fill;  // [NCLASS][CLS_NBIN] placement counters
+    u32 bsh;
 };
 
 // Append-only lists written by the classify / MSD / small-sort kernels.
@@ -232,6 +245,8 @@ struct Level {
 // ---- launchers (k_sort.hip) ----
 void launch_iota(u32* SA, u64 N, hipStream_t s);
 void launch_block_segs(Seg* segs, const Geom& geo, hipStream_t s);
+void launch_classify_bins(const Seg* cur, u32 ncur, const SortArgs& a, const Lists& L, const Level& lv0,
+                          const Bins& bn, hipStream_t s);
 void launch_classify(const Seg* cur, u32 ncur, const SortArgs& a, const Lists& L, const Level& lv0,
                      hipStream_t s);
 void launch_keypos(const SortArgs& a, u32* KP, hipStream_t s);
