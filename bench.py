@@ -40,14 +40,14 @@ from kolm.parallel import gather_payloads  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # kernels whose limiter is not HBM bandwidth (measured)
 LIMITER = {
-    "k_lz_spec<true>": "latency: the dependent greedy-parse chain (one wave per 4 KiB chunk; each token's "
-                       "candidate search starts where the previous token ended)",
-    "k_lz_spec<false>": "latency: the dependent greedy-parse chain",
-    "k_lz_spec2": "latency: the dependent greedy-parse chains (two 2 KiB chunks per wave, one per half)",
     "k_lz_local": "LDS latency / issue: in-LDS 3-gram index + 16 dependent greedy-parse chains per workgroup "
                   "(4 waves/SIMD, LDS-limited); HBM traffic is only the text window and the token records; "
                   "it runs beside the sort stream at lower priority, so its overlapped duration is inflated",
     "k_repair": "latency: one workgroup per block, barrier-separated batches of dependent global accesses",
+    "k_duval_span": "LDS latency: sequential Duval over each thread's 128-byte chunk, then tree merges of "
+                    "adjacent factorisations (dependent LDS byte compares / bitmap scans); reads the text once",
+    "k_lsd_scatter_w<3, 2, 1>": "random 4-byte gathers of the next key by position (one 32-64 B request each) "
+                                "beside the streaming LSD scatter",
 }
 MB = 1e6
 
@@ -276,7 +276,7 @@ def main():
                 "achieved_traffic_GBs": round(ctraffic / (cavg * 1e-3) / 1e9, 2) if ctraffic else None,
                 "frac_traffic": round(ctraffic / (cavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if ctraffic else None,
                 "achieved_traffic_uncorrected_GBs": round(craw / (cavg * 1e-3) / 1e9, 2) if craw else None,
-                "limiter": "random 4-byte gathers / scatters (one 32-64 B HBM request each)"}
+                "limiter": LIMITER.get(cname, "random 4-byte gathers / scatters (one 32-64 B HBM request each)")}
     # whole pipeline: every kernel's algorithmic bytes per step / wall time per step (the two
     # streams overlap, so this is the chip-level rate the path sustains)
     alg_step = sum(v["bytes"] for v in ktimes.values()) / a.steps
