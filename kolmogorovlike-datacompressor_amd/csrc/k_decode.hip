@@ -455,19 +455,39 @@ __global__ __launch_bounds__(256) void k_rice_bitplane(BwArgs a) {
 // MTF decode.  One "move the entry at position idx to the front" step on a 256-entry table
 // held as 64 words per thread (tab[w * RT + t]); returns the entry.
 constexpr int DRT = 128;
-__device__ inline u32 mtf_pop_front(u32* tab, u32 t, u32 idx) {
+// word x with its byte j moved out: bytes [0, j) shift up one, `in` enters byte 0
+__device__ inline u32 mtf_front(u32 x, u32 j, u32 in) {
+    const u32 lowmask = j ? ((1u << (8 * j)) - 1) : 0u;
+    const u32 highmask = j == 3 ? 0u : ~((1u << (8 * (j + 1))) - 1);
+    return (x & highmask) | ((x & lowmask) << 8) | in;
+}
+// Pop entry idx to the front.  Entries 0..7 (words 0, 1) are held in registers r0, r1 (MTF
+// indices of BBWT output are mostly small: no LDS round trip); words 2..63 are in LDS.
+__device__ inline u32 mtf_pop_front(u32* tab, u32 t, u32 idx, u32& r0, u32& r1) {
+    if (idx < 4) {
+        const u32 b = (r0 >> (8 * idx)) & 0xFFu;
+        r0 = mtf_front(r0, idx, b);
+        return b;
+    }
+    const u32 c0 = r0 >> 24;
+    if (idx < 8) {
+        const u32 j = idx - 4, b = (r1 >> (8 * j)) & 0xFFu;
+        r0 = (r0 << 8) | b;
+        r1 = mtf_front(r1, j, c0);
+        return b;
+    }
     const u32 w = idx >> 2, j = idx & 3;
     const u32 x = tab[w * DRT + t];
     const u32 b = (x >> (8 * j)) & 0xFFu;
-    u32 carry = b;
-    for (u32 v = 0; v < w; ++v) {
+    u32 carry = r1 >> 24;
+    r1 = (r1 << 8) | c0;
+    r0 = (r0 << 8) | b;
+    for (u32 v = 2; v < w; ++v) {
         const u32 xv = tab[v * DRT + t];
         tab[v * DRT + t] = (xv << 8) | carry;
         carry = xv >> 24;
     }
-    const u32 lowmask = j ? ((1u << (8 * j)) - 1) : 0u;
-    const u32 highmask = j == 3 ? 0u : ~((1u << (8 * (j + 1))) - 1);
-    tab[w * DRT + t] = (x & highmask) | ((x & lowmask) << 8) | carry;
+    tab[w * DRT + t] = mtf_front(x, j, carry);
     return b;
 }
 
@@ -487,10 +507,13 @@ __global__ __launch_bounds__(DRT) void k_dec_mtf_summary(BwArgs a, u32 nch) {
     const u32 t = threadIdx.x, c = blockIdx.x * DRT + t;
     u32 b, lo, hi;
     if (c >= nch || !dec_chunk(a, c, b, lo, hi)) return;
-    for (u32 w = 0; w < 64; ++w) tab[w * DRT + t] = (4 * w) | ((4 * w + 1) << 8) | ((4 * w + 2) << 16) | ((4 * w + 3) << 24);
-    for (u32 i = lo; i < hi; ++i) mtf_pop_front(tab, t, a.mi[i]);
+    for (u32 w = 2; w < 64; ++w) tab[w * DRT + t] = (4 * w) | ((4 * w + 1) << 8) | ((4 * w + 2) << 16) | ((4 * w + 3) << 24);
+    u32 r0 = 0x03020100u, r1 = 0x07060504u;
+    for (u32 i = lo; i < hi; ++i) mtf_pop_front(tab, t, a.mi[i], r0, r1);
     u32* out = reinterpret_cast<u32*>(a.summ + (u64)c * 256);
-    for (u32 w = 0; w < 64; ++w) out[w] = tab[w * DRT + t];
+    out[0] = r0;
+    out[1] = r1;
+    for (u32 w = 2; w < 64; ++w) out[w] = tab[w * DRT + t];
 }
 
 // per block: entry state of every chunk; state' = state o summary
@@ -518,8 +541,9 @@ __global__ __launch_bounds__(DRT) void k_dec_mtf_replay(BwArgs a, u32 nch) {
     u32 b, lo, hi;
     if (c >= nch || !dec_chunk(a, c, b, lo, hi)) return;
     const u32* s = reinterpret_cast<const u32*>(a.states + (u64)c * 256);
-    for (u32 w = 0; w < 64; ++w) tab[w * DRT + t] = s[w];
-    for (u32 i = lo; i < hi; ++i) a.bw[i] = (u8)mtf_pop_front(tab, t, a.mi[i]);
+    u32 r0 = s[0], r1 = s[1];
+    for (u32 w = 2; w < 64; ++w) tab[w * DRT + t] = s[w];
+    for (u32 i = lo; i < hi; ++i) a.bw[i] = (u8)mtf_pop_front(tab, t, a.mi[i], r0, r1);
 }
 
 // Inverse BBWT (PY:425-454), grid-wide.  PI = stable counting sort of the BBWT string L

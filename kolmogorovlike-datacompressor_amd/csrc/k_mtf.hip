@@ -226,28 +226,51 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
     u32 lo, hi;
     if (!cg.range(c, lo, hi)) return;
     const u32* s = reinterpret_cast<const u32*>(states + (u64)c * 256);
-    for (int w = 0; w < 64; ++w) tab[w * RT + t] = s[w];
+    // entries 0..7 (words 0, 1) live in registers: BBWT output is mostly short MTF indices,
+    // which then cost no LDS round trip; words 2..63 stay in LDS
+    u32 r0 = s[0], r1 = s[1];
+    for (int w = 2; w < 64; ++w) tab[w * RT + t] = s[w];
+    auto haszero = [](u32 y) { return (y - 0x01010101u) & ~y & 0x80808080u; };
+    // word x with its byte j moved to byte 0's side: bytes [0, j) shift up, byte 0 = in
+    auto front = [](u32 x, u32 j, u32 in) {
+        const u32 lowmask = j ? ((1u << (8 * j)) - 1) : 0u;
+        const u32 highmask = j == 3 ? 0u : ~((1u << (8 * (j + 1))) - 1);
+        return (x & highmask) | ((x & lowmask) << 8) | in;
+    };
     auto step = [&](u32 b) -> u32 {
         const u32 bb = b * 0x01010101u;
-        u32 w = 0, x, z;
+        u32 z = haszero(r0 ^ bb);
+        if (z) {
+            const u32 j = (__ffs(z) - 1) >> 3;
+            r0 = front(r0, j, b);
+            return j;
+        }
+        const u32 c0 = r0 >> 24;
+        z = haszero(r1 ^ bb);
+        if (z) {
+            const u32 j = (__ffs(z) - 1) >> 3;
+            r0 = (r0 << 8) | b;
+            r1 = front(r1, j, c0);
+            return 4 + j;
+        }
+        u32 w = 2, x;
         for (;;) {
             x = tab[w * RT + t];
-            const u32 y = x ^ bb;
-            z = (y - 0x01010101u) & ~y & 0x80808080u;
+            z = haszero(x ^ bb);
             if (z) break;
             ++w;
         }
         const u32 j = (__ffs(z) - 1) >> 3;  // byte index inside word w
         // move to front: shift entries [0, 4w+j) up by one, entry 0 = b
-        u32 carry = b;
-        for (u32 v = 0; v < w; ++v) {
+        u32 carry = r1 >> 24;
+        r1 = (r1 << 8) | c0;
+        r0 = (r0 << 8) | b;
+        for (u32 v = 2; v < w; ++v) {
             const u32 xv = tab[v * RT + t];
             tab[v * RT + t] = (xv << 8) | carry;
             carry = xv >> 24;
         }
-        const u32 lowmask = j ? ((1u << (8 * j)) - 1) : 0u;
-        const u32 highmask = j == 3 ? 0u : ~((1u << (8 * (j + 1))) - 1);
-        tab[w * RT + t] = (x & highmask) | ((x & lowmask) << 8) | carry;
+        tab[w * RT + t] = front(x, j, carry);
         return 4 * w + j;
     };
     RiceAcc acc;
