@@ -7,21 +7,29 @@ HBM, 1 MiB fixed blocks, all candidates 0..8 evaluated per block, MDL winner emi
 One step = one full compress of the rank's batch from HBM to a device payload arena
 (+ for N > 1 the RCCL gather of every rank's payloads and method ids to rank 0).
 Weak scaling: per-GPU work is fixed; value = all ranks' input bytes / max-over-ranks time.
+The timed steps run with kernel timing OFF; a separate pass of --kt-steps steps records
+HIP events around every launch (per-kernel durations), and at N=1 one more step runs
+with the streams serialised (each kernel's solo duration).
 
 Also reported:
-  roofline      the dominant single kernel (largest summed device time in the timed
-                steps, HIP events on the library's stream): algorithmic bytes per launch
-                (DESIGN.md §5) / average launch time, against 8 TB/s HBM peak;
-                traffic = PMC-measured HBM bytes per launch from profiles/pmc_summary.json
-                when present (collected by tools/pmc_traffic.py), else null.
+  roofline      the critical path: the SORT STREAM (Lyndon -> omega-order sort -> BBWT
+                gather -> MTF + Rice sizes; the LZ77 parse runs beside it on the index
+                stream and is hidden).  achieved = SURVEY §8d contract bytes of that stream
+                per step / summed device time of its kernels per step (HIP events on that
+                stream); traffic = PMC-measured HBM bytes of the same kernels per step
+                (profiles/pmc_summary.json, tools/pmc_traffic.py).  The dominant single
+                kernel and the LZ77 parse (overlapped and solo) are reported beside it.
   cpu_baseline  the oracle (faithful C++ restatement of the reference CPU path, 5x BBWT
                 as in PY) on a bounded sample of the same stream, rank 0 at N=1 only.
+  detail.parity_blocks  every block of the timed output (sizes of ids 0..8, winner, winner
+                sha256) against tests/golden/bench_stream.json (oracle answers).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 via
 python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 """
 import argparse
 import ctypes
+import hashlib
 import json
 import os
 import sys
@@ -38,17 +46,20 @@ from kolm import _lib, datagen  # noqa: E402
 from kolm.parallel import gather_payloads  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-# kernels whose limiter is not HBM bandwidth (measured)
+GOLDEN = os.path.join(REPO, "tests", "golden")
+# what stops a kernel short of the HBM roof when it is not bandwidth (measured)
 LIMITER = {
     "k_lz_local": "LDS latency / issue: in-LDS 3-gram index + 16 dependent greedy-parse chains per workgroup "
-                  "(4 waves/SIMD, LDS-limited); HBM traffic is only the text window and the token records; "
-                  "it runs beside the sort stream at lower priority, so its overlapped duration is inflated",
+                  "(4 waves/SIMD, LDS-limited); HBM traffic is only the text window and the token records",
     "k_repair": "latency: one workgroup per block, barrier-separated batches of dependent global accesses",
     "k_duval_span": "LDS latency: sequential Duval over each thread's 128-byte chunk, then tree merges of "
                     "adjacent factorisations (dependent LDS byte compares / bitmap scans); reads the text once",
-    "k_lsd_scatter_w<3, 2, 1>": "random 4-byte gathers of the next key by position (one 32-64 B request each) "
-                                "beside the streaming LSD scatter",
+    "k_lsd_scatter<3, 2, 1>": "random 4-byte gathers of the next key by position (one 32-64 B request each) "
+                              "beside the streaming LSD scatter",
 }
+SORT_STREAM_LIMITER = ("random 4-byte gathers / scatters of ranks and keys by position (one 32-64 B HBM "
+                       "request per element in the doubling rounds and the RK scatter), streaming LSD passes at "
+                       "2-3 TB/s, and latency-bound Lyndon / MTF-compose chains (DESIGN.md §4)")
 MB = 1e6
 
 
@@ -125,6 +136,46 @@ def cpu_baseline(data: bytes, bs: int, budget_s: float):
                           f"({rp_s:.2f} s per {bs >> 20} MiB block, 2 blocks), scaled to {T} block-parallel threads"}}
 
 
+def load_golden_stream(rank: int, n: int, bs: int):
+    """Per-block oracle answers for this rank's stream (make_golden_bench.py), or None."""
+    path = os.path.join(GOLDEN, "bench_stream.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        g = json.load(f).get("ranks", {}).get(str(rank))
+    if not g or g["bytes"] != n or g["block_size"] != bs:
+        return None
+    return g
+
+
+def check_blocks(g, sizes, method, arena_host, off, ncand, wkey, shakey):
+    """Blocks whose sizes (ids < ncand), winner and winner sha256 all match the oracle."""
+    ok = 0
+    for i, rec in enumerate(g["blocks"]):
+        if list(map(int, sizes[i][:ncand])) != rec["sizes"][:ncand] or int(method[i]) != rec[wkey]:
+            continue
+        pay = arena_host[int(off[i]):int(off[i + 1])]
+        if hashlib.sha256(pay).hexdigest() == rec.get(shakey, rec["sha9"]):
+            ok += 1
+    return ok
+
+
+def sync_max(el, world):
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt[0])
+    return el
+
+
+def sum_all(v, world):
+    if world > 1:
+        tt = torch.tensor([v], dtype=torch.int64, device="cuda")
+        dist.all_reduce(tt)
+        v = int(tt[0])
+    return v
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -132,6 +183,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--mib", type=int, default=256, help="input MiB per GPU")
     ap.add_argument("--bs", type=int, default=1 << 20, help="block size")
+    ap.add_argument("--kt-steps", type=int, default=2, help="steps of the kernel-timed pass (HIP events per launch)")
+    ap.add_argument("--no-serial-pass", action="store_true", help="skip the serialised-streams step (N=1)")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of oracle CPU work (N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--full-steps", type=int, default=2,
@@ -143,6 +196,10 @@ def main():
     ap.add_argument("--v2-steps", type=int, default=1,
                     help="timed steps of the candidate list 0..10 (+ v2_new, opt-in) on --v2-mib MiB; 0 = skip")
     ap.add_argument("--v2-mib", type=int, default=32, help="input MiB of the v2_new leg")
+    ap.add_argument("--config-steps", type=int, default=3,
+                    help="timed repetitions of the config-2 / config-5 legs (gradient block, mixed corpus); 0 = skip")
+    ap.add_argument("--host-steps", type=int, default=2,
+                    help="timed kolm.compress_blocks_fixed(bytes) calls on the host buffer (PCIe-inclusive); 0 = skip")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -199,87 +256,115 @@ def main():
                 pending[j] = None
         torch.cuda.synchronize()
 
+    def timed(fn, k):
+        """k calls of fn between barriers + device syncs; max over ranks of the wall time"""
+        drain()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = [fn() for _ in range(k)]
+        drain()
+        if world > 1:
+            dist.barrier()
+        return sync_max(time.perf_counter() - t0, world), res
+
     for _ in range(a.warmup):
         step(_lib.Stats())
-    drain()
-    _lib.check(L.kolm_ctx_set_timing(ctx, 1))
-    kern = {}
-    stats = []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        st = _lib.Stats()
-        arena = step(st)
-        d = st.as_dict()
-        stats.append(d)
-        for k, v in d["kernels"].items():
-            e = kern.setdefault(k, {"ms": 0.0, "launches": 0, "bytes": 0})
-            for f in ("ms", "launches", "bytes"):
-                e[f] += v[f]
-    drain()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    _lib.check(L.kolm_ctx_set_timing(ctx, 0))
-    if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt[0])
+    # ---- the headline: K steps, no per-launch timing events ----
+    el, _ = timed(lambda: step(_lib.Stats()), a.steps)
+    arena = arenas[(nstep[0] - 1) % len(arenas)]
     ms_step = el / a.steps * 1e3
     value = world * n * a.steps / el / MB
 
-    # roofline of the dominant single kernel (largest summed device time over the timed
-    # steps; HIP events recorded on the library's stream around every launch)
+    # ---- parity of the timed output, block by block, against the oracle's answers ----
+    golden = load_golden_stream(rank, n, a.bs)
+    arena_host = arena[:int(off[-1])].cpu().numpy().tobytes() if golden else None
+    parity_ok = check_blocks(golden, sizes, method, arena_host, off, 9, "w9", "sha9") if golden else 0
+    parity_checked = nb if golden else 0
+    parity = {"ok": sum_all(parity_ok, world), "checked": sum_all(parity_checked, world), "blocks": world * nb}
+    log(rank, f"[bench] parity {parity}")
+
+    # ---- kernel-timed pass (HIP events around every launch) ----
+    _lib.check(L.kolm_ctx_set_timing(ctx, 1))
+    kt_stats = []
+
+    def kt_step():
+        kt_stats.append(_lib.Stats())
+        return step(kt_stats[-1])
+
+    elk, _ = timed(kt_step, max(1, a.kt_steps))
+    _lib.check(L.kolm_ctx_set_timing(ctx, 0))
     ktimes = _lib.kernel_times(ctx)
-    singles = {k: v for k, v in ktimes.items() if "+" not in k and "(" not in k and k != "emit"}
-    name, k = max(singles.items(), key=lambda kv: kv[1]["ms"])
-    avg_ms = k["ms"] / k["launches"]
-    bytes_per_launch = k["bytes"] / k["launches"]
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    ks = max(1, a.kt_steps)
+    stats = [s.as_dict() for s in kt_stats]
+    s0 = stats[-1]
+
+    # ---- one serialised step (N=1): every kernel's solo duration ----
+    solo = None
+    if world == 1 and not a.no_serial_pass:
+        _lib.check(L.kolm_ctx_set_serial(ctx, 1))
+        _lib.check(L.kolm_ctx_set_timing(ctx, 1))
+        els, _ = timed(lambda: step(_lib.Stats()), 1)
+        _lib.check(L.kolm_ctx_set_timing(ctx, 0))
+        _lib.check(L.kolm_ctx_set_serial(ctx, 0))
+        solo = {"times": _lib.kernel_times(ctx), "ms_step": els * 1e3}
+
+    # ---- roofline of the critical path: the sort stream, SURVEY §8d byte contract ----
+    pmc_path = os.path.join(REPO, "profiles", "pmc_summary.json")
+    pmc = {}
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pmc = json.load(f).get("kernels", {})
+    sort_k = {k: v for k, v in ktimes.items() if v.get("stream") == "sort"}
+    sort_ms = sum(v["ms"] for v in sort_k.values()) / ks
+    rsum = s0["cyc_rounds_sum"]  # sum over blocks of the doubling rounds each block needed
+    lens = np.full(nb, a.bs, np.int64)
+    lens[-1] = n - a.bs * (nb - 1)
+    r_avg = rsum / nb  # equal blocks: sum_b n_b R_b = bs * rsum
+    out_w = int(sizes[:, 2:7].min(axis=1).astype(np.int64).sum())  # the BBWT family's emitted size
+    # per block: n(44 R_lin + 8) Lyndon (R_lin = 0: Duval, no linear SA) + n(44 R + 7)
+    # cyclic SA + BBWT gather + 2n MTF + n Rice size pass + (n + out_w) winner emit
+    contract = int(n * (8 + 7 + 2 + 1 + 1) + 44 * float((lens * r_avg).sum()) + out_w)
+    achieved = contract / (sort_ms * 1e-3) / 1e9
+    builder = sum(v["bytes"] for v in sort_k.values()) / ks
+    tr_have = [k for k in sort_k if pmc.get(k, {}).get("hbm_bytes_per_launch")]
     traffic = None
-    pmc = os.path.join(REPO, "profiles", "pmc_summary.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            tr = json.load(f).get("kernels", {}).get(name)
-        if tr and tr.get("hbm_bytes_per_launch"):
-            traffic = int(tr["hbm_bytes_per_launch"])
-    # "bound"/"peak": the roof the kernel is priced against (integer/byte work: HBM);
-    # "limiter": what actually stops it short of that roof
+    if sort_k and len(tr_have) == len(sort_k):
+        traffic = int(sum(pmc[k]["hbm_bytes_per_launch"] * sort_k[k]["launches"] for k in sort_k) / ks)
+    dom_name, dom = max(sort_k.items(), key=lambda kv: kv[1]["ms"]) if sort_k else ("", {"ms": 0, "launches": 1,
+                                                                                          "bytes": 0})
+    dom_avg = dom["ms"] / max(dom["launches"], 1)
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": name,
-            "limiter": LIMITER.get(name, "hbm"),
-            "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": int(bytes_per_launch),
-            "launches_per_step": k["launches"] // a.steps}
-    # the critical path's own roofline: the sort stream's largest kernel (the LZ77 parse runs
-    # beside it), algorithmic bytes and PMC-measured HBM traffic per launch / launch time
-    sort_fams = ("keygen", "small_sort", "lsd", "msd", "classify", "lyndon_gather", "mtf")
-    crit = None
-    cands = {k: v for k, v in singles.items() if _lib.KT_NAMES[v.get("family", 0)] in sort_fams}
-    if cands:
-        cname, cv = max(cands.items(), key=lambda kv: kv[1]["ms"])
-        cavg = cv["ms"] / cv["launches"]
-        ctraffic = craw = None
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                tr = json.load(f).get("kernels", {}).get(cname)
-            if tr and tr.get("hbm_bytes_per_launch"):
-                ctraffic = tr["hbm_bytes_per_launch"]
-                # FETCH_SIZE x2 is the guide's correction for wide streaming reads; for 4-byte
-                # gathers the uncorrected figure is the plausible one, so both are reported
-                craw = tr.get("fetch_bytes_raw", 0) + tr.get("write_bytes", 0)
-        cach = cv["bytes"] / cv["launches"] / (cavg * 1e-3) / 1e9
-        crit = {"kernel": cname, "avg_launch_ms": round(cavg, 4), "launches_per_step": cv["launches"] // a.steps,
-                "achieved_algorithmic_GBs": round(cach, 2), "frac_algorithmic": round(cach / HBM_PEAK_GBS, 5),
-                "traffic_per_launch": int(ctraffic) if ctraffic else None,
-                "achieved_traffic_GBs": round(ctraffic / (cavg * 1e-3) / 1e9, 2) if ctraffic else None,
-                "frac_traffic": round(ctraffic / (cavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if ctraffic else None,
-                "achieved_traffic_uncorrected_GBs": round(craw / (cavg * 1e-3) / 1e9, 2) if craw else None,
-                "limiter": LIMITER.get(cname, "random 4-byte gathers / scatters (one 32-64 B HBM request each)")}
-    # whole pipeline: every kernel's algorithmic bytes per step / wall time per step (the two
-    # streams overlap, so this is the chip-level rate the path sustains)
-    alg_step = sum(v["bytes"] for v in ktimes.values()) / a.steps
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "kernel": f"sort stream (critical path: {len(sort_k)} kernels, Lyndon -> omega-order sort -> "
+                      "BBWT gather -> MTF + Rice sizes)",
+            "kernel_ms_per_step": round(sort_ms, 3),
+            "contract_bytes_per_step": contract,
+            "contract": f"SURVEY 8d: n(44 R_lin + 8) + n(44 R + 7) + 2n + n + (n + out_w) per block, R_lin = 0 "
+                        f"(Duval), R = per-block doubling rounds (mean {r_avg:.2f}), out_w = {out_w}",
+            "builder_bytes_per_step": int(builder),
+            "builder_frac": round(builder / (sort_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if sort_ms else None,
+            "traffic_frac": round(traffic / (sort_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if traffic else None,
+            "stream_span_ms": round(s0["ms_sa"] + s0["ms_entropy"], 3),
+            "limiter": SORT_STREAM_LIMITER,
+            "dominant_kernel": {"name": dom_name, "avg_launch_ms": round(dom_avg, 4),
+                                "launches_per_step": dom["launches"] // ks,
+                                "achieved_GBs": round(dom["bytes"] / max(dom["launches"], 1) / (dom_avg * 1e-3) / 1e9, 2)
+                                if dom_avg else None,
+                                "limiter": LIMITER.get(dom_name, "random 4-byte gathers / scatters")}}
+    lz = ktimes.get("k_lz_local")
+    lz_detail = None
+    if lz:
+        lz_avg = lz["ms"] / lz["launches"]
+        lz_detail = {"avg_launch_ms_overlapped": round(lz_avg, 3),
+                     "avg_launch_ms_solo": round(solo["times"]["k_lz_local"]["ms"], 3)
+                     if solo and "k_lz_local" in solo["times"] else None,
+                     "algorithmic_bytes_per_launch": int(lz["bytes"] / lz["launches"]),
+                     "contract_bytes_per_launch": int(35 * n + int(sizes[:, 7].astype(np.int64).sum())),  # 35n + out_lz
+                     "limiter": LIMITER["k_lz_local"]}
+    # whole pipeline: every kernel's algorithmic bytes per step / wall time per step
+    alg_step = sum(v["bytes"] for v in ktimes.values()) / ks
     pipe = {"algorithmic_bytes_per_step": int(alg_step),
             "achieved_GBs": round(alg_step / (ms_step * 1e-3) / 1e9, 2),
             "frac": round(alg_step / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
@@ -287,42 +372,31 @@ def main():
     # Decode side (decompress, PY:2451-2550): the payloads still resident in the arena
     # decoded back on the device (kolm_decode_blocks_device, every id 0..9); checked
     # against the input once, then timed with the same discipline.
-    lens = np.full(nb, a.bs, np.uint32)
-    lens[-1] = n - a.bs * (nb - 1)
+    blens = np.full(nb, a.bs, np.uint32)
+    blens[-1] = n - a.bs * (nb - 1)
+    cur_arena = [arenas[(nstep[0] - 1) % len(arenas)]]
 
     def decode_leg():
         d_out = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
         dms = ctypes.c_double(0.0)
+        acc = [0.0]
 
         def dstep():
-            _lib.check(L.kolm_decode_blocks_device(ctx, arena.data_ptr(), off.ctypes.data, method.ctypes.data,
-                                                   lens.ctypes.data, nb, d_out.data_ptr(), n + 64, ctypes.byref(dms)))
+            _lib.check(L.kolm_decode_blocks_device(ctx, cur_arena[0].data_ptr(), off.ctypes.data, method.ctypes.data,
+                                                   blens.ctypes.data, nb, d_out.data_ptr(), n + 64, ctypes.byref(dms)))
+            acc[0] += dms.value
 
         dstep()
         torch.cuda.synchronize()
         ok = bool(torch.equal(d_out[:n], d_in[:n]))
         if not ok:
             raise SystemExit("decode leg: device round trip differs from the input")
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        dk = 0.0
-        for _ in range(a.decode_steps):
-            dstep()
-            dk += dms.value
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        eld = time.perf_counter() - t0
-        if world > 1:
-            tt = torch.tensor([eld], dtype=torch.float64, device="cuda")
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            eld = float(tt[0])
+        acc[0] = 0.0
+        eld, _ = timed(dstep, a.decode_steps)
         del d_out
         return {"value": round(world * n * a.decode_steps / eld / MB, 2), "unit": "MB/s", "steps": a.decode_steps,
                 "ms_per_step": round(eld / a.decode_steps * 1e3, 2),
-                "kernel_ms_per_step": round(dk / a.decode_steps, 2), "round_trip_exact": ok,
+                "kernel_ms_per_step": round(acc[0] / a.decode_steps, 2), "round_trip_exact": ok,
                 "methods": np.bincount(method, minlength=10).tolist()}
 
     dec = decode_leg() if a.decode_steps > 0 else None
@@ -331,41 +405,31 @@ def main():
     # the hot path): same data, same timing discipline; reported beside the hot-path value.
     full = None
     if a.full_steps > 0:
-        method_hot = method.copy()
-        off_hot = off.copy()
-        arena_hot = arena
+        method_hot, off_hot, sizes_hot = method.copy(), off.copy(), sizes.copy()
         step(_lib.Stats(), _lib.KOLM_DEFAULT_MASK)
-        drain()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
         fst = []
-        for _ in range(a.full_steps):
-            st = _lib.Stats()
-            arena = step(st, _lib.KOLM_DEFAULT_MASK)
-            fst.append(st.as_dict())
-        drain()
-        if world > 1:
-            dist.barrier()
-        elf = time.perf_counter() - t0
-        if world > 1:
-            tt = torch.tensor([elf], dtype=torch.float64, device="cuda")
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            elf = float(tt[0])
-        f0 = fst[-1]
+
+        def full_step():
+            fst.append(_lib.Stats())
+            return step(fst[-1], _lib.KOLM_DEFAULT_MASK)
+
+        elf, _ = timed(full_step, a.full_steps)
+        cur_arena[0] = arenas[(nstep[0] - 1) % len(arenas)]
+        f0 = fst[-1].as_dict()
         full = {"value": round(world * n * a.full_steps / elf / MB, 2), "unit": "MB/s", "steps": a.full_steps,
                 "ms_per_step": round(elf / a.full_steps * 1e3, 2), "candidates": "0..9 (PY's full list)",
                 "ms_repair": round(f0["ms_repair"], 2), "ratio": round(float(off[-1]) / n, 4),
                 "methods": np.bincount(method, minlength=10).tolist(),
                 "repair_rules_per_block": round(f0["rp_rules"] / nb, 1),
                 "repair_batches_per_block": round(f0["rp_batches"] / nb, 1)}
+        if golden:
+            fh = cur_arena[0][:int(off[-1])].cpu().numpy().tobytes()
+            fok = check_blocks(golden, sizes, method, fh, off, 10, "w10", "sha10")
+            full["parity_blocks"] = f"{sum_all(fok, world)}/{sum_all(nb, world)}"
         # decode of those payloads (Re-Pair wins every text block): grammar expansion on the device
         if a.decode_steps > 0:
             full["decode"] = decode_leg()
-        method[:] = method_hot
-        off[:] = off_hot
-        arena = arena_hot
+        method[:], off[:], sizes[:] = method_hot, off_hot, sizes_hot
 
     # Content-defined mode (compress_blocks_cdc, PY:2213-2326): FastCDC boundaries on the
     # device (PY's default 4096/8192/16384) + candidates 0..8 over the variable-length
@@ -387,25 +451,12 @@ def main():
             cst["ms_bounds"] = (time.perf_counter() - t_b) * 1e3
             st = _lib.Stats()
             _lib.check(L.kolm_encode_blocks_device_var(ctx, d_in.data_ptr(), hst.ctypes.data, int(nch.value),
-                                                       _lib.KOLM_HOTPATH_MASK, None, arena.data_ptr(), cap,
+                                                       _lib.KOLM_HOTPATH_MASK, None, arenas[0].data_ptr(), cap,
                                                        csz.ctypes.data, cmeth.ctypes.data, coff.ctypes.data,
                                                        ctypes.byref(st)))
 
         cdc_step()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(a.cdc_steps):
-            cdc_step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        elc = time.perf_counter() - t0
-        if world > 1:
-            tt = torch.tensor([elc], dtype=torch.float64, device="cuda")
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            elc = float(tt[0])
+        elc, _ = timed(cdc_step, a.cdc_steps)
         nbc = int(nch.value)
         cdc = {"value": round(world * n * a.cdc_steps / elc / MB, 2), "unit": "MB/s", "steps": a.cdc_steps,
                "ms_per_step": round(elc / a.cdc_steps * 1e3, 2), "ms_boundaries": round(cst["ms_bounds"], 2),
@@ -426,36 +477,106 @@ def main():
         def v2_step():
             st = _lib.Stats()
             _lib.check(L.kolm_encode_blocks_device(ctx, d_in.data_ptr(), n2, a.bs, _lib.KOLM_FULL_MASK, None,
-                                                   arena.data_ptr(), cap, sz2.ctypes.data, m2.ctypes.data,
+                                                   arenas[0].data_ptr(), cap, sz2.ctypes.data, m2.ctypes.data,
                                                    o2.ctypes.data, ctypes.byref(st)))
 
         v2_step()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(a.v2_steps):
-            v2_step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        el2 = time.perf_counter() - t0
-        if world > 1:
-            tt = torch.tensor([el2], dtype=torch.float64, device="cuda")
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            el2 = float(tt[0])
+        el2, _ = timed(v2_step, a.v2_steps)
         v2 = {"value": round(world * n2 * a.v2_steps / el2 / MB, 2), "unit": "MB/s", "steps": a.v2_steps,
               "ms_per_step": round(el2 / a.v2_steps * 1e3, 2), "mib_per_gpu": n2 >> 20,
               "candidates": "0..10 (v2_new opt-in)", "ratio": round(float(o2[-1]) / n2, 4),
               "methods": np.bincount(m2, minlength=11).tolist(),
               "v2_new_size_ratio": round(float(sz2[:, 10].astype(np.float64).sum()) / n2, 4)}
 
+    # BASELINE configs 2 and 5 at their stated shapes (rank-local, resident in HBM): the
+    # gradient BMP's first 1 MiB as one block, and the mixed corpus (sine WAV || checker
+    # BMP || 1 MiB random) in 1 MiB blocks (3 blocks, a short tail) with per-block model
+    # selection; both checked against tests/golden/mixed_corpus.json (oracle answers).
+    configs = None
+    if a.config_steps > 0:
+        configs = {}
+        mg_path = os.path.join(GOLDEN, "mixed_corpus.json")
+        mg = json.load(open(mg_path)) if os.path.exists(mg_path) else {}
+        for name, gen in (("gradient_1m", lambda: datagen.gradient_bmp()[: 1 << 20]),
+                          ("mixed_corpus", datagen.mixed_corpus)):
+            cdata = gen()
+            cn = len(cdata)
+            cbs = 1 << 20
+            cnb = (cn + cbs - 1) // cbs
+            d_c = torch.empty(cn + 64, dtype=torch.uint8, device="cuda")
+            d_c[:cn].copy_(torch.frombuffer(bytearray(cdata), dtype=torch.uint8))
+            ccap2 = 9 * cn + 4096
+            d_ar = torch.empty(ccap2, dtype=torch.uint8, device="cuda")
+            res = {}
+            for label, mask, wkey, shakey, ncand in (("ids0_8", _lib.KOLM_HOTPATH_MASK, "w9", "sha9", 9),
+                                                     ("ids0_9", _lib.KOLM_DEFAULT_MASK, "w10", "sha10", 10)):
+                csz = np.zeros((cnb, _lib.KOLM_NCAND), np.uint32)
+                cm = np.zeros(cnb, np.uint32)
+                co = np.zeros(cnb + 1, np.uint64)
+                cst = [_lib.Stats()]
+
+                def cstep():
+                    cst[0] = _lib.Stats()
+                    _lib.check(L.kolm_encode_blocks_device(ctx, d_c.data_ptr(), cn, cbs, mask, None, d_ar.data_ptr(),
+                                                           ccap2, csz.ctypes.data, cm.ctypes.data, co.ctypes.data,
+                                                           ctypes.byref(cst[0])))
+
+                cstep()
+                elx, _ = timed(cstep, a.config_steps)
+                sd = cst[0].as_dict()
+                r = {"value": round(world * cn * a.config_steps / elx / MB, 2), "unit": "MB/s",
+                     "ms_per_call": round(elx / a.config_steps * 1e3, 3), "device_ms": round(sd["ms_total"], 3),
+                     "ms_sa": round(sd["ms_sa"], 3), "ms_lz": round(sd["ms_lz"], 3),
+                     "cyclic_rounds": sd["cyc_rounds"], "ratio": round(float(co[-1]) / cn, 4),
+                     "methods": cm.tolist()}
+                if mask == _lib.KOLM_DEFAULT_MASK:
+                    r["ms_repair"] = round(sd["ms_repair"], 3)
+                g = mg.get(name)
+                if g and g["input"]["len"] == cn:
+                    hostp = d_ar[:int(co[-1])].cpu().numpy().tobytes()
+                    r["parity_blocks"] = f"{check_blocks(g, csz, cm, hostp, co, ncand, wkey, shakey)}/{cnb}"
+                res[label] = r
+            res["bytes"] = cn
+            res["blocks"] = cnb
+            configs[name] = res
+            del d_c, d_ar
+
+    # The reference's own API on a host buffer (PCIe-inclusive, never the headline):
+    # kolm.compress_blocks_fixed(bytes, 1 MiB) -> container bytes, on the bench stream.
+    host = None
+    if a.host_steps > 0 and world == 1:
+        import kolm
+        kolm._lib.ensure_init(local)
+        blob = kolm.compress_blocks_fixed(data, a.bs, hot_path=True)  # warm-up (allocations)
+        t0 = time.perf_counter()
+        for _ in range(a.host_steps):
+            blob = kolm.compress_blocks_fixed(data, a.bs, hot_path=True)
+        elh = (time.perf_counter() - t0) / a.host_steps
+        # its parts: PCIe H2D of the input and D2H of the payloads (pageable host memory,
+        # as the API receives it), and the device encode of the same batch
+        hb = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        d_in[:n].copy_(hb)
+        torch.cuda.synchronize()
+        h2d = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        _ = arena[:int(off[-1])].cpu()
+        d2h = time.perf_counter() - t0
+        host = {"value": round(n / elh / MB, 2), "unit": "MB/s", "steps": a.host_steps,
+                "ms_per_call": round(elh * 1e3, 2), "container_bytes": len(blob),
+                "ms_h2d_pageable": round(h2d * 1e3, 2), "ms_d2h_pageable": round(d2h * 1e3, 2),
+                "ms_device_step": round(ms_step, 2),
+                "pcie_share": round((h2d + d2h) / elh, 3),
+                "note": "kolm.compress_blocks_fixed(bytes, 1 MiB, hot_path=True) on the bench stream: H2D of the "
+                        "pageable input, the batched device encode, D2H of the payloads, native TOC + container join"}
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(data, a.bs, a.cpu_budget)
 
     if rank == 0:
-        s0 = stats[-1]
+        hot = {kk: round(v["ms"] / ks, 3) for kk, v in sorted(ktimes.items(), key=lambda kv: -kv[1]["ms"])[:14]}
         out = {
             "metric": "compress MB/s at fixed block size, bit-exact vs reference; 1/2/4/8-GPU scaling",
             "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -469,25 +590,38 @@ def main():
                        "parallelism": f"block-shard x{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,
-            "detail": {"ratio": round(float(off[-1]) / n, 4),
+            "detail": {"parity_blocks": f"{parity['ok']}/{parity['blocks']}"
+                                        + ("" if parity["checked"] == parity["blocks"]
+                                           else f" ({parity['checked']} with fixtures)"),
+                       "ratio": round(float(off[-1]) / n, 4),
                        "methods": np.bincount(method, minlength=10).tolist(),
+                       "kernel_timed_pass_ms_per_step": round(elk / ks * 1e3, 2),
+                       "serialised_step_ms": round(solo["ms_step"], 2) if solo else None,
+                       "lz77_parse": lz_detail,
                        "decode": dec,
                        "full_candidates": full,
                        "cdc_mode": cdc,
                        "v2_new": v2,
+                       "configs": configs,
+                       "host_e2e": host,
                        "device_ms": {k: round(s0[k], 2) for k in ("ms_total", "ms_sa", "ms_lz", "ms_entropy", "ms_emit")},
-                       "cyclic_rounds": s0["cyc_rounds"],
+                       "cyclic_rounds": s0["cyc_rounds"], "cyclic_rounds_mean_per_block": round(r_avg, 3),
                        "lz77": {"tokens": s0["lz_tokens"], "stitch_fixups": s0["lz_fix"],
                                 "long_extensions": s0["lz_long"]},
                        "pipeline_roofline": pipe,
-                       "critical_path_roofline": crit,
-                       "families_ms_per_step": {kk: round(v["ms"] / a.steps, 2) for kk, v in
-                                                sorted(kern.items(), key=lambda kv: -kv[1]["ms"])},
-                       "kernels_ms_per_step": {kk: round(v["ms"] / a.steps, 3) for kk, v in
-                                               sorted(ktimes.items(), key=lambda kv: -kv[1]["ms"])[:12]}},
+                       "families_ms_per_step": {KN: round(sum(v["ms"] for v in ktimes.values()
+                                                              if _lib.KT_NAMES[v["family"]] == KN) / ks, 2)
+                                                for KN in _lib.KT_NAMES
+                                                if any(_lib.KT_NAMES[v["family"]] == KN for v in ktimes.values())},
+                       "kernels_ms_per_step": hot,
+                       "sort_stream_kernels_ms_per_step": {kk: round(v["ms"] / ks, 3) for kk, v in
+                                                           sorted(sort_k.items(), key=lambda kv: -kv[1]["ms"])},
+                       "solo_kernels_ms": {kk: round(v["ms"], 3) for kk, v in
+                                           sorted(solo["times"].items(), key=lambda kv: -kv[1]["ms"])[:14]}
+                       if solo else None},
         }
         if os.environ.get("KOLM_BENCH_ALLK"):  # A/B tooling (tools/kab.sh): every kernel
-            out["detail"]["kernels_all_ms_per_step"] = {kk: round(v["ms"] / a.steps, 3) for kk, v in ktimes.items()}
+            out["detail"]["kernels_all_ms_per_step"] = {kk: round(v["ms"] / ks, 3) for kk, v in ktimes.items()}
         if cpu:
             out["detail"]["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         print(json.dumps(out), flush=True)

@@ -16,7 +16,8 @@
  *   kolm_encode_blocks_multi: same as kolm_encode_blocks over several devices of one
  *                             process (contiguous block shards, one host thread and
  *                             context per device).
- * The container/TOC writer stays on the host (PY:2375-2445), see kolm/container.py.
+ *   kolm_toc_write / kolm_toc_read: the KOLR container's header + TOC on the host
+ *                             (PY:2375-2445 writer, PY:2451-2530 reader; kolm_toc.cpp).
  *
  * Conventions: plain pointers and sizes; caller-allocated buffers with explicit
  * capacities; every function returns 0 (KOLM_OK) or a negative code; no exception
@@ -40,6 +41,8 @@ extern "C" {
 #define KOLM_EHIP (-3)     /* HIP runtime error (message: kolm_last_error) */
 #define KOLM_ERCCL (-4)    /* reserved: collective error */
 #define KOLM_ENOINIT (-5)  /* kolm_init not called */
+#define KOLM_EFORMAT (-6)  /* malformed container (message: PY's ValueError text) */
+#define KOLM_ERANGE (-7)   /* a container field overflows (PY: struct.error) */
 
 /* Candidate method ids (index into PY _select_encoders(), PY:2152-2165). */
 #define KOLM_M_RAW 0
@@ -101,6 +104,8 @@ typedef struct kolm_stats {
     uint64_t rp_batches;      /* Re-Pair batches (sequential depth) summed over blocks */
     uint64_t rp_final;        /* Re-Pair final sequence symbols over all blocks */
     uint64_t lz_fix;          /* LZ77 tokens the stitch computed off the speculative paths */
+    uint64_t cyc_rounds_sum;  /* sum over blocks of the doubling rounds each block needed (round 0
+                                 counted; SURVEY §8d's per-block R, used for the byte contract) */
 } kolm_stats;
 
 /* ---- library / default context ------------------------------------------------ */
@@ -143,6 +148,24 @@ int kolm_cdc_boundaries(const uint8_t* data, uint64_t n, uint32_t min_size, uint
 int kolm_decode_blocks(const uint8_t* payloads, const uint64_t* payload_off, const uint32_t* methods,
                        const uint32_t* orig_lens, uint32_t nblocks, uint8_t* out, uint64_t out_cap);
 
+/* ---- container (host only: no device call, usable without a GPU) ---------------- */
+/* Header + TOC of a KOLR container (PY:2213-2326 CDC, PY:2332-2445 fixed): mode 0 fixed /
+ * 1 CDC, size_field = block size (fixed) or avg_size (CDC), nblocks entries of method id,
+ * original length and payload length.  Writes every byte that precedes the payload area
+ * (the payloads follow back to back) into out[0, cap); *out_len receives the count (out
+ * may be NULL to query it).  KOLM_ERANGE when nblocks > 65535 or total_len >= 2^32. */
+int kolm_toc_write(int mode, uint32_t size_field, uint64_t total_len, uint32_t nblocks,
+                   const uint32_t* methods, const uint32_t* orig_lens, const uint64_t* payload_lens,
+                   uint8_t* out, uint64_t cap, uint64_t* out_len);
+/* Parses a whole container buf[0, n): fields[4] = {mode, size_field, total_len, nblocks},
+ * *payload_start = offset of the payload area, methods / orig_lens (cap >= nblocks
+ * entries) and payload_off (nblocks + 1 entries, relative to the payload area).  Checks
+ * exactly what PY's decompress checks before decoding (magic, truncations, RLE size, EF
+ * sum, trailing bytes): KOLM_EFORMAT with PY's message otherwise; KOLM_ECAP (fields and
+ * *payload_start filled) when cap < nblocks. */
+int kolm_toc_read(const uint8_t* buf, uint64_t n, uint32_t* fields, uint64_t* payload_start,
+                  uint32_t* methods, uint32_t* orig_lens, uint64_t* payload_off, uint32_t cap);
+
 /* ---- batched hot entry (host buffers, default context) ------------------------- */
 /* Encodes nblocks blocks of `data` (block i = data[starts[i] .. starts[i]+lens[i]);
  * blocks contiguous and non-empty: fixed chunking when all lens are equal except a
@@ -182,9 +205,14 @@ int kolm_memcpy_d2h(kolm_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 int kolm_ctx_sync(kolm_ctx* ctx);
 /* Enable (1) / disable (0) per-launch HIP-event timing of the kernel families. */
 int kolm_ctx_set_timing(kolm_ctx* ctx, int enable);
+/* 1: run every launch of the next batches on one stream (kernels serialised: each kernel's
+ * solo duration, for profiling); 0 (default, or KOLM_SERIAL=1 at context creation): the
+ * sort chain, the LZ77 parse and Re-Pair overlap on their own streams. */
+int kolm_ctx_set_serial(kolm_ctx* ctx, int serial);
 /* Per-kernel timing accumulated since timing was enabled, as JSON text
- * {"k_name": {"ms": .., "launches": .., "bytes": .., "family": KOLM_KT_*}, ...} (bytes =
- * algorithmic HBM bytes).  *len receives the length; buf may be NULL to query it. */
+ * {"k_name": {"ms": .., "launches": .., "bytes": .., "family": KOLM_KT_*, "stream":
+ * "sort"|"index"|"repair"}, ...} (bytes = algorithmic HBM bytes; stream = the
+ * HIP stream the kernel ran on).  *len receives the length; buf may be NULL to query it. */
 int kolm_ctx_kernel_times(kolm_ctx* ctx, char* buf, size_t cap, size_t* len);
 /* Fixed-size blocks of d_data (device pointer, total bytes, block_size).  Payloads go
  * to the device arena d_arena (cap bytes); h_sizes / h_method / h_off are host arrays

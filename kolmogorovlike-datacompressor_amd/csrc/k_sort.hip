@@ -909,11 +909,24 @@ __global__ __launch_bounds__(WG) void k_finalize_eq(const Seg* eq, SortArgs a, L
     if (threadIdx.x == 0) L.next[atomicAdd(L.next_cnt, 1u)] = Seg{s.start, len};
 }
 
-__global__ void k_update_done(u32* done, const u32* split, u32 nb) {
+// done[b] = 1 + the round in which block b stopped splitting (0 while it still splits)
+__global__ void k_update_done(u32* done, const u32* split, u32 nb, u32 round) {
     const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < nb && !split[b]) done[b] = 1;
+    if (b < nb && !split[b] && !done[b]) done[b] = round + 1;
 }
 
+// sum over blocks of the doubling rounds each block needed: the round that first found
+// it converged is not counted (it may only have confirmed convergence); blocks never
+// marked converged ran every round
+__global__ void k_rounds_sum(const u32* done, u32 nb, u32 rounds, unsigned long long* out) {
+    u64 acc = 0;
+    for (u32 b = threadIdx.x; b < nb; b += blockDim.x) {
+        const u32 d = done[b];
+        acc += d ? (d > 1 ? d - 1 : 1) : rounds;
+    }
+    for (int o = 32; o; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)acc);
+}
 
 // ------------------------------------------------------------------------------------
 // launchers
@@ -1018,8 +1031,13 @@ void launch_small_sort(int c, const Seg* segs, u32 count, const SortArgs& a, con
 void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists& L, hipStream_t s) {
     if (count) k_finalize_eq<<<count, WG, 0, s>>>(eq, a, L);
 }
-void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, hipStream_t s) {
-    if (nb) k_update_done<<<cdiv(nb, 256), 256, 0, s>>>(blk_done, blk_split, nb);
+void launch_rounds_sum(const u32* blk_done, u32 nb, u32 rounds, u64* out, hipStream_t s) {
+    KOLM_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(u64), s));
+    k_rounds_sum<<<1, 256, 0, s>>>(blk_done, nb, rounds, reinterpret_cast<unsigned long long*>(out));
+}
+
+void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, u32 round, hipStream_t s) {
+    if (nb) k_update_done<<<cdiv(nb, 256), 256, 0, s>>>(blk_done, blk_split, nb, round);
 }
 
 // ------------------------------------------------------------------------------------

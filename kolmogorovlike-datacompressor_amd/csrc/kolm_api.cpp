@@ -26,11 +26,12 @@
 
 using namespace kolm;
 
-namespace {
-
-thread_local std::string g_err;
-
+namespace kolm {
+thread_local std::string g_err;  // kolm_last_error(); also set by kolm_toc.cpp
 void set_err(const std::string& s) { g_err = s; }
+}  // namespace kolm
+
+namespace {
 
 struct DevBuf {
     void* p = nullptr;
@@ -56,7 +57,9 @@ enum : int {
     C_L0ELEM = 36,
     C_L1ELEM = 37,
     C_CDC = 40,      // FastCDC cut count
-    C_N = 48
+    C_N = 48,
+    H_RSUM = C_N,    // host mirror only (2 words): summed per-block cyclic rounds
+    H_N = C_N + 16
 };
 
 }  // namespace
@@ -81,6 +84,7 @@ struct kolm_ctx {
     hipStream_t aux = nullptr;     // second stream: Lyndon + cyclic sort chain runs beside LZ77
     hipStream_t active = nullptr;  // stream used by launches / TScope / sync()
     hipStream_t rp = nullptr;      // third stream: Re-Pair (candidate 9), one workgroup per block
+    bool serial = false;           // every launch of a batch on one stream (kolm_ctx_set_serial; KOLM_SERIAL=1)
     hipEvent_t evj[4] = {};        // join events
     hipEvent_t evr[2] = {};        // Re-Pair start / done
     std::mutex mu;
@@ -96,12 +100,15 @@ struct kolm_ctx {
         const char* name;
         hipEvent_t a, b;
         u64 bytes;
+        int strm;  // 0 index stream, 1 sort stream, 2 Re-Pair stream
     };
+    int strm_of(hipStream_t s) const { return s == aux ? 1 : s == rp ? 2 : 0; }
     std::vector<Pend> pend;
     struct Acc {
         double ms = 0;
         u64 launches = 0, bytes = 0;
-        int fam = 0;  // KOLM_KT_* family of the kernel
+        int fam = 0;   // KOLM_KT_* family of the kernel
+        int strm = 0;  // stream of its last launch (Pend::strm)
     };
     std::map<std::string, Acc> kacc;  // per kernel, accumulated while timing is enabled
     // KTimer for multi-kernel launchers: events on the active stream, nested scopes allowed
@@ -124,7 +131,7 @@ struct kolm_ctx {
             open.pop_back();
             hipEvent_t b = c->ev_take();
             KOLM_HIP_CHECK(hipEventRecord(b, c->active));
-            c->pend.push_back({o.fam, o.name, o.a, b, o.bytes});
+            c->pend.push_back({o.fam, o.name, o.a, b, o.bytes, c->strm_of(c->active)});
         }
     } hook;
     KTimer* kt() {
@@ -152,6 +159,7 @@ struct kolm_ctx {
             st->kt[p.fam].bytes += p.bytes;
             Acc& a = kacc[p.name];
             a.fam = p.fam;
+            a.strm = p.strm;
             a.ms += ms;
             a.launches += 1;
             a.bytes += p.bytes;
@@ -206,7 +214,7 @@ TScope::~TScope() noexcept(false) {
     if (c->timing) {
         hipEvent_t b = c->ev_take();
         KOLM_HIP_CHECK(hipEventRecord(b, c->active));
-        c->pend.push_back({fam, name, a, b, bytes});
+        c->pend.push_back({fam, name, a, b, bytes, c->strm_of(c->active)});
     }
 }
 
@@ -338,7 +346,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
             launch_round0(geo, r, nxt, L.next_cnt, a.blk_split, s, c->kt());
             out.active += N;
             out.rounds = 1;
-            launch_update_done(blk_done, a.blk_split, geo.nb, s);
+            launch_update_done(blk_done, a.blk_split, geo.nb, 0, s);
             KOLM_HIP_CHECK(hipMemcpyAsync(h + C_NEXT, cnt + C_NEXT, sizeof(u32), hipMemcpyDeviceToHost, s));
             if (after_round0) {
                 after_round0();
@@ -459,13 +467,14 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
             TScope t(c, KOLM_KT_SMALLSORT, "k_finalize_eq", (u64)h[C_EQ] * TILE * 8);
             launch_finalize_eq(L.eq, h[C_EQ], a, L, s);
         }
-        if (cyclic) launch_update_done(blk_done, a.blk_split, geo.nb, s);
+        if (cyclic) launch_update_done(blk_done, a.blk_split, geo.nb, round, s);
         KOLM_HIP_CHECK(hipMemcpyAsync(h + C_NEXT, cnt + C_NEXT, sizeof(u32), hipMemcpyDeviceToHost, s));
         c->sync();
         round_done(round);
         ncur = h[C_NEXT];
         std::swap(cur, nxt);
     }
+    if (cyclic) launch_rounds_sum(blk_done, geo.nb, out.rounds, c->get<u64>("rsum", 1), s);
     return out;
 }
 
@@ -684,6 +693,15 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         if (stats) *stats = kolm_stats{};
         return KOLM_OK;
     }
+    // every argument check before the first launch: an error return never leaves work in flight
+    if (((mask >> KOLM_M_V2NEW) & 1u) && 8 * N >= (1ull << 32)) {
+        set_err("v2_new (candidate 10): batches up to 512 MiB");
+        return KOLM_EARG;
+    }
+    if (((mask >> KOLM_M_REPAIR) & 1u) && bs > RP_MAX_N) {
+        set_err("Re-Pair (candidate 9) supports blocks up to 4 MiB (KOLM_REPAIR_MAX_BLOCK)");
+        return KOLM_EARG;
+    }
     // Two streams: the index stream (main) runs the xor/lfsr size counters, the BBWT
     // predecessor bytes and the LZ77 parse (k_lz_local + stitch); the sort stream (aux,
     // higher priority: the critical path) runs the Lyndon factorisation, the cyclic sort,
@@ -692,7 +710,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     // LZ77 starts: 0 (default) at once, 1 after the Lyndon factorisation, 2 after round 0 of
     // the cyclic sort.  With the 8-character round 0 (eight streaming LSD passes beside the
     // LDS-bound parse): 53.8-54.2 ms per 256 MiB for 0, 54.1-54.2 for 1, 55.4-56.2 for 2.
-    static const bool serial = getenv("KOLM_SERIAL") && atoi(getenv("KOLM_SERIAL")) != 0;
+    const bool serial = c->serial;
     static const int overlap = getenv("KOLM_OVERLAP") ? atoi(getenv("KOLM_OVERLAP")) : 0;
     hipStream_t ms = c->stream, s = serial ? c->stream : c->aux;
     Pipeline P{c, geo, d_text};
@@ -713,10 +731,6 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     const bool want_rp = (mask >> KOLM_M_REPAIR) & 1u;
     RpArgs rpa{};
     if (want_rp) {
-        if (bs > RP_MAX_N) {
-            set_err("Re-Pair (candidate 9) supports blocks up to 4 MiB (KOLM_REPAIR_MAX_BLOCK)");
-            return KOLM_EARG;
-        }
         rpa.geo = geo;
         rpa.text = d_text;
         rpa.ws_stride = repair_ws_bytes(bs);
@@ -735,15 +749,23 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         }
         // Blocks run in groups whose workspaces fit the budget (~258 MB per 1 MiB block);
         // a second group serialises behind the first, so the default budget is most of the
-        // device memory still free (KOLM_RP_WS_GB overrides), not a fixed figure.
+        // device memory still free (KOLM_RP_WS_GB overrides), not a fixed figure: 3/4 of
+        // what is free (the workspace already held counts as free) after the rest of the
+        // batch's scratch (about 96 B per position for the sort / LZ77 / emission arrays,
+        // minus what this context already holds) is set aside.
         u64 budget;
         if (getenv("KOLM_RP_WS_GB")) {
             budget = (u64)(atof(getenv("KOLM_RP_WS_GB")) * (double)(1ull << 30));
         } else {
             size_t fr = 0, total = 0;
             KOLM_HIP_CHECK(hipMemGetInfo(&fr, &total));
-            const u64 held = c->bytes_held("rp_ws");  // reused below: counts as free
-            budget = std::max<u64>((u64)((fr + held) * 0.75), 8ull << 30);
+            const u64 held_rp = c->bytes_held("rp_ws");
+            u64 held_other = 0;
+            for (const auto& kv : c->bufs)
+                if (kv.first != "rp_ws") held_other += kv.second.cap;
+            const u64 need_other = 96 * N > held_other ? 96 * N - held_other : 0;
+            const u64 avail = fr + held_rp > need_other ? fr + held_rp - need_other : 0;
+            budget = (u64)(avail * 0.75);
         }
         const u32 group = (u32)std::max<u64>(1, std::min<u64>(nb, budget / rpa.ws_stride));
         rpa.ws = c->get<char>("rp_ws", (u64)group * rpa.ws_stride);
@@ -805,6 +827,8 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         c->active = s;
         bw = P.cyclic();
     }
+    // per-block doubling rounds of the omega-order sort (R per block)
+    KOLM_HIP_CHECK(hipMemcpyAsync(c->h_cnt + H_RSUM, c->get<u64>("rsum", 1), sizeof(u64), hipMemcpyDeviceToHost, s));
     KOLM_HIP_CHECK(hipEventRecord(ev[1], s));
     u8* mt = P.mtf(bw, d_bits);
     EmitArgs e{};
@@ -833,7 +857,14 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     // Rice sizes; the plane BBWTs reuse the sort scratch (the blocks' own sort is done)
     const bool want_v2 = (mask >> KOLM_M_V2NEW) & 1u;
     V2State v2{};
+    std::map<std::string, size_t> caps_before_v2;
     if (want_v2) {
+        // the plane sorts reuse the sort scratch at up to 8x the batch's positions: the
+        // buffers they grow are reallocated here, so the sort stream's own work on them
+        // is drained first (the LZ77 / Re-Pair streams use none of them), and they are
+        // released again once the batch is complete (hot-path batches keep their size)
+        KOLM_HIP_CHECK(hipStreamSynchronize(s));
+        for (const auto& kv : c->bufs) caps_before_v2[kv.first] = kv.second.cap;
         if (!v2_stage(c, geo, d_text, s, v2)) return KOLM_EARG;
     }
     KOLM_HIP_CHECK(hipEventRecord(ev[2], s));
@@ -905,6 +936,16 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     std::vector<u32> ntok(want_lz ? nb : 0);
     if (want_lz) KOLM_HIP_CHECK(hipMemcpyAsync(ntok.data(), z.ntok, sizeof(u32) * nb, hipMemcpyDeviceToHost, s));
     c->sync();
+    if (want_v2) {
+        KOLM_HIP_CHECK(hipDeviceSynchronize());
+        for (auto& kv : c->bufs) {
+            const auto it = caps_before_v2.find(kv.first);
+            if (kv.second.p && (it == caps_before_v2.end() || kv.second.cap > it->second)) {
+                KOLM_HIP_CHECK(hipFree(kv.second.p));
+                kv.second = DevBuf{};
+            }
+        }
+    }
     if (h_off) std::memcpy(h_off, off.data(), sizeof(u64) * (nb + 1));
     if (want_lz && z.prof) {
         u64 pr[8];
@@ -926,6 +967,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         if (c->timing && want_lz) c->kacc[lz_spec_name()].bytes += tokens * 16;  // token records
         st.lz_long = c->h_cnt[C_NLONG];
         st.lz_fix = c->h_cnt[C_NFIX];
+        std::memcpy(&st.cyc_rounds_sum, c->h_cnt + H_RSUM, sizeof(u64));
         st.ms_sa = ev_ms(ev[0], ev[1]);
         st.ms_entropy = ev_ms(ev[1], ev[2]);
         st.ms_lz = ev_ms(ej[2], ej[1]);
@@ -981,9 +1023,10 @@ int ctx_create(int device, kolm_ctx** out) {
         }
         KOLM_HIP_CHECK(hipStreamCreateWithFlags(&c->rp, hipStreamNonBlocking));
         c->active = c->stream;
+        c->serial = getenv("KOLM_SERIAL") && atoi(getenv("KOLM_SERIAL")) != 0;
         for (auto& e : c->evj) KOLM_HIP_CHECK(hipEventCreate(&e));
         for (auto& e : c->evr) KOLM_HIP_CHECK(hipEventCreate(&e));
-        KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_cnt, sizeof(u32) * C_N, hipHostMallocDefault));
+        KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_cnt, sizeof(u32) * H_N, hipHostMallocDefault));
         for (auto& e : c->ev) KOLM_HIP_CHECK(hipEventCreate(&e));
         *out = c.release();
         return KOLM_OK;
@@ -1121,6 +1164,13 @@ int kolm_ctx_set_timing(kolm_ctx* c, int enable) {
     return KOLM_OK;
 }
 
+int kolm_ctx_set_serial(kolm_ctx* c, int serial) {
+    if (!c) return KOLM_EARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->serial = serial != 0;
+    return KOLM_OK;
+}
+
 int kolm_ctx_kernel_times(kolm_ctx* c, char* buf, size_t cap, size_t* len) {
     if (!c) return KOLM_EARG;
     std::lock_guard<std::mutex> g(c->mu);
@@ -1128,9 +1178,11 @@ int kolm_ctx_kernel_times(kolm_ctx* c, char* buf, size_t cap, size_t* len) {
     bool first = true;
     for (auto& kv : c->kacc) {
         char tmp[320];
-        snprintf(tmp, sizeof tmp, "%s\"%s\": {\"ms\": %.6f, \"launches\": %llu, \"bytes\": %llu, \"family\": %d}",
+        static const char* const sn[3] = {"index", "sort", "repair"};
+        snprintf(tmp, sizeof tmp,
+                 "%s\"%s\": {\"ms\": %.6f, \"launches\": %llu, \"bytes\": %llu, \"family\": %d, \"stream\": \"%s\"}",
                  first ? "" : ", ", kv.first.c_str(), kv.second.ms, (unsigned long long)kv.second.launches,
-                 (unsigned long long)kv.second.bytes, kv.second.fam);
+                 (unsigned long long)kv.second.bytes, kv.second.fam, sn[kv.second.strm]);
         js += tmp;
         first = false;
     }
@@ -1325,6 +1377,7 @@ int kolm_encode_blocks_multi(int ngpu, const uint8_t* data, uint64_t total, uint
             agg.cyc_rounds = std::max(agg.cyc_rounds, s.cyc_rounds);
             agg.lin_active += s.lin_active;
             agg.cyc_active += s.cyc_active;
+            agg.cyc_rounds_sum += s.cyc_rounds_sum;
             agg.lz_tokens += s.lz_tokens;
             agg.lz_long += s.lz_long;
             agg.lz_fix += s.lz_fix;

@@ -9,7 +9,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace kolm {
+
+void set_err(const std::string& s);  // message returned by kolm_last_error()
 
 using u8 = uint8_t;
 using u16 = uint16_t;
@@ -266,7 +270,8 @@ void launch_tiny_sort(int c, const Seg* segs, u32 count, const SortArgs& a, cons
 void launch_small_sort(int c, const Seg* segs, u32 count, const SortArgs& a, const Lists& L,
                        hipStream_t s);
 void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists& L, hipStream_t s);
-void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, hipStream_t s);
+void launch_rounds_sum(const u32* blk_done, u32 nb, u32 rounds, u64* out, hipStream_t s);
+void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, u32 round, hipStream_t s);
 
 // ---- k_blocks.hip: per-block scans, Lyndon factors, BBWT gather ----
 void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u8* FEd, u32* fstart, uint4* fpre, u32* nfac,

@@ -236,6 +236,9 @@ def candidate_mask(hot_path: bool = False, v2_new: Optional[bool] = None) -> int
         idx = CANDIDATE_NAMES.index(name)
         if idx >= GPU_CANDIDATES:
             raise ValueError(f"--only={G_ONLY_METHOD}: candidate not offloaded")
+        if idx == 10 and not (G_V2_NEW if v2_new is None else v2_new):
+            # PY: the only candidate raises, and so does its raw fallback call (PY:2363-2364)
+            raise NameError("v2_new raises in the reference (PY:1037-1043); enable G_V2_NEW to compute it")
         mask = 1 << idx
     return mask
 

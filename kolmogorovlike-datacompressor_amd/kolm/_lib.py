@@ -24,8 +24,10 @@ KOLM_DEFAULT_MASK = 0x3FF   # the reference's candidates 0..9 as shipped (kolm.h
 KOLM_FULL_MASK = 0x7FF      # + v2_new (id 10), automaton evaluated serially (opt-in)
 KOLM_HOTPATH_MASK = 0x1FF  # BBWT / MTF+Rice / LZ77 path, ids 0..8
 KOLM_REPAIR_MAX_BLOCK = 1 << 22
+KOLM_EFORMAT = -6
+KOLM_ERANGE = -7
 ERRORS = {-1: "bad argument", -2: "capacity too small", -3: "HIP error", -4: "collective error",
-          -5: "not initialised"}
+          -5: "not initialised", -6: "malformed container", -7: "field overflow"}
 
 
 class KolmUnavailable(ImportError):
@@ -65,6 +67,7 @@ class Stats(ctypes.Structure):
         ("rp_batches", ctypes.c_uint64),
         ("rp_final", ctypes.c_uint64),
         ("lz_fix", ctypes.c_uint64),
+        ("cyc_rounds_sum", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -107,6 +110,7 @@ SIGNATURES = [
     ("kolm_memcpy_d2h", I32, [P, P, P, U64]),
     ("kolm_ctx_sync", I32, [P]),
     ("kolm_ctx_set_timing", I32, [P, I32]),
+    ("kolm_ctx_set_serial", I32, [P, I32]),
     ("kolm_ctx_kernel_times", I32, [P, P, SZ, ctypes.POINTER(SZ)]),
     ("kolm_encode_blocks_device", I32, [P, P, U64, U32, U32, P, P, U64, P, P, P, P]),
     ("kolm_encode_blocks_device_var", I32, [P, P, P, U32, U32, P, P, U64, P, P, P, P]),
@@ -114,6 +118,8 @@ SIGNATURES = [
     ("kolm_cdc_boundaries_device", I32, [P, P, U64, U32, U32, U32, I32, P, U64, ctypes.POINTER(U64)]),
     ("kolm_decode_blocks", I32, [P, P, P, P, U32, P, U64]),
     ("kolm_decode_blocks_device", I32, [P, P, P, P, P, U32, P, U64, ctypes.POINTER(ctypes.c_double)]),
+    ("kolm_toc_write", I32, [I32, U32, U64, U32, P, P, P, P, U64, ctypes.POINTER(U64)]),
+    ("kolm_toc_read", I32, [U8P, U64, P, ctypes.POINTER(U64), P, P, P, U32]),
 ]
 KOLM_DECODE_MASK = 0x3FF  # methods decoded on the device: every id 0..9 (kolm.h)
 

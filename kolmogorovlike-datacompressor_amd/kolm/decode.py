@@ -174,53 +174,82 @@ def decode_lz77(data: bytes, orig_len: int) -> bytes:  # PY:1765-1812
     return bytes(out)
 
 
-def repair_decompress(data: bytes, orig_len: int) -> bytes:  # PY:1913-1978
+def _uleb_values(buf: bytes) -> Tuple[np.ndarray, np.ndarray]:
+    """Every ULEB128 value of buf at once: (values, end offset of each value)."""
+    a = np.frombuffer(buf, dtype=np.uint8)
+    ends = np.flatnonzero(a < 0x80)  # the last byte of every value
+    starts = np.concatenate([[0], ends[:-1] + 1]).astype(np.int64)
+    vals = np.zeros(ends.size, dtype=object)
+    # values of up to 9 groups fit in 63 bits and are summed vectorised; longer ones
+    # (never produced by the encoder) are folded one by one
+    width = ends - starts + 1
+    short = width <= 9
+    acc = np.zeros(ends.size, dtype=np.int64)
+    for g in range(9):
+        sel = short & (width > g)
+        acc[sel] |= (a[starts[sel] + g].astype(np.int64) & 0x7F) << (7 * g)
+    vals[short] = acc[short].tolist()
+    for j in np.flatnonzero(~short):
+        vals[j] = sum((int(b) & 0x7F) << (7 * g) for g, b in enumerate(a[starts[j]:ends[j] + 1]))
+    return vals, ends + 1
+
+
+def repair_decompress(data: bytes, orig_len: int) -> bytes:
+    """Re-Pair grammar expansion (inverse of repair_compress, PY:1913-1978): rules are
+    materialised children-first in a topological order of the rules the sequence reaches
+    (a rule referencing an undefined symbol or itself is rejected), then the sequence is
+    a join of its symbols' expansions."""
     if len(data) < 2 or data[:2] != b"RP":
         raise ValueError("Bad magic")
-    i = 2
-    terminals, i = uleb128_decode_stream(data, i)
-    if terminals != 256:
+    vals, ends = _uleb_values(bytes(data[2:]))
+
+    def field(i: int) -> int:
+        if i >= len(vals):
+            raise ValueError("Truncated ULEB128")
+        return int(vals[i])
+
+    if field(0) != 256:
         raise ValueError("Unsupported terminal alphabet")
-    nrules, i = uleb128_decode_stream(data, i)
-    rules: Dict[int, Tuple[int, int]] = {}
-    for r in range(nrules):
-        a, i = uleb128_decode_stream(data, i)
-        b, i = uleb128_decode_stream(data, i)
-        rules[256 + r] = (a, b)
-    seq_len, i = uleb128_decode_stream(data, i)
-    cache: Dict[int, bytes] = {}
-
-    def expand(sym: int) -> bytes:
-        if sym < 256:
-            return bytes((sym,))
-        if sym in cache:
-            return cache[sym]
-        stack = [(sym, 0)]
-        outs: List[bytes] = []
-        while stack:
-            node, st = stack.pop()
-            if node < 256:
-                outs.append(bytes((node,)))
+    nrules = field(1)
+    pairs = 2 + 2 * nrules
+    seq_len = field(pairs)
+    field(pairs + seq_len)  # the last symbol exists
+    rhs = {256 + r: (field(2 + 2 * r), field(3 + 2 * r)) for r in range(nrules)}
+    seq = vals[pairs + 1:pairs + 1 + seq_len]
+    # children-first order of the reachable rules (iterative DFS, gray = on the path)
+    order: List[int] = []
+    state: Dict[int, int] = {}
+    for root in {int(s) for s in seq if s >= 256}:
+        if state.get(root) == 2:
+            continue
+        path = [(root, 0)]
+        state[root] = 1
+        while path:
+            sym, k = path[-1]
+            if k == 2:
+                path.pop()
+                state[sym] = 2
+                order.append(sym)
                 continue
-            if st == 0:
-                a, b = rules[node]
-                stack.append((node, 1))
-                stack.append((b, 0))
-                stack.append((a, 0))
-            else:
-                right = outs.pop()
-                left = outs.pop()
-                cache[node] = left + right
-                outs.append(cache[node])
-        return outs[-1]
-
-    out = bytearray()
-    for _ in range(seq_len):
-        s, i = uleb128_decode_stream(data, i)
-        out += expand(s)
+            path[-1] = (sym, k + 1)
+            if sym not in rhs:
+                raise ValueError(f"Re-Pair: undefined symbol {sym}")
+            child = rhs[sym][k]
+            if child >= 256:
+                st = state.get(child, 0)
+                if st == 1:
+                    raise ValueError(f"Re-Pair: rule {child} expands into itself")
+                if st == 0:
+                    state[child] = 1
+                    path.append((child, 0))
+    table: Dict[int, bytes] = {t: bytes((t,)) for t in range(256)}
+    for sym in order:
+        a, b = rhs[sym]
+        table[sym] = table[a] + table[b]
+    out = b"".join(table[int(s)] for s in seq)
     if len(out) != orig_len:
-        raise RuntimeError("RePair output length mismatch")
-    return bytes(out)
+        raise RuntimeError(f"RePair output length mismatch: got {len(out)}, expect {orig_len}")
+    return out
 
 
 BBWT_FLAGS = {2: 0, 3: 1, 4: 4, 5: 8, 6: 16}

@@ -41,10 +41,10 @@ def test_ctypes_signatures_cover_header():
 
 
 def test_stats_struct_size_matches_header(tmp_path):
-    # kolm_stats: 2 u32 + 4 u64 + 5 double + KOLM_NKT(12) x {double, u64, u64} + double + 4 u64
+    # kolm_stats: 2 u32 + 4 u64 + 5 double + KOLM_NKT(12) x {double, u64, u64} + double + 5 u64
     nkt = int(re.search(r"#define KOLM_NKT (\d+)", open(HEADER).read()).group(1))
     assert nkt == len(_lib.KT_NAMES) == 12
-    assert ctypes.sizeof(_lib.Stats) == 8 + 4 * 8 + 5 * 8 + nkt * 24 + 8 + 4 * 8
+    assert ctypes.sizeof(_lib.Stats) == 8 + 4 * 8 + 5 * 8 + nkt * 24 + 8 + 5 * 8
     # the C compiler's layout of the header struct: size and every field offset
     src = tmp_path / "sz.c"
     fields = [f for f, _ in _lib.Stats._fields_]

@@ -101,6 +101,15 @@ def test_registry_ids_stable():
         kolm.G_ONLY_METHOD = None
     with pytest.raises(NameError):
         kolm._select_encoders()[10][0](b"x")  # v2_new raises as in PY
+    kolm.G_ONLY_METHOD = "v2_new"
+    try:
+        with pytest.raises(NameError):  # PY: the only candidate and its fallback raise
+            kolm.candidate_mask()
+        kolm.G_V2_NEW = True
+        assert kolm.candidate_mask() == 1 << 10
+    finally:
+        kolm.G_ONLY_METHOD = None
+        kolm.G_V2_NEW = False
     kolm.G_V2_NEW = True
     try:
         assert kolm.candidate_mask() == 0x7FF
@@ -142,3 +151,54 @@ def test_host_v2new_decoder_goldens():
         assert decode_new_pipeline(z[f"{n}/v2new"].tobytes(), len(data)) == data, n
     for c in m["containers"]:
         assert kolm.decompress(z[f"C/{c}/full10"].tobytes(), device=False) == z[f"C/{c}/input"].tobytes(), c
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_toc_writer_matches_reference_heapq(seed):
+    """The native TOC writer (kolm_toc.cpp) against the oracle's restatement of PY's writer
+    (Python heapq + _HuffNode ordering, PY:1267-1300, 2375-2445) on random method-id
+    sequences built to produce many equal-weight merged entries (2..11 distinct ids, runs
+    of 1..4): fixed and CDC mode, byte for byte, and read back."""
+    import oracle
+    rng = np.random.default_rng(seed)
+    k = int(rng.integers(2, 12))
+    alphabet = rng.choice(11, k, replace=False)
+    ids = []
+    while len(ids) < int(rng.integers(1, 400)):
+        ids += [int(rng.choice(alphabet))] * int(rng.integers(1, 5))
+    nb = len(ids)
+    bs = int(rng.integers(1, 5000))
+    cdc = bool(seed & 1)
+    lens = ([int(x) for x in rng.integers(1, 3 * bs, nb)] if cdc else [bs] * (nb - 1) + [int(rng.integers(1, bs + 1))])
+    pays = [bytes(int(rng.integers(0, 40))) for _ in range(nb)]
+    want = oracle.write_container_fixed(sum(lens), bs, ids, lens, pays, cdc=cdc)
+    got = container.write_container(container.MODE_CDC if cdc else container.MODE_FIXED, bs, sum(lens), ids, lens, pays)
+    assert got == want
+    mode, sz, tot, mids, orig, p2 = container.read_container(got)
+    assert (mode, sz, tot, mids, orig, p2) == (int(cdc), bs, sum(lens), ids, lens, pays)
+
+
+def test_toc_reader_errors():
+    blob = container.write_container(container.MODE_FIXED, 8, 20, [2, 7, 7], [8, 8, 4], [b"ab", b"c", b"def"])
+    for bad, msg in ((b"KOLX" + blob[4:], "Invalid magic"), (blob[:-1], "Truncated payload area"),
+                     (blob + b"\0\0", "Extra trailing 2 bytes"), (blob[:16], "Truncated")):
+        with pytest.raises(ValueError, match=msg):
+            container.read_container(bad)
+    assert kolm.uleb128_decode_stream(b"\x80\x80\x01", 0) == (16384, 3)
+    with pytest.raises(ValueError):
+        kolm.uleb128_decode_stream(b"\x80\x80", 0)
+
+
+def test_bench_stream_fixture_consistent():
+    """tests/golden/bench_stream.json (make_golden_bench.py) describes bench.py's rank-0
+    stream: same input bytes, winners = argmin of the recorded sizes (ties -> lowest id)."""
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bench_stream.json")))["ranks"]["0"]
+    data = D.enwik_like(g["bytes"], seed=g["seed"])
+    assert hashlib.sha256(data).hexdigest() == g["input_sha256"] and g["seed"] == D.ENWIK_SEED
+    for rec in g["blocks"]:
+        s = rec["sizes"]
+        assert rec["w9"] == min(range(9), key=lambda m: (s[m], m))
+        assert rec["w10"] == min(range(10), key=lambda m: (s[m], m))
+        assert s[0] == g["block_size"]
