@@ -181,6 +181,17 @@ int kolm_encode_blocks(const uint8_t* data, const uint64_t* starts, const uint32
                        uint32_t* sizes, uint32_t* method, uint8_t* payload_arena,
                        uint64_t arena_cap, uint64_t* payload_off, kolm_stats* stats);
 
+/* compress_blocks_fixed (PY:2332-2445) in one call on the default context: the host
+ * buffer data[0, n) goes up through a ring of pinned staging chunks (parallel host copies
+ * beside the DMA), every block of block_size bytes is encoded (candidates cand_mask, MDL),
+ * and the KOLR container (header + TOC by kolm_toc_write, then the winners' payloads copied
+ * straight from device memory) is assembled in a pinned host buffer owned by the context:
+ * *out / *out_len describe it until the next call on the default context.  Inputs above
+ * 2^31 bytes run as several device batches.  KOLM_ERANGE when the block count exceeds
+ * 65535 or n >= 2^32 (PY's struct.error). */
+int kolm_compress_fixed(const uint8_t* data, uint64_t n, uint32_t block_size, uint32_t cand_mask,
+                        const uint8_t** out, uint64_t* out_len, kolm_stats* stats);
+
 /* kolm_encode_blocks over ngpu devices (0..ngpu-1, clamped to the device count and the
  * block count) of this process: fixed blocks of block_size over data[0, total), block i
  * of shard r lives on device r, shards are contiguous block ranges.  Outputs exactly as

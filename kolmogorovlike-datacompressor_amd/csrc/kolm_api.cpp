@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -36,6 +37,68 @@ namespace {
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
+};
+
+// Host-side copy workers for the pinned staging buffers: a host buffer of the caller
+// (pageable) is copied into pinned memory by several threads at once, so the DMA engine
+// sees pinned memory and the host side keeps up with PCIe (one thread's memcpy does not).
+class CopyPool {
+  public:
+    explicit CopyPool(unsigned n) {
+        for (unsigned i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    // dst[0, n) = src[0, n), split over the workers and the calling thread
+    void copy(void* dst, const void* src, size_t n) {
+        const size_t parts = th_.size() + 1, piece = ((n + parts - 1) / parts + 4095) & ~(size_t)4095;
+        std::vector<Job> jobs;
+        for (size_t o = piece; o < n; o += piece)
+            jobs.push_back({(char*)dst + o, (const char*)src + o, std::min(piece, n - o)});
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            for (auto& j : jobs) q_.push_back(j);
+            pending_ += jobs.size();
+        }
+        cv_.notify_all();
+        std::memcpy(dst, src, std::min(piece, n));
+        std::unique_lock<std::mutex> g(mu_);
+        done_cv_.wait(g, [this] { return pending_ == 0; });
+    }
+
+  private:
+    struct Job {
+        char* d;
+        const char* s;
+        size_t n;
+    };
+    void loop() {
+        for (;;) {
+            Job j;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+                if (stop_ && q_.empty()) return;
+                j = q_.back();
+                q_.pop_back();
+            }
+            std::memcpy(j.d, j.s, j.n);
+            std::lock_guard<std::mutex> g(mu_);
+            if (--pending_ == 0) done_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::vector<Job> q_;
+    size_t pending_ = 0;
+    bool stop_ = false;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
 };
 
 // counter slots in the device counter array
@@ -85,6 +148,14 @@ struct kolm_ctx {
     hipStream_t active = nullptr;  // stream used by launches / TScope / sync()
     hipStream_t rp = nullptr;      // third stream: Re-Pair (candidate 9), one workgroup per block
     bool serial = false;           // every launch of a batch on one stream (kolm_ctx_set_serial; KOLM_SERIAL=1)
+    // pinned host staging: an upload ring (input chunks) and the result buffer of
+    // kolm_compress_fixed (container bytes, valid until the next call on this context)
+    static constexpr int NSTAGE = 4;
+    u8* stage[NSTAGE] = {};
+    hipEvent_t stage_ev[NSTAGE] = {};
+    u8* h_res = nullptr;
+    size_t h_res_cap = 0;
+    std::unique_ptr<CopyPool> pool;
     hipEvent_t evj[4] = {};        // join events
     hipEvent_t evr[2] = {};        // Re-Pair start / done
     std::mutex mu;
@@ -1038,10 +1109,40 @@ kolm_ctx* need_default() {
     return g_default;
 }
 
-// Upload n host bytes to the context's "text" buffer (+8 bytes of zero padding).
+// Upload n host bytes to the context's "text" buffer (+64 bytes of zero padding).
 u8* upload(kolm_ctx* c, const uint8_t* in, size_t n) {
     u8* d = c->get<u8>("text", n + 64);
     if (n) KOLM_HIP_CHECK(hipMemcpyAsync(d, in, n, hipMemcpyHostToDevice, c->stream));
+    KOLM_HIP_CHECK(hipMemsetAsync(d + n, 0, 64, c->stream));
+    return d;
+}
+
+constexpr size_t STAGE_BYTES = 32u << 20;
+
+CopyPool& copy_pool(kolm_ctx* c) {
+    if (!c->pool) c->pool.reset(new CopyPool(std::max(1u, std::min(8u, std::thread::hardware_concurrency()) - 1)));
+    return *c->pool;
+}
+
+// The same upload from pageable memory through a ring of pinned chunks: the copy workers
+// fill chunk k + 1 while the DMA engine moves chunk k (hipMemcpy from pageable memory
+// stages through the runtime's own buffers at about half the PCIe rate).
+u8* upload_staged(kolm_ctx* c, const uint8_t* in, size_t n) {
+    u8* d = c->get<u8>("text", n + 64);
+    CopyPool& pool = copy_pool(c);
+    for (size_t o = 0, k = 0; o < n; o += STAGE_BYTES, ++k) {
+        const int j = (int)(k % kolm_ctx::NSTAGE);
+        if (!c->stage[j]) {
+            KOLM_HIP_CHECK(hipHostMalloc((void**)&c->stage[j], STAGE_BYTES, hipHostMallocDefault));
+            KOLM_HIP_CHECK(hipEventCreateWithFlags(&c->stage_ev[j], hipEventDisableTiming));
+        } else if (k >= kolm_ctx::NSTAGE) {
+            KOLM_HIP_CHECK(hipEventSynchronize(c->stage_ev[j]));  // its previous chunk has left
+        }
+        const size_t len = std::min(STAGE_BYTES, n - o);
+        pool.copy(c->stage[j], in + o, len);
+        KOLM_HIP_CHECK(hipMemcpyAsync(d + o, c->stage[j], len, hipMemcpyHostToDevice, c->stream));
+        KOLM_HIP_CHECK(hipEventRecord(c->stage_ev[j], c->stream));
+    }
     KOLM_HIP_CHECK(hipMemsetAsync(d + n, 0, 64, c->stream));
     return d;
 }
@@ -1079,6 +1180,11 @@ int kolm_ctx_destroy(kolm_ctx* c) {
         for (auto& e : c->evr) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evpool) KOLM_HIP_CHECK(hipEventDestroy(e));
         KOLM_HIP_CHECK(hipHostFree(c->h_cnt));
+        for (int i = 0; i < kolm_ctx::NSTAGE; ++i) {
+            if (c->stage[i]) KOLM_HIP_CHECK(hipHostFree(c->stage[i]));
+            if (c->stage_ev[i]) KOLM_HIP_CHECK(hipEventDestroy(c->stage_ev[i]));
+        }
+        if (c->h_res) KOLM_HIP_CHECK(hipHostFree(c->h_res));
         KOLM_HIP_CHECK(hipStreamDestroy(c->stream));
         KOLM_HIP_CHECK(hipStreamDestroy(c->aux));
         KOLM_HIP_CHECK(hipStreamDestroy(c->rp));
@@ -1272,6 +1378,85 @@ int kolm_encode_blocks(const uint8_t* data, const uint64_t* starts, const uint32
             c->sync();
         }
         std::memcpy(payload_off, off.data(), sizeof(u64) * (nblocks + 1));
+        return KOLM_OK;
+    });
+}
+
+int kolm_compress_fixed(const uint8_t* data, uint64_t n, uint32_t block_size, uint32_t cand_mask,
+                        const uint8_t** out, uint64_t* out_len, kolm_stats* stats) {
+    kolm_ctx* c = need_default();
+    if (!c) return KOLM_ENOINIT;
+    if ((!data && n) || !out || !out_len || block_size == 0 || block_size > 0x7FFFFFFFu) return KOLM_EARG;
+    if ((cand_mask & KOLM_FULL_MASK) == 0) return KOLM_EARG;
+    const u64 nb = (n + block_size - 1) / block_size;
+    if (nb > 0xFFFFu || n > 0xFFFFFFFFull) {  // PY: struct.pack('<H' / '<I') raises
+        set_err(nb > 0xFFFFu ? "'H' format requires 0 <= number <= 65535"
+                             : "'I' format requires 0 <= number <= 4294967295");
+        return KOLM_ERANGE;
+    }
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        std::vector<u32> method(nb), lens(nb);
+        std::vector<u64> plen(nb), off(nb + 1, 0);
+        for (u64 b = 0; b < nb; ++b) lens[b] = (u32)std::min<u64>(block_size, n - b * block_size);
+        // batches of whole blocks below the 2^31-position limit of one encode batch; the
+        // payloads of every batch land in one device arena, back to back
+        const u64 per = std::max<u64>(1, ((1ull << 31) - 1) / block_size);
+        const bool has_raw = (cand_mask & 1u) != 0;
+        const u64 acap = (has_raw ? n : 9 * n) + 64 * nb + 256;
+        u8* arena = c->get<u8>("arena_c", acap);
+        u64 pos = 0;
+        kolm_stats agg{};
+        for (u64 b0 = 0; b0 < nb; b0 += per) {
+            const u64 k = std::min(per, nb - b0);
+            const u64 lo = b0 * block_size, len = std::min<u64>(n, (b0 + k) * block_size) - lo;
+            if (int e = check_geom(len, block_size)) return e;
+            u8* d = upload_staged(c, data + lo, len);
+            std::vector<u64> o(k + 1);
+            kolm_stats st{};
+            int r = encode_batch(c, d, len, block_size, nullptr, 0, cand_mask & KOLM_FULL_MASK, nullptr, arena + pos,
+                                 acap - pos, nullptr, method.data() + b0, o.data(), &st);
+            if (r) return r;
+            for (u64 i = 0; i < k; ++i) plen[b0 + i] = o[i + 1] - o[i];
+            pos += o[k];
+            pos = (pos + 3) & ~(u64)3;  // the next batch's arena is 4-byte aligned
+            if (b0 == 0) agg = st;
+        }
+        // the container: header + TOC (kolm_toc.cpp), then the payloads straight from the
+        // device arena into the pinned result buffer (batch padding skipped)
+        u64 toc_len = 0;
+        if (int e = kolm_toc_write(0, block_size, n, (u32)nb, method.data(), lens.data(), plen.data(), nullptr, 0,
+                                   &toc_len))
+            return e;
+        u64 total_pay = 0;
+        for (u64 b = 0; b < nb; ++b) total_pay += plen[b];
+        const size_t need = toc_len + total_pay;
+        if (c->h_res_cap < need) {
+            if (c->h_res) KOLM_HIP_CHECK(hipHostFree(c->h_res));
+            c->h_res = nullptr;
+            c->h_res_cap = 0;
+            KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_res, need + (need >> 3) + 4096, hipHostMallocDefault));
+            c->h_res_cap = need + (need >> 3) + 4096;
+        }
+        if (int e = kolm_toc_write(0, block_size, n, (u32)nb, method.data(), lens.data(), plen.data(), c->h_res,
+                                   c->h_res_cap, &toc_len))
+            return e;
+        // one copy per batch (its payloads are contiguous in the arena)
+        u64 src = 0, dst = toc_len;
+        for (u64 b0 = 0; b0 < nb; b0 += per) {
+            const u64 k = std::min(per, nb - b0);
+            u64 bytes = 0;
+            for (u64 i = 0; i < k; ++i) bytes += plen[b0 + i];
+            if (bytes)
+                KOLM_HIP_CHECK(hipMemcpyAsync(c->h_res + dst, arena + src, bytes, hipMemcpyDeviceToHost, c->stream));
+            dst += bytes;
+            src = (src + bytes + 3) & ~(u64)3;
+        }
+        KOLM_HIP_CHECK(hipStreamSynchronize(c->stream));
+        *out = c->h_res;
+        *out_len = need;
+        if (stats) *stats = agg;
         return KOLM_OK;
     });
 }

@@ -275,12 +275,20 @@ def compress_blocks_fixed(data: bytes, block_size: int = 8192, devices: int = 1,
     G_V2_NEW) adds candidate 10 (see the module docstring)."""
     if block_size <= 0:
         raise ValueError("block_size must be positive")
+    global _last_stats
     n = len(data)
     nb = (n + block_size - 1) // block_size
     if nb > 0xFFFF:
         raise struct.error("'H' format requires 0 <= number <= 65535")
-    mids, orig, payloads, _ = encode_blocks(data, block_size, devices=devices, hot_path=hot_path, v2_new=v2_new)
-    return write_container(MODE_FIXED, block_size, n, mids, orig, payloads)
+    if devices > 1:
+        mids, orig, payloads, _ = encode_blocks(data, block_size, devices=devices, hot_path=hot_path, v2_new=v2_new)
+        return write_container(MODE_FIXED, block_size, n, mids, orig, payloads)
+    if n == 0:
+        return write_container(MODE_FIXED, block_size, 0, [], [], [])
+    # one native call: staged upload, batched encode, TOC, payloads into the container
+    blob, st = _lib.compress_fixed(data, block_size, candidate_mask(hot_path, v2_new))
+    _last_stats = st
+    return blob
 
 
 def compress_blocks_cdc(data: bytes, min_size: int = 4096, avg_size: int = 8192, max_size: int = 16384,

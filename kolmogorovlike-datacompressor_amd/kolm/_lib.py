@@ -118,6 +118,7 @@ SIGNATURES = [
     ("kolm_cdc_boundaries_device", I32, [P, P, U64, U32, U32, U32, I32, P, U64, ctypes.POINTER(U64)]),
     ("kolm_decode_blocks", I32, [P, P, P, P, U32, P, U64]),
     ("kolm_decode_blocks_device", I32, [P, P, P, P, P, U32, P, U64, ctypes.POINTER(ctypes.c_double)]),
+    ("kolm_compress_fixed", I32, [P, U64, U32, U32, ctypes.POINTER(P), ctypes.POINTER(U64), P]),
     ("kolm_toc_write", I32, [I32, U32, U64, U32, P, P, P, P, U64, ctypes.POINTER(U64)]),
     ("kolm_toc_read", I32, [U8P, U64, P, ctypes.POINTER(U64), P, P, P, U32]),
 ]
@@ -276,6 +277,23 @@ def encode_blocks(data: bytes, block_size: int, cand_mask: int = KOLM_DEFAULT_MA
         ctypes.byref(st)))
     payloads = [arena[int(off[i]):int(off[i + 1])].tobytes() for i in range(nb)]
     return sizes[:nb], method[:nb], payloads, st.as_dict()
+
+
+def compress_fixed(data, block_size: int, cand_mask: int = KOLM_DEFAULT_MASK):
+    """The whole KOLR container of data in fixed blocks (kolm_compress_fixed): (bytes, stats)."""
+    ensure_init()
+    n = len(data)
+    src = np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8) if n else np.zeros(1, np.uint8)
+    out = ctypes.c_void_p()
+    ln = ctypes.c_uint64(0)
+    st = Stats()
+    rc = load().kolm_compress_fixed(src.ctypes.data, n, block_size, cand_mask, ctypes.byref(out), ctypes.byref(ln),
+                                    ctypes.byref(st))
+    if rc == KOLM_ERANGE:
+        import struct
+        raise struct.error(load().kolm_last_error().decode())
+    check(rc)
+    return ctypes.string_at(out.value, ln.value), st.as_dict()
 
 
 def encode_blocks_var(data: bytes, bounds, cand_mask: int = KOLM_DEFAULT_MASK, force=None):
