@@ -338,24 +338,49 @@ __global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8*
     __syncthreads();
     dprof(prof, 0, tlast);
     // Duval on the thread's chunk; factor starts -> bitmap (bits of one chunk are 4 words
-    // owned by this thread only)
+    // owned by this thread only).  One flat loop: every trip advances the lane's own state
+    // machine by exactly one step — a comparison (scan phase) or one factor emitted (emit
+    // phase) — so the lanes of a wave stay in step instead of serialising the nested
+    // loops' data-dependent trip counts.
     {
         const u32 clo = tid * DUVAL_CH, chi = min(clo + DUVAL_CH, n);
-        u32 i = clo;
+        u32 i = clo, j = clo + 1, kk = clo, p = 1;
+        bool emit = false;
+        u32 w0 = 0, w1 = 0, w2 = 0, w3 = 0;  // the chunk's 128 start bits
+        static_assert(DUVAL_CH == 128, "four bitmap words per chunk");
         while (i < chi) {
-            u32 j = i + 1, kk = i;
-            while (j < chi) {
-                const u8 a = t[lds_addr(kk)], bb = t[lds_addr(j)];
-                if (a > bb) break;
-                kk = (a < bb) ? i : kk + 1;
-                ++j;
-            }
-            const u32 p = j - kk;
-            while (i <= kk) {
-                bm[i >> 5] |= 1u << (i & 31);
+            if (!emit) {
+                bool stop = j >= chi;
+                if (!stop) {
+                    const u8 a = t[lds_addr(kk)], bb = t[lds_addr(j)];
+                    stop = a > bb;
+                    if (!stop) {
+                        kk = (a < bb) ? i : kk + 1;
+                        ++j;
+                    }
+                }
+                if (stop) {
+                    emit = true;
+                    p = j - kk;
+                }
+            } else {
+                const u32 li = i - clo, bit = 1u << (li & 31), wq = li >> 5;
+                w0 |= wq == 0 ? bit : 0u;
+                w1 |= wq == 1 ? bit : 0u;
+                w2 |= wq == 2 ? bit : 0u;
+                w3 |= wq == 3 ? bit : 0u;
                 i += p;
+                if (i > kk) {  // the run of equal factors is out: scan from the next start
+                    emit = false;
+                    kk = i;
+                    j = i + 1;
+                }
             }
         }
+        bm[clo / 32] = w0;
+        bm[clo / 32 + 1] = w1;
+        bm[clo / 32 + 2] = w2;
+        bm[clo / 32 + 3] = w3;
     }
     __syncthreads();
     dprof(prof, 1, tlast);

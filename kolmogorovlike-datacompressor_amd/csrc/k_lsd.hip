@@ -61,6 +61,25 @@ __device__ inline void load16(const u32* X, u32 i0, u32 hi, u32 (&v)[LSD_PT]) {
     }
 }
 
+// the same with non-temporal loads (streamed through, not kept in L2)
+__device__ inline void load16nt(const u32* X, u32 i0, u32 hi, u32 (&v)[LSD_PT]) {
+    if ((i0 & 3) == 0 && i0 + LSD_PT <= hi) {
+        typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4* p = reinterpret_cast<const u32x4*>(X + i0);
+#pragma unroll
+        for (int q = 0; q < (int)LSD_PT / 4; ++q) {
+            const u32x4 t = __builtin_nontemporal_load(p + q);
+            v[4 * q] = t.x;
+            v[4 * q + 1] = t.y;
+            v[4 * q + 2] = t.z;
+            v[4 * q + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (u32 e = 0; e < LSD_PT; ++e) v[e] = i0 + e < hi ? __builtin_nontemporal_load(X + i0 + e) : 0u;
+    }
+}
+
 // where a pass reads its (key, position) pairs: keys by position (first pass) or pairs
 enum Src { SRC_KP = 1, SRC_PAIR = 2 };
 
@@ -304,6 +323,8 @@ __global__ __launch_bounds__(WG) void k_tiles_max_scan(const u32* in, u32* out, 
 // round; a block with more than one group has split.
 // ---------------------------------------------------------------------------------
 constexpr u32 BIG = 0xFFFFFFFFu;
+constexpr u32 R0_WS = 12;             // position windows of the RK write (k_r0_rk below)
+constexpr u32 R0_WIN = 1u << R0_WS;
 
 __device__ inline u32 wave_min(u32 v) { return wave_reduce(v, OpMinU(), BIG); }
 
@@ -312,9 +333,16 @@ __device__ inline u32 wave_min(u32 v) { return wave_reduce(v, OpMinU(), BIG); }
 // 8-character round 0, K = characters 0..3 — also when characters 4..7, KA[SA[slot]],
 // differ).  tmax / tmin = the tile's last / first head.
 __global__ __launch_bounds__(WG) void k_r0_tile_heads(LsdGeom g, const u32* K, const u32* SA, const u32* KA, u32* HF,
-                                                      u32* tmax, u32* tmin) {
+                                                      u32* tmax, u32* tmin, u32* BH) {
     __shared__ u32 s1[WG / 64], s2[WG / 64];
+    __shared__ u32 bh[WG / 64][256];  // BH: per wave, slots of this tile per position window
     const u32 t = xcd_tile();
+    const u32 w = threadIdx.x >> 6;
+    if (BH) {
+#pragma unroll
+        for (int i = 0; i < WG / 64; ++i) bh[i][threadIdx.x] = 0;
+        __syncthreads();
+    }
     u32 lo, hi, b;
     u32 mx = 0, mn = BIG;
     if (g.range(t, lo, hi, b)) {
@@ -325,9 +353,14 @@ __global__ __launch_bounds__(WG) void k_r0_tile_heads(LsdGeom g, const u32* K, c
             u32 kv[LSD_PT], av[LSD_PT];
             load16(K, i0, hi, kv);
             u32 kprev = i0 > base ? K[i0 - 1] : 0u, aprev = 0;
+            u32 sv[LSD_PT];
+            if (BH || KA) load16(SA, i0, hi, sv);
+            if (BH) {
+#pragma unroll
+                for (u32 e = 0; e < LSD_PT; ++e)
+                    if (i0 + e < hi) atomicAdd(&bh[w][(sv[e] - base) >> R0_WS], 1u);
+            }
             if (KA) {
-                u32 sv[LSD_PT];
-                load16(SA, i0, hi, sv);
 #pragma unroll
                 for (u32 e = 0; e < LSD_PT; ++e) av[e] = i0 + e < hi ? KA[sv[e]] : 0u;
                 aprev = i0 > base ? KA[SA[i0 - 1]] : 0u;
@@ -349,6 +382,10 @@ __global__ __launch_bounds__(WG) void k_r0_tile_heads(LsdGeom g, const u32* K, c
         }
         HF[(u64)t * WG + threadIdx.x] = hm;
     }
+    if (BH) {
+        __syncthreads();
+        BH[(u64)t * 256 + threadIdx.x] = bh[0][threadIdx.x] + bh[1][threadIdx.x] + bh[2][threadIdx.x] + bh[3][threadIdx.x];
+    }
     mx = wave_max(mx);
     mn = wave_min(mn);
     if ((threadIdx.x & 63) == 0) {
@@ -362,6 +399,15 @@ __global__ __launch_bounds__(WG) void k_r0_tile_heads(LsdGeom g, const u32* K, c
     }
 }
 
+// RK without a random scatter (blocks of at most 1 MiB = 256 windows of 2^R0_WS
+// positions): k_r0_tile_heads counts every tile's slots per position window (BH),
+// k_lsd_scan turns the counts into each (tile, window)'s place in the window-major pair
+// array, the final pass stages its tile's pairs (position in the window << 20 | rank in
+// the block) grouped by window in LDS and writes every window's run with consecutive
+// lanes, and k_r0_rk assembles each window's 16 KB of RK in LDS and writes it with
+// whole-line stores.  Every global store is then part of a coalesced wave store: stores
+// that meet a line only across instructions are not merged well (PMC, 256 MiB: the direct
+// 4-byte scatter wrote 8.4x the RK bytes, unstaged pair runs of ~16 entries 2.7x).
 // per block: exclusive suffix min over its tiles (one workgroup per block)
 __global__ __launch_bounds__(WG) void k_r0_tiles_rscan(const u32* in, u32* out, u32 tpb) {
     __shared__ u32 sh[WG / 64];
@@ -390,21 +436,34 @@ __global__ __launch_bounds__(WG) void k_r0_tiles_rscan(const u32* in, u32* out, 
 // over disjoint position windows keep one XCD's concurrent scatters inside a part of the
 // block's RK that its L2 holds, so partial lines combine before write-back); `segs`: this
 // launch also writes the next-round segments and split flags; `xcd`: XCD-contiguous tiles.
+// PP (null: scatter RK directly): the window-major packed pair array; BH its offsets
 __global__ __launch_bounds__(WG) void k_r0_final(LsdGeom g, const u32* HF, const u32* SA, const u32* cmax,
                                                  const u32* cmin, u32* RK, Seg* next, u32* next_cnt,
-                                                 u32* blk_split, u32 plo, u32 phi, u32 segs, u32 xcd) {
-    __shared__ u32 sh[WG / 64], sh2[WG / 64], sh3[WG / 64];
+                                                 u32* blk_split, u32 plo, u32 phi, u32 segs, u32 xcd, u32 nt,
+                                                 const u32* BH, u32* PP) {
+    __shared__ u32 sh[WG / 64], sh2[WG / 64], sh3[WG / 64], sh4[WG / 64];
     __shared__ u32 wbase, anysplit;
+    __shared__ u32 wo[256];     // PP: per window, where this tile's pairs go in PP
+    __shared__ u32 wc[256];     // PP: per window, this tile's pair count, then its staging offset
+    __shared__ u32 stg[LSD_T];  // PP: the tile's pairs grouped by window
+    __shared__ u8 sbin[LSD_T];  // PP: window of each staged pair
     u32 lo, hi, b;
     const u32 t = xcd ? xcd_tile() : blockIdx.x;
     if (!g.range(t, lo, hi, b)) return;
     const u32 base = g.geo.base(b), bend = g.geo.end(b);
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid == 0) anysplit = 0;
+    if (PP) {
+        wo[tid] = BH[(u64)t * 256 + tid];
+        wc[tid] = 0;
+    }
     const u32 i0 = lo + tid * LSD_PT;
     u32 sv[LSD_PT];
-    load16(SA, i0, hi, sv);
-    const u32 hm = HF[(u64)t * WG + tid];
+    if (nt)  // SA / HF streamed past L2, which keeps the RK lines being filled
+        load16nt(SA, i0, hi, sv);
+    else
+        load16(SA, i0, hi, sv);
+    const u32 hm = nt ? __builtin_nontemporal_load(HF + (u64)t * WG + tid) : HF[(u64)t * WG + tid];
     bool hd[LSD_PT];
     u32 lmax = 0, lmin = BIG;
 #pragma unroll
@@ -430,15 +489,44 @@ __global__ __launch_bounds__(WG) void k_r0_final(LsdGeom g, const u32* HF, const
     if (nh == BIG) nh = bend;
     // ranks
     bool split = false;
+    u32 pk[LSD_PT], loc[LSD_PT];
 #pragma unroll
     for (u32 e = 0; e < LSD_PT; ++e) {
         const u32 i = i0 + e;
+        pk[e] = loc[e] = 0;
         if (i < hi) {
             if (hd[e]) {
                 run = i;
                 split |= i != base;
             }
-            if (sv[e] - base - plo < phi - plo) RK[sv[e]] = run;
+            if (PP) {  // the window counts are ready: barrier above
+                pk[e] = ((sv[e] - base) & (R0_WIN - 1)) << 20 | (run - base);
+                loc[e] = atomicAdd(&wc[(sv[e] - base) >> R0_WS], 1u);
+            } else if (sv[e] - base - plo < phi - plo) {
+                RK[sv[e]] = run;
+            }
+        }
+    }
+    if (PP) {
+        __syncthreads();
+        const u32 c = wc[tid], inc = wave_incl_scan(c, OpAddU(), 0u);
+        if (lane == 63) sh4[w] = inc;
+        __syncthreads();
+        u32 so = inc - c;
+        for (u32 q = 0; q < w; ++q) so += sh4[q];
+        wc[tid] = so;
+        __syncthreads();
+#pragma unroll
+        for (u32 e = 0; e < LSD_PT; ++e)
+            if (i0 + e < hi) {
+                const u32 k = (sv[e] - base) >> R0_WS, q = wc[k] + loc[e];
+                stg[q] = pk[e];
+                sbin[q] = (u8)k;
+            }
+        __syncthreads();
+        for (u32 q = tid; q < hi - lo; q += WG) {
+            const u32 k = sbin[q];
+            PP[wo[k] + q - wc[k]] = stg[q];
         }
     }
     if (!segs) return;
@@ -471,6 +559,28 @@ __global__ __launch_bounds__(WG) void k_r0_final(LsdGeom g, const u32* HF, const
 #pragma unroll
     for (u32 e = 0; e < LSD_PT; ++e)
         if (len[e] >= 2) next[off++] = Seg{i0 + e, len[e]};
+}
+
+// RK of one position window from its pairs (exactly the window's positions), through LDS
+__global__ __launch_bounds__(WG) void k_r0_rk(Geom geo, u32 nwin, const u32* PP, u32* RK) {
+    __shared__ u32 win[R0_WIN];
+    const u32 b = blockIdx.x / nwin, k = blockIdx.x - b * nwin;
+    const u32 base = geo.base(b), e = geo.end(b);
+    const u32 lo = base + k * R0_WIN;
+    if (lo >= e) return;
+    const u32 n = min(R0_WIN, e - lo);
+    for (u32 d = threadIdx.x; d < n; d += WG) {
+        const u32 v = PP[lo + d];
+        win[v >> 20] = base + (v & 0xFFFFFu);
+    }
+    __syncthreads();
+    if ((lo & 3) == 0 && (n & 1023) == 0) {
+        uint4* dst = reinterpret_cast<uint4*>(RK + lo);
+        const uint4* src = reinterpret_cast<const uint4*>(win);
+        for (u32 i = threadIdx.x; i < n / 4; i += WG) dst[i] = src[i];
+    } else {
+        for (u32 i = threadIdx.x; i < n; i += WG) RK[lo + i] = win[i];
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -705,12 +815,32 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
         run_pass((int)q, false, false, g, nt, K[o ^ 1], S[o ^ 1], K[o], S[o], nullptr, t.hist, s, kt);
         o ^= 1;
     }
+    // RK through position windows (k_r0_rk) when every block has at most 256 of them;
+    // KOLM_R0F_WIN=0: the direct scatter
+    static const bool win_ok = !(getenv("KOLM_R0F_WIN") && atoi(getenv("KOLM_R0F_WIN")) == 0);
+    const bool win = win_ok && geo.bs <= 256 * R0_WIN;
     {
         // K 4 (+ SA 4 + the KA gather 4) read, head masks written
-        KScope k(kt, KT_LSD, "k_r0_tile_heads", (pb ? 12 : 4) * N);
-        k_r0_tile_heads<<<nt, WG, 0, s>>>(g, t.K2, t.SA, pb ? t.RK : nullptr, t.HF, t.tmax, t.tmin);
+        KScope k(kt, KT_LSD, "k_r0_tile_heads", (pb || win ? 12 : 4) * N);
+        k_r0_tile_heads<<<nt, WG, 0, s>>>(g, t.K2, t.SA, pb ? t.RK : nullptr, t.HF, t.tmax, t.tmin,
+                                          win ? t.hist : nullptr);
         k_tiles_max_scan<<<geo.nb, WG, 0, s>>>(t.tmax, t.cmax, g.tpb);
         k_r0_tiles_rscan<<<geo.nb, WG, 0, s>>>(t.tmin, t.cmin, g.tpb);
+    }
+    if (win) {
+        const u32 nwin = (geo.bs + R0_WIN - 1) / R0_WIN;
+        k_lsd_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);  // window counts -> pair offsets
+        {
+            // SA 4 read, pairs 4 written (+ head masks, 8 B per new segment)
+            KScope k(kt, KT_LSD, "k_r0_final", 8 * N);
+            k_r0_final<<<nt, WG, 0, s>>>(g, t.HF, t.SA, t.cmax, t.cmin, t.RK, next, next_cnt, blk_split, 0, 0, 1, 1, 0,
+                                         t.hist, t.K22);
+        }
+        {
+            KScope k(kt, KT_LSD, "k_r0_rk", 8 * N);  // pairs 4 read, RK 4 written
+            k_r0_rk<<<nwin * geo.nb, WG, 0, s>>>(geo, nwin, t.K22, t.RK);
+        }
+        return;
     }
     {
         // SA 4 read, RK 4 scattered (+ head masks, 8 B per new segment)
@@ -719,10 +849,12 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
         // (default: two windows on XCD-contiguous tiles, 256 MiB text 3.24 -> 2.42 ms per step)
         static const u32 parts = getenv("KOLM_R0F_PARTS") ? std::max(1, atoi(getenv("KOLM_R0F_PARTS"))) : 2u;
         static const u32 xcd = getenv("KOLM_R0F_XCD") ? (u32)atoi(getenv("KOLM_R0F_XCD")) : 1u;
+        static const u32 ntl = getenv("KOLM_R0F_NT") ? (u32)atoi(getenv("KOLM_R0F_NT")) : 0u;
         const u32 step = (geo.bs + parts - 1) / parts;
         for (u32 q = 0; q < parts; ++q)
             k_r0_final<<<nt, WG, 0, s>>>(g, t.HF, t.SA, t.cmax, t.cmin, t.RK, next, next_cnt, blk_split, q * step,
-                                         q + 1 == parts ? 0xFFFFFFFFu : (q + 1) * step, q == 0, xcd);
+                                         q + 1 == parts ? 0xFFFFFFFFu : (q + 1) * step, q == 0, xcd, ntl, nullptr,
+                                         nullptr);
     }
 }
 

@@ -1,8 +1,11 @@
 """Multi-GPU block sharding + container reassembly (one process per GPU).
 
 Blocks are independent (PY:2350-2369: no state crosses blocks), so a batch shards with
-no data-path collective: rank r encodes the contiguous block range
-``shard_blocks(nblocks, r, world)``.  The only exchange step is reassembling the output
+no data-path collective: rank r encodes the blocks ``rank_blocks(nblocks, r, world,
+partition)`` — by default the contiguous range ``shard_blocks(nblocks, r, world)`` (a
+rank's blocks are one contiguous slice of the input: one upload, and rank order is
+container order), or ``partition="round_robin"`` (block i on rank i mod world, BASELINE
+config 4's assignment; for equal blocks both give every rank the same work).  The only exchange step is reassembling the output
 stream on the destination rank: a tiny all-gather of per-rank (nblocks, payload bytes),
 then a gather of the per-rank payload arenas (padded to the largest) and of the method
 ids.  With the ``nccl`` backend (RCCL over xGMI on MI355X) the tensors live in HBM; with
@@ -23,6 +26,21 @@ def shard_blocks(nblocks: int, rank: int, world: int) -> Tuple[int, int]:
     base, extra = divmod(nblocks, world)
     first = rank * base + min(rank, extra)
     return first, base + (1 if rank < extra else 0)
+
+
+PARTITIONS = ("contiguous", "round_robin")
+
+
+def rank_blocks(nblocks: int, rank: int, world: int, partition: str = "contiguous") -> range:
+    """Global block indices encoded by `rank`, in container order."""
+    if partition == "contiguous":
+        first, count = shard_blocks(nblocks, rank, world)
+        return range(first, first + count)
+    if partition == "round_robin":
+        if world <= 0 or not 0 <= rank < world:
+            raise ValueError("bad rank/world")
+        return range(rank, nblocks, world)
+    raise ValueError(f"partition must be one of {PARTITIONS}")
 
 
 class PendingGather:
@@ -91,24 +109,31 @@ def gather_payloads(arena, nbytes: int, method_ids, dst: int = 0, group=None, as
 
 
 def assemble_container(block_size: int, total_len: int, per_rank_ids: Sequence[Sequence[int]],
-                       per_rank_payloads: Sequence[bytes], per_rank_offsets: Sequence[Sequence[int]]) -> bytes:
-    """Host TOC + payloads in global block order (contiguous shards -> rank order)."""
+                       per_rank_payloads: Sequence[bytes], per_rank_offsets: Sequence[Sequence[int]],
+                       partition: str = "contiguous") -> bytes:
+    """Host TOC + payloads in global block order (each rank's blocks: rank_blocks)."""
     from .container import MODE_FIXED, write_container
-    mids: List[int] = []
-    pays: List[bytes] = []
-    for ids, buf, off in zip(per_rank_ids, per_rank_payloads, per_rank_offsets):
-        mids.extend(int(x) for x in ids)
-        pays.extend(bytes(buf[int(off[i]):int(off[i + 1])]) for i in range(len(ids)))
-    nb = len(mids)
+    world = len(per_rank_ids)
+    nb = sum(len(ids) for ids in per_rank_ids)
+    mids: List[int] = [0] * nb
+    pays: List[bytes] = [b""] * nb
+    for r, (ids, buf, off) in enumerate(zip(per_rank_ids, per_rank_payloads, per_rank_offsets)):
+        blocks = rank_blocks(nb, r, world, partition)
+        if len(blocks) != len(ids):
+            raise ValueError("per-rank block counts do not match the partition")
+        for i, g in enumerate(blocks):
+            mids[g] = int(ids[i])
+            pays[g] = bytes(buf[int(off[i]):int(off[i + 1])])
     orig = [min(block_size, total_len - i * block_size) for i in range(nb)]
     return write_container(MODE_FIXED, block_size, total_len, mids, orig, pays)
 
 
 def compress_blocks_fixed_distributed(data: bytes, block_size: int, dst: int = 0, group=None,
-                                      cand_mask: Optional[int] = None) -> Optional[bytes]:
-    """Every rank calls this with the same `data`; rank r encodes its shard on its GPU,
-    payloads + ids are gathered to `dst` over the process group, `dst` returns the
-    container (others return None).  Bit-identical to compress_blocks_fixed(data)."""
+                                      cand_mask: Optional[int] = None, partition: str = "contiguous") -> Optional[bytes]:
+    """Every rank calls this with the same `data`; rank r encodes its blocks
+    (rank_blocks(.., partition)) on its GPU, payloads + ids are gathered to `dst` over the
+    process group, `dst` returns the container (others return None).  Bit-identical to
+    compress_blocks_fixed(data) for either partition."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -117,9 +142,11 @@ def compress_blocks_fixed_distributed(data: bytes, block_size: int, dst: int = 0
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     n = len(data)
     nb = (n + block_size - 1) // block_size
-    first, count = shard_blocks(nb, rank, world)
-    lo, hi = first * block_size, min(n, (first + count) * block_size)
-    mids, orig, payloads, _ = encode_blocks(data[lo:hi], block_size, cand_mask) if count else ([], [], [], None)
+    mine = rank_blocks(nb, rank, world, partition)
+    # the rank's blocks back to back: equal blocks, the input's short tail (if it is this
+    # rank's) last, so they form one fixed-size batch
+    part = b"".join(data[i * block_size:(i + 1) * block_size] for i in mine)
+    mids, orig, payloads, _ = encode_blocks(part, block_size, cand_mask) if len(mine) else ([], [], [], None)
     blob = b"".join(payloads)
     offs = np.concatenate([[0], np.cumsum([len(p) for p in payloads])]).astype(np.int64)
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
@@ -136,4 +163,4 @@ def compress_blocks_fixed_distributed(data: bytes, block_size: int, dst: int = 0
     if rank != dst:
         return None
     return assemble_container(block_size, n, [i.cpu().tolist() for i in idl],
-                              [p.cpu().numpy().tobytes() for p in pays], all_offs)
+                              [p.cpu().numpy().tobytes() for p in pays], all_offs, partition)

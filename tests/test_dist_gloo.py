@@ -21,20 +21,19 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, data, bs, q, use_async=False):
+def _worker(rank, world, port, data, bs, q, use_async=False, partition="contiguous"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
     sys.path[:0] = [os.path.join(repo, "kolmogorovlike-datacompressor_amd"), os.path.join(repo, "oracle")]
     import oracle as O
-    from kolm.parallel import assemble_container, gather_payloads, shard_blocks
+    from kolm.parallel import assemble_container, gather_payloads, rank_blocks
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         nb = (len(data) + bs - 1) // bs
-        first, count = shard_blocks(nb, rank, world)
         mids, pays = [], []
-        for i in range(first, first + count):
+        for i in rank_blocks(nb, rank, world, partition):
             blk = data[i * bs:(i + 1) * bs]
             cands = [O.candidate(m, blk) for m in range(10)]
             m = int(np.argmin([len(c) for c in cands]))
@@ -56,7 +55,7 @@ def _worker(rank, world, port, data, bs, q, use_async=False):
         dist.all_gather_object(all_offs, offs)
         if rank == 0:
             c = assemble_container(bs, len(data), [i.tolist() for i in got_i],
-                                   [p.numpy().tobytes() for p in got_p], all_offs)
+                                   [p.numpy().tobytes() for p in got_p], all_offs, partition)
             q.put(c)
         else:
             assert got_p is None and got_i is None
@@ -64,16 +63,19 @@ def _worker(rank, world, port, data, bs, q, use_async=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,bs,n,use_async", [(2, 4096, 4096 * 5 + 123, False), (2, 1000, 999, False),
-                                                 (3, 2048, 2048 * 4, False), (2, 4096, 4096 * 3 + 7, True)])
-def test_gloo_sharded_reassembly(world, bs, n, use_async):
+@pytest.mark.parametrize("world,bs,n,use_async,partition", [
+    (2, 4096, 4096 * 5 + 123, False, "contiguous"), (2, 1000, 999, False, "contiguous"),
+    (3, 2048, 2048 * 4, False, "contiguous"), (2, 4096, 4096 * 3 + 7, True, "contiguous"),
+    (2, 4096, 4096 * 5 + 123, False, "round_robin"), (3, 2048, 2048 * 7 + 5, True, "round_robin")])
+def test_gloo_sharded_reassembly(world, bs, n, use_async, partition):
     import oracle as O
     from kolm import datagen as D
     data = (D.enwik_like(n // 2, seed=5) + bytes(n // 4) + D.splitmix64_bytes(n, seed=9))[:n]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, data, bs, q, use_async)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, data, bs, q, use_async, partition))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)

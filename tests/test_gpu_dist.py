@@ -18,7 +18,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, data, bs, q):
+def _worker(rank, world, port, data, bs, q, partition):
     import sys
     import torch  # noqa: F401  (first: shared HIP runtime)
     import torch.distributed as dist
@@ -28,7 +28,7 @@ def _worker(rank, world, port, data, bs, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out = compress_blocks_fixed_distributed(data, bs)
+        out = compress_blocks_fixed_distributed(data, bs, partition=partition)
         if rank == 0:
             q.put(out)
         else:
@@ -37,7 +37,8 @@ def _worker(rank, world, port, data, bs, q):
         dist.destroy_process_group()
 
 
-def test_distributed_gpu_encode_matches_single():
+@pytest.mark.parametrize("partition", ["contiguous", "round_robin"])
+def test_distributed_gpu_encode_matches_single(partition):
     import oracle as O
     from kolm import datagen as D
     bs = 65536
@@ -45,7 +46,7 @@ def test_distributed_gpu_encode_matches_single():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, data, bs, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, data, bs, q, partition)) for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=300)

@@ -202,3 +202,12 @@ def test_bench_stream_fixture_consistent():
         assert rec["w9"] == min(range(9), key=lambda m: (s[m], m))
         assert rec["w10"] == min(range(10), key=lambda m: (s[m], m))
         assert s[0] == g["block_size"]
+
+
+@pytest.mark.parametrize("nb,world", [(0, 2), (7, 2), (256, 8), (5, 8), (1000, 3)])
+def test_rank_blocks_partitions(nb, world):
+    from kolm.parallel import rank_blocks
+    for part in ("contiguous", "round_robin"):
+        seen = sorted(i for r in range(world) for i in rank_blocks(nb, r, world, part))
+        assert seen == list(range(nb))
+    assert list(rank_blocks(10, 1, 4, "round_robin")) == [1, 5, 9]
