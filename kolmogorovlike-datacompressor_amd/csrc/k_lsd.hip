@@ -633,11 +633,23 @@ __global__ __launch_bounds__(WG) void k_alpha_codes(const u32* pres, u8* code, u
 // LDS, 16 consecutive positions per thread with a rolling key (drop the oldest character,
 // append the next); positions whose C characters wrap inside their Lyndon factor (FEd <
 // C) are rebuilt from the factor record.
-__global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32 C, u32 w, u32 sh, u32* KA, u32* KB) {
+// hist0 (optional): the first LSD pass's per-tile digit counts (digit 0 of KA), so that
+// pass needs no histogram kernel of its own.
+__global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32 C, u32 w, u32 sh, u32* KA, u32* KB,
+                                                  u32* hist0) {
     __shared__ __align__(16) u8 tx[LSD_T + 64];
     __shared__ u8 cd[256];
+    __shared__ u32 h0[WG / 64][256];
     u32 lo, hi, b;
-    if (!g.range(xcd_tile(), lo, hi, b)) return;
+    const u32 tile = xcd_tile();
+    if (!g.range(tile, lo, hi, b)) {  // a tile past its block's end (the whole workgroup)
+        if (hist0) hist0[(u64)tile * 256 + threadIdx.x] = 0;
+        return;
+    }
+    if (hist0) {
+#pragma unroll
+        for (int i = 0; i < WG / 64; ++i) h0[i][threadIdx.x] = 0;
+    }
     const u32 N = (u32)g.geo.N;
     cd[threadIdx.x] = code[(u64)b * 256 + threadIdx.x];
     const u32 n = min(hi + C, N) - lo;
@@ -650,7 +662,7 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
     }
     __syncthreads();
     const u32 i0 = threadIdx.x * LSD_PT;
-    if (lo + i0 >= hi) return;
+    if (lo + i0 < hi) {  // (no return: every thread reaches the histogram's barrier)
     // the 16 distances to the factor end (one 16-byte load when aligned and whole)
     u8 fed[LSD_PT];
     if (((lo + i0) & 15) == 0 && lo + i0 + LSD_PT <= hi) {
@@ -705,16 +717,28 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
             if (KB) KB[p0 + e] = kb[e];
         }
     }
+    if (hist0) {
+        const u32 wv = threadIdx.x >> 6;
+#pragma unroll
+        for (u32 e = 0; e < LSD_PT; ++e)
+            if (p0 + e < hi) atomicAdd(&h0[wv][digit<0>(ka[e])], 1u);
+    }
+    }
+    if (hist0) {
+        __syncthreads();
+        hist0[(u64)tile * 256 + threadIdx.x] = h0[0][threadIdx.x] + h0[1][threadIdx.x] + h0[2][threadIdx.x] +
+                                               h0[3][threadIdx.x];
+    }
 }
 
 template <int P, int SRC, int G>
 void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kout, u32* pout, const u32* kg,
-              u32* hist, hipStream_t s, KTimer* kt) {
+              u32* hist, bool counted, hipStream_t s, KTimer* kt) {
     static const std::string hn = "k_lsd_hist<" + std::to_string(P) + ", " + std::to_string(SRC) + ">";
     static const std::string sn =
         "k_lsd_scatter<" + std::to_string(P) + ", " + std::to_string(SRC) + ", " + std::to_string(G) + ">";
     const u64 N = g.geo.N, H = (u64)nt * 1024;  // H: per-tile histogram bytes
-    {
+    if (!counted) {  // counted: the producer of kin wrote the tile histograms
         KScope k(kt, KT_LSD, hn.c_str(), 4 * N + H);
         k_lsd_hist<P, SRC><<<nt, WG, 0, s>>>(g, kin, hist);
     }
@@ -736,7 +760,7 @@ void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kou
     }
 }
 
-using PassFn = void (*)(const LsdGeom&, u32, const u32*, const u32*, u32*, u32*, const u32*, u32*, hipStream_t,
+using PassFn = void (*)(const LsdGeom&, u32, const u32*, const u32*, u32*, u32*, const u32*, u32*, bool, hipStream_t,
                         KTimer*);
 template <int P>
 constexpr PassFn pass_of(int src_kp, int gat) {
@@ -744,10 +768,10 @@ constexpr PassFn pass_of(int src_kp, int gat) {
                   : (gat ? lsd_pass<P, SRC_PAIR, 1> : lsd_pass<P, SRC_PAIR, 0>);
 }
 void run_pass(int P, bool src_kp, bool gat, const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kout,
-              u32* pout, const u32* kg, u32* hist, hipStream_t s, KTimer* kt) {
+              u32* pout, const u32* kg, u32* hist, bool counted, hipStream_t s, KTimer* kt) {
     const int a = src_kp ? 1 : 0, c = gat ? 1 : 0;
     const PassFn f = P == 0 ? pass_of<0>(a, c) : P == 1 ? pass_of<1>(a, c) : P == 2 ? pass_of<2>(a, c) : pass_of<3>(a, c);
-    f(g, nt, kin, pin, kout, pout, kg, hist, s, kt);
+    f(g, nt, kin, pin, kout, pout, kg, hist, counted, s, kt);
 }
 
 }  // namespace
@@ -799,7 +823,7 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
     {
         // text + FEd 2 (+ FSL near factor ends), KA 4 (+ KB 4)
         KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6));
-        k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr);
+        k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist);
     }
     u32* K[2] = {t.K2, t.K22};
     u32* S[2] = {t.SA, t.SA2};
@@ -808,11 +832,11 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
     for (u32 q = 0; q < pa; ++q) {
         const bool first = q == 0, gat = q + 1 == pa && pb > 0;
         run_pass((int)q, first, gat, g, nt, first ? t.RK : K[o ^ 1], first ? nullptr : S[o ^ 1], K[o], S[o],
-                 gat ? t.KP : nullptr, t.hist, s, kt);
+                 gat ? t.KP : nullptr, t.hist, first, s, kt);
         o ^= 1;
     }
     for (u32 q = 0; q < pb; ++q) {
-        run_pass((int)q, false, false, g, nt, K[o ^ 1], S[o ^ 1], K[o], S[o], nullptr, t.hist, s, kt);
+        run_pass((int)q, false, false, g, nt, K[o ^ 1], S[o ^ 1], K[o], S[o], nullptr, t.hist, false, s, kt);
         o ^= 1;
     }
     // RK through position windows (k_r0_rk) when every block has at most 256 of them;
