@@ -352,6 +352,25 @@ __global__ __launch_bounds__(WG) void k_rice_emit(TileG tg, const u8* seq, const
     for (u32 i = threadIdx.x; i < lds_words; i += WG) lds[i] = 0;
     __syncthreads();
     u32 pos = lead + my;
+    if (cnt <= 64) {
+        // the thread's whole code (usually a few dozen bits) assembled in one register and
+        // OR-ed into at most three LDS words, instead of one atomic per symbol
+        u64 acc = 0;
+        for (int e = 0; e < ns; ++e) {
+            const u32 s = sym[e], q = s >> k, len = q + 1 + k;  // q < 64 here
+            const u64 code = (((q ? ~0ull >> (64 - q) : 0ull)) << (1 + k)) | (s & ((1u << k) - 1));
+            acc = len >= 64 ? code : (acc << len) | code;
+        }
+        if (cnt) {
+            const u64 v = acc << (64 - cnt);  // left-aligned
+            const u32 w = pos >> 5, o = pos & 31, h32 = (u32)(v >> 32), l32 = (u32)v;
+            const u32 x0 = h32 >> o, x1 = (o ? h32 << (32 - o) : 0u) | (l32 >> o), x2 = o ? l32 << (32 - o) : 0u;
+            if (x0) atomicOr(&lds[w], x0);
+            if (x1) atomicOr(&lds[w + 1], x1);
+            if (x2) atomicOr(&lds[w + 2], x2);
+        }
+        pos += cnt;
+    } else
     for (int e = 0; e < ns; ++e) {
         const u32 s = sym[e];
         u32 q = s >> k;

@@ -217,19 +217,26 @@ struct RiceAcc {
     }
 };
 
+constexpr u32 MTF_SLAB = 64;  // bytes per thread and round of the whole-workgroup path
+
 __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, const u8* states, u8* out,
                                                    u32 nchunks, u64* bits, int rice_k) {
     __shared__ u32 tab[64 * RT];  // word w of thread t at tab[w * RT + t]
+    __shared__ u32 sl[RT * MTF_SLAB / 4];  // one slab per thread (whole-workgroup path)
+    __shared__ u32 slo[RT];                // chunk start of every thread
     const u32 t = threadIdx.x;
     const u32 c = blockIdx.x * RT + t;
-    if (c >= nchunks) return;
-    u32 lo, hi;
-    if (!cg.range(c, lo, hi)) return;
-    const u32* s = reinterpret_cast<const u32*>(states + (u64)c * 256);
+    u32 lo = 0, hi = 0;
+    const bool valid = c < nchunks && cg.range(c, lo, hi);  // (no early return: barriers below)
     // entries 0..7 (words 0, 1) live in registers: BBWT output is mostly short MTF indices,
     // which then cost no LDS round trip; words 2..63 stay in LDS
-    u32 r0 = s[0], r1 = s[1];
-    for (int w = 2; w < 64; ++w) tab[w * RT + t] = s[w];
+    u32 r0 = 0, r1 = 0;
+    if (valid) {
+        const u32* s = reinterpret_cast<const u32*>(states + (u64)c * 256);
+        r0 = s[0];
+        r1 = s[1];
+        for (int w = 2; w < 64; ++w) tab[w * RT + t] = s[w];
+    }
     auto haszero = [](u32 y) { return (y - 0x01010101u) & ~y & 0x80808080u; };
     // word x with its byte j moved to byte 0's side: bytes [0, j) shift up, byte 0 = in
     auto front = [](u32 x, u32 j, u32 in) {
@@ -275,7 +282,48 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
     };
     RiceAcc acc;
     acc.k = rice_k;
-    if (((lo | hi) & 15) == 0) {
+    // Whole-workgroup path (every chunk of the workgroup a full, 16-byte aligned 1 KiB):
+    // the chunks advance together 64 bytes at a time through an LDS slab per thread, loaded
+    // and stored by the whole workgroup so that every wave instruction moves whole 64-byte
+    // lines (16 threads' slabs per instruction); the per-thread 16-byte accesses below touch
+    // 64 lines per instruction, 1 KiB apart (PMC: ~4x the output bytes written).
+    const bool full = valid && hi - lo == MTF_CHUNK && (lo & 15) == 0;
+    if (__syncthreads_and(full)) {
+        u32* slab = sl + t * (MTF_SLAB / 4);
+        slo[t] = lo;
+        __syncthreads();
+        for (u32 r = 0; r < MTF_CHUNK; r += MTF_SLAB) {
+            // load: uint4 m of the round = part (m & 3) of thread (m >> 2)'s slab
+#pragma unroll
+            for (u32 q = 0; q < MTF_SLAB / 16; ++q) {
+                const u32 m = q * RT + t, owner = m >> 2, part = m & 3;
+                reinterpret_cast<uint4*>(sl)[m] = *reinterpret_cast<const uint4*>(in + slo[owner] + r + 16 * part);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < MTF_SLAB / 4; ++q) {
+                const u32 wv = slab[q];
+                u32 o = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const u32 m = step((wv >> (8 * j)) & 0xFF);
+                    if (bits) acc.add(m);
+                    o |= m << (8 * j);
+                }
+                slab[q] = o;
+                if (bits && (q & 1)) acc.group(slab[q - 1], o);
+            }
+            __syncthreads();
+#pragma unroll
+            for (u32 q = 0; q < MTF_SLAB / 16; ++q) {
+                const u32 m = q * RT + t, owner = m >> 2, part = m & 3;
+                *reinterpret_cast<uint4*>(out + slo[owner] + r + 16 * part) = reinterpret_cast<const uint4*>(sl)[m];
+            }
+            __syncthreads();
+        }
+    } else if (!valid) {
+        return;
+    } else if (((lo | hi) & 15) == 0) {
         // 16 bytes in / 16 bytes out per global access (threads are 1 KiB apart); chunk
         // starts are multiples of 1 KiB from the block start, so 8-byte groups align
         for (u32 i = lo; i < hi; i += 16) {

@@ -950,8 +950,9 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
                    cnt + C_STATUS, s);
     }
     std::vector<u64> off(nb + 1);
-    std::vector<u32> rpres(want_rp ? (u64)nb * RP_RS_N : 0);
+    std::vector<u32> rpres(want_rp ? (u64)nb * RP_RS_N : 0), win(nb);
     KOLM_HIP_CHECK(hipMemcpyAsync(off.data(), e.off, sizeof(u64) * (nb + 1), hipMemcpyDeviceToHost, s));
+    KOLM_HIP_CHECK(hipMemcpyAsync(win.data(), e.method, sizeof(u32) * nb, hipMemcpyDeviceToHost, s));
     KOLM_HIP_CHECK(hipMemcpyAsync(c->h_cnt, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
     if (want_rp)
         KOLM_HIP_CHECK(hipMemcpyAsync(rpres.data(), rpa.result, sizeof(u32) * rpres.size(), hipMemcpyDeviceToHost, s));
@@ -991,13 +992,16 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         return KOLM_ECAP;
     }
     {
+        // only the emitters of methods some block chose (the winners are on the host now)
+        u32 used = 0;
+        for (u32 m : win) used |= 1u << std::min<u32>(m, 31);
         TScope t(c, KOLM_KT_EMIT, "emit", N + 2 * off[nb]);
         KOLM_HIP_CHECK(hipMemsetAsync(d_arena, 0, (off[nb] + 8) & ~(u64)3, s));
-        launch_emit_simple(e, s);
-        launch_emit_rice(e, s);
-        if (want_lz) launch_lz_emit(z, e.method, e.off, d_arena, s);
-        if (want_rp) launch_rp_emit(rpa, e.method, e.off, d_arena, s);
-        if (want_v2) launch_v2_emit(geo, v2.pb, v2.meta, e.method, e.off, v2.U, v2.L, d_arena, s);
+        if (used & ((1u << KOLM_M_RAW) | (1u << KOLM_M_XOR) | (1u << KOLM_M_LFSR))) launch_emit_simple(e, s);
+        if (used & (0x1Fu << KOLM_M_BBWT)) launch_emit_rice(e, s);
+        if (want_lz && (used & (1u << KOLM_M_LZ77))) launch_lz_emit(z, e.method, e.off, d_arena, s);
+        if (want_rp && (used & (1u << KOLM_M_REPAIR))) launch_rp_emit(rpa, e.method, e.off, d_arena, s);
+        if (want_v2 && (used & (1u << KOLM_M_V2NEW))) launch_v2_emit(geo, v2.pb, v2.meta, e.method, e.off, v2.U, v2.L, d_arena, s);
     }
     KOLM_HIP_CHECK(hipEventRecord(ev[4], s));
     if (h_sizes)
