@@ -92,9 +92,9 @@ __global__ __launch_bounds__(WG) void k_lsd_hist(LsdGeom g, const u32* K, u32* h
     __syncthreads();
     u32 lo, hi, b;
     if (g.range(xcd_tile(), lo, hi, b)) {
-        // 16 consecutive keys per thread, four 16-byte loads when aligned (order is irrelevant)
         const u32 i0 = lo + tid * LSD_PT;
         if ((i0 & 3) == 0 && i0 + LSD_PT <= hi) {
+            // 16 consecutive keys per thread, four 16-byte loads when aligned (order is irrelevant)
             const uint4* p = reinterpret_cast<const uint4*>(K + i0);
             uint4 v[LSD_PT / 4];
 #pragma unroll

@@ -29,13 +29,61 @@ struct ChunkGeom {
     }
 };
 
+constexpr u32 MTF_SLAB = 64;  // bytes per thread and round of the whole-workgroup paths
+
 __global__ __launch_bounds__(256) void k_mtf_summary(ChunkGeom cg, const u8* in, u8* summary,
                                                      u16* scnt, u32 nchunks) {
-    const u32 c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nchunks) return;
-    u32 lo, hi;
+    __shared__ u32 sl[256 * MTF_SLAB / 4];
+    __shared__ u32 slo[256];
+    const u32 t = threadIdx.x;
+    const u32 c = blockIdx.x * blockDim.x + t;
+    u32 lo = 0, hi = 0;
+    const bool valid = c < nchunks && cg.range(c, lo, hi);
     u16 cnt = 0;
-    if (cg.range(c, lo, hi)) {
+    // whole-workgroup path (every chunk a full aligned 1 KiB): the chunks are read backwards
+    // 64 bytes at a time through LDS slabs that the workgroup loads as whole 64-byte lines
+    // (per-thread 16-byte loads 1 KiB apart over-fetched ~4x, PMC)
+    if (__syncthreads_and(valid && hi - lo == MTF_CHUNK && (lo & 15) == 0)) {
+        u32 seen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        u8* out = summary + (u64)c * 256;
+        slo[t] = lo;
+        __syncthreads();
+        for (u32 r = MTF_CHUNK; r > 0; r -= MTF_SLAB) {
+#pragma unroll
+            for (u32 q = 0; q < MTF_SLAB / 16; ++q) {
+                const u32 m = q * 256 + t, owner = m >> 2, part = m & 3;
+                reinterpret_cast<uint4*>(sl)[m] =
+                    *reinterpret_cast<const uint4*>(in + slo[owner] + r - MTF_SLAB + 16 * part);
+            }
+            __syncthreads();
+            const u32* slab = sl + t * (MTF_SLAB / 4);
+#pragma unroll
+            for (int q = MTF_SLAB / 4 - 1; q >= 0; --q) {
+                const u32 wv = slab[q];
+#pragma unroll
+                for (int j = 3; j >= 0; --j) {
+                    const u32 b = (wv >> (8 * j)) & 0xFF, w = b >> 5, bit = 1u << (b & 31);
+                    u32 sw = 0;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) sw = (k == (int)w) ? seen[k] : sw;
+                    if (!(sw & bit)) {
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            if (k == (int)w) seen[k] |= bit;
+                        out[cnt++] = (u8)b;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        scnt[c] = cnt;
+        return;
+    }
+    if (!valid) {
+        if (c < nchunks) scnt[c] = 0;
+        return;
+    }
+    {
         u32 seen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         u8* out = summary + (u64)c * 256;
         auto visit = [&](u32 b) {
@@ -217,13 +265,9 @@ struct RiceAcc {
     }
 };
 
-constexpr u32 MTF_SLAB = 64;  // bytes per thread and round of the whole-workgroup path
-
 __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, const u8* states, u8* out,
                                                    u32 nchunks, u64* bits, int rice_k) {
     __shared__ u32 tab[64 * RT];  // word w of thread t at tab[w * RT + t]
-    __shared__ u32 sl[RT * MTF_SLAB / 4];  // one slab per thread (whole-workgroup path)
-    __shared__ u32 slo[RT];                // chunk start of every thread
     const u32 t = threadIdx.x;
     const u32 c = blockIdx.x * RT + t;
     u32 lo = 0, hi = 0;
@@ -282,50 +326,37 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
     };
     RiceAcc acc;
     acc.k = rice_k;
-    // Whole-workgroup path (every chunk of the workgroup a full, 16-byte aligned 1 KiB):
-    // the chunks advance together 64 bytes at a time through an LDS slab per thread, loaded
-    // and stored by the whole workgroup so that every wave instruction moves whole 64-byte
-    // lines (16 threads' slabs per instruction); the per-thread 16-byte accesses below touch
-    // 64 lines per instruction, 1 KiB apart (PMC: ~4x the output bytes written).
-    const bool full = valid && hi - lo == MTF_CHUNK && (lo & 15) == 0;
-    if (__syncthreads_and(full)) {
-        u32* slab = sl + t * (MTF_SLAB / 4);
-        slo[t] = lo;
-        __syncthreads();
-        for (u32 r = 0; r < MTF_CHUNK; r += MTF_SLAB) {
-            // load: uint4 m of the round = part (m & 3) of thread (m >> 2)'s slab
+    if (!valid) return;
+    if (((lo | hi) & 63) == 0) {
+        // 64 bytes in / 64 bytes out per step as four back-to-back 16-byte accesses, so a
+        // line is completed by consecutive instructions (threads are 1 KiB apart: one 16-byte
+        // store per step left the lines' quarters to be merged across many steps — PMC:
+        // ~4x the output bytes written); chunk starts are multiples of 1 KiB from the block
+        // start, so 8-byte groups align
+        for (u32 i = lo; i < hi; i += 64) {
+            uint4 v[4];
 #pragma unroll
-            for (u32 q = 0; q < MTF_SLAB / 16; ++q) {
-                const u32 m = q * RT + t, owner = m >> 2, part = m & 3;
-                reinterpret_cast<uint4*>(sl)[m] = *reinterpret_cast<const uint4*>(in + slo[owner] + r + 16 * part);
-            }
-            __syncthreads();
+            for (int h = 0; h < 4; ++h) v[h] = *reinterpret_cast<const uint4*>(in + i + 16 * h);
+            u32 ov[16];
 #pragma unroll
-            for (int q = 0; q < MTF_SLAB / 4; ++q) {
-                const u32 wv = slab[q];
+            for (int q = 0; q < 16; ++q) {
+                const u32 wq = q % 4 == 0 ? v[q / 4].x : q % 4 == 1 ? v[q / 4].y : q % 4 == 2 ? v[q / 4].z : v[q / 4].w;
                 u32 o = 0;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const u32 m = step((wv >> (8 * j)) & 0xFF);
+                    const u32 m = step((wq >> (8 * j)) & 0xFF);
                     if (bits) acc.add(m);
                     o |= m << (8 * j);
                 }
-                slab[q] = o;
-                if (bits && (q & 1)) acc.group(slab[q - 1], o);
+                ov[q] = o;
+                if (bits && (q & 1)) acc.group(ov[q - 1], o);
             }
-            __syncthreads();
 #pragma unroll
-            for (u32 q = 0; q < MTF_SLAB / 16; ++q) {
-                const u32 m = q * RT + t, owner = m >> 2, part = m & 3;
-                *reinterpret_cast<uint4*>(out + slo[owner] + r + 16 * part) = reinterpret_cast<const uint4*>(sl)[m];
-            }
-            __syncthreads();
+            for (int h = 0; h < 4; ++h)
+                *reinterpret_cast<uint4*>(out + i + 16 * h) = make_uint4(ov[4 * h], ov[4 * h + 1], ov[4 * h + 2], ov[4 * h + 3]);
         }
-    } else if (!valid) {
-        return;
     } else if (((lo | hi) & 15) == 0) {
-        // 16 bytes in / 16 bytes out per global access (threads are 1 KiB apart); chunk
-        // starts are multiples of 1 KiB from the block start, so 8-byte groups align
+        // 16 bytes in / 16 bytes out per global access
         for (u32 i = lo; i < hi; i += 16) {
             const uint4 v = *reinterpret_cast<const uint4*>(in + i);
             const u32 wv[4] = {v.x, v.y, v.z, v.w};
