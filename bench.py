@@ -54,8 +54,8 @@ LIMITER = {
     "k_repair": "latency: one workgroup per block, barrier-separated batches of dependent global accesses",
     "k_duval_span": "LDS latency: sequential Duval over each thread's 128-byte chunk, then tree merges of "
                     "adjacent factorisations (dependent LDS byte compares / bitmap scans); reads the text once",
-    "k_lsd_scatter<3, 2, 1>": "random 4-byte gathers of the next key by position (one 32-64 B request each) "
-                              "beside the streaming LSD scatter",
+    "k_lsd_scatter_w<3, 2, 1>": "random 4-byte gathers of the next key by position (one 32-64 B request each) "
+                                "beside the streaming LSD scatter",
 }
 SORT_STREAM_LIMITER = ("random 4-byte gathers / scatters of ranks and keys by position (one 32-64 B HBM "
                        "request per element in the doubling rounds and the RK scatter), streaming LSD passes at "
@@ -328,10 +328,13 @@ def main():
     contract = int(n * (8 + 7 + 2 + 1 + 1) + 44 * float((lens * r_avg).sum()) + out_w)
     achieved = contract / (sort_ms * 1e-3) / 1e9
     builder = sum(v["bytes"] for v in sort_k.values()) / ks
-    tr_have = [k for k in sort_k if pmc.get(k, {}).get("hbm_bytes_per_launch")]
-    traffic = None
-    if sort_k and len(tr_have) == len(sort_k):
-        traffic = int(sum(pmc[k]["hbm_bytes_per_launch"] * sort_k[k]["launches"] for k in sort_k) / ks)
+    # PMC traffic of the sort stream per step: every profiled kernel except the index
+    # stream's (LZ77 parse + stitch, cheap sizes, predecessor bytes) and the runtime's copy /
+    # fill kernels, per encode batch of the profiled run (tools/pmc_traffic.py BATCHES)
+    idx_k = ("k_lz_local", "k_lz_stitch", "k_cheap_sizes", "k_prevc", "k_lz_emit", "k_repair", "k_rp_")
+    per_batch = [v["bytes_per_batch"] for k, v in pmc.items()
+                 if "bytes_per_batch" in v and not k.startswith("__amd") and not k.startswith(idx_k)]
+    traffic = int(sum(per_batch)) if per_batch else None
     dom_name, dom = max(sort_k.items(), key=lambda kv: kv[1]["ms"]) if sort_k else ("", {"ms": 0, "launches": 1,
                                                                                           "bytes": 0})
     dom_avg = dom["ms"] / max(dom["launches"], 1)

@@ -735,8 +735,13 @@ template <int P, int SRC, int G>
 void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kout, u32* pout, const u32* kg,
               u32* hist, bool counted, hipStream_t s, KTimer* kt) {
     static const std::string hn = "k_lsd_hist<" + std::to_string(P) + ", " + std::to_string(SRC) + ">";
-    static const std::string sn =
-        "k_lsd_scatter<" + std::to_string(P) + ", " + std::to_string(SRC) + ", " + std::to_string(G) + ">";
+    // A/B switch KOLM_LSD_SW: 0 = k_lsd_scatter everywhere, 1 = except the first pass (keys
+    // by position), 2 = k_lsd_scatter_w everywhere (default); the timer carries the launched name
+    static const int sw = getenv("KOLM_LSD_SW") ? atoi(getenv("KOLM_LSD_SW")) : 2;
+    const bool use_w = sw == 2 || (sw == 1 && SRC == SRC_PAIR);
+    static const std::string tail = "<" + std::to_string(P) + ", " + std::to_string(SRC) + ", " + std::to_string(G) + ">";
+    static const std::string sn_w = "k_lsd_scatter_w" + tail, sn_p = "k_lsd_scatter" + tail;
+    const std::string& sn = use_w ? sn_w : sn_p;
     const u64 N = g.geo.N, H = (u64)nt * 1024;  // H: per-tile histogram bytes
     if (!counted) {  // counted: the producer of kin wrote the tile histograms
         KScope k(kt, KT_LSD, hn.c_str(), 4 * N + H);
@@ -750,10 +755,8 @@ void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kou
         // key + position in (the first pass reads the key by position only) and out; G: + the gather
         KScope k(kt, KT_LSD, sn.c_str(), (SRC == SRC_KP ? 12 : 16) * N + (G ? 4 * N : 0) + H);
         // k_lsd_scatter_w (three barriers per tile; 256 MiB text, overlapped: 1.5-1.7 -> 0.9-1.0
-        // ms per pass).  A/B switch KOLM_LSD_SW: 0 = k_lsd_scatter everywhere, 1 = except the
-        // first pass (keys by position), 2 = everywhere (default)
-        static const int sw = getenv("KOLM_LSD_SW") ? atoi(getenv("KOLM_LSD_SW")) : 2;
-        if (sw == 2 || (sw == 1 && SRC == SRC_PAIR))
+        // ms per pass)
+        if (use_w)
             k_lsd_scatter_w<P, SRC, G><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
         else
             k_lsd_scatter<P, SRC, G><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);

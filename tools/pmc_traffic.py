@@ -6,7 +6,10 @@ never combined with sys/runtime traces), e.g.:
     rocprofv3 --pmc FETCH_SIZE  -d OUT/fetch --output-format csv -- python3 bench.py ...
     rocprofv3 --pmc WRITE_SIZE  -d OUT/write --output-format csv -- python3 bench.py ...
     rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d OUT/hit --output-format csv -- ...
-then:  python tools/pmc_traffic.py OUT > profiles/pmc_summary.json
+then:  python tools/pmc_traffic.py OUT [BATCHES] > profiles/pmc_summary.json
+BATCHES = encode batches the profiled command ran (bench.py --warmup 1 --steps 1 --kt-steps 1
+--no-serial-pass with every leg off: 3); with it every kernel also gets "bytes_per_batch"
+(its summed HBM bytes / BATCHES), which bench.py adds up over the sort-stream kernels.
 
 Corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are in KiB;
 on gfx950 FETCH_SIZE reports half the bytes of wide coalesced streaming reads, so the
@@ -59,6 +62,7 @@ def load(outdir):
 
 def main():
     outdir = sys.argv[1]
+    batches = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     per = load(outdir)
     kernels = {}
     fams = defaultdict(lambda: {"fetch_kib": 0.0, "write_kib": 0.0, "dispatches": 0})
@@ -74,6 +78,8 @@ def main():
             ent["fetch_bytes_x2"] = 2 * fb
             ent["write_bytes"] = wb
             ent["hbm_bytes_per_launch"] = 2 * fb + wb
+            if batches:
+                ent["bytes_per_batch"] = (2 * fb + wb) * ent["dispatches"] / batches
         if "TCC_HIT_sum_avg" in ent and "TCC_MISS_sum_avg" in ent:
             h, m = ent["TCC_HIT_sum_avg"], ent["TCC_MISS_sum_avg"]
             ent["l2_hit_rate"] = h / (h + m) if h + m else None
@@ -88,7 +94,8 @@ def main():
     for fam, v in fams.items():
         fam_out[fam] = {"fetch_bytes_x2_total": 2 * v["fetch_kib"] * 1024, "write_bytes_total": v["write_kib"] * 1024,
                         "dispatches": v["dispatches"]}
-    print(json.dumps({"source": os.path.abspath(outdir), "note": __doc__.split("Corrections")[1].strip(),
+    print(json.dumps({"source": os.path.abspath(outdir), "batches": batches,
+                      "note": __doc__.split("Corrections")[1].strip(),
                       "kernels": kernels, "families_total": fam_out}, indent=1, sort_keys=True))
 
 
