@@ -316,8 +316,11 @@ def main():
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
             pmc = json.load(f).get("kernels", {})
+    idx_k = ("k_lz_local", "k_lz_stitch", "k_cheap_sizes", "k_prevc", "k_lz_emit", "k_repair", "k_rp_")
     sort_k = {k: v for k, v in ktimes.items() if v.get("stream") == "sort"}
-    sort_ms = sum(v["ms"] for v in sort_k.values()) / ks
+    if not sort_k:  # streams serialised (KOLM_SERIAL=1): every kernel but the index stream's
+        sort_k = {k: v for k, v in ktimes.items() if not k.startswith(idx_k) and v.get("stream") != "repair"}
+    sort_ms = max(sum(v["ms"] for v in sort_k.values()) / ks, 1e-9)
     rsum = s0["cyc_rounds_sum"]  # sum over blocks of the doubling rounds each block needed
     lens = np.full(nb, a.bs, np.int64)
     lens[-1] = n - a.bs * (nb - 1)
@@ -331,7 +334,6 @@ def main():
     # PMC traffic of the sort stream per step: every profiled kernel except the index
     # stream's (LZ77 parse + stitch, cheap sizes, predecessor bytes) and the runtime's copy /
     # fill kernels, per encode batch of the profiled run (tools/pmc_traffic.py BATCHES)
-    idx_k = ("k_lz_local", "k_lz_stitch", "k_cheap_sizes", "k_prevc", "k_lz_emit", "k_repair", "k_rp_")
     per_batch = [v["bytes_per_batch"] for k, v in pmc.items()
                  if "bytes_per_batch" in v and not k.startswith("__amd") and not k.startswith(idx_k)]
     traffic = int(sum(per_batch)) if per_batch else None
