@@ -60,20 +60,6 @@ __device__ inline u32 wg_excl(u32 v, u32 ident, u32* sh) {
     return MAX ? max(carry, ex) : min(carry, ex);
 }
 
-// Phase A: per-tile min of RK.
-__global__ __launch_bounds__(WG) void k_tile_min_rk(TileGeom tg, const u32* RK, u32* tmin) {
-    __shared__ u32 sh[WG / 64];
-    u32 lo, hi, b;
-    const bool ok = tg.range(blockIdx.x, lo, hi, b);
-    u32 m = BIG;
-    if (ok)
-        for (u32 i = lo + threadIdx.x; i < hi; i += WG) m = min(m, RK[i]);
-    m = wave_reduce_min(m);
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) tmin[blockIdx.x] = min(min(sh[0], sh[1]), min(sh[2], sh[3]));
-}
-
 // Phase B: per block, exclusive scan over the block's tiles (one workgroup per block).
 template <bool REV, bool MAX>
 __global__ __launch_bounds__(WG) void k_tiles_scan(const u32* in, u32* out, u32 tpb, u32 ident) {
@@ -98,117 +84,58 @@ __global__ __launch_bounds__(WG) void k_tiles_scan(const u32* in, u32* out, u32 
     }
 }
 
-// Phase C: factor-start flags.
-__global__ __launch_bounds__(WG) void k_lyn_flags(TileGeom tg, const u32* RK, const u32* tcarry,
-                                                  u8* flag) {
+// Phase A': per-tile first factor start.
+__global__ __launch_bounds__(WG) void k_tile_starts(TileGeom tg, const u8* flag, u32* tmin) {
     __shared__ u32 sh[WG / 64];
     u32 lo, hi, b;
-    if (!tg.range(blockIdx.x, lo, hi, b)) return;
-    // each thread: PER_THREAD consecutive elements
-    const u32 i0 = lo + threadIdx.x * PER_THREAD;
-    u32 v[PER_THREAD];
-    u32 loc = BIG;
-#pragma unroll
-    for (int e = 0; e < PER_THREAD; ++e) {
-        v[e] = (i0 + e < hi) ? RK[i0 + e] : BIG;
-        loc = min(loc, v[e]);
-    }
-    u32 run = min(tcarry[blockIdx.x], wg_excl<false, false>(loc, BIG, sh));
-#pragma unroll
-    for (int e = 0; e < PER_THREAD; ++e) {
-        if (i0 + e < hi) flag[i0 + e] = v[e] < run ? 1 : 0;
-        run = min(run, v[e]);
-    }
-}
-
-// Phase A': per-tile max start position and min start position.
-__global__ __launch_bounds__(WG) void k_tile_starts(TileGeom tg, const u8* flag, u32* tmax, u32* tmin) {
-    __shared__ u32 sh1[WG / 64], sh2[WG / 64];
-    u32 lo, hi, b;
     const bool ok = tg.range(blockIdx.x, lo, hi, b);
-    u32 mx = 0, mn = BIG;
+    u32 mn = BIG;
     if (ok) {
         const u32 i0 = lo + threadIdx.x * PER_THREAD;
         if ((i0 & 7) == 0 && i0 + PER_THREAD <= hi) {
             const u64 f8 = *reinterpret_cast<const u64*>(flag + i0);  // 8 flags (0/1 bytes)
-            if (f8) {
-                mn = i0 + ((u32)__ffsll((long long)f8) - 1) / 8;
-                mx = i0 + (63 - (u32)__clzll((long long)f8)) / 8;
-            }
+            if (f8) mn = i0 + ((u32)__ffsll((long long)f8) - 1) / 8;
         } else {
             for (u32 i = i0; i < min(i0 + PER_THREAD, hi); ++i)
-                if (flag[i]) {
-                    mx = max(mx, i);
-                    mn = min(mn, i);
-                }
+                if (flag[i]) mn = min(mn, i);
         }
     }
-    mx = wave_reduce_max(mx);
     mn = wave_reduce_min(mn);
-    if ((threadIdx.x & 63) == 0) {
-        sh1[threadIdx.x >> 6] = mx;
-        sh2[threadIdx.x >> 6] = mn;
-    }
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = mn;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        tmax[blockIdx.x] = max(max(sh1[0], sh1[1]), max(sh1[2], sh1[3]));
-        tmin[blockIdx.x] = min(min(sh2[0], sh2[1]), min(sh2[2], sh2[3]));
-    }
+    if (threadIdx.x == 0) tmin[blockIdx.x] = min(min(sh[0], sh[1]), min(sh[2], sh[3]));
 }
 
-// Phase C': FS = last start <= p, FL = (next start > p, or block end) - FS.
-__global__ __launch_bounds__(WG) void k_fsfl(TileGeom tg, const u8* flag, const u32* cmax,
-                                             const u32* cmin, u64* FSL, u8* FEd) {
+// Phase C': FEd[p] = min(distance from p to its factor's end (next start or block end), 255).
+__global__ __launch_bounds__(WG) void k_fed(TileGeom tg, const u8* flag, const u32* cmin, u8* FEd) {
     __shared__ u32 sh[WG / 64];
     u32 lo, hi, b;
     if (!tg.range(blockIdx.x, lo, hi, b)) return;
     const u32 bend = tg.geo.end(b);
     const u32 i0 = lo + threadIdx.x * PER_THREAD;
-    const bool full = (i0 & 7) == 0 && i0 + PER_THREAD <= hi;  // 8-byte flag load, 16-byte stores
+    const bool full = (i0 & 7) == 0 && i0 + PER_THREAD <= hi;  // 8-byte flag load and store
     u64 fl8 = 0;
     if (full) fl8 = *reinterpret_cast<const u64*>(flag + i0);
     bool f[PER_THREAD];
-    u32 lmax = 0, lmin = BIG;
+    u32 lmin = BIG;
 #pragma unroll
     for (int e = 0; e < PER_THREAD; ++e) {
         const u32 i = i0 + e;
         f[e] = full ? ((fl8 >> (8 * e)) & 0xFF) != 0 : (i < hi && flag[i]);
-        if (f[e]) {
-            lmax = max(lmax, i);
-            lmin = min(lmin, i);
-        }
+        if (f[e]) lmin = min(lmin, i);
     }
-    u32 fs = max(cmax[blockIdx.x], wg_excl<false, true>(lmax, 0u, sh));
     u32 fe = min(cmin[blockIdx.x], wg_excl<true, false>(lmin, BIG, sh));
-    u32 fsv[PER_THREAD];
-#pragma unroll
-    for (int e = 0; e < PER_THREAD; ++e) {
-        if (f[e]) fs = i0 + e;
-        fsv[e] = fs;
-    }
-    u64 fslv[PER_THREAD];
     u64 fed8 = 0;
 #pragma unroll
     for (int e = PER_THREAD - 1; e >= 0; --e) {
         const u32 i = i0 + e;
         const u32 end = fe == BIG ? bend : fe;
-        fslv[e] = (u64)fsv[e] | ((u64)(end - fsv[e]) << 32);  // factor start | length << 32
-        const u32 d = min(end - i, 255u);                       // distance to the factor end
+        const u32 d = min(end - i, 255u);
         fed8 |= (u64)d << (8 * e);
-        if (!full && i < hi) {
-            FSL[i] = fslv[e];
-            FEd[i] = (u8)d;
-        }
+        if (!full && i < hi) FEd[i] = (u8)d;
         if (f[e]) fe = i0 + e;
     }
-    if (full) {
-        uint4* o = reinterpret_cast<uint4*>(FSL + i0);
-#pragma unroll
-        for (int q = 0; q < PER_THREAD / 2; ++q)
-            o[q] = make_uint4((u32)fslv[2 * q], (u32)(fslv[2 * q] >> 32), (u32)fslv[2 * q + 1],
-                              (u32)(fslv[2 * q + 1] >> 32));
-        *reinterpret_cast<u64*>(FEd + i0) = fed8;
-    }
+    if (full) *reinterpret_cast<u64*>(FEd + i0) = fed8;
 }
 
 // ---------------------------------------------------------------------------------
@@ -581,8 +508,8 @@ __device__ inline Pre shf(const Pre& p, u32 l) {
 // agree on 32 bytes compare the text in global memory: the chain of ~800 dependent
 // comparisons per 1 MiB text block cost ~0.7 us of load latency each.
 __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8* s, const u32* fstart,
-                                                    const uint4* fpre, const u32* nfac, u32* stack, u8* flag,
-                                                    u64* prof) {
+                                                    const uint4* fpre, const u32* nfac, u32* stack, u32* fcount,
+                                                    u8* flag, u64* prof) {
     __shared__ u32 lstk[MERGE_LDS];
     __shared__ Pre lpre[PRE_LDS];
     __shared__ u32 lok[PRE_LDS];
@@ -690,7 +617,14 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
         }
         __builtin_amdgcn_s_waitcnt(0);
     }
-    for (u32 i = lane; i < sp; i += 64) flag[stk[i]] = 1;
+    // the block's factor starts: flags, and the sorted list at stack + base (in place when
+    // the stack spilled to global memory)
+    for (u32 i = lane; i < sp; i += 64) {
+        const u32 v = stk[i];
+        flag[v] = 1;
+        if (tot <= MERGE_LDS) stack[base + i] = v;
+    }
+    if (lane == 0) fcount[b] = sp;
     if (prof && lane == 0) {
         atomicAdd((unsigned long long*)&prof[11], (unsigned long long)(wall_clock64() - t0));
         atomicMax((unsigned long long*)&prof[12], (unsigned long long)(wall_clock64() - t0));
@@ -702,20 +636,23 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
 
 // prevc[p] = the character preceding p cyclically inside its factor (streaming pass), so
 // the BBWT gather needs one random byte per slot instead of a factor lookup + a byte.
-__global__ void k_prevc1(Geom geo, const u8* text, const u8* flag, const u64* FSL, u8* prevc) {
+__global__ void k_prevc1(Geom geo, const u8* text, const u8* flag, Factors fac, u8* prevc) {
     for (u32 p = blockIdx.x * blockDim.x + threadIdx.x; p < geo.N; p += gridDim.x * blockDim.x) {
         u32 src = p - 1;
         if (flag[p]) {  // factor start: its predecessor is the factor's last byte
-            const u64 f = FSL[p];
-            src = (u32)f + (u32)(f >> 32) - 1;
+            u32 fs, m;
+            fac.locate(geo, p, fs, m);
+            src = fs + m - 1;
         }
         prevc[p] = text[src];
     }
 }
 
 // 16 positions per thread: flags and output as 16-byte words, text bytes p-1 .. p+14 from
-// aligned words (text 16-byte aligned; the launcher checks).
-__global__ __launch_bounds__(256) void k_prevc(Geom geo, const u8* text, const u8* flag, const u64* FSL, u8* prevc) {
+// aligned words (text 16-byte aligned; the launcher checks).  A factor start's end is the
+// next flag inside the 16 (every block's first position is flagged, so a flag past the
+// block's end is that end) or, past them, a search of the block's factor starts.
+__global__ __launch_bounds__(256) void k_prevc(Geom geo, const u8* text, const u8* flag, Factors fac, u8* prevc) {
     const u32 p0 = (blockIdx.x * 256 + threadIdx.x) * 16;
     const u32 N = (u32)geo.N;
     if (p0 >= N) return;
@@ -723,8 +660,9 @@ __global__ __launch_bounds__(256) void k_prevc(Geom geo, const u8* text, const u
         for (u32 p = p0; p < min(p0 + 16, N); ++p) {
             u32 src = p - 1;
             if (flag[p]) {
-                const u64 f = FSL[p];
-                src = (u32)f + (u32)(f >> 32) - 1;
+                u32 fs, m;
+                fac.locate(geo, p, fs, m);
+                src = fs + m - 1;
             }
             prevc[p] = text[src];
         }
@@ -732,6 +670,9 @@ __global__ __launch_bounds__(256) void k_prevc(Geom geo, const u8* text, const u
     }
     const uint4 fv = *reinterpret_cast<const uint4*>(flag + p0);
     const u32 fw[4] = {fv.x, fv.y, fv.z, fv.w};
+    u32 fm = 0;  // bit e: position p0+e starts a factor
+#pragma unroll
+    for (int e = 0; e < 16; ++e) fm |= ((fw[e >> 2] >> (8 * (e & 3))) & 1u) << e;
     const u32* tw = reinterpret_cast<const u32*>(text + p0) - 1;  // bytes p0-4 .. p0+15
     u32 w[5];
 #pragma unroll
@@ -741,9 +682,17 @@ __global__ __launch_bounds__(256) void k_prevc(Geom geo, const u8* text, const u
     for (int e = 0; e < 16; ++e) {
         // byte p0+e-1 = byte (e+3) of the 20-byte window starting at p0-4
         u32 c = (w[(e + 3) >> 2] >> (8 * ((e + 3) & 3))) & 0xFF;
-        if ((fw[e >> 2] >> (8 * (e & 3))) & 0xFF) {  // factor start: the factor's last byte
-            const u64 f = FSL[p0 + e];
-            c = text[(u32)f + (u32)(f >> 32) - 1];
+        if ((fm >> e) & 1u) {  // factor start: the factor's last byte
+            const u32 rest = fm >> (e + 1);
+            u32 last;
+            if (rest) {
+                last = p0 + e + __builtin_ctz(rest);  // next start - 1
+            } else {
+                u32 fs, m;
+                fac.locate(geo, p0 + e, fs, m);
+                last = fs + m - 1;
+            }
+            c = text[last];
         }
         o[e >> 2] |= c << (8 * (e & 3));
     }
@@ -763,17 +712,6 @@ __global__ __launch_bounds__(256) void k_bbwt_gather(Geom geo, const u32* SA, co
 
 }  // namespace
 
-// Lyndon factor starts by the ISA left-to-right-minima rule (needs a complete linear
-// suffix order in RK); kept as an alternative to the parallel Duval path.
-void launch_lyndon_isa(const Geom& geo, const u32* RK, u8* flag, u32* tile_tmp, u32* tile_tmp2, hipStream_t s) {
-    if (!geo.N) return;
-    TileGeom tg{geo, (geo.bs + TILE - 1) / TILE};
-    const u32 nt = tg.tpb * geo.nb;
-    k_tile_min_rk<<<nt, WG, 0, s>>>(tg, RK, tile_tmp);
-    k_tiles_scan<false, false><<<geo.nb, WG, 0, s>>>(tile_tmp, tile_tmp + nt, tg.tpb, BIG);
-    k_lyn_flags<<<nt, WG, 0, s>>>(tg, RK, tile_tmp + nt, flag);
-}
-
 // KOLM_DUVAL_PROF=1 (debug): per-phase wall-clock of k_duval_span and k_duval_merge
 u64* dprof_buf() {
     static u64* prof = nullptr;
@@ -785,16 +723,15 @@ u64* dprof_buf() {
     return prof;
 }
 
-// Lyndon factorisation of every block (parallel Duval + merge) -> per-position FSL.
-void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u8* FEd, u32* fstart, uint4* fpre, u32* nfac,
-                   u32* stack, u32* tile_tmp, u32* tile_tmp2, hipStream_t s, KTimer* kt) {
+// Lyndon factorisation of every block (parallel Duval + merge) -> factor-start lists,
+// flags and FEd.
+void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fstart, uint4* fpre, u32* nfac,
+                   u32* stack, u32* fcount, u32* tile_tmp, hipStream_t s, KTimer* kt) {
     if (!geo.N) return;
     TileGeom tg{geo, (geo.bs + TILE - 1) / TILE};
     const u32 nt = tg.tpb * geo.nb;
     u32* A = tile_tmp;        // [nt]
     u32* B = tile_tmp + nt;   // [nt]
-    u32* C2 = tile_tmp2;      // [nt]
-    u32* D = tile_tmp2 + nt;  // [nt]
     const u32 cpb = (geo.bs + DUVAL_SPAN - 1) / DUVAL_SPAN;
     const u32 nch = cpb * geo.nb;
     const u64 N = geo.N;
@@ -805,7 +742,7 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u8* FEd,
     }
     {
         KScope k(kt, KT_LYNDON, "k_duval_merge", (u64)nch * 8);
-        k_duval_merge<<<geo.nb, 64, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, stack, flag, dprof_buf());
+        k_duval_merge<<<geo.nb, 64, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, stack, fcount, flag, dprof_buf());
     }
     if (u64* prof = dprof_buf()) {
         u64 h[16];
@@ -820,23 +757,22 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u8* FEd,
     }
     {
         KScope k(kt, KT_LYNDON, "k_tile_starts", N);
-        k_tile_starts<<<nt, WG, 0, s>>>(tg, flag, A, C2);
-        k_tiles_scan<false, true><<<geo.nb, WG, 0, s>>>(A, B, tg.tpb, 0u);
-        k_tiles_scan<true, false><<<geo.nb, WG, 0, s>>>(C2, D, tg.tpb, BIG);
+        k_tile_starts<<<nt, WG, 0, s>>>(tg, flag, A);
+        k_tiles_scan<true, false><<<geo.nb, WG, 0, s>>>(A, B, tg.tpb, BIG);
     }
     {
-        KScope k(kt, KT_LYNDON, "k_fsfl", 10 * N);  // flag 1 + FSL 8 + FEd 1
-        k_fsfl<<<nt, WG, 0, s>>>(tg, flag, B, D, FSL, FEd);
+        KScope k(kt, KT_LYNDON, "k_fed", 2 * N);  // flag 1 + FEd 1
+        k_fed<<<nt, WG, 0, s>>>(tg, flag, B, FEd);
     }
 }
 
-void launch_prevc(const Geom& geo, const u8* text, const u8* flag, const u64* FSL, u8* prevc, hipStream_t s) {
+void launch_prevc(const Geom& geo, const u8* text, const u8* flag, Factors fac, u8* prevc, hipStream_t s) {
     if (!geo.N) return;
     const u32 grid = (u32)std::min<u64>((geo.N + 255) / 256, 65535);
     if (((uintptr_t)text & 15) == 0)
-        k_prevc<<<(u32)((geo.N + 4095) / 4096), 256, 0, s>>>(geo, text, flag, FSL, prevc);
+        k_prevc<<<(u32)((geo.N + 4095) / 4096), 256, 0, s>>>(geo, text, flag, fac, prevc);
     else  // caller's device buffer not 16-byte aligned
-        k_prevc1<<<grid, 256, 0, s>>>(geo, text, flag, FSL, prevc);
+        k_prevc1<<<grid, 256, 0, s>>>(geo, text, flag, fac, prevc);
 }
 
 void launch_bbwt_gather(const Geom& geo, const u32* SA, const u8* prevc, u8* out, hipStream_t s) {

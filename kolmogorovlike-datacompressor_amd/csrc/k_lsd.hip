@@ -26,7 +26,7 @@ struct LsdGeom {
     u32 tpb;  // tiles per block
     const u8* text;
     const u8* FEd;    // min(distance to the factor end, 255)
-    const u64* FSL;   // factor start | length << 32
+    Factors fac;      // Lyndon factor starts per block
     __device__ inline bool range(u32 t, u32& lo, u32& hi, u32& b) const {
         b = t / tpb;
         const u32 k = t - b * tpb;
@@ -692,8 +692,8 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
     for (u32 e = 0; e < LSD_PT; ++e) {
         const u32 p = lo + i0 + e;
         if (p < hi && fed[e] < C) {  // the C characters wrap inside the factor
-            const u64 f = g.FSL[p];
-            const u32 fs = (u32)f, m = (u32)(f >> 32);
+            u32 fs, m;
+            g.fac.locate(g.geo, p, fs, m);
             u32 t = p - fs;
             u64 k2 = 0;
             for (u32 k = 0; k < C; ++k) {
@@ -816,7 +816,7 @@ u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w,
 void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s,
                    KTimer* kt) {
     if (!geo.N) return;
-    LsdGeom g{geo, (geo.bs + LSD_T - 1) / LSD_T, t.text, t.FEd, t.FSL};
+    LsdGeom g{geo, (geo.bs + LSD_T - 1) / LSD_T, t.text, t.FEd, t.fac};
     const u32 nt = g.tpb * geo.nb;
     const u64 N = geo.N;
     // D byte digits; the packed codes are left-aligned in them, so the 8 D - C w padding bits
@@ -824,7 +824,7 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
     const u32 bits = t.chars * t.w, D = (bits + 7) / 8, sh = 8 * D - bits;
     const u32 pa = std::min<u32>(4, D), pb = D - pa;
     {
-        // text + FEd 2 (+ FSL near factor ends), KA 4 (+ KB 4)
+        // text + FEd 2 (+ factor starts near factor ends), KA 4 (+ KB 4)
         KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6));
         k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist);
     }

@@ -73,8 +73,8 @@ __device__ inline int size_class(u32 len) { return len <= 1 ? 0 : 32 - __clz(len
 // keys
 // ------------------------------------------------------------------------------------
 __device__ inline u32 cyc_succ(const SortArgs& a, u32 p, u32 h) {
-    const u64 f = a.FSL[p];
-    const u32 fs = (u32)f, m = (u32)(f >> 32);
+    u32 fs, m;
+    a.fac.locate(a.geo, p, fs, m);
     u32 hm = h < m ? h : h % m;
     u32 t = (p - fs) + hm;
     if (t >= m) t -= m;
@@ -88,8 +88,8 @@ __device__ inline u32 cyc_chars(const SortArgs& a, u32 p, u32 off) {
         const u8* t = a.text + p + off;
         return ((u32)t[0] << 24) | ((u32)t[1] << 16) | ((u32)t[2] << 8) | t[3];
     }
-    const u64 f = a.FSL[p];
-    const u32 fs = (u32)f, m = (u32)(f >> 32);
+    u32 fs, m;
+    a.fac.locate(a.geo, p, fs, m);
     u32 t = (p - fs) + off % m, k = 0;
     if (t >= m) t -= m;
 #pragma unroll
@@ -115,7 +115,7 @@ __device__ inline u32 make_key(const SortArgs& a, u32 p, u32 base, u32 end) {
         const u32 q = p + a.h;
         return q < end ? a.RK[q] - base + 1 : 0;
     }
-    if (a.h < a.FEd[p]) return a.RK[p + a.h] - base;  // no wrap: FSL not needed
+    if (a.h < a.FEd[p]) return a.RK[p + a.h] - base;  // no wrap: no factor lookup
     return a.RK[cyc_succ(a, p, a.h)] - base;
 }
 

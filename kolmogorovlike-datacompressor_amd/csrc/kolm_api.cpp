@@ -315,7 +315,7 @@ struct SortOut {
 // Segmented prefix-doubling suffix sort of every block of the batch (k_sort.hip).
 // after_round0 (optional) runs on the host right after round 0 is enqueued (cyclic pass),
 // before the pass waits for its counts: encode_batch hooks the LZ77 launch there.
-SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, const u64* FSL, const u8* FEd,
+SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Factors fac, const u8* FEd,
                   const std::function<void()>& after_round0 = {}) {
     hipStream_t s = c->active;
     const u64 N = geo.N;
@@ -328,7 +328,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
     a.K2 = c->get<u32>("K2", N);
     a.SA2 = c->get<u32>("SA2", N);
     a.K22 = c->get<u32>("K22", N);
-    a.FSL = FSL;
+    a.fac = fac;
     a.FEd = FEd;
     a.blk_split = c->get<u32>("blk_split", geo.nb);
     u32* blk_done = c->get<u32>("blk_done", geo.nb);
@@ -409,7 +409,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
             static const u32 cmax = getenv("KOLM_R0_CMAX") ? (u32)atoi(getenv("KOLM_R0_CMAX")) : 32u;  // A/B (<= 64)
             const u32 C = std::max<u32>(1, std::min<u32>(std::min<u32>(64, cmax), 64 / w));
             h0 = C;
-            R0Bufs r{text, FEd, FSL, code, C, w, c->get<u32>("KP", N), a.K2, a.SA, a.K22, a.SA2, a.RK,
+            R0Bufs r{text, FEd, fac, code, C, w, c->get<u32>("KP", N), a.K2, a.SA, a.K22, a.SA2, a.RK,
                      c->get<u32>("r0hist", nt * 256), c->get<u32>("r0tmax", nt), c->get<u32>("r0tmin", nt),
                      c->get<u32>("r0cmax", nt), c->get<u32>("r0cmin", nt), c->get<u32>("r0hf", nt * WG)};
             out.r0_chars = C;
@@ -461,7 +461,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, con
             a.KP = nullptr;
             if ((u64)h[C_ACTIVE] * 8 > N) {
                 u32* KP = c->get<u32>("KP", N);
-                // cyclic: FEd 1 + RK 4 + KP 4 (FSL only within h of a factor end); linear: RK 4 + KP 4
+                // cyclic: FEd 1 + RK 4 + KP 4 (factor starts only within h of a factor end); linear: RK 4 + KP 4
                 TScope t(c, KOLM_KT_KEYGEN, "k_keypos", N * (cyclic ? 9 : 8));
                 launch_keypos(a, KP, s);
                 a.KP = KP;
@@ -556,28 +556,28 @@ struct Pipeline {
     kolm_stats st{};
     float t_sa = 0, t_lz = 0, t_ent = 0, t_emit = 0;
 
-    // Lyndon factorisation of every block -> FSL (on the active stream)
+    // Lyndon factorisation of every block -> factor-start lists + FEd (on the active stream)
     void lyndon() {
         const u64 N = geo.N;
         const u64 ntiles = (u64)((geo.bs + TILE - 1) / TILE) * geo.nb + 16;
         const u64 nch = (geo.bs + 32767) / 32768 * (u64)geo.nb + 1;  // DUVAL_SPAN
-        launch_lyndon(geo, text, c->get<u8>("flag", N), c->get<u64>("FSL", N), c->get<u8>("FEd", N),
+        launch_lyndon(geo, text, c->get<u8>("flag", N), c->get<u8>("FEd", N),
                       c->get<u32>("lyn_fstart", N), c->get<uint4>("lyn_fpre", nch * 128),
-                      c->get<u32>("lyn_nfac", nch), c->get<u32>("lyn_stack", N), c->get<u32>("lyn_t1", 2 * ntiles + 16),
-                      c->get<u32>("lyn_t2", 2 * ntiles + 2 * geo.nb + 16), c->active, c->kt());
+                      c->get<u32>("lyn_nfac", nch), c->get<u32>("lyn_stack", N), c->get<u32>("lyn_fcount", geo.nb + 1), c->get<u32>("lyn_t1", 2 * ntiles + 16),
+                      c->active, c->kt());
     }
+    Factors factors() { return Factors{c->get<u32>("lyn_stack", geo.N), c->get<u32>("lyn_fcount", geo.nb + 1)}; }
     // omega-order of all rotations of the Lyndon factors + BBWT gather -> "bbwt"
     // cyclic predecessor byte of every position (needs the Lyndon factors only)
     hipEvent_t prevc_ready = nullptr;  // set when prevc() ran on another stream
     void prevc() {
         const u64 N = geo.N;
-        TScope t(c, KOLM_KT_LYNDON, "k_prevc", N * 3);  // flag 1 + text 1 + prevc 1 (FSL at factor starts)
-        launch_prevc(geo, text, c->get<u8>("flag", N), c->get<u64>("FSL", N), c->get<u8>("prevc", N), c->active);
+        TScope t(c, KOLM_KT_LYNDON, "k_prevc", N * 3);  // flag 1 + text 1 + prevc 1 (+ factor starts)
+        launch_prevc(geo, text, c->get<u8>("flag", N), factors(), c->get<u8>("prevc", N), c->active);
     }
     u8* cyclic(const std::function<void()>& after_round0 = {}, u8* out = nullptr) {
         const u64 N = geo.N;
-        u64* FSL = c->get<u64>("FSL", N);
-        SortOut cyc = sort_pass(c, geo, text, true, FSL, c->get<u8>("FEd", N), after_round0);
+        SortOut cyc = sort_pass(c, geo, text, true, factors(), c->get<u8>("FEd", N), after_round0);
         if (!out) out = c->get<u8>("bbwt", N);
         u8* prevc = c->get<u8>("prevc", N);
         if (prevc_ready)

@@ -192,6 +192,29 @@ __device__ inline u32 xcd_tile() {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
 }
 
+// Lyndon factors of every block as sorted factor-start lists (k_duval_merge): block b's
+// count[b] starts sit at start[geo.base(b) ..], the first one = base(b).  Read only where
+// a rotation wraps (within a few characters of a factor end), so a block's few dozen
+// starts stay in L2 and no per-position factor record is materialised.
+struct Factors {
+    const u32* start;
+    const u32* count;
+    // p's factor: start fs and length m (binary search over the block's starts)
+    __device__ inline void locate(const Geom& geo, u32 p, u32& fs, u32& m) const {
+        const u32 b = geo.block_of(p);
+        const u32* s = start + geo.base(b);
+        const u32 n = count[b];
+        u32 lo = 0, len = n;
+        while (len > 1) {
+            const u32 half = len >> 1;
+            if (s[lo + half] <= p) lo += half;
+            len -= half;
+        }
+        fs = s[lo];
+        m = (lo + 1 < n ? s[lo + 1] : geo.end(b)) - fs;
+    }
+};
+
 // Everything the suffix-sorting kernels touch for one pass (linear or cyclic).
 struct SortArgs {
     Geom geo;
@@ -201,8 +224,8 @@ struct SortArgs {
     u32* K2;
     u32* SA2;
     u32* K22;
-    const u64* FSL;    // cyclic: start (low 32) | length (high 32) of each position's Lyndon factor
-    const u8* FEd;     // cyclic: min(distance to the factor end, 255): FSL is read only near the end
+    Factors fac;       // cyclic: Lyndon factor starts per block
+    const u8* FEd;     // cyclic: min(distance to the factor end, 255): fac is read only near the end
     u32* blk_split;    // [nb] set to 1 when a group of block b split this round
     const u32* blk_done;  // [nb] cyclic: block converged (no further splits possible)
     int cyclic;
@@ -274,10 +297,9 @@ void launch_rounds_sum(const u32* blk_done, u32 nb, u32 rounds, u64* out, hipStr
 void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, u32 round, hipStream_t s);
 
 // ---- k_blocks.hip: per-block scans, Lyndon factors, BBWT gather ----
-void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u64* FSL, u8* FEd, u32* fstart, uint4* fpre, u32* nfac,
-                   u32* stack, u32* tile_tmp, u32* tile_tmp2, hipStream_t s, KTimer* kt = nullptr);
-void launch_lyndon_isa(const Geom& geo, const u32* RK, u8* flag, u32* tile_tmp, u32* tile_tmp2, hipStream_t s);
-void launch_prevc(const Geom& geo, const u8* text, const u8* flag, const u64* FSL, u8* prevc, hipStream_t s);
+void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fstart, uint4* fpre, u32* nfac,
+                   u32* stack, u32* fcount, u32* tile_tmp, hipStream_t s, KTimer* kt = nullptr);
+void launch_prevc(const Geom& geo, const u8* text, const u8* flag, Factors fac, u8* prevc, hipStream_t s);
 void launch_bbwt_gather(const Geom& geo, const u32* SA, const u8* prevc, u8* out, hipStream_t s);
 
 // ---- k_lsd.hip: per-block LSD radix passes: round 0 of the cyclic sort ----
@@ -285,7 +307,7 @@ u32 lsd_tiles(const Geom& geo);
 struct R0Bufs {
     const u8* text;
     const u8* FEd;    // min(distance to the factor end, 255)
-    const u64* FSL;   // factor start | length << 32 (read only where the C characters wrap)
+    Factors fac;      // Lyndon factor starts (read only where the C characters wrap)
     const u8* code;   // [nb * 256] per-block byte -> code (launch_alpha)
     u32 chars;        // C rotation characters per key
     u32 w;            // bits per code

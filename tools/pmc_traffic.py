@@ -32,7 +32,7 @@ FAMILY = [
     ("k_duval", "lyndon_gather"), ("k_prevc", "lyndon_gather"), ("k_keypos", "keygen"),
     ("k_mtf", "mtf"), ("k_sizes", "sizes"), ("k_mdl", "sizes"), ("k_offsets", "sizes"),
     ("k_emit", "emit"), ("k_rice", "emit"), ("k_simple", "emit"), ("k_lz_emit", "emit"),
-    ("k_tile", "lyndon_gather"), ("k_lyn", "lyndon_gather"), ("k_fsfl", "lyndon_gather"),
+    ("k_tile", "lyndon_gather"), ("k_lyn", "lyndon_gather"), ("k_fed", "lyndon_gather"),
     ("k_bbwt_gather", "lyndon_gather"), ("k_prev3", "lyndon_gather"),
 ]
 
