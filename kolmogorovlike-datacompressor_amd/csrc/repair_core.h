@@ -47,8 +47,15 @@ using u8 = uint8_t;
 using u32 = uint32_t;
 using u64 = uint64_t;
 
-constexpr u32 NT = 1024;          // threads of the block's workgroup (512 measured: the hot-path
-                                  // streams then run beside it, but Re-Pair itself is 30 % slower)
+// KOLM_RP_NT / KOLM_RP_RK: compile-time A/B knobs (tools/rp_variants.sh)
+#ifndef KOLM_RP_NT
+#define KOLM_RP_NT 1024
+#endif
+constexpr u32 NT = KOLM_RP_NT;    // threads of the block's workgroup (NT divides 2048).  At 1024 the
+                                  // kernel holds 128 VGPRs x 4 waves per SIMD (the whole register file),
+                                  // so no other stream's kernel runs on a CU beside it; 512 (170 VGPRs,
+                                  // 2 waves) leaves registers, but its 94 KB of LDS still keeps the
+                                  // 38-50 KB LDS kernels of the hot path off the CU (measured r3)
 constexpr u32 W = 512;            // max rounds (members) per batch (<= NT: one window of NT entries)
 constexpr u32 CAPR = 1u << 16;    // occurrence-region entries per batch beyond its first member
 constexpr u32 SORT_LDS = 4096;    // level lists up to this size are sorted in LDS
@@ -59,7 +66,10 @@ constexpr u64 EMPTY = ~0ull;
 constexpr u32 BMAX = 1u << 22;    // owner tags (BMAX - batch) * W + member: batch < BMAX
 constexpr u32 NBASE = 65536;      // ids of the byte pairs: (a << 8) | b
 constexpr u32 MAX_N = 1u << 22;   // block length limit of the device Re-Pair
-constexpr u32 RK = 4;             // occurrences per thread per step in the occurrence loops
+#ifndef KOLM_RP_RK
+#define KOLM_RP_RK 4
+#endif
+constexpr u32 RK = KOLM_RP_RK;    // occurrences per thread per step in the occurrence loops
 constexpr u32 AGG_MIN = 2048;     // batches with at least this many occurrences aggregate atomics
 constexpr u32 WIN_MIN = 32;       // smallest adaptive window (members per batch)
 constexpr u32 NCNT = 2048;        // batches creating at most this many pairs count them in LDS
