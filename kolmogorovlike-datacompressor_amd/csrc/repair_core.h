@@ -63,7 +63,8 @@ constexpr u32 QLIM = 4096;        // level cache: the rescan picks flow so that 
 constexpr u32 NIL = 0xFFFFFFFFu;
 constexpr u32 DEAD = 0xFFFFFFFFu;
 constexpr u64 EMPTY = ~0ull;
-constexpr u32 BMAX = 1u << 22;    // owner tags (BMAX - batch) * W + member: batch < BMAX
+constexpr u32 BMAX = 1u << 21;    // mark tags ((BMAX - b) * W + member) << 1 | s, b = batch - tbase < BMAX
+                                  // (the marks are reset and tbase moved when b reaches BMAX - 1)
 constexpr u32 NBASE = 65536;      // ids of the byte pairs: (a << 8) | b
 constexpr u32 MAX_N = 1u << 22;   // block length limit of the device Re-Pair
 #ifndef KOLM_RP_RK
@@ -80,28 +81,33 @@ enum : u32 { P_INIT = 0, P_LVSCAN, P_LVSORT, P_WINDOW, P_GATHER, P_CHAINS, P_SEL
              P_SER, P_APPLY_A2, P_N };
 enum : u32 { RE_OK = 0, RE_CAP = 1, RE_LOOP = 2, RE_LEN = 3 };
 
-// Per position, one 32-byte record (AoS): an occurrence's neighbourhood (prev, next and
-// their marks) is a few cache lines instead of a line per field.
-//   sym    symbol (DEAD once merged into its left neighbour)
+// Per position, one 16-byte record: the live sequence.  Every field an occurrence needs
+// from a neighbour (its symbol, its links, the pair that starts there) is one vector load.
 //   nxt/prv  the live doubly linked list
-//   opair  id of the pair starting here (NIL: none)
-//   ctag   batch*W + member of a chosen occurrence;  owner: min span owner tag this batch
-//   oidx   occurrence index in this batch ((a,a) chains)
-// Field order: the pairs read together are adjacent (nxt+opair in the gather; the 16-byte
-// halves in the conflict scan).
-struct alignas(32) Node {
-    u32 nxt, opair, prv, sym, owner, ctag, oidx, pad;
+//   sym      symbol (DEAD once merged into its left neighbour)
+//   opair    id of the pair starting here (NIL: none)
+// The per-batch marks live beside it in mark[] (one word per position):
+//   mark = min over the chosen occurrences covering the position of
+//          ((BMAX - batch) * W + member) << 1 | (1 for the span's second position)
+// so an earlier member's span (conflict), the same member's second position (left
+// neighbour replaced too) and the same member's start (right neighbour replaced too) are
+// all read from one word.  oidx[] (occurrence index by position) is used by (a,a) runs only.
+struct alignas(16) Node {
+    u32 nxt, prv, sym, opair;
 };
 
 // Per-block workspace (all device pointers).  Sizes for a block of length n:
-//   n:      nd (32 B each);  opos omem od0 od1 ot0 ot1 oidl oidr oj op oq
+//   n:      nd (16 B each), mark, oidx;  opos omem od0 od1 ot0 ot1 oidl oidr oj op oq
+//           ox oy opj opp onp (occurrence neighbourhoods, by occurrence index)
 //   3n+16:  occpos          PC = NBASE + 2n + 16: cnt poff plen pkey, lists (3 x key+id)
 //   HS = pow2 >= n + 64:     hkey hval;  n + 16: husd;  n/2 + 16: rules
 struct Block {
     const u8* text;
     u32 n;
-    Node* nd;  // per position: the live sequence and its per-batch marks
+    Node* nd;  // per position: the live sequence
+    u32 *mark, *oidx;
     u32 *opos, *omem, *od0, *od1, *ot0, *ot1, *oidl, *oidr, *oj, *op, *oq;
+    u32 *ox, *oy, *opj, *opp, *onp;
     u32* occpos;
     u32 *cnt, *poff, *plen;
     u64* pkey;
@@ -127,7 +133,7 @@ struct Shared {
     u64 skey[SORT_LDS];
     u32 sval[SORT_LDS];
     u32 f, lp, lsize, M, V, T, tot, nocc, npairs, next_sym, nrules, pool, batch, hused, nlate;
-    u32 t1, t2, ts, any_aa, cut, maxc, err, total, levels;
+    u32 t1, t2, ts, any_aa, cut, maxc, err, total, levels, tbase, hovf;
     u32 flow, qn, qn2, qvalid;  // level cache: Q = every pair with count >= flow
     u32 mcap;                   // adaptive window: members gathered per batch (<= W)
     u32 ncnt[NCNT];             // new pairs of a batch (id - npairs < NCNT): counts, then fill counters
@@ -147,7 +153,8 @@ RP_HD inline u64 workspace_layout(char* base, u32 n, Block& B) {
     u32 HS = 64;
     while (HS < n + 64) HS <<= 1;
     B.nd = (Node*)take(N * sizeof(Node));
-    u32** n32[] = {&B.opos, &B.omem, &B.od0, &B.od1, &B.ot0, &B.ot1, &B.oidl, &B.oidr, &B.oj, &B.op, &B.oq, &B.husd};
+    u32** n32[] = {&B.mark, &B.oidx, &B.opos, &B.omem, &B.od0, &B.od1, &B.ot0, &B.ot1, &B.oidl, &B.oidr,
+                   &B.oj, &B.op, &B.oq, &B.ox, &B.oy, &B.opj, &B.opp, &B.onp, &B.husd};
     for (u32** p : n32) *p = (u32*)take(N * 4);
     B.occpos = (u32*)take(3 * N * 4);
     B.cnt = (u32*)take(PC * 4);
@@ -241,6 +248,26 @@ RP_HD inline u32 hash_insert_wave(E& ex, const Block& B, Shared& sh, const HTab&
     u32 s = 0;
     if (act && ex.is_leader(ld)) s = hash_insert(ex, B, sh, h, key);
     return ex.from_leader(s, ld);
+}
+
+// Claim key's slot in the batch's LDS table (ids are given out afterwards, in slot order).
+// A probe run longer than HPROBE (the table nearly full) flags an overflow instead: the
+// batch then redoes its keys in the global table.
+constexpr u32 HPROBE = 128;
+template <class E>
+RP_HD inline u32 hash_claim(E& ex, Shared& sh, u64 key) {
+    u32 s = hslot(key, SORT_LDS - 1);
+    for (u32 k = 0; k < HPROBE; ++k) {
+        const u64 cur = sh.skey[s];
+        if (cur == key) return s;
+        if (cur == EMPTY) {
+            const u64 old = ex.cas64(&sh.skey[s], EMPTY, key);
+            if (old == EMPTY || old == key) return s;
+        }
+        s = (s + 1) & (SORT_LDS - 1);
+    }
+    ex.max(&sh.hovf, 1u);
+    return 0;
 }
 
 // Sort key/id[0..n) ascending by key (keys unique); tk/ti is scratch of the same size.
@@ -364,23 +391,16 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
         if (t == 0) {
             sh.pool = 0; sh.npairs = NBASE; sh.next_sym = 256; sh.nrules = 0; sh.batch = 0;
             sh.lp = 0; sh.lsize = 0; sh.f = 0; sh.hused = 0; sh.nlate = 0; sh.err = RE_OK; sh.levels = 0;
-            sh.qvalid = 0; sh.qn = 0; sh.flow = NIL; sh.mcap = W;
+            sh.qvalid = 0; sh.qn = 0; sh.flow = NIL; sh.mcap = W; sh.tbase = 0;
         }
     });
     ex.par([&](u32 t) {
         for (u32 i = t; i < n; i += NT) {
-            B.nd[i].sym = B.text[i];
-            B.nd[i].nxt = i + 1 < n ? i + 1 : NIL;
-            B.nd[i].prv = i ? i - 1 : NIL;
-            B.nd[i].ctag = NIL;
-            B.nd[i].owner = NIL;
-            if (i + 1 < n) {
-                const u32 code = ((u32)B.text[i] << 8) | B.text[i + 1];
-                B.nd[i].opair = code;
-                ex.add(&B.cnt[code], 1u);
-            } else {
-                B.nd[i].opair = NIL;
-            }
+            const bool last = i + 1 >= n;
+            const u32 code = last ? NIL : ((u32)B.text[i] << 8) | B.text[i + 1];
+            B.nd[i] = Node{last ? NIL : i + 1, i ? i - 1 : NIL, B.text[i], code};
+            B.mark[i] = NIL;
+            if (!last) ex.add(&B.cnt[code], 1u);
         }
     });
     ex.par([&](u32 t) {
@@ -549,10 +569,16 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
             sort_list(ex, sh, lk, li, tk, ti, sh.lsize);
         }
         ex.mark(P_WINDOW);
+        if (sh.batch - sh.tbase >= BMAX - 1) {  // mark tags exhausted (> 2M batches): start over
+            ex.par([&](u32 t) {
+                for (u32 i = t; i < n; i += NT) B.mark[i] = NIL;
+            });
+            ex.par([&](u32 t) { if (t == 0) sh.tbase = sh.batch; });
+        }
         const u32 f = sh.f;
-        const u32 batch = sh.batch;
-        const u32 ctag0 = batch * W;
-        const u32 otag0 = (BMAX - batch) * W;
+        const u32 otag0 = (BMAX - (sh.batch - sh.tbase)) * W;
+        // this batch's marks of member m: start (m2s(m)) / second position (m2s(m) | 1)
+        auto m2s = [&](u32 m) { return (otag0 + m) << 1; };
         const u32 X0 = sh.next_sym;
         // ---- window: the next valid level entries (count still f), in list order ----
         ex.par([&](u32 t) {
@@ -563,7 +589,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
             for (u32 e = t; e < NCNT; e += NT) sh.ncnt[e] = 0;
             if (t == 0) {
                 sh.cut = NIL; sh.any_aa = 0; sh.nocc = 0; sh.t1 = NIL; sh.t2 = NIL; sh.ts = NIL;
-                sh.hused = 0; sh.nlate = 0;
+                sh.hused = 0; sh.nlate = 0; sh.hovf = 0;
             }
         });
         ex.scan(sh.scan, &sh.V);
@@ -615,11 +641,12 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
         // Wave-aggregated atomics pay off only when a batch has many occurrences (few hot
         // words then take thousands of +-1); below AGG_MIN they cost more than they save.
         const bool agg_g = tot >= AGG_MIN;
-        // ---- gather the members' live occurrences (+ chosen-occurrence marks when no
-        //      member is an (a,a) pair: then every live occurrence is replaced) ----
+        // ---- gather the members' live occurrences with their neighbourhoods (the links and
+        //      symbols do not change before apply 2), + the chosen-occurrence marks when no
+        //      member is an (a,a) pair: then every live occurrence is replaced ----
         ex.par([&](u32 t) {
             for (u32 e0 = 0; e0 < tot; e0 += RK * NT) {
-                u32 pos[RK], lo[RK], nx[RK];
+                u32 pos[RK], lo[RK], p[RK], j[RK], q[RK], o[RK];
                 bool valid[RK];
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
@@ -639,22 +666,45 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
                     const bool in = e0 + k * NT + t < tot;
-                    const u32 op = in ? B.nd[pos[k]].opair : NIL;  // nxt + opair: one 8-byte load
-                    nx[k] = in ? B.nd[pos[k]].nxt : 0u;
-                    valid[k] = in && op == sh.m_id[lo[k]];
+                    const Node c = B.nd[in ? pos[k] : 0u];
+                    valid[k] = in && c.opair == sh.m_id[lo[k]];
+                    j[k] = c.nxt;
+                    p[k] = valid[k] ? c.prv : NIL;
+                }
+                // each field is stored as soon as it arrives (fewer live registers)
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    o[k] = ex.append(&sh.nocc, valid[k]);
+                    if (valid[k]) {
+                        B.opos[o[k]] = pos[k];
+                        B.omem[o[k]] = lo[k];
+                        B.oj[o[k]] = j[k];
+                        B.op[o[k]] = p[k];
+                    }
                 }
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
-                    const u32 o = ex.append(&sh.nocc, valid[k]);
+                    const Node cj = B.nd[valid[k] ? j[k] : 0u];
+                    const Node cp = B.nd[p[k] != NIL ? p[k] : 0u];
+                    q[k] = cj.nxt;
                     if (valid[k]) {
-                        B.opos[o] = pos[k];
-                        B.omem[o] = lo[k];
+                        B.oq[o[k]] = cj.nxt;
+                        B.opj[o[k]] = cj.opair;
+                        B.ox[o[k]] = cp.sym;
+                        B.opp[o[k]] = cp.opair;
+                        B.onp[o[k]] = cp.prv;
+                    }
+                }
+#pragma unroll
+                for (u32 k = 0; k < RK; ++k) {
+                    const u32 y = B.nd[valid[k] && q[k] != NIL ? q[k] : 0u].sym;
+                    if (valid[k]) {
+                        B.oy[o[k]] = y;
                         if (aa) {
-                            B.nd[pos[k]].oidx = o;
+                            B.oidx[pos[k]] = o[k];
                         } else {
-                            B.nd[pos[k]].ctag = ctag0 + lo[k];
-                            ex.min(&B.nd[pos[k]].owner, otag0 + lo[k]);
-                            ex.min(&B.nd[nx[k]].owner, otag0 + lo[k]);
+                            ex.min(&B.mark[pos[k]], m2s(lo[k]));
+                            ex.min(&B.mark[j[k]], m2s(lo[k]) | 1u);
                         }
                     }
                     if (!aa) ex.add_agg(&sh.m_repl[lo[k]], valid[k], agg_g);
@@ -670,11 +720,11 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
         if (aa) {
             ex.par([&](u32 t) {
                 for (u32 o = t; o < nocc; o += NT) {
-                    const u32 m = B.omem[o], pos = B.opos[o];
+                    const u32 m = B.omem[o];
                     u32 pp = NIL;
                     if (sh.m_a[m] == sh.m_b[m]) {
-                        const u32 p = B.nd[pos].prv;
-                        if (p != NIL && B.nd[p].opair == sh.m_id[m]) pp = B.nd[p].oidx;
+                        const u32 p = B.op[o];  // the pair at p (gathered): the same (a,a)?
+                        if (p != NIL && B.opp[o] == sh.m_id[m]) pp = B.oidx[p];
                     }
                     B.ot0[o] = pp;
                     B.od0[o] = pp != NIL ? 1u : 0u;
@@ -711,74 +761,64 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
             ex.par([&](u32 t) {
                 for (u32 o = t; o < nocc; o += NT) {
                     const bool ch = !(dist[o] & 1u);
-                    const u32 m = B.omem[o], i = B.opos[o];
+                    const u32 m = B.omem[o];
                     if (ch) {
-                        B.nd[i].ctag = ctag0 + m;
-                        ex.min(&B.nd[i].owner, otag0 + m);
-                        ex.min(&B.nd[B.nd[i].nxt].owner, otag0 + m);
+                        ex.min(&B.mark[B.opos[o]], m2s(m));
+                        ex.min(&B.mark[B.oj[o]], m2s(m) | 1u);
                     }
                     ex.add_agg(&sh.m_repl[m], ch, agg);
                 }
             });
         }
         ex.mark(P_SELECT);
-        // ---- conflicts (footprint vs earlier spans), left-neighbour uniformity; the
-        //      neighbourhood of every chosen occurrence is kept for the apply phases ----
+        // ---- conflicts (footprint {p, i, j, q} vs earlier members' spans), left-neighbour
+        //      uniformity, the replaced neighbours; one mark word per footprint position ----
         ex.par([&](u32 t) {
             for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
-                bool act[RK], conf[RK];
-                u32 m[RK], i[RK], p[RK], j[RK], q[RK], pp[RK], sp[RK], sq[RK], cq[RK], cpp[RK];
-                // owner in [otag0, otag0 + m) = an earlier member of this batch
-                auto early = [&](u32 w, u32 mm) { return w >= otag0 && w < otag0 + mm; };
+                bool act[RK];
+                u32 m[RK], i[RK], p[RK], j[RK], q[RK], wi[RK], wj[RK], wp[RK], wq[RK];
+                // mark of an earlier member of this batch (either position of its span)
+                auto early = [&](u32 w, u32 mm) { return w >= m2s(0) && w < m2s(mm); };
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
                     const u32 o = o0 + k * NT;
                     act[k] = o < nocc && !(aa && (dist[o] & 1u));
                     m[k] = act[k] ? B.omem[o] : 0u;
                     i[k] = act[k] ? B.opos[o] : 0u;
+                    j[k] = act[k] ? B.oj[o] : 0u;
+                    p[k] = act[k] ? B.op[o] : NIL;
+                    q[k] = act[k] ? B.oq[o] : NIL;
                 }
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
-                    const Node x = B.nd[act[k] ? i[k] : 0u];
-                    p[k] = act[k] ? x.prv : NIL;
-                    j[k] = act[k] ? x.nxt : 0u;
-                    conf[k] = act[k] && early(x.owner, m[k]);
-                }
-#pragma unroll
-                for (u32 k = 0; k < RK; ++k) {
-                    const Node y = B.nd[act[k] ? j[k] : 0u];
-                    q[k] = act[k] ? y.nxt : NIL;
-                    conf[k] = conf[k] || (act[k] && early(y.owner, m[k]));
-                    const bool hp = p[k] != NIL;
-                    const Node z = B.nd[hp ? p[k] : 0u];
-                    conf[k] = conf[k] || (hp && early(z.owner, m[k]));
-                    pp[k] = hp ? z.prv : NIL;
-                    sp[k] = hp ? z.sym : NIL;
-                }
-#pragma unroll
-                for (u32 k = 0; k < RK; ++k) {
-                    const bool hq = q[k] != NIL;
-                    const Node w = B.nd[hq ? q[k] : 0u];
-                    conf[k] = conf[k] || (hq && early(w.owner, m[k]));
-                    cq[k] = hq ? w.ctag : NIL;
-                    sq[k] = hq ? w.sym : NIL;
-                    cpp[k] = pp[k] != NIL ? B.nd[pp[k]].ctag : NIL;
+                    wi[k] = act[k] ? B.mark[i[k]] : NIL;
+                    wj[k] = act[k] ? B.mark[j[k]] : NIL;
+                    wp[k] = p[k] != NIL ? B.mark[p[k]] : NIL;
+                    wq[k] = q[k] != NIL ? B.mark[q[k]] : NIL;
                 }
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
                     if (!act[k]) continue;
                     const u32 o = o0 + k * NT;
-                    if (conf[k]) ex.min(&sh.t1, m[k]);
-                    const bool leftc = pp[k] != NIL && cpp[k] == ctag0 + m[k];
-                    const bool rightc = q[k] != NIL && cq[k] == ctag0 + m[k];
-                    const u32 x = (p[k] != NIL && !leftc) ? sp[k] : NIL;
+                    if (early(wi[k], m[k]) || early(wj[k], m[k]) || early(wp[k], m[k]) || early(wq[k], m[k]))
+                        ex.min(&sh.t1, m[k]);
+                    // p is the second position of a chosen occurrence of this member (its start
+                    // pp becomes X too: the new left pair is (X, X), counted by that occurrence);
+                    // q starts one (the new right pair is (X, X))
+                    const bool leftc = p[k] != NIL && wp[k] == (m2s(m[k]) | 1u);
+                    const bool rightc = q[k] != NIL && wq[k] == m2s(m[k]);
+                    const u32 x = (p[k] != NIL && !leftc) ? B.ox[o] : NIL;
                     ex.min(&sh.m_lmin[m[k]], x);
                     ex.max(&sh.m_lmax[m[k]], x);
-                    B.oj[o] = j[k];
-                    B.op[o] = leftc ? NIL : p[k];
-                    B.oq[o] = q[k];
-                    B.oidl[o] = x;                                                  // left symbol
-                    B.oidr[o] = q[k] == NIL ? NIL : rightc ? X0 + m[k] : sq[k];  // right symbol
+                    if (leftc) {
+                        B.op[o] = NIL;
+                        // B.onp[o] keeps pp: i's new left neighbour
+                    } else {
+                        B.onp[o] = p[k];
+                    }
+                    B.oidl[o] = x;                                                     // left symbol
+                    B.oidr[o] = q[k] == NIL ? NIL : rightc ? X0 + m[k] : B.oy[o];  // right symbol
+                    B.oy[o] = rightc ? 1u : 0u;  // q's link is rewritten by its own occurrence
                 }
             }
         });
@@ -803,17 +843,13 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
         T = sh.ts < T ? sh.ts : T;
         const bool stop = sh.ts != NIL && sh.ts < sh.t1 && sh.ts < sh.t2;
         if (T == 0) break;  // the next round replaces < 2 occurrences (PY:1879-1882)
-        // at most 2 new keys per replaced occurrence: the LDS table while that keeps it at
-        // most half full
-        const bool hglob = nocc > SORT_LDS / 4;
-        const HTab ht = hglob ? HTab{B.hkey, B.hval, B.hmask, true} : HTab{sh.skey, sh.sval, SORT_LDS - 1, false};
         ex.mark(P_APPLY_A);
-        // ---- apply 1: destroy the old pair occurrences; register the new pair keys (the
-        //      inserting thread allocates the id) and keep each occurrence's hash slots ----
+        // ---- apply 1: destroy the old pair occurrences; claim the new pair keys in the
+        //      batch's LDS table (slots kept per occurrence in ox (left) / opj (right)) ----
         ex.par([&](u32 t) {
             for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
                 bool act[RK];
-                u32 m[RK], p[RK], j[RK], q[RK], xl[RK], yr[RK], pj[RK], pp[RK];
+                u32 m[RK], p[RK], q[RK], xl[RK], yr[RK], pj[RK], pp[RK];
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
                     const u32 o = o0 + k * NT;
@@ -821,15 +857,11 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                     m[k] = act[k] ? B.omem[o] : 0u;
                     act[k] = act[k] && m[k] < T;
                     p[k] = act[k] ? B.op[o] : NIL;
-                    j[k] = act[k] ? B.oj[o] : 0u;
                     q[k] = act[k] ? B.oq[o] : NIL;
                     xl[k] = act[k] ? B.oidl[o] : 0u;
                     yr[k] = act[k] ? B.oidr[o] : 0u;
-                }
-#pragma unroll
-                for (u32 k = 0; k < RK; ++k) {
-                    pj[k] = q[k] != NIL ? B.nd[j[k]].opair : 0u;
-                    pp[k] = p[k] != NIL ? B.nd[p[k]].opair : 0u;
+                    pj[k] = q[k] != NIL ? B.opj[o] : 0u;  // pairs at j and p (gathered)
+                    pp[k] = p[k] != NIL ? B.opp[o] : 0u;
                 }
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
@@ -838,14 +870,51 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                     ex.sub_agg(&B.cnt[pj[k]], hq, agg);
                     ex.sub_agg(&B.cnt[pp[k]], hp, agg);
                     const u32 X = X0 + m[k];
-                    const u32 sr = hash_insert_wave(ex, B, sh, ht, pkey_of(X, yr[k]), hq, agg);
-                    const u32 sl = hash_insert_wave(ex, B, sh, ht, pkey_of(xl[k], X), hp, agg);
                     const u32 o = o0 + k * NT;
-                    if (hq) B.oidr[o] = sr;
-                    if (hp) B.oidl[o] = sl;
+                    if (hq) B.opj[o] = hash_claim(ex, sh, pkey_of(X, yr[k]));
+                    if (hp) B.ox[o] = hash_claim(ex, sh, pkey_of(xl[k], X));
                 }
             }
         });
+        // more distinct new keys than the LDS table holds (rare: the big batches of text
+        // create a few dozen): every key goes through the block's global table instead
+        const bool hglob = sh.hovf != 0;
+        const HTab ht = hglob ? HTab{B.hkey, B.hval, B.hmask, true} : HTab{sh.skey, sh.sval, SORT_LDS - 1, false};
+        if (hglob) {
+            ex.par([&](u32 t) {
+                for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
+#pragma unroll
+                    for (u32 k = 0; k < RK; ++k) {
+                        const u32 o = o0 + k * NT;
+                        bool act = o < nocc && !(aa && (dist[o] & 1u));
+                        const u32 m = act ? B.omem[o] : 0u;
+                        act = act && m < T;
+                        const bool hq = act && B.oq[o] != NIL, hp = act && B.op[o] != NIL;
+                        const u32 X = X0 + m;
+                        const u32 sr = hash_insert_wave(ex, B, sh, ht, pkey_of(X, hq ? B.oidr[o] : 0u), hq, agg);
+                        const u32 sl = hash_insert_wave(ex, B, sh, ht, pkey_of(hp ? B.oidl[o] : 0u, X), hp, agg);
+                        if (hq) B.opj[o] = sr;
+                        if (hp) B.ox[o] = sl;
+                    }
+                }
+            });
+        } else {
+            // ids of the claimed keys, in slot order
+            const u32 np = sh.npairs;
+            ex.par([&](u32 t) {
+                for (u32 s0 = 0; s0 < SORT_LDS; s0 += NT) {
+                    const u64 key = sh.skey[s0 + t];
+                    const bool used = key != EMPTY;
+                    const u32 u = ex.append(&sh.hused, used);
+                    if (used) {
+                        sh.sval[s0 + t] = np + u;
+                        B.pkey[np + u] = key;
+                        B.cnt[np + u] = 0;
+                        B.plen[np + u] = 0;
+                    }
+                }
+            });
+        }
         ex.mark(P_APPLY_A2);
         // ---- apply 2: count the new pair occurrences, rewrite the sequence ----
         const bool lcnt = sh.hused <= NCNT;  // new-pair counters in LDS
@@ -854,6 +923,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
             for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
                 bool act[RK];
                 u32 m[RK], i[RK], j[RK], q[RK], p[RK], idr[RK], idl[RK];
+                bool rc[RK];
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
                     const u32 o = o0 + k * NT;
@@ -864,8 +934,9 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                     j[k] = act[k] ? B.oj[o] : 0u;
                     q[k] = act[k] ? B.oq[o] : NIL;
                     p[k] = act[k] ? B.op[o] : NIL;
-                    idr[k] = q[k] != NIL ? B.oidr[o] : 0u;  // hash slots (apply 1)
-                    idl[k] = p[k] != NIL ? B.oidl[o] : 0u;
+                    idr[k] = q[k] != NIL ? B.opj[o] : 0u;  // hash slots (apply 1)
+                    idl[k] = p[k] != NIL ? B.ox[o] : 0u;
+                    rc[k] = act[k] && B.oy[o] != 0u;
                 }
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
@@ -889,12 +960,11 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                         B.oidl[o] = idl[k];
                         B.nd[p[k]].opair = idl[k];
                     }
-                    B.nd[i[k]].sym = X0 + m[k];
-                    B.nd[i[k]].nxt = q[k];
-                    if (hq) B.nd[q[k]].prv = i[k];
-                    B.nd[j[k]].sym = DEAD;
-                    B.nd[j[k]].opair = NIL;
-                    B.nd[i[k]].opair = idr[k];
+                    // i and j are written whole (one 16-byte store each); q's link only when q
+                    // does not start a chosen occurrence itself (that one writes its node)
+                    B.nd[i[k]] = Node{q[k], B.onp[o], X0 + m[k], idr[k]};
+                    B.nd[j[k]] = Node{NIL, NIL, DEAD, NIL};
+                    if (hq && !rc[k]) B.nd[q[k]].prv = i[k];
                 }
             }
         });
