@@ -137,6 +137,7 @@ struct DevExec {
     __device__ inline u32 sub(u32* p, u32 v) { return atomicSub(p, v); }
     __device__ inline u32 min(u32* p, u32 v) { return atomicMin(p, v); }
     __device__ inline u32 max(u32* p, u32 v) { return atomicMax(p, v); }
+    __device__ inline u32 cas32(u32* p, u32 cmp, u32 v) { return atomicCAS(p, cmp, v); }
     __device__ inline u64 cas64(u64* p, u64 cmp, u64 v) {
         return (u64)atomicCAS((unsigned long long*)p, (unsigned long long)cmp, (unsigned long long)v);
     }

@@ -74,6 +74,7 @@ constexpr u32 RK = KOLM_RP_RK;    // occurrences per thread per step in the occu
 constexpr u32 AGG_MIN = 2048;     // batches with at least this many occurrences aggregate atomics
 constexpr u32 WIN_MIN = 32;       // smallest adaptive window (members per batch)
 constexpr u32 NCNT = 2048;        // batches creating at most this many pairs count them in LDS
+constexpr u32 MMAP = 1024;        // member map (pair id -> member index) slots, in sval[0 .. 2 MMAP)
 
 enum : u32 { RS_SIZE = 0, RS_RULES, RS_FINAL, RS_BATCHES, RS_ERR, RS_LEVELS, RS_N };
 // profile sections (ex.mark(id): time since the previous mark is charged to the previous id)
@@ -268,6 +269,24 @@ RP_HD inline u32 hash_claim(E& ex, Shared& sh, u64 key) {
     }
     ex.max(&sh.hovf, 1u);
     return 0;
+}
+
+// The window's member map (LDS, open addressing over sval[0 .. MMAP) keys and
+// sval[MMAP .. 2 MMAP) member indices): which pair ids are members of this batch.
+RP_HD inline u32 mslot(u32 id) { return (id * 0x9E3779B1u) >> 22; }  // 10 bits = MMAP slots
+template <class E>
+RP_HD inline void member_put(E& ex, Shared& sh, u32 id, u32 r) {
+    u32 s = mslot(id);
+    while (ex.cas32(&sh.sval[s], NIL, id) != NIL) s = (s + 1) & (MMAP - 1);
+    sh.sval[MMAP + s] = r;
+}
+RP_HD inline u32 member_of(const Shared& sh, u32 id) {
+    if (id == NIL) return NIL;
+    for (u32 s = mslot(id);; s = (s + 1) & (MMAP - 1)) {
+        const u32 k = sh.sval[s];
+        if (k == id) return sh.sval[MMAP + s];
+        if (k == NIL) return NIL;
+    }
 }
 
 // Sort key/id[0..n) ascending by key (keys unique); tk/ti is scratch of the same size.
@@ -586,6 +605,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
             sh.scan[t] = idx < sh.lsize && B.cnt[li[idx]] == f ? 1u : 0u;
             sh.scan2[t] = 0;
             for (u32 e = t; e < SORT_LDS; e += NT) sh.skey[e] = EMPTY;  // the LDS key table (HTab)
+            for (u32 e = t; e < MMAP; e += NT) sh.sval[e] = NIL;        // the member map
             for (u32 e = t; e < NCNT; e += NT) sh.ncnt[e] = 0;
             if (t == 0) {
                 sh.cut = NIL; sh.any_aa = 0; sh.nocc = 0; sh.t1 = NIL; sh.t2 = NIL; sh.ts = NIL;
@@ -612,6 +632,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                 sh.m_lmax[r] = 0;
                 sh.scan2[r] = len;
                 if (a == b) sh.any_aa = 1;
+                member_put(ex, sh, id, r);
             }
         });
         if (sh.V == 0) {
@@ -641,10 +662,99 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
         // Wave-aggregated atomics pay off only when a batch has many occurrences (few hot
         // words then take thousands of +-1); below AGG_MIN they cost more than they save.
         const bool agg_g = tot >= AGG_MIN;
-        // ---- gather the members' live occurrences with their neighbourhoods (the links and
-        //      symbols do not change before apply 2), + the chosen-occurrence marks when no
-        //      member is an (a,a) pair: then every live occurrence is replaced ----
-        ex.par([&](u32 t) {
+        // ---- no (a,a) member: every live occurrence is replaced, so two members' chosen
+        //      occurrences touch exactly where a neighbouring pair of one occurrence is
+        //      another member's pair.  One pass gathers each occurrence with its neighbourhood
+        //      and decides everything the select phase below does for (a,a) batches: a
+        //      conflict between members m' and m (the pair at p, j or q of one is the other's)
+        //      cuts the batch at max(m, m') — the pair at pp is the one at q of the occurrence
+        //      at pp, which flags it —; q starts a chosen occurrence of the same member iff
+        //      its pair is the member's (right neighbour replaced too); p is the second
+        //      position of one iff the pair at pp is the member's, possible only when the
+        //      symbol at p is the member's b (then pp is read). ----
+        if (!aa) {
+            ex.par([&](u32 t) {
+                for (u32 e0 = 0; e0 < tot; e0 += RK * NT) {
+                    u32 pos[RK], lo[RK], p[RK], j[RK], q[RK], x[RK], pj[RK], pp[RK], ppv[RK], y[RK], pq[RK];
+                    bool valid[RK], lc[RK];
+#pragma unroll
+                    for (u32 k = 0; k < RK; ++k) {
+                        const u32 e = e0 + k * NT + t;
+                        u32 l = 0;
+                        pos[k] = 0;
+                        if (e < tot) {
+                            u32 hi = M;  // member l: m_pre[l] <= e < m_pre[l+1]
+                            while (hi - l > 1) {
+                                const u32 md = (l + hi) >> 1;
+                                if (sh.m_pre[md] <= e) l = md; else hi = md;
+                            }
+                            pos[k] = B.occpos[sh.m_roff[l] + (e - sh.m_pre[l])];
+                        }
+                        lo[k] = l;
+                    }
+#pragma unroll
+                    for (u32 k = 0; k < RK; ++k) {
+                        const bool in = e0 + k * NT + t < tot;
+                        const Node c = B.nd[in ? pos[k] : 0u];
+                        valid[k] = in && c.opair == sh.m_id[lo[k]];
+                        j[k] = c.nxt;
+                        p[k] = valid[k] ? c.prv : NIL;
+                    }
+#pragma unroll
+                    for (u32 k = 0; k < RK; ++k) {
+                        const Node cj = B.nd[valid[k] ? j[k] : 0u];
+                        const Node cp = B.nd[p[k] != NIL ? p[k] : 0u];
+                        q[k] = valid[k] ? cj.nxt : NIL;
+                        pj[k] = cj.opair;
+                        x[k] = cp.sym;
+                        pp[k] = p[k] != NIL ? cp.opair : NIL;
+                        ppv[k] = cp.prv;
+                    }
+#pragma unroll
+                    for (u32 k = 0; k < RK; ++k) {
+                        const Node cq = B.nd[q[k] != NIL ? q[k] : 0u];
+                        y[k] = cq.sym;
+                        pq[k] = q[k] != NIL ? cq.opair : NIL;
+                        lc[k] = p[k] != NIL && ppv[k] != NIL && x[k] == sh.m_b[lo[k]];
+                        lc[k] = lc[k] && B.nd[ppv[k]].opair == sh.m_id[lo[k]];
+                    }
+#pragma unroll
+                    for (u32 k = 0; k < RK; ++k) {
+                        const u32 o = ex.append(&sh.nocc, valid[k]);
+                        if (valid[k]) {
+                            const u32 m = lo[k];
+                            const u32 c1 = member_of(sh, pp[k]), c2 = q[k] != NIL ? member_of(sh, pj[k]) : NIL;
+                            const u32 c3 = member_of(sh, pq[k]);
+                            u32 cut = NIL;
+                            if (c1 != NIL) cut = umax(m, c1);
+                            if (c2 != NIL) cut = umin(cut, umax(m, c2));
+                            if (c3 != NIL && c3 != m) cut = umin(cut, umax(m, c3));
+                            if (cut != NIL) ex.min(&sh.t1, cut);
+                            const bool rightc = c3 == m;
+                            const u32 xl = (p[k] != NIL && !lc[k]) ? x[k] : NIL;
+                            ex.min(&sh.m_lmin[m], xl);
+                            ex.max(&sh.m_lmax[m], xl);
+                            B.opos[o] = pos[k];
+                            B.omem[o] = m;
+                            B.oj[o] = j[k];
+                            B.op[o] = lc[k] ? NIL : p[k];
+                            B.oq[o] = q[k];
+                            B.onp[o] = lc[k] ? ppv[k] : p[k];
+                            B.oidl[o] = xl;                                                  // left symbol
+                            B.oidr[o] = q[k] == NIL ? NIL : rightc ? X0 + m : y[k];  // right symbol
+                            B.oy[o] = rightc ? 1u : 0u;
+                            B.opj[o] = pj[k];
+                            B.opp[o] = pp[k];
+                        }
+                        ex.add_agg(&sh.m_repl[lo[k]], valid[k], agg_g);
+                    }
+                }
+            });
+        }
+        // ---- (a,a) batches: gather the members' live occurrences with their neighbourhoods
+        //      (the links and symbols do not change before apply 2); runs, marks and the
+        //      select phase follow ----
+        if (aa) ex.par([&](u32 t) {
             for (u32 e0 = 0; e0 < tot; e0 += RK * NT) {
                 u32 pos[RK], lo[RK], p[RK], j[RK], q[RK], o[RK];
                 bool valid[RK];
@@ -700,14 +810,8 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                     const u32 y = B.nd[valid[k] && q[k] != NIL ? q[k] : 0u].sym;
                     if (valid[k]) {
                         B.oy[o[k]] = y;
-                        if (aa) {
-                            B.oidx[pos[k]] = o[k];
-                        } else {
-                            ex.min(&B.mark[pos[k]], m2s(lo[k]));
-                            ex.min(&B.mark[j[k]], m2s(lo[k]) | 1u);
-                        }
+                        B.oidx[pos[k]] = o[k];
                     }
-                    if (!aa) ex.add_agg(&sh.m_repl[lo[k]], valid[k], agg_g);
                 }
             }
         });
@@ -771,9 +875,10 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
             });
         }
         ex.mark(P_SELECT);
-        // ---- conflicts (footprint {p, i, j, q} vs earlier members' spans), left-neighbour
-        //      uniformity, the replaced neighbours; one mark word per footprint position ----
-        ex.par([&](u32 t) {
+        // ---- (a,a) batches: conflicts (footprint {p, i, j, q} vs earlier members' spans),
+        //      left-neighbour uniformity, the replaced neighbours; one mark word per footprint
+        //      position ----
+        if (aa) ex.par([&](u32 t) {
             for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
                 bool act[RK];
                 u32 m[RK], i[RK], p[RK], j[RK], q[RK], wi[RK], wj[RK], wp[RK], wq[RK];

@@ -44,6 +44,7 @@ struct HostExec {
     u32 min(u32* p, u32 v) { const u32 o = *p; if (v < o) *p = v; return o; }
     u32 max(u32* p, u32 v) { const u32 o = *p; if (v > o) *p = v; return o; }
     u64 cas64(u64* p, u64 cmp, u64 v) { const u64 o = *p; if (o == cmp) *p = v; return o; }
+    u32 cas32(u32* p, u32 cmp, u32 v) { const u32 o = *p; if (o == cmp) *p = v; return o; }
     void add_agg(u32* p, bool act, bool) { if (act) ++*p; }
     void sub_agg(u32* p, bool act, bool) { if (act) --*p; }
     u32 slot_agg(u32* p, bool act, bool) { return act ? (*p)++ : 0; }
