@@ -59,7 +59,8 @@ constexpr u32 NT = KOLM_RP_NT;    // threads of the block's workgroup (NT divide
 constexpr u32 W = 512;            // max rounds (members) per batch (<= NT: one window of NT entries)
 constexpr u32 CAPR = 1u << 16;    // occurrence-region entries per batch beyond its first member
 constexpr u32 SORT_LDS = 4096;    // level lists up to this size are sorted in LDS
-constexpr u32 QLIM = 4096;        // level cache: the rescan picks flow so that Q holds <= QLIM pairs
+constexpr u32 QLIM = 32768;       // level cache: a scan of all pairs picks flow so that Q holds <= QLIM pairs,
+constexpr u32 TLIM = 2048;        //   a pass over Q picks ftop so that T holds <= TLIM pairs
 constexpr u32 NIL = 0xFFFFFFFFu;
 constexpr u32 DEAD = 0xFFFFFFFFu;
 constexpr u64 EMPTY = ~0ull;
@@ -119,7 +120,7 @@ struct Block {
     u32 hmask;
     u32* husd;
     u64* rules;
-    u64 *qa, *qb;  // level cache (PC entries each): (count when last read) << 32 | pair id
+    u64 *qa, *qb, *ta, *tb;  // level cache tiers Q, T (PC entries each): (count when last read) << 32 | pair id
     u8* out;
     u64 out_cap;
     u32* result;  // RS_N words
@@ -136,6 +137,7 @@ struct Shared {
     u32 f, lp, lsize, M, V, T, tot, nocc, npairs, next_sym, nrules, pool, batch, hused, nlate;
     u32 t1, t2, ts, any_aa, cut, maxc, err, total, levels, tbase, hovf;
     u32 flow, qn, qn2, qvalid;  // level cache: Q = every pair with count >= flow
+    u32 ftop, tn, tn2, tvalid, maxt, thr;  //   T = every pair of Q with count >= ftop
     u32 mcap;                   // adaptive window: members gathered per batch (<= W)
     u32 ncnt[NCNT];             // new pairs of a batch (id - npairs < NCNT): counts, then fill counters
     u32 npoff[NCNT];            //   and region offsets, in LDS instead of global atomics
@@ -174,6 +176,8 @@ RP_HD inline u64 workspace_layout(char* base, u32 n, Block& B) {
     B.rules = (u64*)take((N / 2 + 16) * 8);
     B.qa = (u64*)take(PC * 8);
     B.qb = (u64*)take(PC * 8);
+    B.ta = (u64*)take(PC * 8);
+    B.tb = (u64*)take(PC * 8);
     return off;
 }
 
@@ -411,6 +415,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
             sh.pool = 0; sh.npairs = NBASE; sh.next_sym = 256; sh.nrules = 0; sh.batch = 0;
             sh.lp = 0; sh.lsize = 0; sh.f = 0; sh.hused = 0; sh.nlate = 0; sh.err = RE_OK; sh.levels = 0;
             sh.qvalid = 0; sh.qn = 0; sh.flow = NIL; sh.mcap = W; sh.tbase = 0;
+            sh.tvalid = 0; sh.tn = 0; sh.ftop = NIL;
         }
     });
     ex.par([&](u32 t) {
@@ -439,6 +444,8 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
     u32* ti = B.liB;
     u64* qa = B.qa;  // level cache Q (and its compaction target)
     u64* qb = B.qb;
+    u64* ta = B.ta;  // level cache T (and its compaction target)
+    u64* tb = B.tb;
     u32 guard = 0;
     // ---------------- batches ----------------
     for (;;) {
@@ -449,19 +456,55 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
         }
         if (sh.lp >= sh.lsize) {
             ex.mark(P_LVSCAN);
-            // new level: f = max count; the level list = pairs with count f, sorted.  The
-            // candidates come from the level cache Q, which holds every pair whose count
-            // is >= flow: counts never rise except at creation, and created pairs with a
-            // count >= flow are appended (apply 3).  So while max(Q) >= flow it is the
-            // global maximum; when it drops below flow, all pairs are rescanned for a lower
-            // flow (chosen so that Q holds at most QLIM pairs).
+            // new level: f = max count; the level list = pairs with count f, sorted.  Counts
+            // never rise except at creation, so a cache of every pair whose count is >= a
+            // threshold, plus the pairs created since with a count >= it (apply 3), holds the
+            // global maximum while its own maximum is >= the threshold.  Two tiers: Q = the
+            // pairs with count >= flow (<= QLIM when taken from a scan of all pairs), T = the
+            // pairs of Q with count >= ftop (<= TLIM when taken from Q).  A level reads T only;
+            // T is retaken from Q when its maximum falls below ftop, Q from all pairs when its
+            // maximum falls below flow.
             bool done = false;
+            u32* hist = reinterpret_cast<u32*>(sh.skey);  // 2048 count bins (LDS, idle here)
+            // sh.thr = the smallest bin >= lo whose suffix count is <= lim, at most the highest
+            // non-empty bin (every pair of the top bin is taken); NIL when no count is >= lo
+            auto pick = [&](u32 lo, u32 lim) {
+                // suffix sums over the bins, top down: thread t holds the HB bins
+                // 2047 - HB*t - k, k < HB (descending)
+                constexpr u32 HB = 2048 / NT;
+                ex.par([&](u32 t) {
+                    u32 v = 0;
+                    for (u32 k = 0; k < HB; ++k) v += hist[2047 - HB * t - k];
+                    sh.scan[t] = v;
+                    if (t == 0) { sh.thr = NIL; sh.maxc = 0; }
+                });
+                ex.scan(sh.scan, &sh.total);
+                ex.par([&](u32 t) {
+                    u32 run = sh.scan[t], cand = NIL;
+                    bool top = false;
+                    for (u32 k = 0; k < HB; ++k) {
+                        const u32 bin = 2047 - HB * t - k;
+                        run += hist[bin];  // #(count >= bin)
+                        if (bin >= lo && run <= lim) cand = bin;
+                        if (bin >= lo && hist[bin] && !top) {  // the highest non-empty bin
+                            ex.max(&sh.maxc, bin);
+                            top = true;
+                        }
+                    }
+                    if (cand != NIL) ex.min(&sh.thr, cand);
+                });
+                ex.par([&](u32 t) {
+                    if (t == 0) {
+                        if (sh.maxc == 0) sh.thr = NIL;
+                        else if (sh.thr == NIL || sh.thr > sh.maxc) sh.thr = sh.maxc;
+                    }
+                });
+            };
             for (;;) {
                 if (!sh.qvalid) {
-                    u32* hist = reinterpret_cast<u32*>(sh.skey);  // 2048 count bins (LDS, idle here)
                     ex.par([&](u32 t) {
                         for (u32 i = t; i < 2048; i += NT) hist[i] = 0;
-                        if (t == 0) { sh.flow = NIL; sh.qn = 0; sh.maxc = 0; }
+                        if (t == 0) sh.qn = 0;
                     });
                     ex.par([&](u32 t) {
                         const u32 np = sh.npairs;
@@ -474,43 +517,13 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                                 if (v[k] >= 2) ex.add(&hist[v[k] < 2047 ? v[k] : 2047u], 1u);
                         }
                     });
-                    // suffix sums over the bins, top down: thread t holds the HB bins
-                    // 2047 - HB*t - k, k < HB (descending)
-                    constexpr u32 HB = 2048 / NT;
-                    ex.par([&](u32 t) {
-                        u32 v = 0;
-                        for (u32 k = 0; k < HB; ++k) v += hist[2047 - HB * t - k];
-                        sh.scan[t] = v;
-                    });
-                    ex.scan(sh.scan, &sh.total);
-                    ex.par([&](u32 t) {
-                        u32 run = sh.scan[t], cand = NIL;
-                        bool top = false;
-                        for (u32 k = 0; k < HB; ++k) {
-                            const u32 bin = 2047 - HB * t - k;
-                            run += hist[bin];  // #(count >= bin)
-                            if (bin >= 2 && run <= QLIM) cand = bin;
-                            if (bin >= 2 && hist[bin] && !top) {  // the highest non-empty bin
-                                ex.max(&sh.maxc, bin);
-                                top = true;
-                            }
-                        }
-                        if (cand != NIL) ex.min(&sh.flow, cand);
-                    });
-                    ex.par([&](u32 t) {
-                        if (t == 0) {
-                            // flow <= the top count, so Q is never empty; all pairs in the top
-                            // bin are taken even when they are more than QLIM
-                            if (sh.total == 0) sh.flow = NIL;  // no pair occurs twice
-                            else if (sh.flow == NIL || sh.flow > sh.maxc) sh.flow = sh.maxc;
-                        }
-                    });
-                    if (sh.flow == NIL) {
+                    pick(2, QLIM);
+                    if (sh.thr == NIL) {  // no pair occurs twice
                         done = true;
                         break;
                     }
                     ex.par([&](u32 t) {
-                        const u32 np = sh.npairs, fl = sh.flow;
+                        const u32 np = sh.npairs, fl = sh.thr;
                         for (u32 i0 = 0; i0 < np; i0 += RK * NT) {
                             u32 c[RK];
 #pragma unroll
@@ -523,59 +536,144 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                                 if (keep) qa[slot] = ((u64)c[k] << 32) | id;
                             }
                         }
-                        if (t == 0) sh.qvalid = 1;
+                        if (t == 0) { sh.flow = fl; sh.qvalid = 1; sh.tvalid = 0; }
                     });
                 }
-                // drop the entries below flow, and the maximum of the rest
-                ex.par([&](u32 t) { if (t == 0) { sh.maxc = 0; sh.qn2 = 0; } });
+                if (!sh.tvalid) {
+                    // Q by current counts: drop the entries below flow, histogram of the rest,
+                    // then T = the entries >= ftop (their counts are current: no second load)
+                    ex.par([&](u32 t) {
+                        for (u32 i = t; i < 2048; i += NT) hist[i] = 0;
+                        if (t == 0) { sh.qn2 = 0; sh.tn = 0; sh.maxt = 0; }
+                    });
+                    ex.par([&](u32 t) {
+                        const u32 qn = sh.qn, fl = sh.flow;
+                        for (u32 e0 = 0; e0 < qn; e0 += RK * NT) {
+                            u32 id[RK], c[RK];
+#pragma unroll
+                            for (u32 k = 0; k < RK; ++k) id[k] = e0 + k * NT + t < qn ? (u32)qa[e0 + k * NT + t] : 0u;
+#pragma unroll
+                            for (u32 k = 0; k < RK; ++k) c[k] = e0 + k * NT + t < qn ? B.cnt[id[k]] : 0u;
+#pragma unroll
+                            for (u32 k = 0; k < RK; ++k) {
+                                const bool keep = e0 + k * NT + t < qn && c[k] >= fl;
+                                const u32 slot = ex.append(&sh.qn2, keep);
+                                if (keep) {
+                                    qb[slot] = ((u64)c[k] << 32) | id[k];
+                                    ex.add(&hist[c[k] < 2047 ? c[k] : 2047u], 1u);
+                                }
+                            }
+                        }
+                    });
+                    {
+                        u64* x = qa; qa = qb; qb = x;
+                    }
+                    ex.par([&](u32 t) { if (t == 0) sh.qn = sh.qn2; });
+                    if (sh.qn == 0) {  // every count of Q fell below flow
+                        if (sh.flow <= 2) {  // every count is below 2: no further rule (PY:1879)
+                            done = true;
+                            break;
+                        }
+                        ex.par([&](u32 t) { if (t == 0) sh.qvalid = 0; });
+                        continue;
+                    }
+                    pick(sh.flow, TLIM);
+                    ex.par([&](u32 t) {
+                        const u32 qn = sh.qn, ft = sh.thr;
+                        u32 m = 0;
+                        for (u32 e0 = 0; e0 < qn; e0 += RK * NT) {
+                            u64 q[RK];
+#pragma unroll
+                            for (u32 k = 0; k < RK; ++k) q[k] = e0 + k * NT + t < qn ? qa[e0 + k * NT + t] : 0ull;
+#pragma unroll
+                            for (u32 k = 0; k < RK; ++k) {
+                                const u32 c = (u32)(q[k] >> 32);
+                                const bool keep = e0 + k * NT + t < qn && c >= ft;
+                                const u32 slot = ex.append(&sh.tn, keep);
+                                if (keep) {
+                                    ta[slot] = q[k];
+                                    m = c > m ? c : m;
+                                }
+                            }
+                        }
+                        if (m) ex.max(&sh.maxt, m);
+                        if (t == 0) { sh.ftop = ft; sh.tvalid = 1; }
+                    });
+                    break;
+                }
+                // drop the entries of T below ftop, and the maximum of the rest
+                ex.par([&](u32 t) {
+                    for (u32 i = t; i < 2048; i += NT) hist[i] = 0;
+                    if (t == 0) { sh.maxt = 0; sh.tn2 = 0; }
+                });
                 ex.par([&](u32 t) {
                     // current counts (they only fall between levels); the survivors keep
                     // theirs, so the level list below needs no second count load
                     u32 m = 0;
-                    const u32 qn = sh.qn, fl = sh.flow;
-                    for (u32 e0 = 0; e0 < qn; e0 += RK * NT) {
+                    const u32 tn = sh.tn, fl = sh.ftop;
+                    for (u32 e0 = 0; e0 < tn; e0 += RK * NT) {
                         u32 id[RK], c[RK];
 #pragma unroll
-                        for (u32 k = 0; k < RK; ++k) id[k] = e0 + k * NT + t < qn ? (u32)qa[e0 + k * NT + t] : 0u;
+                        for (u32 k = 0; k < RK; ++k) id[k] = e0 + k * NT + t < tn ? (u32)ta[e0 + k * NT + t] : 0u;
 #pragma unroll
-                        for (u32 k = 0; k < RK; ++k) c[k] = e0 + k * NT + t < qn ? B.cnt[id[k]] : 0u;
+                        for (u32 k = 0; k < RK; ++k) c[k] = e0 + k * NT + t < tn ? B.cnt[id[k]] : 0u;
 #pragma unroll
                         for (u32 k = 0; k < RK; ++k) {
-                            const bool keep = e0 + k * NT + t < qn && c[k] >= fl;
-                            const u32 slot = ex.append(&sh.qn2, keep);
+                            const bool keep = e0 + k * NT + t < tn && c[k] >= fl;
+                            const u32 slot = ex.append(&sh.tn2, keep);
                             if (keep) {
-                                qb[slot] = ((u64)c[k] << 32) | id[k];
+                                tb[slot] = ((u64)c[k] << 32) | id[k];
                                 m = c[k] > m ? c[k] : m;
+                                ex.add(&hist[c[k] < 2047 ? c[k] : 2047u], 1u);
                             }
                         }
                     }
-                    if (m) ex.max(&sh.maxc, m);
+                    if (m) ex.max(&sh.maxt, m);
                 });
                 {
-                    u64* x = qa; qa = qb; qb = x;
+                    u64* x = ta; ta = tb; tb = x;
                 }
-                ex.par([&](u32 t) { if (t == 0) sh.qn = sh.qn2; });
-                if (sh.maxc >= sh.flow) break;
-                if (sh.flow <= 2) {  // every count is below 2: no further rule (PY:1879)
-                    done = true;
-                    break;
+                ex.par([&](u32 t) { if (t == 0) sh.tn = sh.tn2; });
+                if (sh.maxt >= sh.ftop && sh.tn > 2 * TLIM) {
+                    // T grew with created pairs: raise ftop (the dropped entries stay in Q)
+                    pick(sh.ftop, TLIM);
+                    ex.par([&](u32 t) { if (t == 0) sh.tn2 = 0; });
+                    ex.par([&](u32 t) {
+                        const u32 tn = sh.tn, ft = sh.thr;
+                        for (u32 e0 = 0; e0 < tn; e0 += RK * NT) {
+                            u64 q[RK];
+#pragma unroll
+                            for (u32 k = 0; k < RK; ++k) q[k] = e0 + k * NT + t < tn ? ta[e0 + k * NT + t] : 0ull;
+#pragma unroll
+                            for (u32 k = 0; k < RK; ++k) {
+                                const bool keep = e0 + k * NT + t < tn && (u32)(q[k] >> 32) >= ft;
+                                const u32 slot = ex.append(&sh.tn2, keep);
+                                if (keep) tb[slot] = q[k];
+                            }
+                        }
+                    });
+                    {
+                        u64* x = ta; ta = tb; tb = x;
+                    }
+                    ex.par([&](u32 t) { if (t == 0) { sh.tn = sh.tn2; sh.ftop = sh.thr; } });
                 }
-                ex.par([&](u32 t) { if (t == 0) sh.qvalid = 0; });
+                if (sh.maxt >= sh.ftop) break;
+                ex.par([&](u32 t) { if (t == 0) sh.tvalid = 0; });
             }
             if (done) break;
             ex.par([&](u32 t) {
-                if (t == 0) { sh.f = sh.maxc; sh.lsize = 0; sh.lp = 0; sh.levels++; sh.mcap = W; }
+                if (t == 0) { sh.f = sh.maxt; sh.lsize = 0; sh.lp = 0; sh.levels++; sh.mcap = W; }
             });
             ex.par([&](u32 t) {
-                // Q was just filtered: its entries carry their current counts
-                const u32 qn = sh.qn, fl = sh.f;
-                for (u32 e0 = 0; e0 < qn; e0 += RK * NT) {
+                // T was just filtered / taken: its entries carry their current counts
+                const u32 tn = sh.tn, fl = sh.f;
+                for (u32 e0 = 0; e0 < tn; e0 += RK * NT) {
                     u64 q[RK];
 #pragma unroll
-                    for (u32 k = 0; k < RK; ++k) q[k] = e0 + k * NT + t < qn ? qa[e0 + k * NT + t] : 0ull;
+                    for (u32 k = 0; k < RK; ++k) q[k] = e0 + k * NT + t < tn ? ta[e0 + k * NT + t] : 0ull;
 #pragma unroll
                     for (u32 k = 0; k < RK; ++k) {
-                        const bool hit = e0 + k * NT + t < qn && (u32)(q[k] >> 32) == fl;
+                        const bool hit = e0 + k * NT + t < tn && (u32)(q[k] >> 32) == fl;
                         const u32 slot = ex.append(&sh.lsize, hit);
                         if (hit) {
                             lk[slot] = B.pkey[(u32)q[k]];
@@ -1093,6 +1191,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                     B.liL[k] = id;
                 }
                 if (c >= sh.flow) qa[ex.add(&sh.qn, 1u)] = ((u64)c << 32) | id;  // keeps Q complete (level cache)
+                if (c >= sh.ftop) ta[ex.add(&sh.tn, 1u)] = ((u64)c << 32) | id;  // and T
             }
             for (u32 m = t; m < T; m += NT) {
                 B.rules[sh.nrules + m] = pkey_of(sh.m_a[m], sh.m_b[m]);
@@ -1155,7 +1254,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
             }
         });
         {
-            const u32 fr[8] = {f, M, T, nocc, sh.hused, sh.nlate, aa ? 1u : 0u, sh.lsize};
+            const u32 fr[8] = {f, M, T, nocc, sh.hused, sh.nlate, aa ? 1u : 0u, tot};
             ex.record(fr);
         }
         ex.mark(P_LATE);

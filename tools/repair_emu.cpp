@@ -53,11 +53,21 @@ struct HostExec {
     u32 from_leader(u32 v, u32) const { return v; }
     void mark(u32) {}
     void begin(u32) {}
-    void record(const u32 (&)[8]) {}
+    void record(const u32 (&f)[8]);
     u32 append(u32* n, bool pred) { return pred ? (*n)++ : NIL; }
 };
 
+u64 g_stats[8];  // sums of the batch records: iterations, M, T, nocc, hused, nlate, aa, tot
+void HostExec::record(const u32 (&f)[8]) {
+    g_stats[0] += 1;
+    for (u32 k = 1; k < 8; ++k) g_stats[k] += f[k];
+}
+
 }  // namespace
+
+extern "C" void repair_emu_stats(uint64_t* out) {
+    for (int k = 0; k < 8; ++k) { out[k] = g_stats[k]; g_stats[k] = 0; }
+}
 
 extern "C" int64_t repair_emu(const uint8_t* text, int64_t n64, uint8_t* out, int64_t cap, uint32_t* result,
                               uint64_t shuffle_seed) {

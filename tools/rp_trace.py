@@ -5,7 +5,7 @@ KOLM_RP_TRACE set and summarises where the kernel's time goes by batch class.
   anywhere:        python tools/rp_trace.py show <trace file>
 
 Record (u32 x RP_TR_W per loop iteration): f, M (window members), T (rounds executed),
-nocc, hused, nlate, aa, lsize, then 100 MHz ticks per section (repair_core.h P_*)."""
+nocc, hused, nlate, aa, tot (region entries gathered), then 100 MHz ticks per section (repair_core.h P_*)."""
 import os
 import sys
 
@@ -38,10 +38,10 @@ def show(path):
     ticks = t[:, 8:8 + len(SEC)]
     used = np.nonzero(ticks.sum(1))[0]
     t, ticks = t[: used[-1] + 1], ticks[: used[-1] + 1]
-    f, M, T, nocc, hused, nlate, aa, lsize = (t[:, k] for k in range(8))
+    f, M, T, nocc, hused, nlate, aa, tot = (t[:, k] for k in range(8))
     ms = ticks / 1e5
-    tot = ms.sum()
-    print(f"iterations {len(t)}  batches {int((T > 0).sum())}  total {tot:.2f} ms  rounds {int(T.sum())}")
+    tms = ms.sum()
+    print(f"iterations {len(t)}  batches {int((T > 0).sum())}  total {tms:.2f} ms  rounds {int(T.sum())}")
     print("section ms: " + " ".join(f"{s} {ms[:, k].sum():.2f}" for k, s in enumerate(SEC)))
     per = ms.sum(1)
     # by occurrence count class
