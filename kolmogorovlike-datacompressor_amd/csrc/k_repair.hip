@@ -68,6 +68,33 @@ struct DevExec {
         if (t == 0) *total = tot;
         __syncthreads();
     }
+    // two exclusive scans sharing their barriers (a: totals in *ta, b: in *tb)
+    __device__ inline void scan2(u32* a, u32* b, u32* ta, u32* tb) {
+        const u32 t = threadIdx.x, lane = t & 63, w = t >> 6;
+        const u32 va = a[t], vb = b[t];
+        const u32 ia = wave_incl_scan(va, OpAddU(), 0u), ib = wave_incl_scan(vb, OpAddU(), 0u);
+        if (lane == 63) {
+            sh->wtot[w] = ia;
+            sh->wtot2[w] = ib;
+        }
+        __syncthreads();
+        u32 pa = 0, sa = 0, pb = 0, sb = 0;
+#pragma unroll
+        for (u32 i = 0; i < rp::NT / 64; ++i) {
+            const u32 x = sh->wtot[i], y = sh->wtot2[i];
+            pa += i < w ? x : 0u;
+            sa += x;
+            pb += i < w ? y : 0u;
+            sb += y;
+        }
+        a[t] = pa + ia - va;
+        b[t] = pb + ib - vb;
+        if (t == 0) {
+            *ta = sa;
+            *tb = sb;
+        }
+        __syncthreads();
+    }
     // wave-aggregated append: one atomic per wave, slots in lane order among pred lanes
     __device__ inline u32 append(u32* ctr, bool pred) {
         const u64 m = __ballot(pred);

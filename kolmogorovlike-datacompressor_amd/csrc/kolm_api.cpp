@@ -969,6 +969,17 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
             for (u32 b = 0; b < nb; ++b) t += pr[(u64)b * RP_P_N + k];
             fprintf(stderr, " %s %.2f", nm[k], (double)t / nb / 1e5);
         }
+        // spread of the per-block totals (the kernel lasts as long as its slowest block)
+        std::vector<double> tb(nb, 0.0);
+        for (u32 b = 0; b < nb; ++b)
+            for (u32 k = 0; k < RP_P_N; ++k) tb[b] += (double)pr[(u64)b * RP_P_N + k] / 1e5;
+        std::vector<double> so = tb;
+        std::sort(so.begin(), so.end());
+        if (nb) {
+            u32 bmax = 0;
+            for (u32 b = 0; b < nb; ++b) if (tb[b] > tb[bmax]) bmax = b;
+            fprintf(stderr, " | block total ms min %.2f median %.2f max %.2f (block %u)", so[0], so[nb / 2], so[nb - 1], bmax);
+        }
         fprintf(stderr, "\n");
     }
     if (want_rp && rpa.trace) {

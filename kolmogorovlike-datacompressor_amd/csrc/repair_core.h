@@ -6,6 +6,7 @@
 // The includer defines RP_HD (function qualifiers) and provides the Exec policy:
 //   ex.par(f)            f(tid) for every tid in [0, NT), then a workgroup barrier
 //   ex.scan(a, &total)   in-place exclusive scan of a[0..NT) (LDS), total written by all
+//   ex.scan2(a, b, &ta, &tb)  two such scans sharing their barriers
 //   ex.add/sub/min/max/cas  atomics (u32; cas64 on u64)
 //   ex.append(&n, pred)  index n++ for the threads with pred (wave-aggregated on the device), else NIL
 //   ex.add_agg/sub_agg(p, act)  *p += / -= 1 for the threads with act; ex.slot_agg(p, act) the
@@ -74,6 +75,9 @@ constexpr u32 MAX_N = 1u << 22;   // block length limit of the device Re-Pair
 constexpr u32 RK = KOLM_RP_RK;    // occurrences per thread per step in the occurrence loops
 constexpr u32 AGG_MIN = 2048;     // batches with at least this many occurrences aggregate atomics
 constexpr u32 WIN_MIN = 32;       // smallest adaptive window (members per batch)
+#ifndef KOLM_RP_MCAP
+#define KOLM_RP_MCAP(T) (2 * (T) + 16)  // window after a batch cut at T (A/B knob)
+#endif
 constexpr u32 NCNT = 2048;        // batches creating at most this many pairs count them in LDS
 constexpr u32 MMAP = 1024;        // member map (pair id -> member index) slots, in sval[0 .. 2 MMAP)
 
@@ -130,12 +134,15 @@ struct Shared {
     u32 m_id[W], m_a[W], m_b[W], m_lpos[W], m_roff[W], m_rlen[W], m_pre[W + 1], m_repl[W], m_lmin[W], m_lmax[W];
     u32 scan[NT];
     u32 scan2[NT];
-    u32 wtot[NT / 64];
+    u32 wtot[NT / 64], wtot2[NT / 64];
+    u64 st_key[NT];             // window staging by level entry: key, id, region length / offset
+    u32 st_id[NT], st_len[NT], st_off[NT];
+    u32 irank[2 * NT];          // init: slot << 16 | rank of each position of a chunk
     u32 chg[3];
     u64 skey[SORT_LDS];
     u32 sval[SORT_LDS];
     u32 f, lp, lsize, M, V, T, tot, nocc, npairs, next_sym, nrules, pool, batch, hused, nlate;
-    u32 t1, t2, ts, any_aa, cut, maxc, err, total, levels, tbase, hovf;
+    u32 t1, t2, ts, any_aa, cut, maxc, err, total, levels, tbase;
     u32 flow, qn, qn2, qvalid;  // level cache: Q = every pair with count >= flow
     u32 ftop, tn, tn2, tvalid, maxt, thr;  //   T = every pair of Q with count >= ftop
     u32 mcap;                   // adaptive window: members gathered per batch (<= W)
@@ -255,24 +262,55 @@ RP_HD inline u32 hash_insert_wave(E& ex, const Block& B, Shared& sh, const HTab&
     return ex.from_leader(s, ld);
 }
 
-// Claim key's slot in the batch's LDS table (ids are given out afterwards, in slot order).
-// A probe run longer than HPROBE (the table nearly full) flags an overflow instead: the
-// batch then redoes its keys in the global table.
+// The slot of key in the batch's key table: the LDS table first (the thread whose CAS
+// claims a slot allocates the pair id, as hash_insert does), the block's global table for a
+// key whose LDS probe run exceeds HPROBE (table nearly full; rare: the big batches of text
+// create a few dozen keys).  A key is never in both: a probe run that finds only other
+// keys stays that way (slots are never freed within a batch), so every thread with that
+// key goes global.  Global slots are returned with GSLOT set.
 constexpr u32 HPROBE = 128;
+constexpr u32 GSLOT = 0x80000000u;
 template <class E>
-RP_HD inline u32 hash_claim(E& ex, Shared& sh, u64 key) {
+RP_HD inline u32 hash_claim(E& ex, const Block& B, Shared& sh, u64 key) {
     u32 s = hslot(key, SORT_LDS - 1);
     for (u32 k = 0; k < HPROBE; ++k) {
         const u64 cur = sh.skey[s];
         if (cur == key) return s;
         if (cur == EMPTY) {
             const u64 old = ex.cas64(&sh.skey[s], EMPTY, key);
-            if (old == EMPTY || old == key) return s;
+            if (old == EMPTY) {
+                const u32 u = ex.add(&sh.hused, 1u);
+                const u32 id = sh.npairs + u;
+                B.husd[u] = NIL;
+                sh.sval[s] = id;
+                B.pkey[id] = key;
+                B.cnt[id] = 0;
+                B.plen[id] = 0;
+                return s;
+            }
+            if (old == key) return s;
         }
         s = (s + 1) & (SORT_LDS - 1);
     }
-    ex.max(&sh.hovf, 1u);
-    return 0;
+    const HTab g{B.hkey, B.hval, B.hmask, true};
+    return hash_insert(ex, B, sh, g, key) | GSLOT;
+}
+
+// Init-time pair table: slot of a 16-bit byte-pair code (IC positions per chunk into ICT
+// slots: at most half full, so a probe run always ends).
+constexpr u32 IC = 2 * NT;
+constexpr u32 ICT = 4096;
+static_assert(ICT >= 2 * IC && ICT <= SORT_LDS && 2 * ICT <= 2 * SORT_LDS, "init table");
+template <class E>
+RP_HD inline u32 ictab_slot(E& ex, u32* keys, u32 code) {
+    for (u32 s = (code * 0x9E3779B1u) >> 20;; s = (s + 1) & (ICT - 1)) {
+        const u32 k = keys[s];
+        if (k == code) return s;
+        if (k == NIL) {
+            const u32 old = ex.cas32(&keys[s], NIL, code);
+            if (old == NIL || old == code) return s;
+        }
+    }
 }
 
 // The window's member map (LDS, open addressing over sval[0 .. MMAP) keys and
@@ -403,6 +441,11 @@ template <class E>
 RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block& B, Shared& sh) {
     const u32 n = B.n;
     const u32 HS = B.hmask + 1;
+    ex.mark(P_INIT);
+    // init-time LDS pair table (ICT slots: keys in sval, counts / chunk bases in skey)
+    u32* ictk = sh.sval;
+    u32* ictc = reinterpret_cast<u32*>(sh.skey);
+    u32* ictb = reinterpret_cast<u32*>(sh.skey) + ICT;
     // ---------------- init: linked list, byte-pair counts and regions ----------------
     ex.par([&](u32 t) {
         for (u32 i = t; i < NBASE; i += NT) {
@@ -421,22 +464,72 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
     ex.par([&](u32 t) {
         for (u32 i = t; i < n; i += NT) {
             const bool last = i + 1 >= n;
-            const u32 code = last ? NIL : ((u32)B.text[i] << 8) | B.text[i + 1];
-            B.nd[i] = Node{last ? NIL : i + 1, i ? i - 1 : NIL, B.text[i], code};
+            B.nd[i] = Node{last ? NIL : i + 1, i ? i - 1 : NIL, B.text[i], last ? NIL : ((u32)B.text[i] << 8) | B.text[i + 1]};
             B.mark[i] = NIL;
-            if (!last) ex.add(&B.cnt[code], 1u);
         }
+        for (u32 s = t; s < ICT; s += NT) ictk[s] = NIL;
+        for (u32 s = t; s < ICT; s += NT) ictc[s] = 0;
     });
+    // byte-pair counts: every chunk of IC positions is counted in an LDS table first, then
+    // one global atomic per distinct pair of the chunk (a global atomic per position is
+    // throughput-bound at the L2 when every CU runs a block)
+    for (u32 c0 = 0; c0 + 1 < n; c0 += IC) {
+        ex.par([&](u32 t) {
+#pragma unroll
+            for (u32 k = 0; k < IC / NT; ++k) {
+                const u32 i = c0 + k * NT + t;
+                if (i + 1 < n) ex.add(&ictc[ictab_slot(ex, ictk, ((u32)B.text[i] << 8) | B.text[i + 1])], 1u);
+            }
+        });
+        ex.par([&](u32 t) {
+            for (u32 s = t; s < ICT; s += NT) {
+                const u32 code = ictk[s];
+                if (code != NIL) {
+                    ex.add(&B.cnt[code], ictc[s]);
+                    ictk[s] = NIL;
+                    ictc[s] = 0;
+                }
+            }
+        });
+    }
     ex.par([&](u32 t) {
         for (u32 c = t; c < NBASE; c += NT)
             if (B.cnt[c]) B.poff[c] = ex.add(&sh.pool, B.cnt[c]);
     });
-    ex.par([&](u32 t) {
-        for (u32 i = t; i + 1 < n; i += NT) {
-            const u32 code = B.nd[i].opair;
-            B.occpos[B.poff[code] + ex.add(&B.plen[code], 1u)] = i;
-        }
-    });
+    // occurrence regions: per chunk, each position's rank among its pair's positions in the
+    // chunk (LDS), one returning global atomic per distinct pair for the chunk's base
+    for (u32 c0 = 0; c0 + 1 < n; c0 += IC) {
+        ex.par([&](u32 t) {
+#pragma unroll
+            for (u32 k = 0; k < IC / NT; ++k) {
+                const u32 i = c0 + k * NT + t;
+                if (i + 1 < n) {
+                    const u32 sl = ictab_slot(ex, ictk, ((u32)B.text[i] << 8) | B.text[i + 1]);
+                    sh.irank[k * NT + t] = sl << 16 | ex.add(&ictc[sl], 1u);
+                }
+            }
+        });
+        ex.par([&](u32 t) {
+            for (u32 s = t; s < ICT; s += NT) {
+                const u32 code = ictk[s];
+                if (code != NIL) ictb[s] = B.poff[code] + ex.add(&B.plen[code], ictc[s]);
+            }
+        });
+        ex.par([&](u32 t) {
+#pragma unroll
+            for (u32 k = 0; k < IC / NT; ++k) {
+                const u32 i = c0 + k * NT + t;
+                if (i + 1 < n) {
+                    const u32 v = sh.irank[k * NT + t];
+                    B.occpos[ictb[v >> 16] + (v & 0xFFFFu)] = i;
+                }
+            }
+            for (u32 s = t; s < ICT; s += NT) {  // ictb is read above, ictk / ictc no more
+                ictk[s] = NIL;
+                ictc[s] = 0;
+            }
+        });
+    }
     ex.mark(P_INIT);
     u64* lk = B.lkA;
     u32* li = B.liA;
@@ -697,42 +790,32 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
         // this batch's marks of member m: start (m2s(m)) / second position (m2s(m) | 1)
         auto m2s = [&](u32 m) { return (otag0 + m) << 1; };
         const u32 X0 = sh.next_sym;
-        // ---- window: the next valid level entries (count still f), in list order ----
+        // ---- window: the next valid level entries (count still f), in list order; each
+        //      entry's key, region and validity are read at once, the members (valid entries
+        //      ranked by one scan, their region prefix by a second sharing its barriers) are
+        //      then placed from LDS ----
         ex.par([&](u32 t) {
             const u32 idx = sh.lp + t;
-            sh.scan[t] = idx < sh.lsize && B.cnt[li[idx]] == f ? 1u : 0u;
-            sh.scan2[t] = 0;
+            const bool in = idx < sh.lsize;
+            const u32 id = in ? li[idx] : 0u;
+            const u64 key = in ? lk[idx] : 0ull;
+            const u32 c = in ? B.cnt[id] : 0u, len = in ? B.plen[id] : 0u, off = in ? B.poff[id] : 0u;
+            const bool valid = in && c == f;
+            sh.scan[t] = valid ? 1u : 0u;
+            sh.scan2[t] = valid ? len : 0u;
+            sh.st_key[t] = key;
+            sh.st_id[t] = id;
+            sh.st_len[t] = len;
+            sh.st_off[t] = off;
             for (u32 e = t; e < SORT_LDS; e += NT) sh.skey[e] = EMPTY;  // the LDS key table (HTab)
             for (u32 e = t; e < MMAP; e += NT) sh.sval[e] = NIL;        // the member map
             for (u32 e = t; e < NCNT; e += NT) sh.ncnt[e] = 0;
             if (t == 0) {
                 sh.cut = NIL; sh.any_aa = 0; sh.nocc = 0; sh.t1 = NIL; sh.t2 = NIL; sh.ts = NIL;
-                sh.hused = 0; sh.nlate = 0; sh.hovf = 0;
+                sh.hused = 0; sh.nlate = 0;
             }
         });
-        ex.scan(sh.scan, &sh.V);
-        ex.par([&](u32 t) {
-            const u32 idx = sh.lp + t;
-            const u32 r = sh.scan[t];
-            const bool valid = (t + 1 < NT ? sh.scan[t + 1] : sh.V) != r;  // this entry's flag
-            if (valid && r < W) {
-                const u32 id = li[idx];
-                const u64 key = lk[idx];
-                const u32 a = (u32)(key >> 32), b = (u32)key, len = B.plen[id];
-                sh.m_id[r] = id;
-                sh.m_a[r] = a;
-                sh.m_b[r] = b;
-                sh.m_lpos[r] = idx;
-                sh.m_roff[r] = B.poff[id];
-                sh.m_rlen[r] = len;
-                sh.m_repl[r] = 0;
-                sh.m_lmin[r] = NIL;
-                sh.m_lmax[r] = 0;
-                sh.scan2[r] = len;
-                if (a == b) sh.any_aa = 1;
-                member_put(ex, sh, id, r);
-            }
-        });
+        ex.scan2(sh.scan, sh.scan2, &sh.V, &sh.total);
         if (sh.V == 0) {
             ex.par([&](u32 t) {
                 if (t == 0) sh.lp = sh.lp + NT < sh.lsize ? sh.lp + NT : sh.lsize;
@@ -742,16 +825,30 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
         // members beyond T are gathered and scanned for nothing (re-gathered by the next
         // batch): the window follows the previous batch's T (doubling when it was not cut)
         const u32 Mw = umin(sh.V, umin(W, sh.mcap));
-        ex.scan(sh.scan2, &sh.total);  // region prefix over the window's members
         ex.par([&](u32 t) {
-            if (t < Mw) {
-                const u32 pre = sh.scan2[t];
-                sh.m_pre[t] = pre;
-                if (t > 0 && pre + sh.m_rlen[t] > CAPR) ex.min(&sh.cut, t);
+            const u32 r = sh.scan[t];
+            const bool valid = (t + 1 < NT ? sh.scan[t + 1] : sh.V) != r;  // this entry's flag
+            if (valid && r <= W) sh.m_pre[r] = sh.scan2[t];  // region prefix over the members
+            if (valid && r < W) {
+                const u32 id = sh.st_id[t], len = sh.st_len[t];
+                const u64 key = sh.st_key[t];
+                const u32 a = (u32)(key >> 32), b = (u32)key;
+                sh.m_id[r] = id;
+                sh.m_a[r] = a;
+                sh.m_b[r] = b;
+                sh.m_lpos[r] = sh.lp + t;
+                sh.m_roff[r] = sh.st_off[t];
+                sh.m_rlen[r] = len;
+                sh.m_repl[r] = 0;
+                sh.m_lmin[r] = NIL;
+                sh.m_lmax[r] = 0;
+                if (a == b) sh.any_aa = 1;
+                member_put(ex, sh, id, r);
+                if (r > 0 && r < Mw && sh.scan2[t] + len > CAPR) ex.min(&sh.cut, r);
             }
         });
         const u32 M = sh.cut < Mw ? sh.cut : Mw;
-        const u32 tot = M < NT ? sh.scan2[M] : sh.total;  // entries past Mw are 0: prefix at M
+        const u32 tot = M < sh.V ? sh.m_pre[M] : sh.total;
         const bool aa = sh.any_aa != 0;
         ex.mark(P_GATHER);
         // Occurrence loops below take RK occurrences per thread per step, their dependent
@@ -1047,8 +1144,8 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
         const bool stop = sh.ts != NIL && sh.ts < sh.t1 && sh.ts < sh.t2;
         if (T == 0) break;  // the next round replaces < 2 occurrences (PY:1879-1882)
         ex.mark(P_APPLY_A);
-        // ---- apply 1: destroy the old pair occurrences; claim the new pair keys in the
-        //      batch's LDS table (slots kept per occurrence in ox (left) / opj (right)) ----
+        // ---- apply 1: destroy the old pair occurrences; register the new pair keys (the
+        //      inserting thread allocates the id; slots kept in ox (left) / opj (right)) ----
         ex.par([&](u32 t) {
             for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
                 bool act[RK];
@@ -1074,50 +1171,11 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                     ex.sub_agg(&B.cnt[pp[k]], hp, agg);
                     const u32 X = X0 + m[k];
                     const u32 o = o0 + k * NT;
-                    if (hq) B.opj[o] = hash_claim(ex, sh, pkey_of(X, yr[k]));
-                    if (hp) B.ox[o] = hash_claim(ex, sh, pkey_of(xl[k], X));
+                    if (hq) B.opj[o] = hash_claim(ex, B, sh, pkey_of(X, yr[k]));
+                    if (hp) B.ox[o] = hash_claim(ex, B, sh, pkey_of(xl[k], X));
                 }
             }
         });
-        // more distinct new keys than the LDS table holds (rare: the big batches of text
-        // create a few dozen): every key goes through the block's global table instead
-        const bool hglob = sh.hovf != 0;
-        const HTab ht = hglob ? HTab{B.hkey, B.hval, B.hmask, true} : HTab{sh.skey, sh.sval, SORT_LDS - 1, false};
-        if (hglob) {
-            ex.par([&](u32 t) {
-                for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
-#pragma unroll
-                    for (u32 k = 0; k < RK; ++k) {
-                        const u32 o = o0 + k * NT;
-                        bool act = o < nocc && !(aa && (dist[o] & 1u));
-                        const u32 m = act ? B.omem[o] : 0u;
-                        act = act && m < T;
-                        const bool hq = act && B.oq[o] != NIL, hp = act && B.op[o] != NIL;
-                        const u32 X = X0 + m;
-                        const u32 sr = hash_insert_wave(ex, B, sh, ht, pkey_of(X, hq ? B.oidr[o] : 0u), hq, agg);
-                        const u32 sl = hash_insert_wave(ex, B, sh, ht, pkey_of(hp ? B.oidl[o] : 0u, X), hp, agg);
-                        if (hq) B.opj[o] = sr;
-                        if (hp) B.ox[o] = sl;
-                    }
-                }
-            });
-        } else {
-            // ids of the claimed keys, in slot order
-            const u32 np = sh.npairs;
-            ex.par([&](u32 t) {
-                for (u32 s0 = 0; s0 < SORT_LDS; s0 += NT) {
-                    const u64 key = sh.skey[s0 + t];
-                    const bool used = key != EMPTY;
-                    const u32 u = ex.append(&sh.hused, used);
-                    if (used) {
-                        sh.sval[s0 + t] = np + u;
-                        B.pkey[np + u] = key;
-                        B.cnt[np + u] = 0;
-                        B.plen[np + u] = 0;
-                    }
-                }
-            });
-        }
         ex.mark(P_APPLY_A2);
         // ---- apply 2: count the new pair occurrences, rewrite the sequence ----
         const bool lcnt = sh.hused <= NCNT;  // new-pair counters in LDS
@@ -1143,8 +1201,9 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                 }
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
-                    idr[k] = q[k] != NIL ? ht.v[idr[k]] : NIL;
-                    idl[k] = p[k] != NIL ? ht.v[idl[k]] : NIL;
+                    auto id_of = [&](u32 slot) { return slot & GSLOT ? B.hval[slot & ~GSLOT] : sh.sval[slot]; };
+                    idr[k] = q[k] != NIL ? id_of(idr[k]) : NIL;
+                    idl[k] = p[k] != NIL ? id_of(idl[k]) : NIL;
                 }
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
@@ -1242,15 +1301,15 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                     if (hp) B.occpos[bl[k] + sl] = p[k];
                 }
             }
-            if (hglob)
-                for (u32 u = t; u < sh.hused; u += NT) B.hkey[B.husd[u]] = EMPTY;
+            for (u32 u = t; u < sh.hused; u += NT)  // clear the keys that went to the global table
+                if (B.husd[u] != NIL) B.hkey[B.husd[u]] = EMPTY;
             if (t == 0) {
                 sh.lp = sh.m_lpos[T - 1] + 1;
                 sh.next_sym += T;
                 sh.nrules += T;
                 sh.npairs += sh.hused;
                 sh.batch += 1;
-                sh.mcap = T < M ? umax(WIN_MIN, umin(W, 2 * T + 16)) : umin(W, 2 * M);
+                sh.mcap = T < M ? umax(WIN_MIN, umin(W, KOLM_RP_MCAP(T))) : umin(W, 2 * M);
             }
         });
         {

@@ -39,6 +39,10 @@ struct HostExec {
         }
         *total = acc;
     }
+    void scan2(u32* a, u32* b, u32* ta, u32* tb) {
+        scan(a, ta);
+        scan(b, tb);
+    }
     u32 add(u32* p, u32 v) { const u32 o = *p; *p = o + v; return o; }
     u32 sub(u32* p, u32 v) { const u32 o = *p; *p = o - v; return o; }
     u32 min(u32* p, u32 v) { const u32 o = *p; if (v < o) *p = v; return o; }
