@@ -159,10 +159,28 @@ constexpr u32 DUVAL_PF = 64;                  // factors per span with a cached 
 
 __device__ inline u32 lds_addr(u32 q) { return q + (q / DUVAL_CH) * DUVAL_PAD; }
 
-// x = t[x0, x1) < y = t[x1, y1) (span-local positions, proper prefix smaller)
+// bytes q .. q+3 of the staged span (span-local positions, little-endian): two aligned
+// LDS dwords of the logical word stream (a chunk's 128 bytes are whole words, the pad
+// between chunks is skipped by lds_addr) and a byte funnel shift
+__device__ inline u32 lds_word(const u8* t, u32 q) {
+    const u32* d = reinterpret_cast<const u32*>(t);
+    const u32 k = q & ~3u;
+    return __builtin_amdgcn_alignbyte(d[lds_addr(k + 4) >> 2], d[lds_addr(k) >> 2], q & 3);
+}
+
+// x = t[x0, x1) < y = t[x1, y1) (span-local positions, proper prefix smaller); 4 bytes per
+// step (factors of text share long prefixes: repeated words)
 __device__ inline bool span_less(const u8* t, u32 x0, u32 x1, u32 y1) {
     const u32 la = x1 - x0, lb = y1 - x1, m = min(la, lb);
-    for (u32 i = 0; i < m; ++i) {
+    u32 i = 0;
+    for (; i + 4 <= m; i += 4) {
+        const u32 a = lds_word(t, x0 + i), b = lds_word(t, x1 + i);
+        if (a != b) {
+            const u32 sh = (u32)(__ffs(a ^ b) - 1) & ~7u;  // the first differing byte
+            return ((a >> sh) & 255u) < ((b >> sh) & 255u);
+        }
+    }
+    for (; i < m; ++i) {
         const u8 a = t[lds_addr(x0 + i)], b = t[lds_addr(x1 + i)];
         if (a != b) return a < b;
     }
@@ -234,7 +252,7 @@ __device__ inline void dprof(u64* prof, u32 k, u64& last) {
 __global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8* s, u32* fstart, uint4* fpre,
                                                     u32* nfac, u64* prof) {
     u64 tlast = prof ? wall_clock64() : 0;
-    __shared__ __align__(16) u8 t[DUVAL_SPAN + 256 * DUVAL_PAD];
+    __shared__ __align__(16) u8 t[DUVAL_SPAN + 256 * DUVAL_PAD + 4];  // + 4: lds_word's read past the end
     __shared__ u32 bm[DUVAL_SPAN / 32];
     __shared__ u32 sm[DUVAL_SPAN / 1024];
     __shared__ u32 sh[WG / 64];
