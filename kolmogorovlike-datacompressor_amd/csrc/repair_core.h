@@ -78,7 +78,6 @@ constexpr u32 WIN_MIN = 32;       // smallest adaptive window (members per batch
 #ifndef KOLM_RP_MCAP
 #define KOLM_RP_MCAP(T) (2 * (T) + 16)  // window after a batch cut at T (A/B knob)
 #endif
-constexpr u32 NCNT = 2048;        // batches creating at most this many pairs count them in LDS
 constexpr u32 MMAP = 1024;        // member map (pair id -> member index) slots, in sval[0 .. 2 MMAP)
 
 enum : u32 { RS_SIZE = 0, RS_RULES, RS_FINAL, RS_BATCHES, RS_ERR, RS_LEVELS, RS_N };
@@ -106,7 +105,7 @@ struct alignas(16) Node {
 //   n:      nd (16 B each), mark, oidx;  opos omem od0 od1 ot0 ot1 oidl oidr oj op oq
 //           ox oy opj opp onp (occurrence neighbourhoods, by occurrence index)
 //   3n+16:  occpos          PC = NBASE + 2n + 16: cnt poff plen pkey, lists (3 x key+id)
-//   HS = pow2 >= n + 64:     hkey hval;  n + 16: husd;  n/2 + 16: rules
+//   HS = pow2 >= n + 64:     hkey hval hcnt;  n + 16: husd;  n/2 + 16: rules
 struct Block {
     const u8* text;
     u32 n;
@@ -120,7 +119,7 @@ struct Block {
     u64 *lkA, *lkB, *lkL;
     u32 *liA, *liB, *liL;
     u64* hkey;
-    u32* hval;
+    u32 *hval, *hcnt;
     u32 hmask;
     u32* husd;
     u64* rules;
@@ -146,8 +145,8 @@ struct Shared {
     u32 flow, qn, qn2, qvalid;  // level cache: Q = every pair with count >= flow
     u32 ftop, tn, tn2, tvalid, maxt, thr;  //   T = every pair of Q with count >= ftop
     u32 mcap;                   // adaptive window: members gathered per batch (<= W)
-    u32 ncnt[NCNT];             // new pairs of a batch (id - npairs < NCNT): counts, then fill counters
-    u32 npoff[NCNT];            //   and region offsets, in LDS instead of global atomics
+    u32 cslot[SORT_LDS];        // per LDS key slot: occurrences of the new pair, then the region fill counter
+    u32 spoff[SORT_LDS];        //   and its region offset
 };
 
 // Carve a block's workspace out of `base` (nullptr: size query).  Returns the bytes
@@ -179,6 +178,7 @@ RP_HD inline u64 workspace_layout(char* base, u32 n, Block& B) {
     B.liL = (u32*)take(PC * 4);
     B.hkey = (u64*)take((u64)HS * 8);
     B.hval = (u32*)take((u64)HS * 4);
+    B.hcnt = (u32*)take((u64)HS * 4);
     B.hmask = HS - 1;
     B.rules = (u64*)take((N / 2 + 16) * 8);
     B.qa = (u64*)take(PC * 8);
@@ -311,6 +311,17 @@ RP_HD inline u32 ictab_slot(E& ex, u32* keys, u32 code) {
             if (old == NIL || old == code) return s;
         }
     }
+}
+
+// hash_claim + one occurrence counted for the key (LDS slot counter, or the global slot's)
+template <class E>
+RP_HD inline u32 hash_count(E& ex, const Block& B, Shared& sh, u64 key) {
+    const u32 s = hash_claim(ex, B, sh, key);
+    if (s & GSLOT)
+        ex.add(&B.hcnt[s & ~GSLOT], 1u);
+    else
+        ex.add(&sh.cslot[s], 1u);
+    return s;
 }
 
 // The window's member map (LDS, open addressing over sval[0 .. MMAP) keys and
@@ -453,7 +464,10 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
             B.plen[i] = 0;
             B.pkey[i] = pkey_of(i >> 8, i & 255);
         }
-        for (u32 i = t; i < HS; i += NT) B.hkey[i] = EMPTY;
+        for (u32 i = t; i < HS; i += NT) {
+            B.hkey[i] = EMPTY;
+            B.hcnt[i] = 0;
+        }
         if (t == 0) {
             sh.pool = 0; sh.npairs = NBASE; sh.next_sym = 256; sh.nrules = 0; sh.batch = 0;
             sh.lp = 0; sh.lsize = 0; sh.f = 0; sh.hused = 0; sh.nlate = 0; sh.err = RE_OK; sh.levels = 0;
@@ -809,7 +823,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
             sh.st_off[t] = off;
             for (u32 e = t; e < SORT_LDS; e += NT) sh.skey[e] = EMPTY;  // the LDS key table (HTab)
             for (u32 e = t; e < MMAP; e += NT) sh.sval[e] = NIL;        // the member map
-            for (u32 e = t; e < NCNT; e += NT) sh.ncnt[e] = 0;
+            for (u32 e = t; e < SORT_LDS; e += NT) sh.cslot[e] = 0;
             if (t == 0) {
                 sh.cut = NIL; sh.any_aa = 0; sh.nocc = 0; sh.t1 = NIL; sh.t2 = NIL; sh.ts = NIL;
                 sh.hused = 0; sh.nlate = 0;
@@ -1144,8 +1158,10 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
         const bool stop = sh.ts != NIL && sh.ts < sh.t1 && sh.ts < sh.t2;
         if (T == 0) break;  // the next round replaces < 2 occurrences (PY:1879-1882)
         ex.mark(P_APPLY_A);
-        // ---- apply 1: destroy the old pair occurrences; register the new pair keys (the
-        //      inserting thread allocates the id; slots kept in ox (left) / opj (right)) ----
+        // ---- apply 1: destroy the old pair occurrences; claim the new pair keys (the claiming
+        //      thread allocates the id) and count their occurrences per key slot (slots kept in
+        //      ox (left) / opj (right)); j and q's link of the rewritten sequence (i and p's pair
+        //      in apply 4, where the ids are read) ----
         ex.par([&](u32 t) {
             for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
                 bool act[RK];
@@ -1171,79 +1187,29 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                     ex.sub_agg(&B.cnt[pp[k]], hp, agg);
                     const u32 X = X0 + m[k];
                     const u32 o = o0 + k * NT;
-                    if (hq) B.opj[o] = hash_claim(ex, B, sh, pkey_of(X, yr[k]));
-                    if (hp) B.ox[o] = hash_claim(ex, B, sh, pkey_of(xl[k], X));
-                }
-            }
-        });
-        ex.mark(P_APPLY_A2);
-        // ---- apply 2: count the new pair occurrences, rewrite the sequence ----
-        const bool lcnt = sh.hused <= NCNT;  // new-pair counters in LDS
-        const u32 np0 = sh.npairs;
-        ex.par([&](u32 t) {
-            for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
-                bool act[RK];
-                u32 m[RK], i[RK], j[RK], q[RK], p[RK], idr[RK], idl[RK];
-                bool rc[RK];
-#pragma unroll
-                for (u32 k = 0; k < RK; ++k) {
-                    const u32 o = o0 + k * NT;
-                    act[k] = o < nocc && !(aa && (dist[o] & 1u));
-                    m[k] = act[k] ? B.omem[o] : 0u;
-                    act[k] = act[k] && m[k] < T;
-                    i[k] = act[k] ? B.opos[o] : 0u;
-                    j[k] = act[k] ? B.oj[o] : 0u;
-                    q[k] = act[k] ? B.oq[o] : NIL;
-                    p[k] = act[k] ? B.op[o] : NIL;
-                    idr[k] = q[k] != NIL ? B.opj[o] : 0u;  // hash slots (apply 1)
-                    idl[k] = p[k] != NIL ? B.ox[o] : 0u;
-                    rc[k] = act[k] && B.oy[o] != 0u;
+                    if (hq) B.opj[o] = hash_count(ex, B, sh, pkey_of(X, yr[k]));
+                    if (hp) B.ox[o] = hash_count(ex, B, sh, pkey_of(xl[k], X));
                 }
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
-                    auto id_of = [&](u32 slot) { return slot & GSLOT ? B.hval[slot & ~GSLOT] : sh.sval[slot]; };
-                    idr[k] = q[k] != NIL ? id_of(idr[k]) : NIL;
-                    idl[k] = p[k] != NIL ? id_of(idl[k]) : NIL;
-                }
-#pragma unroll
-                for (u32 k = 0; k < RK; ++k) {
-                    const bool hq = q[k] != NIL, hp = p[k] != NIL;
-                    if (lcnt) {
-                        if (hq) ex.add(&sh.ncnt[idr[k] - np0], 1u);
-                        if (hp) ex.add(&sh.ncnt[idl[k] - np0], 1u);
-                    } else {
-                        ex.add_agg(&B.cnt[hq ? idr[k] : 0u], hq, agg);
-                        ex.add_agg(&B.cnt[hp ? idl[k] : 0u], hp, agg);
-                    }
                     if (!act[k]) continue;
                     const u32 o = o0 + k * NT;
-                    if (hq) B.oidr[o] = idr[k];
-                    if (hp) {
-                        B.oidl[o] = idl[k];
-                        B.nd[p[k]].opair = idl[k];
-                    }
-                    // i and j are written whole (one 16-byte store each); q's link only when q
-                    // does not start a chosen occurrence itself (that one writes its node)
-                    B.nd[i[k]] = Node{q[k], B.onp[o], X0 + m[k], idr[k]};
-                    B.nd[j[k]] = Node{NIL, NIL, DEAD, NIL};
-                    if (hq && !rc[k]) B.nd[q[k]].prv = i[k];
+                    // j is written whole (i in apply 4, with its pair id); q's link only when q
+                    // does not start a chosen occurrence itself (that one writes its own record)
+                    B.nd[B.oj[o]] = Node{NIL, NIL, DEAD, NIL};
+                    if (q[k] != NIL && B.oy[o] == 0u) B.nd[q[k]].prv = B.opos[o];
                 }
             }
         });
         ex.mark(P_APPLY_B);
-        // ---- apply 3: regions of the new pairs; count-f pairs join the level late ----
+        // ---- apply 3: regions of the new pairs (LDS-table keys by slot, global-table keys by
+        //      id); count-f pairs join the level late ----
         ex.par([&](u32 t) {
-            for (u32 u = t; u < sh.hused; u += NT) {
-                const u32 id = sh.npairs + u;
-                const u32 c = lcnt ? sh.ncnt[u] : B.cnt[id];
+            const u32 np = sh.npairs;
+            auto region = [&](u32 id, u32 c) {
                 const u32 po = ex.add(&sh.pool, c);
                 B.poff[id] = po;
-                if (lcnt) {
-                    B.cnt[id] = c;
-                    B.plen[id] = c;  // apply 4 fills all c slots of the region
-                    sh.npoff[u] = po;
-                    sh.ncnt[u] = 0;  // now the region's fill counter
-                }
+                B.cnt[id] = c;
                 if (c == f) {
                     const u32 k = ex.add(&sh.nlate, 1u);
                     B.lkL[k] = B.pkey[id];
@@ -1251,54 +1217,64 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                 }
                 if (c >= sh.flow) qa[ex.add(&sh.qn, 1u)] = ((u64)c << 32) | id;  // keeps Q complete (level cache)
                 if (c >= sh.ftop) ta[ex.add(&sh.tn, 1u)] = ((u64)c << 32) | id;  // and T
-            }
+                return po;
+            };
+            for (u32 s = t; s < SORT_LDS; s += NT)
+                if (sh.skey[s] != EMPTY) {
+                    const u32 id = sh.sval[s], c = sh.cslot[s];
+                    B.plen[id] = c;  // apply 4 fills the c slots of the region by the LDS counter
+                    sh.spoff[s] = region(id, c);
+                    sh.cslot[s] = 0;  // now the region's fill counter
+                }
+            for (u32 u = t; u < sh.hused; u += NT)
+                if (B.husd[u] != NIL) {
+                    const u32 g = B.husd[u], c = B.hcnt[g];
+                    B.hcnt[g] = 0;
+                    B.plen[np + u] = 0;  // apply 4 fills by global atomics
+                    region(np + u, c);
+                }
             for (u32 m = t; m < T; m += NT) {
                 B.rules[sh.nrules + m] = pkey_of(sh.m_a[m], sh.m_b[m]);
                 ex.sub(&B.cnt[sh.m_id[m]], sh.m_repl[m]);  // its replaced occurrences (apply 1)
             }
         });
-        // ---- apply 4: occurrence positions of the new pairs ----
+        // ---- apply 4: occurrence positions of the new pairs; i's record, p's pair ----
         ex.par([&](u32 t) {
             for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
                 bool act[RK];
-                u32 p[RK], q[RK], i[RK], idr[RK], idl[RK], br[RK], bl[RK];
+                u32 p[RK], q[RK], i[RK], sr[RK], sl[RK], m[RK];
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
                     const u32 o = o0 + k * NT;
                     act[k] = o < nocc && !(aa && (dist[o] & 1u));
-                    act[k] = act[k] && B.omem[o] < T;
+                    m[k] = act[k] ? B.omem[o] : 0u;
+                    act[k] = act[k] && m[k] < T;
                     q[k] = act[k] ? B.oq[o] : NIL;
                     p[k] = act[k] ? B.op[o] : NIL;
                     i[k] = act[k] ? B.opos[o] : 0u;
-                    idr[k] = q[k] != NIL ? B.oidr[o] : 0u;
-                    idl[k] = p[k] != NIL ? B.oidl[o] : 0u;
+                    sr[k] = q[k] != NIL ? B.opj[o] : 0u;
+                    sl[k] = p[k] != NIL ? B.ox[o] : 0u;
                 }
-                if (lcnt) {
-#pragma unroll
-                    for (u32 k = 0; k < RK; ++k) {
-                        if (q[k] != NIL) {
-                            const u32 u = idr[k] - np0;
-                            B.occpos[sh.npoff[u] + ex.add(&sh.ncnt[u], 1u)] = i[k];
-                        }
-                        if (p[k] != NIL) {
-                            const u32 u = idl[k] - np0;
-                            B.occpos[sh.npoff[u] + ex.add(&sh.ncnt[u], 1u)] = p[k];
-                        }
+                // the new pair's id and this occurrence's place in its region
+                auto place = [&](u32 slot, u32 pos) {
+                    u32 id, at;
+                    if (slot & GSLOT) {
+                        id = B.hval[slot & ~GSLOT];
+                        at = B.poff[id] + ex.add(&B.plen[id], 1u);
+                    } else {
+                        id = sh.sval[slot];
+                        at = sh.spoff[slot] + ex.add(&sh.cslot[slot], 1u);
                     }
-                    continue;
-                }
+                    B.occpos[at] = pos;
+                    return id;
+                };
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
-                    br[k] = q[k] != NIL ? B.poff[idr[k]] : 0u;
-                    bl[k] = p[k] != NIL ? B.poff[idl[k]] : 0u;
-                }
-#pragma unroll
-                for (u32 k = 0; k < RK; ++k) {
-                    const bool hq = q[k] != NIL, hp = p[k] != NIL;
-                    const u32 sr = ex.slot_agg(&B.plen[idr[k]], hq, agg);
-                    const u32 sl = ex.slot_agg(&B.plen[idl[k]], hp, agg);
-                    if (hq) B.occpos[br[k] + sr] = i[k];
-                    if (hp) B.occpos[bl[k] + sl] = p[k];
+                    if (!act[k]) continue;
+                    const u32 o = o0 + k * NT;
+                    const u32 idr = q[k] != NIL ? place(sr[k], i[k]) : NIL;
+                    B.nd[i[k]] = Node{q[k], B.onp[o], X0 + m[k], idr};  // one 16-byte store
+                    if (p[k] != NIL) B.nd[p[k]].opair = place(sl[k], p[k]);
                 }
             }
             for (u32 u = t; u < sh.hused; u += NT)  // clear the keys that went to the global table
