@@ -136,7 +136,7 @@ struct Shared {
     u32 wtot[NT / 64], wtot2[NT / 64];
     u64 st_key[NT];             // window staging by level entry: key, id, region length / offset
     u32 st_id[NT], st_len[NT], st_off[NT];
-    u32 irank[2 * NT];          // init: slot << 16 | rank of each position of a chunk
+    u32 irank[4 * NT];          // init: slot << 16 | rank of each position of a chunk
     u32 chg[3];
     u64 skey[SORT_LDS];
     u32 sval[SORT_LDS];
@@ -297,20 +297,24 @@ RP_HD inline u32 hash_claim(E& ex, const Block& B, Shared& sh, u64 key) {
 }
 
 // Init-time pair table: slot of a 16-bit byte-pair code (IC positions per chunk into ICT
-// slots: at most half full, so a probe run always ends).
-constexpr u32 IC = 2 * NT;
+// slots; text holds ~1000-1500 distinct pairs per chunk).  NIL after IPROBE probes (random
+// bytes nearly fill the table): the caller then counts / places that position directly.
+constexpr u32 IC = 4 * NT;
 constexpr u32 ICT = 4096;
-static_assert(ICT >= 2 * IC && ICT <= SORT_LDS && 2 * ICT <= 2 * SORT_LDS, "init table");
+constexpr u32 IPROBE = 64;
+static_assert(ICT <= SORT_LDS && IC <= 4096, "init table (keys in sval, counts / bases in skey)");
 template <class E>
 RP_HD inline u32 ictab_slot(E& ex, u32* keys, u32 code) {
-    for (u32 s = (code * 0x9E3779B1u) >> 20;; s = (s + 1) & (ICT - 1)) {
-        const u32 k = keys[s];
-        if (k == code) return s;
-        if (k == NIL) {
+    u32 s = (code * 0x9E3779B1u) >> 20;
+    for (u32 k = 0; k < IPROBE; ++k, s = (s + 1) & (ICT - 1)) {
+        const u32 cur = keys[s];
+        if (cur == code) return s;
+        if (cur == NIL) {
             const u32 old = ex.cas32(&keys[s], NIL, code);
             if (old == NIL || old == code) return s;
         }
     }
+    return NIL;
 }
 
 // hash_claim + one occurrence counted for the key (LDS slot counter, or the global slot's)
@@ -492,7 +496,10 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
 #pragma unroll
             for (u32 k = 0; k < IC / NT; ++k) {
                 const u32 i = c0 + k * NT + t;
-                if (i + 1 < n) ex.add(&ictc[ictab_slot(ex, ictk, ((u32)B.text[i] << 8) | B.text[i + 1])], 1u);
+                if (i + 1 < n) {
+                    const u32 code = ((u32)B.text[i] << 8) | B.text[i + 1], sl = ictab_slot(ex, ictk, code);
+                    ex.add(sl != NIL ? &ictc[sl] : &B.cnt[code], 1u);
+                }
             }
         });
         ex.par([&](u32 t) {
@@ -518,8 +525,13 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
             for (u32 k = 0; k < IC / NT; ++k) {
                 const u32 i = c0 + k * NT + t;
                 if (i + 1 < n) {
-                    const u32 sl = ictab_slot(ex, ictk, ((u32)B.text[i] << 8) | B.text[i + 1]);
-                    sh.irank[k * NT + t] = sl << 16 | ex.add(&ictc[sl], 1u);
+                    const u32 code = ((u32)B.text[i] << 8) | B.text[i + 1], sl = ictab_slot(ex, ictk, code);
+                    if (sl != NIL) {
+                        sh.irank[k * NT + t] = sl << 16 | ex.add(&ictc[sl], 1u);
+                    } else {
+                        B.occpos[B.poff[code] + ex.add(&B.plen[code], 1u)] = i;
+                        sh.irank[k * NT + t] = NIL;
+                    }
                 }
             }
         });
@@ -535,7 +547,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                 const u32 i = c0 + k * NT + t;
                 if (i + 1 < n) {
                     const u32 v = sh.irank[k * NT + t];
-                    B.occpos[ictb[v >> 16] + (v & 0xFFFFu)] = i;
+                    if (v != NIL) B.occpos[ictb[v >> 16] + (v & 0xFFFFu)] = i;
                 }
             }
             for (u32 s = t; s < ICT; s += NT) {  // ictb is read above, ictk / ictc no more
