@@ -74,6 +74,77 @@ __device__ inline u64 lds8(const u8* l, u32 x) {
     return ((u64)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
 }
 
+// 8 bytes of the text at x (little-endian) through an LText: the LDS copy when they lie in
+// it, else three aligned global dwords (bytes at or past `end` read as 0; a dword that
+// starts before `end` is allocated)
+__device__ inline u64 text8(const LText& t, u32 x, u32 end) {
+    if (x - t.lo < t.hi - t.lo && x + 8 <= t.hi) return lds8(t.l, x - t.lo);
+    if (x + 12 <= end) {
+        const u32* w = reinterpret_cast<const u32*>(t.g) + (x >> 2);
+        const u32 sh = x & 3;
+        const u32 w0 = w[0], w1 = w[1], w2 = w[2];
+        return ((u64)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
+    }
+    u64 v = 0;
+    for (u32 k = 0; k < 8; ++k)
+        if (x + k < end) v |= (u64)t[x + k] << (8 * k);
+    return v;
+}
+
+// 8 bytes of global text at x (little-endian) from three aligned dwords; x + 12 <= end
+__device__ inline u64 glob8(const u8* g, u32 x) {
+    const u32* w = reinterpret_cast<const u32*>(g) + (x >> 2);
+    const u32 sh = x & 3;
+    const u32 w0 = w[0], w1 = w[1], w2 = w[2];
+    return ((u64)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
+}
+
+// wave_lcp for long extensions in the stitch (matches of periodic data run to hundreds of
+// KB): 8 bytes per lane, 512 per wave step; where both sides lie in global memory well
+// before `end`, four steps per round trip (loads issued unconditionally, compared after)
+__device__ u32 wave_lcp8(const LText& t, u32 p, u32 q, u32 start, u32 maxl, u32 end) {
+    const u32 lane = threadIdx.x & 63;
+    constexpr u32 U = 4;
+    u32 l = start;
+    for (;;) {
+        const u32 hi = max(p, q) + l + 512 * U;  // furthest byte this round trip may touch
+        if (min(p, q) + l >= t.hi && hi + 12 <= end && l + 512 * U <= maxl) {
+            u64 d[U];
+#pragma unroll
+            for (u32 s = 0; s < U; ++s) {
+                const u32 o = l + 512 * s + 8 * lane;
+                d[s] = glob8(t.g, p + o) ^ glob8(t.g, q + o);
+            }
+#pragma unroll
+            for (u32 s = 0; s < U; ++s) {
+                const u64 bal = __ballot(d[s] != 0);
+                if (bal) {
+                    const u32 j = (u32)__ffsll((long long)bal) - 1;
+                    const u32 k = (u32)(__ffsll((long long)d[s]) - 1) >> 3;
+                    return l + 512 * s + 8 * j + (u32)__builtin_amdgcn_readlane((int)k, (int)j);
+                }
+            }
+            l += 512 * U;
+            continue;
+        }
+        const u32 o = l + 8 * lane;
+        u32 k = 8;  // first mismatching byte of this lane's 8 (8: none)
+        if (o >= maxl) {
+            k = 0;
+        } else {
+            const u64 d = text8(t, p + o, end) ^ text8(t, q + o, end);
+            if (d) k = (u32)(__ffsll((long long)d) - 1) >> 3;
+            k = min(k, maxl - o);
+        }
+        const u64 bal = __ballot(k < 8);
+        if (bal) {
+            const u32 j = (u32)__ffsll((long long)bal) - 1;
+            return l + 8 * j + (u32)__builtin_amdgcn_readlane((int)k, (int)j);
+        }
+        l += 512;
+    }
+}
+
 // =====================================================================================
 // Workgroup-local 3-gram index and speculative parse.
 //
@@ -435,8 +506,11 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
 // [wlo, whi) refreshed when q's window is not inside it.  One wave.
 constexpr u32 BF_WIN = LZ_WINDOW + 1024;
 
+// d0s > 0 (an unresolved token of k_lz_local): every distance below d0s matches fewer than
+// l0s bytes and d0s at least l0s (the local parse's capped answer), so the search starts
+// from d0s's exact length and only tries the distances past it.
 __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u32 base, u32 end, u32& out_len,
-                         u32& out_dist, u32& nlong) {
+                         u32& out_dist, u32& nlong, u32 d0s = 0, u32 l0s = 0) {
     const u32 lane = threadIdx.x & 63;
     out_len = 0;
     out_dist = 0;
@@ -465,24 +539,56 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
     const u32 capl = min((u32)LZ_CAP, maxl);
     const u8 c0 = t[q], c1 = t[q + 1], c2 = t[q + 2];
     u32 best = 0, bd = 0;
-    for (u32 d0 = 1; d0 <= dmax; d0 += 64) {
+    if (d0s) {
+        const u64 tl0 = z.prof ? wall_clock64() : 0;
+        best = wave_lcp8(t, q, q - d0s, l0s, maxl, end);
+        bd = d0s;
+        ++nlong;
+        if (z.prof && lane == 0) {
+            atomicAdd(z.prof + 14, wall_clock64() - tl0);
+            atomicAdd(z.prof + 15, (u64)best);
+        }
+    }
+    // No farther distance beats a match at least dmax - 1 long (Fine and Wilf: a strictly
+    // longer match at d > bd would give the text periods d and bd over the last best + bd
+    // bytes, hence period gcd(d, bd), and then the byte at best would match at bd too).
+    for (u32 d0 = d0s + 1; d0 <= dmax && best < maxl && best + 1 < dmax; d0 += 64) {
         const u32 d = d0 + lane;
         const u32 x = q - d;
         bool ok = d <= dmax && t[x] == c0 && t[x + 1] == c1 && t[x + 2] == c2;
         if (ok && best) ok = best < maxl && t[x + best] == t[q + best];
+        if (ok && best > 2 * LZ_CAP) {
+            // a longer match agrees everywhere below best: 8 spread samples reject most
+            // candidates of periodic text that run out earlier (each would be an
+            // extension over KB of text)
+#pragma unroll
+            for (u32 k = 1; k <= 8; ++k) {
+                const u32 y = (u32)(((u64)best * k) / 9);
+                ok = ok && t[x + y] == t[q + y];
+            }
+        }
         u32 l = 0;
         if (ok) {
             l = LZ_MIN;
             while (l < capl && t[x + l] == t[q + l]) ++l;
         }
+        // capped candidates in ascending distance, each extended by the whole wave unless it
+        // cannot be strictly longer than the longest one so far (`bb`): that needs a match at
+        // bb (periodic text otherwise extends every multiple of its period to the same end)
         u64 longm = __ballot(ok && l >= capl && capl < maxl);
+        u32 bb = best;
         while (longm) {
             const u32 j = (u32)__ffsll((long long)longm) - 1;
             const u32 xj = __builtin_amdgcn_readlane(x, j);
-            const u32 lj = wave_lcp(t, q, xj, capl, maxl);
-            if (lane == j) l = lj;
+            if (bb > capl && (bb >= maxl || t[xj + bb] != t[q + bb])) {
+                if (lane == j) l = capl;  // LCP <= bb: an earlier candidate or `best` wins
+            } else {
+                const u32 lj = wave_lcp8(t, q, xj, capl, maxl, end);
+                if (lane == j) l = lj;
+                bb = max(bb, lj);
+                ++nlong;
+            }
             longm &= longm - 1;
-            ++nlong;
         }
         const u32 lv = ok ? l : 0u;
         const u32 lm = wave_reduce(lv, OpMaxU(), 0u);
@@ -491,7 +597,7 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
             best = lm;
             bd = d0 + (u32)__ffsll((long long)eq) - 1;
         }
-        if (best >= maxl) break;
+        if (best >= maxl || best + 1 >= dmax) break;
     }
     if (best >= (u32)LZ_MIN) {
         out_len = best;
@@ -502,6 +608,7 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
 // Per block (one wave): the true path over the chunk summaries of k_lz_local.
 __global__ __launch_bounds__(64) void k_lz_stitch_l(LzArgs z) {
     __shared__ __align__(16) u8 win[BF_WIN + 16];
+    const u64 tst = z.prof ? wall_clock64() : 0;
     const u32 b = blockIdx.x, lane = threadIdx.x;
     const u32 base = z.geo.base(b), bend = z.geo.end(b);
     const u32 CH = 1u << z.cshift;
@@ -534,6 +641,7 @@ __global__ __launch_bounds__(64) void k_lz_stitch_l(LzArgs z) {
                 spec = by;
                 next = ex;
             } else {
+                if (z.prof && lane == 0) atomicAdd(z.prof + 13, (u64)1);
                 u32 q = entry, jt = 0;
                 bool conv = false;
                 while (q < e) {
@@ -556,7 +664,12 @@ __global__ __launch_bounds__(64) void k_lz_stitch_l(LzArgs z) {
                         break;
                     }
                     u32 len, dist;
+                    const u64 tb0 = z.prof ? wall_clock64() : 0;
                     bf_match(z, win, wlo, whi, q, base, bend, len, dist, nlong);
+                    if (z.prof && lane == 0) {
+                        atomicAdd(z.prof + 8, (u64)1);
+                        atomicAdd(z.prof + 9, wall_clock64() - tb0);
+                    }
                     if (lane == 0) {
                         z.fix_pos[base + fi] = q;
                         z.fix_len[base + fi] = len;
@@ -577,7 +690,12 @@ __global__ __launch_bounds__(64) void k_lz_stitch_l(LzArgs z) {
                         const u32 li = s + nt - 1;
                         const u32 pp = z.tok_pos[li], ol = z.tok_len[li], od = z.tok_dist[li];
                         u32 nl, nd;
-                        bf_match(z, win, wlo, whi, pp, base, bend, nl, nd, nlong);
+                        const u64 tb0 = z.prof ? wall_clock64() : 0;
+                        bf_match(z, win, wlo, whi, pp, base, bend, nl, nd, nlong, od, ol);
+                        if (z.prof && lane == 0) {
+                            atomicAdd(z.prof + 10, (u64)1);
+                            atomicAdd(z.prof + 11, wall_clock64() - tb0);
+                        }
                         spec = spec + tok_bytes(nl, nd) - tok_bytes(ol, od);
                         if (lane == 0) {
                             z.tok_len[li] = nl;
@@ -610,6 +728,7 @@ __global__ __launch_bounds__(64) void k_lz_stitch_l(LzArgs z) {
             z.c_off[c] = o_off;
         }
     }
+    if (z.prof && lane == 0) atomicMax((unsigned long long*)(z.prof + 12), (unsigned long long)(wall_clock64() - tst));
     if (lane == 0) {
         z.lz_size[b] = boff;
         z.ntok[b] = ntot;

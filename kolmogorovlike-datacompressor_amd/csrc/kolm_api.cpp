@@ -637,14 +637,14 @@ struct Pipeline {
         z.nlong = c->get<u32>("counters", C_N) + C_NLONG;
         z.nfix = c->get<u32>("counters", C_N) + C_NFIX;
         static const bool lz_prof = getenv("KOLM_LZ_PROF") && atoi(getenv("KOLM_LZ_PROF")) != 0;
-        if (lz_prof) z.prof = c->get<u64>("lz_prof", 8);
+        if (lz_prof) z.prof = c->get<u64>("lz_prof", 16);
         return z;
     }
 
     void lz(const LzArgs& z) {
         KOLM_HIP_CHECK(hipMemsetAsync(z.nlong, 0, sizeof(u32), c->active));
         KOLM_HIP_CHECK(hipMemsetAsync(z.nfix, 0, sizeof(u32), c->active));
-        if (z.prof) KOLM_HIP_CHECK(hipMemsetAsync(z.prof, 0, sizeof(u64) * 8, c->active));
+        if (z.prof) KOLM_HIP_CHECK(hipMemsetAsync(z.prof, 0, sizeof(u64) * 16, c->active));
         launch_lz_parse(z, c->active, c->kt());
     }
 };
@@ -1034,13 +1034,17 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     }
     if (h_off) std::memcpy(h_off, off.data(), sizeof(u64) * (nb + 1));
     if (want_lz && z.prof) {
-        u64 pr[8];
+        u64 pr[16];
         KOLM_HIP_CHECK(hipMemcpy(pr, z.prof, sizeof pr, hipMemcpyDeviceToHost));
         const double nwg = pr[6] ? (double)pr[6] : 1.0;
         fprintf(stderr, "[kolm] k_lz_local us per workgroup: load %.2f sort %.2f index %.2f parse %.2f; "
                 "wave token steps %.1f, candidate batches %.1f per wave (%llu workgroups)\n",
                 pr[0] / nwg / 100.0, pr[1] / nwg / 100.0, pr[2] / nwg / 100.0, pr[3] / nwg / 100.0,
                 pr[4] / nwg / 4.0, pr[5] / nwg / 4.0, (unsigned long long)pr[6]);
+        fprintf(stderr, "[kolm] k_lz_stitch_l: %llu fix-up searches %.1f us, %llu unresolved re-searches %.1f us, "
+                "%llu chunks walked token by token, max block %.1f us; re-search exact lengths: %.1f us, %llu bytes\n",
+                (unsigned long long)pr[8], pr[9] / 100.0, (unsigned long long)pr[10], pr[11] / 100.0,
+                (unsigned long long)pr[13], pr[12] / 100.0, pr[14] / 100.0, (unsigned long long)pr[15]);
     }
     u64 tokens = 0;
     for (u32 v : ntok) tokens += v;
