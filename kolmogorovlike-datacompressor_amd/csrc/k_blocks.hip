@@ -456,7 +456,31 @@ __device__ inline u64 load8u(const u8* s, u32 x) {
 __device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N, u32* nsteps = nullptr, u32 o0 = 0) {
     const u32 lane = threadIdx.x & 63;
     const u32 la = a1 - a0, lb = b1 - a1, m = min(la, lb);
-    for (u32 o = o0; o < m; o += 512) {
+    u32 o = o0;
+    // long common prefixes (periodic data: factors agree on KB): four 512-byte steps per
+    // round trip while they lie wholly inside both factors and s[0, N)
+    constexpr u32 U = 4;
+    while (o + 512 * U <= m && (u64)a1 + o + 512 * U + 12 <= N) {
+        if (nsteps) *nsteps += U;
+        u64 d[U];
+#pragma unroll
+        for (u32 k = 0; k < U; ++k) {
+            const u32 t = o + 512 * k + 8 * lane;
+            d[k] = load8u(s, a0 + t) ^ load8u(s, a1 + t);
+        }
+#pragma unroll
+        for (u32 k = 0; k < U; ++k) {
+            const u64 bal = __ballot(d[k] != 0);
+            if (bal) {
+                const u32 j = (u32)__ffsll((long long)bal) - 1;
+                const u32 dj = (u32)__ffsll((long long)d[k]) - 1;
+                const u32 dpos = o + 512 * k + 8 * j + (u32)__builtin_amdgcn_readlane((int)dj, (int)j) / 8;
+                return s[a0 + dpos] < s[a1 + dpos];
+            }
+        }
+        o += 512 * U;
+    }
+    for (; o < m; o += 512) {
         if (nsteps) ++*nsteps;
         const u32 t = o + 8 * lane;
         u32 dpos = 0xFFFFFFFFu;
