@@ -896,8 +896,8 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
         if (!aa) {
             ex.par([&](u32 t) {
                 for (u32 e0 = 0; e0 < tot; e0 += RK * NT) {
-                    u32 pos[RK], lo[RK], p[RK], j[RK], q[RK], x[RK], pj[RK], pp[RK], ppv[RK], y[RK], pq[RK];
-                    bool valid[RK], lc[RK];
+                    u32 pos[RK], lo[RK], p[RK], j[RK], q[RK], x[RK], pj[RK], pp[RK], ppv[RK], y[RK], pq[RK], lpr[RK];
+                    bool valid[RK];
 #pragma unroll
                     for (u32 k = 0; k < RK; ++k) {
                         const u32 e = e0 + k * NT + t;
@@ -936,34 +936,35 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                         const Node cq = B.nd[q[k] != NIL ? q[k] : 0u];
                         y[k] = cq.sym;
                         pq[k] = q[k] != NIL ? cq.opair : NIL;
-                        lc[k] = p[k] != NIL && ppv[k] != NIL && x[k] == sh.m_b[lo[k]];
-                        lc[k] = lc[k] && B.nd[ppv[k]].opair == sh.m_id[lo[k]];
+                        lpr[k] = p[k] != NIL && ppv[k] != NIL ? B.nd[ppv[k]].opair : NIL;  // pair ending at p
                     }
 #pragma unroll
                     for (u32 k = 0; k < RK; ++k) {
                         const u32 o = ex.append(&sh.nocc, valid[k]);
                         if (valid[k]) {
                             const u32 m = lo[k];
+                            // overlaps: the pair at p or at j is another member's
                             const u32 c1 = member_of(sh, pp[k]), c2 = q[k] != NIL ? member_of(sh, pj[k]) : NIL;
-                            const u32 c3 = member_of(sh, pq[k]);
                             u32 cut = NIL;
                             if (c1 != NIL) cut = umax(m, c1);
                             if (c2 != NIL) cut = umin(cut, umax(m, c2));
-                            if (c3 != NIL && c3 != m) cut = umin(cut, umax(m, c3));
                             if (cut != NIL) ex.min(&sh.t1, cut);
-                            const bool rightc = c3 == m;
-                            const u32 xl = (p[k] != NIL && !lc[k]) ? x[k] : NIL;
+                            // neighbours: the member whose occurrence ends at p (lm) / starts at q (rm)
+                            const u32 lm = member_of(sh, lpr[k]), rm = q[k] != NIL ? member_of(sh, pq[k]) : NIL;
+                            // left symbol when m runs: p's (an earlier or the same member makes it new)
+                            const u32 xl = (p[k] != NIL && !(lm != NIL && lm <= m)) ? x[k] : NIL;
                             ex.min(&sh.m_lmin[m], xl);
                             ex.max(&sh.m_lmax[m], xl);
                             B.opos[o] = pos[k];
                             B.omem[o] = m;
                             B.oj[o] = j[k];
-                            B.op[o] = lc[k] ? NIL : p[k];
+                            B.op[o] = p[k];
                             B.oq[o] = q[k];
-                            B.onp[o] = lc[k] ? ppv[k] : p[k];
-                            B.oidl[o] = xl;                                                  // left symbol
-                            B.oidr[o] = q[k] == NIL ? NIL : rightc ? X0 + m : y[k];  // right symbol
-                            B.oy[o] = rightc ? 1u : 0u;
+                            B.onp[o] = ppv[k];
+                            B.ox[o] = x[k];
+                            B.oy[o] = y[k];
+                            B.oidl[o] = lm;
+                            B.oidr[o] = rm;
                             B.opj[o] = pj[k];
                             B.opp[o] = pp[k];
                         }
@@ -1096,55 +1097,49 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
             });
         }
         ex.mark(P_SELECT);
-        // ---- (a,a) batches: conflicts (footprint {p, i, j, q} vs earlier members' spans),
-        //      left-neighbour uniformity, the replaced neighbours; one mark word per footprint
-        //      position ----
+        // ---- (a,a) batches: overlaps (i or j in an earlier member's span), the neighbouring
+        //      chosen occurrences, left-neighbour uniformity; one mark word per position ----
         if (aa) ex.par([&](u32 t) {
             for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
-                bool act[RK];
+                bool act[RK], in[RK];
                 u32 m[RK], i[RK], p[RK], j[RK], q[RK], wi[RK], wj[RK], wp[RK], wq[RK];
                 // mark of an earlier member of this batch (either position of its span)
                 auto early = [&](u32 w, u32 mm) { return w >= m2s(0) && w < m2s(mm); };
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
                     const u32 o = o0 + k * NT;
-                    act[k] = o < nocc && !(aa && (dist[o] & 1u));
-                    m[k] = act[k] ? B.omem[o] : 0u;
-                    i[k] = act[k] ? B.opos[o] : 0u;
-                    j[k] = act[k] ? B.oj[o] : 0u;
+                    in[k] = o < nocc;
+                    act[k] = in[k] && !(dist[o] & 1u);  // chosen
+                    m[k] = in[k] ? B.omem[o] : 0u;
+                    i[k] = in[k] ? B.opos[o] : 0u;
+                    j[k] = in[k] ? B.oj[o] : 0u;
                     p[k] = act[k] ? B.op[o] : NIL;
                     q[k] = act[k] ? B.oq[o] : NIL;
                 }
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
-                    wi[k] = act[k] ? B.mark[i[k]] : NIL;
-                    wj[k] = act[k] ? B.mark[j[k]] : NIL;
+                    wi[k] = in[k] ? B.mark[i[k]] : NIL;
+                    wj[k] = in[k] ? B.mark[j[k]] : NIL;
                     wp[k] = p[k] != NIL ? B.mark[p[k]] : NIL;
                     wq[k] = q[k] != NIL ? B.mark[q[k]] : NIL;
                 }
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
+                    // an occurrence of the member in an earlier member's span (chosen or not:
+                    // the unchosen ones of a run count too) changes its count
+                    if (in[k] && (early(wi[k], m[k]) || early(wj[k], m[k]))) ex.min(&sh.t1, m[k]);
                     if (!act[k]) continue;
                     const u32 o = o0 + k * NT;
-                    if (early(wi[k], m[k]) || early(wj[k], m[k]) || early(wp[k], m[k]) || early(wq[k], m[k]))
-                        ex.min(&sh.t1, m[k]);
-                    // p is the second position of a chosen occurrence of this member (its start
-                    // pp becomes X too: the new left pair is (X, X), counted by that occurrence);
-                    // q starts one (the new right pair is (X, X))
-                    const bool leftc = p[k] != NIL && wp[k] == (m2s(m[k]) | 1u);
-                    const bool rightc = q[k] != NIL && wq[k] == m2s(m[k]);
-                    const u32 x = (p[k] != NIL && !leftc) ? B.ox[o] : NIL;
+                    // neighbours (resolved against T in apply 1): p the second position of a
+                    // chosen occurrence (lm), q the start of one (rm) — this batch's marks only
+                    auto cur = [&](u32 w) { return w >= m2s(0) && w < m2s(M); };
+                    const u32 lm = p[k] != NIL && cur(wp[k]) && (wp[k] & 1u) ? (wp[k] >> 1) - otag0 : NIL;
+                    const u32 rm = q[k] != NIL && cur(wq[k]) && !(wq[k] & 1u) ? (wq[k] >> 1) - otag0 : NIL;
+                    const u32 x = (p[k] != NIL && !(lm != NIL && lm <= m[k])) ? B.ox[o] : NIL;
                     ex.min(&sh.m_lmin[m[k]], x);
                     ex.max(&sh.m_lmax[m[k]], x);
-                    if (leftc) {
-                        B.op[o] = NIL;
-                        // B.onp[o] keeps pp: i's new left neighbour
-                    } else {
-                        B.onp[o] = p[k];
-                    }
-                    B.oidl[o] = x;                                                     // left symbol
-                    B.oidr[o] = q[k] == NIL ? NIL : rightc ? X0 + m[k] : B.oy[o];  // right symbol
-                    B.oy[o] = rightc ? 1u : 0u;  // q's link is rewritten by its own occurrence
+                    B.oidl[o] = lm;
+                    B.oidr[o] = rm;
                 }
             }
         });
@@ -1176,7 +1171,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
         //      in apply 4, where the ids are read) ----
         ex.par([&](u32 t) {
             for (u32 o0 = t; o0 < nocc; o0 += RK * NT) {
-                bool act[RK];
+                bool act[RK], rcf[RK];
                 u32 m[RK], p[RK], q[RK], xl[RK], yr[RK], pj[RK], pp[RK];
 #pragma unroll
                 for (u32 k = 0; k < RK; ++k) {
@@ -1186,8 +1181,23 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                     act[k] = act[k] && m[k] < T;
                     p[k] = act[k] ? B.op[o] : NIL;
                     q[k] = act[k] ? B.oq[o] : NIL;
-                    xl[k] = act[k] ? B.oidl[o] : 0u;
-                    yr[k] = act[k] ? B.oidr[o] : 0u;
+                    if (act[k]) {
+                        // the occurrences that end at p / start at q are replaced too when their
+                        // members run in this batch: p then belongs to the left one (which makes
+                        // the joint pair (X_lm, X_m) as its right pair), q's symbol becomes X_rm
+                        const u32 lm = B.oidl[o], rm = B.oidr[o];
+                        const bool lc = lm != NIL && lm < T;
+                        rcf[k] = rm != NIL && rm < T;
+                        const u32 pv = p[k];
+                        if (lc) p[k] = NIL;
+                        B.op[o] = p[k];
+                        B.onp[o] = lc ? B.onp[o] : pv;  // i's new left neighbour: pp or p
+                        xl[k] = B.ox[o];
+                        yr[k] = rcf[k] ? X0 + rm : B.oy[o];
+                    } else {
+                        rcf[k] = false;
+                        xl[k] = yr[k] = 0u;
+                    }
                     pj[k] = q[k] != NIL ? B.opj[o] : 0u;  // pairs at j and p (gathered)
                     pp[k] = p[k] != NIL ? B.opp[o] : 0u;
                 }
@@ -1209,7 +1219,7 @@ RP_HD __attribute__((always_inline)) inline void repair_block(E& ex, const Block
                     // j is written whole (i in apply 4, with its pair id); q's link only when q
                     // does not start a chosen occurrence itself (that one writes its own record)
                     B.nd[B.oj[o]] = Node{NIL, NIL, DEAD, NIL};
-                    if (q[k] != NIL && B.oy[o] == 0u) B.nd[q[k]].prv = B.opos[o];
+                    if (q[k] != NIL && !rcf[k]) B.nd[q[k]].prv = B.opos[o];
                 }
             }
         });
