@@ -32,12 +32,16 @@
 //     round can (i) lower the count of a later pair whose occurrences touch its own, and
 //     (ii) create a pair (x, X) with count f that sorts before later ones.
 //   * a BATCH is the longest prefix of the next W level pairs whose rounds commute with
-//     the rounds before them: no member's occurrence footprint {prv, i, nxt, nxt2} meets
-//     an earlier member's occurrence span {i, nxt}, no earlier member creates (x, X_k)
-//     with count f and x < a of the member, and no earlier member stops the run.  All
-//     rounds of a batch then execute in parallel with symbols X_k = next + k, which is
-//     the sequential result bit for bit.  Overlapping runs of (a,a) are resolved by
-//     pointer jumping (greedy left-to-right pairing = even distance from the run start).
+//     the rounds before them: no occurrence of a member (chosen or not) overlaps an earlier
+//     member's chosen occurrence span {i, nxt} (that would change the member's count), no
+//     earlier member creates (x, X_k) with count f and x < a of the member (x = the left
+//     symbol as of the member's turn), and no earlier member stops the run.  All rounds of
+//     a batch then execute in parallel with symbols X_k = next + k, which is the
+//     sequential result bit for bit.  Occurrences of two members that merely touch are
+//     joined: the left one makes the pair (X_left, X_right) once, the right one makes no
+//     left pair (the net effect of the two rounds in either order).  Overlapping runs of
+//     (a,a) are resolved by pointer jumping (greedy left-to-right pairing = even distance
+//     from the run start).
 #pragma once
 #include <stdint.h>
 
