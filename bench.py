@@ -148,6 +148,11 @@ def load_golden_stream(rank: int, n: int, bs: int):
     return g
 
 
+def golden_subset(g, idx):
+    """The oracle records of the blocks idx of a stream (a rank's round-robin shard)."""
+    return {"blocks": [g["blocks"][i] for i in idx]} if g else None
+
+
 def check_blocks(g, sizes, method, arena_host, off, ncand, wkey, shakey):
     """Blocks whose sizes (ids < ncand), winner and winner sha256 all match the oracle."""
     ok = 0
@@ -200,6 +205,12 @@ def main():
                     help="timed repetitions of the config-2 / config-5 legs (gradient block, mixed corpus); 0 = skip")
     ap.add_argument("--host-steps", type=int, default=2,
                     help="timed kolm.compress_blocks_fixed(bytes) calls on the host buffer (PCIe-inclusive); 0 = skip")
+    ap.add_argument("--strong", action="store_true",
+                    help="headline = BASELINE config 4's shape: --mib MiB TOTAL (rank 0's stream) in 1 MiB blocks "
+                         "round-robin over the ranks (block i on rank i mod N), RCCL gather to rank 0; strong scaling")
+    ap.add_argument("--c4-steps", type=int, default=5,
+                    help="timed steps of the config-4 leg (N=1: the 8-GPU shard, blocks i = 0 mod 8 of the stream; "
+                         "N>1: the whole config, --mib MiB total round-robin); 0 = skip")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -212,8 +223,18 @@ def main():
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     n = a.mib << 20
     t = time.time()
-    data = datagen.enwik_like(n, seed=datagen.ENWIK_SEED + rank)
+    stream0 = None  # rank 0's stream: the config-4 data (256 MiB total, sharded)
+    if a.strong or a.c4_steps > 0:
+        stream0 = datagen.enwik_like(n, seed=datagen.ENWIK_SEED)
+    data = stream0 if rank == 0 and stream0 is not None else datagen.enwik_like(n, seed=datagen.ENWIK_SEED + rank)
     log(rank, f"[bench] generated {a.mib} MiB per rank in {time.time() - t:.1f}s")
+    nb_stream = (n + a.bs - 1) // a.bs
+    golden_full = load_golden_stream(rank, n, a.bs)
+    if a.strong:  # this rank's round-robin shard of rank 0's stream is the workload
+        mine = list(range(rank, nb_stream, world))
+        data = b"".join(stream0[i * a.bs:(i + 1) * a.bs] for i in mine)
+        golden_full = golden_subset(load_golden_stream(0, n, a.bs), mine)
+        n = len(data)
 
     L = _lib.load()
     ctx = ctypes.c_void_p()
@@ -245,7 +266,8 @@ def main():
                                                ctypes.byref(st)))
         if world > 1:
             ids = torch.from_numpy(method.astype(np.int32)).cuda()
-            pending[j] = gather_payloads(buf, int(off[-1]), ids, dst=0, async_op=True)
+            offs = torch.from_numpy(off.astype(np.int64)).cuda()
+            pending[j] = gather_payloads(buf, int(off[-1]), ids, dst=0, async_op=True, offsets=offs)
         return buf
 
     def drain():
@@ -275,14 +297,15 @@ def main():
     el, _ = timed(lambda: step(_lib.Stats()), a.steps)
     arena = arenas[(nstep[0] - 1) % len(arenas)]
     ms_step = el / a.steps * 1e3
-    value = world * n * a.steps / el / MB
+    ntot = sum_all(n, world)  # whole-job input bytes per step
+    value = ntot * a.steps / el / MB
 
     # ---- parity of the timed output, block by block, against the oracle's answers ----
-    golden = load_golden_stream(rank, n, a.bs)
+    golden = golden_full
     arena_host = arena[:int(off[-1])].cpu().numpy().tobytes() if golden else None
     parity_ok = check_blocks(golden, sizes, method, arena_host, off, 9, "w9", "sha9") if golden else 0
     parity_checked = nb if golden else 0
-    parity = {"ok": sum_all(parity_ok, world), "checked": sum_all(parity_checked, world), "blocks": world * nb}
+    parity = {"ok": sum_all(parity_ok, world), "checked": sum_all(parity_checked, world), "blocks": sum_all(nb, world)}
     log(rank, f"[bench] parity {parity}")
 
     # ---- kernel-timed pass (HIP events around every launch) ----
@@ -399,7 +422,7 @@ def main():
         acc[0] = 0.0
         eld, _ = timed(dstep, a.decode_steps)
         del d_out
-        return {"value": round(world * n * a.decode_steps / eld / MB, 2), "unit": "MB/s", "steps": a.decode_steps,
+        return {"value": round(ntot * a.decode_steps / eld / MB, 2), "unit": "MB/s", "steps": a.decode_steps,
                 "ms_per_step": round(eld / a.decode_steps * 1e3, 2),
                 "kernel_ms_per_step": round(acc[0] / a.decode_steps, 2), "round_trip_exact": ok,
                 "methods": np.bincount(method, minlength=10).tolist()}
@@ -421,7 +444,7 @@ def main():
         elf, _ = timed(full_step, a.full_steps)
         cur_arena[0] = arenas[(nstep[0] - 1) % len(arenas)]
         f0 = fst[-1].as_dict()
-        full = {"value": round(world * n * a.full_steps / elf / MB, 2), "unit": "MB/s", "steps": a.full_steps,
+        full = {"value": round(ntot * a.full_steps / elf / MB, 2), "unit": "MB/s", "steps": a.full_steps,
                 "ms_per_step": round(elf / a.full_steps * 1e3, 2), "candidates": "0..9 (PY's full list)",
                 "ms_repair": round(f0["ms_repair"], 2), "ratio": round(float(off[-1]) / n, 4),
                 "methods": np.bincount(method, minlength=10).tolist(),
@@ -463,7 +486,7 @@ def main():
         cdc_step()
         elc, _ = timed(cdc_step, a.cdc_steps)
         nbc = int(nch.value)
-        cdc = {"value": round(world * n * a.cdc_steps / elc / MB, 2), "unit": "MB/s", "steps": a.cdc_steps,
+        cdc = {"value": round(ntot * a.cdc_steps / elc / MB, 2), "unit": "MB/s", "steps": a.cdc_steps,
                "ms_per_step": round(elc / a.cdc_steps * 1e3, 2), "ms_boundaries": round(cst["ms_bounds"], 2),
                "params": [4096, 8192, 16384], "chunks_per_gpu": nbc, "candidates": "0..8",
                "ratio": round(float(coff[nbc]) / n, 4)}
@@ -580,6 +603,78 @@ def main():
                         "container buffer, one copy into the returned bytes; ms_h2d/d2h_pageable: plain torch "
                         "copies of the same bytes for comparison"}
 
+    # BASELINE config 4 (256 MiB TOTAL in 1 MiB blocks, round-robin over the GPUs, RCCL
+    # gather to rank 0).  N > 1: the whole config, every rank its shard i = rank (mod N)
+    # of rank 0's stream, gathered asynchronously into rank 0 as in the headline.  N = 1:
+    # what one GPU of the 8-GPU run encodes — the 32 blocks i = 0 (mod 8) — timed alone,
+    # so the per-GPU rate of config 4's shard size is measured beside the 256 MiB one.
+    c4 = None
+    if a.c4_steps > 0 and not a.strong and stream0 is not None:
+        G = world if world > 1 else 8
+        r4 = rank if world > 1 else 0
+        mine4 = list(range(r4, nb_stream, G))
+        n4 = len(mine4) * a.bs  # 1 MiB blocks of a whole-MiB stream: every block full
+        d4 = torch.empty(n4 + 64, dtype=torch.uint8, device="cuda")
+        d4[:n4].copy_(torch.frombuffer(bytearray(b"".join(stream0[i * a.bs:(i + 1) * a.bs] for i in mine4)),
+                                       dtype=torch.uint8))
+        cap4 = n4 + (4 << 20)
+        ar4 = [torch.empty(cap4, dtype=torch.uint8, device="cuda") for _ in range(2)]
+        pend4 = [None, None]
+        cnt4 = [0]
+        sz4 = np.zeros((len(mine4), _lib.KOLM_NCAND), np.uint32)
+        m4 = np.zeros(len(mine4), np.uint32)
+        o4 = np.zeros(len(mine4) + 1, np.uint64)
+
+        def c4_step():
+            j = cnt4[0] % 2
+            cnt4[0] += 1
+            if pend4[j] is not None:
+                pend4[j].wait()
+                pend4[j] = None
+            _lib.check(L.kolm_encode_blocks_device(ctx, d4.data_ptr(), n4, a.bs, _lib.KOLM_HOTPATH_MASK, None,
+                                                   ar4[j].data_ptr(), cap4, sz4.ctypes.data, m4.ctypes.data,
+                                                   o4.ctypes.data, None))
+            if world > 1:
+                ids = torch.from_numpy(m4.astype(np.int32)).cuda()
+                offs = torch.from_numpy(o4.astype(np.int64)).cuda()
+                pend4[j] = gather_payloads(ar4[j], int(o4[-1]), ids, dst=0, async_op=True, offsets=offs)
+
+        def c4_drain():
+            for j in range(2):
+                if pend4[j] is not None:
+                    pend4[j].wait()
+                    pend4[j] = None
+
+        c4_step()
+        c4_drain()
+        drain()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.c4_steps):
+            c4_step()
+        c4_drain()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el4 = sync_max(time.perf_counter() - t0, world)
+        g4 = golden_subset(load_golden_stream(0, a.mib << 20, a.bs), mine4)
+        ok4 = 0
+        if g4:
+            ok4 = check_blocks(g4, sz4, m4, ar4[(cnt4[0] - 1) % 2][:int(o4[-1])].cpu().numpy().tobytes(), o4, 9,
+                               "w9", "sha9")
+        tot4 = sum_all(n4, world)
+        c4 = {"value": round(tot4 * a.c4_steps / el4 / MB, 2), "unit": "MB/s", "steps": a.c4_steps,
+              "ms_per_step": round(el4 / a.c4_steps * 1e3, 3), "blocks_per_gpu": len(mine4),
+              "bytes_per_gpu": n4, "partition": f"round_robin over {G}",
+              "parity_blocks": f"{sum_all(ok4, world)}/{sum_all(len(mine4), world)}" if g4 else None,
+              "note": ("config 4 whole: rank 0's stream, block i on rank i mod N, async RCCL gather (payloads, ids, "
+                       "offsets) to rank 0 inside the timed region") if world > 1 else
+                      ("config 4's per-GPU shard at N = 8 (blocks i = 0 mod 8 of the 256 MiB stream, 32 MiB) on one "
+                       "GPU, no collective; MB/s of this GPU alone")}
+        del d4, ar4
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(data, a.bs, a.cpu_budget)
@@ -589,12 +684,16 @@ def main():
         out = {
             "metric": "compress MB/s at fixed block size, bit-exact vs reference; 1/2/4/8-GPU scaling",
             "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(ms_step, 2), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(ms_step, 2), "higher_is_better": True, "scaling": "strong" if a.strong else "weak",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": "enwik-style synthetic text (kolm.datagen.enwik_like, seed 20251212+rank), "
-                                   f"{a.mib} MiB per GPU resident in HBM, {a.bs >> 20} MiB fixed blocks, "
-                                   "candidates 0..8 + MDL, payloads emitted in HBM"
-                                   + (", RCCL gather to rank 0" if world > 1 else ""),
+            "config": {"workload": ("BASELINE config 4: enwik-style synthetic text (kolm.datagen.enwik_like, seed "
+                                    f"20251212), {a.mib} MiB TOTAL in {a.bs >> 20} MiB blocks sharded round-robin "
+                                    f"over {world} GPU(s), resident in HBM, candidates 0..8 + MDL, payloads emitted "
+                                    "in HBM" + (", RCCL gather to rank 0" if world > 1 else "")) if a.strong else
+                                   ("enwik-style synthetic text (kolm.datagen.enwik_like, seed 20251212+rank), "
+                                    f"{a.mib} MiB per GPU resident in HBM, {a.bs >> 20} MiB fixed blocks, "
+                                    "candidates 0..8 + MDL, payloads emitted in HBM"
+                                    + (", RCCL gather to rank 0" if world > 1 else "")),
                        "block_size": a.bs, "bytes_per_gpu": n, "blocks_per_gpu": nb,
                        "parallelism": f"block-shard x{world}"},
             "roofline": roof,
@@ -613,6 +712,7 @@ def main():
                        "v2_new": v2,
                        "configs": configs,
                        "host_e2e": host,
+                       "config4" if world > 1 else "config4_shard": c4,
                        "device_ms": {k: round(s0[k], 2) for k in ("ms_total", "ms_sa", "ms_lz", "ms_entropy", "ms_emit")},
                        "cyclic_rounds": s0["cyc_rounds"], "cyclic_rounds_mean_per_block": round(r_avg, 3),
                        "lz77": {"tokens": s0["lz_tokens"], "stitch_fixups": s0["lz_fix"],

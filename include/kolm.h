@@ -186,7 +186,9 @@ int kolm_encode_blocks(const uint8_t* data, const uint64_t* starts, const uint32
  * beside the DMA), every block of block_size bytes is encoded (candidates cand_mask, MDL),
  * and the KOLR container (header + TOC by kolm_toc_write, then the winners' payloads copied
  * straight from device memory) is assembled in a pinned host buffer owned by the context:
- * *out / *out_len describe it until the next call on the default context.  Inputs above
+ * *out / *out_len describe it until the next call on the default context: callers on
+ * several threads must serialise the call AND their read of *out (the Python binding holds
+ * one lock across both), since the next call reuses the buffer.  Inputs above
  * 2^31 bytes run as several device batches.  KOLM_ERANGE when the block count exceeds
  * 65535 or n >= 2^32 (PY's struct.error). */
 int kolm_compress_fixed(const uint8_t* data, uint64_t n, uint32_t block_size, uint32_t cand_mask,

@@ -1136,10 +1136,45 @@ u8* upload(kolm_ctx* c, const uint8_t* in, size_t n) {
     return d;
 }
 
+// a += b for the statistics of consecutive batches of one call: counts and times add up,
+// round counts take the maximum (first: a = b)
+void stats_add(kolm_stats& a, const kolm_stats& b, bool first) {
+    if (first) {
+        a = b;
+        return;
+    }
+    a.lin_rounds = std::max(a.lin_rounds, b.lin_rounds);
+    a.cyc_rounds = std::max(a.cyc_rounds, b.cyc_rounds);
+    a.lin_active += b.lin_active;
+    a.cyc_active += b.cyc_active;
+    a.cyc_rounds_sum += b.cyc_rounds_sum;
+    a.lz_tokens += b.lz_tokens;
+    a.lz_long += b.lz_long;
+    a.lz_fix += b.lz_fix;
+    a.ms_total += b.ms_total;
+    a.ms_sa += b.ms_sa;
+    a.ms_lz += b.ms_lz;
+    a.ms_entropy += b.ms_entropy;
+    a.ms_emit += b.ms_emit;
+    a.ms_repair += b.ms_repair;
+    a.rp_rules += b.rp_rules;
+    a.rp_batches += b.rp_batches;
+    a.rp_final += b.rp_final;
+    for (int k = 0; k < KOLM_NKT; ++k) {
+        a.kt[k].ms += b.kt[k].ms;
+        a.kt[k].launches += b.kt[k].launches;
+        a.kt[k].bytes += b.kt[k].bytes;
+    }
+}
+
 constexpr size_t STAGE_BYTES = 32u << 20;
 
 CopyPool& copy_pool(kolm_ctx* c) {
-    if (!c->pool) c->pool.reset(new CopyPool(std::max(1u, std::min(8u, std::thread::hardware_concurrency()) - 1)));
+    if (!c->pool) {
+        // hardware_concurrency() may be 0 (unknown): at least one worker, at most 7
+        const unsigned hc = std::max(2u, std::thread::hardware_concurrency());
+        c->pool.reset(new CopyPool(std::min(8u, hc) - 1));
+    }
     return *c->pool;
 }
 
@@ -1404,9 +1439,18 @@ int kolm_encode_blocks(const uint8_t* data, const uint64_t* starts, const uint32
 int kolm_compress_fixed(const uint8_t* data, uint64_t n, uint32_t block_size, uint32_t cand_mask,
                         const uint8_t** out, uint64_t* out_len, kolm_stats* stats) {
     kolm_ctx* c = need_default();
-    if (!c) return KOLM_ENOINIT;
-    if ((!data && n) || !out || !out_len || block_size == 0 || block_size > 0x7FFFFFFFu) return KOLM_EARG;
-    if ((cand_mask & KOLM_FULL_MASK) == 0) return KOLM_EARG;
+    if (!c) {
+        set_err("kolm_init has not been called");
+        return KOLM_ENOINIT;
+    }
+    if ((!data && n) || !out || !out_len || block_size == 0 || block_size > 0x7FFFFFFFu) {
+        set_err("kolm_compress_fixed: bad argument (null buffer or block size outside [1, 2^31))");
+        return KOLM_EARG;
+    }
+    if ((cand_mask & KOLM_FULL_MASK) == 0) {
+        set_err("kolm_compress_fixed: the candidate mask selects no candidate of ids 0..10");
+        return KOLM_EARG;
+    }
     const u64 nb = (n + block_size - 1) / block_size;
     if (nb > 0xFFFFu || n > 0xFFFFFFFFull) {  // PY: struct.pack('<H' / '<I') raises
         set_err(nb > 0xFFFFu ? "'H' format requires 0 <= number <= 65535"
@@ -1419,9 +1463,13 @@ int kolm_compress_fixed(const uint8_t* data, uint64_t n, uint32_t block_size, ui
         std::vector<u32> method(nb), lens(nb);
         std::vector<u64> plen(nb), off(nb + 1, 0);
         for (u64 b = 0; b < nb; ++b) lens[b] = (u32)std::min<u64>(block_size, n - b * block_size);
-        // batches of whole blocks below the 2^31-position limit of one encode batch; the
-        // payloads of every batch land in one device arena, back to back
-        const u64 per = std::max<u64>(1, ((1ull << 31) - 1) / block_size);
+        // batches of whole blocks below the 2^31-position limit of one encode batch (512 MiB
+        // with v2_new, whose 8 bit planes per byte share that index space); the payloads of
+        // every batch land in one device arena, back to back.  KOLM_BATCH_BYTES lowers the
+        // limit (tests run the multi-batch path on small inputs with it).
+        u64 lim = (cand_mask >> KOLM_M_V2NEW) & 1u ? (1ull << 29) - 1 : (1ull << 31) - 1;
+        if (const char* e = getenv("KOLM_BATCH_BYTES")) lim = std::min<u64>(lim, std::max<u64>(1, strtoull(e, nullptr, 10)));
+        const u64 per = std::max<u64>(1, lim / block_size);
         const bool has_raw = (cand_mask & 1u) != 0;
         const u64 acap = (has_raw ? n : 9 * n) + 64 * nb + 256;
         u8* arena = c->get<u8>("arena_c", acap);
@@ -1440,7 +1488,7 @@ int kolm_compress_fixed(const uint8_t* data, uint64_t n, uint32_t block_size, ui
             for (u64 i = 0; i < k; ++i) plen[b0 + i] = o[i + 1] - o[i];
             pos += o[k];
             pos = (pos + 3) & ~(u64)3;  // the next batch's arena is 4-byte aligned
-            if (b0 == 0) agg = st;
+            stats_add(agg, st, b0 == 0);
         }
         // the container: header + TOC (kolm_toc.cpp), then the payloads straight from the
         // device arena into the pinned result buffer (batch padding skipped)

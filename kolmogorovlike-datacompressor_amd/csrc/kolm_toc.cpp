@@ -26,6 +26,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/kolm.h"
@@ -364,20 +365,35 @@ int kolm_toc_read(const uint8_t* buf, uint64_t n, uint32_t* fields, uint64_t* pa
             return KOLM_ECAP;
         }
         const u64 n_runs = hd.uleb(), K = hd.uleb();
+        // a prefix code over at most 65535 runs is at most 32 deep (Fibonacci weights), so
+        // longer code lengths are rejected (and canonical() never shifts by 64)
         std::vector<Code> codes;
+        std::unordered_map<u64, size_t> at;
         for (u64 i = 0; i < K; ++i) {
             const u64 sym = hd.uleb(), len = hd.uleb();
-            bool dup = false;
-            for (Code& c : codes)  // a repeated symbol keeps its last length (dict semantics)
-                if (c.sym == sym) c.len = (u32)std::min<u64>(len, 64), dup = true;
-            if (!dup) codes.push_back(Code{sym, (u32)std::min<u64>(len, 64), 0});
+            if (len > 32) throw Fail{"Huffman code length out of range"};
+            const auto it = at.find(sym);
+            if (it != at.end()) {  // a repeated symbol keeps its last length (dict semantics)
+                codes[it->second].len = (u32)len;
+            } else {
+                at.emplace(sym, codes.size());
+                codes.push_back(Code{sym, (u32)len, 0});
+            }
         }
         const u64 k_runs = hd.uleb();
         const u64 tail = hd.uleb();  // FIXED: last block's length; CDC: k of the length deltas
         if (k_runs > 63 || (mode == 1 && tail > 63)) throw Fail{"Rice parameter out of range"};
         canonical(codes);
+        // canonical decode table: the codes of length L are first[L] .. first[L] + cnt[L] - 1,
+        // their symbols codes[idx[L] ..] (sorted by (len, sym))
+        u64 first[33] = {}, cnt[33] = {}, idx[33] = {};
         u32 maxlen = 0;
-        for (const Code& c : codes) maxlen = std::max(maxlen, c.len);
+        for (size_t i = codes.size(); i-- > 0;) {
+            const Code& c = codes[i];
+            if (!c.len) continue;
+            first[c.len] = c.bits, idx[c.len] = i, ++cnt[c.len];
+            maxlen = std::max(maxlen, c.len);
+        }
         BitIn br{buf + bits_at, bit_bytes};
         std::vector<u64> syms;
         for (u64 r = 0; r < n_runs; ++r) {
@@ -385,12 +401,10 @@ int kolm_toc_read(const uint8_t* buf, uint64_t n, uint32_t* fields, uint64_t* pa
             bool hit = false;
             for (u32 L = 1; L <= maxlen && !hit; ++L) {
                 v = (v << 1) | br.bit();
-                for (const Code& c : codes)
-                    if (c.len == L && c.bits == v) {
-                        syms.push_back(c.sym);
-                        hit = true;
-                        break;
-                    }
+                if (cnt[L] && v - first[L] < cnt[L]) {
+                    syms.push_back(codes[idx[L] + (v - first[L])].sym);
+                    hit = true;
+                }
             }
             if (!hit) throw Fail{"Huffman decode failed"};
         }

@@ -80,6 +80,7 @@ class Stats(ctypes.Structure):
 
 _lib = None
 _lock = threading.Lock()
+_result_lock = threading.Lock()  # kolm_compress_fixed's result buffer (see compress_fixed)
 _inited_device = None
 
 # (name, restype, argtypes) of every symbol declared in include/kolm.h
@@ -189,6 +190,44 @@ def ensure_init(device: int = None):
     return device
 
 
+_dev_ctx = {}
+
+
+def device_ctx(device: int):
+    """A context of this process on `device` (kolm_ctx_create, cached) for the
+    device-resident entry points (kolm_encode_blocks_device, ...)."""
+    with _lock:
+        ctx = _dev_ctx.get(device)
+    if ctx is None:
+        ctx = ctypes.c_void_p()
+        check(load().kolm_ctx_create(int(device), ctypes.byref(ctx)))
+        with _lock:
+            _dev_ctx.setdefault(device, ctx)
+            ctx = _dev_ctx[device]
+    return ctx
+
+
+def encode_blocks_device(ctx, d_data: int, n: int, block_size: int, d_arena: int, arena_cap: int,
+                         cand_mask: int = KOLM_DEFAULT_MASK):
+    """Batched MDL encode of fixed blocks of the device buffer d_data[0, n) into the
+    device arena (kolm_encode_blocks_device).  Returns (sizes, method, offsets, stats)."""
+    nb = (n + block_size - 1) // block_size if n else 0
+    sizes = np.zeros((max(nb, 1), KOLM_NCAND), dtype=np.uint32)
+    method = np.zeros(max(nb, 1), dtype=np.uint32)
+    off = np.zeros(nb + 1, dtype=np.uint64)
+    st = Stats()
+    check(load().kolm_encode_blocks_device(ctx, d_data, n, block_size, cand_mask, None, d_arena, arena_cap,
+                                           sizes.ctypes.data, method.ctypes.data, off.ctypes.data,
+                                           ctypes.byref(st)))
+    return sizes[:nb], method[:nb], off, st.as_dict()
+
+
+def arena_capacity(n: int, nb: int, cand_mask: int) -> int:
+    """Device arena bytes that always hold the payloads of n input bytes in nb blocks
+    (raw in the mask bounds every winner by its block; kolm_api.cpp sizes it the same)."""
+    return (n if cand_mask & 1 else 9 * n) + 64 * nb + 256
+
+
 def kernel_times(ctx) -> dict:
     """Per-kernel HIP-event timing accumulated while timing was enabled on ctx."""
     import json
@@ -287,13 +326,17 @@ def compress_fixed(data, block_size: int, cand_mask: int = KOLM_DEFAULT_MASK):
     out = ctypes.c_void_p()
     ln = ctypes.c_uint64(0)
     st = Stats()
-    rc = load().kolm_compress_fixed(src.ctypes.data, n, block_size, cand_mask, ctypes.byref(out), ctypes.byref(ln),
-                                    ctypes.byref(st))
-    if rc == KOLM_ERANGE:
-        import struct
-        raise struct.error(load().kolm_last_error().decode())
-    check(rc)
-    return ctypes.string_at(out.value, ln.value), st.as_dict()
+    # the result lives in the context's pinned buffer until the next call: the call and the
+    # copy out of it run under one lock (ctypes drops the GIL inside the call)
+    with _result_lock:
+        rc = load().kolm_compress_fixed(src.ctypes.data, n, block_size, cand_mask, ctypes.byref(out),
+                                        ctypes.byref(ln), ctypes.byref(st))
+        if rc == KOLM_ERANGE:
+            import struct
+            raise struct.error(load().kolm_last_error().decode())
+        check(rc)
+        blob = ctypes.string_at(out.value, ln.value)
+    return blob, st.as_dict()
 
 
 def encode_blocks_var(data: bytes, bounds, cand_mask: int = KOLM_DEFAULT_MASK, force=None):

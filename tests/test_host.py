@@ -211,3 +211,45 @@ def test_rank_blocks_partitions(nb, world):
         seen = sorted(i for r in range(world) for i in rank_blocks(nb, r, world, part))
         assert seen == list(range(nb))
     assert list(rank_blocks(10, 1, 4, "round_robin")) == [1, 5, 9]
+
+
+def _with_code_len(blob: bytes, new_len: int) -> bytes:
+    """blob (one method id, so one prefix-code entry) with that entry's code length
+    replaced: the TOC header is ULEB(hdr_len) ULEB(toc_bits) ULEB(U) then
+    [n_runs, K, sym, len, ...]; every field here is one byte."""
+    assert blob[14] < 0x80 and blob[15] < 0x80 and blob[16] < 0x80
+    hdr = bytearray(blob[17:17 + blob[14]])
+    assert hdr[1] == 1  # K
+    hdr[3] = new_len
+    return blob[:17] + bytes(hdr) + blob[17 + blob[14]:]
+
+
+def test_toc_reader_hostile_code_lengths():
+    """kolm_toc_read rejects prefix-code lengths above 32 (no 64-bit shift in the canonical
+    code) and still decodes every legal length through its canonical decode table."""
+    blob = container.write_container(container.MODE_FIXED, 8, 24, [7, 7, 7], [8, 8, 8], [b"a", b"b", b"c"])
+    assert container.read_container(_with_code_len(blob, 1))[3] == [7, 7, 7]
+    for bad in (33, 64, 127):
+        with pytest.raises(ValueError, match="code length out of range"):
+            container.read_container(_with_code_len(blob, bad))
+
+
+def test_toc_reader_many_codes_fast():
+    """A header with thousands of prefix-code entries (repeated symbols, as a hostile
+    container could carry) is parsed in linear time: the symbols are deduplicated through
+    a hash map, not pairwise."""
+    import time
+    from kolm.container import uleb128_encode as U
+    body = bytearray()
+    K = 40000
+    body += U(1) + U(K)
+    for i in range(K):
+        body += U(i % 5000) + U(1 + i % 20)
+    body += U(0) + U(8)  # k_runs, tail (last block length)
+    hdr = bytes(body)
+    blob = b"KOLR" + (8).to_bytes(4, "little") + (8).to_bytes(4, "little") + (1).to_bytes(2, "little") \
+        + U(len(hdr)) + U(8) + U(0) + hdr + b"\0"
+    t0 = time.time()
+    with pytest.raises(ValueError):
+        container.read_container(blob)
+    assert time.time() - t0 < 2.0

@@ -4,7 +4,7 @@
 #   (FETCH_SIZE / WRITE_SIZE / TCC hit-miss), each its own rocprofv3 invocation, kernel-trace
 #   domain only.  The bench runs 3 encode batches (warmup, timed step, kernel-timed step).
 OUT=${1:-gpurun_out/prof}
-ARGS=${2:-"--mib 256 --steps 1 --warmup 1 --kt-steps 1 --no-serial-pass --no-cpu-baseline --full-steps 0 --decode-steps 0 --cdc-steps 0 --v2-steps 0 --config-steps 0 --host-steps 0"}
+ARGS=${2:-"--mib 256 --steps 1 --warmup 1 --kt-steps 1 --no-serial-pass --no-cpu-baseline --full-steps 0 --decode-steps 0 --cdc-steps 0 --v2-steps 0 --config-steps 0 --host-steps 0 --c4-steps 0"}
 mkdir -p $OUT
 export TMPDIR=/tmp
 ( for i in $(seq 1 60); do sleep 20; echo "tick $i" >> $OUT/ticks.txt; done ) &
