@@ -410,7 +410,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             const u32 C = std::max<u32>(1, std::min<u32>(std::min<u32>(64, cmax), 64 / w));
             h0 = C;
             R0Bufs r{text, FEd, fac, code, C, w, c->get<u32>("KP", N), a.K2, a.SA, a.K22, a.SA2, a.RK,
-                     c->get<u32>("r0hist", nt * 256), c->get<u32>("r0tmax", nt), c->get<u32>("r0tmin", nt),
+                     c->get<u32>("r0hist", nt * 1024), c->get<u32>("r0tmax", nt), c->get<u32>("r0tmin", nt),
                      c->get<u32>("r0cmax", nt), c->get<u32>("r0cmin", nt), c->get<u32>("r0hf", nt * WG)};
             out.r0_chars = C;
             if (dbg) fprintf(stderr, "[kolm] round 0: %u characters of %u bits\n", C, w);
