@@ -8,7 +8,9 @@ Adds to tests/golden/large.json, without touching the entries make_golden_large.
   * "lz77" for enwik_256k and gradient_1m: PY's encode_lz77 (PY:1711-1763) on 256 KiB of
     enwik-style text and on the gradient BMP's first 1 MiB;
   * case "enwik_128k_repair": PY's repair_compress (PY:1841-1911, the O(n * rules)
-    recount) on 128 KiB of enwik-style text (seed 77), "repair" {len, sha256}.
+    recount) on 128 KiB of enwik-style text (seed 77), "repair" {len, sha256};
+  * case "bench_block0_repair": the same on block 0 of bench.py's stream (1 MiB).
+Arguments (optional): the case names to (re)compute.
 The GPU and the oracle are checked against these in test_gpu_parity.py / test_oracle.py.
 """
 from __future__ import annotations
@@ -35,6 +37,9 @@ def inputs():
         ("enwik_256k", "lz77"): lambda: D.enwik_like(1 << 18),
         ("gradient_1m", "lz77"): lambda: D.gradient_bmp()[: 1 << 20],
         (REPAIR_CASE, "repair"): lambda: D.enwik_like(1 << 17, seed=77),
+        # block 0 of bench.py's rank-0 stream (enwik_like(n)[:1 MiB] does not depend on n):
+        # PY's Re-Pair of a whole 1 MiB bench block (about an hour)
+        ("bench_block0_repair", "repair"): lambda: D.enwik_like(1 << 20),
     }
 
 
@@ -54,7 +59,7 @@ def main():
     path = os.path.join(HERE, "large.json")
     with open(path) as f:
         large = json.load(f)
-    keys = list(inputs())
+    keys = [k for k in inputs() if len(sys.argv) < 2 or k[0] in sys.argv[1:]]
     with ProcessPoolExecutor(max_workers=len(keys)) as ex:
         for (name, kind), res in ex.map(run, keys):
             print(name, kind, res["_seconds"], "s", flush=True)

@@ -470,3 +470,18 @@ def test_round0_alphabet_mixed_batch(kolm_gpu):
         cand = _oracle_all(blk)
         assert list(map(int, sizes[i][:10])) == [len(c) for c in cand], f"block {i}"
         assert payloads[i] == cand[int(method[i])], f"block {i}"
+
+
+REPAIR_SCALE = {"enwik_128k_repair": lambda: D.enwik_like(1 << 17, seed=77),
+                "bench_block0_repair": lambda: D.enwik_like(1 << 20)}
+
+
+@pytest.mark.parametrize("case", sorted(REPAIR_SCALE))
+def test_repair_at_scale_vs_py(kolm_gpu, large_known, case):
+    """Device Re-Pair (candidate 9) against PY's own repair_compress at 128 KiB and on the
+    bench stream's block 0 (1 MiB): sha256 of PY's payload (make_golden_scale.py)."""
+    if case not in large_known:
+        pytest.skip(f"{case} not generated yet")
+    ref = large_known[case]
+    out = kolm_gpu.repair_compress(REPAIR_SCALE[case]())[0]
+    assert (len(out), sha(out)) == (ref["repair"]["len"], ref["repair"]["sha256"])
