@@ -24,6 +24,14 @@ Also reported:
   detail.parity_blocks  every block of the timed output (sizes of ids 0..8, winner, winner
                 sha256) against tests/golden/bench_stream.json (oracle answers).
 
+  detail.config4_shard (N = 1) / detail.config4 (N > 1)  BASELINE config 4: 256 MiB TOTAL of
+                rank 0's stream in 1 MiB blocks round-robin over the GPUs (block i on rank
+                i mod N) with the async RCCL gather (payloads, ids, offsets) to rank 0; at N = 1
+                the shard one GPU of the 8-GPU run encodes (blocks i = 0 mod 8, 32 MiB), timed
+                alone, parity per block against the rank-0 fixture.
+  --strong      makes config 4 the headline (scaling "strong"): every rank encodes its
+                round-robin shard of the one 256 MiB stream; value = 256 MiB / time.
+
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 via
 python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 """

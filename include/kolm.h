@@ -194,6 +194,13 @@ int kolm_encode_blocks(const uint8_t* data, const uint64_t* starts, const uint32
 int kolm_compress_fixed(const uint8_t* data, uint64_t n, uint32_t block_size, uint32_t cand_mask,
                         const uint8_t** out, uint64_t* out_len, kolm_stats* stats);
 
+/* Second phase of kolm_compress_fixed: copy the container it described (*out, *out_len)
+ * into the caller's buffer dst[0, n) (n <= *out_len) with the context's host copy
+ * threads (page faults of a fresh destination and the memcpy itself spread over them).
+ * Same serialisation rule as kolm_compress_fixed's *out.  KOLM_ECAP when n exceeds the
+ * container. */
+int kolm_result_copy(uint8_t* dst, uint64_t n);
+
 /* kolm_encode_blocks over ngpu devices (0..ngpu-1, clamped to the device count and the
  * block count) of this process: fixed blocks of block_size over data[0, total), block i
  * of shard r lives on device r, shards are contiguous block ranges.  Outputs exactly as

@@ -19,12 +19,13 @@ namespace {
 struct ChunkGeom {
     Geom geo;
     u32 cpb;  // chunks per block
+    u32 csz;  // bytes per chunk (mtf_chunk_bytes: MTF_CHUNK, smaller for batches of few blocks)
     __device__ inline bool range(u32 c, u32& lo, u32& hi) const {
         const u32 b = c / cpb;
         const u32 k = c - b * cpb;
-        lo = geo.base(b) + k * MTF_CHUNK;
+        lo = geo.base(b) + k * csz;
         const u32 e = geo.end(b);
-        hi = min(lo + (u32)MTF_CHUNK, e);
+        hi = min(lo + csz, e);
         return lo < e;
     }
 };
@@ -43,12 +44,12 @@ __global__ __launch_bounds__(256) void k_mtf_summary(ChunkGeom cg, const u8* in,
     // whole-workgroup path (every chunk a full aligned 1 KiB): the chunks are read backwards
     // 64 bytes at a time through LDS slabs that the workgroup loads as whole 64-byte lines
     // (per-thread 16-byte loads 1 KiB apart over-fetched ~4x, PMC)
-    if (__syncthreads_and(valid && hi - lo == MTF_CHUNK && (lo & 15) == 0)) {
+    if (__syncthreads_and(valid && hi - lo == cg.csz && (lo & 15) == 0)) {
         u32 seen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         u8* out = summary + (u64)c * 256;
         slo[t] = lo;
         __syncthreads();
-        for (u32 r = MTF_CHUNK; r > 0; r -= MTF_SLAB) {
+        for (u32 r = cg.csz; r > 0; r -= MTF_SLAB) {
 #pragma unroll
             for (u32 q = 0; q < MTF_SLAB / 16; ++q) {
                 const u32 m = q * 256 + t, owner = m >> 2, part = m & 3;
@@ -176,7 +177,7 @@ __global__ __launch_bounds__(64 * CW) void k_mtf_compose(ChunkGeom cg, const u8*
     u32 nch = 0;
     {
         const u32 lo0 = cg.geo.base(b), e = cg.geo.end(b);
-        nch = (e - lo0 + MTF_CHUNK - 1) / MTF_CHUNK;
+        nch = (e - lo0 + cg.csz - 1) / cg.csz;
     }
     const u32 per = (nch + CW - 1) / CW;
     const u32 k0 = min(w * per, nch), k1 = min(k0 + per, nch);
@@ -405,10 +406,23 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
 
 }  // namespace
 
+// Bytes per MTF chunk: MTF_CHUNK when the batch has chunks enough to fill the GPU; for
+// batches of few blocks (BASELINE configs 2 and 5: 1 and 3 blocks) smaller chunks, down to
+// 128 bytes, so the replay — one thread per chunk, a sequential walk — runs on 8x more
+// threads (the compose then folds 8x more summaries per block, in 8 waves).
+u32 mtf_chunk_bytes(const Geom& geo) {
+    static const u32 force = getenv("KOLM_MTF_CHUNK") ? (u32)atoi(getenv("KOLM_MTF_CHUNK")) : 0u;
+    if (force >= 64 && force <= MTF_CHUNK && (force & (force - 1)) == 0) return force;
+    u32 csz = MTF_CHUNK;
+    while (csz > 128 && (u64)((geo.bs + csz - 1) / csz) * geo.nb < 65536) csz >>= 1;
+    return csz;
+}
+
 void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summary_cnt, u8* states,
                 hipStream_t s, KTimer* kt, u64* bits, int rice_k) {
     if (!geo.N) return;
-    ChunkGeom cg{geo, (geo.bs + MTF_CHUNK - 1) / MTF_CHUNK};
+    const u32 csz = mtf_chunk_bytes(geo);
+    ChunkGeom cg{geo, (geo.bs + csz - 1) / csz, csz};
     const u32 nchunks = cg.cpb * geo.nb;
     const u64 N = geo.N;
     {

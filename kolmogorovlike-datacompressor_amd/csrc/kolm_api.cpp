@@ -154,7 +154,7 @@ struct kolm_ctx {
     u8* stage[NSTAGE] = {};
     hipEvent_t stage_ev[NSTAGE] = {};
     u8* h_res = nullptr;
-    size_t h_res_cap = 0;
+    size_t h_res_cap = 0, h_res_len = 0;
     std::unique_ptr<CopyPool> pool;
     hipEvent_t evj[4] = {};        // join events
     hipEvent_t evr[2] = {};        // Re-Pair start / done
@@ -599,7 +599,8 @@ struct Pipeline {
 
     u8* mtf(const u8* in, u64* bits = nullptr) {
         const u64 N = geo.N;
-        const u64 nch = (u64)((geo.bs + MTF_CHUNK - 1) / MTF_CHUNK) * geo.nb + 1;
+        const u32 csz = mtf_chunk_bytes(geo);
+        const u64 nch = (u64)((geo.bs + csz - 1) / csz) * geo.nb + 1;
         u8* out = c->get<u8>("mtf", N);
         launch_mtf(geo, in, out, c->get<u8>("mtf_sum", nch * 256), c->get<u16>("mtf_cnt", nch),
                    c->get<u8>("mtf_states", nch * 256), c->active, c->kt(), bits, 2);
@@ -1523,7 +1524,29 @@ int kolm_compress_fixed(const uint8_t* data, uint64_t n, uint32_t block_size, ui
         KOLM_HIP_CHECK(hipStreamSynchronize(c->stream));
         *out = c->h_res;
         *out_len = need;
+        c->h_res_len = need;
         if (stats) *stats = agg;
+        return KOLM_OK;
+    });
+}
+
+int kolm_result_copy(uint8_t* dst, uint64_t n) {
+    kolm_ctx* c = need_default();
+    if (!c) {
+        set_err("kolm_init has not been called");
+        return KOLM_ENOINIT;
+    }
+    if (!dst && n) {
+        set_err("kolm_result_copy: null destination");
+        return KOLM_EARG;
+    }
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(c->mu);
+        if (n > c->h_res_len) {
+            set_err("kolm_result_copy: more bytes than the last container");
+            return KOLM_ECAP;
+        }
+        if (n) copy_pool(c).copy(dst, c->h_res, n);
         return KOLM_OK;
     });
 }

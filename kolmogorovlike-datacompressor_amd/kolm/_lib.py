@@ -120,6 +120,7 @@ SIGNATURES = [
     ("kolm_decode_blocks", I32, [P, P, P, P, U32, P, U64]),
     ("kolm_decode_blocks_device", I32, [P, P, P, P, P, U32, P, U64, ctypes.POINTER(ctypes.c_double)]),
     ("kolm_compress_fixed", I32, [P, U64, U32, U32, ctypes.POINTER(P), ctypes.POINTER(U64), P]),
+    ("kolm_result_copy", I32, [P, U64]),
     ("kolm_toc_write", I32, [I32, U32, U64, U32, P, P, P, P, U64, ctypes.POINTER(U64)]),
     ("kolm_toc_read", I32, [U8P, U64, P, ctypes.POINTER(U64), P, P, P, U32]),
 ]
@@ -335,8 +336,23 @@ def compress_fixed(data, block_size: int, cand_mask: int = KOLM_DEFAULT_MASK):
             import struct
             raise struct.error(load().kolm_last_error().decode())
         check(rc)
-        blob = ctypes.string_at(out.value, ln.value)
+        # the result bytes object is allocated uninitialised and filled by the library's
+        # copy threads (kolm_result_copy) instead of one single-threaded string_at copy
+        blob = _new_bytes(ln.value)
+        if ln.value:
+            check(load().kolm_result_copy(ctypes.cast(ctypes.c_char_p(blob), ctypes.c_void_p), ln.value))
     return blob, st.as_dict()
+
+
+_PyBytes_New = ctypes.pythonapi.PyBytes_FromStringAndSize
+_PyBytes_New.restype = ctypes.py_object
+_PyBytes_New.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
+
+
+def _new_bytes(n: int) -> bytes:
+    """A fresh bytes object of n bytes, contents undefined until written (the C API's
+    PyBytes_FromStringAndSize(NULL, n) idiom); it is filled before anyone else sees it."""
+    return _PyBytes_New(None, n) if n else b""
 
 
 def encode_blocks_var(data: bytes, bounds, cand_mask: int = KOLM_DEFAULT_MASK, force=None):

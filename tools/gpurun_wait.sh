@@ -8,7 +8,7 @@ for i in $(seq 1 12); do
   rc=$?
   st=$(python3 -c "import json;d=json.load(open('gpurun_out/.last_call.json'));print(d.get('status'), d.get('run_s') or 0)" 2>/dev/null)
   case "$st" in
-    "transient 0"*|"transient None"*) echo "[wait] no box (try $i), sleeping 150 s"; sleep 150 ;;
+    "transient 0"*|"transient None"*) echo "[wait] no box (try $i), sleeping 240 s"; sleep 240 ;;
     *) exit $rc ;;
   esac
 done
