@@ -154,7 +154,9 @@ struct kolm_ctx {
     u8* stage[NSTAGE] = {};
     hipEvent_t stage_ev[NSTAGE] = {};
     u8* h_res = nullptr;
-    size_t h_res_cap = 0, h_res_len = 0;
+    size_t h_res_cap = 0, h_res_len = 0, h_res_off = 0;  // the container is h_res[off, off + len)
+    hipStream_t up = nullptr, dl = nullptr;  // kolm_compress_fixed: upload / download streams
+    hipEvent_t up_ev = nullptr;
     std::unique_ptr<CopyPool> pool;
     hipEvent_t evj[4] = {};        // join events
     hipEvent_t evr[2] = {};        // Re-Pair start / done
@@ -1182,8 +1184,9 @@ CopyPool& copy_pool(kolm_ctx* c) {
 // The same upload from pageable memory through a ring of pinned chunks: the copy workers
 // fill chunk k + 1 while the DMA engine moves chunk k (hipMemcpy from pageable memory
 // stages through the runtime's own buffers at about half the PCIe rate).
-u8* upload_staged(kolm_ctx* c, const uint8_t* in, size_t n) {
-    u8* d = c->get<u8>("text", n + 64);
+u8* upload_staged(kolm_ctx* c, const uint8_t* in, size_t n, u8* d = nullptr, hipStream_t st = nullptr) {
+    if (!d) d = c->get<u8>("text", n + 64);
+    if (!st) st = c->stream;
     CopyPool& pool = copy_pool(c);
     for (size_t o = 0, k = 0; o < n; o += STAGE_BYTES, ++k) {
         const int j = (int)(k % kolm_ctx::NSTAGE);
@@ -1195,10 +1198,10 @@ u8* upload_staged(kolm_ctx* c, const uint8_t* in, size_t n) {
         }
         const size_t len = std::min(STAGE_BYTES, n - o);
         pool.copy(c->stage[j], in + o, len);
-        KOLM_HIP_CHECK(hipMemcpyAsync(d + o, c->stage[j], len, hipMemcpyHostToDevice, c->stream));
-        KOLM_HIP_CHECK(hipEventRecord(c->stage_ev[j], c->stream));
+        KOLM_HIP_CHECK(hipMemcpyAsync(d + o, c->stage[j], len, hipMemcpyHostToDevice, st));
+        KOLM_HIP_CHECK(hipEventRecord(c->stage_ev[j], st));
     }
-    KOLM_HIP_CHECK(hipMemsetAsync(d + n, 0, 64, c->stream));
+    KOLM_HIP_CHECK(hipMemsetAsync(d + n, 0, 64, st));
     return d;
 }
 
@@ -1240,6 +1243,9 @@ int kolm_ctx_destroy(kolm_ctx* c) {
             if (c->stage_ev[i]) KOLM_HIP_CHECK(hipEventDestroy(c->stage_ev[i]));
         }
         if (c->h_res) KOLM_HIP_CHECK(hipHostFree(c->h_res));
+        if (c->up) KOLM_HIP_CHECK(hipStreamDestroy(c->up));
+        if (c->dl) KOLM_HIP_CHECK(hipStreamDestroy(c->dl));
+        if (c->up_ev) KOLM_HIP_CHECK(hipEventDestroy(c->up_ev));
         KOLM_HIP_CHECK(hipStreamDestroy(c->stream));
         KOLM_HIP_CHECK(hipStreamDestroy(c->aux));
         KOLM_HIP_CHECK(hipStreamDestroy(c->rp));
@@ -1462,37 +1468,136 @@ int kolm_compress_fixed(const uint8_t* data, uint64_t n, uint32_t block_size, ui
         std::lock_guard<std::mutex> g(c->mu);
         KOLM_HIP_CHECK(hipSetDevice(c->device));
         std::vector<u32> method(nb), lens(nb);
-        std::vector<u64> plen(nb), off(nb + 1, 0);
+        std::vector<u64> plen(nb);
         for (u64 b = 0; b < nb; ++b) lens[b] = (u32)std::min<u64>(block_size, n - b * block_size);
-        // batches of whole blocks below the 2^31-position limit of one encode batch (512 MiB
-        // with v2_new, whose 8 bit planes per byte share that index space); the payloads of
-        // every batch land in one device arena, back to back.  KOLM_BATCH_BYTES lowers the
-        // limit (tests run the multi-batch path on small inputs with it).
+        // Pieces of whole blocks, each one device batch: below the 2^31-position limit of a
+        // batch (512 MiB with v2_new, whose 8 bit planes per byte share that index space;
+        // KOLM_BATCH_BYTES lowers it — the tests run the multi-batch path that way), and
+        // inputs of 128 MiB or more in two pieces so that the upload of piece k + 1 (a host
+        // thread: pageable -> pinned staging -> DMA on the upload stream) and the download of
+        // piece k - 1's payloads (download stream) run while piece k encodes.
         u64 lim = (cand_mask >> KOLM_M_V2NEW) & 1u ? (1ull << 29) - 1 : (1ull << 31) - 1;
         if (const char* e = getenv("KOLM_BATCH_BYTES")) lim = std::min<u64>(lim, std::max<u64>(1, strtoull(e, nullptr, 10)));
-        const u64 per = std::max<u64>(1, lim / block_size);
+        static const u64 pipe_min = getenv("KOLM_PIPE_MIN") ? strtoull(getenv("KOLM_PIPE_MIN"), nullptr, 10) : (128ull << 20);
         const bool has_raw = (cand_mask & 1u) != 0;
-        const u64 acap = (has_raw ? n : 9 * n) + 64 * nb + 256;
+        std::vector<std::pair<u64, u64>> pieces;  // (first block, blocks)
+        {
+            const u64 per = std::max<u64>(1, lim / block_size);
+            for (u64 b0 = 0; b0 < nb; b0 += per) {
+                const u64 k = std::min(per, nb - b0);
+                const u64 len = std::min<u64>(n, (b0 + k) * block_size) - b0 * block_size;
+                if (has_raw && len >= pipe_min && k >= 2) {
+                    pieces.push_back({b0, k / 2});
+                    pieces.push_back({b0 + k / 2, k - k / 2});
+                } else {
+                    pieces.push_back({b0, k});
+                }
+            }
+        }
+        const u64 np = pieces.size();
+        auto piece_bytes = [&](u64 i, u64& lo) {
+            lo = pieces[i].first * block_size;
+            return std::min<u64>(n, (pieces[i].first + pieces[i].second) * block_size) - lo;
+        };
+        for (u64 i = 0; i < np; ++i) {
+            u64 lo;
+            if (int e = check_geom(piece_bytes(i, lo), block_size)) return e;
+        }
+        const u64 acap = (has_raw ? n : 9 * n) + 64 * nb + 256 * np;
         u8* arena = c->get<u8>("arena_c", acap);
-        u64 pos = 0;
+        // the pinned result: the TOC goes in front of the payloads once every method is
+        // known, so the payloads are downloaded behind room for the largest TOC (header and
+        // code table, 4 bits per block of run symbol / run length in the worst case, the
+        // Elias-Fano ends <= 2 + 33 bits per block).  Without raw among the candidates the
+        // payload bound is 9n: then everything is downloaded after the last piece.
+        const u64 head = 4096 + 16 * nb;
+        const u64 need_max = head + (has_raw ? n + 64 * nb : 0) + 4096;
+        if (has_raw && c->h_res_cap < need_max) {
+            if (c->h_res) KOLM_HIP_CHECK(hipHostFree(c->h_res));
+            c->h_res = nullptr;
+            c->h_res_cap = 0;
+            KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_res, need_max, hipHostMallocDefault));
+            c->h_res_cap = need_max;
+        }
+        if (!c->up) {
+            KOLM_HIP_CHECK(hipStreamCreateWithFlags(&c->up, hipStreamNonBlocking));
+            KOLM_HIP_CHECK(hipStreamCreateWithFlags(&c->dl, hipStreamNonBlocking));
+            KOLM_HIP_CHECK(hipEventCreateWithFlags(&c->up_ev, hipEventDisableTiming));
+        }
+        u8* dtext[2] = {nullptr, nullptr};
+        {
+            u64 mx = 0, lo;
+            for (u64 i = 0; i < np; ++i) mx = std::max(mx, piece_bytes(i, lo));
+            dtext[0] = c->get<u8>("text", mx + 64);
+            if (np > 1) dtext[1] = c->get<u8>("text_b", mx + 64);
+        }
+        // piece i's upload (on the calling thread for piece 0, a helper thread otherwise)
+        auto upload = [&](u64 i) {
+            u64 lo;
+            const u64 len = piece_bytes(i, lo);
+            KOLM_HIP_CHECK(hipSetDevice(c->device));
+            upload_staged(c, data + lo, len, dtext[i & 1], c->up);
+            KOLM_HIP_CHECK(hipEventRecord(c->up_ev, c->up));
+        };
+        struct Up {
+            std::thread t;
+            int rc = KOLM_OK;
+            std::string err;
+        } next;
+        auto start_upload = [&](u64 i) {
+            next.rc = KOLM_OK;
+            next.t = std::thread([&, i] {
+                next.rc = guarded([&] {
+                    upload(i);
+                    return KOLM_OK;
+                });
+                if (next.rc) next.err = g_err;
+            });
+        };
+        auto join_upload = [&]() -> int {
+            if (next.t.joinable()) next.t.join();
+            if (next.rc) set_err(next.err);
+            return next.rc;
+        };
+        struct JoinGuard {  // an early error return never leaves the helper running
+            Up& u;
+            ~JoinGuard() {
+                if (u.t.joinable()) u.t.join();
+            }
+        } jg{next};
+        upload(0);
+        u64 pos = 0, dpos = head;
+        std::vector<u64> apos(np), abytes(np);
         kolm_stats agg{};
-        for (u64 b0 = 0; b0 < nb; b0 += per) {
-            const u64 k = std::min(per, nb - b0);
-            const u64 lo = b0 * block_size, len = std::min<u64>(n, (b0 + k) * block_size) - lo;
-            if (int e = check_geom(len, block_size)) return e;
-            u8* d = upload_staged(c, data + lo, len);
+        for (u64 i = 0; i < np; ++i) {
+            u64 lo;
+            const u64 len = piece_bytes(i, lo), b0 = pieces[i].first, k = pieces[i].second;
+            if (i) {
+                if (int e = join_upload()) return e;
+            }
+            // the encode (c->stream first) waits for this piece's upload
+            KOLM_HIP_CHECK(hipStreamWaitEvent(c->stream, c->up_ev, 0));
+            if (i + 1 < np) {
+                // piece i + 1 goes up while piece i encodes; its buffer's previous user (piece
+                // i - 1) is complete: encode_batch returns synchronised
+                start_upload(i + 1);
+            }
             std::vector<u64> o(k + 1);
             kolm_stats st{};
-            int r = encode_batch(c, d, len, block_size, nullptr, 0, cand_mask & KOLM_FULL_MASK, nullptr, arena + pos,
-                                 acap - pos, nullptr, method.data() + b0, o.data(), &st);
+            int r = encode_batch(c, dtext[i & 1], len, block_size, nullptr, 0, cand_mask & KOLM_FULL_MASK, nullptr,
+                                 arena + pos, acap - pos, nullptr, method.data() + b0, o.data(), &st);
             if (r) return r;
-            for (u64 i = 0; i < k; ++i) plen[b0 + i] = o[i + 1] - o[i];
+            for (u64 j = 0; j < k; ++j) plen[b0 + j] = o[j + 1] - o[j];
+            apos[i] = pos;
+            abytes[i] = o[k];
+            if (has_raw && o[k])  // this piece's payloads go down while the next one encodes
+                KOLM_HIP_CHECK(hipMemcpyAsync(c->h_res + dpos, arena + pos, o[k], hipMemcpyDeviceToHost, c->dl));
+            dpos += o[k];
             pos += o[k];
-            pos = (pos + 3) & ~(u64)3;  // the next batch's arena is 4-byte aligned
-            stats_add(agg, st, b0 == 0);
+            pos = (pos + 3) & ~(u64)3;  // the next piece's arena is 4-byte aligned
+            stats_add(agg, st, i == 0);
         }
-        // the container: header + TOC (kolm_toc.cpp), then the payloads straight from the
-        // device arena into the pinned result buffer (batch padding skipped)
+        // the container: header + TOC (kolm_toc.cpp) right in front of the payloads
         u64 toc_len = 0;
         if (int e = kolm_toc_write(0, block_size, n, (u32)nb, method.data(), lens.data(), plen.data(), nullptr, 0,
                                    &toc_len))
@@ -1500,30 +1605,33 @@ int kolm_compress_fixed(const uint8_t* data, uint64_t n, uint32_t block_size, ui
         u64 total_pay = 0;
         for (u64 b = 0; b < nb; ++b) total_pay += plen[b];
         const size_t need = toc_len + total_pay;
-        if (c->h_res_cap < need) {
-            if (c->h_res) KOLM_HIP_CHECK(hipHostFree(c->h_res));
-            c->h_res = nullptr;
-            c->h_res_cap = 0;
-            KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_res, need + (need >> 3) + 4096, hipHostMallocDefault));
-            c->h_res_cap = need + (need >> 3) + 4096;
+        u64 at = head - toc_len;
+        if (!has_raw) {  // payload size known only now: allocate and download everything
+            if (c->h_res_cap < need) {
+                if (c->h_res) KOLM_HIP_CHECK(hipHostFree(c->h_res));
+                c->h_res = nullptr;
+                c->h_res_cap = 0;
+                KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_res, need + (need >> 3) + 4096, hipHostMallocDefault));
+                c->h_res_cap = need + (need >> 3) + 4096;
+            }
+            at = 0;
+            u64 d = toc_len;
+            for (u64 i = 0; i < np; ++i) {
+                if (abytes[i])
+                    KOLM_HIP_CHECK(hipMemcpyAsync(c->h_res + d, arena + apos[i], abytes[i], hipMemcpyDeviceToHost, c->dl));
+                d += abytes[i];
+            }
+        } else if (toc_len > head) {
+            set_err("kolm_compress_fixed: TOC larger than its reserved room");
+            return KOLM_EHIP;
         }
-        if (int e = kolm_toc_write(0, block_size, n, (u32)nb, method.data(), lens.data(), plen.data(), c->h_res,
-                                   c->h_res_cap, &toc_len))
+        if (int e = kolm_toc_write(0, block_size, n, (u32)nb, method.data(), lens.data(), plen.data(), c->h_res + at,
+                                   toc_len, &toc_len))
             return e;
-        // one copy per batch (its payloads are contiguous in the arena)
-        u64 src = 0, dst = toc_len;
-        for (u64 b0 = 0; b0 < nb; b0 += per) {
-            const u64 k = std::min(per, nb - b0);
-            u64 bytes = 0;
-            for (u64 i = 0; i < k; ++i) bytes += plen[b0 + i];
-            if (bytes)
-                KOLM_HIP_CHECK(hipMemcpyAsync(c->h_res + dst, arena + src, bytes, hipMemcpyDeviceToHost, c->stream));
-            dst += bytes;
-            src = (src + bytes + 3) & ~(u64)3;
-        }
-        KOLM_HIP_CHECK(hipStreamSynchronize(c->stream));
-        *out = c->h_res;
+        KOLM_HIP_CHECK(hipStreamSynchronize(c->dl));
+        *out = c->h_res + at;
         *out_len = need;
+        c->h_res_off = at;
         c->h_res_len = need;
         if (stats) *stats = agg;
         return KOLM_OK;
@@ -1546,7 +1654,7 @@ int kolm_result_copy(uint8_t* dst, uint64_t n) {
             set_err("kolm_result_copy: more bytes than the last container");
             return KOLM_ECAP;
         }
-        if (n) copy_pool(c).copy(dst, c->h_res, n);
+        if (n) copy_pool(c).copy(dst, c->h_res + c->h_res_off, n);
         return KOLM_OK;
     });
 }
