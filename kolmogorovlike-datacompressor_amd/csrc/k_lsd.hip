@@ -778,7 +778,7 @@ struct SweepArgs {
     u32 first;
 };
 
-template <int HASB, int SW_NW, int SW_SPW>
+template <int HASB, int SW_NW, int SW_SPW, int PF = 1>  // PF: chunks of loads in flight ahead (1 or 2)
 __global__ __launch_bounds__(SW_NW * 64) void k_r0_sweep(SweepArgs a) {
     constexpr u32 SW_NT = SW_NW * 64, SW_CH = SW_NT * SW_SPW;
     __shared__ u32 run[2][SW_R];      // per chunk parity: running destination of every digit
@@ -835,11 +835,17 @@ __global__ __launch_bounds__(SW_NW * 64) void k_r0_sweep(SweepArgs a) {
                 xq[j] = v ? (sq ? sq[i] : i) : 0u;
             }
         };
+        u32 fa[SW_SPW], fb[SW_SPW], fq[SW_SPW];  // PF = 2: chunk c + 1, loaded one chunk earlier
         load(0, ka, kb, kq);
+        if (PF == 2 && 1 < nch) load(1, fa, fb, fq);
         for (u32 c = 0; c < nch; ++c) {
             const u32 par = c & 1;
             u32 na[SW_SPW], nbv[SW_SPW], nq[SW_SPW];
-            if (c + 1 < nch) load(c + 1, na, nbv, nq);
+            if (PF == 2) {
+                if (c + 2 < nch) load(c + 2, na, nbv, nq);
+            } else if (c + 1 < nch) {
+                load(c + 1, na, nbv, nq);
+            }
             const u32 q0 = base + c * SW_CH + w * (SW_CH / SW_NW);
             u32 dr[SW_SPW];  // digit | rank among the wave's equal digits << 16
 #pragma unroll
@@ -884,7 +890,13 @@ __global__ __launch_bounds__(SW_NW * 64) void k_r0_sweep(SweepArgs a) {
             }
             // this wave's counters back to zero for the next chunk (only this wave reads its row)
             for (u32 i = lane; i < SW_R / 2; i += 64) reinterpret_cast<u32*>(&wc[w][0])[i] = 0;
-            if (c + 1 < nch) {
+            if (PF == 2) {
+#pragma unroll
+                for (u32 j = 0; j < SW_SPW; ++j) {
+                    ka[j] = fa[j], kb[j] = fb[j], kq[j] = fq[j];
+                    fa[j] = na[j], fb[j] = nbv[j], fq[j] = nq[j];
+                }
+            } else if (c + 1 < nch) {
 #pragma unroll
                 for (u32 j = 0; j < SW_SPW; ++j) ka[j] = na[j], kb[j] = nbv[j], kq[j] = nq[j];
             }
@@ -1014,9 +1026,12 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
             const u64 rec = pb ? 12 : 8;
             KScope k(kt, KT_LSD, "k_r0_sweep",
                      N * (2 * rec * P - 4) + (u64)nt * SW_R * 4);
-            // KOLM_R0_SWEEP_CFG: waves x steps per wave of a chunk (0: 4 x 8, 1: 8 x 8, 2: 4 x 16)
+            // KOLM_R0_SWEEP_CFG: waves x steps per wave of a chunk (0: 4 x 8, 1: 8 x 8, 2: 4 x 16,
+            // 3: 4 x 8 with two chunks of loads in flight)
             static const int cfg = getenv("KOLM_R0_SWEEP_CFG") ? atoi(getenv("KOLM_R0_SWEEP_CFG")) : 0;
-            if (cfg == 1)
+            if (cfg == 3)
+                pb ? k_r0_sweep<1, 4, 8, 2><<<geo.nb, 256, 0, s>>>(sa) : k_r0_sweep<0, 4, 8, 2><<<geo.nb, 256, 0, s>>>(sa);
+            else if (cfg == 1)
                 pb ? k_r0_sweep<1, 8, 8><<<geo.nb, 512, 0, s>>>(sa) : k_r0_sweep<0, 8, 8><<<geo.nb, 512, 0, s>>>(sa);
             else if (cfg == 2)
                 pb ? k_r0_sweep<1, 4, 16><<<geo.nb, 256, 0, s>>>(sa) : k_r0_sweep<0, 4, 16><<<geo.nb, 256, 0, s>>>(sa);
