@@ -624,10 +624,10 @@ __global__ __launch_bounds__(WG) void k_alpha_codes(const u32* pres, u8* code, u
     for (u32 k = 0; k < (c >> 5); ++k) r += __popc(pw[k]);
     r += __popc(pw[c >> 5] & ((1u << (c & 31)) - 1u));
     code[(u64)b * 256 + c] = (u8)r;
-    if (c == 255) {
+    if (c == 255) {  // (sigma << 8 | w): the batch's largest alphabet and its code width
         const u32 sigma = r + ((pw[7] >> 31) & 1u);
         const u32 w = sigma > 1 ? 32 - __clz(sigma - 1) : 1u;
-        atomicMax(wmax, w);
+        atomicMax(wmax, sigma << 8 | w);
     }
 }
 
@@ -642,9 +642,12 @@ __global__ __launch_bounds__(WG) void k_alpha_codes(const u32* pres, u8* code, u
 // HB = 8: hist0 = digit 0 (bits 0..7 of KA, padding included) in per-wave LDS copies, 256
 // bins per tile (the tile LSD).  HB = 10: the block sweep's digit 0 (bits sh .. sh + 9 of
 // the key), 1024 bins per tile in one LDS array.
+// R > 0: mixed-radix packing, key = sum of code_k * R^(C-1-k) (order-preserving as codes < R;
+// top = R^(C-1)), so C = floor(64 / log2 R) characters fit (enwik-style text, R = 50: 11
+// instead of 10 six-bit codes); R = 0: w-bit codes side by side.
 template <int HB>
 __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32 C, u32 w, u32 sh, u32* KA, u32* KB,
-                                                  u32* hist0) {
+                                                  u32* hist0, u32 R, u64 top) {
     constexpr u32 HR = 1u << HB, HC = HB == 8 ? WG / 64 : 1;
     __shared__ __align__(16) u8 tx[LSD_T + 64];
     __shared__ u8 cd[256];
@@ -688,14 +691,25 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
     }
     const u64 mask = C * w >= 64 ? ~0ull : ((1ull << (C * w)) - 1);
     u64 key = 0;
-    for (u32 k = 0; k < C; ++k) key = (key << w) | (i0 + k < n ? cd[tx[i0 + k]] : 0u);
     u32 ka[LSD_PT], kb[LSD_PT];
+    if (R) {
+        for (u32 k = 0; k < C; ++k) key = key * R + (i0 + k < n ? cd[tx[i0 + k]] : 0u);
 #pragma unroll
-    for (u32 e = 0; e < LSD_PT; ++e) {
-        ka[e] = (u32)(key << sh);
-        kb[e] = (u32)((key << sh) >> 32);
-        const u32 x = i0 + e + C;
-        key = ((key << w) | (x < n ? cd[tx[x]] : 0u)) & mask;
+        for (u32 e = 0; e < LSD_PT; ++e) {
+            ka[e] = (u32)(key << sh);
+            kb[e] = (u32)((key << sh) >> 32);
+            const u32 x = i0 + e + C;
+            key = (key - top * cd[tx[i0 + e]]) * R + (x < n ? cd[tx[x]] : 0u);
+        }
+    } else {
+        for (u32 k = 0; k < C; ++k) key = (key << w) | (i0 + k < n ? cd[tx[i0 + k]] : 0u);
+#pragma unroll
+        for (u32 e = 0; e < LSD_PT; ++e) {
+            ka[e] = (u32)(key << sh);
+            kb[e] = (u32)((key << sh) >> 32);
+            const u32 x = i0 + e + C;
+            key = ((key << w) | (x < n ? cd[tx[x]] : 0u)) & mask;
+        }
     }
 #pragma unroll
     for (u32 e = 0; e < LSD_PT; ++e) {
@@ -706,7 +720,7 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
             u32 t = p - fs;
             u64 k2 = 0;
             for (u32 k = 0; k < C; ++k) {
-                k2 = (k2 << w) | cd[g.text[fs + t]];
+                k2 = R ? k2 * R + cd[g.text[fs + t]] : (k2 << w) | cd[g.text[fs + t]];
                 if (++t == m) t = 0;
             }
             ka[e] = (u32)(k2 << sh);
@@ -964,7 +978,8 @@ u32 lsd_tiles(const Geom& geo) { return (geo.bs + LSD_T - 1) / LSD_T * geo.nb; }
 // Per-block code tables (alphabet compaction); returns the max code width w of the batch
 // (one host round trip).  compact = false: identity codes, w = 8.
 u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w, u32* h_w, bool compact,
-                 hipStream_t s, KTimer* kt) {
+                 hipStream_t s, KTimer* kt, u32* sigma) {
+    if (sigma) *sigma = 256;
     if (!geo.N) return 8;
     if (!compact) {
         std::vector<u8> id(256 * (size_t)geo.nb);
@@ -983,7 +998,8 @@ u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w,
     }
     KOLM_HIP_CHECK(hipMemcpyAsync(h_w, d_w, sizeof(u32), hipMemcpyDeviceToHost, s));
     KOLM_HIP_CHECK(hipStreamSynchronize(s));
-    return std::max<u32>(1, std::min<u32>(8, *h_w));
+    if (sigma) *sigma = std::max<u32>(1, std::min<u32>(256, *h_w >> 8));
+    return std::max<u32>(1, std::min<u32>(8, *h_w & 255u));
 }
 
 // Round 0 of the cyclic sort: a stable sort of every block's positions by the packed codes
@@ -1001,7 +1017,7 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
     const u64 N = geo.N;
     // D byte digits; the packed codes are left-aligned in them, so the 8 D - C w padding bits
     // fall into the first pass's digit (its few distinct values keep that scatter's runs long)
-    const u32 bits = t.chars * t.w, D = (bits + 7) / 8, sh = 8 * D - bits;
+    const u32 bits = t.bits, D = (bits + 7) / 8, sh = 8 * D - bits;
     const u32 pa = std::min<u32>(4, D), pb = D - pa;
     // The block sweep (k_r0_sweep) when the batch has enough blocks to give every CU one
     // (KOLM_R0_SWEEP_MIN, default 192; 0 = always, a large value = never) and the block fits
@@ -1017,7 +1033,7 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
         u32* KB0 = pb ? (odd ? t.K22 : t.KP) : nullptr;
         {
             KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6) + (u64)nt * SW_R * 4);
-            k_keypos_r0<SW_DB><<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, KA0, KB0, t.hist);
+            k_keypos_r0<SW_DB><<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, KA0, KB0, t.hist, t.radix, t.top);
         }
         SweepArgs sa{geo, g.tpb, sh, P, t.hist, KA0, KB0, {t.RK, t.K2}, {t.KP, t.K22}, {t.SA, t.SA2}, odd ? 0u : 1u};
         {
@@ -1042,7 +1058,8 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
         {
             // text + FEd 2 (+ factor starts near factor ends), KA 4 (+ KB 4)
             KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6));
-            k_keypos_r0<8><<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist);
+            k_keypos_r0<8><<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist, t.radix,
+                                             t.top);
         }
         u32* K[2] = {t.K2, t.K22};
         u32* S[2] = {t.SA, t.SA2};

@@ -42,6 +42,13 @@ for step in "$@"; do
     quick)
       timeout -k 10 300 python bench.py $QUICK > "$OUT/quick.json" 2> "$OUT/quick.err" || { tail -30 "$OUT/quick.err"; exit 1; }
       summ "$OUT/quick.json" ;;
+    ab:*)
+      # ab:VAR=v+VAR2=w  the hot-path quick bench under those environment settings
+      envs=$(echo "${step#ab:}" | tr '+' ' ')
+      tag=$(echo "${step#ab:}" | tr -c 'A-Za-z0-9=_\n' '_')
+      env $envs KOLM_BENCH_ALLK=1 timeout -k 10 300 python bench.py $QUICK > "$OUT/ab_$tag.json" 2> "$OUT/ab_$tag.err" \
+        || { tail -30 "$OUT/ab_$tag.err"; exit 1; }
+      echo "[$envs]"; summ "$OUT/ab_$tag.json" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
         || { tail -30 "$OUT/smoke.log"; exit 1; }
