@@ -453,10 +453,45 @@ __device__ inline u64 load8u(const u8* s, u32 x) {
 
 // x = s[a0, a1) < y = s[a1, b1) lexicographically (proper prefix smaller); wave-uniform.
 // 8 bytes per lane per step (512 per wave) while the loads stay inside s[0, N).
-__device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N, u32* nsteps = nullptr, u32 o0 = 0) {
+// NW > 1: the NW waves of the workgroup call it together with the same arguments (they run
+// the merge in lockstep) and split the long stretches (every NW-th 2 KiB per wave), their
+// first differences combined through `red` (LDS).
+template <int NW = 1>
+__device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N, u32* nsteps = nullptr, u32 o0 = 0,
+                         u32* red = nullptr) {
     const u32 lane = threadIdx.x & 63;
     const u32 la = a1 - a0, lb = b1 - a1, m = min(la, lb);
     u32 o = o0;
+    if (NW > 1) {
+        constexpr u32 SPAN = 2048;
+        const u32 wv = threadIdx.x >> 6;
+        while (o + SPAN * NW <= m && (u64)a1 + o + SPAN * NW + 12 <= N) {
+            u64 d[4];
+#pragma unroll
+            for (u32 k = 0; k < 4; ++k) {
+                const u32 t = o + SPAN * wv + 512 * k + 8 * lane;
+                d[k] = load8u(s, a0 + t) ^ load8u(s, a1 + t);
+            }
+            u32 dpos = 0xFFFFFFFFu;
+#pragma unroll
+            for (u32 k = 0; k < 4; ++k) {  // positions grow with k: the minimum is the first
+                const u64 bal = __ballot(d[k] != 0);
+                const u32 j = bal ? (u32)__ffsll((long long)bal) - 1 : 0u;
+                const u32 dj = (u32)__ffsll((long long)d[k]) - 1;
+                const u32 bj = (u32)__builtin_amdgcn_readlane((int)dj, (int)j) / 8;
+                dpos = min(dpos, bal ? o + SPAN * wv + 512 * k + 8 * j + bj : 0xFFFFFFFFu);
+            }
+            if (lane == 0) red[wv] = dpos;
+            __syncthreads();
+            u32 dm = 0xFFFFFFFFu;
+#pragma unroll
+            for (u32 w2 = 0; w2 < NW; ++w2) dm = min(dm, red[w2]);
+            __syncthreads();
+            if (nsteps) *nsteps += 4;
+            if (dm != 0xFFFFFFFFu) return s[a0 + dm] < s[a1 + dm];
+            o += SPAN * NW;
+        }
+    }
     // long common prefixes (periodic data: factors agree on KB): four 512-byte steps per
     // round trip while they lie wholly inside both factors and s[0, N)
     constexpr u32 U = 4;
@@ -549,15 +584,20 @@ __device__ inline Pre shf(const Pre& p, u32 l) {
 // prefix in LDS, so nearly all comparisons are decided in registers.  Only factors that
 // agree on 32 bytes compare the text in global memory: the chain of ~800 dependent
 // comparisons per 1 MiB text block cost ~0.7 us of load latency each.
-__global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8* s, const u32* fstart,
-                                                    const uint4* fpre, const u32* nfac, u32* stack, u32* fcount,
-                                                    u8* flag, u64* prof) {
+// NW > 1 (batches of few blocks, where one block's merge of a periodic region is the
+// critical path): NW waves run the merge in lockstep — each keeps the same stack, written
+// with the same values — and share the long comparisons (lyn_less<NW>).
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_duval_merge(Geom geo, u32 cpb, const u8* s, const u32* fstart,
+                                                         const uint4* fpre, const u32* nfac, u32* stack, u32* fcount,
+                                                         u8* flag, u64* prof) {
     __shared__ u32 lstk[MERGE_LDS];
     __shared__ Pre lpre[PRE_LDS];
     __shared__ u32 lok[PRE_LDS];
+    __shared__ u32 red[NW];
     const u64 t0 = prof ? wall_clock64() : 0;
     u32 ncmp = 0, nstep = 0;
-    const u32 b = blockIdx.x, lane = threadIdx.x;
+    const u32 b = blockIdx.x, lane = threadIdx.x & 63;
     const u32 base = geo.base(b), end = geo.end(b);
     // the stack never holds more entries than the span factorisations together: in LDS
     // when they fit (text: a few dozen), else in global memory (e.g. a run: n factors)
@@ -615,7 +655,8 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
                 else if (xok && yok && m <= 32)
                     less = la < lb;
                 else
-                    less = lyn_less(s, xs, ys, frontier, (u32)geo.N, prof ? &nstep : nullptr, xok && yok ? 32u : 0u);
+                    less = lyn_less<NW>(s, xs, ys, frontier, (u32)geo.N, prof ? &nstep : nullptr, xok && yok ? 32u : 0u,
+                                        red);
                 if (!less) break;
                 --sp;  // x absorbs y: the merged factor keeps x's start and prefix
                 ys = xs;
@@ -661,13 +702,15 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
     }
     // the block's factor starts: flags, and the sorted list at stack + base (in place when
     // the stack spilled to global memory)
-    for (u32 i = lane; i < sp; i += 64) {
-        const u32 v = stk[i];
-        flag[v] = 1;
-        if (tot <= MERGE_LDS) stack[base + i] = v;
+    if (threadIdx.x < 64) {
+        for (u32 i = lane; i < sp; i += 64) {
+            const u32 v = stk[i];
+            flag[v] = 1;
+            if (tot <= MERGE_LDS) stack[base + i] = v;
+        }
     }
-    if (lane == 0) fcount[b] = sp;
-    if (prof && lane == 0) {
+    if (threadIdx.x == 0) fcount[b] = sp;
+    if (prof && threadIdx.x == 0) {
         atomicAdd((unsigned long long*)&prof[11], (unsigned long long)(wall_clock64() - t0));
         atomicMax((unsigned long long*)&prof[12], (unsigned long long)(wall_clock64() - t0));
         atomicAdd((unsigned long long*)&prof[13], (unsigned long long)ncmp);
@@ -784,7 +827,13 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fsta
     }
     {
         KScope k(kt, KT_LYNDON, "k_duval_merge", (u64)nch * 8);
-        k_duval_merge<<<geo.nb, 64, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, stack, fcount, flag, dprof_buf());
+        // batches of few blocks: 8 waves per block share the long comparisons (KOLM_DUVAL_NW = 1
+        // or 8 forces one form)
+        static const int fw = getenv("KOLM_DUVAL_NW") ? atoi(getenv("KOLM_DUVAL_NW")) : 0;
+        if (fw == 8 || (fw == 0 && geo.nb < 64))
+            k_duval_merge<8><<<geo.nb, 512, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, stack, fcount, flag, dprof_buf());
+        else
+            k_duval_merge<1><<<geo.nb, 64, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, stack, fcount, flag, dprof_buf());
     }
     if (u64* prof = dprof_buf()) {
         u64 h[16];
