@@ -451,21 +451,17 @@ __device__ inline u64 load8u(const u8* s, u32 x) {
     return ((u64)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
 }
 
-// x = s[a0, a1) < y = s[a1, b1) lexicographically (proper prefix smaller); wave-uniform.
-// 8 bytes per lane per step (512 per wave) while the loads stay inside s[0, N).
-// NW > 1: the NW waves of the workgroup call it together with the same arguments (they run
-// the merge in lockstep) and split the long stretches (every NW-th 2 KiB per wave), their
-// first differences combined through `red` (LDS).
-template <int NW = 1>
-__device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N, u32* nsteps = nullptr, u32 o0 = 0,
-                         u32* red = nullptr) {
+// Cooperative stretches of a long comparison (NW waves; see k_duval_merge): wave w takes
+// every NW-th 2 KiB, the first differences are combined through `red` (LDS).  Every wave of
+// the workgroup calls it with the same arguments (two barriers per stretch).  Returns the
+// first differing offset, or 0xFFFFFFFF with *o advanced past the stretches compared.
+template <int NW>
+__device__ u32 lyn_coop(const u8* s, u32 a0, u32 a1, u32 m, u32 N, u32& o, u32* red, u32* nsteps) {
     const u32 lane = threadIdx.x & 63;
-    const u32 la = a1 - a0, lb = b1 - a1, m = min(la, lb);
-    u32 o = o0;
-    if (NW > 1) {
-        constexpr u32 SPAN = 2048;
-        const u32 wv = threadIdx.x >> 6;
-        while (o + SPAN * NW <= m && (u64)a1 + o + SPAN * NW + 12 <= N) {
+    constexpr u32 SPAN = 2048;
+    const u32 wv = threadIdx.x >> 6;
+    while (o + SPAN * NW <= m && (u64)a1 + o + SPAN * NW + 12 <= N) {
+        {
             u64 d[4];
 #pragma unroll
             for (u32 k = 0; k < 4; ++k) {
@@ -488,9 +484,34 @@ __device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N, u32* nsteps
             for (u32 w2 = 0; w2 < NW; ++w2) dm = min(dm, red[w2]);
             __syncthreads();
             if (nsteps) *nsteps += 4;
-            if (dm != 0xFFFFFFFFu) return s[a0 + dm] < s[a1 + dm];
+            if (dm != 0xFFFFFFFFu) return dm;
             o += SPAN * NW;
         }
+    }
+    return 0xFFFFFFFFu;
+}
+
+// The command the merging wave posts for its helper waves (k_duval_merge<NW > 1>).
+struct LynCmd {
+    u32 op;  // 1 = compare (a0, a1, m, o), 2 = exit
+    u32 a0, a1, m, o;
+};
+
+// x = s[a0, a1) < y = s[a1, b1) lexicographically (proper prefix smaller); wave-uniform.
+// 8 bytes per lane per step (512 per wave) while the loads stay inside s[0, N).
+// NW > 1: called by the merging wave 0 only; a comparison long enough for a cooperative
+// stretch is posted to the helper waves (cmd, one barrier) and run by all NW waves.
+template <int NW = 1>
+__device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N, u32* nsteps = nullptr, u32 o0 = 0,
+                         u32* red = nullptr, LynCmd* cmd = nullptr) {
+    const u32 lane = threadIdx.x & 63;
+    const u32 la = a1 - a0, lb = b1 - a1, m = min(la, lb);
+    u32 o = o0;
+    if (NW > 1 && o + 2048 * NW <= m && (u64)a1 + o + 2048 * NW + 12 <= N) {
+        if (lane == 0) *cmd = LynCmd{1u, a0, a1, m, o};
+        __syncthreads();  // the helpers read the command
+        const u32 dm = lyn_coop<NW>(s, a0, a1, m, N, o, red, nsteps);
+        if (dm != 0xFFFFFFFFu) return s[a0 + dm] < s[a1 + dm];
     }
     // long common prefixes (periodic data: factors agree on KB): four 512-byte steps per
     // round trip while they lie wholly inside both factors and s[0, N)
@@ -585,8 +606,10 @@ __device__ inline Pre shf(const Pre& p, u32 l) {
 // agree on 32 bytes compare the text in global memory: the chain of ~800 dependent
 // comparisons per 1 MiB text block cost ~0.7 us of load latency each.
 // NW > 1 (batches of few blocks, where one block's merge of a periodic region is the
-// critical path): NW waves run the merge in lockstep — each keeps the same stack, written
-// with the same values — and share the long comparisons (lyn_less<NW>).
+// critical path): wave 0 merges; waves 1 .. NW-1 only help with the long comparisons — they
+// wait at a barrier for a command (lyn_less<NW> posts one per comparison long enough for a
+// cooperative stretch), run the stretches with wave 0 (lyn_coop), and leave on the exit
+// command.  The stack is wave 0's alone.
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void k_duval_merge(Geom geo, u32 cpb, const u8* s, const u32* fstart,
                                                          const uint4* fpre, const u32* nfac, u32* stack, u32* fcount,
@@ -595,6 +618,16 @@ __global__ __launch_bounds__(64 * NW) void k_duval_merge(Geom geo, u32 cpb, cons
     __shared__ Pre lpre[PRE_LDS];
     __shared__ u32 lok[PRE_LDS];
     __shared__ u32 red[NW];
+    __shared__ LynCmd cmd;
+    if (NW > 1 && threadIdx.x >= 64) {  // helper waves
+        for (;;) {
+            __syncthreads();
+            const LynCmd c = cmd;
+            if (c.op != 1) return;
+            u32 o = c.o;
+            lyn_coop<NW>(s, c.a0, c.a1, c.m, (u32)geo.N, o, red, nullptr);
+        }
+    }
     const u64 t0 = prof ? wall_clock64() : 0;
     u32 ncmp = 0, nstep = 0;
     const u32 b = blockIdx.x, lane = threadIdx.x & 63;
@@ -656,7 +689,7 @@ __global__ __launch_bounds__(64 * NW) void k_duval_merge(Geom geo, u32 cpb, cons
                     less = la < lb;
                 else
                     less = lyn_less<NW>(s, xs, ys, frontier, (u32)geo.N, prof ? &nstep : nullptr, xok && yok ? 32u : 0u,
-                                        red);
+                                        red, &cmd);
                 if (!less) break;
                 --sp;  // x absorbs y: the merged factor keeps x's start and prefix
                 ys = xs;
@@ -702,12 +735,14 @@ __global__ __launch_bounds__(64 * NW) void k_duval_merge(Geom geo, u32 cpb, cons
     }
     // the block's factor starts: flags, and the sorted list at stack + base (in place when
     // the stack spilled to global memory)
-    if (threadIdx.x < 64) {
-        for (u32 i = lane; i < sp; i += 64) {
-            const u32 v = stk[i];
-            flag[v] = 1;
-            if (tot <= MERGE_LDS) stack[base + i] = v;
-        }
+    for (u32 i = lane; i < sp; i += 64) {
+        const u32 v = stk[i];
+        flag[v] = 1;
+        if (tot <= MERGE_LDS) stack[base + i] = v;
+    }
+    if (NW > 1) {  // release the helpers
+        if (lane == 0) cmd.op = 2;
+        __syncthreads();
     }
     if (threadIdx.x == 0) fcount[b] = sp;
     if (prof && threadIdx.x == 0) {
