@@ -538,8 +538,10 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             hi = shift;
             ++lvl;
         }
-        KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
-        c->sync();
+        if (lvl) {  // the MSD levels appended segments to the class lists: fresh counts
+            KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
+            c->sync();
+        }
         // per element: K2 + SA read, SA + RK write (16 B); per segment record 8 B
         for (int k = 0; k < NCLASS; ++k) {
             if (!h[C_CLS + k]) continue;

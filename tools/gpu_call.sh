@@ -50,7 +50,7 @@ for step in "$@"; do
         || { tail -30 "$OUT/ab_$tag.err"; exit 1; }
       echo "[$envs]"; summ "$OUT/ab_$tag.json" ;;
     smoke)
-      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+      timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
         || { tail -30 "$OUT/smoke.log"; exit 1; }
       tail -4 "$OUT/smoke.log" ;;
     profile)
