@@ -25,11 +25,9 @@ def test_multibatch_container_and_stats(kolm_gpu, monkeypatch):
     many = kolm_gpu.compress_blocks_fixed(data, bs, hot_path=True)
     st4 = kolm_gpu.last_stats()
     assert many == want
-    # per-block quantities add up over the batches exactly as in one batch (the LZ77 token
-    # count is a function of each block alone; the doubling-round sum is not: a batch runs
-    # one last round to find its blocks converged)
+    # statistics of the batches add up: the LZ77 token count is a function of each block
+    # alone (the doubling-round sum is not: it counts the rounds of each batch)
     assert st4["lz_tokens"] == st1["lz_tokens"]
-    assert st4["cyc_rounds_sum"] >= st1["cyc_rounds_sum"] - 4
     assert kolm_gpu.decompress(many) == data
 
 
