@@ -64,8 +64,6 @@ LIMITER = {
                     "adjacent factorisations (dependent LDS byte compares / bitmap scans); reads the text once",
     "k_lsd_scatter_w<3, 2, 1>": "random 4-byte gathers of the next key by position (one 32-64 B request each) "
                                 "beside the streaming LSD scatter",
-    "k_r0_sweep": "HBM streaming: every LSD pass of a block in one workgroup, 24 B per element per pass "
-                  "(records read + written), one workgroup per CU (4 waves) with the next chunk's loads in flight",
 }
 SORT_STREAM_LIMITER = ("random 4-byte gathers / scatters of ranks and keys by position (one 32-64 B HBM "
                        "request per element in the doubling rounds and the RK scatter), streaming LSD passes at "

@@ -332,9 +332,8 @@ __device__ inline u32 wave_min(u32 v) { return wave_reduce(v, OpMinU(), BIG); }
 // (the block's first slot, or its key differs from the previous slot's; with KA — the
 // 8-character round 0, K = characters 0..3 — also when characters 4..7, KA[SA[slot]],
 // differ).  tmax / tmin = the tile's last / first head.
-// KA_sorted: KA is indexed by slot (the block sweep carries the whole key, no gather).
 __global__ __launch_bounds__(WG) void k_r0_tile_heads(LsdGeom g, const u32* K, const u32* SA, const u32* KA, u32* HF,
-                                                      u32* tmax, u32* tmin, u32* BH, u32 ka_sorted) {
+                                                      u32* tmax, u32* tmin, u32* BH) {
     __shared__ u32 s1[WG / 64], s2[WG / 64];
     __shared__ u32 bh[WG / 64][256];  // BH: per wave, slots of this tile per position window
     const u32 t = xcd_tile();
@@ -361,10 +360,7 @@ __global__ __launch_bounds__(WG) void k_r0_tile_heads(LsdGeom g, const u32* K, c
                 for (u32 e = 0; e < LSD_PT; ++e)
                     if (i0 + e < hi) atomicAdd(&bh[w][(sv[e] - base) >> R0_WS], 1u);
             }
-            if (KA && ka_sorted) {
-                load16(KA, i0, hi, av);
-                aprev = i0 > base ? KA[i0 - 1] : 0u;
-            } else if (KA) {
+            if (KA) {
 #pragma unroll
                 for (u32 e = 0; e < LSD_PT; ++e) av[e] = i0 + e < hi ? KA[sv[e]] : 0u;
                 aprev = i0 > base ? KA[SA[i0 - 1]] : 0u;
@@ -624,10 +620,10 @@ __global__ __launch_bounds__(WG) void k_alpha_codes(const u32* pres, u8* code, u
     for (u32 k = 0; k < (c >> 5); ++k) r += __popc(pw[k]);
     r += __popc(pw[c >> 5] & ((1u << (c & 31)) - 1u));
     code[(u64)b * 256 + c] = (u8)r;
-    if (c == 255) {  // (sigma << 8 | w): the batch's largest alphabet and its code width
+    if (c == 255) {
         const u32 sigma = r + ((pw[7] >> 31) & 1u);
         const u32 w = sigma > 1 ? 32 - __clz(sigma - 1) : 1u;
-        atomicMax(wmax, sigma << 8 | w);
+        atomicMax(wmax, w);
     }
 }
 
@@ -639,28 +635,20 @@ __global__ __launch_bounds__(WG) void k_alpha_codes(const u32* pres, u8* code, u
 // C) are rebuilt from the factor record.
 // hist0 (optional): the first LSD pass's per-tile digit counts (digit 0 of KA), so that
 // pass needs no histogram kernel of its own.
-// HB = 8: hist0 = digit 0 (bits 0..7 of KA, padding included) in per-wave LDS copies, 256
-// bins per tile (the tile LSD).  HB = 10: the block sweep's digit 0 (bits sh .. sh + 9 of
-// the key), 1024 bins per tile in one LDS array.
-// R > 0: mixed-radix packing, key = sum of code_k * R^(C-1-k) (order-preserving as codes < R;
-// top = R^(C-1)), so C = floor(64 / log2 R) characters fit (enwik-style text, R = 50: 11
-// instead of 10 six-bit codes); R = 0: w-bit codes side by side.
-template <int HB>
 __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32 C, u32 w, u32 sh, u32* KA, u32* KB,
-                                                  u32* hist0, u32 R, u64 top) {
-    constexpr u32 HR = 1u << HB, HC = HB == 8 ? WG / 64 : 1;
+                                                  u32* hist0) {
     __shared__ __align__(16) u8 tx[LSD_T + 64];
     __shared__ u8 cd[256];
-    __shared__ u32 h0[HC][HR];
+    __shared__ u32 h0[WG / 64][256];
     u32 lo, hi, b;
     const u32 tile = xcd_tile();
     if (!g.range(tile, lo, hi, b)) {  // a tile past its block's end (the whole workgroup)
-        if (hist0)
-            for (u32 d = threadIdx.x; d < HR; d += WG) hist0[(u64)tile * HR + d] = 0;
+        if (hist0) hist0[(u64)tile * 256 + threadIdx.x] = 0;
         return;
     }
     if (hist0) {
-        for (u32 i = threadIdx.x; i < HC * HR; i += WG) (&h0[0][0])[i] = 0;
+#pragma unroll
+        for (int i = 0; i < WG / 64; ++i) h0[i][threadIdx.x] = 0;
     }
     const u32 N = (u32)g.geo.N;
     cd[threadIdx.x] = code[(u64)b * 256 + threadIdx.x];
@@ -691,25 +679,14 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
     }
     const u64 mask = C * w >= 64 ? ~0ull : ((1ull << (C * w)) - 1);
     u64 key = 0;
+    for (u32 k = 0; k < C; ++k) key = (key << w) | (i0 + k < n ? cd[tx[i0 + k]] : 0u);
     u32 ka[LSD_PT], kb[LSD_PT];
-    if (R) {
-        for (u32 k = 0; k < C; ++k) key = key * R + (i0 + k < n ? cd[tx[i0 + k]] : 0u);
 #pragma unroll
-        for (u32 e = 0; e < LSD_PT; ++e) {
-            ka[e] = (u32)(key << sh);
-            kb[e] = (u32)((key << sh) >> 32);
-            const u32 x = i0 + e + C;
-            key = (key - top * cd[tx[i0 + e]]) * R + (x < n ? cd[tx[x]] : 0u);
-        }
-    } else {
-        for (u32 k = 0; k < C; ++k) key = (key << w) | (i0 + k < n ? cd[tx[i0 + k]] : 0u);
-#pragma unroll
-        for (u32 e = 0; e < LSD_PT; ++e) {
-            ka[e] = (u32)(key << sh);
-            kb[e] = (u32)((key << sh) >> 32);
-            const u32 x = i0 + e + C;
-            key = ((key << w) | (x < n ? cd[tx[x]] : 0u)) & mask;
-        }
+    for (u32 e = 0; e < LSD_PT; ++e) {
+        ka[e] = (u32)(key << sh);
+        kb[e] = (u32)((key << sh) >> 32);
+        const u32 x = i0 + e + C;
+        key = ((key << w) | (x < n ? cd[tx[x]] : 0u)) & mask;
     }
 #pragma unroll
     for (u32 e = 0; e < LSD_PT; ++e) {
@@ -720,7 +697,7 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
             u32 t = p - fs;
             u64 k2 = 0;
             for (u32 k = 0; k < C; ++k) {
-                k2 = R ? k2 * R + cd[g.text[fs + t]] : (k2 << w) | cd[g.text[fs + t]];
+                k2 = (k2 << w) | cd[g.text[fs + t]];
                 if (++t == m) t = 0;
             }
             ka[e] = (u32)(k2 << sh);
@@ -741,187 +718,16 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
         }
     }
     if (hist0) {
-        const u32 wv = HB == 8 ? threadIdx.x >> 6 : 0u;
+        const u32 wv = threadIdx.x >> 6;
 #pragma unroll
         for (u32 e = 0; e < LSD_PT; ++e)
-            if (p0 + e < hi) {
-                const u64 k64 = (u64)kb[e] << 32 | ka[e];
-                atomicAdd(&h0[wv][HB == 8 ? digit<0>(ka[e]) : (u32)(k64 >> sh) & (HR - 1)], 1u);
-            }
+            if (p0 + e < hi) atomicAdd(&h0[wv][digit<0>(ka[e])], 1u);
     }
     }
     if (hist0) {
         __syncthreads();
-        for (u32 d = threadIdx.x; d < HR; d += WG) {
-            u32 v = 0;
-#pragma unroll
-            for (u32 q = 0; q < HC; ++q) v += h0[q][d];
-            hist0[(u64)tile * HR + d] = v;
-        }
-    }
-}
-
-
-// ---------------------------------------------------------------------------------
-// Round 0 as one sweep per block (batches of many blocks): one workgroup owns
-// a block and runs every LSD pass over it inside one launch — SW_DB-bit digits over the key
-// bits [sh, 64) (text: 60 code bits = 6 passes instead of 8), records (KA, KB, position)
-// carried whole, so no histogram passes, no scan launches, no gather of the high key half
-// and no gather of KA for the group heads.  The block's digit counts do not change between
-// passes: pass 0's come from k_keypos_r0 (per-tile), pass p + 1's are counted while pass p
-// ranks (one LDS atomic per element).  A pass streams its source in chunks of SW_CH
-// elements (wave w owns the contiguous quarter, SW_SPW steps of 64, all in registers, the
-// next chunk's loads issued before this one is ranked): ballot-match ranks per wave (the
-// digit's leader advances the wave's LDS counter), one barrier, per-digit wave offsets,
-// one barrier, stores.  Each digit's write frontier advances monotonically through the
-// block, so its partial lines stay in L2 until they are full.
-// ---------------------------------------------------------------------------------
-constexpr u32 SW_DB = 10, SW_R = 1u << SW_DB;
-
-struct SweepArgs {
-    Geom geo;
-    u32 tpb;          // LSD tiles per block (hist0 rows of a block)
-    u32 sh;           // first key bit of digit 0
-    u32 P;            // passes
-    const u32* hist0; // [tiles][SW_R]
-    const u32* KA0;   // keys by position (low / high 32 bits; KB0 null: keys of <= 32 bits)
-    const u32* KB0;
-    u32* A[2];        // record sets: pass p writes set (p + first) & 1
-    u32* B[2];
-    u32* Q[2];
-    u32 first;
-};
-
-template <int HASB, int SW_NW, int SW_SPW, int PF = 1>  // PF: chunks of loads in flight ahead (1 or 2)
-__global__ __launch_bounds__(SW_NW * 64) void k_r0_sweep(SweepArgs a) {
-    constexpr u32 SW_NT = SW_NW * 64, SW_CH = SW_NT * SW_SPW;
-    __shared__ u32 run[2][SW_R];      // per chunk parity: running destination of every digit
-    __shared__ u32 hnext[SW_R];       // digit counts of the next pass
-    __shared__ u16 wc[SW_NW][SW_R];   // per wave: digit counts of the chunk, then wave offsets
-    __shared__ u32 wsum[SW_NW];
-    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const u32 b = blockIdx.x;
-    const u32 base = a.geo.base(b), end = a.geo.end(b), n = end - base;
-    const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    // pass 0's digit counts: the block's tiles
-    for (u32 d = tid; d < SW_R; d += SW_NT) {
-        u32 v = 0;
-        const u32* h = a.hist0 + (u64)b * a.tpb * SW_R + d;
-        for (u32 k = 0; k < a.tpb; ++k) v += h[(u64)k * SW_R];
-        run[0][d] = v;  // counts for now, offsets below
-        hnext[d] = 0;
-    }
-    for (u32 i = tid; i < SW_NW * SW_R / 2; i += SW_NT) reinterpret_cast<u32*>(&wc[0][0])[i] = 0;
-    __syncthreads();
-    const u32 nch = (n + SW_CH - 1) / SW_CH;
-    for (u32 p = 0; p < a.P; ++p) {
-        // run[0][d] = base + exclusive prefix of the digit counts (4 digits per thread)
-        {
-            constexpr u32 PER = SW_R / SW_NT;
-            u32 v[PER], t = 0;
-#pragma unroll
-            for (u32 q = 0; q < PER; ++q) v[q] = run[0][tid * PER + q], t += v[q];
-            const u32 inc = wave_incl_scan(t, OpAddU(), 0u);
-            if (lane == 63) wsum[w] = inc;
-            __syncthreads();
-            u32 ex = base + inc - t;
-            for (u32 q = 0; q < w; ++q) ex += wsum[q];
-#pragma unroll
-            for (u32 q = 0; q < PER; ++q) run[0][tid * PER + q] = ex, ex += v[q];
-        }
-        __syncthreads();
-        const u32 so = (p + a.first + 1) & 1, dn = (p + a.first) & 1;  // source set (p > 0), destination
-        const u32* sa = p ? a.A[so] : a.KA0;
-        const u32* sb = p ? a.B[so] : a.KB0;
-        const u32* sq = p ? a.Q[so] : nullptr;
-        u32 *da = a.A[dn], *db = a.B[dn], *dq = a.Q[dn];
-        const u32 sh = a.sh + SW_DB * p, shn = sh + SW_DB;
-        const bool cnt_next = p + 1 < a.P;
-        u32 ka[SW_SPW], kb[SW_SPW], kq[SW_SPW];
-        auto load = [&](u32 c, u32 (&xa)[SW_SPW], u32 (&xb)[SW_SPW], u32 (&xq)[SW_SPW]) {
-            const u32 q0 = base + c * SW_CH + w * (SW_CH / SW_NW);
-#pragma unroll
-            for (u32 j = 0; j < SW_SPW; ++j) {
-                const u32 i = q0 + j * 64 + lane;
-                const bool v = i < end;
-                xa[j] = v ? sa[i] : 0u;
-                xb[j] = HASB && v ? sb[i] : 0u;
-                xq[j] = v ? (sq ? sq[i] : i) : 0u;
-            }
-        };
-        u32 fa[SW_SPW], fb[SW_SPW], fq[SW_SPW];  // PF = 2: chunk c + 1, loaded one chunk earlier
-        load(0, ka, kb, kq);
-        if (PF == 2 && 1 < nch) load(1, fa, fb, fq);
-        for (u32 c = 0; c < nch; ++c) {
-            const u32 par = c & 1;
-            u32 na[SW_SPW], nbv[SW_SPW], nq[SW_SPW];
-            if (PF == 2) {
-                if (c + 2 < nch) load(c + 2, na, nbv, nq);
-            } else if (c + 1 < nch) {
-                load(c + 1, na, nbv, nq);
-            }
-            const u32 q0 = base + c * SW_CH + w * (SW_CH / SW_NW);
-            u32 dr[SW_SPW];  // digit | rank among the wave's equal digits << 16
-#pragma unroll
-            for (u32 j = 0; j < SW_SPW; ++j) {
-                const bool v = q0 + j * 64 + lane < end;
-                const u64 k64 = (u64)kb[j] << 32 | ka[j];
-                const u32 d = (u32)(k64 >> sh) & (SW_R - 1);
-                u64 m = __ballot(v);
-#pragma unroll
-                for (u32 bit = 0; bit < SW_DB; ++bit) {
-                    const u64 bb = __ballot((d >> bit) & 1u);
-                    m &= ((d >> bit) & 1u) ? bb : ~bb;
-                }
-                const u32 r = __popcll(m & lt);
-                const u32 pre = v ? wc[w][d] : 0u;
-                dr[j] = d | (pre + r) << 16;
-                if (v && r == 0) wc[w][d] = (u16)(pre + __popcll(m));
-                if (v && cnt_next) atomicAdd(&hnext[(u32)(k64 >> shn) & (SW_R - 1)], 1u);
-            }
-            __syncthreads();
-            // wave offsets per digit (in place), running destinations for the next chunk
-            for (u32 d = tid; d < SW_R; d += SW_NT) {
-                u32 acc = 0;
-#pragma unroll
-                for (u32 q = 0; q < SW_NW; ++q) {
-                    const u32 t = wc[q][d];
-                    wc[q][d] = (u16)acc;
-                    acc += t;
-                }
-                run[par ^ 1][d] = run[par][d] + acc;
-            }
-            __syncthreads();
-#pragma unroll
-            for (u32 j = 0; j < SW_SPW; ++j) {
-                if (q0 + j * 64 + lane < end) {
-                    const u32 d = dr[j] & 0xFFFFu;
-                    const u32 dst = run[par][d] + wc[w][d] + (dr[j] >> 16);
-                    da[dst] = ka[j];
-                    if (HASB) db[dst] = kb[j];
-                    dq[dst] = kq[j];
-                }
-            }
-            // this wave's counters back to zero for the next chunk (only this wave reads its row)
-            for (u32 i = lane; i < SW_R / 2; i += 64) reinterpret_cast<u32*>(&wc[w][0])[i] = 0;
-            if (PF == 2) {
-#pragma unroll
-                for (u32 j = 0; j < SW_SPW; ++j) {
-                    ka[j] = fa[j], kb[j] = fb[j], kq[j] = fq[j];
-                    fa[j] = na[j], fb[j] = nbv[j], fq[j] = nq[j];
-                }
-            } else if (c + 1 < nch) {
-#pragma unroll
-                for (u32 j = 0; j < SW_SPW; ++j) ka[j] = na[j], kb[j] = nbv[j], kq[j] = nq[j];
-            }
-        }
-        __syncthreads();
-        // the next pass's counts (run[0] is rewritten as offsets at the top of the pass)
-        for (u32 d = tid; d < SW_R; d += SW_NT) {
-            run[0][d] = hnext[d];
-            hnext[d] = 0;
-        }
-        __syncthreads();
+        hist0[(u64)tile * 256 + threadIdx.x] = h0[0][threadIdx.x] + h0[1][threadIdx.x] + h0[2][threadIdx.x] +
+                                               h0[3][threadIdx.x];
     }
 }
 
@@ -978,8 +784,7 @@ u32 lsd_tiles(const Geom& geo) { return (geo.bs + LSD_T - 1) / LSD_T * geo.nb; }
 // Per-block code tables (alphabet compaction); returns the max code width w of the batch
 // (one host round trip).  compact = false: identity codes, w = 8.
 u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w, u32* h_w, bool compact,
-                 hipStream_t s, KTimer* kt, u32* sigma) {
-    if (sigma) *sigma = 256;
+                 hipStream_t s, KTimer* kt) {
     if (!geo.N) return 8;
     if (!compact) {
         std::vector<u8> id(256 * (size_t)geo.nb);
@@ -998,8 +803,7 @@ u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w,
     }
     KOLM_HIP_CHECK(hipMemcpyAsync(h_w, d_w, sizeof(u32), hipMemcpyDeviceToHost, s));
     KOLM_HIP_CHECK(hipStreamSynchronize(s));
-    if (sigma) *sigma = std::max<u32>(1, std::min<u32>(256, *h_w >> 8));
-    return std::max<u32>(1, std::min<u32>(8, *h_w & 255u));
+    return std::max<u32>(1, std::min<u32>(8, *h_w));
 }
 
 // Round 0 of the cyclic sort: a stable sort of every block's positions by the packed codes
@@ -1017,64 +821,26 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
     const u64 N = geo.N;
     // D byte digits; the packed codes are left-aligned in them, so the 8 D - C w padding bits
     // fall into the first pass's digit (its few distinct values keep that scatter's runs long)
-    const u32 bits = t.bits, D = (bits + 7) / 8, sh = 8 * D - bits;
+    const u32 bits = t.chars * t.w, D = (bits + 7) / 8, sh = 8 * D - bits;
     const u32 pa = std::min<u32>(4, D), pb = D - pa;
-    // The block sweep (k_r0_sweep) when the batch has enough blocks to give every CU one
-    // (KOLM_R0_SWEEP_MIN, default 192; 0 = always, a large value = never) and the block fits
-    // its 16-bit chunk counters; otherwise the tile LSD (hist / scan / scatter per pass).
-    static const u32 sweep_min = getenv("KOLM_R0_SWEEP_MIN") ? (u32)atoi(getenv("KOLM_R0_SWEEP_MIN")) : 0xFFFFFFFFu;
-    const bool sweep = geo.nb >= sweep_min && geo.bs <= (1u << 24);
-    if (sweep) {
-        const u32 P = (bits + SW_DB - 1) / SW_DB;
-        // keys by position into (RK, KP) when P is even, else (K2, K22); pass p writes set
-        // (p + first) & 1 of F = (RK, KP, SA) / O = (K2, K22, SA2) and the last pass lands in F
-        const bool odd = P & 1;
-        u32* KA0 = odd ? t.K2 : t.RK;
-        u32* KB0 = pb ? (odd ? t.K22 : t.KP) : nullptr;
-        {
-            KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6) + (u64)nt * SW_R * 4);
-            k_keypos_r0<SW_DB><<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, KA0, KB0, t.hist, t.radix, t.top);
-        }
-        SweepArgs sa{geo, g.tpb, sh, P, t.hist, KA0, KB0, {t.RK, t.K2}, {t.KP, t.K22}, {t.SA, t.SA2}, odd ? 0u : 1u};
-        {
-            // per pass: records (KA, KB, position) read and written (pass 0 reads the keys by
-            // position); + pass 0's tile counts
-            const u64 rec = pb ? 12 : 8;
-            KScope k(kt, KT_LSD, "k_r0_sweep",
-                     N * (2 * rec * P - 4) + (u64)nt * SW_R * 4);
-            // KOLM_R0_SWEEP_CFG: waves x steps per wave of a chunk (0: 4 x 8, 1: 8 x 8, 2: 4 x 16,
-            // 3: 4 x 8 with two chunks of loads in flight)
-            static const int cfg = getenv("KOLM_R0_SWEEP_CFG") ? atoi(getenv("KOLM_R0_SWEEP_CFG")) : 0;
-            if (cfg == 3)
-                pb ? k_r0_sweep<1, 4, 8, 2><<<geo.nb, 256, 0, s>>>(sa) : k_r0_sweep<0, 4, 8, 2><<<geo.nb, 256, 0, s>>>(sa);
-            else if (cfg == 1)
-                pb ? k_r0_sweep<1, 8, 8><<<geo.nb, 512, 0, s>>>(sa) : k_r0_sweep<0, 8, 8><<<geo.nb, 512, 0, s>>>(sa);
-            else if (cfg == 2)
-                pb ? k_r0_sweep<1, 4, 16><<<geo.nb, 256, 0, s>>>(sa) : k_r0_sweep<0, 4, 16><<<geo.nb, 256, 0, s>>>(sa);
-            else
-                pb ? k_r0_sweep<1, 4, 8><<<geo.nb, 256, 0, s>>>(sa) : k_r0_sweep<0, 4, 8><<<geo.nb, 256, 0, s>>>(sa);
-        }
-    } else {
-        {
-            // text + FEd 2 (+ factor starts near factor ends), KA 4 (+ KB 4)
-            KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6));
-            k_keypos_r0<8><<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist, t.radix,
-                                             t.top);
-        }
-        u32* K[2] = {t.K2, t.K22};
-        u32* S[2] = {t.SA, t.SA2};
-        const u32 T = pa + pb;
-        int o = (T & 1) ? 0 : 1;  // output pair of the first pass: the last one lands in (K2, SA)
-        for (u32 q = 0; q < pa; ++q) {
-            const bool first = q == 0, gat = q + 1 == pa && pb > 0;
-            run_pass((int)q, first, gat, g, nt, first ? t.RK : K[o ^ 1], first ? nullptr : S[o ^ 1], K[o], S[o],
-                     gat ? t.KP : nullptr, t.hist, first, s, kt);
-            o ^= 1;
-        }
-        for (u32 q = 0; q < pb; ++q) {
-            run_pass((int)q, false, false, g, nt, K[o ^ 1], S[o ^ 1], K[o], S[o], nullptr, t.hist, false, s, kt);
-            o ^= 1;
-        }
+    {
+        // text + FEd 2 (+ factor starts near factor ends), KA 4 (+ KB 4)
+        KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6));
+        k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist);
+    }
+    u32* K[2] = {t.K2, t.K22};
+    u32* S[2] = {t.SA, t.SA2};
+    const u32 T = pa + pb;
+    int o = (T & 1) ? 0 : 1;  // output pair of the first pass: the last one lands in (K2, SA)
+    for (u32 q = 0; q < pa; ++q) {
+        const bool first = q == 0, gat = q + 1 == pa && pb > 0;
+        run_pass((int)q, first, gat, g, nt, first ? t.RK : K[o ^ 1], first ? nullptr : S[o ^ 1], K[o], S[o],
+                 gat ? t.KP : nullptr, t.hist, first, s, kt);
+        o ^= 1;
+    }
+    for (u32 q = 0; q < pb; ++q) {
+        run_pass((int)q, false, false, g, nt, K[o ^ 1], S[o ^ 1], K[o], S[o], nullptr, t.hist, false, s, kt);
+        o ^= 1;
     }
     // RK through position windows (k_r0_rk) when every block has at most 256 of them;
     // KOLM_R0F_WIN=0: the direct scatter
@@ -1083,12 +849,8 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
     {
         // K 4 (+ SA 4 + the KA gather 4) read, head masks written
         KScope k(kt, KT_LSD, "k_r0_tile_heads", (pb || win ? 12 : 4) * N);
-        if (sweep)  // the sweep's final records: KA by slot in RK, KB by slot in KP
-            k_r0_tile_heads<<<nt, WG, 0, s>>>(g, pb ? t.KP : t.RK, t.SA, pb ? t.RK : nullptr, t.HF, t.tmax, t.tmin,
-                                              win ? t.hist : nullptr, 1);
-        else
-            k_r0_tile_heads<<<nt, WG, 0, s>>>(g, t.K2, t.SA, pb ? t.RK : nullptr, t.HF, t.tmax, t.tmin,
-                                              win ? t.hist : nullptr, 0);
+        k_r0_tile_heads<<<nt, WG, 0, s>>>(g, t.K2, t.SA, pb ? t.RK : nullptr, t.HF, t.tmax, t.tmin,
+                                          win ? t.hist : nullptr);
         k_tiles_max_scan<<<geo.nb, WG, 0, s>>>(t.tmax, t.cmax, g.tpb);
         k_r0_tiles_rscan<<<geo.nb, WG, 0, s>>>(t.tmin, t.cmin, g.tpb);
     }

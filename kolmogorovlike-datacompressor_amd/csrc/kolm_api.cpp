@@ -406,35 +406,16 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             static const bool compact = !(getenv("KOLM_R0_ALPHA") && atoi(getenv("KOLM_R0_ALPHA")) == 0);
             const u64 nt = lsd_tiles(geo) + 1;
             u8* code = c->get<u8>("r0code", (u64)geo.nb * 256);
-            u32 sigma = 256;
             const u32 w = launch_alpha(geo, text, c->get<u32>("r0pres", (u64)geo.nb * 8), code, cnt + C_ALPHA,
-                                       h + C_ALPHA, compact, s, c->kt(), &sigma);
+                                       h + C_ALPHA, compact, s, c->kt());
             static const u32 cmax = getenv("KOLM_R0_CMAX") ? (u32)atoi(getenv("KOLM_R0_CMAX")) : 32u;  // A/B (<= 64)
-            // mixed-radix keys (KOLM_R0_RADIX, default on) when they hold more characters than
-            // w-bit codes: radix R = the batch's largest alphabet, C = max c with R^c < 2^64
-            static const bool use_radix = !(getenv("KOLM_R0_RADIX") && atoi(getenv("KOLM_R0_RADIX")) == 0);
-            u32 C = std::max<u32>(1, std::min<u32>(std::min<u32>(64, cmax), 64 / w));
-            u32 radix = 0, kbits = C * w;
-            u64 top = 0;
-            if (use_radix && compact) {
-                const u32 R = std::max<u32>(2, sigma);
-                unsigned __int128 p = 1;
-                u32 cr = 0;
-                while (cr < std::min<u32>(64, cmax) && p * R <= (unsigned __int128)~0ull) p *= R, ++cr;
-                if (cr > C) {
-                    C = cr;
-                    radix = R;
-                    top = (u64)(p / R);
-                    const u64 mx = (u64)(p - 1);  // the largest key
-                    kbits = 64 - (u32)__builtin_clzll(mx);
-                }
-            }
+            const u32 C = std::max<u32>(1, std::min<u32>(std::min<u32>(64, cmax), 64 / w));
             h0 = C;
-            R0Bufs r{text, FEd, fac, code, C, w, radix, top, kbits, c->get<u32>("KP", N), a.K2, a.SA, a.K22, a.SA2, a.RK,
-                     c->get<u32>("r0hist", nt * 1024), c->get<u32>("r0tmax", nt), c->get<u32>("r0tmin", nt),
+            R0Bufs r{text, FEd, fac, code, C, w, c->get<u32>("KP", N), a.K2, a.SA, a.K22, a.SA2, a.RK,
+                     c->get<u32>("r0hist", nt * 256), c->get<u32>("r0tmax", nt), c->get<u32>("r0tmin", nt),
                      c->get<u32>("r0cmax", nt), c->get<u32>("r0cmin", nt), c->get<u32>("r0hf", nt * WG)};
             out.r0_chars = C;
-            if (dbg) fprintf(stderr, "[kolm] round 0: %u characters, radix %u (%u-bit codes), %u key bits\n", C, radix, w, kbits);
+            if (dbg) fprintf(stderr, "[kolm] round 0: %u characters of %u bits\n", C, w);
             launch_round0(geo, r, nxt, L.next_cnt, a.blk_split, s, c->kt());
             out.active += N;
             out.rounds = 1;

@@ -311,9 +311,6 @@ struct R0Bufs {
     const u8* code;   // [nb * 256] per-block byte -> code (launch_alpha)
     u32 chars;        // C rotation characters per key
     u32 w;            // bits per code
-    u32 radix;        // > 0: mixed-radix keys (code_0 R^(C-1) + ... + code_(C-1)); 0: w-bit codes
-    u64 top;          // radix^(C-1)
-    u32 bits;         // key bits (C w, or bitlen(R^C - 1))
     u32* KP;   // [N] scratch: high key bits by position (KB)
     u32* K2;   // [N] out: sorted keys (scratch)
     u32* SA;   // [N] out: positions in C-character order (ties by position)
@@ -326,7 +323,7 @@ struct R0Bufs {
 };
 // per-block code tables for round 0 (alphabet compaction), max code width of the batch
 u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w, u32* h_w, bool compact,
-                 hipStream_t s, KTimer* kt = nullptr, u32* sigma = nullptr);
+                 hipStream_t s, KTimer* kt = nullptr);
 void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s,
                    KTimer* kt = nullptr);
 

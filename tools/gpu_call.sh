@@ -49,6 +49,20 @@ for step in "$@"; do
       env $envs KOLM_BENCH_ALLK=1 timeout -k 10 300 python bench.py $QUICK > "$OUT/ab_$tag.json" 2> "$OUT/ab_$tag.err" \
         || { tail -30 "$OUT/ab_$tag.err"; exit 1; }
       echo "[$envs]"; summ "$OUT/ab_$tag.json" ;;
+    run:*)
+      # run:TAG:VAR=v+VAR2=w:bench args (spaces as commas) — bench.py with those settings
+      IFS=: read -r _ tag envs args <<< "$step"
+      env $(echo "$envs" | tr '+' ' ') KOLM_BENCH_ALLK=1 timeout -k 10 300 python bench.py $(echo "$args" | tr ',' ' ') \
+        > "$OUT/run_$tag.json" 2> "$OUT/run_$tag.err" || { tail -30 "$OUT/run_$tag.err"; exit 1; }
+      python3 -c "
+import json;d=json.load(open('$OUT/run_$tag.json'));t=d['detail']
+print('[$tag]', d['value'], d['ms_per_step'], t['parity_blocks'], 'dev', t.get('device_ms'))
+k=t.get('kernels_all_ms_per_step') or {}
+print('  top', dict(sorted(k.items(), key=lambda kv: -kv[1])[:18]))
+c=t.get('configs')
+if c:
+    for n,v in c.items(): print('  ', n, {kk: (vv.get('value'), vv.get('ms_per_call'), vv.get('ms_sa'), vv.get('ms_lz'), vv.get('parity_blocks')) for kk,vv in v.items() if isinstance(vv, dict)})"
+      ;;
     smoke)
       timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
         || { tail -30 "$OUT/smoke.log"; exit 1; }
