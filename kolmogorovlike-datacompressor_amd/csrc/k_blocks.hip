@@ -451,68 +451,12 @@ __device__ inline u64 load8u(const u8* s, u32 x) {
     return ((u64)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
 }
 
-// Cooperative stretches of a long comparison (NW waves; see k_duval_merge): wave w takes
-// every NW-th 2 KiB, the first differences are combined through `red` (LDS).  Every wave of
-// the workgroup calls it with the same arguments (two barriers per stretch).  Returns the
-// first differing offset, or 0xFFFFFFFF with *o advanced past the stretches compared.
-template <int NW>
-__device__ u32 lyn_coop(const u8* s, u32 a0, u32 a1, u32 m, u32 N, u32& o, u32* red, u32* nsteps) {
-    const u32 lane = threadIdx.x & 63;
-    constexpr u32 SPAN = 2048;
-    const u32 wv = threadIdx.x >> 6;
-    while (o + SPAN * NW <= m && (u64)a1 + o + SPAN * NW + 12 <= N) {
-        {
-            u64 d[4];
-#pragma unroll
-            for (u32 k = 0; k < 4; ++k) {
-                const u32 t = o + SPAN * wv + 512 * k + 8 * lane;
-                d[k] = load8u(s, a0 + t) ^ load8u(s, a1 + t);
-            }
-            u32 dpos = 0xFFFFFFFFu;
-#pragma unroll
-            for (u32 k = 0; k < 4; ++k) {  // positions grow with k: the minimum is the first
-                const u64 bal = __ballot(d[k] != 0);
-                const u32 j = bal ? (u32)__ffsll((long long)bal) - 1 : 0u;
-                const u32 dj = (u32)__ffsll((long long)d[k]) - 1;
-                const u32 bj = (u32)__builtin_amdgcn_readlane((int)dj, (int)j) / 8;
-                dpos = min(dpos, bal ? o + SPAN * wv + 512 * k + 8 * j + bj : 0xFFFFFFFFu);
-            }
-            if (lane == 0) red[wv] = dpos;
-            __syncthreads();
-            u32 dm = 0xFFFFFFFFu;
-#pragma unroll
-            for (u32 w2 = 0; w2 < NW; ++w2) dm = min(dm, red[w2]);
-            __syncthreads();
-            if (nsteps) *nsteps += 4;
-            if (dm != 0xFFFFFFFFu) return dm;
-            o += SPAN * NW;
-        }
-    }
-    return 0xFFFFFFFFu;
-}
-
-// The command the merging wave posts for its helper waves (k_duval_merge<NW > 1>).
-struct LynCmd {
-    u32 op;  // 1 = compare (a0, a1, m, o), 2 = exit
-    u32 a0, a1, m, o;
-};
-
 // x = s[a0, a1) < y = s[a1, b1) lexicographically (proper prefix smaller); wave-uniform.
 // 8 bytes per lane per step (512 per wave) while the loads stay inside s[0, N).
-// NW > 1: called by the merging wave 0 only; a comparison long enough for a cooperative
-// stretch is posted to the helper waves (cmd, one barrier) and run by all NW waves.
-template <int NW = 1>
-__device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N, u32* nsteps = nullptr, u32 o0 = 0,
-                         u32* red = nullptr, LynCmd* cmd = nullptr) {
+__device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N, u32* nsteps = nullptr, u32 o0 = 0) {
     const u32 lane = threadIdx.x & 63;
     const u32 la = a1 - a0, lb = b1 - a1, m = min(la, lb);
     u32 o = o0;
-    if (NW > 1 && o + 2048 * NW <= m && (u64)a1 + o + 2048 * NW + 12 <= N) {
-        if (lane == 0) *cmd = LynCmd{1u, a0, a1, m, o};
-        __syncthreads();  // the helpers read the command
-        const u32 dm = lyn_coop<NW>(s, a0, a1, m, N, o, red, nsteps);
-        if (dm != 0xFFFFFFFFu) return s[a0 + dm] < s[a1 + dm];
-    }
     // long common prefixes (periodic data: factors agree on KB): four 512-byte steps per
     // round trip while they lie wholly inside both factors and s[0, N)
     constexpr u32 U = 4;
@@ -605,32 +549,15 @@ __device__ inline Pre shf(const Pre& p, u32 l) {
 // prefix in LDS, so nearly all comparisons are decided in registers.  Only factors that
 // agree on 32 bytes compare the text in global memory: the chain of ~800 dependent
 // comparisons per 1 MiB text block cost ~0.7 us of load latency each.
-// NW > 1 (batches of few blocks, where one block's merge of a periodic region is the
-// critical path): wave 0 merges; waves 1 .. NW-1 only help with the long comparisons — they
-// wait at a barrier for a command (lyn_less<NW> posts one per comparison long enough for a
-// cooperative stretch), run the stretches with wave 0 (lyn_coop), and leave on the exit
-// command.  The stack is wave 0's alone.
-template <int NW>
-__global__ __launch_bounds__(64 * NW) void k_duval_merge(Geom geo, u32 cpb, const u8* s, const u32* fstart,
-                                                         const uint4* fpre, const u32* nfac, u32* stack, u32* fcount,
-                                                         u8* flag, u64* prof) {
+__global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8* s, const u32* fstart,
+                                                    const uint4* fpre, const u32* nfac, u32* stack, u32* fcount,
+                                                    u8* flag, u64* prof) {
     __shared__ u32 lstk[MERGE_LDS];
     __shared__ Pre lpre[PRE_LDS];
     __shared__ u32 lok[PRE_LDS];
-    __shared__ u32 red[NW];
-    __shared__ LynCmd cmd;
-    if (NW > 1 && threadIdx.x >= 64) {  // helper waves
-        for (;;) {
-            __syncthreads();
-            const LynCmd c = cmd;
-            if (c.op != 1) return;
-            u32 o = c.o;
-            lyn_coop<NW>(s, c.a0, c.a1, c.m, (u32)geo.N, o, red, nullptr);
-        }
-    }
     const u64 t0 = prof ? wall_clock64() : 0;
     u32 ncmp = 0, nstep = 0;
-    const u32 b = blockIdx.x, lane = threadIdx.x & 63;
+    const u32 b = blockIdx.x, lane = threadIdx.x;
     const u32 base = geo.base(b), end = geo.end(b);
     // the stack never holds more entries than the span factorisations together: in LDS
     // when they fit (text: a few dozen), else in global memory (e.g. a run: n factors)
@@ -688,8 +615,7 @@ __global__ __launch_bounds__(64 * NW) void k_duval_merge(Geom geo, u32 cpb, cons
                 else if (xok && yok && m <= 32)
                     less = la < lb;
                 else
-                    less = lyn_less<NW>(s, xs, ys, frontier, (u32)geo.N, prof ? &nstep : nullptr, xok && yok ? 32u : 0u,
-                                        red, &cmd);
+                    less = lyn_less(s, xs, ys, frontier, (u32)geo.N, prof ? &nstep : nullptr, xok && yok ? 32u : 0u);
                 if (!less) break;
                 --sp;  // x absorbs y: the merged factor keeps x's start and prefix
                 ys = xs;
@@ -740,12 +666,8 @@ __global__ __launch_bounds__(64 * NW) void k_duval_merge(Geom geo, u32 cpb, cons
         flag[v] = 1;
         if (tot <= MERGE_LDS) stack[base + i] = v;
     }
-    if (NW > 1) {  // release the helpers
-        if (lane == 0) cmd.op = 2;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) fcount[b] = sp;
-    if (prof && threadIdx.x == 0) {
+    if (lane == 0) fcount[b] = sp;
+    if (prof && lane == 0) {
         atomicAdd((unsigned long long*)&prof[11], (unsigned long long)(wall_clock64() - t0));
         atomicMax((unsigned long long*)&prof[12], (unsigned long long)(wall_clock64() - t0));
         atomicAdd((unsigned long long*)&prof[13], (unsigned long long)ncmp);
@@ -862,13 +784,7 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fsta
     }
     {
         KScope k(kt, KT_LYNDON, "k_duval_merge", (u64)nch * 8);
-        // batches of few blocks: 8 waves per block share the long comparisons (KOLM_DUVAL_NW = 1
-        // or 8 forces one form)
-        static const int fw = getenv("KOLM_DUVAL_NW") ? atoi(getenv("KOLM_DUVAL_NW")) : 0;
-        if (fw == 8 || (fw == 0 && geo.nb < 64))
-            k_duval_merge<8><<<geo.nb, 512, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, stack, fcount, flag, dprof_buf());
-        else
-            k_duval_merge<1><<<geo.nb, 64, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, stack, fcount, flag, dprof_buf());
+        k_duval_merge<<<geo.nb, 64, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, stack, fcount, flag, dprof_buf());
     }
     if (u64* prof = dprof_buf()) {
         u64 h[16];

@@ -101,49 +101,11 @@ __device__ inline u64 glob8(const u8* g, u32 x) {
 
 // wave_lcp for long extensions in the stitch (matches of periodic data run to hundreds of
 // KB): 8 bytes per lane, 512 per wave step; where both sides lie in global memory well
-// before `end`, four steps per round trip (loads issued unconditionally, compared after).
-// NW > 1: the NW waves of the workgroup run the stitch's control flow in lockstep (same
-// inputs, same decisions), and every wave of them calls this with the same arguments; the
-// global round trips are then split over the waves (wave w takes every NW-th 2 KiB of the
-// stretch) and their first mismatches combined through `red` (LDS) — NW times the bytes
-// per round trip for the long extensions of periodic data.
-template <int NW = 1>
-__device__ u32 wave_lcp8(const LText& t, u32 p, u32 q, u32 start, u32 maxl, u32 end, u32* red = nullptr) {
+// before `end`, four steps per round trip (loads issued unconditionally, compared after)
+__device__ u32 wave_lcp8(const LText& t, u32 p, u32 q, u32 start, u32 maxl, u32 end) {
     const u32 lane = threadIdx.x & 63;
     constexpr u32 U = 4;
     u32 l = start;
-    if (NW > 1) {
-        // cooperative stretches while the whole stretch lies in global memory before `end`
-        const u32 wv = threadIdx.x >> 6;
-        constexpr u32 SPAN = 512 * U;
-        for (;;) {
-            const u32 hi = max(p, q) + l + SPAN * NW;
-            if (!(min(p, q) + l >= t.hi && hi + 12 <= end && l + SPAN * NW <= maxl)) break;
-            u32 mism = 0xFFFFFFFFu;
-            u64 d[U];
-#pragma unroll
-            for (u32 s2 = 0; s2 < U; ++s2) {
-                const u32 o = l + SPAN * wv + 512 * s2 + 8 * lane;
-                d[s2] = glob8(t.g, p + o) ^ glob8(t.g, q + o);
-            }
-#pragma unroll
-            for (u32 s2 = 0; s2 < U; ++s2) {  // positions grow with s2: the minimum is the first
-                const u64 bal = __ballot(d[s2] != 0);
-                const u32 j = bal ? (u32)__ffsll((long long)bal) - 1 : 0u;
-                const u32 k = (u32)(__ffsll((long long)d[s2]) - 1) >> 3;
-                const u32 kj = (u32)__builtin_amdgcn_readlane((int)k, (int)j);
-                mism = min(mism, bal ? l + SPAN * wv + 512 * s2 + 8 * j + kj : 0xFFFFFFFFu);
-            }
-            if (lane == 0) red[wv] = mism;
-            __syncthreads();
-            u32 m = 0xFFFFFFFFu;
-#pragma unroll
-            for (u32 w2 = 0; w2 < NW; ++w2) m = min(m, red[w2]);
-            __syncthreads();
-            if (m != 0xFFFFFFFFu) return m;
-            l += SPAN * NW;
-        }
-    }
     for (;;) {
         const u32 hi = max(p, q) + l + 512 * U;  // furthest byte this round trip may touch
         if (min(p, q) + l >= t.hi && hi + 12 <= end && l + 512 * U <= maxl) {
@@ -547,9 +509,8 @@ constexpr u32 BF_WIN = LZ_WINDOW + 1024;
 // d0s > 0 (an unresolved token of k_lz_local): every distance below d0s matches fewer than
 // l0s bytes and d0s at least l0s (the local parse's capped answer), so the search starts
 // from d0s's exact length and only tries the distances past it.
-template <int NW>
 __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u32 base, u32 end, u32& out_len,
-                         u32& out_dist, u32& nlong, u32* red, u32 d0s = 0, u32 l0s = 0) {
+                         u32& out_dist, u32& nlong, u32 d0s = 0, u32 l0s = 0) {
     const u32 lane = threadIdx.x & 63;
     out_len = 0;
     out_dist = 0;
@@ -563,14 +524,13 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
         whi = min(end, tlo + BF_WIN);
         const u32 n = whi - tlo;
         __syncthreads();
-        const u32 t0 = threadIdx.x, TS = 64 * NW;  // every wave of the workgroup loads
         if (((uintptr_t)z.text & 3) == 0) {
             const u32* src = reinterpret_cast<const u32*>(z.text + tlo);
             u32* dst = reinterpret_cast<u32*>(win);
-            for (u32 i = t0; i < n / 4; i += TS) dst[i] = src[i];
-            for (u32 i = (n & ~3u) + t0; i < n; i += TS) win[i] = z.text[tlo + i];
+            for (u32 i = lane; i < n / 4; i += 64) dst[i] = src[i];
+            for (u32 i = (n & ~3u) + lane; i < n; i += 64) win[i] = z.text[tlo + i];
         } else {
-            for (u32 i = t0; i < n; i += TS) win[i] = z.text[tlo + i];
+            for (u32 i = lane; i < n; i += 64) win[i] = z.text[tlo + i];
         }
         __syncthreads();
     }
@@ -581,10 +541,10 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
     u32 best = 0, bd = 0;
     if (d0s) {
         const u64 tl0 = z.prof ? wall_clock64() : 0;
-        best = wave_lcp8<NW>(t, q, q - d0s, l0s, maxl, end, red);
+        best = wave_lcp8(t, q, q - d0s, l0s, maxl, end);
         bd = d0s;
         ++nlong;
-        if (z.prof && threadIdx.x == 0) {
+        if (z.prof && lane == 0) {
             atomicAdd(z.prof + 14, wall_clock64() - tl0);
             atomicAdd(z.prof + 15, (u64)best);
         }
@@ -623,7 +583,7 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
             if (bb > capl && (bb >= maxl || t[xj + bb] != t[q + bb])) {
                 if (lane == j) l = capl;  // LCP <= bb: an earlier candidate or `best` wins
             } else {
-                const u32 lj = wave_lcp8<NW>(t, q, xj, capl, maxl, end, red);
+                const u32 lj = wave_lcp8(t, q, xj, capl, maxl, end);
                 if (lane == j) l = lj;
                 bb = max(bb, lj);
                 ++nlong;
@@ -645,17 +605,11 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
     }
 }
 
-// Per block: the true path over the chunk summaries of k_lz_local.  NW = 1: one wave.
-// NW > 1 (batches of few blocks, where the stitch of one periodic block is the critical
-// path): NW waves run the same walk in lockstep and share the long extensions
-// (wave_lcp8<NW>); only wave 0 writes.
-template <int NW>
-__global__ __launch_bounds__(64 * NW) void k_lz_stitch_l(LzArgs z) {
+// Per block (one wave): the true path over the chunk summaries of k_lz_local.
+__global__ __launch_bounds__(64) void k_lz_stitch_l(LzArgs z) {
     __shared__ __align__(16) u8 win[BF_WIN + 16];
-    __shared__ u32 red[NW];
     const u64 tst = z.prof ? wall_clock64() : 0;
-    const u32 b = blockIdx.x, lane = threadIdx.x & 63;
-    const bool w0 = threadIdx.x < 64;  // the writing wave
+    const u32 b = blockIdx.x, lane = threadIdx.x;
     const u32 base = z.geo.base(b), bend = z.geo.end(b);
     const u32 CH = 1u << z.cshift;
     const u32 nck = (bend - base + CH - 1) >> z.cshift;
@@ -687,7 +641,7 @@ __global__ __launch_bounds__(64 * NW) void k_lz_stitch_l(LzArgs z) {
                 spec = by;
                 next = ex;
             } else {
-                if (z.prof && threadIdx.x == 0) atomicAdd(z.prof + 13, (u64)1);
+                if (z.prof && lane == 0) atomicAdd(z.prof + 13, (u64)1);
                 u32 q = entry, jt = 0;
                 bool conv = false;
                 while (q < e) {
@@ -711,12 +665,12 @@ __global__ __launch_bounds__(64 * NW) void k_lz_stitch_l(LzArgs z) {
                     }
                     u32 len, dist;
                     const u64 tb0 = z.prof ? wall_clock64() : 0;
-                    bf_match<NW>(z, win, wlo, whi, q, base, bend, len, dist, nlong, red);
-                    if (z.prof && threadIdx.x == 0) {
+                    bf_match(z, win, wlo, whi, q, base, bend, len, dist, nlong);
+                    if (z.prof && lane == 0) {
                         atomicAdd(z.prof + 8, (u64)1);
                         atomicAdd(z.prof + 9, wall_clock64() - tb0);
                     }
-                    if (threadIdx.x == 0) {
+                    if (lane == 0) {
                         z.fix_pos[base + fi] = q;
                         z.fix_len[base + fi] = len;
                         z.fix_dist[base + fi] = dist;
@@ -737,13 +691,13 @@ __global__ __launch_bounds__(64 * NW) void k_lz_stitch_l(LzArgs z) {
                         const u32 pp = z.tok_pos[li], ol = z.tok_len[li], od = z.tok_dist[li];
                         u32 nl, nd;
                         const u64 tb0 = z.prof ? wall_clock64() : 0;
-                        bf_match<NW>(z, win, wlo, whi, pp, base, bend, nl, nd, nlong, red, od, ol);
-                        if (z.prof && threadIdx.x == 0) {
+                        bf_match(z, win, wlo, whi, pp, base, bend, nl, nd, nlong, od, ol);
+                        if (z.prof && lane == 0) {
                             atomicAdd(z.prof + 10, (u64)1);
                             atomicAdd(z.prof + 11, wall_clock64() - tb0);
                         }
                         spec = spec + tok_bytes(nl, nd) - tok_bytes(ol, od);
-                        if (threadIdx.x == 0) {
+                        if (lane == 0) {
                             z.tok_len[li] = nl;
                             z.tok_dist[li] = nd;
                         }
@@ -766,7 +720,7 @@ __global__ __launch_bounds__(64 * NW) void k_lz_stitch_l(LzArgs z) {
             ntot += nfix + (nt - first);
             entry = next;
         }
-        if (have && w0) {
+        if (have) {
             z.c_first[c] = o_first;
             z.c_fix0[c] = o_fix0;
             z.c_nfix[c] = o_nfix;
@@ -774,8 +728,8 @@ __global__ __launch_bounds__(64 * NW) void k_lz_stitch_l(LzArgs z) {
             z.c_off[c] = o_off;
         }
     }
-    if (z.prof && threadIdx.x == 0) atomicMax((unsigned long long*)(z.prof + 12), (unsigned long long)(wall_clock64() - tst));
-    if (threadIdx.x == 0) {
+    if (z.prof && lane == 0) atomicMax((unsigned long long*)(z.prof + 12), (unsigned long long)(wall_clock64() - tst));
+    if (lane == 0) {
         z.lz_size[b] = boff;
         z.ntok[b] = ntot;
         z.b_nfix[b] = fi;
@@ -847,13 +801,7 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
     }
     {
         KScope k(kt, KT_LZPARSE, "k_lz_stitch", (u64)z.cpb * z.geo.nb * 16);
-        // batches of few blocks: 8 waves per block share the long extensions (KOLM_LZ_STITCH_NW
-        // = 1 or 8 forces one form)
-        static const int fw = getenv("KOLM_LZ_STITCH_NW") ? atoi(getenv("KOLM_LZ_STITCH_NW")) : 0;
-        if (fw == 8 || (fw == 0 && z.geo.nb < 64))
-            k_lz_stitch_l<8><<<z.geo.nb, 512, 0, s>>>(z);
-        else
-            k_lz_stitch_l<1><<<z.geo.nb, 64, 0, s>>>(z);
+        k_lz_stitch_l<<<z.geo.nb, 64, 0, s>>>(z);
     }
 }
 

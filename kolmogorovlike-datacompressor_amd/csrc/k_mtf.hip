@@ -408,13 +408,15 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
 
 // Bytes per MTF chunk: MTF_CHUNK when the batch has chunks enough to fill the GPU; for
 // batches of few blocks (BASELINE configs 2 and 5: 1 and 3 blocks) smaller chunks, down to
-// 128 bytes, so the replay — one thread per chunk, a sequential walk — runs on 8x more
-// threads (the compose then folds 8x more summaries per block, in 8 waves).
+// 128 bytes, so the replay — one thread per chunk, a sequential walk — runs on up to 8x more
+// threads (the compose then folds as many more summaries per block, in 8 waves: 32 blocks
+// at 512 B measured compose 0.35 -> 0.70 ms for replay 0.48 -> 0.44 ms, so the halving
+// stops at 16 K chunks; one gradient block at 128 B: 8.5 -> 6.0 ms per call).
 u32 mtf_chunk_bytes(const Geom& geo) {
     static const u32 force = getenv("KOLM_MTF_CHUNK") ? (u32)atoi(getenv("KOLM_MTF_CHUNK")) : 0u;
     if (force >= 64 && force <= MTF_CHUNK && (force & (force - 1)) == 0) return force;
     u32 csz = MTF_CHUNK;
-    while (csz > 128 && (u64)((geo.bs + csz - 1) / csz) * geo.nb < 65536) csz >>= 1;
+    while (csz > 128 && (u64)((geo.bs + csz - 1) / csz) * geo.nb < 16384) csz >>= 1;
     return csz;
 }
 
