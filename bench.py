@@ -316,6 +316,79 @@ def main():
     parity = {"ok": sum_all(parity_ok, world), "checked": sum_all(parity_checked, world), "blocks": sum_all(nb, world)}
     log(rank, f"[bench] parity {parity}")
 
+    # BASELINE config 4 (256 MiB TOTAL in 1 MiB blocks, round-robin over the GPUs, RCCL
+    # gather to rank 0).  N > 1: the whole config, every rank its shard i = rank (mod N)
+    # of rank 0's stream, gathered asynchronously into rank 0 as in the headline.  N = 1:
+    # what one GPU of the 8-GPU run encodes — the 32 blocks i = 0 (mod 8) — timed alone,
+    # so the per-GPU rate of config 4's shard size is measured beside the 256 MiB one.
+    c4 = None
+    if a.c4_steps > 0 and not a.strong and stream0 is not None:
+        G = world if world > 1 else 8
+        r4 = rank if world > 1 else 0
+        mine4 = list(range(r4, nb_stream, G))
+        n4 = len(mine4) * a.bs  # 1 MiB blocks of a whole-MiB stream: every block full
+        d4 = torch.empty(n4 + 64, dtype=torch.uint8, device="cuda")
+        d4[:n4].copy_(torch.frombuffer(bytearray(b"".join(stream0[i * a.bs:(i + 1) * a.bs] for i in mine4)),
+                                       dtype=torch.uint8))
+        cap4 = n4 + (4 << 20)
+        ar4 = [torch.empty(cap4, dtype=torch.uint8, device="cuda") for _ in range(2)]
+        pend4 = [None, None]
+        cnt4 = [0]
+        sz4 = np.zeros((len(mine4), _lib.KOLM_NCAND), np.uint32)
+        m4 = np.zeros(len(mine4), np.uint32)
+        o4 = np.zeros(len(mine4) + 1, np.uint64)
+
+        def c4_step():
+            j = cnt4[0] % 2
+            cnt4[0] += 1
+            if pend4[j] is not None:
+                pend4[j].wait()
+                pend4[j] = None
+            _lib.check(L.kolm_encode_blocks_device(ctx, d4.data_ptr(), n4, a.bs, _lib.KOLM_HOTPATH_MASK, None,
+                                                   ar4[j].data_ptr(), cap4, sz4.ctypes.data, m4.ctypes.data,
+                                                   o4.ctypes.data, None))
+            if world > 1:
+                ids = torch.from_numpy(m4.astype(np.int32)).cuda()
+                offs = torch.from_numpy(o4.astype(np.int64)).cuda()
+                pend4[j] = gather_payloads(ar4[j], int(o4[-1]), ids, dst=0, async_op=True, offsets=offs)
+
+        def c4_drain():
+            for j in range(2):
+                if pend4[j] is not None:
+                    pend4[j].wait()
+                    pend4[j] = None
+
+        c4_step()
+        c4_drain()
+        drain()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.c4_steps):
+            c4_step()
+        c4_drain()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el4 = sync_max(time.perf_counter() - t0, world)
+        g4 = golden_subset(load_golden_stream(0, a.mib << 20, a.bs), mine4)
+        ok4 = 0
+        if g4:
+            ok4 = check_blocks(g4, sz4, m4, ar4[(cnt4[0] - 1) % 2][:int(o4[-1])].cpu().numpy().tobytes(), o4, 9,
+                               "w9", "sha9")
+        tot4 = sum_all(n4, world)
+        c4 = {"value": round(tot4 * a.c4_steps / el4 / MB, 2), "unit": "MB/s", "steps": a.c4_steps,
+              "ms_per_step": round(el4 / a.c4_steps * 1e3, 3), "blocks_per_gpu": len(mine4),
+              "bytes_per_gpu": n4, "partition": f"round_robin over {G}",
+              "parity_blocks": f"{sum_all(ok4, world)}/{sum_all(len(mine4), world)}" if g4 else None,
+              "note": ("config 4 whole: rank 0's stream, block i on rank i mod N, async RCCL gather (payloads, ids, "
+                       "offsets) to rank 0 inside the timed region") if world > 1 else
+                      ("config 4's per-GPU shard at N = 8 (blocks i = 0 mod 8 of the 256 MiB stream, 32 MiB) on one "
+                       "GPU, no collective; MB/s of this GPU alone")}
+        del d4, ar4
+
+
     # ---- kernel-timed pass (HIP events around every launch) ----
     _lib.check(L.kolm_ctx_set_timing(ctx, 1))
     kt_stats = []
@@ -610,78 +683,6 @@ def main():
                         "copies beside the DMA), the batched device encode, TOC + payloads D2H into a pinned "
                         "container buffer, one copy into the returned bytes; ms_h2d/d2h_pageable: plain torch "
                         "copies of the same bytes for comparison"}
-
-    # BASELINE config 4 (256 MiB TOTAL in 1 MiB blocks, round-robin over the GPUs, RCCL
-    # gather to rank 0).  N > 1: the whole config, every rank its shard i = rank (mod N)
-    # of rank 0's stream, gathered asynchronously into rank 0 as in the headline.  N = 1:
-    # what one GPU of the 8-GPU run encodes — the 32 blocks i = 0 (mod 8) — timed alone,
-    # so the per-GPU rate of config 4's shard size is measured beside the 256 MiB one.
-    c4 = None
-    if a.c4_steps > 0 and not a.strong and stream0 is not None:
-        G = world if world > 1 else 8
-        r4 = rank if world > 1 else 0
-        mine4 = list(range(r4, nb_stream, G))
-        n4 = len(mine4) * a.bs  # 1 MiB blocks of a whole-MiB stream: every block full
-        d4 = torch.empty(n4 + 64, dtype=torch.uint8, device="cuda")
-        d4[:n4].copy_(torch.frombuffer(bytearray(b"".join(stream0[i * a.bs:(i + 1) * a.bs] for i in mine4)),
-                                       dtype=torch.uint8))
-        cap4 = n4 + (4 << 20)
-        ar4 = [torch.empty(cap4, dtype=torch.uint8, device="cuda") for _ in range(2)]
-        pend4 = [None, None]
-        cnt4 = [0]
-        sz4 = np.zeros((len(mine4), _lib.KOLM_NCAND), np.uint32)
-        m4 = np.zeros(len(mine4), np.uint32)
-        o4 = np.zeros(len(mine4) + 1, np.uint64)
-
-        def c4_step():
-            j = cnt4[0] % 2
-            cnt4[0] += 1
-            if pend4[j] is not None:
-                pend4[j].wait()
-                pend4[j] = None
-            _lib.check(L.kolm_encode_blocks_device(ctx, d4.data_ptr(), n4, a.bs, _lib.KOLM_HOTPATH_MASK, None,
-                                                   ar4[j].data_ptr(), cap4, sz4.ctypes.data, m4.ctypes.data,
-                                                   o4.ctypes.data, None))
-            if world > 1:
-                ids = torch.from_numpy(m4.astype(np.int32)).cuda()
-                offs = torch.from_numpy(o4.astype(np.int64)).cuda()
-                pend4[j] = gather_payloads(ar4[j], int(o4[-1]), ids, dst=0, async_op=True, offsets=offs)
-
-        def c4_drain():
-            for j in range(2):
-                if pend4[j] is not None:
-                    pend4[j].wait()
-                    pend4[j] = None
-
-        c4_step()
-        c4_drain()
-        drain()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(a.c4_steps):
-            c4_step()
-        c4_drain()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        el4 = sync_max(time.perf_counter() - t0, world)
-        g4 = golden_subset(load_golden_stream(0, a.mib << 20, a.bs), mine4)
-        ok4 = 0
-        if g4:
-            ok4 = check_blocks(g4, sz4, m4, ar4[(cnt4[0] - 1) % 2][:int(o4[-1])].cpu().numpy().tobytes(), o4, 9,
-                               "w9", "sha9")
-        tot4 = sum_all(n4, world)
-        c4 = {"value": round(tot4 * a.c4_steps / el4 / MB, 2), "unit": "MB/s", "steps": a.c4_steps,
-              "ms_per_step": round(el4 / a.c4_steps * 1e3, 3), "blocks_per_gpu": len(mine4),
-              "bytes_per_gpu": n4, "partition": f"round_robin over {G}",
-              "parity_blocks": f"{sum_all(ok4, world)}/{sum_all(len(mine4), world)}" if g4 else None,
-              "note": ("config 4 whole: rank 0's stream, block i on rank i mod N, async RCCL gather (payloads, ids, "
-                       "offsets) to rank 0 inside the timed region") if world > 1 else
-                      ("config 4's per-GPU shard at N = 8 (blocks i = 0 mod 8 of the 256 MiB stream, 32 MiB) on one "
-                       "GPU, no collective; MB/s of this GPU alone")}
-        del d4, ar4
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -59,6 +59,9 @@ import json;d=json.load(open('$OUT/run_$tag.json'));t=d['detail']
 print('[$tag]', d['value'], d['ms_per_step'], t['parity_blocks'], 'dev', t.get('device_ms'))
 k=t.get('kernels_all_ms_per_step') or {}
 print('  top', dict(sorted(k.items(), key=lambda kv: -kv[1])[:18]))
+for kk in ('config4_shard', 'config4', 'host_e2e'):
+    v=t.get(kk)
+    if v: print('  ', kk, v.get('value'), v.get('ms_per_step', v.get('ms_per_call')), v.get('parity_blocks'), v.get('device_ms_of_call'))
 c=t.get('configs')
 if c:
     for n,v in c.items(): print('  ', n, {kk: (vv.get('value'), vv.get('ms_per_call'), vv.get('ms_sa'), vv.get('ms_lz'), vv.get('parity_blocks')) for kk,vv in v.items() if isinstance(vv, dict)})"
