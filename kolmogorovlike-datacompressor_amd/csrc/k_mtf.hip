@@ -162,7 +162,9 @@ __device__ inline void mtf_apply(u32* st, u8* nst, u32* member, const u8* sm, u3
 // (d = distinct symbols of the range) are the range's own recency summary.  Phase 2: wave
 // 0 chains the range summaries into each range's entry state.  Phase 3: each wave
 // re-walks its range from its entry state and publishes the state at every chunk start.
-constexpr int CW = 8;
+// CW = 8 waves per block; 16 for the small chunks of batches of few blocks (more summaries
+// per block to fold: one gradient / checker block at 128-byte chunks has 8192)
+template <int CW>
 __global__ __launch_bounds__(64 * CW) void k_mtf_compose(ChunkGeom cg, const u8* summary, const u16* scnt,
                                                          u8* states) {
     __shared__ u32 st[CW][64];
@@ -433,7 +435,10 @@ void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summar
     }
     {
         KScope k(kt, KT_MTF, "k_mtf_compose", (u64)nchunks * 512);
-        k_mtf_compose<<<geo.nb, 64 * CW, 0, s>>>(cg, summary, summary_cnt, states);
+        if (csz < MTF_CHUNK)
+            k_mtf_compose<16><<<geo.nb, 64 * 16, 0, s>>>(cg, summary, summary_cnt, states);
+        else
+            k_mtf_compose<8><<<geo.nb, 64 * 8, 0, s>>>(cg, summary, summary_cnt, states);
     }
     {
         KScope k(kt, KT_MTF, "k_mtf_replay", 2 * N + (u64)nchunks * 256);
