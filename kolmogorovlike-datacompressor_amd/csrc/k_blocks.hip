@@ -451,11 +451,15 @@ __device__ inline u64 load8u(const u8* s, u32 x) {
     return ((u64)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
 }
 
-// U steps of 512 bytes per round trip while [o, o + 512 U) lies inside both factors and
-// s[0, N): 1 / 0 when x < y / x > y is decided there, -1 with o advanced past the match
-template <u32 U>
-__device__ inline int lyn_stretch(const u8* s, u32 a0, u32 a1, u32 m, u32 N, u32& o, u32* nsteps) {
+// x = s[a0, a1) < y = s[a1, b1) lexicographically (proper prefix smaller); wave-uniform.
+// 8 bytes per lane per step (512 per wave) while the loads stay inside s[0, N).
+__device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N, u32* nsteps = nullptr, u32 o0 = 0) {
     const u32 lane = threadIdx.x & 63;
+    const u32 la = a1 - a0, lb = b1 - a1, m = min(la, lb);
+    u32 o = o0;
+    // long common prefixes (periodic data: factors agree on KB): four 512-byte steps per
+    // round trip while they lie wholly inside both factors and s[0, N)
+    constexpr u32 U = 4;
     while (o + 512 * U <= m && (u64)a1 + o + 512 * U + 12 <= N) {
         if (nsteps) *nsteps += U;
         u64 d[U];
@@ -471,25 +475,11 @@ __device__ inline int lyn_stretch(const u8* s, u32 a0, u32 a1, u32 m, u32 N, u32
                 const u32 j = (u32)__ffsll((long long)bal) - 1;
                 const u32 dj = (u32)__ffsll((long long)d[k]) - 1;
                 const u32 dpos = o + 512 * k + 8 * j + (u32)__builtin_amdgcn_readlane((int)dj, (int)j) / 8;
-                return s[a0 + dpos] < s[a1 + dpos] ? 1 : 0;
+                return s[a0 + dpos] < s[a1 + dpos];
             }
         }
         o += 512 * U;
     }
-    return -1;
-}
-
-// x = s[a0, a1) < y = s[a1, b1) lexicographically (proper prefix smaller); wave-uniform.
-// 8 bytes per lane per step (512 per wave) while the loads stay inside s[0, N).
-__device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N, u32* nsteps = nullptr, u32 o0 = 0) {
-    const u32 lane = threadIdx.x & 63;
-    const u32 la = a1 - a0, lb = b1 - a1, m = min(la, lb);
-    u32 o = o0;
-    // long common prefixes (periodic data: factors agree on KB): 16 and then 4 512-byte
-    // steps per round trip while they lie wholly inside both factors and s[0, N)
-    int r = lyn_stretch<16>(s, a0, a1, m, N, o, nsteps);
-    if (r < 0) r = lyn_stretch<4>(s, a0, a1, m, N, o, nsteps);
-    if (r >= 0) return r != 0;
     for (; o < m; o += 512) {
         if (nsteps) ++*nsteps;
         const u32 t = o + 8 * lane;

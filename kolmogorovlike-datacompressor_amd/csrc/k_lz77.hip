@@ -101,43 +101,32 @@ __device__ inline u64 glob8(const u8* g, u32 x) {
 
 // wave_lcp for long extensions in the stitch (matches of periodic data run to hundreds of
 // KB): 8 bytes per lane, 512 per wave step; where both sides lie in global memory well
-// before `end`, U steps per round trip (loads issued unconditionally, compared after).
-// lcp_stretch: U steps of 512 bytes per round trip while [l, l + 512 U) lies in global
-// memory before `end`: the first mismatch, or 0xFFFFFFFF with l advanced past the match
-template <u32 U>
-__device__ inline u32 lcp_stretch(const LText& t, u32 p, u32 q, u32& l, u32 maxl, u32 end) {
-    const u32 lane = threadIdx.x & 63;
-    for (;;) {
-        const u32 hi = max(p, q) + l + 512 * U;  // furthest byte this round trip may touch
-        if (!(min(p, q) + l >= t.hi && hi + 12 <= end && l + 512 * U <= maxl)) return 0xFFFFFFFFu;
-        u64 d[U];
-#pragma unroll
-        for (u32 s = 0; s < U; ++s) {
-            const u32 o = l + 512 * s + 8 * lane;
-            d[s] = glob8(t.g, p + o) ^ glob8(t.g, q + o);
-        }
-#pragma unroll
-        for (u32 s = 0; s < U; ++s) {
-            const u64 bal = __ballot(d[s] != 0);
-            if (bal) {
-                const u32 j = (u32)__ffsll((long long)bal) - 1;
-                const u32 k = (u32)(__ffsll((long long)d[s]) - 1) >> 3;
-                return l + 512 * s + 8 * j + (u32)__builtin_amdgcn_readlane((int)k, (int)j);
-            }
-        }
-        l += 512 * U;
-    }
-}
-
+// before `end`, four steps per round trip (loads issued unconditionally, compared after)
 __device__ u32 wave_lcp8(const LText& t, u32 p, u32 q, u32 start, u32 maxl, u32 end) {
     const u32 lane = threadIdx.x & 63;
+    constexpr u32 U = 4;
     u32 l = start;
     for (;;) {
-        // 8 KiB round trips while 8 KiB remain (periodic data: extensions of ~100 KB), then
-        // 2 KiB ones, then single 512-byte steps (LDS window / the end of the block)
-        u32 r = lcp_stretch<16>(t, p, q, l, maxl, end);
-        if (r == 0xFFFFFFFFu) r = lcp_stretch<4>(t, p, q, l, maxl, end);
-        if (r != 0xFFFFFFFFu) return r;
+        const u32 hi = max(p, q) + l + 512 * U;  // furthest byte this round trip may touch
+        if (min(p, q) + l >= t.hi && hi + 12 <= end && l + 512 * U <= maxl) {
+            u64 d[U];
+#pragma unroll
+            for (u32 s = 0; s < U; ++s) {
+                const u32 o = l + 512 * s + 8 * lane;
+                d[s] = glob8(t.g, p + o) ^ glob8(t.g, q + o);
+            }
+#pragma unroll
+            for (u32 s = 0; s < U; ++s) {
+                const u64 bal = __ballot(d[s] != 0);
+                if (bal) {
+                    const u32 j = (u32)__ffsll((long long)bal) - 1;
+                    const u32 k = (u32)(__ffsll((long long)d[s]) - 1) >> 3;
+                    return l + 512 * s + 8 * j + (u32)__builtin_amdgcn_readlane((int)k, (int)j);
+                }
+            }
+            l += 512 * U;
+            continue;
+        }
         const u32 o = l + 8 * lane;
         u32 k = 8;  // first mismatching byte of this lane's 8 (8: none)
         if (o >= maxl) {

@@ -418,28 +418,6 @@ __global__ __launch_bounds__(WG) void k_keygen_small(const Seg* segs, u32 count,
     }
 }
 
-// Dense rounds, all slots at once in slot order: K2[g] = KP[SA[g]] for every slot of the
-// blocks still refining.  Tiles are XCD-contiguous, so the workgroups on one XCD cover about
-// one block at a time and its KP (4 MB per 1 MiB block) stays in that XCD's L2; the per-class
-// keygen (and the tiny sorts' own KP gathers) then read K2 sequentially instead.
-__global__ __launch_bounds__(WG) void k_keygen_dense(SortArgs a) {
-    const u32 g0 = xcd_tile() * TILE, N = (u32)a.geo.N;
-    if (g0 >= N) return;
-    u32 g[PER_THREAD], v[PER_THREAD];
-#pragma unroll
-    for (int j = 0; j < PER_THREAD; ++j) {
-        const u32 x = g0 + j * WG + threadIdx.x;
-        g[j] = x < N && !a.blk_done[a.geo.block_of(x)] ? x : ~0u;
-    }
-#pragma unroll
-    for (int j = 0; j < PER_THREAD; ++j) v[j] = g[j] != ~0u ? a.SA[g[j]] : 0u;
-#pragma unroll
-    for (int j = 0; j < PER_THREAD; ++j) v[j] = g[j] != ~0u ? a.KP[v[j]] : 0u;
-#pragma unroll
-    for (int j = 0; j < PER_THREAD; ++j)
-        if (g[j] != ~0u) a.K2[g[j]] = v[j];
-}
-
 __global__ __launch_bounds__(WG) void k_keygen_large(const LTile* tiles, const LSeg* segs, SortArgs a) {
     const LTile t = tiles[blockIdx.x];
     const LSeg s = segs[t.seg];
@@ -988,9 +966,6 @@ void launch_keypos(const SortArgs& a, u32* KP, hipStream_t s) {
 
 void launch_keygen_small(int c, const Seg* segs, u32 count, const SortArgs& a, hipStream_t s) {
     if (count) k_keygen_small<<<cdiv(count, TILE >> c), WG, 0, s>>>(segs, count, c, a);
-}
-void launch_keygen_dense(const SortArgs& a, hipStream_t s) {
-    if (a.geo.N) k_keygen_dense<<<cdiv((u32)a.geo.N, TILE), WG, 0, s>>>(a);
 }
 void launch_keygen_large(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
                          hipStream_t s) {

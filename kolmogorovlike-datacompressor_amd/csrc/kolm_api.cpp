@@ -470,22 +470,13 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             }
             // algorithmic bytes per element: SA read + key inputs + K2 write
             const u64 per = a.KP ? 12 : a.initial ? (cyclic ? 20 : 11) : (cyclic ? 20 : 12);
-            // KOLM_KEYGEN_DENSE=1: in dense rounds one slot-ordered pass gathers every key
-            // (k_keygen_dense) and the tiny sorts read K2 instead of gathering KP themselves
-            static const bool dense_kg = getenv("KOLM_KEYGEN_DENSE") && atoi(getenv("KOLM_KEYGEN_DENSE")) != 0;
-            const bool kdense = a.KP && dense_kg;
-            if (kdense) {
-                TScope t(c, KOLM_KT_KEYGEN, "k_keygen_dense", N * 12);
-                launch_keygen_dense(a, s);
-                a.KP = nullptr;  // K2 holds every key of the round: the sorts read it
-            }
-            for (int k = 1; k < NCLASS && !kdense; ++k) {
+            for (int k = 1; k < NCLASS; ++k) {
                 if (!h[C_CLS + k]) continue;
                 if (a.KP && k <= tiny_c) continue;  // k_tiny_sort gathers KP itself
                 TScope t(c, KOLM_KT_KEYGEN, "k_keygen_small", (u64)h[C_CLSE + k] * per);
                 launch_keygen_small(k, L.cls[k], h[C_CLS + k], a, s);
             }
-            if (h[C_L0TILE] && !kdense) {
+            if (h[C_L0TILE]) {
                 TScope t(c, KOLM_KT_KEYGEN, "k_keygen_large", (u64)h[C_L0ELEM] * per);
                 launch_keygen_large(lv[0].tiles, h[C_L0TILE], lv[0].segs, a, s);
             }

@@ -278,7 +278,6 @@ void launch_classify(const Seg* cur, u32 ncur, const SortArgs& a, const Lists& L
                      hipStream_t s);
 void launch_keypos(const SortArgs& a, u32* KP, hipStream_t s);
 void launch_keygen_small(int c, const Seg* segs, u32 count, const SortArgs& a, hipStream_t s);
-void launch_keygen_dense(const SortArgs& a, hipStream_t s);  // K2[g] = KP[SA[g]], every slot
 void launch_keygen_large(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
                          hipStream_t s);
 void launch_msd_hist(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
