@@ -73,7 +73,7 @@ if c:
     profile)
       bash tools/gpu_profile.sh "$OUT/prof" || exit 1 ;;
     profile_full)
-      bash tools/gpu_profile.sh "$OUT/prof_full" "--mib 256 --steps 1 --warmup 1 --kt-steps 1 --no-serial-pass --no-cpu-baseline --full-steps 1 --decode-steps 0 --cdc-steps 0 --v2-steps 0 --config-steps 0 --host-steps 0 --c4-steps 0" || exit 1 ;;
+      bash tools/gpu_profile.sh "$OUT/prof_full" "--mib 256 --steps 1 --warmup 1 --kt-steps 1 --no-serial-pass --no-cpu-baseline --full-steps 1 --decode-steps 0 --cdc-steps 0 --v2-steps 0 --config-steps 0 --host-steps 0 --c4-steps 0" stats || exit 1 ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

@@ -11,6 +11,7 @@ export TMPDIR=/tmp
 TICK=$!
 trap "kill $TICK 2>/dev/null" EXIT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python3 bench.py $ARGS > $OUT/kt.log 2>&1 || exit 1
+if [ "$3" = "stats" ]; then echo profile done; exit 0; fi  # kernel stats of the overlapped run only
 KOLM_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kts -o kts --output-format csv -- python3 bench.py $ARGS > $OUT/kts.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o pmc --output-format csv -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o pmc --output-format csv -- python3 bench.py $ARGS > $OUT/write.log 2>&1 || exit 1
