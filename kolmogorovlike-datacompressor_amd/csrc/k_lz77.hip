@@ -505,10 +505,16 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
 // wins, unbounded length) by brute force over the window, from an LDS copy of the text
 // [wlo, whi) refreshed when q's window is not inside it.  One wave.
 constexpr u32 BF_WIN = LZ_WINDOW + 1024;
+// batches of few blocks (BASELINE config 5): a 64 KiB window, so the re-searches of periodic
+// data — candidate checks at q + best and the samples below best, best ~2 KB on the checker
+// BMP — read LDS instead of global memory (one stitch wave per block, nothing else to share
+// the CU with)
+constexpr u32 BF_WIN_BIG = 64 * 1024;
 
 // d0s > 0 (an unresolved token of k_lz_local): every distance below d0s matches fewer than
 // l0s bytes and d0s at least l0s (the local parse's capped answer), so the search starts
 // from d0s's exact length and only tries the distances past it.
+template <u32 WIN>
 __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u32 base, u32 end, u32& out_len,
                          u32& out_dist, u32& nlong, u32 d0s = 0, u32 l0s = 0) {
     const u32 lane = threadIdx.x & 63;
@@ -521,10 +527,20 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
     if (!(wlo <= need && wlo <= whi && (q + 256 <= whi || whi == end))) {
         wlo = need;
         const u32 tlo = need & ~3u;
-        whi = min(end, tlo + BF_WIN);
+        whi = min(end, tlo + WIN);
         const u32 n = whi - tlo;
         __syncthreads();
-        if (((uintptr_t)z.text & 3) == 0) {
+        if (((uintptr_t)z.text & 15) == 0 && WIN > BF_WIN) {  // 16-byte copies (tlo is 4-aligned)
+            const u32 h = (16 - (tlo & 15)) & 15;  // bytes before the first 16-byte source boundary
+            for (u32 i = lane; i < min(h, n); i += 64) win[i] = z.text[tlo + i];
+            const uint4* src = reinterpret_cast<const uint4*>(z.text + tlo + h);
+            for (u32 i = lane; i < (n - min(h, n)) / 16; i += 64) {
+                const uint4 v = src[i];
+                u32* d = reinterpret_cast<u32*>(win + h + 16 * i);  // 4-byte aligned (h and tlo are)
+                d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
+            }
+            for (u32 i = h + ((n - min(h, n)) & ~15u) + lane; i < n; i += 64) win[i] = z.text[tlo + i];
+        } else if (((uintptr_t)z.text & 3) == 0) {
             const u32* src = reinterpret_cast<const u32*>(z.text + tlo);
             u32* dst = reinterpret_cast<u32*>(win);
             for (u32 i = lane; i < n / 4; i += 64) dst[i] = src[i];
@@ -605,9 +621,11 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
     }
 }
 
-// Per block (one wave): the true path over the chunk summaries of k_lz_local.
+// Per block (one wave): the true path over the chunk summaries of k_lz_local.  WIN: the
+// brute-force searches' LDS text window (BF_WIN, or BF_WIN_BIG for batches of few blocks).
+template <u32 WIN>
 __global__ __launch_bounds__(64) void k_lz_stitch_l(LzArgs z) {
-    __shared__ __align__(16) u8 win[BF_WIN + 16];
+    __shared__ __align__(16) u8 win[WIN + 16];
     const u64 tst = z.prof ? wall_clock64() : 0;
     const u32 b = blockIdx.x, lane = threadIdx.x;
     const u32 base = z.geo.base(b), bend = z.geo.end(b);
@@ -665,7 +683,7 @@ __global__ __launch_bounds__(64) void k_lz_stitch_l(LzArgs z) {
                     }
                     u32 len, dist;
                     const u64 tb0 = z.prof ? wall_clock64() : 0;
-                    bf_match(z, win, wlo, whi, q, base, bend, len, dist, nlong);
+                    bf_match<WIN>(z, win, wlo, whi, q, base, bend, len, dist, nlong);
                     if (z.prof && lane == 0) {
                         atomicAdd(z.prof + 8, (u64)1);
                         atomicAdd(z.prof + 9, wall_clock64() - tb0);
@@ -691,7 +709,7 @@ __global__ __launch_bounds__(64) void k_lz_stitch_l(LzArgs z) {
                         const u32 pp = z.tok_pos[li], ol = z.tok_len[li], od = z.tok_dist[li];
                         u32 nl, nd;
                         const u64 tb0 = z.prof ? wall_clock64() : 0;
-                        bf_match(z, win, wlo, whi, pp, base, bend, nl, nd, nlong, od, ol);
+                        bf_match<WIN>(z, win, wlo, whi, pp, base, bend, nl, nd, nlong, od, ol);
                         if (z.prof && lane == 0) {
                             atomicAdd(z.prof + 10, (u64)1);
                             atomicAdd(z.prof + 11, wall_clock64() - tb0);
@@ -801,7 +819,12 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
     }
     {
         KScope k(kt, KT_LZPARSE, "k_lz_stitch", (u64)z.cpb * z.geo.nb * 16);
-        k_lz_stitch_l<<<z.geo.nb, 64, 0, s>>>(z);
+        // KOLM_LZ_BIGWIN = 0 / 1 forces the window; default: 64 KiB below 64 blocks
+        static const int bw = getenv("KOLM_LZ_BIGWIN") ? atoi(getenv("KOLM_LZ_BIGWIN")) : -1;
+        if (bw == 1 || (bw < 0 && z.geo.nb < 64))
+            k_lz_stitch_l<BF_WIN_BIG><<<z.geo.nb, 64, 0, s>>>(z);
+        else
+            k_lz_stitch_l<BF_WIN><<<z.geo.nb, 64, 0, s>>>(z);
     }
 }
 
