@@ -505,11 +505,65 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
 // wins, unbounded length) by brute force over the window, from an LDS copy of the text
 // [wlo, whi) refreshed when q's window is not inside it.  One wave.
 constexpr u32 BF_WIN = LZ_WINDOW + 1024;
-// batches of few blocks (BASELINE config 5): a 64 KiB window, so the re-searches of periodic
+// batches of few blocks (BASELINE config 5): a 62 KiB window, so the re-searches of periodic
 // data — candidate checks at q + best and the samples below best, best ~2 KB on the checker
 // BMP — read LDS instead of global memory (one stitch wave per block, nothing else to share
 // the CU with)
-constexpr u32 BF_WIN_BIG = 64 * 1024;
+// (62 KiB: with the fingerprint array beside it, a 64 KiB window makes this ROCm's gfx950
+// backend emit an invalid V_CMP on src_shared_base — "Operand has incorrect register class")
+constexpr u32 BF_WIN_BIG = 62 * 1024;
+
+// Fingerprint filter of the big-window searches.  A distance can only beat `best` if its
+// match covers [q, q + best]; the sampled byte checks below let through thousands of
+// candidates of periodic text (the checker BMP: runs of 48 equal bytes, period 96) that
+// match for hundreds of bytes and then fail, each one extended by the wave.  With prefix
+// fingerprints H(i) = sum_{hlo <= j < i} t[j] B^(j - hlo) (mod 2^64, B odd) over
+// [q - dmax, q + dmax] in LDS, (H(x + L) - H(x)) B^(q - x) == H(q + L) - H(q) is necessary
+// for t[x, x + L) == t[q, q + L): a candidate that fails it is rejected exactly, one that
+// passes is still extended byte-exactly, so a collision costs time, never the result.
+constexpr u32 HF_N = 2 * LZ_WINDOW + 1;  // H(hlo .. hlo + 2 * dmax)
+constexpr u64 HF_B = 0x9E3779B97F4A7C15ull;
+
+__device__ inline u64 hf_pow(u64 b, u32 e) {
+    u64 r = 1;
+    while (e) {
+        if (e & 1) r *= b;
+        b *= b;
+        e >>= 1;
+    }
+    return r;
+}
+
+// hh[k] = H(hlo + k) for k in [0, n]; one wave: per-lane partial sums over contiguous
+// ranges, an exclusive scan of the scaled partials, then the prefix values.
+__device__ void hf_build(const LText& t, u64* hh, u32 hlo, u32 n) {
+    const u32 lane = threadIdx.x & 63;
+    const u32 per = (n + 63) / 64;
+    const u32 k0 = min(n, lane * per), k1 = min(n, k0 + per);
+    u64 sum = 0, pw = 1;
+    for (u32 k = k0; k < k1; ++k) {
+        sum += (u64)t[hlo + k] * pw;
+        pw *= HF_B;
+    }
+    const u64 w = hf_pow(HF_B, k0);
+    u64 g = sum * w;  // lane's contribution to H, scaled to hlo
+    // exclusive scan over the wave
+    u64 inc = g;
+    for (u32 o = 1; o < 64; o <<= 1) {
+        const u64 v = __shfl_up(inc, o);
+        if (lane >= o) inc += v;
+    }
+    u64 h = inc - g;
+    pw = w;
+    for (u32 k = k0; k < k1; ++k) {
+        hh[k] = h;
+        h += (u64)t[hlo + k] * pw;
+        pw *= HF_B;
+    }
+    if (k1 == n && k0 < k1) hh[n] = h;
+    if (n == 0 && lane == 0) hh[0] = 0;
+    __syncthreads();
+}
 
 // d0s > 0 (an unresolved token of k_lz_local): every distance below d0s matches fewer than
 // l0s bytes and d0s at least l0s (the local parse's capped answer), so the search starts
@@ -517,6 +571,8 @@ constexpr u32 BF_WIN_BIG = 64 * 1024;
 template <u32 WIN>
 __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u32 base, u32 end, u32& out_len,
                          u32& out_dist, u32& nlong, u32 d0s = 0, u32 l0s = 0) {
+    constexpr bool HF = WIN > BF_WIN;  // fingerprint filter
+    __shared__ u64 hh[HF ? HF_N + 1 : 1];
     const u32 lane = threadIdx.x & 63;
     out_len = 0;
     out_dist = 0;
@@ -525,6 +581,7 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
     if (!dmax) return;
     const u32 need = q - dmax;
     if (!(wlo <= need && wlo <= whi && (q + 256 <= whi || whi == end))) {
+        const u64 tr0 = z.prof ? wall_clock64() : 0;
         wlo = need;
         const u32 tlo = need & ~3u;
         whi = min(end, tlo + WIN);
@@ -549,12 +606,19 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
             for (u32 i = lane; i < n; i += 64) win[i] = z.text[tlo + i];
         }
         __syncthreads();
+        if (z.prof && lane == 0) {
+            atomicAdd(z.prof + 24, wall_clock64() - tr0);
+            atomicAdd(z.prof + 26, (u64)1);
+        }
     }
     const LText t{z.text, win, wlo & ~3u, whi};
     const u32 maxl = end - q;
     const u32 capl = min((u32)LZ_CAP, maxl);
     const u8 c0 = t[q], c1 = t[q + 1], c2 = t[q + 2];
     u32 best = 0, bd = 0;
+    const u32 hlo = q - dmax, hn = min(end, q + dmax) - hlo;  // fingerprints over [hlo, hlo + hn]
+    bool hbuilt = false;
+    const u64 blane = HF ? hf_pow(HF_B, lane) : 0;
     if (d0s) {
         const u64 tl0 = z.prof ? wall_clock64() : 0;
         best = wave_lcp8(t, q, q - d0s, l0s, maxl, end);
@@ -565,15 +629,32 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
             atomicAdd(z.prof + 15, (u64)best);
         }
     }
-    // No farther distance beats a match at least dmax - 1 long (Fine and Wilf: a strictly
-    // longer match at d > bd would give the text periods d and bd over the last best + bd
-    // bytes, hence period gcd(d, bd), and then the byte at best would match at bd too).
-    for (u32 d0 = d0s + 1; d0 <= dmax && best < maxl && best + 1 < dmax; d0 += 64) {
+    // No distance d > bd with d - gcd(d, bd) <= best beats the match at bd (Fine and Wilf: a
+    // strictly longer match at d would give t[q - bd, q + best) the periods d and bd, hence
+    // period gcd(d, bd), and then the byte at q + best would match at bd too).  So the scan
+    // starts past best + 1 (gcd >= 1) once a match is known, skips the multiples of bd up to best + bd, and ends
+    // once best + 1 >= dmax.
+    const u64 tlp0 = z.prof ? wall_clock64() : 0;
+    for (u32 d0 = bd ? max(d0s + 1, best + 2) : d0s + 1; d0 <= dmax && best < maxl && best + 1 < dmax;
+         d0 = bd ? max(d0 + 64, best + 2) : d0 + 64) {
         const u32 d = d0 + lane;
         const u32 x = q - d;
         bool ok = d <= dmax && t[x] == c0 && t[x + 1] == c1 && t[x + 2] == c2;
+        if (ok && bd && d <= best + bd) ok = d % bd != 0;
         if (ok && best) ok = best < maxl && t[x + best] == t[q + best];
-        if (ok && best > 2 * LZ_CAP) {
+        if (HF && best > 2 * LZ_CAP) {
+            // inside the loop best + 1 < dmax, so x + best + 1 <= q + best + 1 <= hlo + hn
+            if (!hbuilt) {
+                const u64 th0 = z.prof ? wall_clock64() : 0;
+                hf_build(t, hh, hlo, hn);
+                hbuilt = true;
+                if (z.prof && lane == 0) atomicAdd(z.prof + 23, wall_clock64() - th0);
+            }
+            const u32 L = best + 1;
+            const u64 hq = hh[q + L - hlo] - hh[q - hlo];
+            const u64 bd0 = hf_pow(HF_B, d0);
+            if (ok) ok = (hh[x + L - hlo] - hh[x - hlo]) * (bd0 * blane) == hq;
+        } else if (ok && best > 2 * LZ_CAP) {
             // a longer match agrees everywhere below best: 8 spread samples reject most
             // candidates of periodic text that run out earlier (each would be an
             // extension over KB of text)
@@ -592,6 +673,12 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
         // cannot be strictly longer than the longest one so far (`bb`): that needs a match at
         // bb (periodic text otherwise extends every multiple of its period to the same end)
         u64 longm = __ballot(ok && l >= capl && capl < maxl);
+        const u64 okm = z.prof ? __ballot(ok) : 0;
+        if (z.prof && d0s && lane == 0) {
+            atomicAdd(z.prof + 16, (u64)1);
+            atomicAdd(z.prof + 17, (u64)__popcll(okm));
+            atomicAdd(z.prof + 18, (u64)__popcll(longm));
+        }
         u32 bb = best;
         while (longm) {
             const u32 j = (u32)__ffsll((long long)longm) - 1;
@@ -599,7 +686,14 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
             if (bb > capl && (bb >= maxl || t[xj + bb] != t[q + bb])) {
                 if (lane == j) l = capl;  // LCP <= bb: an earlier candidate or `best` wins
             } else {
+                const u64 te0 = z.prof ? wall_clock64() : 0;
                 const u32 lj = wave_lcp8(t, q, xj, capl, maxl, end);
+                if (z.prof && d0s && lane == 0) {
+                    atomicAdd(z.prof + 19, (u64)1);
+                    atomicAdd(z.prof + 20, (u64)(lj - capl));
+                    atomicAdd(z.prof + 21, wall_clock64() - te0);
+                    atomicAdd(z.prof + 22, (u64)(lj > bb));
+                }
                 if (lane == j) l = lj;
                 bb = max(bb, lj);
                 ++nlong;
@@ -615,6 +709,7 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
         }
         if (best >= maxl || best + 1 >= dmax) break;
     }
+    if (z.prof && d0s && lane == 0) atomicAdd(z.prof + 25, wall_clock64() - tlp0);
     if (best >= (u32)LZ_MIN) {
         out_len = best;
         out_dist = bd;
@@ -819,7 +914,7 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
     }
     {
         KScope k(kt, KT_LZPARSE, "k_lz_stitch", (u64)z.cpb * z.geo.nb * 16);
-        // KOLM_LZ_BIGWIN = 0 / 1 forces the window; default: 64 KiB below 64 blocks
+        // KOLM_LZ_BIGWIN = 0 / 1 forces the window; default: 62 KiB (+ fingerprints) below 64 blocks
         static const int bw = getenv("KOLM_LZ_BIGWIN") ? atoi(getenv("KOLM_LZ_BIGWIN")) : -1;
         if (bw == 1 || (bw < 0 && z.geo.nb < 64))
             k_lz_stitch_l<BF_WIN_BIG><<<z.geo.nb, 64, 0, s>>>(z);

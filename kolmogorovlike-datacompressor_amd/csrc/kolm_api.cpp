@@ -642,14 +642,14 @@ struct Pipeline {
         z.nlong = c->get<u32>("counters", C_N) + C_NLONG;
         z.nfix = c->get<u32>("counters", C_N) + C_NFIX;
         static const bool lz_prof = getenv("KOLM_LZ_PROF") && atoi(getenv("KOLM_LZ_PROF")) != 0;
-        if (lz_prof) z.prof = c->get<u64>("lz_prof", 16);
+        if (lz_prof) z.prof = c->get<u64>("lz_prof", 32);
         return z;
     }
 
     void lz(const LzArgs& z) {
         KOLM_HIP_CHECK(hipMemsetAsync(z.nlong, 0, sizeof(u32), c->active));
         KOLM_HIP_CHECK(hipMemsetAsync(z.nfix, 0, sizeof(u32), c->active));
-        if (z.prof) KOLM_HIP_CHECK(hipMemsetAsync(z.prof, 0, sizeof(u64) * 16, c->active));
+        if (z.prof) KOLM_HIP_CHECK(hipMemsetAsync(z.prof, 0, sizeof(u64) * 32, c->active));
         launch_lz_parse(z, c->active, c->kt());
     }
 };
@@ -1039,7 +1039,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     }
     if (h_off) std::memcpy(h_off, off.data(), sizeof(u64) * (nb + 1));
     if (want_lz && z.prof) {
-        u64 pr[16];
+        u64 pr[32];
         KOLM_HIP_CHECK(hipMemcpy(pr, z.prof, sizeof pr, hipMemcpyDeviceToHost));
         const double nwg = pr[6] ? (double)pr[6] : 1.0;
         fprintf(stderr, "[kolm] k_lz_local us per workgroup: load %.2f sort %.2f index %.2f parse %.2f; "
@@ -1050,6 +1050,12 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
                 "%llu chunks walked token by token, max block %.1f us; re-search exact lengths: %.1f us, %llu bytes\n",
                 (unsigned long long)pr[8], pr[9] / 100.0, (unsigned long long)pr[10], pr[11] / 100.0,
                 (unsigned long long)pr[13], pr[12] / 100.0, pr[14] / 100.0, (unsigned long long)pr[15]);
+        fprintf(stderr, "[kolm] re-search loop: %llu distance batches, %llu candidates, %llu capped, %llu extended "
+                "(%llu longer) over %llu bytes in %.1f us\n", (unsigned long long)pr[16], (unsigned long long)pr[17],
+                (unsigned long long)pr[18], (unsigned long long)pr[19], (unsigned long long)pr[22],
+                (unsigned long long)pr[20], pr[21] / 100.0);
+        fprintf(stderr, "[kolm] re-search phases: loop %.1f us, fingerprints %.1f us, %llu window loads %.1f us\n",
+                pr[25] / 100.0, pr[23] / 100.0, (unsigned long long)pr[26], pr[24] / 100.0);
     }
     u64 tokens = 0;
     for (u32 v : ntok) tokens += v;
