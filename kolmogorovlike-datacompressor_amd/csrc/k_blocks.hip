@@ -531,20 +531,42 @@ __device__ inline int pre_cmp(const Pre& x, const Pre& y, u32 m) {
     return 0;
 }
 
+// The first 32 bytes of the text at x as a Pre (bytes at or past e read as 0: the layout
+// k_duval_span writes to fpre)
+__device__ inline Pre text_pre(const u8* s, u32 x, u32 e) {
+    u32 w[8];
+    if (x + 48 <= e) {
+#pragma unroll
+        for (u32 k = 0; k < 4; ++k) {
+            const u64 v = load8u(s, x + 8 * k);
+            w[2 * k] = __builtin_bswap32((u32)v);
+            w[2 * k + 1] = __builtin_bswap32((u32)(v >> 32));
+        }
+    } else {
+#pragma unroll
+        for (u32 k = 0; k < 8; ++k) {
+            u32 v4 = 0;
+            for (u32 b = 0; b < 4; ++b) {
+                const u32 y = x + 4 * k + b;
+                v4 = (v4 << 8) | (y < e ? s[y] : 0u);
+            }
+            w[k] = v4;
+        }
+    }
+    return Pre{make_uint4(w[0], w[1], w[2], w[3]), make_uint4(w[4], w[5], w[6], w[7])};
+}
+
 __device__ inline u32 rdl(u32 v, u32 l) { return (u32)__builtin_amdgcn_readlane((int)v, l); }
 __device__ inline Pre rdl(const Pre& p, u32 l) {
     return Pre{make_uint4(rdl(p.a.x, l), rdl(p.a.y, l), rdl(p.a.z, l), rdl(p.a.w, l)),
                make_uint4(rdl(p.b.x, l), rdl(p.b.y, l), rdl(p.b.z, l), rdl(p.b.w, l))};
 }
-__device__ inline u32 shf(u32 v, u32 l) { return (u32)__shfl((int)v, (int)l); }
-__device__ inline Pre shf(const Pre& p, u32 l) {
-    return Pre{make_uint4(shf(p.a.x, l), shf(p.a.y, l), shf(p.a.z, l), shf(p.a.w, l)),
-               make_uint4(shf(p.b.x, l), shf(p.b.y, l), shf(p.b.z, l), shf(p.b.w, l))};
-}
 
 // One wave per block merges the span factorisations left to right (stack rule of
-// k_duval_span).  A span's first DUVAL_PF factor starts and 32-byte prefixes arrive in
-// one vector load; the two stack entries under comparison are held in registers (the
+// k_duval_span).  A span's factor starts and 32-byte prefixes arrive 64 at a time, one per
+// lane (the first DUVAL_PF from fpre, the later ones read from the text by their lanes, so
+// spans of many factors — audio, images — do not pay a dependent global round trip per
+// factor); the two stack entries under comparison are held in registers (the
 // one below them is re-read from LDS only after a merge) and every entry keeps its
 // prefix in LDS, so nearly all comparisons are decided in registers.  Only factors that
 // agree on 32 bytes compare the text in global memory: the chain of ~800 dependent
@@ -577,8 +599,11 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
         if (lo >= end) break;
         const u32 hi = min(lo + DUVAL_SPAN, end);
         const u32 nf = nfac[c];
-        // the span's first 64 factor starts and prefixes, one per lane
-        const u32 vst = lane < nf ? fstart[lo + lane] : hi;
+        // factors g0 .. g0 + 63 of the span: start, next start (or hi), prefix — one per lane
+        static_assert(DUVAL_PF == 64, "group 0 of the span comes from fpre");
+        u32 g0 = 0;
+        u32 vst = lane < nf ? fstart[lo + lane] : hi;
+        u32 vnx = lane + 1 < nf ? fstart[lo + lane + 1] : hi;
         Pre vpr{};
         if (lane < nf) {
             vpr.a = fpre[((u64)c * DUVAL_PF + lane) * 2];
@@ -586,10 +611,17 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
         }
         u32 t = 0;
         while (t < nf) {
-            const u32 cached = t < DUVAL_PF ? 1u : 0u;
-            const u32 r = cached ? rdl(vst, t) : fstart[lo + t];
-            const u32 frontier = t + 1 >= nf ? hi : t + 1 < DUVAL_PF ? rdl(vst, t + 1) : fstart[lo + t + 1];
-            const Pre rp = cached ? rdl(vpr, t) : Pre{};
+            if (t - g0 >= 64) {
+                g0 += 64;
+                const u32 gi = g0 + lane;
+                vst = gi < nf ? fstart[lo + gi] : hi;
+                vnx = gi + 1 < nf ? fstart[lo + gi + 1] : hi;
+                if (gi < nf) vpr = text_pre(s, vst, end);
+            }
+            const u32 cached = 1u;
+            const u32 r = rdl(vst, t - g0);
+            const u32 frontier = rdl(vnx, t - g0);
+            const Pre rp = rdl(vpr, t - g0);
             if (lane == 0) {
                 stk[sp] = r;
                 if (sp < PRE_LDS) {
@@ -635,27 +667,25 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
             ++t;
             if (!merged) break;
         }
-        // remaining right factors cannot merge: append in bulk
+        // remaining right factors cannot merge: append in bulk (prefixes of the entries that
+        // land in the LDS prefix cache read from the text, lane-parallel)
         for (u32 o = t; o < nf; o += 64) {
             const u32 idx = o + lane;
-            // shuffles with every lane active (a source lane may be past nf)
-            const Pre pv = shf(vpr, idx & 63);
-            const u32 sv = shf(vst, idx & 63);
             if (idx < nf) {
                 const u32 d = sp + (idx - t);
-                stk[d] = idx < DUVAL_PF ? sv : fstart[lo + idx];
+                const u32 sv = fstart[lo + idx];
+                stk[d] = sv;
                 if (d < PRE_LDS) {
-                    lok[d] = idx < DUVAL_PF ? 1u : 0u;
-                    lpre[d] = pv;
+                    lok[d] = 1u;
+                    lpre[d] = text_pre(s, sv, end);
                 }
             }
         }
         if (t < nf) {
             sp += nf - t;
-            const u32 l = nf - 1;  // the new top
-            top = l < DUVAL_PF ? rdl(vst, l) : fstart[lo + l];
-            tok = l < DUVAL_PF ? 1u : 0u;
-            if (tok) tpre = rdl(vpr, l);
+            top = fstart[lo + nf - 1];  // the new top
+            tok = 1u;
+            tpre = text_pre(s, top, end);
         }
         __builtin_amdgcn_s_waitcnt(0);
     }

@@ -540,11 +540,8 @@ __device__ void hf_build(const LText& t, u64* hh, u32 hlo, u32 n) {
     const u32 lane = threadIdx.x & 63;
     const u32 per = (n + 63) / 64;
     const u32 k0 = min(n, lane * per), k1 = min(n, k0 + per);
-    u64 sum = 0, pw = 1;
-    for (u32 k = k0; k < k1; ++k) {
-        sum += (u64)t[hlo + k] * pw;
-        pw *= HF_B;
-    }
+    u64 sum = 0;
+    for (u32 k = k1; k > k0; --k) sum = sum * HF_B + t[hlo + k - 1];  // Horner
     const u64 w = hf_pow(HF_B, k0);
     u64 g = sum * w;  // lane's contribution to H, scaled to hlo
     // exclusive scan over the wave
@@ -553,8 +550,7 @@ __device__ void hf_build(const LText& t, u64* hh, u32 hlo, u32 n) {
         const u64 v = __shfl_up(inc, o);
         if (lane >= o) inc += v;
     }
-    u64 h = inc - g;
-    pw = w;
+    u64 h = inc - g, pw = w;
     for (u32 k = k0; k < k1; ++k) {
         hh[k] = h;
         h += (u64)t[hlo + k] * pw;
@@ -618,7 +614,9 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
     u32 best = 0, bd = 0;
     const u32 hlo = q - dmax, hn = min(end, q + dmax) - hlo;  // fingerprints over [hlo, hlo + hn]
     bool hbuilt = false;
-    const u64 blane = HF ? hf_pow(HF_B, lane) : 0;
+    const u64 blane = HF ? hf_pow(HF_B, lane) : 0, b64 = HF ? hf_pow(HF_B, 64) : 0;
+    u32 hd0 = 0;   // distance whose power hbd0 holds
+    u64 hbd0 = 1;
     if (d0s) {
         const u64 tl0 = z.prof ? wall_clock64() : 0;
         best = wave_lcp8(t, q, q - d0s, l0s, maxl, end);
@@ -639,10 +637,13 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
          d0 = bd ? max(d0 + 64, best + 2) : d0 + 64) {
         const u32 d = d0 + lane;
         const u32 x = q - d;
-        bool ok = d <= dmax && t[x] == c0 && t[x + 1] == c1 && t[x + 2] == c2;
-        if (ok && bd && d <= best + bd) ok = d % bd != 0;
-        if (ok && best) ok = best < maxl && t[x + best] == t[q + best];
-        if (HF && best > 2 * LZ_CAP) {
+        // fingerprint mode: a lane passes iff t[x, x + best] fingerprints equal to t[q, q + best]
+        // (which covers the 3-gram, the byte at best and the Fine-Wilf exclusions); a passing
+        // lane is then extended from 0 by the wave, so a collision cannot change the result
+        const bool hfm = HF && best > 2 * LZ_CAP;
+        bool ok;
+        u32 l = 0;
+        if (hfm) {
             // inside the loop best + 1 < dmax, so x + best + 1 <= q + best + 1 <= hlo + hn
             if (!hbuilt) {
                 const u64 th0 = z.prof ? wall_clock64() : 0;
@@ -650,11 +651,20 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
                 hbuilt = true;
                 if (z.prof && lane == 0) atomicAdd(z.prof + 23, wall_clock64() - th0);
             }
+            if (d0 != hd0) {
+                hbd0 = d0 == hd0 + 64 ? hbd0 * b64 : hf_pow(HF_B, d0);
+                hd0 = d0;
+            }
             const u32 L = best + 1;
             const u64 hq = hh[q + L - hlo] - hh[q - hlo];
-            const u64 bd0 = hf_pow(HF_B, d0);
-            if (ok) ok = (hh[x + L - hlo] - hh[x - hlo]) * (bd0 * blane) == hq;
-        } else if (ok && best > 2 * LZ_CAP) {
+            ok = d <= dmax && (hh[x + L - hlo] - hh[x - hlo]) * (hbd0 * blane) == hq;
+            if (ok) l = capl;
+        } else {
+            ok = d <= dmax && t[x] == c0 && t[x + 1] == c1 && t[x + 2] == c2;
+            if (ok && bd && d <= best + bd) ok = d % bd != 0;
+            if (ok && best) ok = best < maxl && t[x + best] == t[q + best];
+        }
+        if (!hfm && ok && best > 2 * LZ_CAP) {
             // a longer match agrees everywhere below best: 8 spread samples reject most
             // candidates of periodic text that run out earlier (each would be an
             // extension over KB of text)
@@ -664,8 +674,7 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
                 ok = ok && t[x + y] == t[q + y];
             }
         }
-        u32 l = 0;
-        if (ok) {
+        if (ok && !hfm) {
             l = LZ_MIN;
             while (l < capl && t[x + l] == t[q + l]) ++l;
         }
@@ -687,7 +696,7 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
                 if (lane == j) l = capl;  // LCP <= bb: an earlier candidate or `best` wins
             } else {
                 const u64 te0 = z.prof ? wall_clock64() : 0;
-                const u32 lj = wave_lcp8(t, q, xj, capl, maxl, end);
+                const u32 lj = wave_lcp8(t, q, xj, hfm ? 0u : capl, maxl, end);
                 if (z.prof && d0s && lane == 0) {
                     atomicAdd(z.prof + 19, (u64)1);
                     atomicAdd(z.prof + 20, (u64)(lj - capl));

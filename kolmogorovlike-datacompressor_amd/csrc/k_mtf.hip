@@ -406,7 +406,113 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
     }
 }
 
+// Position-parallel replay for batches of few blocks: one wave per chunk, 64 bytes per step
+// with one lane per byte, from the chunk's entry state S (k_mtf_compose).  With Seen = the
+// distinct symbols of the chunk before byte i (most recent first), MTF's list before i is
+// Seen ++ (S minus Seen), so byte i = s gets
+//   * if s occurred before in the chunk (last at p): the number of distinct symbols in (p, i);
+//   * else: |Seen| + pos_S(s) - #{u in Seen : pos_S(u) < pos_S(s)}.
+// Per step the lanes of each distinct symbol are found with one ballot per symbol (the
+// symbol's class mask E); two passes over the classes give p, the window counts, |Seen| and
+// the rank term; the state then moves to the step's recency summary ++ the rest (mtf_apply).
+// No lane walks the list, so deep indices (images, audio: the gradient BMP's BBWT has most
+// indices past 8) cost the same as shallow ones, and a 1 MiB block runs on 1024 waves
+// instead of 8192 sequential 128-byte walks.
+__global__ __launch_bounds__(256) void k_mtf_wave(ChunkGeom cg, const u8* in, const u8* states, u8* out,
+                                                  u32 nchunks, u64* bits, int rice_k) {
+    __shared__ u32 st[4][64];
+    __shared__ u8 nst[4][256];
+    __shared__ u32 member[4][8];
+    __shared__ u8 inv[4][256];  // position of each symbol in the current state
+    __shared__ u8 smy[4][64];   // the step's recency summary
+    __shared__ __align__(8) u8 mb[4][64];  // the step's output bytes (bit-plane groups)
+    const u32 w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const u32 c = blockIdx.x * 4 + w;
+    u32 lo = 0, hi = 0;
+    if (!(c < nchunks && cg.range(c, lo, hi))) return;  // whole waves (wave-level sync only)
+    {
+        const u32 word = reinterpret_cast<const u32*>(states + (u64)c * 256)[lane];
+        st[w][lane] = word;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) inv[w][(word >> (8 * j)) & 0xFF] = (u8)(4 * lane + j);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    RiceAcc acc;
+    acc.k = rice_k;
+    const u64 below = (1ull << lane) - 1ull;  // lanes before this one
+    for (u32 p = lo; p < hi; p += 64) {
+        const u32 i = p + lane;
+        const bool v = i < hi;
+        const u32 sym = v ? in[i] : 0u;
+        const u64 vm = __ballot(v);
+        const u32 mypos = inv[w][sym];
+        // pass 1: this lane's class (lanes holding the same symbol)
+        u64 rem = vm, mine = 0;
+        while (rem) {
+            const u32 k = (u32)__ffsll((long long)rem) - 1;
+            const u32 sk = __builtin_amdgcn_readlane(sym, k);
+            const u64 eq = __ballot(v && sym == sk);
+            if (sym == sk) mine = eq;
+            rem &= ~eq;
+        }
+        const u64 pm = mine & below;  // earlier lanes with my symbol
+        const u32 prev = pm ? 63u - (u32)__clzll((long long)pm) : 0u;
+        const u64 win = pm ? below & ~((2ull << prev) - 1ull) : 0ull;  // lanes in (prev, lane)
+        // pass 2: distinct symbols in the window / before this lane, and their state ranks
+        u32 cnt = 0, seen = 0, less = 0;
+        rem = vm;
+        while (rem) {
+            const u32 k = (u32)__ffsll((long long)rem) - 1;  // the class's first lane
+            const u32 sk = __builtin_amdgcn_readlane(sym, k);
+            const u32 pk = __builtin_amdgcn_readlane(mypos, k);
+            const u64 eq = __ballot(v && sym == sk);
+            cnt += (eq & win) ? 1u : 0u;
+            if (k < lane) {
+                ++seen;
+                less += pk < mypos ? 1u : 0u;
+            }
+            rem &= ~eq;
+        }
+        const u32 m = pm ? cnt : seen + mypos - less;
+        if (v) out[i] = (u8)m;
+        mb[w][lane] = v ? (u8)m : (u8)0;
+        if (bits && v) acc.add(m);
+        // recency summary of the step: last lanes of each symbol, most recent first
+        const bool last = v && (mine >> lane) == 1ull;
+        const u64 lm = __ballot(last);
+        if (last) smy[w][__popcll(lm >> lane) - 1] = (u8)sym;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (bits && (lane & 7) == 0 && v) {
+            const u32* g = reinterpret_cast<const u32*>(&mb[w][lane]);
+            acc.group(g[0], g[1]);  // (a short last group reads the zeroed lanes)
+        }
+        mtf_apply(st[w], nst[w], member[w], smy[w], (u32)__popcll(lm));
+        const u32 word = st[w][lane];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) inv[w][(word >> (8 * j)) & 0xFF] = (u8)(4 * lane + j);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (bits) {
+        u64* dst = bits + (u64)(c / cg.cpb) * 8;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const u32 sum = wave_reduce(acc.c[q], OpAddU(), 0u);
+            if (lane == 0 && sum) atomicAdd((unsigned long long*)&dst[q], (unsigned long long)sum);
+        }
+    }
+}
+
 }  // namespace
+
+// The position-parallel replay (k_mtf_wave, 1 KiB chunks) for batches of few blocks;
+// KOLM_MTF_WAVE = 0 / 1 forces it off / on.
+bool mtf_wave_mode(const Geom& geo) {
+    static const int force = getenv("KOLM_MTF_WAVE") ? atoi(getenv("KOLM_MTF_WAVE")) : -1;
+    return force >= 0 ? force != 0 : geo.nb < 64;
+}
 
 // Bytes per MTF chunk: MTF_CHUNK when the batch has chunks enough to fill the GPU; for
 // batches of few blocks (BASELINE configs 2 and 5: 1 and 3 blocks) smaller chunks, down to
@@ -418,6 +524,7 @@ u32 mtf_chunk_bytes(const Geom& geo) {
     static const u32 force = getenv("KOLM_MTF_CHUNK") ? (u32)atoi(getenv("KOLM_MTF_CHUNK")) : 0u;
     if (force >= 64 && force <= MTF_CHUNK && (force & (force - 1)) == 0) return force;
     u32 csz = MTF_CHUNK;
+    if (mtf_wave_mode(geo)) return csz;
     while (csz > 128 && (u64)((geo.bs + csz - 1) / csz) * geo.nb < 16384) csz >>= 1;
     return csz;
 }
@@ -435,12 +542,15 @@ void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summar
     }
     {
         KScope k(kt, KT_MTF, "k_mtf_compose", (u64)nchunks * 512);
-        if (csz < MTF_CHUNK)
+        if (csz < MTF_CHUNK || geo.nb < 64)
             k_mtf_compose<16><<<geo.nb, 64 * 16, 0, s>>>(cg, summary, summary_cnt, states);
         else
             k_mtf_compose<8><<<geo.nb, 64 * 8, 0, s>>>(cg, summary, summary_cnt, states);
     }
-    {
+    if (mtf_wave_mode(geo)) {
+        KScope k(kt, KT_MTF, "k_mtf_wave", 2 * N + (u64)nchunks * 256);
+        k_mtf_wave<<<(nchunks + 3) / 4, 256, 0, s>>>(cg, in, states, out, nchunks, bits, rice_k);
+    } else {
         KScope k(kt, KT_MTF, "k_mtf_replay", 2 * N + (u64)nchunks * 256);
         k_mtf_replay<<<(nchunks + RT - 1) / RT, RT, 0, s>>>(cg, in, states, out, nchunks, bits, rice_k);
     }

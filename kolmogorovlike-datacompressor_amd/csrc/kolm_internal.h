@@ -330,6 +330,7 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
 // ---- k_mtf.hip ----
 // bits (optional, [nb * 8], zeroed by the caller): the replay also adds each block's Rice-k
 // bit counts of the 5 BBWT candidates (counters 0..4, see k_entropy.hip) — no extra pass
+bool mtf_wave_mode(const Geom& geo);  // position-parallel MTF replay (batches of few blocks)
 u32 mtf_chunk_bytes(const Geom& geo);  // bytes per MTF chunk of this batch (launch_mtf's choice)
 void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summary_cnt, u8* states,
                 hipStream_t s, KTimer* kt = nullptr, u64* bits = nullptr, int rice_k = 2);

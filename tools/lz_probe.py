@@ -47,7 +47,7 @@ def main():
     sd = st.as_dict()
     print(kind, part, len(data), "stats", {k: v for k, v in sd.items() if k != "kernels"}, "methods", m.tolist())
     kt = _lib.kernel_times(ctx)
-    for k, v in sorted(kt.items(), key=lambda kv: -kv[1]["ms"])[:10]:
+    for k, v in sorted(kt.items(), key=lambda kv: -kv[1]["ms"])[:40]:
         print(f"  {k:32s} {v['ms']:8.3f} {v['launches']}")
 
 
