@@ -236,8 +236,12 @@ __device__ inline int seg_class(const SortArgs& a, const Seg* cur, u32 ncur, u32
 // MODE 0: all segments placed by per-workgroup reservations (list order arbitrary).
 // MODE 1: counts as MODE 0 plus per-(class, bin) counts; only the large segments are written.
 // MODE 2: small segments placed at their bin's offset (after k_bin_scan).
+// ncur_dev (when set): the list's length as the previous round left it in device memory, so
+// the host does not wait for the round's end to launch the next one (the grid covers a bound)
 template <int MODE>
-__global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur, SortArgs a, Lists L, Level lv, Bins bn) {
+__global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur_in, const u32* ncur_dev, SortArgs a,
+                                                  Lists L, Level lv, Bins bn) {
+    const u32 ncur = ncur_dev ? *ncur_dev : ncur_in;
     __shared__ u32 lcnt[NCLASS + 1], lbase[NCLASS + 1], lel[NCLASS + 1], lcur[NCLASS + 1];
     __shared__ u32 lact, ltiles, ltb;
     const u32 tid = threadIdx.x, lane = tid & 63;
@@ -940,19 +944,20 @@ void launch_iota(u32* SA, u64 N, hipStream_t s) {
 void launch_block_segs(Seg* segs, const Geom& geo, hipStream_t s) {
     if (geo.nb) k_block_segs<<<cdiv(geo.nb, 256), 256, 0, s>>>(segs, geo);
 }
-void launch_classify(const Seg* cur, u32 ncur, const SortArgs& a, const Lists& L, const Level& lv0,
-                     hipStream_t s) {
-    if (ncur) k_classify<0><<<std::min<u32>(cdiv(ncur, 256), 2048u), 256, 0, s>>>(cur, ncur, a, L, lv0, Bins{});
+void launch_classify(const Seg* cur, u32 ncur, const u32* ncur_dev, const SortArgs& a, const Lists& L,
+                     const Level& lv0, hipStream_t s) {
+    if (ncur)
+        k_classify<0><<<std::min<u32>(cdiv(ncur, 256), 2048u), 256, 0, s>>>(cur, ncur, ncur_dev, a, L, lv0, Bins{});
 }
-void launch_classify_bins(const Seg* cur, u32 ncur, const SortArgs& a, const Lists& L, const Level& lv0,
-                          const Bins& bn, hipStream_t s) {
+void launch_classify_bins(const Seg* cur, u32 ncur, const u32* ncur_dev, const SortArgs& a, const Lists& L,
+                          const Level& lv0, const Bins& bn, hipStream_t s) {
     if (!ncur) return;
     const u32 grid = std::min<u32>(cdiv(ncur, 256), 2048u);
     KOLM_HIP_CHECK(hipMemsetAsync(bn.cnt, 0, sizeof(u32) * NCLASS * CLS_NBIN, s));
     KOLM_HIP_CHECK(hipMemsetAsync(bn.fill, 0, sizeof(u32) * NCLASS * CLS_NBIN, s));
-    k_classify<1><<<grid, 256, 0, s>>>(cur, ncur, a, L, lv0, bn);
+    k_classify<1><<<grid, 256, 0, s>>>(cur, ncur, ncur_dev, a, L, lv0, bn);
     k_bin_scan<<<NCLASS, 256, 0, s>>>(bn);
-    k_classify<2><<<grid, 256, 0, s>>>(cur, ncur, a, L, lv0, bn);
+    k_classify<2><<<grid, 256, 0, s>>>(cur, ncur, ncur_dev, a, L, lv0, bn);
 }
 void launch_keypos(const SortArgs& a, u32* KP, hipStream_t s) {
     if (!a.geo.N) return;

@@ -346,7 +346,11 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
         L.cls[k] = c->get<Seg>(nm, cap);
     }
     L.cls_cnt = cnt + C_CLS;
-    L.next_cnt = cnt + C_NEXT;
+    // the next list's length, double-buffered in device memory: round r appends to slot
+    // r & 1 while its classify reads slot (r - 1) & 1, so the host launches round r + 1
+    // without waiting for round r's count (the classify grid covers a bound instead)
+    u32* ncnt = c->get<u32>("next_cnt2", 2);
+    const u32* ncur_dev = nullptr;
     L.eq_cnt = cnt + C_EQ;
     L.misc = cnt + C_ACTIVE;
     L.cls_elems = cnt + C_CLSE;
@@ -397,6 +401,8 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
         // round 0: packed characters (cyclic 32 bits, linear 27); later: ranks (+1 linear)
         a.key_bits = a.initial ? (cyclic ? 32u : 27u) : bitlen(cyclic ? geo.bs - 1 : geo.bs);
         L.next = nxt;
+        L.next_cnt = ncnt + (round & 1);
+        KOLM_HIP_CHECK(hipMemsetAsync(L.next_cnt, 0, sizeof(u32), s));
         KOLM_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(u32) * C_STATUS, s));
         KOLM_HIP_CHECK(hipMemsetAsync(cnt + C_CLSE, 0, sizeof(u32) * (C_N - C_CLSE), s));
         KOLM_HIP_CHECK(hipMemsetAsync(a.blk_split, 0, sizeof(u32) * geo.nb, s));
@@ -420,14 +426,13 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             out.active += N;
             out.rounds = 1;
             launch_update_done(blk_done, a.blk_split, geo.nb, 0, s);
-            KOLM_HIP_CHECK(hipMemcpyAsync(h + C_NEXT, cnt + C_NEXT, sizeof(u32), hipMemcpyDeviceToHost, s));
             if (after_round0) {
                 after_round0();
                 c->active = s;
             }
-            c->sync();
             round_done(round);
-            ncur = h[C_NEXT];
+            ncur = (u32)std::min<u64>(N / 2 + geo.nb, 0xFFFFFFFFu);  // bound: segments hold >= 2
+            ncur_dev = L.next_cnt;
             std::swap(cur, nxt);
             continue;
         }
@@ -439,10 +444,10 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
                 const u32 nbits = bitlen((u32)(N - 1));
                 const Bins bn{c->get<u32>("cls_bins", NCLASS * CLS_NBIN), c->get<u32>("cls_fill", NCLASS * CLS_NBIN),
                               nbits > 10 ? nbits - 10 : 0u};
-                launch_classify_bins(cur, ncur, a, L, lv[0], bn, s);
+                launch_classify_bins(cur, ncur, ncur_dev, a, L, lv[0], bn, s);
                 a.xcd = 1;
             } else {
-                launch_classify(cur, ncur, a, L, lv[0], s);
+                launch_classify(cur, ncur, ncur_dev, a, L, lv[0], s);
                 a.xcd = 0;
             }
         }
@@ -519,10 +524,8 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             hi = shift;
             ++lvl;
         }
-        if (lvl) {  // the MSD levels appended segments to the class lists: fresh counts
-            KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
-            c->sync();
-        }
+        // (after MSD levels h holds the counts their last level read back: the class lists
+        // they appended to are complete)
         // per element: K2 + SA read, SA + RK write (16 B); per segment record 8 B
         for (int k = 0; k < NCLASS; ++k) {
             if (!h[C_CLS + k]) continue;
@@ -543,10 +546,10 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             launch_finalize_eq(L.eq, h[C_EQ], a, L, s);
         }
         if (cyclic) launch_update_done(blk_done, a.blk_split, geo.nb, round, s);
-        KOLM_HIP_CHECK(hipMemcpyAsync(h + C_NEXT, cnt + C_NEXT, sizeof(u32), hipMemcpyDeviceToHost, s));
-        c->sync();
         round_done(round);
-        ncur = h[C_NEXT];
+        // the next list holds unresolved segments of >= 2 active elements each
+        ncur = (u32)std::min<u64>(h[C_ACTIVE] / 2 + geo.nb, N / 2 + geo.nb);
+        ncur_dev = L.next_cnt;
         std::swap(cur, nxt);
     }
     if (cyclic) launch_rounds_sum(blk_done, geo.nb, out.rounds, c->get<u64>("rsum", 1), s);
