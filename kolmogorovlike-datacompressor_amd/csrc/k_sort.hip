@@ -439,8 +439,11 @@ __global__ __launch_bounds__(WG) void k_keygen_large(const LTile* tiles, const L
 // ------------------------------------------------------------------------------------
 // MSD radix passes for segments longer than a tile
 // ------------------------------------------------------------------------------------
+// MSD kernels: ndev (when set) is the level's tile / segment count in device memory and
+// the grid a bound on it (levels after the first are launched without a host round trip)
 __global__ __launch_bounds__(WG) void k_msd_hist(const LTile* tiles, const LSeg* segs, SortArgs a,
-                                                 u32 shift, u32 mask, u32* hist) {
+                                                 u32 shift, u32 mask, u32* hist, const u32* ndev) {
+    if (ndev && blockIdx.x >= *ndev) return;
     __shared__ u32 h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
@@ -461,7 +464,8 @@ __global__ __launch_bounds__(WG) void k_msd_hist(const LTile* tiles, const LSeg*
 // starts, and classification of the buckets (small -> class list, large -> next level,
 // large after the last digit -> equal-key run).
 __global__ __launch_bounds__(WG) void k_msd_scan(const LSeg* segs, SortArgs a, u32* hist, int last_level,
-                                                 Lists L, Level nx) {
+                                                 Lists L, Level nx, const u32* ndev) {
+    if (ndev && blockIdx.x >= *ndev) return;
     __shared__ u32 sh[WG / 64];
     const LSeg s = segs[blockIdx.x];
     const u32 d = threadIdx.x;
@@ -543,7 +547,8 @@ __global__ __launch_bounds__(WG) void k_msd_scan(const LSeg* segs, SortArgs a, u
 // each wave ranks its 64 elements per digit with ballots; per-wave digit counts are
 // combined through LDS in (j, wave) order, so equal digits keep their tile order.
 __global__ __launch_bounds__(WG) void k_msd_scatter(const LTile* tiles, const LSeg* segs, SortArgs a,
-                                                    u32 shift, u32 width, const u32* hist) {
+                                                    u32 shift, u32 width, const u32* hist, const u32* ndev) {
+    if (ndev && blockIdx.x >= *ndev) return;
     __shared__ u32 wcnt[WG / 64][256];
     __shared__ u32 running[256];
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -594,7 +599,9 @@ __global__ __launch_bounds__(WG) void k_msd_scatter(const LTile* tiles, const LS
     }
 }
 
-__global__ __launch_bounds__(WG) void k_copy_back(const LTile* tiles, const LSeg* segs, SortArgs a) {
+__global__ __launch_bounds__(WG) void k_copy_back(const LTile* tiles, const LSeg* segs, SortArgs a,
+                                                  const u32* ndev) {
+    if (ndev && blockIdx.x >= *ndev) return;
     const LTile t = tiles[blockIdx.x];
     const LSeg s = segs[t.seg];
     const u32 base = s.start + t.k * TILE;
@@ -976,22 +983,22 @@ void launch_keygen_large(const LTile* tiles, u32 ntiles, const LSeg* segs, const
                          hipStream_t s) {
     if (ntiles) k_keygen_large<<<ntiles, WG, 0, s>>>(tiles, segs, a);
 }
-void launch_msd_hist(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a, u32 shift,
-                     u32 width, u32* hist, hipStream_t s) {
-    if (ntiles) k_msd_hist<<<ntiles, WG, 0, s>>>(tiles, segs, a, shift, (1u << width) - 1, hist);
+void launch_msd_hist(const LTile* tiles, u32 ntiles, const u32* ndev, const LSeg* segs, const SortArgs& a,
+                     u32 shift, u32 width, u32* hist, hipStream_t s) {
+    if (ntiles) k_msd_hist<<<ntiles, WG, 0, s>>>(tiles, segs, a, shift, (1u << width) - 1, hist, ndev);
 }
-void launch_msd_scan(const LSeg* segs, u32 nseg, const SortArgs& a, u32 width, u32* hist,
+void launch_msd_scan(const LSeg* segs, u32 nseg, const u32* ndev, const SortArgs& a, u32 width, u32* hist,
                      bool last_level, const Lists& L, const Level& next, hipStream_t s) {
     (void)width;
-    if (nseg) k_msd_scan<<<nseg, WG, 0, s>>>(segs, a, hist, last_level ? 1 : 0, L, next);
+    if (nseg) k_msd_scan<<<nseg, WG, 0, s>>>(segs, a, hist, last_level ? 1 : 0, L, next, ndev);
 }
-void launch_msd_scatter(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
+void launch_msd_scatter(const LTile* tiles, u32 ntiles, const u32* ndev, const LSeg* segs, const SortArgs& a,
                         u32 shift, u32 width, const u32* hist, hipStream_t s) {
-    if (ntiles) k_msd_scatter<<<ntiles, WG, 0, s>>>(tiles, segs, a, shift, width, hist);
+    if (ntiles) k_msd_scatter<<<ntiles, WG, 0, s>>>(tiles, segs, a, shift, width, hist, ndev);
 }
-void launch_copy_back(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
+void launch_copy_back(const LTile* tiles, u32 ntiles, const u32* ndev, const LSeg* segs, const SortArgs& a,
                       hipStream_t s) {
-    if (ntiles) k_copy_back<<<ntiles, WG, 0, s>>>(tiles, segs, a);
+    if (ntiles) k_copy_back<<<ntiles, WG, 0, s>>>(tiles, segs, a, ndev);
 }
 
 template <int C>

@@ -486,46 +486,48 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
                 launch_keygen_large(lv[0].tiles, h[C_L0TILE], lv[0].segs, a, s);
             }
         }
-        u32 nelem = h[C_L0ELEM];
-        u32 nseg = h[C_L0SEG], ntiles = h[C_L0TILE];
+        // MSD levels of the large segments, one per 8-bit digit down to the last, with no host
+        // round trip between them: level 0's counts are known here, later levels read theirs
+        // from device memory under bounds (a level's large buckets hold > TILE elements each
+        // and at most the elements of level 0: nseg <= nelem / TILE, ntiles <= 2 nelem / TILE)
+        const u32 nelem0 = h[C_L0ELEM], nseg0 = h[C_L0SEG], ntiles0 = h[C_L0TILE];
         u32 hi = a.initial ? (cyclic ? 32u : 27u) : kb_rank;
         int lvl = 0;
-        while (nseg) {
+        for (; nseg0 && hi; ++lvl) {
             const u32 width = std::min<u32>(8, hi);
             const u32 shift = hi - width;
             const bool last = shift == 0;
             Level& lc = lv[lvl & 1];
             Level& ln = lv[(lvl + 1) & 1];
+            const u32 nseg = lvl ? nelem0 / TILE + 1 : nseg0;
+            const u32 ntiles = lvl ? 2 * (nelem0 / TILE) + 1 : ntiles0;
+            const u32* dseg = lvl ? lc.nseg : nullptr;
+            const u32* dtile = lvl ? lc.ntiles : nullptr;
             KOLM_HIP_CHECK(hipMemsetAsync(ln.nseg, 0, sizeof(u32), s));
             KOLM_HIP_CHECK(hipMemsetAsync(ln.ntiles, 0, sizeof(u32), s));
             KOLM_HIP_CHECK(hipMemsetAsync(ln.nelem, 0, sizeof(u32), s));
             {
-                TScope t(c, KOLM_KT_MSD, "k_msd_hist", (u64)nelem * 4 + (u64)ntiles * 1024);
-                launch_msd_hist(lc.tiles, ntiles, lc.segs, a, shift, width, hist, s);
+                TScope t(c, KOLM_KT_MSD, "k_msd_hist", (u64)nelem0 * 4 + (u64)ntiles0 * 1024);
+                launch_msd_hist(lc.tiles, ntiles, dtile, lc.segs, a, shift, width, hist, s);
             }
             {
-                TScope t(c, KOLM_KT_MSD, "k_msd_scan", (u64)ntiles * 1024 * 3);
-                launch_msd_scan(lc.segs, nseg, a, width, hist, last, L, ln, s);
+                TScope t(c, KOLM_KT_MSD, "k_msd_scan", (u64)ntiles0 * 1024 * 3);
+                launch_msd_scan(lc.segs, nseg, dseg, a, width, hist, last, L, ln, s);
             }
             {
-                TScope t(c, KOLM_KT_MSD, "k_msd_scatter", (u64)nelem * 16 + (u64)ntiles * 1024);
-                launch_msd_scatter(lc.tiles, ntiles, lc.segs, a, shift, width, hist, s);
+                TScope t(c, KOLM_KT_MSD, "k_msd_scatter", (u64)nelem0 * 16 + (u64)ntiles0 * 1024);
+                launch_msd_scatter(lc.tiles, ntiles, dtile, lc.segs, a, shift, width, hist, s);
             }
             {
-                TScope t(c, KOLM_KT_MSD, "k_copy_back", (u64)nelem * 16);
-                launch_copy_back(lc.tiles, ntiles, lc.segs, a, s);
+                TScope t(c, KOLM_KT_MSD, "k_copy_back", (u64)nelem0 * 16);
+                launch_copy_back(lc.tiles, ntiles, dtile, lc.segs, a, s);
             }
+            hi = shift;
+        }
+        if (lvl) {  // the MSD levels appended segments to the class lists: fresh counts
             KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
             c->sync();
-            const bool n0 = ln.nseg == cnt + C_L0SEG;
-            nseg = h[n0 ? C_L0SEG : C_L1SEG];
-            ntiles = h[n0 ? C_L0TILE : C_L1TILE];
-            nelem = h[n0 ? C_L0ELEM : C_L1ELEM];
-            hi = shift;
-            ++lvl;
         }
-        // (after MSD levels h holds the counts their last level read back: the class lists
-        // they appended to are complete)
         // per element: K2 + SA read, SA + RK write (16 B); per segment record 8 B
         for (int k = 0; k < NCLASS; ++k) {
             if (!h[C_CLS + k]) continue;

@@ -281,13 +281,14 @@ void launch_keypos(const SortArgs& a, u32* KP, hipStream_t s);
 void launch_keygen_small(int c, const Seg* segs, u32 count, const SortArgs& a, hipStream_t s);
 void launch_keygen_large(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
                          hipStream_t s);
-void launch_msd_hist(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
+// MSD levels: ntiles / nseg is the count, or (ndev set) a bound with the count in ndev
+void launch_msd_hist(const LTile* tiles, u32 ntiles, const u32* ndev, const LSeg* segs, const SortArgs& a,
                      u32 shift, u32 width, u32* hist, hipStream_t s);
-void launch_msd_scan(const LSeg* segs, u32 nseg, const SortArgs& a, u32 width, u32* hist,
+void launch_msd_scan(const LSeg* segs, u32 nseg, const u32* ndev, const SortArgs& a, u32 width, u32* hist,
                      bool last_level, const Lists& L, const Level& next, hipStream_t s);
-void launch_msd_scatter(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
+void launch_msd_scatter(const LTile* tiles, u32 ntiles, const u32* ndev, const LSeg* segs, const SortArgs& a,
                         u32 shift, u32 width, const u32* hist, hipStream_t s);
-void launch_copy_back(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
+void launch_copy_back(const LTile* tiles, u32 ntiles, const u32* ndev, const LSeg* segs, const SortArgs& a,
                       hipStream_t s);
 constexpr int TINY_C = 5;  // classes 1..TINY_C (<= 32 elements): one thread per segment
 void launch_tiny_sort(int c, const Seg* segs, u32 count, const SortArgs& a, const Lists& L, hipStream_t s);
