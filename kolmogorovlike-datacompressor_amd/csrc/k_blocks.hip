@@ -451,34 +451,56 @@ __device__ inline u64 load8u(const u8* s, u32 x) {
     return ((u64)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
 }
 
+// One round trip of U 512-byte steps of lyn_less at offset o: the first differing offset,
+// or ~0u when all U * 512 bytes agree.
+template <u32 U>
+__device__ inline u32 lyn_trip(const u8* s, u32 a0, u32 a1, u32 o, u32 lane) {
+    u64 d[U];
+#pragma unroll
+    for (u32 k = 0; k < U; ++k) {
+        const u32 t = o + 512 * k + 8 * lane;
+        d[k] = load8u(s, a0 + t) ^ load8u(s, a1 + t);
+    }
+#pragma unroll
+    for (u32 k = 0; k < U; ++k) {
+        const u64 bal = __ballot(d[k] != 0);
+        if (bal) {
+            const u32 j = (u32)__ffsll((long long)bal) - 1;
+            const u32 dj = (u32)__ffsll((long long)d[k]) - 1;
+            return o + 512 * k + 8 * j + (u32)__builtin_amdgcn_readlane((int)dj, (int)j) / 8;
+        }
+    }
+    return ~0u;
+}
+
 // x = s[a0, a1) < y = s[a1, b1) lexicographically (proper prefix smaller); wave-uniform.
 // 8 bytes per lane per step (512 per wave) while the loads stay inside s[0, N).
 __device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N, u32* nsteps = nullptr, u32 o0 = 0) {
     const u32 lane = threadIdx.x & 63;
     const u32 la = a1 - a0, lb = b1 - a1, m = min(la, lb);
     u32 o = o0;
-    // long common prefixes (periodic data: factors agree on KB): four 512-byte steps per
-    // round trip while they lie wholly inside both factors and s[0, N)
-    constexpr u32 U = 4;
-    while (o + 512 * U <= m && (u64)a1 + o + 512 * U + 12 <= N) {
+    // long common prefixes (periodic data: factors agree on KB): round trips of 2, 4, then
+    // 8 KB while they lie wholly inside both factors and s[0, N) — a comparison that runs
+    // long probably runs longer (the checker BMP's factors agree on ~10 KB), one that stops
+    // early fetched little past its end
+    auto fits = [&](u32 bytes) { return o + bytes <= m && (u64)a1 + o + bytes + 12 <= N; };
+    u32 trip = 0;
+    while (fits(512u * (trip == 0 ? 4u : trip == 1 ? 8u : 16u))) {
+        const u32 U = trip == 0 ? 4u : trip == 1 ? 8u : 16u;
         if (nsteps) *nsteps += U;
-        u64 d[U];
-#pragma unroll
-        for (u32 k = 0; k < U; ++k) {
-            const u32 t = o + 512 * k + 8 * lane;
-            d[k] = load8u(s, a0 + t) ^ load8u(s, a1 + t);
-        }
-#pragma unroll
-        for (u32 k = 0; k < U; ++k) {
-            const u64 bal = __ballot(d[k] != 0);
-            if (bal) {
-                const u32 j = (u32)__ffsll((long long)bal) - 1;
-                const u32 dj = (u32)__ffsll((long long)d[k]) - 1;
-                const u32 dpos = o + 512 * k + 8 * j + (u32)__builtin_amdgcn_readlane((int)dj, (int)j) / 8;
-                return s[a0 + dpos] < s[a1 + dpos];
-            }
-        }
+        const u32 dpos = U == 4 ? lyn_trip<4>(s, a0, a1, o, lane)
+                         : U == 8 ? lyn_trip<8>(s, a0, a1, o, lane)
+                                  : lyn_trip<16>(s, a0, a1, o, lane);
+        if (dpos != ~0u) return s[a0 + dpos] < s[a1 + dpos];
         o += 512 * U;
+        trip = min(trip + 1, 2u);
+    }
+    // (the tail below: 512-byte steps)
+    while (fits(2048)) {
+        if (nsteps) *nsteps += 4;
+        const u32 dpos = lyn_trip<4>(s, a0, a1, o, lane);
+        if (dpos != ~0u) return s[a0 + dpos] < s[a1 + dpos];
+        o += 2048;
     }
     for (; o < m; o += 512) {
         if (nsteps) ++*nsteps;
@@ -578,7 +600,8 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
     __shared__ Pre lpre[PRE_LDS];
     __shared__ u32 lok[PRE_LDS];
     const u64 t0 = prof ? wall_clock64() : 0;
-    u32 ncmp = 0, nstep = 0;
+    u32 ncmp = 0, nstep = 0, npush = 0, nmerge = 0, nlyn = 0;
+    u64 tlyn = 0;
     const u32 b = blockIdx.x, lane = threadIdx.x;
     const u32 base = geo.base(b), end = geo.end(b);
     // the stack never holds more entries than the span factorisations together: in LDS
@@ -618,6 +641,36 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
                 vnx = gi + 1 < nf ? fstart[lo + gi + 1] : hi;
                 if (gi < nf) vpr = text_pre(s, vst, end);
             }
+            // Batch absorption: while the top T keeps absorbing the span's factors (T' = T f_t
+            // ... f_(i-1) < f_i; audio and images merge thousands of span factors into a few),
+            // the decisions for a whole group come from one lane-parallel prefix comparison
+            // against T's prefix (T' starts with T).  Valid while nothing below T can merge
+            // into T': the entry below differs from T within T's first bytes and is larger.
+            if (sp >= 1 && tok) {
+                bool safe = sp == 1;
+                const u32 lT = rdl(vst, t - g0) - top;  // |T'| before factor t
+                if (sp >= 2 && sp - 2 < PRE_LDS && lok[sp - 2]) {
+                    const u32 bst = stk[sp - 2];
+                    safe = pre_cmp(lpre[sp - 2], tpre, min(top - bst, lT)) > 0;
+                }
+                if (safe) {
+                    const u32 l0 = t - g0;
+                    bool ok = false;
+                    if (lane >= l0 && g0 + lane < nf) {
+                        const u32 la = vst - top, lb = vnx - vst, m = min(la, lb);
+                        const int cr = pre_cmp(tpre, vpr, m);
+                        ok = cr < 0 || (cr == 0 && m <= 32 && la < lb);
+                    }
+                    const u64 okm = __ballot(ok) >> l0;
+                    const u32 k = okm == ~0ull ? 64u : (u32)__ffsll((long long)~okm) - 1;
+                    if (k) {
+                        t += k;
+                        npush += k;
+                        nmerge += k;
+                        continue;
+                    }
+                }
+            }
             const u32 cached = 1u;
             const u32 r = rdl(vst, t - g0);
             const u32 frontier = rdl(vnx, t - g0);
@@ -630,6 +683,7 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
                 }
             }
             ++sp;
+            ++npush;
             // y = the top (r, or what r merged into), x = the entry below it
             u32 ys = r, yok = cached;
             Pre yp = rp;
@@ -646,9 +700,16 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
                     less = cr < 0;
                 else if (xok && yok && m <= 32)
                     less = la < lb;
-                else
+                else {
+                    const u64 tl = prof ? wall_clock64() : 0;
                     less = lyn_less(s, xs, ys, frontier, (u32)geo.N, prof ? &nstep : nullptr, xok && yok ? 32u : 0u);
+                    if (prof) {
+                        ++nlyn;
+                        tlyn += wall_clock64() - tl;
+                    }
+                }
                 if (!less) break;
+                ++nmerge;
                 --sp;  // x absorbs y: the merged factor keeps x's start and prefix
                 ys = xs;
                 yok = xok;
@@ -703,6 +764,11 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
         atomicAdd((unsigned long long*)&prof[13], (unsigned long long)ncmp);
         atomicAdd((unsigned long long*)&prof[14], (unsigned long long)nstep);
         atomicAdd((unsigned long long*)&prof[15], (unsigned long long)tot);
+        atomicAdd((unsigned long long*)&prof[16], (unsigned long long)npush);
+        atomicAdd((unsigned long long*)&prof[17], (unsigned long long)nmerge);
+        atomicAdd((unsigned long long*)&prof[18], (unsigned long long)nlyn);
+        atomicAdd((unsigned long long*)&prof[19], (unsigned long long)tlyn);
+        atomicAdd((unsigned long long*)&prof[20], (unsigned long long)sp);
     }
 }
 
@@ -789,8 +855,8 @@ u64* dprof_buf() {
     static u64* prof = nullptr;
     static const bool dp = getenv("KOLM_DUVAL_PROF") && atoi(getenv("KOLM_DUVAL_PROF"));
     if (dp && !prof) {
-        KOLM_HIP_CHECK(hipMalloc(&prof, 16 * sizeof(u64)));
-        KOLM_HIP_CHECK(hipMemset(prof, 0, 16 * sizeof(u64)));
+        KOLM_HIP_CHECK(hipMalloc(&prof, 24 * sizeof(u64)));
+        KOLM_HIP_CHECK(hipMemset(prof, 0, 24 * sizeof(u64)));
     }
     return prof;
 }
@@ -817,15 +883,18 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fsta
         k_duval_merge<<<geo.nb, 64, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, stack, fcount, flag, dprof_buf());
     }
     if (u64* prof = dprof_buf()) {
-        u64 h[16];
+        u64 h[24];
         KOLM_HIP_CHECK(hipStreamSynchronize(s));
         KOLM_HIP_CHECK(hipMemcpy(h, prof, sizeof h, hipMemcpyDeviceToHost));
-        KOLM_HIP_CHECK(hipMemset(prof, 0, 16 * sizeof(u64)));
+        KOLM_HIP_CHECK(hipMemset(prof, 0, 24 * sizeof(u64)));
         fprintf(stderr, "[kolm] duval_span us per workgroup:");
         for (int k = 0; k < 11; ++k) fprintf(stderr, " %d:%.1f", k, (double)h[k] / nch / 100.0);
         fprintf(stderr, " | merge us per block mean %.1f max %.1f, compares/block %.1f, 512-B steps/block %.1f, "
                 "span factors/block %.1f\n", (double)h[11] / geo.nb / 100.0, (double)h[12] / 100.0,
                 (double)h[13] / geo.nb, (double)h[14] / geo.nb, (double)h[15] / geo.nb);
+        fprintf(stderr, "[kolm] merge per block: pushes %.1f merges %.1f text compares %.1f (%.1f us), final factors %.1f\n",
+                (double)h[16] / geo.nb, (double)h[17] / geo.nb, (double)h[18] / geo.nb, (double)h[19] / geo.nb / 100.0,
+                (double)h[20] / geo.nb);
     }
     {
         KScope k(kt, KT_LYNDON, "k_tile_starts", N);

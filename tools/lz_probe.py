@@ -16,7 +16,7 @@ from kolm import _lib, datagen  # noqa: E402
 
 def main():
     kind = sys.argv[1] if len(sys.argv) > 1 else "mixed"
-    mask = int(sys.argv[2], 0) if len(sys.argv) > 2 else _lib.KOLM_HOTPATH_MASK
+    mask = int(sys.argv[2], 0) if len(sys.argv) > 2 and sys.argv[2] != "-" else _lib.KOLM_HOTPATH_MASK
     part = int(sys.argv[3]) if len(sys.argv) > 3 else -1  # one 1 MiB block of the input only
     data = {"mixed": datagen.mixed_corpus, "gradient": lambda: datagen.gradient_bmp()[: 1 << 20],
             "wav": datagen.sine_wav, "checker": datagen.checker_bmp}[kind]()
