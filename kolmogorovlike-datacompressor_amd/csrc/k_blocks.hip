@@ -474,32 +474,24 @@ __device__ inline u32 lyn_trip(const u8* s, u32 a0, u32 a1, u32 o, u32 lane) {
 }
 
 // x = s[a0, a1) < y = s[a1, b1) lexicographically (proper prefix smaller); wave-uniform.
-// 8 bytes per lane per step (512 per wave) while the loads stay inside s[0, N).
-__device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N, u32* nsteps = nullptr, u32 o0 = 0) {
+// 8 bytes per lane per step (512 per wave) while the loads stay inside s[0, N).  The bytes
+// from o0 on are compared (the first o0 are known equal).  lcp / exact: where it stopped —
+// the text's LCP of a0 and a1 is lcp (exact) or at least lcp (no difference below min(la, lb)).
+__device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N, u32* nsteps, u32 o0, u32& lcp, bool& exact) {
     const u32 lane = threadIdx.x & 63;
     const u32 la = a1 - a0, lb = b1 - a1, m = min(la, lb);
     u32 o = o0;
-    // long common prefixes (periodic data: factors agree on KB): round trips of 2, 4, then
-    // 8 KB while they lie wholly inside both factors and s[0, N) — a comparison that runs
-    // long probably runs longer (the checker BMP's factors agree on ~10 KB), one that stops
-    // early fetched little past its end
-    auto fits = [&](u32 bytes) { return o + bytes <= m && (u64)a1 + o + bytes + 12 <= N; };
-    u32 trip = 0;
-    while (fits(512u * (trip == 0 ? 4u : trip == 1 ? 8u : 16u))) {
-        const u32 U = trip == 0 ? 4u : trip == 1 ? 8u : 16u;
-        if (nsteps) *nsteps += U;
-        const u32 dpos = U == 4 ? lyn_trip<4>(s, a0, a1, o, lane)
-                         : U == 8 ? lyn_trip<8>(s, a0, a1, o, lane)
-                                  : lyn_trip<16>(s, a0, a1, o, lane);
-        if (dpos != ~0u) return s[a0 + dpos] < s[a1 + dpos];
-        o += 512 * U;
-        trip = min(trip + 1, 2u);
-    }
-    // (the tail below: 512-byte steps)
-    while (fits(2048)) {
+    // long common prefixes (periodic data: factors agree on KB): four 512-byte steps per
+    // round trip while they lie wholly inside both factors and s[0, N) (larger trips measured
+    // slower: a single wave is bound by its own load issue, not by the latency)
+    while (o + 2048 <= m && (u64)a1 + o + 2048 + 12 <= N) {
         if (nsteps) *nsteps += 4;
         const u32 dpos = lyn_trip<4>(s, a0, a1, o, lane);
-        if (dpos != ~0u) return s[a0 + dpos] < s[a1 + dpos];
+        if (dpos != ~0u) {
+            lcp = dpos;
+            exact = true;
+            return s[a0 + dpos] < s[a1 + dpos];
+        }
         o += 2048;
     }
     for (; o < m; o += 512) {
@@ -524,9 +516,13 @@ __device__ bool lyn_less(const u8* s, u32 a0, u32 a1, u32 b1, u32 N, u32* nsteps
         const u64 bal = __ballot(dpos != 0xFFFFFFFFu);
         if (bal) {
             const u32 d = __builtin_amdgcn_readlane(dpos, __ffsll((long long)bal) - 1);
+            lcp = d;
+            exact = true;
             return s[a0 + d] < s[a1 + d];
         }
     }
+    lcp = m;
+    exact = false;
     return la < lb;
 }
 
@@ -601,6 +597,9 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
     __shared__ u32 lok[PRE_LDS];
     const u64 t0 = prof ? wall_clock64() : 0;
     u32 ncmp = 0, nstep = 0, npush = 0, nmerge = 0, nlyn = 0;
+    // the last text comparison: pair (mxs, mys), LCP mL (exact: mex, then x < y is mlt)
+    u32 mxs = ~0u, mys = ~0u, mL = 0;
+    bool mex = false, mlt = false;
     u64 tlyn = 0;
     const u32 b = blockIdx.x, lane = threadIdx.x;
     const u32 base = geo.base(b), end = geo.end(b);
@@ -700,9 +699,22 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
                     less = cr < 0;
                 else if (xok && yok && m <= 32)
                     less = la < lb;
-                else {
+                else if (xs == mxs && ys == mys && mex) {
+                    // the same pair as the last text comparison (y grew since): its LCP stands
+                    less = mL < m ? mlt : la < lb;
+                } else {
+                    // the same pair with y grown: its first mL bytes are known equal (the
+                    // checker BMP's merges re-compare one long factor against a growing one)
+                    const u32 o0 = max(xok && yok ? 32u : 0u, xs == mxs && ys == mys ? min(mL, m) : 0u);
                     const u64 tl = prof ? wall_clock64() : 0;
-                    less = lyn_less(s, xs, ys, frontier, (u32)geo.N, prof ? &nstep : nullptr, xok && yok ? 32u : 0u);
+                    u32 L;
+                    bool ex;
+                    less = lyn_less(s, xs, ys, frontier, (u32)geo.N, prof ? &nstep : nullptr, o0, L, ex);
+                    mxs = xs;
+                    mys = ys;
+                    mL = L;
+                    mex = ex;
+                    mlt = less;
                     if (prof) {
                         ++nlyn;
                         tlyn += wall_clock64() - tl;
