@@ -597,9 +597,10 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
     __shared__ u32 lok[PRE_LDS];
     const u64 t0 = prof ? wall_clock64() : 0;
     u32 ncmp = 0, nstep = 0, npush = 0, nmerge = 0, nlyn = 0;
-    // the last text comparison: pair (mxs, mys), LCP mL (exact: mex, then x < y is mlt)
-    u32 mxs = ~0u, mys = ~0u, mL = 0;
-    bool mex = false, mlt = false;
+    // the last two text comparisons: pair (mxs, mys), LCP mL (exact: mex, then x < y is mlt)
+    u32 mxs[2] = {~0u, ~0u}, mys[2] = {~0u, ~0u}, mL[2] = {0, 0};
+    bool mex[2] = {false, false}, mlt[2] = {false, false};
+    int mold = 0;  // the slot to replace
     u64 tlyn = 0;
     const u32 b = blockIdx.x, lane = threadIdx.x;
     const u32 base = geo.base(b), end = geo.end(b);
@@ -699,26 +700,32 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
                     less = cr < 0;
                 else if (xok && yok && m <= 32)
                     less = la < lb;
-                else if (xs == mxs && ys == mys && mex) {
-                    // the same pair as the last text comparison (y grew since): its LCP stands
-                    less = mL < m ? mlt : la < lb;
-                } else {
-                    // the same pair with y grown: its first mL bytes are known equal (the
-                    // checker BMP's merges re-compare one long factor against a growing one)
-                    const u32 o0 = max(xok && yok ? 32u : 0u, xs == mxs && ys == mys ? min(mL, m) : 0u);
-                    const u64 tl = prof ? wall_clock64() : 0;
-                    u32 L;
-                    bool ex;
-                    less = lyn_less(s, xs, ys, frontier, (u32)geo.N, prof ? &nstep : nullptr, o0, L, ex);
-                    mxs = xs;
-                    mys = ys;
-                    mL = L;
-                    mex = ex;
-                    mlt = less;
-                    if (prof) {
-                        ++nlyn;
-                        tlyn += wall_clock64() - tl;
+                else {
+                    // memo of the last two text comparisons (pairs alternate: the checker
+                    // BMP's merges re-compare one long factor against a growing one between
+                    // short comparisons): a known pair resumes past its known-equal bytes, or
+                    // is decided by its exact LCP
+                    const int hit = xs == mxs[0] && ys == mys[0] ? 0 : xs == mxs[1] && ys == mys[1] ? 1 : -1;
+                    if (hit >= 0 && mex[hit]) {
+                        less = mL[hit] < m ? mlt[hit] : la < lb;
+                    } else {
+                        const u32 o0 = max(xok && yok ? 32u : 0u, hit >= 0 ? min(mL[hit], m) : 0u);
+                        const u64 tl = prof ? wall_clock64() : 0;
+                        u32 L;
+                        bool ex;
+                        less = lyn_less(s, xs, ys, frontier, (u32)geo.N, prof ? &nstep : nullptr, o0, L, ex);
+                        const int sl = hit >= 0 ? hit : mold;
+                        mxs[sl] = xs;
+                        mys[sl] = ys;
+                        mL[sl] = L;
+                        mex[sl] = ex;
+                        mlt[sl] = less;
+                        if (prof) {
+                            ++nlyn;
+                            tlyn += wall_clock64() - tl;
+                        }
                     }
+                    mold = hit >= 0 ? 1 - hit : 1 - mold;  // the slot not used now is replaced next
                 }
                 if (!less) break;
                 ++nmerge;
