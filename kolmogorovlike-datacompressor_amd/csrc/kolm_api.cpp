@@ -1578,7 +1578,12 @@ int kolm_compress_fixed(const uint8_t* data, uint64_t n, uint32_t block_size, ui
                 if (u.t.joinable()) u.t.join();
             }
         } jg{next};
+        // KOLM_HOST_PROF=1 (debug): wall-clock phases of the call on stderr
+        static const bool hprof = getenv("KOLM_HOST_PROF") && atoi(getenv("KOLM_HOST_PROF"));
+        const auto th0 = std::chrono::steady_clock::now();
+        auto hms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count(); };
         upload(0);
+        if (hprof) fprintf(stderr, "[kolm] host: piece 0 upload queued %.2f ms\n", hms());
         u64 pos = 0, dpos = head;
         std::vector<u64> apos(np), abytes(np);
         kolm_stats agg{};
@@ -1600,6 +1605,7 @@ int kolm_compress_fixed(const uint8_t* data, uint64_t n, uint32_t block_size, ui
             int r = encode_batch(c, dtext[i & 1], len, block_size, nullptr, 0, cand_mask & KOLM_FULL_MASK, nullptr,
                                  arena + pos, acap - pos, nullptr, method.data() + b0, o.data(), &st);
             if (r) return r;
+            if (hprof) fprintf(stderr, "[kolm] host: piece %llu encoded %.2f ms\n", (unsigned long long)i, hms());
             for (u64 j = 0; j < k; ++j) plen[b0 + j] = o[j + 1] - o[j];
             apos[i] = pos;
             abytes[i] = o[k];
@@ -1642,6 +1648,7 @@ int kolm_compress_fixed(const uint8_t* data, uint64_t n, uint32_t block_size, ui
                                    toc_len, &toc_len))
             return e;
         KOLM_HIP_CHECK(hipStreamSynchronize(c->dl));
+        if (hprof) fprintf(stderr, "[kolm] host: payloads down, TOC written %.2f ms\n", hms());
         *out = c->h_res + at;
         *out_len = need;
         c->h_res_off = at;

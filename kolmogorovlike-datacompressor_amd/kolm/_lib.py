@@ -12,7 +12,9 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import threading
+import time
 
 import numpy as np
 
@@ -338,11 +340,18 @@ def compress_fixed(data, block_size: int, cand_mask: int = KOLM_DEFAULT_MASK):
         check(rc)
         # the result bytes object is allocated uninitialised and filled by the library's
         # copy threads (kolm_result_copy) instead of one single-threaded string_at copy
+        t0 = time.perf_counter() if _HOST_PROF else 0.0
         blob = _new_bytes(ln.value)
+        t1 = time.perf_counter() if _HOST_PROF else 0.0
         if ln.value:
             check(load().kolm_result_copy(ctypes.cast(ctypes.c_char_p(blob), ctypes.c_void_p), ln.value))
+        if _HOST_PROF:
+            print(f"[kolm] host: bytes alloc {1e3 * (t1 - t0):.2f} ms, result copy "
+                  f"{1e3 * (time.perf_counter() - t1):.2f} ms", file=sys.stderr)
     return blob, st.as_dict()
 
+
+_HOST_PROF = os.environ.get("KOLM_HOST_PROF", "0") not in ("", "0")  # debug: phase times on stderr
 
 _PyBytes_New = ctypes.pythonapi.PyBytes_FromStringAndSize
 _PyBytes_New.restype = ctypes.py_object
