@@ -249,26 +249,30 @@ __device__ inline void dprof(u64* prof, u32 k, u64& last) {
         last = now;
     }
 }
-__global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8* s, u32* fstart, uint4* fpre,
-                                                    u32* nfac, u64* prof) {
+// NT threads (of DUVAL_CH bytes each) per span: 256 (32 KiB spans), or 64 (8 KiB, opt-in: see
+// duval_span_bytes)
+template <u32 NT>
+__global__ __launch_bounds__(NT) void k_duval_span(Geom geo, u32 spb, const u8* s, u32* fstart, uint4* fpre,
+                                                   u32* nfac, u64* prof) {
+    constexpr u32 SPAN = DUVAL_CH * NT;
     u64 tlast = prof ? wall_clock64() : 0;
-    __shared__ __align__(16) u8 t[DUVAL_SPAN + 256 * DUVAL_PAD + 4];  // + 4: lds_word's read past the end
-    __shared__ u32 bm[DUVAL_SPAN / 32];
-    __shared__ u32 sm[DUVAL_SPAN / 1024];
-    __shared__ u32 sh[WG / 64];
+    __shared__ __align__(16) u8 t[SPAN + NT * DUVAL_PAD + 4];  // + 4: lds_word's read past the end
+    __shared__ u32 bm[SPAN / 32];
+    __shared__ u32 sm[(SPAN + 1023) / 1024];
+    __shared__ u32 sh[NT / 64];
     const u32 sp = blockIdx.x, tid = threadIdx.x;
     const u32 b = sp / spb, k = sp - b * spb;
-    const u32 lo = geo.base(b) + k * DUVAL_SPAN;
+    const u32 lo = geo.base(b) + k * SPAN;
     const u32 e = geo.end(b), e_blk = e;
     if (lo >= e) {
         if (tid == 0) nfac[sp] = 0;
         return;
     }
-    const u32 n = min(DUVAL_SPAN, e - lo);
+    const u32 n = min(SPAN, e - lo);
     // stage the span (16-byte loads when aligned and whole)
-    if (n == DUVAL_SPAN && (lo & 15) == 0) {
+    if (n == SPAN && (lo & 15) == 0) {
         const uint4* src = reinterpret_cast<const uint4*>(s + lo);
-        for (u32 i = tid; i < DUVAL_SPAN / 16; i += 256) {
+        for (u32 i = tid; i < SPAN / 16; i += NT) {
             const uint4 v = src[i];
             u32* d = reinterpret_cast<u32*>(&t[lds_addr(i * 16)]);  // 4-byte aligned, inside one chunk
             d[0] = v.x;
@@ -277,9 +281,9 @@ __global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8*
             d[3] = v.w;
         }
     } else {
-        for (u32 i = tid; i < n; i += 256) t[lds_addr(i)] = s[lo + i];
+        for (u32 i = tid; i < n; i += NT) t[lds_addr(i)] = s[lo + i];
     }
-    for (u32 i = tid; i < DUVAL_SPAN / 32; i += 256) bm[i] = 0;
+    for (u32 i = tid; i < SPAN / 32; i += NT) bm[i] = 0;
     __syncthreads();
     dprof(prof, 0, tlast);
     // Duval on the thread's chunk; factor starts -> bitmap (bits of one chunk are 4 words
@@ -329,19 +333,19 @@ __global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8*
     }
     __syncthreads();
     dprof(prof, 1, tlast);
-    if (tid < DUVAL_SPAN / 1024) {
+    if (tid < (SPAN + 1023) / 1024) {
         u32 v = 0;
-        for (u32 q = 0; q < 32; ++q) v |= (bm[tid * 32 + q] != 0) << q;
+        for (u32 q = 0; q < 32 && tid * 32 + q < SPAN / 32; ++q) v |= (bm[tid * 32 + q] != 0) << q;
         sm[tid] = v;
     }
     __syncthreads();
     // tree merge of adjacent factorizations: a thread per merge on the low levels, a wave
     // per merge (64-lane factor comparisons) from DUVAL_WAVE_W up, where few merges remain
     // and adjacent factors of text share long prefixes
-    for (u32 w = DUVAL_CH; w < DUVAL_SPAN; w <<= 1) {
+    for (u32 w = DUVAL_CH; w < SPAN; w <<= 1) {
         if (w >= DUVAL_WAVE_W) {
             const u32 lane = tid & 63, wv = tid >> 6;
-            for (u32 a0 = wv * 2 * w; a0 + w < n; a0 += 2 * w * (256 / 64)) {
+            for (u32 a0 = wv * 2 * w; a0 + w < n; a0 += 2 * w * (NT / 64)) {
                 const u32 m = a0 + w, hi = min(m + w, n);
                 u32 r = m;
                 while (r < hi) {
@@ -398,7 +402,7 @@ __global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8*
     for (u32 q = 0; q < DUVAL_CH / 32; ++q) cnt += __popc(bm[tid * (DUVAL_CH / 32) + q]);
     u32 o = 0;
     {
-        // exclusive scan over 256 threads
+        // exclusive scan over the NT threads
         const u32 lane = tid & 63, wv = tid >> 6;
         u32 incl = cnt;
         for (u32 d = 1; d < 64; d <<= 1) {
@@ -410,7 +414,7 @@ __global__ __launch_bounds__(256) void k_duval_span(Geom geo, u32 spb, const u8*
         u32 carry = 0;
         for (u32 i = 0; i < wv; ++i) carry += sh[i];
         o = carry + incl - cnt;
-        if (tid == 255) nfac[sp] = carry + incl;
+        if (tid == NT - 1) nfac[sp] = carry + incl;
     }
     for (u32 q = 0; q < DUVAL_CH / 32; ++q) {
         u32 v = bm[tid * (DUVAL_CH / 32) + q];
@@ -589,7 +593,7 @@ __device__ inline Pre rdl(const Pre& p, u32 l) {
 // prefix in LDS, so nearly all comparisons are decided in registers.  Only factors that
 // agree on 32 bytes compare the text in global memory: the chain of ~800 dependent
 // comparisons per 1 MiB text block cost ~0.7 us of load latency each.
-__global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8* s, const u32* fstart,
+__global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, u32 span, const u8* s, const u32* fstart,
                                                     const uint4* fpre, const u32* nfac, u32* stack, u32* fcount,
                                                     u8* flag, u64* prof) {
     __shared__ u32 lstk[MERGE_LDS];
@@ -608,7 +612,7 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
     // when they fit (text: a few dozen), else in global memory (e.g. a run: n factors)
     u32 tot = 0;
     for (u32 k = lane; k < cpb; k += 64)
-        if (base + k * DUVAL_SPAN < end) tot += nfac[b * cpb + k];
+        if (base + k * span < end) tot += nfac[b * cpb + k];
     tot = wave_reduce(tot, OpAddU(), 0u);
     // written by lane 0, re-read uniformly: volatile keeps the reads off the scalar cache
     volatile u32* stk = tot <= MERGE_LDS ? lstk : stack + base;
@@ -618,9 +622,9 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, const u8*
     Pre tpre{};
     for (u32 k = 0; k < cpb; ++k) {
         const u32 c = b * cpb + k;
-        const u32 lo = base + k * DUVAL_SPAN;
+        const u32 lo = base + k * span;
         if (lo >= end) break;
-        const u32 hi = min(lo + DUVAL_SPAN, end);
+        const u32 hi = min(lo + span, end);
         const u32 nf = nfac[c];
         // factors g0 .. g0 + 63 of the span: start, next start (or hi), prefix — one per lane
         static_assert(DUVAL_PF == 64, "group 0 of the span comes from fpre");
@@ -882,6 +886,16 @@ u64* dprof_buf() {
 
 // Lyndon factorisation of every block (parallel Duval + merge) -> factor-start lists,
 // flags and FEd.
+// Bytes per Duval span: DUVAL_SPAN (32 KiB); KOLM_DUVAL_SPAN=8192 selects 8 KiB spans (64-thread
+// workgroups, 4x more of them).  Measured on batches of few blocks: the span pass gets faster
+// (config 5 1.82 -> 1.20 ms, config 2 ms per call 2.39 -> 2.26) but the merge pushes 4x more span
+// factorisations (config 5's checker block: merge 3.1 -> 6.3 ms), so 32 KiB stays the default.
+u32 duval_span_bytes(const Geom& geo) {
+    (void)geo;
+    static const u32 force = getenv("KOLM_DUVAL_SPAN") ? (u32)atoi(getenv("KOLM_DUVAL_SPAN")) : 0u;
+    return force == DUVAL_CH * 64 ? force : DUVAL_SPAN;
+}
+
 void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fstart, uint4* fpre, u32* nfac,
                    u32* stack, u32* fcount, u32* tile_tmp, hipStream_t s, KTimer* kt) {
     if (!geo.N) return;
@@ -889,17 +903,22 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fsta
     const u32 nt = tg.tpb * geo.nb;
     u32* A = tile_tmp;        // [nt]
     u32* B = tile_tmp + nt;   // [nt]
-    const u32 cpb = (geo.bs + DUVAL_SPAN - 1) / DUVAL_SPAN;
+    const u32 span = duval_span_bytes(geo);
+    const u32 cpb = (geo.bs + span - 1) / span;
     const u32 nch = cpb * geo.nb;
     const u64 N = geo.N;
     KOLM_HIP_CHECK(hipMemsetAsync(flag, 0, geo.N, s));
     {
         KScope k(kt, KT_LYNDON, "k_duval_span", N);  // text once (+ 4 B per factor start)
-        k_duval_span<<<nch, 256, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, dprof_buf());
+        if (span == DUVAL_SPAN)
+            k_duval_span<256><<<nch, 256, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, dprof_buf());
+        else
+            k_duval_span<64><<<nch, 64, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, dprof_buf());
     }
     {
         KScope k(kt, KT_LYNDON, "k_duval_merge", (u64)nch * 8);
-        k_duval_merge<<<geo.nb, 64, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, stack, fcount, flag, dprof_buf());
+        k_duval_merge<<<geo.nb, 64, 0, s>>>(geo, cpb, span, text, fstart, fpre, nfac, stack, fcount, flag,
+                                             dprof_buf());
     }
     if (u64* prof = dprof_buf()) {
         u64 h[24];

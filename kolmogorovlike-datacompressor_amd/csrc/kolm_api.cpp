@@ -570,7 +570,7 @@ struct Pipeline {
     void lyndon() {
         const u64 N = geo.N;
         const u64 ntiles = (u64)((geo.bs + TILE - 1) / TILE) * geo.nb + 16;
-        const u64 nch = (geo.bs + 32767) / 32768 * (u64)geo.nb + 1;  // DUVAL_SPAN
+        const u64 nch = (geo.bs + duval_span_bytes(geo) - 1) / duval_span_bytes(geo) * (u64)geo.nb + 1;
         launch_lyndon(geo, text, c->get<u8>("flag", N), c->get<u8>("FEd", N),
                       c->get<u32>("lyn_fstart", N), c->get<uint4>("lyn_fpre", nch * 128),
                       c->get<u32>("lyn_nfac", nch), c->get<u32>("lyn_stack", N), c->get<u32>("lyn_fcount", geo.nb + 1), c->get<u32>("lyn_t1", 2 * ntiles + 16),

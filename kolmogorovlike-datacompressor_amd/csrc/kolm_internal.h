@@ -299,6 +299,7 @@ void launch_rounds_sum(const u32* blk_done, u32 nb, u32 rounds, u64* out, hipStr
 void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, u32 round, hipStream_t s);
 
 // ---- k_blocks.hip: per-block scans, Lyndon factors, BBWT gather ----
+u32 duval_span_bytes(const Geom& geo);  // bytes per Duval span of this batch (launch_lyndon's choice)
 void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fstart, uint4* fpre, u32* nfac,
                    u32* stack, u32* fcount, u32* tile_tmp, hipStream_t s, KTimer* kt = nullptr);
 void launch_prevc(const Geom& geo, const u8* text, const u8* flag, Factors fac, u8* prevc, hipStream_t s);
