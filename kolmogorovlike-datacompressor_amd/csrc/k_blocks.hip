@@ -600,7 +600,7 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, u32 span,
     __shared__ Pre lpre[PRE_LDS];
     __shared__ u32 lok[PRE_LDS];
     const u64 t0 = prof ? wall_clock64() : 0;
-    u32 ncmp = 0, nstep = 0, npush = 0, nmerge = 0, nlyn = 0;
+    u32 ncmp = 0, nstep = 0, npush = 0, nmerge = 0, nlyn = 0, nb_try = 0, nb_lim = 0, nb_hit = 0;
     // the last two text comparisons: pair (mxs, mys), LCP mL (exact: mex, then x < y is mlt)
     u32 mxs[2] = {~0u, ~0u}, mys[2] = {~0u, ~0u}, mL[2] = {0, 0};
     bool mex[2] = {false, false}, mlt[2] = {false, false};
@@ -650,24 +650,79 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, u32 span,
             // the decisions for a whole group come from one lane-parallel prefix comparison
             // against T's prefix (T' starts with T).  Valid while nothing below T can merge
             // into T': the entry below differs from T within T's first bytes and is larger.
+            // When the entry below, x, shares T's first bytes (periodic data: the checker BMP's
+            // factors), T' = T f_t ... stays no larger than x while it is a prefix of x or
+            // first differs from x downwards: the text LCP of x and T (memoised, extended to
+            // the group's reach) bounds how far T' may grow (xlim) without x absorbing it.
             if (sp >= 1 && tok) {
                 bool safe = sp == 1;
+                u32 xlim = 0;
                 const u32 lT = rdl(vst, t - g0) - top;  // |T'| before factor t
                 if (sp >= 2 && sp - 2 < PRE_LDS && lok[sp - 2]) {
-                    const u32 bst = stk[sp - 2];
-                    safe = pre_cmp(lpre[sp - 2], tpre, min(top - bst, lT)) > 0;
+                    const u32 bst = stk[sp - 2], lx = top - bst;
+                    const int cb = pre_cmp(lpre[sp - 2], tpre, min(lx, lT));
+                    safe = cb > 0;
+                    if (cb == 0 && min(lx, lT) > 32) {
+                        ++nb_try;
+                        const u32 last = min(63u, nf - 1 - g0);
+                        const u32 need = min(lx, rdl(vnx, last) - top);  // the group's reach
+                        const int hit = bst == mxs[0] && top == mys[0] ? 0 : bst == mxs[1] && top == mys[1] ? 1 : -1;
+                        u32 L;
+                        bool ex;
+                        if (hit >= 0 && (mex[hit] || mL[hit] >= need)) {
+                            L = mL[hit];
+                            ex = mex[hit];
+                        } else {
+                            const u32 o0 = max(32u, hit >= 0 ? mL[hit] : 0u);
+                            (void)lyn_less(s, bst, top, top + need, (u32)geo.N, prof ? &nstep : nullptr, min(o0, need),
+                                           L, ex);
+                            const int sl = hit >= 0 ? hit : mold;
+                            mxs[sl] = bst;
+                            mys[sl] = top;
+                            mL[sl] = L;
+                            mex[sl] = ex;
+                            mlt[sl] = ex && L < need ? s[bst + L] < s[top + L] : false;
+                            mold = 1 - sl;
+                        }
+                        if (ex && L < need) {
+                            // x and T' first differ at L (for every T' reaching past L)
+                            if (s[bst + L] > s[top + L]) safe = L < lx;  // x stays larger
+                            else xlim = min(L, lx - 1);
+                        } else {
+                            xlim = min(L, lx - 1);  // T' a prefix of x up to L
+                        }
+                    }
                 }
-                if (safe) {
+                if (safe || xlim) {
+                    nb_lim += xlim ? 1u : 0u;
                     const u32 l0 = t - g0;
                     bool ok = false;
                     if (lane >= l0 && g0 + lane < nf) {
                         const u32 la = vst - top, lb = vnx - vst, m = min(la, lb);
                         const int cr = pre_cmp(tpre, vpr, m);
-                        ok = cr < 0 || (cr == 0 && m <= 32 && la < lb);
+                        bool dec = cr != 0 || m <= 32;
+                        bool lt = cr < 0 || (cr == 0 && m <= 32 && la < lb);
+                        if (!dec && m <= 512) {
+                            // T' and f agree on 32 bytes (periodic data): the lane compares
+                            // the rest itself, 8 bytes per step (the text has 64 bytes of slack)
+                            dec = true;
+                            lt = la < lb;
+                            for (u32 o = 32; o < m; o += 8) {
+                                u64 d = load8u(s, top + o) ^ load8u(s, vst + o);
+                                if (o + 8 > m) d &= (1ull << (8 * (m - o))) - 1ull;
+                                if (d) {
+                                    const u32 k8 = (u32)(__ffsll((long long)d) - 1) >> 3;
+                                    lt = s[top + o + k8] < s[vst + o + k8];
+                                    break;
+                                }
+                            }
+                        }
+                        ok = dec && lt && (safe || vnx - top <= xlim);
                     }
                     const u64 okm = __ballot(ok) >> l0;
                     const u32 k = okm == ~0ull ? 64u : (u32)__ffsll((long long)~okm) - 1;
                     if (k) {
+                        ++nb_hit;
                         t += k;
                         npush += k;
                         nmerge += k;
@@ -792,6 +847,9 @@ __global__ __launch_bounds__(64) void k_duval_merge(Geom geo, u32 cpb, u32 span,
         atomicAdd((unsigned long long*)&prof[18], (unsigned long long)nlyn);
         atomicAdd((unsigned long long*)&prof[19], (unsigned long long)tlyn);
         atomicAdd((unsigned long long*)&prof[20], (unsigned long long)sp);
+        atomicAdd((unsigned long long*)&prof[21], (unsigned long long)nb_try);
+        atomicAdd((unsigned long long*)&prof[22], (unsigned long long)nb_lim);
+        atomicAdd((unsigned long long*)&prof[23], (unsigned long long)nb_hit);
     }
 }
 
@@ -930,9 +988,10 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fsta
         fprintf(stderr, " | merge us per block mean %.1f max %.1f, compares/block %.1f, 512-B steps/block %.1f, "
                 "span factors/block %.1f\n", (double)h[11] / geo.nb / 100.0, (double)h[12] / 100.0,
                 (double)h[13] / geo.nb, (double)h[14] / geo.nb, (double)h[15] / geo.nb);
-        fprintf(stderr, "[kolm] merge per block: pushes %.1f merges %.1f text compares %.1f (%.1f us), final factors %.1f\n",
+        fprintf(stderr, "[kolm] merge per block: pushes %.1f merges %.1f text compares %.1f (%.1f us), final factors %.1f; "
+                "batch: LCP-bounded tries %.1f, bounded %.1f, batches taken %.1f\n",
                 (double)h[16] / geo.nb, (double)h[17] / geo.nb, (double)h[18] / geo.nb, (double)h[19] / geo.nb / 100.0,
-                (double)h[20] / geo.nb);
+                (double)h[20] / geo.nb, (double)h[21] / geo.nb, (double)h[22] / geo.nb, (double)h[23] / geo.nb);
     }
     {
         KScope k(kt, KT_LYNDON, "k_tile_starts", N);
