@@ -50,8 +50,8 @@ struct OpAdd {
 };
 
 // Exclusive scan over the threads of the workgroup (REV: from the last thread down).
-template <bool REV, class Op>
-__device__ inline u32 wg_excl_scan(u32 v, Op op, u32 ident, u32* sh /*[4]*/) {
+template <bool REV, class Op, u32 NW = WG / 64>
+__device__ inline u32 wg_excl_scan(u32 v, Op op, u32 ident, u32* sh /*[NW]*/) {
     const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const u32 incl = REV ? wave_incl_scan_rev(v, op, ident) : wave_incl_scan(v, op, ident);
     const u32 ex = REV ? KOLM_DPP(ident, incl, DPP_WAVE_SHL1, 0xF) : KOLM_DPP(ident, incl, DPP_WAVE_SHR1, 0xF);
@@ -61,7 +61,7 @@ __device__ inline u32 wg_excl_scan(u32 v, Op op, u32 ident, u32* sh /*[4]*/) {
     if (!REV) {
         for (u32 i = 0; i < w; ++i) carry = op(carry, sh[i]);
     } else {
-        for (u32 i = w + 1; i < WG / 64; ++i) carry = op(carry, sh[i]);
+        for (u32 i = w + 1; i < NW; ++i) carry = op(carry, sh[i]);
     }
     __syncthreads();
     return op(carry, ex);
@@ -297,6 +297,10 @@ __global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur_in, c
         u32 nt = c == NCLASS ? (s.len + TILE - 1) / TILE : 0u;
         nt = wave_reduce(nt, OpAddU(), 0u);
         if (lane == 0 && nt) atomicAdd(&ltiles, nt);
+        if (nt) {  // the longest large segment (the host picks the medium sort or the MSD levels)
+            const u32 lm = wave_reduce(c == NCLASS ? (s.len & SEG_LEN) : 0u, OpMaxU(), 0u);
+            if (lane == 0) atomicMax(L.lmax, lm);
+        }
         while (pend) {
             const u32 f = (u32)__ffsll((long long)pend) - 1;
             const int cc = __builtin_amdgcn_readlane(c, f);
@@ -444,6 +448,7 @@ __global__ __launch_bounds__(WG) void k_keygen_large(const LTile* tiles, const L
 __global__ __launch_bounds__(WG) void k_msd_hist(const LTile* tiles, const LSeg* segs, SortArgs a,
                                                  u32 shift, u32 mask, u32* hist, const u32* ndev) {
     if (ndev && blockIdx.x >= *ndev) return;
+    if (a.med && (segs[tiles[blockIdx.x].seg].len & SEG_LEN) <= MED_T) return;  // sorted by the medium form
     __shared__ u32 h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
@@ -466,6 +471,7 @@ __global__ __launch_bounds__(WG) void k_msd_hist(const LTile* tiles, const LSeg*
 __global__ __launch_bounds__(WG) void k_msd_scan(const LSeg* segs, SortArgs a, u32* hist, int last_level,
                                                  Lists L, Level nx, const u32* ndev) {
     if (ndev && blockIdx.x >= *ndev) return;
+    if (a.med && (segs[blockIdx.x].len & SEG_LEN) <= MED_T) return;
     __shared__ u32 sh[WG / 64];
     const LSeg s = segs[blockIdx.x];
     const u32 d = threadIdx.x;
@@ -549,6 +555,7 @@ __global__ __launch_bounds__(WG) void k_msd_scan(const LSeg* segs, SortArgs a, u
 __global__ __launch_bounds__(WG) void k_msd_scatter(const LTile* tiles, const LSeg* segs, SortArgs a,
                                                     u32 shift, u32 width, const u32* hist, const u32* ndev) {
     if (ndev && blockIdx.x >= *ndev) return;
+    if (a.med && (segs[tiles[blockIdx.x].seg].len & SEG_LEN) <= MED_T) return;
     __shared__ u32 wcnt[WG / 64][256];
     __shared__ u32 running[256];
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -602,6 +609,7 @@ __global__ __launch_bounds__(WG) void k_msd_scatter(const LTile* tiles, const LS
 __global__ __launch_bounds__(WG) void k_copy_back(const LTile* tiles, const LSeg* segs, SortArgs a,
                                                   const u32* ndev) {
     if (ndev && blockIdx.x >= *ndev) return;
+    if (a.med && (segs[tiles[blockIdx.x].seg].len & SEG_LEN) <= MED_T) return;
     const LTile t = tiles[blockIdx.x];
     const LSeg s = segs[t.seg];
     const u32 base = s.start + t.k * TILE;
@@ -640,30 +648,52 @@ __device__ inline void reg_stage(KT (&r)[8], u32 tid, u32 k, u32 S) {
 
 __device__ inline u32 SKI(u32 i) { return i + (i >> 6); }
 
-template <int C, class KT>
-__global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, SortArgs a, Lists L) {
+// T elements per workgroup of NT threads (8 per thread).  The medium form (MED: T = 8192,
+// NT = 1024, one segment per workgroup) sorts the large groups of TILE < len <= T of an MSD
+// level list (LSeg records, count in device memory) in one pass instead of the level's
+// hist / scan / scatter / copy launches (which skip those groups).
+template <int C, class KT, u32 T = TILE, u32 NT = WG, bool MED = false>
+__global__ __launch_bounds__(NT) void k_small_sort(const Seg* segs, u32 count, SortArgs a, Lists L,
+                                                   const LSeg* msegs = nullptr, const u32* mcount = nullptr) {
+    static_assert(T == 8 * NT, "8 elements per thread");
+    constexpr u32 NWV = NT / 64;
+    constexpr u32 PT = T / NT;
     constexpr u32 S = 1u << C;
-    constexpr u32 SPT = TILE / S;
+    constexpr u32 SPT = T / S;
     constexpr bool W32 = sizeof(KT) == 4;
     constexpr KT NONEK = ~(KT)0;
     // one pad word per 64: the per-thread 8-element runs (8*tid + e) hit 64 distinct banks
-    __shared__ KT sk[TILE + TILE / 64];
-    __shared__ u32 sa_l[W32 ? TILE : 1];
+    __shared__ KT sk[T + T / 64];
+    __shared__ u32 sa_l[W32 ? T : 1];
     __shared__ Seg ss[SPT];
-    __shared__ u32 sh[WG / 64];
-    __shared__ u32 last_hi[WG];
+    __shared__ u32 sh[NWV];
+    __shared__ u32 last_hi[NT];
     __shared__ u8 ssplit[SPT];  // sub-array split by this round's key
     const u32 tid = threadIdx.x;
-    const u32 first = (a.xcd ? xcd_tile() : blockIdx.x) * SPT;
-    const u32 nthis = min(SPT, count - first);
-    for (u32 i = tid; i < SPT; i += WG) {
-        ss[i] = i < nthis ? segs[first + i] : Seg{0, 0};
-        ssplit[i] = 0;
+    u32 first, nthis;
+    if constexpr (MED) {
+        static_assert(SPT == 1, "one segment per workgroup");
+        if (blockIdx.x >= *mcount) return;
+        const LSeg ls = msegs[blockIdx.x];
+        if ((ls.len & SEG_LEN) > T) return;  // left to the MSD levels
+        first = 0;
+        nthis = 1;
+        if (tid == 0) {
+            ss[0] = Seg{ls.start, ls.len};
+            ssplit[0] = 0;
+        }
+    } else {
+        first = (a.xcd ? xcd_tile() : blockIdx.x) * SPT;
+        nthis = min(SPT, count - first);
+        for (u32 i = tid; i < SPT; i += NT) {
+            ss[i] = i < nthis ? segs[first + i] : Seg{0, 0};
+            ssplit[i] = 0;
+        }
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < PER_THREAD; ++j) {
-        const u32 slot = j * WG + tid;
+    for (int j = 0; j < (int)PT; ++j) {
+        const u32 slot = j * NT + tid;
         const u32 si = slot >> C, k = slot & (S - 1);
         KT key = NONEK;
         if (si < nthis && k < (ss[si].len & SEG_LEN)) {
@@ -693,8 +723,8 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
             for (u32 j = k >> 1; j >= 8; j >>= 1) {
                 const u32 lj = 31 - __clz(j);
 #pragma unroll
-                for (int q0 = 0; q0 < TILE / 2 / WG; ++q0) {
-                    const u32 q = q0 * WG + tid;
+                for (int q0 = 0; q0 < (int)(T / 2 / NT); ++q0) {
+                    const u32 q = q0 * NT + tid;
                     const u32 i = ((q >> lj) << (lj + 1)) | (q & (j - 1));
                     const u32 l = i + j;
                     const bool up = (k == S) || ((i & k) == 0);
@@ -741,16 +771,16 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
         if (head[e]) agg = 8 * tid + e;
         loc[e] = agg;
     }
-    const u32 carry = wg_excl_scan<false>(agg, OpMax(), 0u, sh);
+    const u32 carry = wg_excl_scan<false, OpMax, NWV>(agg, OpMax(), 0u, sh);
     u32 start_idx[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) start_idx[e] = loc[e] > carry ? loc[e] : carry;
     // run end: exclusive suffix min of stop indices
-    u32 sagg = TILE;
+    u32 sagg = T;
 #pragma unroll
     for (int e = 0; e < 8; ++e)
         if (stop[e] && (u32)(8 * tid + e) < sagg) sagg = 8 * tid + e;
-    const u32 scarry = wg_excl_scan<true>(sagg, OpMin(), (u32)TILE, sh);
+    const u32 scarry = wg_excl_scan<true, OpMin, NWV>(sagg, OpMin(), (u32)T, sh);
     u32 nxt[8];
     u32 run_min = scarry;
 #pragma unroll
@@ -762,8 +792,8 @@ __global__ __launch_bounds__(WG) void k_small_sort(const Seg* segs, u32 count, S
     u32 nnew = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) nnew += (valid[e] && head[e] && nxt[e] - (8 * tid + e) >= 2) ? 1u : 0u;
-    const u32 my_off = wg_excl_scan<false>(nnew, OpAdd(), 0u, sh);
-    if (tid == WG - 1) last_hi[0] = my_off + nnew;  // reuse LDS: workgroup total
+    const u32 my_off = wg_excl_scan<false, OpAdd, NWV>(nnew, OpAdd(), 0u, sh);
+    if (tid == NT - 1) last_hi[0] = my_off + nnew;  // reuse LDS: workgroup total
     __syncthreads();
     const u32 total_new = last_hi[0];
     __syncthreads();
@@ -1039,6 +1069,14 @@ void launch_small_sort(int c, const Seg* segs, u32 count, const SortArgs& a, con
         case 11: small_sort_c<11>(segs, count, a, L, s); break;
         default: break;
     }
+}
+void launch_med_sort(const LSeg* segs, u32 nseg, const u32* ndev, const SortArgs& a, const Lists& L,
+                     hipStream_t s) {
+    if (!nseg || !a.med) return;
+    if (a.key_bits + 13 <= 31)
+        k_small_sort<13, u32, MED_T, MED_T / 8, true><<<nseg, MED_T / 8, 0, s>>>(nullptr, 0, a, L, segs, ndev);
+    else
+        k_small_sort<13, u64, MED_T, MED_T / 8, true><<<nseg, MED_T / 8, 0, s>>>(nullptr, 0, a, L, segs, ndev);
 }
 void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists& L, hipStream_t s) {
     if (count) k_finalize_eq<<<count, WG, 0, s>>>(eq, a, L);

@@ -120,6 +120,7 @@ enum : int {
     C_CLSE = 24,     // 12 slots: elements per small class
     C_L0ELEM = 36,
     C_L1ELEM = 37,
+    C_LMAX = 38,     // the round's longest large segment
     C_CDC = 40,      // FastCDC cut count
     C_N = 48,
     H_RSUM = C_N,    // host mirror only (2 words): summed per-block cyclic rounds
@@ -337,6 +338,13 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
     u32* blk_done = c->get<u32>("blk_done", geo.nb);
     a.blk_done = blk_done;
     a.cyclic = cyclic ? 1 : 0;
+    // large groups of at most MED_T elements: one-workgroup LDS sort instead of the MSD levels
+    // (KOLM_MED_SORT=0: every large group through the MSD levels)
+    // (batches of fewer than 64 blocks: its 71 KB of LDS would wait for the LZ77 parse's
+    // workgroups on a full batch, whose large groups are few anyway — 256 MiB text: 41.8 vs
+    // 37.5 ms per step with it)
+    static const int med = getenv("KOLM_MED_SORT") ? atoi(getenv("KOLM_MED_SORT")) : -1;
+    a.med = (med > 0 || (med < 0 && geo.nb < 64)) ? 1u : 0u;
 
     u32* cnt = c->get<u32>("counters", C_N);
     Lists L{};
@@ -355,6 +363,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
     L.eq_cnt = cnt + C_EQ;
     L.misc = cnt + C_ACTIVE;
     L.cls_elems = cnt + C_CLSE;
+    L.lmax = cnt + C_LMAX;
     L.eq = c->get<Seg>("eq", N / TILE + 16);
     const u64 seg_cap = N / 2 + geo.nb + 16;
     Seg* segA = c->get<Seg>("segA", seg_cap);
@@ -494,6 +503,13 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
         const u32 nelem0 = h[C_L0ELEM], nseg0 = h[C_L0SEG], ntiles0 = h[C_L0TILE];
         u32 hi = a.initial ? (cyclic ? 32u : 27u) : kb_rank;
         int lvl = 0;
+        if (a.med && nseg0 && h[C_LMAX] <= MED_T) {
+            // every large group fits the medium sort: one launch, no MSD level (its runs go to
+            // the next round's list directly, so the class counts stay as classify left them)
+            TScope t(c, KOLM_KT_SMALLSORT, "k_small_sort<13> (medium)", (u64)nelem0 * 16);
+            launch_med_sort(lv[0].segs, nseg0, lv[0].nseg, a, L, s);
+            hi = 0;
+        }
         for (; nseg0 && hi; ++lvl) {
             const u32 width = std::min<u32>(8, hi);
             const u32 shift = hi - width;
@@ -507,6 +523,10 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             KOLM_HIP_CHECK(hipMemsetAsync(ln.nseg, 0, sizeof(u32), s));
             KOLM_HIP_CHECK(hipMemsetAsync(ln.ntiles, 0, sizeof(u32), s));
             KOLM_HIP_CHECK(hipMemsetAsync(ln.nelem, 0, sizeof(u32), s));
+            if (a.med) {
+                TScope t(c, KOLM_KT_SMALLSORT, "k_small_sort<13> (medium)", (u64)nelem0 * 16);
+                launch_med_sort(lc.segs, nseg, lc.nseg, a, L, s);
+            }
             {
                 TScope t(c, KOLM_KT_MSD, "k_msd_hist", (u64)nelem0 * 4 + (u64)ntiles0 * 1024);
                 launch_msd_hist(lc.tiles, ntiles, dtile, lc.segs, a, shift, width, hist, s);

@@ -227,6 +227,7 @@ struct SortArgs {
     Factors fac;       // cyclic: Lyndon factor starts per block
     const u8* FEd;     // cyclic: min(distance to the factor end, 255): fac is read only near the end
     u32* blk_split;    // [nb] set to 1 when a group of block b split this round
+    u32 med;           // large groups of at most MED_T elements sorted by the medium form (launch_med_sort)
     const u32* blk_done;  // [nb] cyclic: block converged (no further splits possible)
     int cyclic;
     int initial;       // round 0: keys are packed characters
@@ -259,6 +260,7 @@ struct Lists {
     Seg* eq;
     u32* misc;             // [1] active elements of the round
     u32* cls_elems;        // [NCLASS] elements per small class (timing/bytes bookkeeping)
+    u32* lmax;             // [1] the round's longest large segment (k_classify)
 };
 
 struct Level {
@@ -281,6 +283,10 @@ void launch_keypos(const SortArgs& a, u32* KP, hipStream_t s);
 void launch_keygen_small(int c, const Seg* segs, u32 count, const SortArgs& a, hipStream_t s);
 void launch_keygen_large(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
                          hipStream_t s);
+constexpr u32 MED_T = 8192;  // the medium sort's capacity (one 1024-thread workgroup per large group)
+// the medium sort of an MSD level's groups of at most MED_T elements (count in ndev when set)
+void launch_med_sort(const LSeg* segs, u32 nseg, const u32* ndev, const SortArgs& a, const Lists& L,
+                     hipStream_t s);
 // MSD levels: ntiles / nseg is the count, or (ndev set) a bound with the count in ndev
 void launch_msd_hist(const LTile* tiles, u32 ntiles, const u32* ndev, const LSeg* segs, const SortArgs& a,
                      u32 shift, u32 width, u32* hist, hipStream_t s);
