@@ -648,102 +648,18 @@ __device__ inline void reg_stage(KT (&r)[8], u32 tid, u32 k, u32 S) {
 
 __device__ inline u32 SKI(u32 i) { return i + (i >> 6); }
 
-// T elements per workgroup of NT threads (8 per thread).  The medium form (MED: T = 8192,
-// NT = 1024, one segment per workgroup) sorts the large groups of TILE < len <= T of an MSD
-// level list (LSeg records, count in device memory) in one pass instead of the level's
-// hist / scan / scatter / copy launches (which skip those groups).
-template <int C, class KT, u32 T = TILE, u32 NT = WG, bool MED = false>
-__global__ __launch_bounds__(NT) void k_small_sort(const Seg* segs, u32 count, SortArgs a, Lists L,
-                                                   const LSeg* msegs = nullptr, const u32* mcount = nullptr) {
-    static_assert(T == 8 * NT, "8 elements per thread");
+// Shared tail of the small and medium sorts: r[8] = this thread's sorted words 8 tid .. 8 tid + 7
+// of sub-arrays of S slots (KT: (key << C | index) with sa_l, or (key << 32 | position));
+// runs of equal key -> RK of their heads, SA where a sub-array split, new groups of >= 2
+// elements to the next round, split flags.
+template <int C, class KT, u32 T, u32 NT>
+__device__ inline void sort_epilogue(KT (&r)[8], const Seg* ss, u8* ssplit, const u32* sa_l, u32* sh, u32* last_hi,
+                                     const SortArgs& a, const Lists& L) {
     constexpr u32 NWV = NT / 64;
-    constexpr u32 PT = T / NT;
     constexpr u32 S = 1u << C;
-    constexpr u32 SPT = T / S;
     constexpr bool W32 = sizeof(KT) == 4;
     constexpr KT NONEK = ~(KT)0;
-    // one pad word per 64: the per-thread 8-element runs (8*tid + e) hit 64 distinct banks
-    __shared__ KT sk[T + T / 64];
-    __shared__ u32 sa_l[W32 ? T : 1];
-    __shared__ Seg ss[SPT];
-    __shared__ u32 sh[NWV];
-    __shared__ u32 last_hi[NT];
-    __shared__ u8 ssplit[SPT];  // sub-array split by this round's key
     const u32 tid = threadIdx.x;
-    u32 first, nthis;
-    if constexpr (MED) {
-        static_assert(SPT == 1, "one segment per workgroup");
-        if (blockIdx.x >= *mcount) return;
-        const LSeg ls = msegs[blockIdx.x];
-        if ((ls.len & SEG_LEN) > T) return;  // left to the MSD levels
-        first = 0;
-        nthis = 1;
-        if (tid == 0) {
-            ss[0] = Seg{ls.start, ls.len};
-            ssplit[0] = 0;
-        }
-    } else {
-        first = (a.xcd ? xcd_tile() : blockIdx.x) * SPT;
-        nthis = min(SPT, count - first);
-        for (u32 i = tid; i < SPT; i += NT) {
-            ss[i] = i < nthis ? segs[first + i] : Seg{0, 0};
-            ssplit[i] = 0;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < (int)PT; ++j) {
-        const u32 slot = j * NT + tid;
-        const u32 si = slot >> C, k = slot & (S - 1);
-        KT key = NONEK;
-        if (si < nthis && k < (ss[si].len & SEG_LEN)) {
-            const u32 g = ss[si].start + k;
-            // (gathering KP[SA[g]] here instead of in k_keygen_small measured slower: the
-            // dependent gather is exposed at the sort's LDS-limited occupancy)
-            const u32 p = a.SA[g];
-            const u32 kv = a.K2[g];
-            if constexpr (W32) {
-                key = (kv << C) | k;
-                sa_l[slot] = p;
-            } else {
-                key = ((u64)kv << 32) | p;
-            }
-        }
-        sk[SKI(slot)] = key;
-    }
-    __syncthreads();
-    KT r[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) r[e] = sk[SKI(8 * tid + e)];
-    for (u32 k = 2; k <= S; k <<= 1) {
-        if (k > 8) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) sk[SKI(8 * tid + e)] = r[e];
-            __syncthreads();
-            for (u32 j = k >> 1; j >= 8; j >>= 1) {
-                const u32 lj = 31 - __clz(j);
-#pragma unroll
-                for (int q0 = 0; q0 < (int)(T / 2 / NT); ++q0) {
-                    const u32 q = q0 * NT + tid;
-                    const u32 i = ((q >> lj) << (lj + 1)) | (q & (j - 1));
-                    const u32 l = i + j;
-                    const bool up = (k == S) || ((i & k) == 0);
-                    const KT x = sk[SKI(i)], y = sk[SKI(l)];
-                    if ((x > y) == up) {
-                        sk[SKI(i)] = y;
-                        sk[SKI(l)] = x;
-                    }
-                }
-                __syncthreads();
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) r[e] = sk[SKI(8 * tid + e)];
-            __syncthreads();
-        }
-        if (k >= 8) reg_stage<4>(r, tid, k, S);
-        if (k >= 4) reg_stage<2>(r, tid, k, S);
-        reg_stage<1>(r, tid, k, S);
-    }
     constexpr u32 HS = W32 ? C : 32;  // key = word >> HS
     // runs of equal key inside each sub-array
     last_hi[tid] = (u32)(r[7] >> HS);
@@ -822,6 +738,207 @@ __global__ __launch_bounds__(NT) void k_small_sort(const Seg* segs, u32 count, S
             if (kk > 0) a.blk_split[a.geo.block_of(sg.start)] = 1;
         }
     }
+}
+
+template <int C, class KT, u32 T = TILE, u32 NT = WG>
+__global__ __launch_bounds__(NT) void k_small_sort(const Seg* segs, u32 count, SortArgs a, Lists L) {
+    static_assert(T == 8 * NT, "8 elements per thread");
+    constexpr u32 NWV = NT / 64;
+    constexpr u32 PT = T / NT;
+    constexpr u32 S = 1u << C;
+    constexpr u32 SPT = T / S;
+    constexpr bool W32 = sizeof(KT) == 4;
+    constexpr KT NONEK = ~(KT)0;
+    // one pad word per 64: the per-thread 8-element runs (8*tid + e) hit 64 distinct banks
+    __shared__ KT sk[T + T / 64];
+    __shared__ u32 sa_l[W32 ? T : 1];
+    __shared__ Seg ss[SPT];
+    __shared__ u32 sh[NWV];
+    __shared__ u32 last_hi[NT];
+    __shared__ u8 ssplit[SPT];  // sub-array split by this round's key
+    const u32 tid = threadIdx.x;
+    const u32 first = (a.xcd ? xcd_tile() : blockIdx.x) * SPT;
+    const u32 nthis = min(SPT, count - first);
+    for (u32 i = tid; i < SPT; i += NT) {
+        ss[i] = i < nthis ? segs[first + i] : Seg{0, 0};
+        ssplit[i] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < (int)PT; ++j) {
+        const u32 slot = j * NT + tid;
+        const u32 si = slot >> C, k = slot & (S - 1);
+        KT key = NONEK;
+        if (si < nthis && k < (ss[si].len & SEG_LEN)) {
+            const u32 g = ss[si].start + k;
+            // (gathering KP[SA[g]] here instead of in k_keygen_small measured slower: the
+            // dependent gather is exposed at the sort's LDS-limited occupancy)
+            const u32 p = a.SA[g];
+            const u32 kv = a.K2[g];
+            if constexpr (W32) {
+                key = (kv << C) | k;
+                sa_l[slot] = p;
+            } else {
+                key = ((u64)kv << 32) | p;
+            }
+        }
+        sk[SKI(slot)] = key;
+    }
+    __syncthreads();
+    KT r[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] = sk[SKI(8 * tid + e)];
+    for (u32 k = 2; k <= S; k <<= 1) {
+        if (k > 8) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sk[SKI(8 * tid + e)] = r[e];
+            __syncthreads();
+            for (u32 j = k >> 1; j >= 8; j >>= 1) {
+                const u32 lj = 31 - __clz(j);
+#pragma unroll
+                for (int q0 = 0; q0 < (int)(T / 2 / NT); ++q0) {
+                    const u32 q = q0 * NT + tid;
+                    const u32 i = ((q >> lj) << (lj + 1)) | (q & (j - 1));
+                    const u32 l = i + j;
+                    const bool up = (k == S) || ((i & k) == 0);
+                    const KT x = sk[SKI(i)], y = sk[SKI(l)];
+                    if ((x > y) == up) {
+                        sk[SKI(i)] = y;
+                        sk[SKI(l)] = x;
+                    }
+                }
+                __syncthreads();
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) r[e] = sk[SKI(8 * tid + e)];
+            __syncthreads();
+        }
+        if (k >= 8) reg_stage<4>(r, tid, k, S);
+        if (k >= 4) reg_stage<2>(r, tid, k, S);
+        reg_stage<1>(r, tid, k, S);
+    }
+    sort_epilogue<C, KT, T, NT>(r, ss, ssplit, sa_l, sh, last_hi, a, L);
+}
+
+// Medium sort (batches of few blocks): one 1024-thread workgroup sorts one large group of
+// TILE < len <= MED_T elements of an MSD level list by its key (K2), in place of the level's
+// hist / scan / scatter / copy launches.  Stable LSD radix over 8-bit digits in LDS: keys and
+// 16-bit element indices ping-pong between two buffers; per 1024-element chunk each wave ranks
+// its lanes per digit with 8 ballots (as k_msd_scatter), the waves' digit counts combine in
+// chunk / wave order, so equal keys keep their index (= position) order.  The sorted words
+// (key << 32 | position) then go through the small sorts' epilogue.
+constexpr u32 MED_NT = MED_T / 8;  // 1024 threads
+__global__ __launch_bounds__(MED_NT) void k_med_sort(const LSeg* msegs, const u32* mcount, SortArgs a, Lists L) {
+    constexpr u32 NWV = MED_NT / 64;
+    __shared__ u32 kb[2][MED_T];
+    __shared__ u16 ib[2][MED_T];
+    __shared__ u32 wcnt[NWV][256];
+    __shared__ u32 base[256];
+    __shared__ u32 running[256];
+    __shared__ Seg ss[1];
+    __shared__ u8 ssplit[1];
+    __shared__ u32 sh[NWV];
+    __shared__ u32 last_hi[MED_NT];
+    if (blockIdx.x >= *mcount) return;
+    const LSeg ls = msegs[blockIdx.x];
+    const u32 n = ls.len & SEG_LEN;
+    if (n > MED_T) return;  // left to the MSD levels
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) {
+        ss[0] = Seg{ls.start, ls.len};
+        ssplit[0] = 0;
+    }
+    for (u32 i = tid; i < n; i += MED_NT) {
+        kb[0][i] = a.K2[ls.start + i];
+        ib[0][i] = (u16)i;
+    }
+    const u64 lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
+    u32 cur = 0;
+    for (u32 shift = 0; shift < a.key_bits; shift += 8, cur ^= 1) {
+        const u32 width = min(8u, a.key_bits - shift), dmask = (1u << width) - 1;
+        if (tid < 256) {
+            base[tid] = 0;
+            running[tid] = 0;
+        }
+        for (u32 i = tid; i < NWV * 256; i += MED_NT) (&wcnt[0][0])[i] = 0;
+        __syncthreads();
+        // digit totals without LDS atomics (a group's keys often share their digits: 8192
+        // atomics on one counter serialise): per wave and chunk, one add per distinct digit
+        for (u32 c0 = 0; c0 < n; c0 += MED_NT) {
+            const u32 i = c0 + tid;
+            const bool v = i < n;
+            const u32 dg = v ? (kb[cur][i] >> shift) & dmask : 0u;
+            u64 m = __ballot(v);
+            for (u32 bit = 0; bit < width; ++bit) {
+                const u64 bal = __ballot((dg >> bit) & 1u);
+                m &= ((dg >> bit) & 1u) ? bal : ~bal;
+            }
+            if (v && __popcll(m & lt_mask) == 0) wcnt[w][dg] += __popcll(m);
+        }
+        __syncthreads();
+        if (tid < 256) {
+            u32 t = 0;
+            for (u32 q = 0; q < NWV; ++q) {
+                t += wcnt[q][tid];
+                wcnt[q][tid] = 0;
+            }
+            base[tid] = t;
+        }
+        __syncthreads();
+        if (tid < 64) {  // exclusive scan of the 256 digit counts by wave 0 (4 per lane)
+            const u32 c0 = base[4 * tid], c1 = base[4 * tid + 1], c2 = base[4 * tid + 2], c3 = base[4 * tid + 3];
+            const u32 t4 = c0 + c1 + c2 + c3;
+            const u32 ex = wave_incl_scan(t4, OpAddU(), 0u) - t4;
+            base[4 * tid] = ex;
+            base[4 * tid + 1] = ex + c0;
+            base[4 * tid + 2] = ex + c0 + c1;
+            base[4 * tid + 3] = ex + c0 + c1 + c2;
+        }
+        __syncthreads();
+        for (u32 c0 = 0; c0 < n; c0 += MED_NT) {
+            const u32 i = c0 + tid;
+            const bool v = i < n;
+            u32 key = 0, idx = 0, dg = 0;
+            if (v) {
+                key = kb[cur][i];
+                idx = ib[cur][i];
+                dg = (key >> shift) & dmask;
+            }
+            u64 m = __ballot(v);
+            for (u32 bit = 0; bit < width; ++bit) {
+                const u64 bal = __ballot((dg >> bit) & 1u);
+                m &= ((dg >> bit) & 1u) ? bal : ~bal;
+            }
+            const u32 rank = __popcll(m & lt_mask);
+            if (v && rank == 0) wcnt[w][dg] = __popcll(m);
+            __syncthreads();
+            if (v) {
+                u32 pre = base[dg] + running[dg];
+                for (u32 q = 0; q < w; ++q) pre += wcnt[q][dg];
+                kb[cur ^ 1][pre + rank] = key;
+                ib[cur ^ 1][pre + rank] = (u16)idx;
+            }
+            __syncthreads();
+            if (tid < 256) {
+                u32 add = 0;
+                for (u32 q = 0; q < NWV; ++q) {
+                    add += wcnt[q][tid];
+                    wcnt[q][tid] = 0;
+                }
+                running[tid] += add;
+            }
+            __syncthreads();
+        }
+    }
+    // this thread's sorted words 8 tid .. 8 tid + 7: (key << 32 | position)
+    u64 r[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const u32 i = 8 * tid + e;
+        r[e] = i < n ? ((u64)kb[cur][i] << 32) | a.SA[ls.start + ib[cur][i]] : ~0ull;
+    }
+    __syncthreads();
+    sort_epilogue<13, u64, MED_T, MED_NT>(r, ss, ssplit, nullptr, sh, last_hi, a, L);
 }
 
 // Tiny segments (class C <= TINY_C, at most 16 elements): one thread per segment, the
@@ -1073,10 +1190,7 @@ void launch_small_sort(int c, const Seg* segs, u32 count, const SortArgs& a, con
 void launch_med_sort(const LSeg* segs, u32 nseg, const u32* ndev, const SortArgs& a, const Lists& L,
                      hipStream_t s) {
     if (!nseg || !a.med) return;
-    if (a.key_bits + 13 <= 31)
-        k_small_sort<13, u32, MED_T, MED_T / 8, true><<<nseg, MED_T / 8, 0, s>>>(nullptr, 0, a, L, segs, ndev);
-    else
-        k_small_sort<13, u64, MED_T, MED_T / 8, true><<<nseg, MED_T / 8, 0, s>>>(nullptr, 0, a, L, segs, ndev);
+    k_med_sort<<<nseg, MED_NT, 0, s>>>(segs, ndev, a, L);
 }
 void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists& L, hipStream_t s) {
     if (count) k_finalize_eq<<<count, WG, 0, s>>>(eq, a, L);

@@ -476,7 +476,8 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             // Dense rounds: keys by position first (sequential pass), then one gather per
             // slot; sparse rounds gather the key inputs per active slot directly.
             a.KP = nullptr;
-            if ((u64)h[C_ACTIVE] * 8 > N) {
+            static const u64 ddiv = getenv("KOLM_DENSE_DIV") ? strtoull(getenv("KOLM_DENSE_DIV"), nullptr, 10) : 8;  // A/B
+            if ((u64)h[C_ACTIVE] * ddiv > N) {
                 u32* KP = c->get<u32>("KP", N);
                 // cyclic: FEd 1 + RK 4 + KP 4 (factor starts only within h of a factor end); linear: RK 4 + KP 4
                 TScope t(c, KOLM_KT_KEYGEN, "k_keypos", N * (cyclic ? 9 : 8));
