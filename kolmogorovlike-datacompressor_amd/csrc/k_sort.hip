@@ -1054,17 +1054,18 @@ __global__ void k_single(const Seg* segs, u32 count, SortArgs a) {
     }
 }
 
+// gridDim.y workgroups share one run (periodic data: runs of 10^5-10^6 equal keys)
 __global__ __launch_bounds__(WG) void k_finalize_eq(const Seg* eq, SortArgs a, Lists L) {
     const Seg s = eq[blockIdx.x];
     const u32 len = s.len & SEG_LEN;
     // a FIRST run keeps its group's rank after round 0
     if (a.initial || !(s.len & SEG_FIRST)) {
-        for (u32 i = threadIdx.x; i < len; i += WG) {
+        for (u32 i = blockIdx.y * WG + threadIdx.x; i < len; i += gridDim.y * WG) {
             const u32 p = a.SA[s.start + i];
             a.RK[p] = s.start;
         }
     }
-    if (threadIdx.x == 0) L.next[atomicAdd(L.next_cnt, 1u)] = Seg{s.start, len};
+    if (blockIdx.y == 0 && threadIdx.x == 0) L.next[atomicAdd(L.next_cnt, 1u)] = Seg{s.start, len};
 }
 
 // done[b] = 1 + the round in which block b stopped splitting (0 while it still splits)
@@ -1193,7 +1194,7 @@ void launch_med_sort(const LSeg* segs, u32 nseg, const u32* ndev, const SortArgs
     k_med_sort<<<nseg, MED_NT, 0, s>>>(segs, ndev, a, L);
 }
 void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists& L, hipStream_t s) {
-    if (count) k_finalize_eq<<<count, WG, 0, s>>>(eq, a, L);
+    if (count) k_finalize_eq<<<dim3(count, 32), WG, 0, s>>>(eq, a, L);
 }
 void launch_rounds_sum(const u32* blk_done, u32 nb, u32 rounds, u64* out, hipStream_t s) {
     KOLM_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(u64), s));
