@@ -150,6 +150,59 @@ __global__ __launch_bounds__(WG) void k_lsd_scan(LsdGeom g, u32* hist) {
     }
 }
 
+// The same scan with four threads per digit (1024-thread workgroup), each over a quarter of
+// the block's tiles: the per-digit dependent chains are a quarter as long (the scan is
+// latency-bound: one workgroup per block, 256 tiles of loads per thread).
+__global__ __launch_bounds__(4 * WG) void k_lsd_scan4(LsdGeom g, u32* hist) {
+    __shared__ u32 pt[4][256];
+    __shared__ u32 sh[4];
+    const u32 b = blockIdx.x, d = threadIdx.x & 255, q = threadIdx.x >> 8;
+    const u64 t0 = (u64)b * g.tpb;
+    const u32 per = (g.tpb + 3) / 4, k0 = min(g.tpb, q * per), k1 = min(g.tpb, k0 + per);
+    constexpr u32 B = 16;
+    u32 acc = 0;
+    for (u32 k = k0; k < k1; k += B) {
+        u32 v[B];
+#pragma unroll
+        for (u32 j = 0; j < B; ++j) v[j] = k + j < k1 ? hist[(t0 + k + j) * 256 + d] : 0u;
+#pragma unroll
+        for (u32 j = 0; j < B; ++j) acc += v[j];
+    }
+    pt[q][d] = acc;
+    __syncthreads();
+    // digit totals -> exclusive scan over the 256 digits (waves 0..3), then each part's start
+    u32 tot = 0, incl = 0;
+    if (q == 0) {
+        tot = pt[0][d] + pt[1][d] + pt[2][d] + pt[3][d];
+        incl = wave_incl_scan(tot, OpAddU(), 0u);
+        if ((d & 63) == 63) sh[d >> 6] = incl;
+    }
+    __syncthreads();
+    if (q == 0) {
+        u32 carry = 0;
+        for (u32 i = 0; i < (d >> 6); ++i) carry += sh[i];
+        const u32 c0 = pt[0][d], c1 = pt[1][d], c2 = pt[2][d];
+        const u32 base = g.geo.base(b) + carry + incl - tot;
+        pt[0][d] = base;
+        pt[1][d] = base + c0;
+        pt[2][d] = base + c0 + c1;
+        pt[3][d] = base + c0 + c1 + c2;
+    }
+    __syncthreads();
+    u32 run = pt[q][d];
+    for (u32 k = k0; k < k1; k += B) {
+        u32 v[B];
+#pragma unroll
+        for (u32 j = 0; j < B; ++j) v[j] = k + j < k1 ? hist[(t0 + k + j) * 256 + d] : 0u;
+#pragma unroll
+        for (u32 j = 0; j < B; ++j)
+            if (k + j < k1) {
+                hist[(t0 + k + j) * 256 + d] = run;
+                run += v[j];
+            }
+    }
+}
+
 // Stable scatter of one tile by digit P: element order e = j*WG + tid; each wave ranks
 // its 64 elements per digit with ballots, per-wave counts are combined in (j, wave)
 // order.  SRC_KP reads the keys by position (positions implicit).
@@ -751,7 +804,15 @@ void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kou
     }
     {
         KScope k(kt, KT_LSD, "k_lsd_scan", 3 * H);
-        k_lsd_scan<<<g.geo.nb, WG, 0, s>>>(g, hist);
+        // four threads per digit for batches of fewer than 64 blocks (a latency-bound workgroup
+        // per block; on full batches the 1024-thread workgroups wait beside the LZ77 parse:
+        // 256 MiB LSD 18.4 -> 19.2 ms with them).  KOLM_LSD_SCAN4 = 0 / 1 forces it.
+        static const int s4e = getenv("KOLM_LSD_SCAN4") ? atoi(getenv("KOLM_LSD_SCAN4")) : -1;
+        const bool s4 = s4e > 0 || (s4e < 0 && g.geo.nb < 64);
+        if (s4)
+            k_lsd_scan4<<<g.geo.nb, 4 * WG, 0, s>>>(g, hist);
+        else
+            k_lsd_scan<<<g.geo.nb, WG, 0, s>>>(g, hist);
     }
     {
         // key + position in (the first pass reads the key by position only) and out; G: + the gather
@@ -858,7 +919,11 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
     }
     if (win) {
         const u32 nwin = (geo.bs + R0_WIN - 1) / R0_WIN;
-        k_lsd_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);  // window counts -> pair offsets
+        static const int s4e = getenv("KOLM_LSD_SCAN4") ? atoi(getenv("KOLM_LSD_SCAN4")) : -1;
+        if (s4e > 0 || (s4e < 0 && geo.nb < 64))
+            k_lsd_scan4<<<geo.nb, 4 * WG, 0, s>>>(g, t.hist);  // window counts -> pair offsets
+        else
+            k_lsd_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
         {
             // SA 4 read, pairs 4 written (+ head masks, 8 B per new segment)
             KScope k(kt, KT_LSD, "k_r0_final", 8 * N);
