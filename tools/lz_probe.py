@@ -20,7 +20,7 @@ def main():
     part = int(sys.argv[3]) if len(sys.argv) > 3 else -1  # one 1 MiB block of the input only
     data = {"mixed": datagen.mixed_corpus, "gradient": lambda: datagen.gradient_bmp()[: 1 << 20],
             "wav": datagen.sine_wav, "checker": datagen.checker_bmp,
-            "text": lambda: datagen.enwik_like(256 << 20)}[kind]()
+            "text": lambda: datagen.enwik_like(256 << 20), "text32": lambda: datagen.enwik_like(32 << 20)}[kind]()
     if part >= 0:
         data = data[part << 20:(part + 1) << 20]
     torch.cuda.init()
