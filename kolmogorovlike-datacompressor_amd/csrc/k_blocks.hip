@@ -249,8 +249,8 @@ __device__ inline void dprof(u64* prof, u32 k, u64& last) {
         last = now;
     }
 }
-// NT threads (of DUVAL_CH bytes each) per span: 256 (32 KiB spans), or 64 (8 KiB, batches of
-// few blocks: duval_span_bytes)
+// NT threads (of DUVAL_CH bytes each) per span: 64 (8 KiB spans, the default: duval_span_bytes)
+// or 256 (32 KiB)
 template <u32 NT>
 __global__ __launch_bounds__(NT) void k_duval_span(Geom geo, u32 spb, const u8* s, u32* fstart, uint4* fpre,
                                                    u32* nfac, u64* prof) {
@@ -944,14 +944,15 @@ u64* dprof_buf() {
 
 // Lyndon factorisation of every block (parallel Duval + merge) -> factor-start lists,
 // flags and FEd.
-// Bytes per Duval span: DUVAL_SPAN (32 KiB), or 8 KiB (64-thread workgroups, 4x more of them)
-// for batches of fewer than 64 blocks, whose few span workgroups otherwise leave most CUs idle
-// (config 5: span pass 1.82 -> 1.19 ms, merge 0.18 -> 0.41 ms for 4x more span factorisations,
-// 8.82 -> 8.54 ms per call; config 2 2.35 -> 2.27 ms).  KOLM_DUVAL_SPAN = 8192 / 32768 forces it.
+// Bytes per Duval span: 8 KiB (64-thread workgroups, 4x as many as 32 KiB spans) for every batch:
+// the span pass's tree levels are latency-bound per workgroup, and the merge absorbs the extra
+// span factorisations in batches.  Config 5: span 1.82 -> 1.19 ms, merge 0.18 -> 0.41 ms, 8.82 ->
+// 8.54 ms per call; 256 MiB text (two alternating A/B runs): Lyndon family 4.37 -> 3.94 ms, step
+// 37.08 -> 36.58 ms.  KOLM_DUVAL_SPAN = 32768 restores DUVAL_SPAN.
 u32 duval_span_bytes(const Geom& geo) {
+    (void)geo;
     static const u32 force = getenv("KOLM_DUVAL_SPAN") ? (u32)atoi(getenv("KOLM_DUVAL_SPAN")) : 0u;
-    if (force == DUVAL_CH * 64 || force == DUVAL_SPAN) return force;
-    return geo.nb < 64 ? DUVAL_CH * 64 : DUVAL_SPAN;
+    return force == DUVAL_SPAN ? DUVAL_SPAN : DUVAL_CH * 64;
 }
 
 void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fstart, uint4* fpre, u32* nfac,
