@@ -150,15 +150,17 @@ __global__ __launch_bounds__(WG) void k_lsd_scan(LsdGeom g, u32* hist) {
     }
 }
 
-// The same scan with four threads per digit (1024-thread workgroup), each over a quarter of
-// the block's tiles: the per-digit dependent chains are a quarter as long (the scan is
+// The same scan with NP threads per digit (NP * 256-thread workgroup), each over 1 / NP of
+// the block's tiles: the per-digit dependent chains are 1 / NP as long (the scan is
 // latency-bound: one workgroup per block, 256 tiles of loads per thread).
-__global__ __launch_bounds__(4 * WG) void k_lsd_scan4(LsdGeom g, u32* hist) {
-    __shared__ u32 pt[4][256];
+template <u32 NP>
+__global__ __launch_bounds__(NP * WG) void k_lsd_scanp(LsdGeom g, u32* hist) {
+    static_assert(NP == 2 || NP == 4, "2 or 4 parts");
+    __shared__ u32 pt[NP][256];
     __shared__ u32 sh[4];
     const u32 b = blockIdx.x, d = threadIdx.x & 255, q = threadIdx.x >> 8;
     const u64 t0 = (u64)b * g.tpb;
-    const u32 per = (g.tpb + 3) / 4, k0 = min(g.tpb, q * per), k1 = min(g.tpb, k0 + per);
+    const u32 per = (g.tpb + NP - 1) / NP, k0 = min(g.tpb, q * per), k1 = min(g.tpb, k0 + per);
     constexpr u32 B = 16;
     u32 acc = 0;
     for (u32 k = k0; k < k1; k += B) {
@@ -173,7 +175,7 @@ __global__ __launch_bounds__(4 * WG) void k_lsd_scan4(LsdGeom g, u32* hist) {
     // digit totals -> exclusive scan over the 256 digits (waves 0..3), then each part's start
     u32 tot = 0, incl = 0;
     if (q == 0) {
-        tot = pt[0][d] + pt[1][d] + pt[2][d] + pt[3][d];
+        for (u32 i = 0; i < NP; ++i) tot += pt[i][d];
         incl = wave_incl_scan(tot, OpAddU(), 0u);
         if ((d & 63) == 63) sh[d >> 6] = incl;
     }
@@ -181,12 +183,12 @@ __global__ __launch_bounds__(4 * WG) void k_lsd_scan4(LsdGeom g, u32* hist) {
     if (q == 0) {
         u32 carry = 0;
         for (u32 i = 0; i < (d >> 6); ++i) carry += sh[i];
-        const u32 c0 = pt[0][d], c1 = pt[1][d], c2 = pt[2][d];
-        const u32 base = g.geo.base(b) + carry + incl - tot;
-        pt[0][d] = base;
-        pt[1][d] = base + c0;
-        pt[2][d] = base + c0 + c1;
-        pt[3][d] = base + c0 + c1 + c2;
+        u32 run = g.geo.base(b) + carry + incl - tot;
+        for (u32 i = 0; i < NP; ++i) {
+            const u32 c = pt[i][d];
+            pt[i][d] = run;
+            run += c;
+        }
     }
     __syncthreads();
     u32 run = pt[q][d];
@@ -807,10 +809,13 @@ void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kou
         // four threads per digit for batches of fewer than 64 blocks (a latency-bound workgroup
         // per block; on full batches the 1024-thread workgroups wait beside the LZ77 parse:
         // 256 MiB LSD 18.4 -> 19.2 ms with them).  KOLM_LSD_SCAN4 = 0 / 1 forces it.
+        // KOLM_LSD_SCAN4 = 0 / 1 / 2: one / four / two threads per digit
         static const int s4e = getenv("KOLM_LSD_SCAN4") ? atoi(getenv("KOLM_LSD_SCAN4")) : -1;
-        const bool s4 = s4e > 0 || (s4e < 0 && g.geo.nb < 64);
-        if (s4)
-            k_lsd_scan4<<<g.geo.nb, 4 * WG, 0, s>>>(g, hist);
+        const int mode = s4e >= 0 ? s4e : (g.geo.nb < 64 ? 1 : 0);
+        if (mode == 1)
+            k_lsd_scanp<4><<<g.geo.nb, 4 * WG, 0, s>>>(g, hist);
+        else if (mode == 2)
+            k_lsd_scanp<2><<<g.geo.nb, 2 * WG, 0, s>>>(g, hist);
         else
             k_lsd_scan<<<g.geo.nb, WG, 0, s>>>(g, hist);
     }
@@ -920,8 +925,11 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
     if (win) {
         const u32 nwin = (geo.bs + R0_WIN - 1) / R0_WIN;
         static const int s4e = getenv("KOLM_LSD_SCAN4") ? atoi(getenv("KOLM_LSD_SCAN4")) : -1;
-        if (s4e > 0 || (s4e < 0 && geo.nb < 64))
-            k_lsd_scan4<<<geo.nb, 4 * WG, 0, s>>>(g, t.hist);  // window counts -> pair offsets
+        const int mode = s4e >= 0 ? s4e : (geo.nb < 64 ? 1 : 0);
+        if (mode == 1)
+            k_lsd_scanp<4><<<geo.nb, 4 * WG, 0, s>>>(g, t.hist);  // window counts -> pair offsets
+        else if (mode == 2)
+            k_lsd_scanp<2><<<geo.nb, 2 * WG, 0, s>>>(g, t.hist);
         else
             k_lsd_scan<<<geo.nb, WG, 0, s>>>(g, t.hist);
         {
