@@ -485,3 +485,43 @@ def test_repair_at_scale_vs_py(kolm_gpu, large_known, case):
     ref = large_known[case]
     out = kolm_gpu.repair_compress(REPAIR_SCALE[case]())[0]
     assert (len(out), sha(out)) == (ref["repair"]["len"], ref["repair"]["sha256"])
+
+
+def _image_like(kind: str, n: int) -> bytes:
+    """Periodic image / audio structures of BASELINE config 5 at other periods: long
+    periodic Lyndon factors (merge batch absorption, text LCP memo), rotation groups of
+    2-8 K tied positions (the medium sort), LZ77 matches of KBs with short periods (the
+    stitch's fingerprint filter), deep MTF indices (the position-parallel replay)."""
+    if kind.startswith("checker"):
+        run, rows_band, row = {"checker96": (48, 16, 1920), "checker12": (6, 5, 600),
+                               "checker_odd": (37, 3, 999)}[kind]
+        out = bytearray()
+        y = 0
+        while len(out) < n:
+            flip = (y // rows_band) & 1
+            x = np.arange(row)
+            out += np.where(((x // run) + flip) % 2 == 0, 240, 40).astype(np.uint8).tobytes()
+            y += 1
+        return bytes(out[:n])
+    if kind == "sine16":
+        i = np.arange(n // 2 + 1)
+        return (np.round(32767 * np.sin(2 * np.pi * 440 * i / 44100)).astype("<i2")).tobytes()[:n]
+    if kind == "stripes":  # a 2 KiB random tile repeated with sparse mutations
+        rng = np.random.default_rng(3)
+        base = bytearray(rng.integers(0, 256, 2048).astype(np.uint8).tobytes() * (n // 2048 + 1))
+        for p in rng.integers(0, n, 24):
+            base[int(p)] ^= 0x55
+        return bytes(base[:n])
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["checker96", "checker12", "checker_odd", "sine16", "stripes"])
+def test_image_like_batches_vs_oracle(kolm_gpu, kind):
+    """Batches of few blocks (the small-batch kernels) on periodic images and audio: the
+    hot-path container against the oracle's, and the per-kernel BBWT / LZ77 of one block."""
+    data = _image_like(kind, 2 * 65536 + 4321)
+    bs = 65536
+    assert kolm_gpu.compress_blocks_fixed(data, bs, hot_path=True) == O.compress_blocks_fixed(data, bs, range(9))
+    blk = data[bs:2 * bs]
+    assert kolm_gpu.bbwt_forward(blk) == O.bbwt_forward(blk), "bbwt"
+    assert kolm_gpu.encode_lz77(blk)[0] == O.encode_lz77(blk), "lz77"
