@@ -1104,12 +1104,29 @@ void launch_classify(const Seg* cur, u32 ncur, const u32* ncur_dev, const SortAr
     if (ncur)
         k_classify<0><<<std::min<u32>(cdiv(ncur, 256), 2048u), 256, 0, s>>>(cur, ncur, ncur_dev, a, L, lv0, Bins{});
 }
+__global__ void k_zero_spans(ZeroSpans z) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int k = 0; k < 6; ++k) {
+        if (i < z.n[k]) {
+            z.p[k][i] = 0;
+            return;
+        }
+        i -= z.n[k];
+    }
+}
+void launch_zero_spans(const ZeroSpans& z, hipStream_t s) {
+    u64 tot = 0;
+    for (int k = 0; k < 6; ++k) tot += z.p[k] ? z.n[k] : 0;
+    if (tot) k_zero_spans<<<cdiv(tot, 256), 256, 0, s>>>(z);
+}
 void launch_classify_bins(const Seg* cur, u32 ncur, const u32* ncur_dev, const SortArgs& a, const Lists& L,
-                          const Level& lv0, const Bins& bn, hipStream_t s) {
+                          const Level& lv0, const Bins& bn, hipStream_t s, bool bins_zeroed) {
     if (!ncur) return;
     const u32 grid = std::min<u32>(cdiv(ncur, 256), 2048u);
-    KOLM_HIP_CHECK(hipMemsetAsync(bn.cnt, 0, sizeof(u32) * NCLASS * CLS_NBIN, s));
-    KOLM_HIP_CHECK(hipMemsetAsync(bn.fill, 0, sizeof(u32) * NCLASS * CLS_NBIN, s));
+    if (!bins_zeroed) {
+        KOLM_HIP_CHECK(hipMemsetAsync(bn.cnt, 0, sizeof(u32) * NCLASS * CLS_NBIN, s));
+        KOLM_HIP_CHECK(hipMemsetAsync(bn.fill, 0, sizeof(u32) * NCLASS * CLS_NBIN, s));
+    }
     k_classify<1><<<grid, 256, 0, s>>>(cur, ncur, ncur_dev, a, L, lv0, bn);
     k_bin_scan<<<NCLASS, 256, 0, s>>>(bn);
     k_classify<2><<<grid, 256, 0, s>>>(cur, ncur, ncur_dev, a, L, lv0, bn);

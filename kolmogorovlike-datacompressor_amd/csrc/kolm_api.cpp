@@ -412,10 +412,29 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
         a.key_bits = a.initial ? (cyclic ? 32u : 27u) : bitlen(cyclic ? geo.bs - 1 : geo.bs);
         L.next = nxt;
         L.next_cnt = ncnt + (round & 1);
-        KOLM_HIP_CHECK(hipMemsetAsync(L.next_cnt, 0, sizeof(u32), s));
-        KOLM_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(u32) * C_STATUS, s));
-        KOLM_HIP_CHECK(hipMemsetAsync(cnt + C_CLSE, 0, sizeof(u32) * (C_N - C_CLSE), s));
-        KOLM_HIP_CHECK(hipMemsetAsync(a.blk_split, 0, sizeof(u32) * geo.nb, s));
+        // the round's counters, split flags and (position-ordered lists) classify bins in one
+        // launch: hipMemsetAsync fills are ~4.5 us kernels each on the sort stream (config 5:
+        // 151 per batch, 0.68 ms)
+        static const bool bin_lists = !(getenv("KOLM_CLS_BIN") && atoi(getenv("KOLM_CLS_BIN")) == 0);
+        const bool zero_bins = bin_lists && !(round == 0 && cyclic);
+        {
+            ZeroSpans z{};
+            z.p[0] = L.next_cnt;
+            z.n[0] = 1;
+            z.p[1] = cnt;
+            z.n[1] = C_STATUS;
+            z.p[2] = cnt + C_CLSE;
+            z.n[2] = C_N - C_CLSE;
+            z.p[3] = a.blk_split;
+            z.n[3] = (u32)geo.nb;
+            if (zero_bins) {
+                z.p[4] = c->get<u32>("cls_bins", NCLASS * CLS_NBIN);
+                z.n[4] = NCLASS * CLS_NBIN;
+                z.p[5] = c->get<u32>("cls_fill", NCLASS * CLS_NBIN);
+                z.n[5] = NCLASS * CLS_NBIN;
+            }
+            launch_zero_spans(z, s);
+        }
         if (round == 0 && cyclic) {
             // round 0: stable LSD passes over the packed codes of the first C rotation
             // characters (KOLM_R0_ALPHA=0: raw bytes, C = 8), no host round trips but one
@@ -454,7 +473,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
                 const u32 nbits = bitlen((u32)(N - 1));
                 const Bins bn{c->get<u32>("cls_bins", NCLASS * CLS_NBIN), c->get<u32>("cls_fill", NCLASS * CLS_NBIN),
                               nbits > 10 ? nbits - 10 : 0u};
-                launch_classify_bins(cur, ncur, ncur_dev, a, L, lv[0], bn, s);
+                launch_classify_bins(cur, ncur, ncur_dev, a, L, lv[0], bn, s, zero_bins);
                 a.xcd = 1;
             } else {
                 launch_classify(cur, ncur, ncur_dev, a, L, lv[0], s);

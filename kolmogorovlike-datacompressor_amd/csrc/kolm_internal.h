@@ -274,9 +274,16 @@ struct Level {
 // ---- launchers (k_sort.hip) ----
 void launch_iota(u32* SA, u64 N, hipStream_t s);
 void launch_block_segs(Seg* segs, const Geom& geo, hipStream_t s);
+// Up to 6 u32 ranges zeroed by one launch (a round's counters: one kernel instead of 4-6
+// hipMemsetAsync fills, each a ~4.5 us launch on the sort stream)
+struct ZeroSpans {
+    u32* p[6];
+    u32 n[6];
+};
+void launch_zero_spans(const ZeroSpans& z, hipStream_t s);
 // ncur: the list length, or (ncur_dev set) a bound for the grid with the length in ncur_dev
 void launch_classify_bins(const Seg* cur, u32 ncur, const u32* ncur_dev, const SortArgs& a, const Lists& L,
-                          const Level& lv0, const Bins& bn, hipStream_t s);
+                          const Level& lv0, const Bins& bn, hipStream_t s, bool bins_zeroed = false);
 void launch_classify(const Seg* cur, u32 ncur, const u32* ncur_dev, const SortArgs& a, const Lists& L,
                      const Level& lv0, hipStream_t s);
 void launch_keypos(const SortArgs& a, u32* KP, hipStream_t s);
