@@ -34,6 +34,9 @@ Also reported:
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 via
 python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+(the launcher only sets RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*: this process uses no PyTorch —
+device memory, the RCCL communicator, barriers and reductions all go through libkolm_hip.so's
+C ABI, kolm.parallel.Comm; the communicator id travels over TCP at MASTER_ADDR:MASTER_PORT+1)
 """
 import argparse
 import ctypes
@@ -43,15 +46,15 @@ import os
 import sys
 import time
 
-import torch  # first: libkolm_hip.so must bind to torch's already-loaded HIP runtime
-import torch.distributed as dist
+if os.environ.get("KOLM_BENCH_TORCH_RT"):  # A/B only: bind to torch's bundled HIP runtime instead
+    import torch  # noqa: F401
 import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "kolmogorovlike-datacompressor_amd"))
 
 from kolm import _lib, datagen  # noqa: E402
-from kolm.parallel import gather_payloads  # noqa: E402
+from kolm.parallel import Comm  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 GOLDEN = os.path.join(REPO, "tests", "golden")
@@ -173,19 +176,18 @@ def check_blocks(g, sizes, method, arena_host, off, ncand, wkey, shakey):
     return ok
 
 
+COMM = None  # kolm.parallel.Comm (RCCL behind the C ABI) when WORLD_SIZE > 1
+
+
 def sync_max(el, world):
     if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt[0])
+        el = float(COMM.allreduce([float(el)], op="max")[0])
     return el
 
 
 def sum_all(v, world):
     if world > 1:
-        tt = torch.tensor([v], dtype=torch.int64, device="cuda")
-        dist.all_reduce(tt)
-        v = int(tt[0])
+        v = int(COMM.allreduce([int(v)])[0])
     return v
 
 
@@ -226,9 +228,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         log(rank, f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
+    global COMM
     if world > 1:
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        COMM = Comm.from_env(device=local)
     n = a.mib << 20
     t = time.time()
     stream0 = None  # rank 0's stream: the config-4 data (256 MiB total, sharded)
@@ -245,14 +247,16 @@ def main():
         n = len(data)
 
     L = _lib.load()
-    ctx = ctypes.c_void_p()
-    _lib.check(L.kolm_ctx_create(local, ctypes.byref(ctx)))
-    d_in = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
-    d_in[:n].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    ctx = _lib.device_ctx(local)
+
+    def dsync():
+        _lib.check(L.kolm_ctx_sync(ctx))
+
+    d_in = _lib.input_buffer(ctx, data)
     cap = n + (4 << 20)
     # payload arenas: N > 1 double-buffers them, so the RCCL gather of step k (over xGMI,
-    # on the NCCL stream) overlaps step k+1's encoding instead of serialising behind it
-    arenas = [torch.empty(cap, dtype=torch.uint8, device="cuda") for _ in range(2 if world > 1 else 1)]
+    # on the communicator's stream) overlaps step k+1's encoding instead of serialising behind it
+    arenas = [_lib.DeviceBuffer(ctx, cap) for _ in range(2 if world > 1 else 1)]
     pending = [None] * len(arenas)
     nstep = [0]
     arena = arenas[0]
@@ -260,7 +264,7 @@ def main():
     sizes = np.zeros((nb, _lib.KOLM_NCAND), np.uint32)
     method = np.zeros(nb, np.uint32)
     off = np.zeros(nb + 1, np.uint64)
-    torch.cuda.synchronize()
+    dsync()
 
     def step(st, mask=_lib.KOLM_HOTPATH_MASK):
         j = nstep[0] % len(arenas)
@@ -269,13 +273,12 @@ def main():
         if pending[j] is not None:  # the gather of two steps ago still reads this buffer
             pending[j].wait()
             pending[j] = None
-        _lib.check(L.kolm_encode_blocks_device(ctx, d_in.data_ptr(), n, a.bs, mask, None, buf.data_ptr(), cap,
+        _lib.check(L.kolm_encode_blocks_device(ctx, d_in.ptr, n, a.bs, mask, None, buf.ptr, cap,
                                                sizes.ctypes.data, method.ctypes.data, off.ctypes.data,
                                                ctypes.byref(st)))
         if world > 1:
-            ids = torch.from_numpy(method.astype(np.int32)).cuda()
-            offs = torch.from_numpy(off.astype(np.int64)).cuda()
-            pending[j] = gather_payloads(buf, int(off[-1]), ids, dst=0, async_op=True, offsets=offs)
+            pending[j] = COMM.gather_payloads(buf.ptr, int(off[-1]), method, off, dst=0, async_op=True,
+                                              dst_cap_blocks=nb)
         return buf
 
     def drain():
@@ -284,19 +287,19 @@ def main():
             if w is not None:
                 w.wait()
                 pending[j] = None
-        torch.cuda.synchronize()
+        dsync()
 
     def timed(fn, k):
         """k calls of fn between barriers + device syncs; max over ranks of the wall time"""
         drain()
         if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
+            COMM.barrier()
+        dsync()
         t0 = time.perf_counter()
         res = [fn() for _ in range(k)]
         drain()
         if world > 1:
-            dist.barrier()
+            COMM.barrier()
         return sync_max(time.perf_counter() - t0, world), res
 
     for _ in range(a.warmup):
@@ -310,7 +313,7 @@ def main():
 
     # ---- parity of the timed output, block by block, against the oracle's answers ----
     golden = golden_full
-    arena_host = arena[:int(off[-1])].cpu().numpy().tobytes() if golden else None
+    arena_host = arena.download(int(off[-1])) if golden else None
     parity_ok = check_blocks(golden, sizes, method, arena_host, off, 9, "w9", "sha9") if golden else 0
     parity_checked = nb if golden else 0
     parity = {"ok": sum_all(parity_ok, world), "checked": sum_all(parity_checked, world), "blocks": sum_all(nb, world)}
@@ -327,11 +330,9 @@ def main():
         r4 = rank if world > 1 else 0
         mine4 = list(range(r4, nb_stream, G))
         n4 = len(mine4) * a.bs  # 1 MiB blocks of a whole-MiB stream: every block full
-        d4 = torch.empty(n4 + 64, dtype=torch.uint8, device="cuda")
-        d4[:n4].copy_(torch.frombuffer(bytearray(b"".join(stream0[i * a.bs:(i + 1) * a.bs] for i in mine4)),
-                                       dtype=torch.uint8))
+        d4 = _lib.input_buffer(ctx, b"".join(stream0[i * a.bs:(i + 1) * a.bs] for i in mine4))
         cap4 = n4 + (4 << 20)
-        ar4 = [torch.empty(cap4, dtype=torch.uint8, device="cuda") for _ in range(2)]
+        ar4 = [_lib.DeviceBuffer(ctx, cap4) for _ in range(2)]
         pend4 = [None, None]
         cnt4 = [0]
         sz4 = np.zeros((len(mine4), _lib.KOLM_NCAND), np.uint32)
@@ -344,13 +345,12 @@ def main():
             if pend4[j] is not None:
                 pend4[j].wait()
                 pend4[j] = None
-            _lib.check(L.kolm_encode_blocks_device(ctx, d4.data_ptr(), n4, a.bs, _lib.KOLM_HOTPATH_MASK, None,
-                                                   ar4[j].data_ptr(), cap4, sz4.ctypes.data, m4.ctypes.data,
+            _lib.check(L.kolm_encode_blocks_device(ctx, d4.ptr, n4, a.bs, _lib.KOLM_HOTPATH_MASK, None,
+                                                   ar4[j].ptr, cap4, sz4.ctypes.data, m4.ctypes.data,
                                                    o4.ctypes.data, None))
             if world > 1:
-                ids = torch.from_numpy(m4.astype(np.int32)).cuda()
-                offs = torch.from_numpy(o4.astype(np.int64)).cuda()
-                pend4[j] = gather_payloads(ar4[j], int(o4[-1]), ids, dst=0, async_op=True, offsets=offs)
+                pend4[j] = COMM.gather_payloads(ar4[j].ptr, int(o4[-1]), m4, o4, dst=0, async_op=True,
+                                                dst_cap_blocks=nb_stream)
 
         def c4_drain():
             for j in range(2):
@@ -362,21 +362,20 @@ def main():
         c4_drain()
         drain()
         if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
+            COMM.barrier()
+        dsync()
         t0 = time.perf_counter()
         for _ in range(a.c4_steps):
             c4_step()
         c4_drain()
-        torch.cuda.synchronize()
+        dsync()
         if world > 1:
-            dist.barrier()
+            COMM.barrier()
         el4 = sync_max(time.perf_counter() - t0, world)
         g4 = golden_subset(load_golden_stream(0, a.mib << 20, a.bs), mine4)
         ok4 = 0
         if g4:
-            ok4 = check_blocks(g4, sz4, m4, ar4[(cnt4[0] - 1) % 2][:int(o4[-1])].cpu().numpy().tobytes(), o4, 9,
-                               "w9", "sha9")
+            ok4 = check_blocks(g4, sz4, m4, ar4[(cnt4[0] - 1) % 2].download(int(o4[-1])), o4, 9, "w9", "sha9")
         tot4 = sum_all(n4, world)
         c4 = {"value": round(tot4 * a.c4_steps / el4 / MB, 2), "unit": "MB/s", "steps": a.c4_steps,
               "ms_per_step": round(el4 / a.c4_steps * 1e3, 3), "blocks_per_gpu": len(mine4),
@@ -486,23 +485,23 @@ def main():
     cur_arena = [arenas[(nstep[0] - 1) % len(arenas)]]
 
     def decode_leg():
-        d_out = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        d_out = _lib.DeviceBuffer(ctx, n + 64)
         dms = ctypes.c_double(0.0)
         acc = [0.0]
 
         def dstep():
-            _lib.check(L.kolm_decode_blocks_device(ctx, cur_arena[0].data_ptr(), off.ctypes.data, method.ctypes.data,
-                                                   blens.ctypes.data, nb, d_out.data_ptr(), n + 64, ctypes.byref(dms)))
+            _lib.check(L.kolm_decode_blocks_device(ctx, cur_arena[0].ptr, off.ctypes.data, method.ctypes.data,
+                                                   blens.ctypes.data, nb, d_out.ptr, n + 64, ctypes.byref(dms)))
             acc[0] += dms.value
 
         dstep()
-        torch.cuda.synchronize()
-        ok = bool(torch.equal(d_out[:n], d_in[:n]))
+        dsync()
+        ok = d_out.download(n) == data
         if not ok:
             raise SystemExit("decode leg: device round trip differs from the input")
         acc[0] = 0.0
         eld, _ = timed(dstep, a.decode_steps)
-        del d_out
+        d_out.free()
         return {"value": round(ntot * a.decode_steps / eld / MB, 2), "unit": "MB/s", "steps": a.decode_steps,
                 "ms_per_step": round(eld / a.decode_steps * 1e3, 2),
                 "kernel_ms_per_step": round(acc[0] / a.decode_steps, 2), "round_trip_exact": ok,
@@ -532,7 +531,7 @@ def main():
                 "repair_rules_per_block": round(f0["rp_rules"] / nb, 1),
                 "repair_batches_per_block": round(f0["rp_batches"] / nb, 1)}
         if golden:
-            fh = cur_arena[0][:int(off[-1])].cpu().numpy().tobytes()
+            fh = cur_arena[0].download(int(off[-1]))
             fok = check_blocks(golden, sizes, method, fh, off, 10, "w10", "sha10")
             full["parity_blocks"] = f"{sum_all(fok, world)}/{sum_all(nb, world)}"
         # decode of those payloads (Re-Pair wins every text block): grammar expansion on the device
@@ -555,12 +554,12 @@ def main():
 
         def cdc_step():
             t_b = time.perf_counter()
-            _lib.check(L.kolm_cdc_boundaries_device(ctx, d_in.data_ptr(), n, 4096, 8192, 16384, 1, hst.ctypes.data,
+            _lib.check(L.kolm_cdc_boundaries_device(ctx, d_in.ptr, n, 4096, 8192, 16384, 1, hst.ctypes.data,
                                                     ccap, ctypes.byref(nch)))
             cst["ms_bounds"] = (time.perf_counter() - t_b) * 1e3
             st = _lib.Stats()
-            _lib.check(L.kolm_encode_blocks_device_var(ctx, d_in.data_ptr(), hst.ctypes.data, int(nch.value),
-                                                       _lib.KOLM_HOTPATH_MASK, None, arenas[0].data_ptr(), cap,
+            _lib.check(L.kolm_encode_blocks_device_var(ctx, d_in.ptr, hst.ctypes.data, int(nch.value),
+                                                       _lib.KOLM_HOTPATH_MASK, None, arenas[0].ptr, cap,
                                                        csz.ctypes.data, cmeth.ctypes.data, coff.ctypes.data,
                                                        ctypes.byref(st)))
 
@@ -585,8 +584,8 @@ def main():
 
         def v2_step():
             st = _lib.Stats()
-            _lib.check(L.kolm_encode_blocks_device(ctx, d_in.data_ptr(), n2, a.bs, _lib.KOLM_FULL_MASK, None,
-                                                   arenas[0].data_ptr(), cap, sz2.ctypes.data, m2.ctypes.data,
+            _lib.check(L.kolm_encode_blocks_device(ctx, d_in.ptr, n2, a.bs, _lib.KOLM_FULL_MASK, None,
+                                                   arenas[0].ptr, cap, sz2.ctypes.data, m2.ctypes.data,
                                                    o2.ctypes.data, ctypes.byref(st)))
 
         v2_step()
@@ -612,10 +611,9 @@ def main():
             cn = len(cdata)
             cbs = 1 << 20
             cnb = (cn + cbs - 1) // cbs
-            d_c = torch.empty(cn + 64, dtype=torch.uint8, device="cuda")
-            d_c[:cn].copy_(torch.frombuffer(bytearray(cdata), dtype=torch.uint8))
+            d_c = _lib.input_buffer(ctx, cdata)
             ccap2 = 9 * cn + 4096
-            d_ar = torch.empty(ccap2, dtype=torch.uint8, device="cuda")
+            d_ar = _lib.DeviceBuffer(ctx, ccap2)
             res = {}
             for label, mask, wkey, shakey, ncand in (("ids0_8", _lib.KOLM_HOTPATH_MASK, "w9", "sha9", 9),
                                                      ("ids0_9", _lib.KOLM_DEFAULT_MASK, "w10", "sha10", 10)):
@@ -626,7 +624,7 @@ def main():
 
                 def cstep():
                     cst[0] = _lib.Stats()
-                    _lib.check(L.kolm_encode_blocks_device(ctx, d_c.data_ptr(), cn, cbs, mask, None, d_ar.data_ptr(),
+                    _lib.check(L.kolm_encode_blocks_device(ctx, d_c.ptr, cn, cbs, mask, None, d_ar.ptr,
                                                            ccap2, csz.ctypes.data, cm.ctypes.data, co.ctypes.data,
                                                            ctypes.byref(cst[0])))
 
@@ -642,7 +640,7 @@ def main():
                     r["ms_repair"] = round(sd["ms_repair"], 3)
                 g = mg.get(name)
                 if g and g["input"]["len"] == cn:
-                    hostp = d_ar[:int(co[-1])].cpu().numpy().tobytes()
+                    hostp = d_ar.download(int(co[-1]))
                     r["parity_blocks"] = f"{check_blocks(g, csz, cm, hostp, co, ncand, wkey, shakey)}/{cnb}"
                 res[label] = r
             res["bytes"] = cn
@@ -663,14 +661,12 @@ def main():
         elh = (time.perf_counter() - t0) / a.host_steps
         # its parts: PCIe H2D of the input and D2H of the payloads (pageable host memory,
         # as the API receives it), and the device encode of the same batch
-        hb = torch.frombuffer(bytearray(data), dtype=torch.uint8)
-        torch.cuda.synchronize()
+        dsync()
         t0 = time.perf_counter()
-        d_in[:n].copy_(hb)
-        torch.cuda.synchronize()
+        d_in.upload(data)
         h2d = time.perf_counter() - t0
         t0 = time.perf_counter()
-        _ = arena[:int(off[-1])].cpu()
+        _ = arena.download(int(off[-1]))
         d2h = time.perf_counter() - t0
         host = {"value": round(n / elh / MB, 2), "unit": "MB/s", "steps": a.host_steps,
                 "ms_per_call": round(elh * 1e3, 2), "container_bytes": len(blob),
@@ -681,8 +677,8 @@ def main():
                 "note": "kolm.compress_blocks_fixed(bytes, 1 MiB, hot_path=True) on the bench stream = one "
                         "kolm_compress_fixed call: the pageable input staged through pinned chunks (parallel host "
                         "copies beside the DMA), the batched device encode, TOC + payloads D2H into a pinned "
-                        "container buffer, one copy into the returned bytes; ms_h2d/d2h_pageable: plain torch "
-                        "copies of the same bytes for comparison"}
+                        "container buffer, one copy into the returned bytes; ms_h2d/d2h_pageable: plain "
+                        "hipMemcpy of the same bytes (kolm_memcpy_h2d/d2h) for comparison"}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -743,9 +739,8 @@ def main():
         if cpu:
             out["detail"]["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         print(json.dumps(out), flush=True)
-    L.kolm_ctx_destroy(ctx)
     if world > 1:
-        dist.destroy_process_group()
+        COMM.close()
 
 
 if __name__ == "__main__":

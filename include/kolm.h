@@ -18,6 +18,9 @@
  *                             context per device).
  *   kolm_toc_write / kolm_toc_read: the KOLR container's header + TOC on the host
  *                             (PY:2375-2445 writer, PY:2451-2530 reader; kolm_toc.cpp).
+ *   kolm_comm_* / kolm_gather_payloads: RCCL over xGMI (kolm_comm.cpp) — the reassembly
+ *                             of independently encoded block shards (PY:2350-2369 blocks,
+ *                             PY:2375-2445 the container they feed) onto one rank.
  *
  * Conventions: plain pointers and sizes; caller-allocated buffers with explicit
  * capacities; every function returns 0 (KOLM_OK) or a negative code; no exception
@@ -39,7 +42,7 @@ extern "C" {
 #define KOLM_EARG (-1)     /* bad argument */
 #define KOLM_ECAP (-2)     /* output capacity too small */
 #define KOLM_EHIP (-3)     /* HIP runtime error (message: kolm_last_error) */
-#define KOLM_ERCCL (-4)    /* reserved: collective error */
+#define KOLM_ERCCL (-4)    /* RCCL (collective) error (message: kolm_last_error) */
 #define KOLM_ENOINIT (-5)  /* kolm_init not called */
 #define KOLM_EFORMAT (-6)  /* malformed container (message: PY's ValueError text) */
 #define KOLM_ERANGE (-7)   /* a container field overflows (PY: struct.error) */
@@ -104,8 +107,10 @@ typedef struct kolm_stats {
     uint64_t rp_batches;      /* Re-Pair batches (sequential depth) summed over blocks */
     uint64_t rp_final;        /* Re-Pair final sequence symbols over all blocks */
     uint64_t lz_fix;          /* LZ77 tokens the stitch computed off the speculative paths */
-    uint64_t cyc_rounds_sum;  /* sum over blocks of the doubling rounds each block needed (round 0
-                                 counted; SURVEY §8d's per-block R, used for the byte contract) */
+    uint64_t cyc_rounds_sum;  /* sum over blocks of the rounds each block needed: round 0 through
+                                 the last round that split one of its groups (>= 1; independent of
+                                 how blocks are batched; SURVEY §8d's per-block R, used for the
+                                 byte contract) */
 } kolm_stats;
 
 /* ---- library / default context ------------------------------------------------ */
@@ -203,9 +208,15 @@ int kolm_result_copy(uint8_t* dst, uint64_t n);
 
 /* kolm_encode_blocks over ngpu devices (0..ngpu-1, clamped to the device count and the
  * block count) of this process: fixed blocks of block_size over data[0, total), block i
- * of shard r lives on device r, shards are contiguous block ranges.  Outputs exactly as
- * kolm_encode_blocks (block order; sizes [nblocks*KOLM_NCAND], method [nblocks], payload_off
- * [nblocks+1]).  stats (optional) sums counts and takes the max of times over devices. */
+ * of shard r lives on device r, shards are contiguous block ranges, one host thread and
+ * context per device.  The shards' payloads are reassembled with RCCL: one
+ * ncclCommInitAll communicator over the devices (created on first use, kept until
+ * kolm_shutdown), every device's payload arena received into device 0 in one group over
+ * xGMI, then one copy into payload_arena (KOLM_MULTI_GATHER=host: each device copies its
+ * own payloads to the host instead).  Outputs exactly as kolm_encode_blocks (block order;
+ * sizes [nblocks*KOLM_NCAND], method [nblocks], payload_off [nblocks+1]).  stats
+ * (optional) sums counts and takes the max of times over devices.  KOLM_ERCCL on a
+ * collective error. */
 int kolm_encode_blocks_multi(int ngpu, const uint8_t* data, uint64_t total, uint32_t block_size,
                              uint32_t cand_mask, const int32_t* force_method, uint32_t* sizes,
                              uint32_t* method, uint8_t* payload_arena, uint64_t arena_cap,
@@ -260,6 +271,47 @@ int kolm_cdc_boundaries_device(kolm_ctx* ctx, const uint8_t* d_data, uint64_t n,
 int kolm_decode_blocks_device(kolm_ctx* ctx, const void* d_payloads, const uint64_t* payload_off,
                               const uint32_t* methods, const uint32_t* orig_lens, uint32_t nblocks,
                               void* d_out, uint64_t out_cap, double* ms);
+
+/* ---- collectives: RCCL over xGMI, one process per GPU (kolm_comm.cpp) ------------- */
+/* The only data exchange of the multi-GPU path: blocks are independent (PY:2350-2369), so
+ * each rank encodes its block shard alone and the payloads are gathered onto one rank to
+ * write the container (PY:2375-2445).  Every function returns KOLM_ERCCL on an RCCL error
+ * (message: kolm_last_error).  Calls on one communicator are serialised. */
+#define KOLM_COMM_ID_BYTES 128
+typedef struct kolm_comm kolm_comm;
+/* A fresh communicator id (ncclGetUniqueId): one rank creates it, every rank passes the
+ * same KOLM_COMM_ID_BYTES bytes to kolm_comm_init (the caller moves them between the
+ * processes: kolm.parallel does it over a TCP socket at MASTER_ADDR). */
+int kolm_comm_unique_id(uint8_t* id);
+/* Rank `rank` of an nranks-rank communicator on ctx's device (ncclCommInitRank: returns
+ * when every rank has joined).  One rank per device. */
+int kolm_comm_init(kolm_ctx* ctx, int nranks, int rank, const uint8_t* id, kolm_comm** out);
+int kolm_comm_destroy(kolm_comm* comm);
+int kolm_comm_rank(kolm_comm* comm, int* rank, int* nranks);
+/* values[0, count) (host memory, 8-byte elements: dtype 0 uint64, 1 double) reduced over
+ * every rank in place (op 0 sum, 1 max); synchronous.  kolm_comm_barrier: an all-reduce of
+ * one word. */
+int kolm_comm_allreduce(kolm_comm* comm, void* values, uint32_t count, int dtype, int op);
+int kolm_comm_barrier(kolm_comm* comm);
+/* Gathers every rank's payloads onto rank dst.  Each rank passes its payload arena
+ * d_arena[0, nbytes) (device memory of its context, complete — e.g. as
+ * kolm_encode_blocks_device returned it) and its nblocks method ids / nblocks + 1 payload
+ * offsets (host arrays, as kolm_encode_blocks_device returned them).  On dst, d_dst
+ * (device, dst_cap bytes) receives the ranks' payloads back to back in rank order,
+ * method_all / off_all (host, dst_cap_blocks / dst_cap_blocks + 1 entries; either may be
+ * NULL) the ranks' ids in rank order and their offsets into d_dst (off_all[total blocks] =
+ * total bytes).  On every rank rank_bytes / rank_blocks (nranks entries, optional)
+ * receive each rank's sizes.  When the payloads or ids do not fit dst's capacities every
+ * rank returns KOLM_ECAP (sizes filled) and nothing is transferred.  async_op != 0:
+ * returns once the transfers are queued on the communicator's stream; d_arena must stay
+ * unmodified and the outputs are valid only after kolm_comm_wait (or the next call on the
+ * communicator) — the transfer of one batch then runs while the next one encodes. */
+int kolm_gather_payloads(kolm_comm* comm, const void* d_arena, uint64_t nbytes, const uint32_t* method,
+                         const uint64_t* payload_off, uint32_t nblocks, int dst, void* d_dst, uint64_t dst_cap,
+                         uint32_t dst_cap_blocks, uint64_t* rank_bytes, uint32_t* rank_blocks,
+                         uint32_t* method_all, uint64_t* off_all, int async_op);
+/* Completes the communicator's asynchronous gather, if any (every rank). */
+int kolm_comm_wait(kolm_comm* comm);
 
 #ifdef __cplusplus
 }

@@ -691,9 +691,10 @@ __global__ __launch_bounds__(WG) void k_alpha_codes(const u32* pres, u8* code, u
 // append the next); positions whose C characters wrap inside their Lyndon factor (FEd <
 // C) are rebuilt from the factor record.
 // hist0 (optional): the first LSD pass's per-tile digit counts (digit 0 of KA), so that
-// pass needs no histogram kernel of its own.
+// pass needs no histogram kernel of its own; top: the counts of KB's top byte instead (the
+// first MSD digit of the MSD round 0, k_r0m.hip, which passes sh = 64 - C w).
 __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32 C, u32 w, u32 sh, u32* KA, u32* KB,
-                                                  u32* hist0) {
+                                                  u32* hist0, u32 top) {
     __shared__ __align__(16) u8 tx[LSD_T + 64];
     __shared__ u8 cd[256];
     __shared__ u32 h0[WG / 64][256];
@@ -778,7 +779,7 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
         const u32 wv = threadIdx.x >> 6;
 #pragma unroll
         for (u32 e = 0; e < LSD_PT; ++e)
-            if (p0 + e < hi) atomicAdd(&h0[wv][digit<0>(ka[e])], 1u);
+            if (p0 + e < hi) atomicAdd(&h0[wv][top ? kb[e] >> 24 : digit<0>(ka[e])], 1u);
     }
     }
     if (hist0) {
@@ -849,6 +850,15 @@ void run_pass(int P, bool src_kp, bool gat, const LsdGeom& g, u32 nt, const u32*
 
 u32 lsd_tiles(const Geom& geo) { return (geo.bs + LSD_T - 1) / LSD_T * geo.nb; }
 
+// MSD round 0 (k_r0m.hip): the keys left-aligned in 64 bits by position (KL = low word, KH =
+// high word) and the per-LSD-tile counts of KH's top byte
+void launch_r0_keys64(const Geom& geo, const R0Bufs& t, u32* KL, u32* KH, u32* hist, hipStream_t s, KTimer* kt) {
+    LsdGeom g{geo, (geo.bs + LSD_T - 1) / LSD_T, t.text, t.FEd, t.fac};
+    const u32 nt = g.tpb * geo.nb;
+    KScope k(kt, KT_KEYGEN, "k_keypos_r0", geo.N * 10);
+    k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, 64 - t.chars * t.w, KL, KH, hist, 1);
+}
+
 // Per-block code tables (alphabet compaction); returns the max code width w of the batch
 // (one host round trip).  compact = false: identity codes, w = 8.
 u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w, u32* h_w, bool compact,
@@ -894,7 +904,7 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
     {
         // text + FEd 2 (+ factor starts near factor ends), KA 4 (+ KB 4)
         KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6));
-        k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist);
+        k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist, 0);
     }
     u32* K[2] = {t.K2, t.K22};
     u32* S[2] = {t.SA, t.SA2};

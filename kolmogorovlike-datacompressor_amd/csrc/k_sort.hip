@@ -839,6 +839,10 @@ __global__ __launch_bounds__(MED_NT) void k_med_sort(const LSeg* msegs, const u3
     __shared__ u8 ssplit[1];
     __shared__ u32 sh[NWV];
     __shared__ u32 last_hi[MED_NT];
+    // ~118 KiB of LDS: one workgroup per CU, gfx950's 160 KiB LDS only (a 64 KiB part fails here)
+    static_assert(sizeof(kb) + sizeof(ib) + sizeof(wcnt) + sizeof(base) + sizeof(running) + sizeof(last_hi) +
+                      sizeof(sh) <= 160 * 1024 && sizeof(kb) + sizeof(ib) + sizeof(wcnt) > 64 * 1024,
+                  "k_med_sort is sized for the 160 KiB LDS of gfx950");
     if (blockIdx.x >= *mcount) return;
     const LSeg ls = msegs[blockIdx.x];
     const u32 n = ls.len & SEG_LEN;
@@ -1068,21 +1072,21 @@ __global__ __launch_bounds__(WG) void k_finalize_eq(const Seg* eq, SortArgs a, L
     if (blockIdx.y == 0 && threadIdx.x == 0) L.next[atomicAdd(L.next_cnt, 1u)] = Seg{s.start, len};
 }
 
-// done[b] = 1 + the round in which block b stopped splitting (0 while it still splits)
-__global__ void k_update_done(u32* done, const u32* split, u32 nb, u32 round) {
+// done[b] = 1 + the round in which block b stopped splitting (0 while it still splits);
+// last[b] = 1 + the last round in which one of block b's groups split
+__global__ void k_update_done(u32* done, u32* last, const u32* split, u32 nb, u32 round) {
     const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < nb && !split[b] && !done[b]) done[b] = round + 1;
+    if (b >= nb) return;
+    if (split[b]) last[b] = round + 1;
+    else if (!done[b]) done[b] = round + 1;
 }
 
-// sum over blocks of the doubling rounds each block needed: the round that first found
-// it converged is not counted (it may only have confirmed convergence); blocks never
-// marked converged ran every round
-__global__ void k_rounds_sum(const u32* done, u32 nb, u32 rounds, unsigned long long* out) {
+// sum over blocks of the rounds each block needed: round 0 through the last round that split
+// one of its groups (at least 1).  A function of the block alone — the rounds a batch runs to
+// confirm convergence, or runs for its other blocks, are not counted
+__global__ void k_rounds_sum(const u32* last, u32 nb, unsigned long long* out) {
     u64 acc = 0;
-    for (u32 b = threadIdx.x; b < nb; b += blockDim.x) {
-        const u32 d = done[b];
-        acc += d ? (d > 1 ? d - 1 : 1) : rounds;
-    }
+    for (u32 b = threadIdx.x; b < nb; b += blockDim.x) acc += max(last[b], 1u);
     for (int o = 32; o; o >>= 1) acc += __shfl_xor(acc, o);
     if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)acc);
 }
@@ -1213,13 +1217,13 @@ void launch_med_sort(const LSeg* segs, u32 nseg, const u32* ndev, const SortArgs
 void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists& L, hipStream_t s) {
     if (count) k_finalize_eq<<<dim3(count, 32), WG, 0, s>>>(eq, a, L);
 }
-void launch_rounds_sum(const u32* blk_done, u32 nb, u32 rounds, u64* out, hipStream_t s) {
+void launch_rounds_sum(const u32* blk_last, u32 nb, u64* out, hipStream_t s) {
     KOLM_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(u64), s));
-    k_rounds_sum<<<1, 256, 0, s>>>(blk_done, nb, rounds, reinterpret_cast<unsigned long long*>(out));
+    k_rounds_sum<<<1, 256, 0, s>>>(blk_last, nb, reinterpret_cast<unsigned long long*>(out));
 }
 
-void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, u32 round, hipStream_t s) {
-    if (nb) k_update_done<<<cdiv(nb, 256), 256, 0, s>>>(blk_done, blk_split, nb, round);
+void launch_update_done(u32* blk_done, u32* blk_last, const u32* blk_split, u32 nb, u32 round, hipStream_t s) {
+    if (nb) k_update_done<<<cdiv(nb, 256), 256, 0, s>>>(blk_done, blk_last, blk_split, nb, round);
 }
 
 // ------------------------------------------------------------------------------------

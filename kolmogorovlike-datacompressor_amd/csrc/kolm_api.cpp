@@ -277,6 +277,10 @@ struct kolm_ctx {
     }
 };
 
+namespace kolm {
+int ctx_device(const kolm_ctx* c) { return c->device; }
+}  // namespace kolm
+
 namespace {
 
 TScope::TScope(kolm_ctx* c_, int fam_, const char* name_, u64 bytes_) : c(c_), fam(fam_), name(name_), bytes(bytes_) {
@@ -291,6 +295,13 @@ TScope::~TScope() noexcept(false) {
         KOLM_HIP_CHECK(hipEventRecord(b, c->active));
         c->pend.push_back({fam, name, a, b, bytes, c->strm_of(c->active)});
     }
+}
+
+// round 0 of the cyclic sort: 1 = MSD radix partitions + LDS bucket sorts (k_r0m.hip),
+// 0 = eight LSD passes (k_lsd.hip); KOLM_R0_MSD overrides (read per batch: tests switch it)
+int r0_msd_mode() {
+    const char* e = getenv("KOLM_R0_MSD");
+    return e ? atoi(e) : 0;
 }
 
 std::mutex g_mu;
@@ -337,12 +348,13 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
     a.blk_split = c->get<u32>("blk_split", geo.nb);
     u32* blk_done = c->get<u32>("blk_done", geo.nb);
     a.blk_done = blk_done;
+    u32* blk_last = c->get<u32>("blk_last", geo.nb);
     a.cyclic = cyclic ? 1 : 0;
     // large groups of at most MED_T elements: one-workgroup LDS sort instead of the MSD levels
     // (KOLM_MED_SORT=0: every large group through the MSD levels)
-    // (batches of fewer than 64 blocks: its 71 KB of LDS would wait for the LZ77 parse's
-    // workgroups on a full batch, whose large groups are few anyway — 256 MiB text: 41.8 vs
-    // 37.5 ms per step with it)
+    // (batches of fewer than 64 blocks: its ~118 KiB of LDS — one workgroup per CU, needs the
+    // 160 KiB LDS of gfx950 — would wait for the LZ77 parse's workgroups on a full batch, whose
+    // large groups are few anyway — 256 MiB text: 41.8 vs 37.5 ms per step with it)
     static const int med = getenv("KOLM_MED_SORT") ? atoi(getenv("KOLM_MED_SORT")) : -1;
     a.med = (med > 0 || (med < 0 && geo.nb < 64)) ? 1u : 0u;
 
@@ -382,6 +394,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
         launch_block_segs(segA, geo, s);
     }
     KOLM_HIP_CHECK(hipMemsetAsync(blk_done, 0, sizeof(u32) * geo.nb, s));
+    if (cyclic) KOLM_HIP_CHECK(hipMemsetAsync(blk_last, 0, sizeof(u32) * geo.nb, s));
     Seg* cur = segA;
     Seg* nxt = segB;
     u32 ncur = geo.nb;
@@ -451,10 +464,26 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
                      c->get<u32>("r0cmax", nt), c->get<u32>("r0cmin", nt), c->get<u32>("r0hf", nt * WG)};
             out.r0_chars = C;
             if (dbg) fprintf(stderr, "[kolm] round 0: %u characters of %u bits\n", C, w);
-            launch_round0(geo, r, nxt, L.next_cnt, a.blk_split, s, c->kt());
+            if (r0_msd_mode()) {
+                R0MBufs mb{};
+                mb.x0 = c->get<u32>("r0m_x0", N);
+                mb.x1 = c->get<u32>("r0m_x1", N);
+                mb.hist = c->get<u32>("r0m_hist", r0m_tile_cap(N, geo.nb, geo.bs) * 256);
+                mb.cnt = c->get<u32>("r0m_cnt", 16);
+                static const char* const fn[6] = {"r0m_f0", "r0m_f1", "r0m_f2", "r0m_f3", "r0m_f4", "r0m_f5"};
+                for (int k = 0; k < 6; ++k) mb.fin[k] = c->get<u32>(fn[k], 3 * r0m_fin_cap(N, geo.nb, k));
+                for (int k = 0; k < 2; ++k) {
+                    mb.segs[k] = c->get<LSeg>(k ? "r0m_s1" : "r0m_s0", r0m_seg_cap(N, geo.nb));
+                    mb.tiles[k] = c->get<LTile>(k ? "r0m_t1" : "r0m_t0", r0m_tile_cap(N, geo.nb, geo.bs));
+                }
+                const u32 lv = launch_round0_msd(geo, r, nxt, L.next_cnt, a.blk_split, mb, s, c->kt(), h);
+                if (dbg) fprintf(stderr, "[kolm] round 0: %u MSD levels\n", lv);
+            } else {
+                launch_round0(geo, r, nxt, L.next_cnt, a.blk_split, s, c->kt());
+            }
             out.active += N;
             out.rounds = 1;
-            launch_update_done(blk_done, a.blk_split, geo.nb, 0, s);
+            launch_update_done(blk_done, blk_last, a.blk_split, geo.nb, 0, s);
             if (after_round0) {
                 after_round0();
                 c->active = s;
@@ -588,14 +617,14 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             TScope t(c, KOLM_KT_SMALLSORT, "k_finalize_eq", (u64)h[C_EQ] * TILE * 8);
             launch_finalize_eq(L.eq, h[C_EQ], a, L, s);
         }
-        if (cyclic) launch_update_done(blk_done, a.blk_split, geo.nb, round, s);
+        if (cyclic) launch_update_done(blk_done, blk_last, a.blk_split, geo.nb, round, s);
         round_done(round);
         // the next list holds unresolved segments of >= 2 active elements each
         ncur = (u32)std::min<u64>(h[C_ACTIVE] / 2 + geo.nb, N / 2 + geo.nb);
         ncur_dev = L.next_cnt;
         std::swap(cur, nxt);
     }
-    if (cyclic) launch_rounds_sum(blk_done, geo.nb, out.rounds, c->get<u64>("rsum", 1), s);
+    if (cyclic) launch_rounds_sum(blk_last, geo.nb, c->get<u64>("rsum", 1), s);
     return out;
 }
 
@@ -833,7 +862,8 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     // the cyclic sort.  With the 8-character round 0 (eight streaming LSD passes beside the
     // LDS-bound parse): 53.8-54.2 ms per 256 MiB for 0, 54.1-54.2 for 1, 55.4-56.2 for 2.
     const bool serial = c->serial;
-    static const int overlap = getenv("KOLM_OVERLAP") ? atoi(getenv("KOLM_OVERLAP")) : 0;
+    // (the MSD round 0's LDS bucket sorts need whole CUs: the parse starts after round 0 there)
+    const int overlap = getenv("KOLM_OVERLAP") ? atoi(getenv("KOLM_OVERLAP")) : (r0_msd_mode() ? 2 : 0);
     hipStream_t ms = c->stream, s = serial ? c->stream : c->aux;
     Pipeline P{c, geo, d_text};
     hipEvent_t* ev = c->ev;
@@ -1247,8 +1277,10 @@ u8* upload_staged(kolm_ctx* c, const uint8_t* in, size_t n, u8* d = nullptr, hip
         if (!c->stage[j]) {
             KOLM_HIP_CHECK(hipHostMalloc((void**)&c->stage[j], STAGE_BYTES, hipHostMallocDefault));
             KOLM_HIP_CHECK(hipEventCreateWithFlags(&c->stage_ev[j], hipEventDisableTiming));
-        } else if (k >= kolm_ctx::NSTAGE) {
-            KOLM_HIP_CHECK(hipEventSynchronize(c->stage_ev[j]));  // its previous chunk has left
+        } else {
+            // the chunk's previous copy — of this call or of an earlier piece's call, whose
+            // DMA may still be reading it — has left (normally long complete: no wait)
+            KOLM_HIP_CHECK(hipEventSynchronize(c->stage_ev[j]));
         }
         const size_t len = std::min(STAGE_BYTES, n - o);
         pool.copy(c->stage[j], in + o, len);
@@ -1315,6 +1347,7 @@ int kolm_init(int device) {
 }
 
 int kolm_shutdown(void) {
+    comm_shutdown();
     std::lock_guard<std::mutex> g(g_mu);
     int r = KOLM_OK;
     for (kolm_ctx*& c : g_multi)
@@ -1362,8 +1395,10 @@ int kolm_dev_free(kolm_ctx* c, void* dptr) {
 int kolm_memcpy_h2d(kolm_ctx* c, void* dst, const void* src, uint64_t bytes) {
     if (!c) return KOLM_EARG;
     return guarded([&] {
-        KOLM_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
-        c->sync();
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        if (bytes) KOLM_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+        KOLM_HIP_CHECK(hipStreamSynchronize(c->stream));
         return KOLM_OK;
     });
 }
@@ -1371,8 +1406,10 @@ int kolm_memcpy_h2d(kolm_ctx* c, void* dst, const void* src, uint64_t bytes) {
 int kolm_memcpy_d2h(kolm_ctx* c, void* dst, const void* src, uint64_t bytes) {
     if (!c) return KOLM_EARG;
     return guarded([&] {
-        KOLM_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
-        c->sync();
+        std::lock_guard<std::mutex> g(c->mu);
+        KOLM_HIP_CHECK(hipSetDevice(c->device));
+        if (bytes) KOLM_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+        KOLM_HIP_CHECK(hipStreamSynchronize(c->stream));
         return KOLM_OK;
     });
 }
@@ -1750,14 +1787,17 @@ int kolm_encode_blocks_multi(int ngpu, const uint8_t* data, uint64_t total, uint
     // contiguous shards of whole blocks (the last block may be short)
     std::vector<u32> b0(G + 1);
     for (u32 r = 0; r <= G; ++r) b0[r] = (u32)((u64)nb * r / G);
+    // the shards' payloads stay in each device's arena until the reassembly below
+    static const bool host_gather = getenv("KOLM_MULTI_GATHER") && !strcmp(getenv("KOLM_MULTI_GATHER"), "host");
     struct Part {
         int rc = KOLM_OK;
         std::string err;
-        std::vector<u8> pay;
+        const u8* d_pay = nullptr;
         std::vector<u64> off;
         kolm_stats st{};
     };
     std::vector<Part> part(G);
+    std::vector<u64> pbase(G + 1, 0);
     auto run = [&](u32 r) {
         Part& P = part[r];
         const u32 nbr = b0[r + 1] - b0[r];
@@ -1791,35 +1831,69 @@ int kolm_encode_blocks_multi(int ngpu, const uint8_t* data, uint64_t total, uint
                                   sizes ? sizes + (u64)b0[r] * KOLM_NCAND : nullptr, method ? method + b0[r] : nullptr,
                                   P.off.data(), stats ? &P.st : nullptr);
             if (rc) return rc;
-            P.pay.resize(P.off[nbr]);
-            if (P.off[nbr]) {
-                KOLM_HIP_CHECK(hipMemcpyAsync(P.pay.data(), arena, P.off[nbr], hipMemcpyDeviceToHost, c->stream));
-                c->sync();
-            }
+            P.d_pay = arena;
             return KOLM_OK;
         });
         if (P.rc) P.err = g_err;
     };
-    std::vector<std::thread> th;
-    for (u32 r = 1; r < G; ++r) th.emplace_back(run, r);
-    run(0);
-    for (auto& t : th) t.join();
-    for (u32 r = 0; r < G; ++r)
-        if (part[r].rc) {
-            set_err(part[r].err);
-            return part[r].rc;
-        }
-    u64 pos = 0;
+    // host reassembly (KOLM_MULTI_GATHER=host): every device copies its payloads into its
+    // place in payload_arena (offsets known once every shard is encoded)
+    auto download = [&](u32 r) {
+        Part& P = part[r];
+        const u64 nbytes = P.off.back();
+        if (!nbytes || P.rc) return;
+        kolm_ctx* c = g_multi[r];
+        P.rc = guarded([&] {
+            std::lock_guard<std::mutex> g(c->mu);
+            KOLM_HIP_CHECK(hipSetDevice(c->device));
+            KOLM_HIP_CHECK(hipMemcpyAsync(payload_arena + pbase[r], P.d_pay, nbytes, hipMemcpyDeviceToHost, c->stream));
+            c->sync();
+            return KOLM_OK;
+        });
+        if (P.rc) P.err = g_err;
+    };
+    auto each = [&](const std::function<void(u32)>& f) {
+        std::vector<std::thread> th;
+        for (u32 r = 1; r < G; ++r) th.emplace_back(f, r);
+        f(0);
+        for (auto& t : th) t.join();
+        for (u32 r = 0; r < G; ++r)
+            if (part[r].rc) {
+                set_err(part[r].err);
+                return part[r].rc;
+            }
+        return (int)KOLM_OK;
+    };
+    if (int e = each(run)) return e;
+    for (u32 r = 0; r < G; ++r) pbase[r + 1] = pbase[r] + part[r].off.back();
+    if (pbase[G] > arena_cap) {
+        set_err("payload_arena too small");
+        return KOLM_ECAP;
+    }
     payload_off[0] = 0;
     for (u32 r = 0; r < G; ++r) {
         const u32 nbr = b0[r + 1] - b0[r];
-        if (pos + part[r].pay.size() > arena_cap) {
-            set_err("payload_arena too small");
-            return KOLM_ECAP;
+        for (u32 i = 1; i <= nbr; ++i) payload_off[b0[r] + i] = pbase[r] + part[r].off[i];
+    }
+    if (pbase[G] == 0) {
+        // no payload bytes (empty input): nothing to reassemble
+    } else if (host_gather) {
+        if (int e = each(download)) return e;
+    } else {
+        // RCCL: every device's payloads into device 0 over xGMI, one copy to the host
+        std::vector<int> devs(G);
+        std::vector<const u8*> dp(G);
+        std::vector<u64> nbytes(G);
+        for (u32 r = 0; r < G; ++r) {
+            devs[r] = (int)r;
+            dp[r] = part[r].d_pay;
+            nbytes[r] = part[r].off.back();
         }
-        if (!part[r].pay.empty()) std::memcpy(payload_arena + pos, part[r].pay.data(), part[r].pay.size());
-        for (u32 i = 1; i <= nbr; ++i) payload_off[b0[r] + i] = pos + part[r].off[i];
-        pos += part[r].pay.size();
+        std::unique_lock<std::mutex> g(g_mu);
+        std::vector<std::unique_lock<std::mutex>> held;
+        for (u32 r = 0; r < G; ++r) held.emplace_back(g_multi[r]->mu);
+        g.unlock();
+        if (int e = multi_rccl_gather(devs, dp, nbytes, payload_arena, arena_cap)) return e;
     }
     if (stats) {
         kolm_stats agg{};

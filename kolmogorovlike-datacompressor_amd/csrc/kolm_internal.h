@@ -308,8 +308,8 @@ void launch_tiny_sort(int c, const Seg* segs, u32 count, const SortArgs& a, cons
 void launch_small_sort(int c, const Seg* segs, u32 count, const SortArgs& a, const Lists& L,
                        hipStream_t s);
 void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists& L, hipStream_t s);
-void launch_rounds_sum(const u32* blk_done, u32 nb, u32 rounds, u64* out, hipStream_t s);
-void launch_update_done(u32* blk_done, const u32* blk_split, u32 nb, u32 round, hipStream_t s);
+void launch_rounds_sum(const u32* blk_last, u32 nb, u64* out, hipStream_t s);
+void launch_update_done(u32* blk_done, u32* blk_last, const u32* blk_split, u32 nb, u32 round, hipStream_t s);
 
 // ---- k_blocks.hip: per-block scans, Lyndon factors, BBWT gather ----
 u32 duval_span_bytes(const Geom& geo);  // bytes per Duval span of this batch (launch_lyndon's choice)
@@ -342,6 +342,24 @@ u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w,
                  hipStream_t s, KTimer* kt = nullptr);
 void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s,
                    KTimer* kt = nullptr);
+
+// ---- k_r0m.hip: round 0 as MSD radix partitions + LDS bucket sorts (same outputs) ----
+struct R0MBufs {
+    u32* x0;          // [N] level buffer B: low key words
+    u32* x1;          // [N] level buffer B: positions
+    u32* hist;        // [r0m_hist_rows * 256]
+    u32* cnt;         // [16] counters
+    void* fin[6];     // final bucket lists per class (12-byte records), capacities r0m_fin_cap
+    LSeg* segs[2];    // next-level segments per level parity [r0m_seg_cap]
+    LTile* tiles[2];  // their tiles [r0m_tile_cap]
+};
+u64 r0m_fin_cap(u64 N, u32 nb, int cls);
+u64 r0m_seg_cap(u64 N, u32 nb);
+u64 r0m_tile_cap(u64 N, u32 nb, u32 bs);
+u32 r0m_tiles(const Geom& geo);
+// returns the number of MSD levels run; h_cnt: pinned host scratch of >= 16 words
+u32 launch_round0_msd(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, R0MBufs& mb,
+                      hipStream_t s, KTimer* kt, u32* h_cnt);
 
 // ---- k_mtf.hip ----
 // bits (optional, [nb * 8], zeroed by the caller): the replay also adds each block's Rice-k
@@ -537,4 +555,15 @@ struct HipError {
     int line;
     HipError(hipError_t e, const char* w, int l) : err(e), what(w), line(l) {}
 };
+}  // namespace kolm
+
+// host-side links between kolm_api.cpp and kolm_comm.cpp (RCCL)
+#include <vector>
+struct kolm_ctx;
+namespace kolm {
+int ctx_device(const kolm_ctx* c);
+// kolm_encode_blocks_multi's reassembly over the process's devices (kolm_comm.cpp)
+int multi_rccl_gather(const std::vector<int>& devs, const std::vector<const u8*>& d_pay, const std::vector<u64>& nbytes,
+                      u8* host, u64 cap);
+void comm_shutdown();
 }  // namespace kolm

@@ -125,7 +125,18 @@ SIGNATURES = [
     ("kolm_result_copy", I32, [P, U64]),
     ("kolm_toc_write", I32, [I32, U32, U64, U32, P, P, P, P, U64, ctypes.POINTER(U64)]),
     ("kolm_toc_read", I32, [U8P, U64, P, ctypes.POINTER(U64), P, P, P, U32]),
+    ("kolm_comm_unique_id", I32, [P]),
+    ("kolm_comm_init", I32, [P, I32, I32, U8P, ctypes.POINTER(P)]),
+    ("kolm_comm_destroy", I32, [P]),
+    ("kolm_comm_rank", I32, [P, ctypes.POINTER(I32), ctypes.POINTER(I32)]),
+    ("kolm_comm_allreduce", I32, [P, P, U32, I32, I32]),
+    ("kolm_comm_barrier", I32, [P]),
+    ("kolm_gather_payloads", I32, [P, P, U64, P, P, U32, I32, P, U64, U32, P, P, P, P, I32]),
+    ("kolm_comm_wait", I32, [P]),
 ]
+KOLM_COMM_ID_BYTES = 128
+KOLM_ECAP = -2
+KOLM_ERCCL = -4
 KOLM_DECODE_MASK = 0x3FF  # methods decoded on the device: every id 0..9 (kolm.h)
 
 
@@ -223,6 +234,66 @@ def encode_blocks_device(ctx, d_data: int, n: int, block_size: int, d_arena: int
                                            sizes.ctypes.data, method.ctypes.data, off.ctypes.data,
                                            ctypes.byref(st)))
     return sizes[:nb], method[:nb], off, st.as_dict()
+
+
+class DeviceBuffer:
+    """Device memory of a context (kolm_dev_alloc): the input and payload arenas of the
+    device-resident entry points, without any other framework.  ptr is the device address."""
+
+    def __init__(self, ctx, nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        check(load().kolm_dev_alloc(ctx, max(self.nbytes, 1), ctypes.byref(p)))
+        self.ptr = int(p.value)
+
+    def upload(self, data, offset: int = 0):
+        """Copies host bytes (bytes / bytearray / memoryview / numpy) to ptr + offset."""
+        src = np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8) if len(data) else None
+        if src is None:
+            return
+        if offset + src.size > self.nbytes:
+            raise ValueError("upload exceeds the buffer")
+        check(load().kolm_memcpy_h2d(self.ctx, self.ptr + offset, src.ctypes.data, src.size))
+
+    def download(self, n: int = None, offset: int = 0) -> bytes:
+        n = self.nbytes - offset if n is None else int(n)
+        if offset + n > self.nbytes:
+            raise ValueError("download exceeds the buffer")
+        if n <= 0:
+            return b""
+        out = _new_bytes(n)
+        check(load().kolm_memcpy_d2h(self.ctx, ctypes.cast(ctypes.c_char_p(out), ctypes.c_void_p), self.ptr + offset,
+                                     n))
+        return out
+
+    def zero_tail(self, start: int):
+        """Zeroes [start, nbytes) (the 64-byte read-ahead padding behind an input)."""
+        if start < self.nbytes:
+            self.upload(bytes(self.nbytes - start), start)
+
+    def free(self):
+        if self.ptr:
+            check(load().kolm_dev_free(self.ctx, self.ptr))
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            if self.ptr and _lib is not None:
+                _lib.kolm_dev_free(self.ctx, self.ptr)
+                self.ptr = 0
+        except Exception:  # noqa: BLE001  (interpreter shutdown)
+            pass
+
+
+def input_buffer(ctx, data) -> "DeviceBuffer":
+    """The device copy of an input batch with its 64 bytes of zero read-ahead padding
+    (the layout kolm_encode_blocks_device expects)."""
+    n = len(data)
+    buf = DeviceBuffer(ctx, n + 64)
+    buf.upload(data)
+    buf.zero_tail(n)
+    return buf
 
 
 def arena_capacity(n: int, nb: int, cand_mask: int) -> int:

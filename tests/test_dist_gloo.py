@@ -1,16 +1,21 @@
-"""N>1 path on CPU: world_size-2 gloo process group.  Each rank encodes its contiguous
-block shard (here with the oracle standing in for the GPU encoder, which needs a
-device), the payload arenas and method ids are gathered with the same
-kolm.parallel.gather_payloads used on MI355X (RCCL there), and rank 0's reassembled
-container must equal the single-process container."""
+"""N>1 path on CPU: world_size-2/3 gloo process groups.  Each rank encodes its block shard
+(the oracle stands in for the GPU encoder, which needs a device), the shards travel through
+a gloo test transport with kolm.parallel.Comm's interface (tests/gloo_transport.py; the
+product gathers with RCCL behind the C ABI), and rank 0's container is built by the
+product's own reassembly (kolm.parallel.container_from_gathered) — it must equal the
+single-process container.  Also: the communicator-id bootstrap (TCP, no torch) at world 3,
+and kolm.parallel importing without torch."""
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
-import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
@@ -21,13 +26,18 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, data, bs, q, use_async=False, partition="contiguous"):
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    repo = os.path.dirname(here)
-    sys.path[:0] = [os.path.join(repo, "kolmogorovlike-datacompressor_amd"), os.path.join(repo, "oracle")]
+def _paths():
+    for p in (os.path.join(REPO, "kolmogorovlike-datacompressor_amd"), os.path.join(REPO, "oracle"),
+              os.path.join(REPO, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def _worker(rank, world, port, data, bs, q, partition="contiguous"):
+    _paths()
     import oracle as O
-    from kolm.parallel import assemble_container, gather_payloads, rank_blocks
+    from gloo_transport import GlooTransport
+    from kolm.parallel import container_from_gathered, rank_blocks
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -39,43 +49,29 @@ def _worker(rank, world, port, data, bs, q, use_async=False, partition="contiguo
             m = int(np.argmin([len(c) for c in cands]))
             mids.append(m)
             pays.append(cands[m])
-        blob = b"".join(pays)
-        offs = np.concatenate([[0], np.cumsum([len(p) for p in pays])]).astype(np.int64).tolist()
-        mx = torch.tensor([len(blob)], dtype=torch.int64)
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        arena = torch.zeros(max(int(mx[0]), 1), dtype=torch.uint8)
-        if blob:
-            arena[: len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
-        ids = torch.tensor(mids, dtype=torch.int32)
-        if use_async:  # bench.py's double-buffered form: the gather completes at wait()/result()
-            got_p, got_i = gather_payloads(arena, len(blob), ids, dst=0, async_op=True).result()
-        else:
-            got_p, got_i = gather_payloads(arena, len(blob), ids, dst=0)
-        all_offs = [None] * world
-        dist.all_gather_object(all_offs, offs)
+        offs = np.concatenate([[0], np.cumsum([len(p) for p in pays])]).astype(np.uint64)
+        g = GlooTransport().gather_host(b"".join(pays), mids, offs, dst=0)
         if rank == 0:
-            c = assemble_container(bs, len(data), [i.tolist() for i in got_i],
-                                   [p.numpy().tobytes() for p in got_p], all_offs, partition)
-            q.put(c)
+            q.put(container_from_gathered(g, bs, len(data), partition))
         else:
-            assert got_p is None and got_i is None
+            assert g is None
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,bs,n,use_async,partition", [
-    (2, 4096, 4096 * 5 + 123, False, "contiguous"), (2, 1000, 999, False, "contiguous"),
-    (3, 2048, 2048 * 4, False, "contiguous"), (2, 4096, 4096 * 3 + 7, True, "contiguous"),
-    (2, 4096, 4096 * 5 + 123, False, "round_robin"), (3, 2048, 2048 * 7 + 5, True, "round_robin")])
-def test_gloo_sharded_reassembly(world, bs, n, use_async, partition):
+@pytest.mark.parametrize("world,bs,n,partition", [
+    (2, 4096, 4096 * 5 + 123, "contiguous"), (2, 1000, 999, "contiguous"),
+    (3, 2048, 2048 * 4, "contiguous"), (2, 4096, 4096 * 3 + 7, "contiguous"),
+    (2, 4096, 4096 * 5 + 123, "round_robin"), (3, 2048, 2048 * 7 + 5, "round_robin"),
+    (3, 2048, 2048, "round_robin")])  # ranks 1 and 2 hold no block
+def test_gloo_sharded_reassembly(world, bs, n, partition):
     import oracle as O
     from kolm import datagen as D
     data = (D.enwik_like(n // 2, seed=5) + bytes(n // 4) + D.splitmix64_bytes(n, seed=9))[:n]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, data, bs, q, use_async, partition))
-             for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, data, bs, q, partition)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)
@@ -83,3 +79,48 @@ def test_gloo_sharded_reassembly(world, bs, n, use_async, partition):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got == O.compress_blocks_fixed(data, bs, range(10))
+
+
+def _boot(rank, world, port, q):
+    _paths()
+    from kolm.parallel import exchange_unique_id
+    uid = bytes(range(128)) if rank == 0 else None
+    q.put((rank, exchange_unique_id(rank, world, "127.0.0.1", port, uid, timeout=60)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_unique_id_bootstrap(world):
+    """kolm.parallel.exchange_unique_id: rank 0 serves the RCCL id's 128 bytes over TCP, every
+    rank ends with the same bytes (clients started first must wait for the server)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_boot, args=(r, world, port, q)) for r in reversed(range(world))]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=60) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert sorted(got) == list(range(world))
+    assert all(v == bytes(range(128)) for v in got.values())
+
+
+def test_parallel_imports_no_torch():
+    code = ("import sys; sys.path.insert(0, %r); import kolm.parallel, kolm; "
+            "assert 'torch' not in sys.modules, 'kolm.parallel pulled in torch'" %
+            os.path.join(REPO, "kolmogorovlike-datacompressor_amd"))
+    subprocess.run([sys.executable, "-c", code], check=True, timeout=120)
+
+
+def test_env_rendezvous(monkeypatch):
+    from kolm.parallel import env_rendezvous
+    monkeypatch.setenv("RANK", "3")
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", "29400")
+    monkeypatch.delenv("KOLM_COMM_PORT", raising=False)
+    assert env_rendezvous() == (3, 8, 3, "127.0.0.1", 29401)
+    monkeypatch.setenv("KOLM_COMM_PORT", "31000")
+    assert env_rendezvous()[4] == 31000

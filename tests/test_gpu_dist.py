@@ -1,6 +1,8 @@
-"""Distributed compress with real GPU encoding: 2 ranks share the box's one GPU (gloo for
-the exchange; RCCL needs one GPU per rank), each encodes its block shard through the C
-ABI, rank 0 reassembles; the container must equal the single-process one."""
+"""Distributed compress with real GPU encoding: 2 ranks share the box's one GPU (RCCL
+needs one GPU per rank, so the shards travel through the gloo test transport here), each
+encodes its block shard through the C ABI into a device arena, rank 0 reassembles with
+the product's kolm.parallel.compress_blocks_fixed_distributed; the container must equal
+the oracle's."""
 import os
 import socket
 
@@ -20,15 +22,17 @@ def _port():
 
 def _worker(rank, world, port, data, bs, q, partition):
     import sys
-    import torch  # noqa: F401  (first: shared HIP runtime)
     import torch.distributed as dist
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path[:0] = [os.path.join(repo, "kolmogorovlike-datacompressor_amd")]
+    sys.path[:0] = [os.path.join(repo, "kolmogorovlike-datacompressor_amd"), os.path.join(repo, "tests")]
+    from gloo_transport import GlooTransport
+    from kolm import _lib
     from kolm.parallel import compress_blocks_fixed_distributed
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out = compress_blocks_fixed_distributed(data, bs, partition=partition)
+        comm = GlooTransport(0, _lib.device_ctx(0))
+        out = compress_blocks_fixed_distributed(data, bs, comm=comm, partition=partition)
         if rank == 0:
             q.put(out)
         else:

@@ -25,10 +25,32 @@ def test_multibatch_container_and_stats(kolm_gpu, monkeypatch):
     many = kolm_gpu.compress_blocks_fixed(data, bs, hot_path=True)
     st4 = kolm_gpu.last_stats()
     assert many == want
-    # statistics of the batches add up: the LZ77 token count is a function of each block
-    # alone (the doubling-round sum is not: it counts the rounds of each batch)
+    # per-block statistics add up over the batches: the LZ77 token count is a function of
+    # each block alone.  The round sum counts round 0 through each block's last splitting
+    # round, but round 0 sorts by C = 64 / w characters with w the widest alphabet code of
+    # the BATCH (the random block has w = 8: C = 8; text alone w = 6: C = 10), so the 2-block
+    # batches without the random block start their doubling from 10 characters and need at
+    # most as many rounds (equality per batch composition: test_round_sum_batch_invariant)
     assert st4["lz_tokens"] == st1["lz_tokens"]
+    assert st4["cyc_rounds_sum"] <= st1["cyc_rounds_sum"]
     assert kolm_gpu.decompress(many) == data
+
+
+def test_round_sum_batch_invariant(kolm_gpu, monkeypatch):
+    """cyc_rounds_sum (SURVEY §8d's per-block R, the roofline contract's input) is a sum of
+    per-block quantities: batches of equal round-0 width give exactly the one-batch sum."""
+    bs = 65536
+    data = D.enwik_like(7 * bs, seed=21)  # every block: 50 distinct bytes, 6-bit codes
+    want = O.compress_blocks_fixed(data, bs, range(9))
+    one = kolm_gpu.compress_blocks_fixed(data, bs, hot_path=True)
+    st1 = kolm_gpu.last_stats()
+    for per in (1, 3):
+        monkeypatch.setenv("KOLM_BATCH_BYTES", str(per * bs + 100))
+        many = kolm_gpu.compress_blocks_fixed(data, bs, hot_path=True)
+        st = kolm_gpu.last_stats()
+        assert one == want and many == want
+        assert st["cyc_rounds_sum"] == st1["cyc_rounds_sum"], per
+        assert st["cyc_rounds_sum"] >= 8  # at least round 0 per block
 
 
 def test_concurrent_callers(kolm_gpu):

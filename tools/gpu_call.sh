@@ -32,8 +32,9 @@ for step in "$@"; do
         || { tail -40 "$OUT/gpu_tests.log"; exit 1; }
       tail -2 "$OUT/gpu_tests.log" ;;
     tests:*)
-      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${step#tests:}" \
-        > "$OUT/gpu_tests_k.log" 2>&1 || { tail -40 "$OUT/gpu_tests_k.log"; exit 1; }
+      # tests:EXPR with '+' for ' or ' (e.g. tests:rccl+gpu_dist)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        -k "$(echo "${step#tests:}" | sed 's/+/ or /g')" > "$OUT/gpu_tests_k.log" 2>&1 || { tail -40 "$OUT/gpu_tests_k.log"; exit 1; }
       tail -3 "$OUT/gpu_tests_k.log" ;;
     bench)
       timeout -k 10 600 python bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" \
@@ -74,6 +75,14 @@ if c:
       bash tools/gpu_profile.sh "$OUT/prof" || exit 1 ;;
     profile_full)
       bash tools/gpu_profile.sh "$OUT/prof_full" "--mib 256 --steps 1 --warmup 1 --kt-steps 1 --no-serial-pass --no-cpu-baseline --full-steps 1 --decode-steps 0 --cdc-steps 0 --v2-steps 0 --config-steps 0 --host-steps 0 --c4-steps 0" stats || exit 1 ;;
+    probe:*)
+      # probe:KIND — rocprofv3 kernel trace of tools/lz_probe.py KIND (4 batches, the last kernel-timed)
+      kind=${step#probe:}
+      PROBE_ITERS=4 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/probe_$kind" -o kt --output-format csv \
+        -- python3 tools/lz_probe.py "$kind" > "$OUT/probe_$kind.log" 2>&1 || { tail -30 "$OUT/probe_$kind.log"; exit 1; }
+      KOLM_DEBUG_ROUNDS=1 KOLM_HOST_PROF=1 PROBE_ITERS=3 timeout -k 10 300 python3 tools/lz_probe.py "$kind" \
+        > "$OUT/probe_${kind}_rounds.log" 2>&1 || { tail -30 "$OUT/probe_${kind}_rounds.log"; exit 1; }
+      head -3 "$OUT/probe_$kind.log" | cut -c1-400 ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

@@ -7,7 +7,6 @@ import os
 import sys
 
 import numpy as np
-import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "kolmogorovlike-datacompressor_amd")]
@@ -20,29 +19,30 @@ def main():
     part = int(sys.argv[3]) if len(sys.argv) > 3 else -1  # one 1 MiB block of the input only
     data = {"mixed": datagen.mixed_corpus, "gradient": lambda: datagen.gradient_bmp()[: 1 << 20],
             "wav": datagen.sine_wav, "checker": datagen.checker_bmp,
-            "text": lambda: datagen.enwik_like(256 << 20), "text32": lambda: datagen.enwik_like(32 << 20)}[kind]()
+            "text": lambda: datagen.enwik_like(256 << 20), "text32": lambda: datagen.enwik_like(32 << 20),
+            # BASELINE config 4's per-GPU shard at N = 8: blocks i = 0 (mod 8) of the 256 MiB stream
+            "c4shard": lambda: b"".join(memoryview(datagen.enwik_like(256 << 20))[i << 20:(i + 1) << 20]
+                                        for i in range(0, 256, 8))}[kind]()
     if part >= 0:
         data = data[part << 20:(part + 1) << 20]
-    torch.cuda.init()
-    torch.empty(1, device="cuda")
     _lib.ensure_init(0)
     L = _lib.load()
     ctx = ctypes.c_void_p()
     _lib.check(L.kolm_ctx_create(0, ctypes.byref(ctx)))
     n, bs = len(data), 1 << 20
     nb = (n + bs - 1) // bs
-    d = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
-    d[:n].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    d = _lib.input_buffer(ctx, data)
     cap = 9 * n + 4096
-    ar = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    ar = _lib.DeviceBuffer(ctx, cap)
     sz = np.zeros((nb, _lib.KOLM_NCAND), np.uint32)
     m = np.zeros(nb, np.uint32)
     o = np.zeros(nb + 1, np.uint64)
-    for it in range(3):
+    iters = int(os.environ.get("PROBE_ITERS", "3"))
+    for it in range(iters):
         st = _lib.Stats()
-        if it == 2:
+        if it == iters - 1:
             _lib.check(L.kolm_ctx_set_timing(ctx, 1))
-        _lib.check(L.kolm_encode_blocks_device(ctx, d.data_ptr(), n, bs, mask, None, ar.data_ptr(), cap,
+        _lib.check(L.kolm_encode_blocks_device(ctx, d.ptr, n, bs, mask, None, ar.ptr, cap,
                                                sz.ctypes.data, m.ctypes.data, o.ctypes.data, ctypes.byref(st)))
     _lib.check(L.kolm_ctx_set_timing(ctx, 0))
     sd = st.as_dict()
