@@ -470,8 +470,9 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
                 mb.x1 = c->get<u32>("r0m_x1", N);
                 mb.hist = c->get<u32>("r0m_hist", r0m_tile_cap(N, geo.nb, geo.bs) * 256);
                 mb.cnt = c->get<u32>("r0m_cnt", 16);
-                static const char* const fn[6] = {"r0m_f0", "r0m_f1", "r0m_f2", "r0m_f3", "r0m_f4", "r0m_f5"};
-                for (int k = 0; k < 6; ++k) mb.fin[k] = c->get<u32>(fn[k], 3 * r0m_fin_cap(N, geo.nb, k));
+                static const char* const fn[R0M_NCLS] = {"r0m_f0", "r0m_f1", "r0m_f2", "r0m_f3", "r0m_f4", "r0m_f5",
+                                                         "r0m_f6", "r0m_f7", "r0m_f8", "r0m_f9", "r0m_f10"};
+                for (int k = 0; k < R0M_NCLS; ++k) mb.fin[k] = c->get<u32>(fn[k], 3 * r0m_fin_cap(N, geo.nb, k));
                 for (int k = 0; k < 2; ++k) {
                     mb.segs[k] = c->get<LSeg>(k ? "r0m_s1" : "r0m_s0", r0m_seg_cap(N, geo.nb));
                     mb.tiles[k] = c->get<LTile>(k ? "r0m_t1" : "r0m_t0", r0m_tile_cap(N, geo.nb, geo.bs));

@@ -344,12 +344,13 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
                    KTimer* kt = nullptr);
 
 // ---- k_r0m.hip: round 0 as MSD radix partitions + LDS bucket sorts (same outputs) ----
+constexpr int R0M_NCLS = 11;  // final bucket classes of k_r0m.hip
 struct R0MBufs {
     u32* x0;          // [N] level buffer B: low key words
     u32* x1;          // [N] level buffer B: positions
     u32* hist;        // [r0m_hist_rows * 256]
     u32* cnt;         // [16] counters
-    void* fin[6];     // final bucket lists per class (12-byte records), capacities r0m_fin_cap
+    void* fin[R0M_NCLS];  // final bucket lists per class (12-byte records), capacities r0m_fin_cap
     LSeg* segs[2];    // next-level segments per level parity [r0m_seg_cap]
     LTile* tiles[2];  // their tiles [r0m_tile_cap]
 };

@@ -96,10 +96,10 @@ def test_rccl_c_abi_world1_matches_oracle():
     rc, msg = got["erccl"]
     assert rc == -4 and "RCCL" in msg, (rc, msg)
     ids, pays = got["multi"]
-    data = cases[0][1]
+    data, bs0 = cases[0][1], cases[0][2]
     wids = []
-    for i in range(0, len(data), bs):
-        blk = data[i:i + bs]
+    for i in range(0, len(data), bs0):
+        blk = data[i:i + bs0]
         c = [O.candidate(m, blk) for m in range(10)]
         m = min(range(10), key=lambda k: len(c[k]))
         wids.append(m)
