@@ -346,6 +346,121 @@ __global__ __launch_bounds__(WG) void k_lsd_scatter_w(LsdGeom g, const u32* Kin,
     }
 }
 
+// LSD pass without a histogram pass ("sweep"): every block is cut into S segments of 2^lt
+// tiles; one workgroup per (block, segment) walks its tiles in order with running per-digit
+// destinations in LDS (k_lsd_scatter_w's ranking per tile), so no per-tile histograms or scan
+// launch are needed.  The bases come from per-(block, segment) digit counts that the previous
+// pass (or k_keypos_r0, for the first) accumulated: while it scatters, every element also
+// counts the NEXT pass's digit (NM: 0 none, 1 digit P + 1 of the same key, 2 digit 0 of the
+// gathered key Kg) for the segment its destination slot falls in (LDS, one global atomic per
+// nonzero (segment, digit) per workgroup).
+constexpr u32 SW_SMAX = 8;  // segments per block (8 KB of next-digit counters: the kernel's 21 KB of
+                            // LDS still fits beside the LZ77 parse's 137.7 KB per CU)
+constexpr u32 LSD_TS = 12;
+static_assert((1u << LSD_TS) == LSD_T, "sweep segments are counted in 2^12-element tiles");
+template <int P, int SRC, int G, int NM>
+__global__ __launch_bounds__(WG) void k_lsd_sweep(LsdGeom g, u32 S, u32 lt, const u32* Kin, const u32* Pin, u32* Kout,
+                                                  u32* Pout, const u32* Kg, const u32* cin, u32* cout) {
+    __shared__ u32 wc[WG / 64][256];
+    __shared__ u32 running[256];
+    __shared__ u16 loc[LSD_T];
+    __shared__ u32 nc[NM ? SW_SMAX : 1][256];
+    __shared__ u32 sh[WG / 64];
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u32 id = xcd_tile();  // (block, segment): one block's segments on one XCD
+    const u32 b = id / S, sg = id - b * S;
+    const u32 base = g.geo.base(b), bend = g.geo.end(b);
+    {
+        u32 tot = 0, pre = 0;
+        for (u32 q = 0; q < S; ++q) {
+            const u32 c = cin[((u64)b * S + q) * 256 + tid];
+            tot += c;
+            pre += q < sg ? c : 0u;
+        }
+        const u32 incl = wave_incl_scan(tot, OpAddU(), 0u);
+        if (lane == 63) sh[w] = incl;
+        __syncthreads();
+        u32 carry = 0;
+        for (u32 i = 0; i < w; ++i) carry += sh[i];
+        running[tid] = base + carry + incl - tot + pre;
+        if (NM) {
+            for (u32 q = 0; q < S; ++q) nc[q][tid] = 0;
+        }
+    }
+    const u32 k0 = sg << lt, k1 = min(g.tpb, (sg + 1) << lt);
+    const u64 lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    u16* lw = loc + w * (LSD_T / 4) + lane;
+    for (u32 kt = k0; kt < k1; ++kt) {
+        const u32 lo = base + kt * LSD_T;
+        if (lo >= bend) break;
+        const u32 hi = min(lo + LSD_T, bend);
+#pragma unroll
+        for (int i = 0; i < WG / 64; ++i) wc[i][tid] = 0;
+        u32 key[LSD_PT], pos[LSD_PT];
+        const u32 q0 = lo + w * (LSD_T / 4);
+#pragma unroll
+        for (u32 j = 0; j < LSD_PT; ++j) {
+            const u32 i = q0 + j * 64 + lane;
+            key[j] = 0;
+            pos[j] = 0;
+            if (i < hi) {
+                key[j] = Kin[i];
+                pos[j] = SRC == SRC_KP ? i : Pin[i];
+            }
+        }
+        u32 kg[G ? LSD_PT : 1];
+        if (G) {
+#pragma unroll
+            for (u32 j = 0; j < LSD_PT; ++j) kg[j] = q0 + j * 64 + lane < hi ? Kg[pos[j]] : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (u32 j = 0; j < LSD_PT; ++j) {
+            const bool valid = q0 + j * 64 + lane < hi;
+            const u32 dg = digit<P>(key[j]);
+            u64 m = __ballot(valid);
+#pragma unroll
+            for (u32 bit = 0; bit < 8; ++bit) {
+                const u64 bal = __ballot((dg >> bit) & 1u);
+                m &= ((dg >> bit) & 1u) ? bal : ~bal;
+            }
+            const u32 rank = __popcll(m & lt_mask);
+            const u32 pre = valid ? wc[w][dg] : 0u;
+            lw[j * 64] = (u16)(pre + rank);
+            if (valid && rank == 0) wc[w][dg] = pre + (u32)__popcll(m);
+        }
+        __syncthreads();
+        {
+            u32 acc = running[tid];
+#pragma unroll
+            for (int q = 0; q < WG / 64; ++q) {
+                const u32 c = wc[q][tid];
+                wc[q][tid] = acc;
+                acc += c;
+            }
+            running[tid] = acc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (u32 j = 0; j < LSD_PT; ++j) {
+            if (q0 + j * 64 + lane < hi) {
+                const u32 dst = wc[w][digit<P>(key[j])] + lw[j * 64];
+                const u32 kout = G ? kg[G ? j : 0] : key[j];
+                Kout[dst] = kout;
+                Pout[dst] = pos[j];
+                if (NM) atomicAdd(&nc[(dst - base) >> (LSD_TS + lt)][NM == 2 ? digit<0>(kout) : digit<(P + 1) & 3>(kout)], 1u);
+            }
+        }
+        __syncthreads();
+    }
+    if (NM) {
+        for (u32 q = 0; q < S; ++q) {
+            const u32 v = nc[q][tid];
+            if (v) atomicAdd(&cout[((u64)b * S + q) * 256 + tid], v);
+        }
+    }
+}
+
 __device__ inline u32 wave_max(u32 v) { return wave_reduce(v, OpMaxU(), 0u); }
 
 // per block: exclusive max over its tiles (one workgroup per block)
@@ -694,14 +809,14 @@ __global__ __launch_bounds__(WG) void k_alpha_codes(const u32* pres, u8* code, u
 // pass needs no histogram kernel of its own; top: the counts of KB's top byte instead (the
 // first MSD digit of the MSD round 0, k_r0m.hip, which passes sh = 64 - C w).
 __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32 C, u32 w, u32 sh, u32* KA, u32* KB,
-                                                  u32* hist0, u32 top) {
+                                                  u32* hist0, u32 top, u32 segS = 0, u32 seglt = 0) {
     __shared__ __align__(16) u8 tx[LSD_T + 64];
     __shared__ u8 cd[256];
     __shared__ u32 h0[WG / 64][256];
     u32 lo, hi, b;
     const u32 tile = xcd_tile();
     if (!g.range(tile, lo, hi, b)) {  // a tile past its block's end (the whole workgroup)
-        if (hist0) hist0[(u64)tile * 256 + threadIdx.x] = 0;
+        if (hist0 && !segS) hist0[(u64)tile * 256 + threadIdx.x] = 0;
         return;
     }
     if (hist0) {
@@ -784,8 +899,13 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
     }
     if (hist0) {
         __syncthreads();
-        hist0[(u64)tile * 256 + threadIdx.x] = h0[0][threadIdx.x] + h0[1][threadIdx.x] + h0[2][threadIdx.x] +
-                                               h0[3][threadIdx.x];
+        const u32 v = h0[0][threadIdx.x] + h0[1][threadIdx.x] + h0[2][threadIdx.x] + h0[3][threadIdx.x];
+        if (!segS) {
+            hist0[(u64)tile * 256 + threadIdx.x] = v;
+        } else if (v) {  // sweep passes: counts per (block, segment of 2^seglt tiles), zeroed by the host
+            const u32 seg = (tile - b * g.tpb) >> seglt;
+            atomicAdd(&hist0[((u64)b * segS + seg) * 256 + threadIdx.x], v);
+        }
     }
 }
 
@@ -829,6 +949,45 @@ void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kou
             k_lsd_scatter_w<P, SRC, G><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
         else
             k_lsd_scatter<P, SRC, G><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
+    }
+}
+
+// one sweep pass (k_lsd_sweep): nm = the next pass's digit mode (0 none, 1 P + 1, 2 digit 0 of Kg)
+template <int P, int SRC, int G, int NM>
+void sweep_one(const LsdGeom& g, u32 S, u32 lt, const u32* kin, const u32* pin, u32* kout, u32* pout, const u32* kg,
+               const u32* cin, u32* cout, hipStream_t s, KTimer* kt) {
+    static const std::string nm = "k_lsd_sweep<" + std::to_string(P) + ", " + std::to_string(SRC) + ", " +
+                                  std::to_string(G) + ", " + std::to_string(NM) + ">";
+    const u64 N = g.geo.N;
+    KScope k(kt, KT_LSD, nm.c_str(), (SRC == SRC_KP ? 12 : 16) * N + (G ? 4 * N : 0));
+    k_lsd_sweep<P, SRC, G, NM><<<g.geo.nb * S, WG, 0, s>>>(g, S, lt, kin, pin, kout, pout, kg, cin, cout);
+}
+template <int P, int SRC>
+void sweep_pg(int gat, int nm, const LsdGeom& g, u32 S, u32 lt, const u32* kin, const u32* pin, u32* kout, u32* pout,
+              const u32* kg, const u32* cin, u32* cout, hipStream_t s, KTimer* kt) {
+    if (gat) {
+        if constexpr (P == 3 && SRC == SRC_PAIR) sweep_one<P, SRC, 1, 2>(g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
+        return;
+    }
+    if (nm == 1) {
+        if constexpr (P < 3) sweep_one<P, SRC, 0, 1>(g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
+    } else {
+        sweep_one<P, SRC, 0, 0>(g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
+    }
+}
+void sweep_pass(int P, bool src_kp, bool gat, int nm, const LsdGeom& g, u32 S, u32 lt, const u32* kin, const u32* pin,
+                u32* kout, u32* pout, const u32* kg, const u32* cin, u32* cout, hipStream_t s, KTimer* kt) {
+    if (src_kp) {  // the first pass: keys by position
+        switch (P) {
+            case 0: return sweep_pg<0, SRC_KP>(gat, nm, g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
+            default: return;
+        }
+    }
+    switch (P) {
+        case 0: return sweep_pg<0, SRC_PAIR>(gat, nm, g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
+        case 1: return sweep_pg<1, SRC_PAIR>(gat, nm, g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
+        case 2: return sweep_pg<2, SRC_PAIR>(gat, nm, g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
+        default: return sweep_pg<3, SRC_PAIR>(gat, nm, g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
     }
 }
 
@@ -901,24 +1060,53 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
     // fall into the first pass's digit (its few distinct values keep that scatter's runs long)
     const u32 bits = t.chars * t.w, D = (bits + 7) / 8, sh = 8 * D - bits;
     const u32 pa = std::min<u32>(4, D), pb = D - pa;
-    {
-        // text + FEd 2 (+ factor starts near factor ends), KA 4 (+ KB 4)
-        KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6));
-        k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist, 0);
-    }
     u32* K[2] = {t.K2, t.K22};
     u32* S[2] = {t.SA, t.SA2};
     const u32 T = pa + pb;
     int o = (T & 1) ? 0 : 1;  // output pair of the first pass: the last one lands in (K2, SA)
-    for (u32 q = 0; q < pa; ++q) {
-        const bool first = q == 0, gat = q + 1 == pa && pb > 0;
-        run_pass((int)q, first, gat, g, nt, first ? t.RK : K[o ^ 1], first ? nullptr : S[o ^ 1], K[o], S[o],
-                 gat ? t.KP : nullptr, t.hist, first, s, kt);
-        o ^= 1;
-    }
-    for (u32 q = 0; q < pb; ++q) {
-        run_pass((int)q, false, false, g, nt, K[o ^ 1], S[o ^ 1], K[o], S[o], nullptr, t.hist, false, s, kt);
-        o ^= 1;
+    // KOLM_LSD_SWEEP=1: sweep passes (no histogram / scan launches; measured slower);
+    // default: per-tile histogram + scan + scatter launches
+    const char* swe = getenv("KOLM_LSD_SWEEP");
+    const bool sweep = swe && atoi(swe) != 0 && t.swc;
+    if (sweep) {
+        u32 lt = 0;
+        while (((g.tpb + (1u << lt) - 1) >> lt) > SW_SMAX) ++lt;
+        const u32 SS = (g.tpb + (1u << lt) - 1) >> lt;
+        const u64 cw = (u64)geo.nb * SS * 256;
+        u32* cnt[2] = {t.swc, t.swc + cw};
+        KOLM_HIP_CHECK(hipMemsetAsync(cnt[0], 0, sizeof(u32) * cw, s));
+        {
+            KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6));
+            k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, cnt[0], 0, SS, lt);
+        }
+        u32 pidx = 0;
+        for (u32 half = 0; half < 2; ++half) {
+            const u32 np = half ? pb : pa;
+            for (u32 q = 0; q < np; ++q, ++pidx) {
+                const bool first = half == 0 && q == 0, gat = half == 0 && q + 1 == pa && pb > 0;
+                const int nm = q + 1 < np ? 1 : (half == 0 && pb > 0 ? 2 : 0);
+                if (nm) KOLM_HIP_CHECK(hipMemsetAsync(cnt[(pidx + 1) & 1], 0, sizeof(u32) * cw, s));
+                sweep_pass((int)q, first, gat, nm, g, SS, lt, first ? t.RK : K[o ^ 1], first ? nullptr : S[o ^ 1], K[o],
+                           S[o], gat ? t.KP : nullptr, cnt[pidx & 1], cnt[(pidx + 1) & 1], s, kt);
+                o ^= 1;
+            }
+        }
+    } else {
+        {
+            // text + FEd 2 (+ factor starts near factor ends), KA 4 (+ KB 4)
+            KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6));
+            k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist, 0);
+        }
+        for (u32 q = 0; q < pa; ++q) {
+            const bool first = q == 0, gat = q + 1 == pa && pb > 0;
+            run_pass((int)q, first, gat, g, nt, first ? t.RK : K[o ^ 1], first ? nullptr : S[o ^ 1], K[o], S[o],
+                     gat ? t.KP : nullptr, t.hist, first, s, kt);
+            o ^= 1;
+        }
+        for (u32 q = 0; q < pb; ++q) {
+            run_pass((int)q, false, false, g, nt, K[o ^ 1], S[o ^ 1], K[o], S[o], nullptr, t.hist, false, s, kt);
+            o ^= 1;
+        }
     }
     // RK through position windows (k_r0_rk) when every block has at most 256 of them;
     // KOLM_R0F_WIN=0: the direct scatter
