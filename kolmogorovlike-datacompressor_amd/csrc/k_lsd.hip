@@ -81,10 +81,25 @@ __device__ inline void load16nt(const u32* X, u32 i0, u32 hi, u32 (&v)[LSD_PT]) 
 }
 
 // where a pass reads its (key, position) pairs: keys by position (first pass) or pairs
-enum Src { SRC_KP = 1, SRC_PAIR = 2 };
+// SRC_PK: one packed word per element, (digit 3 of the key) << 24 | position - block base (the
+// first half's last pass reads what its previous pass wrote that way: 8 bytes less per element)
+enum Src { SRC_KP = 1, SRC_PAIR = 2, SRC_PK = 3 };
+
+// Per-(block, part) digit totals for k_lsd_scan2: a block's tiles form parts of 2^plt tiles.
+struct ScanParts {
+    u32* cur = nullptr;    // [nb * np * 256] this pass's totals (accumulated by the histogram)
+    u32* other = nullptr;  // the other buffer: k_lsd_scan2 zeroes it for the pass after next
+    u32 np = 0, plt = 0;
+};
+__device__ inline void add_part_total(const LsdGeom& g, const ScanParts& sp, u32 t, u32 v) {
+    if (sp.cur && v) {
+        const u32 b = t / g.tpb, k = t - b * g.tpb;
+        atomicAdd(&sp.cur[((u64)b * sp.np + (k >> sp.plt)) * 256 + threadIdx.x], v);
+    }
+}
 
 template <int P, int SRC>
-__global__ __launch_bounds__(WG) void k_lsd_hist(LsdGeom g, const u32* K, u32* hist) {
+__global__ __launch_bounds__(WG) void k_lsd_hist(LsdGeom g, const u32* K, u32* hist, ScanParts sp) {
     __shared__ u32 h[WG / 64][256];
     const u32 tid = threadIdx.x, w = tid >> 6;
 #pragma unroll
@@ -113,7 +128,45 @@ __global__ __launch_bounds__(WG) void k_lsd_hist(LsdGeom g, const u32* K, u32* h
         }
     }
     __syncthreads();
-    hist[(u64)xcd_tile() * 256 + tid] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+    const u32 v = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+    hist[(u64)xcd_tile() * 256 + tid] = v;
+    add_part_total(g, sp, xcd_tile(), v);
+}
+
+// hist[t][d] -> absolute destination of the first element of digit d in tile t, one
+// workgroup per (block, part of 2^plt tiles): the block's digit totals and the earlier parts'
+// counts come from the per-part totals, so the sequential chain is one part long.  Zeroes its
+// entries of the other totals buffer (the pass after next accumulates there).
+__global__ __launch_bounds__(WG) void k_lsd_scan2(LsdGeom g, u32* hist, ScanParts sp) {
+    __shared__ u32 sh[WG / 64];
+    const u32 b = blockIdx.x / sp.np, part = blockIdx.x - b * sp.np, d = threadIdx.x, lane = d & 63, w = d >> 6;
+    u32 tot = 0, pre = 0;
+    for (u32 q = 0; q < sp.np; ++q) {
+        const u32 c = sp.cur[((u64)b * sp.np + q) * 256 + d];
+        tot += c;
+        pre += q < part ? c : 0u;
+    }
+    const u32 incl = wave_incl_scan(tot, OpAddU(), 0u);
+    if (lane == 63) sh[w] = incl;
+    __syncthreads();
+    u32 carry = 0;
+    for (u32 i = 0; i < w; ++i) carry += sh[i];
+    u32 run = g.geo.base(b) + carry + incl - tot + pre;
+    const u64 t0 = (u64)b * g.tpb;
+    const u32 k0 = part << sp.plt, k1 = min(g.tpb, (part + 1) << sp.plt);
+    constexpr u32 B = 16;
+    for (u32 k = k0; k < k1; k += B) {
+        u32 v[B];
+#pragma unroll
+        for (u32 j = 0; j < B; ++j) v[j] = k + j < k1 ? hist[(t0 + k + j) * 256 + d] : 0u;
+#pragma unroll
+        for (u32 j = 0; j < B; ++j)
+            if (k + j < k1) {
+                hist[(t0 + k + j) * 256 + d] = run;
+                run += v[j];
+            }
+    }
+    sp.other[((u64)b * sp.np + part) * 256 + d] = 0;
 }
 
 // hist[t][d] -> absolute destination of the first element of digit d in tile t.
@@ -273,9 +326,11 @@ __global__ __launch_bounds__(WG) void k_lsd_scatter(LsdGeom g, const u32* Kin, c
 // per digit the waves' counts become bases (tile base + counts of the lower waves), and
 // pass 2 writes every element to base + offset.  Same order as k_lsd_scatter: (wave, step,
 // lane) is tile order.
-template <int P, int SRC, int G>
+// OPK: write the packed word (digit 3 << 24 | position - block base) instead of (key, position)
+template <int P, int SRC, int G, int OPK = 0>
 __global__ __launch_bounds__(WG) void k_lsd_scatter_w(LsdGeom g, const u32* Kin, const u32* Pin, u32* Kout,
                                                      u32* Pout, const u32* Kg, const u32* hist) {
+    static_assert(SRC != SRC_PK || P == 3, "packed words hold digit 3 only");
     // few registers on purpose (keys and positions, offsets in LDS): the pass runs beside
     // the LZ77 parse, which holds 4 waves per SIMD, and a 108-VGPR version of this kernel
     // was starved for the parse's whole duration (one pass 1.7 -> 11 ms)
@@ -297,7 +352,7 @@ __global__ __launch_bounds__(WG) void k_lsd_scatter_w(LsdGeom g, const u32* Kin,
         pos[j] = 0;
         if (i < hi) {
             key[j] = Kin[i];
-            pos[j] = SRC == SRC_KP ? i : Pin[i];
+            pos[j] = SRC == SRC_KP ? i : SRC == SRC_PK ? g.geo.base(b) + (key[j] & 0xFFFFFFu) : Pin[i];
         }
     }
     // G: the next key gathered by position up front (its latency under the ranking; at
@@ -340,8 +395,12 @@ __global__ __launch_bounds__(WG) void k_lsd_scatter_w(LsdGeom g, const u32* Kin,
     for (u32 j = 0; j < LSD_PT; ++j) {
         if (q0 + j * 64 + lane < hi) {
             const u32 dst = wc[w][digit<P>(key[j])] + lw[j * 64];
-            Kout[dst] = G ? kg[G ? j : 0] : key[j];
-            Pout[dst] = pos[j];
+            if (OPK) {
+                Kout[dst] = (key[j] & 0xFF000000u) | (pos[j] - g.geo.base(b));
+            } else {
+                Kout[dst] = G ? kg[G ? j : 0] : key[j];
+                Pout[dst] = pos[j];
+            }
         }
     }
 }
@@ -809,7 +868,8 @@ __global__ __launch_bounds__(WG) void k_alpha_codes(const u32* pres, u8* code, u
 // pass needs no histogram kernel of its own; top: the counts of KB's top byte instead (the
 // first MSD digit of the MSD round 0, k_r0m.hip, which passes sh = 64 - C w).
 __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32 C, u32 w, u32 sh, u32* KA, u32* KB,
-                                                  u32* hist0, u32 top, u32 segS = 0, u32 seglt = 0) {
+                                                  u32* hist0, u32 top, u32 segS = 0, u32 seglt = 0,
+                                                  ScanParts sp = ScanParts{}) {
     __shared__ __align__(16) u8 tx[LSD_T + 64];
     __shared__ u8 cd[256];
     __shared__ u32 h0[WG / 64][256];
@@ -902,6 +962,7 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
         const u32 v = h0[0][threadIdx.x] + h0[1][threadIdx.x] + h0[2][threadIdx.x] + h0[3][threadIdx.x];
         if (!segS) {
             hist0[(u64)tile * 256 + threadIdx.x] = v;
+            add_part_total(g, sp, tile, v);
         } else if (v) {  // sweep passes: counts per (block, segment of 2^seglt tiles), zeroed by the host
             const u32 seg = (tile - b * g.tpb) >> seglt;
             atomicAdd(&hist0[((u64)b * segS + seg) * 256 + threadIdx.x], v);
@@ -909,23 +970,27 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
     }
 }
 
-template <int P, int SRC, int G>
+template <int P, int SRC, int G, int OPK>
 void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kout, u32* pout, const u32* kg,
-              u32* hist, bool counted, hipStream_t s, KTimer* kt) {
+              u32* hist, bool counted, hipStream_t s, KTimer* kt, const ScanParts& sp) {
     static const std::string hn = "k_lsd_hist<" + std::to_string(P) + ", " + std::to_string(SRC) + ">";
     // A/B switch KOLM_LSD_SW: 0 = k_lsd_scatter everywhere, 1 = except the first pass (keys
     // by position), 2 = k_lsd_scatter_w everywhere (default); the timer carries the launched name
     static const int sw = getenv("KOLM_LSD_SW") ? atoi(getenv("KOLM_LSD_SW")) : 2;
     const bool use_w = sw == 2 || (sw == 1 && SRC == SRC_PAIR);
-    static const std::string tail = "<" + std::to_string(P) + ", " + std::to_string(SRC) + ", " + std::to_string(G) + ">";
+    static const std::string tail = "<" + std::to_string(P) + ", " + std::to_string(SRC) + ", " + std::to_string(G) +
+                                    (OPK ? ", 1>" : ">");
     static const std::string sn_w = "k_lsd_scatter_w" + tail, sn_p = "k_lsd_scatter" + tail;
     const std::string& sn = use_w ? sn_w : sn_p;
     const u64 N = g.geo.N, H = (u64)nt * 1024;  // H: per-tile histogram bytes
     if (!counted) {  // counted: the producer of kin wrote the tile histograms
         KScope k(kt, KT_LSD, hn.c_str(), 4 * N + H);
-        k_lsd_hist<P, SRC><<<nt, WG, 0, s>>>(g, kin, hist);
+        k_lsd_hist<P, SRC><<<nt, WG, 0, s>>>(g, kin, hist, sp);
     }
-    {
+    if (sp.cur) {
+        KScope k(kt, KT_LSD, "k_lsd_scan2", 2 * H);
+        k_lsd_scan2<<<g.geo.nb * sp.np, WG, 0, s>>>(g, hist, sp);
+    } else {
         KScope k(kt, KT_LSD, "k_lsd_scan", 3 * H);
         // four threads per digit for batches of fewer than 64 blocks (a latency-bound workgroup
         // per block; on full batches the 1024-thread workgroups wait beside the LZ77 parse:
@@ -942,12 +1007,14 @@ void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kou
     }
     {
         // key + position in (the first pass reads the key by position only) and out; G: + the gather
-        KScope k(kt, KT_LSD, sn.c_str(), (SRC == SRC_KP ? 12 : 16) * N + (G ? 4 * N : 0) + H);
+        // bytes in: key (+ position unless implicit or packed); out: key + position, or the packed word
+        const u64 in = SRC == SRC_PAIR ? 8 : 4, outb = OPK ? 4 : 8;
+        KScope k(kt, KT_LSD, sn.c_str(), (in + outb) * N + (G ? 4 * N : 0) + H);
         // k_lsd_scatter_w (three barriers per tile; 256 MiB text, overlapped: 1.5-1.7 -> 0.9-1.0
         // ms per pass)
-        if (use_w)
-            k_lsd_scatter_w<P, SRC, G><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
-        else
+        if (use_w || OPK || SRC == SRC_PK)
+            k_lsd_scatter_w<P, SRC, G, OPK><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
+        else if constexpr (SRC != SRC_PK)
             k_lsd_scatter<P, SRC, G><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
     }
 }
@@ -992,17 +1059,21 @@ void sweep_pass(int P, bool src_kp, bool gat, int nm, const LsdGeom& g, u32 S, u
 }
 
 using PassFn = void (*)(const LsdGeom&, u32, const u32*, const u32*, u32*, u32*, const u32*, u32*, bool, hipStream_t,
-                        KTimer*);
+                        KTimer*, const ScanParts&);
 template <int P>
 constexpr PassFn pass_of(int src_kp, int gat) {
-    return src_kp ? (gat ? lsd_pass<P, SRC_KP, 1> : lsd_pass<P, SRC_KP, 0>)
-                  : (gat ? lsd_pass<P, SRC_PAIR, 1> : lsd_pass<P, SRC_PAIR, 0>);
+    return src_kp ? (gat ? lsd_pass<P, SRC_KP, 1, 0> : lsd_pass<P, SRC_KP, 0, 0>)
+                  : (gat ? lsd_pass<P, SRC_PAIR, 1, 0> : lsd_pass<P, SRC_PAIR, 0, 0>);
 }
+// pk: 1 = this pass (P = 2, pairs in) writes packed words, 2 = this pass (P = 3, gather) reads them
 void run_pass(int P, bool src_kp, bool gat, const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kout,
-              u32* pout, const u32* kg, u32* hist, bool counted, hipStream_t s, KTimer* kt) {
+              u32* pout, const u32* kg, u32* hist, bool counted, hipStream_t s, KTimer* kt, int pk,
+              const ScanParts& sp) {
+    if (pk == 1) return lsd_pass<2, SRC_PAIR, 0, 1>(g, nt, kin, pin, kout, pout, kg, hist, counted, s, kt, sp);
+    if (pk == 2) return lsd_pass<3, SRC_PK, 1, 0>(g, nt, kin, pin, kout, pout, kg, hist, counted, s, kt, sp);
     const int a = src_kp ? 1 : 0, c = gat ? 1 : 0;
     const PassFn f = P == 0 ? pass_of<0>(a, c) : P == 1 ? pass_of<1>(a, c) : P == 2 ? pass_of<2>(a, c) : pass_of<3>(a, c);
-    f(g, nt, kin, pin, kout, pout, kg, hist, counted, s, kt);
+    f(g, nt, kin, pin, kout, pout, kg, hist, counted, s, kt, sp);
 }
 
 }  // namespace
@@ -1092,20 +1163,43 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
             }
         }
     } else {
+        // per-(block, part) totals for the one-part-long scans (KOLM_LSD_SCAN2=0: per-block scans)
+        const char* s2e = getenv("KOLM_LSD_SCAN2");
+        const bool parts = !(s2e && atoi(s2e) == 0) && t.swc && g.tpb > 1;
+        ScanParts sp[2];
+        if (parts) {
+            u32 plt = 0;
+            while (((g.tpb + (1u << plt) - 1) >> plt) > 16) ++plt;
+            const u32 np = (g.tpb + (1u << plt) - 1) >> plt;
+            const u64 cw = (u64)geo.nb * np * 256;  // np <= 16: t.swc holds 2 * nb * 16 * 256 words
+            sp[0] = ScanParts{t.swc, t.swc + cw, np, plt};
+            sp[1] = ScanParts{t.swc + cw, t.swc, np, plt};
+            KOLM_HIP_CHECK(hipMemsetAsync(t.swc, 0, sizeof(u32) * 2 * cw, s));
+        }
+        u32 pidx = 0;
+        auto spp = [&]() -> const ScanParts& { return sp[parts ? (pidx & 1) : 0]; };
         {
             // text + FEd 2 (+ factor starts near factor ends), KA 4 (+ KB 4)
             KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6));
-            k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist, 0);
+            k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist, 0, 0, 0, spp());
         }
+        // the first half's passes 2 -> 3 exchange one packed word per element (digit 3 and the
+        // position inside the block) when a block position fits 24 bits (KOLM_LSD_PACK=0: off)
+        const char* pke = getenv("KOLM_LSD_PACK");
+        const bool pack = !(pke && atoi(pke) == 0) && pa == 4 && pb > 0 && geo.bs <= (1u << 24);
         for (u32 q = 0; q < pa; ++q) {
             const bool first = q == 0, gat = q + 1 == pa && pb > 0;
+            const int pk = pack ? (q == 2 ? 1 : q == 3 ? 2 : 0) : 0;
             run_pass((int)q, first, gat, g, nt, first ? t.RK : K[o ^ 1], first ? nullptr : S[o ^ 1], K[o], S[o],
-                     gat ? t.KP : nullptr, t.hist, first, s, kt);
+                     gat ? t.KP : nullptr, t.hist, first, s, kt, pk, spp());
             o ^= 1;
+            ++pidx;
         }
         for (u32 q = 0; q < pb; ++q) {
-            run_pass((int)q, false, false, g, nt, K[o ^ 1], S[o ^ 1], K[o], S[o], nullptr, t.hist, false, s, kt);
+            run_pass((int)q, false, false, g, nt, K[o ^ 1], S[o ^ 1], K[o], S[o], nullptr, t.hist, false, s, kt, 0,
+                     spp());
             o ^= 1;
+            ++pidx;
         }
     }
     // RK through position windows (k_r0_rk) when every block has at most 256 of them;

@@ -462,7 +462,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             R0Bufs r{text, FEd, fac, code, C, w, c->get<u32>("KP", N), a.K2, a.SA, a.K22, a.SA2, a.RK,
                      c->get<u32>("r0hist", nt * 256), c->get<u32>("r0tmax", nt), c->get<u32>("r0tmin", nt),
                      c->get<u32>("r0cmax", nt), c->get<u32>("r0cmin", nt), c->get<u32>("r0hf", nt * WG),
-                     c->get<u32>("r0swc", (u64)2 * geo.nb * 8 * 256)};
+                     c->get<u32>("r0swc", (u64)2 * geo.nb * 16 * 256)};
             out.r0_chars = C;
             if (dbg) fprintf(stderr, "[kolm] round 0: %u characters of %u bits\n", C, w);
             if (r0_msd_mode()) {
