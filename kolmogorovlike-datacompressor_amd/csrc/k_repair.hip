@@ -170,14 +170,7 @@ struct DevExec {
     }
 };
 
-// KOLM_RP_WAVES (compile-time A/B): at least that many waves per SIMD, i.e. a VGPR cap of
-// 512 / waves, so that kernels of the other streams fit beside Re-Pair's workgroups
-#ifdef KOLM_RP_WAVES
-#define KOLM_RP_ATTR __attribute__((amdgpu_waves_per_eu(KOLM_RP_WAVES)))
-#else
-#define KOLM_RP_ATTR
-#endif
-__global__ __launch_bounds__(rp::NT) KOLM_RP_ATTR void k_repair(RpArgs a, u32 b0) {
+__global__ __launch_bounds__(rp::NT) void k_repair(RpArgs a, u32 b0) {
     __shared__ rp::Shared sh;
     const u32 b = b0 + blockIdx.x;
     const u32 base = a.geo.base(b);
