@@ -10,6 +10,7 @@
 //
 // BBWT gather (PY:417: out.append(w[(i - 1) % m])): out[r] = text[prev(SA[r])] where
 // prev steps back cyclically inside the factor.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -154,7 +155,7 @@ __global__ __launch_bounds__(WG) void k_fed(TileGeom tg, const u8* flag, const u
 constexpr u32 DUVAL_CH = 128;                 // bytes per thread
 constexpr u32 DUVAL_SPAN = DUVAL_CH * 256;    // bytes per workgroup (32 KiB)
 constexpr u32 DUVAL_PAD = 4;                  // LDS pad per chunk (bank spread)
-constexpr u32 DUVAL_WAVE_W = 4096;            // tree levels merged by whole waves (<= 4 merges)
+constexpr u32 DUVAL_WAVE_W = 4096;            // tree levels merged by whole waves (<= 4 merges; see duval_wave_w)
 constexpr u32 DUVAL_PF = 64;                  // factors per span with a cached 32-byte prefix
 
 __device__ inline u32 lds_addr(u32 q) { return q + (q / DUVAL_CH) * DUVAL_PAD; }
@@ -183,6 +184,36 @@ __device__ inline bool span_less(const u8* t, u32 x0, u32 x1, u32 y1) {
     for (; i < m; ++i) {
         const u8 a = t[lds_addr(x0 + i)], b = t[lds_addr(x1 + i)];
         if (a != b) return a < b;
+    }
+    return la < lb;
+}
+
+// The same comparison by the G lanes of this lane's aligned group (G = 2 .. 64, a power of
+// two; the group's lanes are converged and agree on every argument): 4 G bytes per step, the
+// first differing word found by a ballot over the group.  Reads up to 7 bytes past y1 inside
+// the staged array (padded); bytes at or past m are masked.
+__device__ inline bool span_less_grp(const u8* t, u32 x0, u32 x1, u32 y1, u32 G) {
+    const u32 la = x1 - x0, lb = y1 - x1, m = min(la, lb);
+    const u32 lane = threadIdx.x & 63, gl = lane & (G - 1);
+    const u64 gm = (G >= 64 ? ~0ull : ((1ull << G) - 1ull)) << (lane & ~(G - 1) & 63u);
+    for (u32 o = 0; o < m; o += 4 * G) {
+        const u32 i = o + 4 * gl;
+        u32 a = 0, b = 0, x = 0;
+        if (i < m) {
+            a = lds_word(t, x0 + i);
+            b = lds_word(t, x1 + i);
+            x = a ^ b;
+            if (m - i < 4) x &= (1u << (8 * (m - i))) - 1u;
+        }
+        const u64 bal = __ballot(x != 0) & gm;
+        if (bal) {
+            u32 r = 0;
+            if (x) {
+                const u32 sh = (u32)(__ffs(x) - 1) & ~7u;  // the first differing byte
+                r = ((a >> sh) & 255u) < ((b >> sh) & 255u) ? 1u : 0u;
+            }
+            return __shfl((int)r, (int)(__ffsll((unsigned long long)bal) - 1)) != 0;
+        }
     }
     return la < lb;
 }
@@ -253,10 +284,10 @@ __device__ inline void dprof(u64* prof, u32 k, u64& last) {
 // or 256 (32 KiB)
 template <u32 NT>
 __global__ __launch_bounds__(NT) void k_duval_span(Geom geo, u32 spb, const u8* s, u32* fstart, uint4* fpre,
-                                                   u32* nfac, u64* prof) {
+                                                   u32* nfac, u64* prof, u32 wave_w, u32 grp) {
     constexpr u32 SPAN = DUVAL_CH * NT;
     u64 tlast = prof ? wall_clock64() : 0;
-    __shared__ __align__(16) u8 t[SPAN + NT * DUVAL_PAD + 4];  // + 4: lds_word's read past the end
+    __shared__ __align__(16) u8 t[SPAN + NT * DUVAL_PAD + 16];  // + 16: lds_word's reads past the end
     __shared__ u32 bm[SPAN / 32];
     __shared__ u32 sm[(SPAN + 1023) / 1024];
     __shared__ u32 sh[NT / 64];
@@ -340,10 +371,41 @@ __global__ __launch_bounds__(NT) void k_duval_span(Geom geo, u32 spb, const u8* 
     }
     __syncthreads();
     // tree merge of adjacent factorizations: a thread per merge on the low levels, a wave
-    // per merge (64-lane factor comparisons) from DUVAL_WAVE_W up, where few merges remain
+    // per merge (64-lane factor comparisons) from wave_w up, where few merges remain
     // and adjacent factors of text share long prefixes
     for (u32 w = DUVAL_CH; w < SPAN; w <<= 1) {
-        if (w >= DUVAL_WAVE_W) {
+        if (grp) {
+            // a group of G = w / 64 lanes per merge (NT / G groups = the level's SPAN / 2w merges;
+            // G capped at one wave): the merges of a level run in parallel as in the thread form
+            // and every factor comparison reads 4 G bytes per step
+            const u32 G = min(64u, w / 64);
+            const u32 a0 = (tid / G) * 2 * w, m = a0 + w;
+            if (m < n) {
+                const u32 hi = min(m + w, n);
+                u32 r = m;
+                while (r < hi) {
+                    const u32 re = bm_next(bm, sm, r + 1, hi);
+                    u32 ts = r;
+                    bool merged = false;
+                    while (ts > a0) {
+                        const u32 ps = bm_prev(bm, sm, ts - 1);
+                        if (!span_less_grp(t, ps, ts, re, G)) break;
+                        // the group's lanes write the same value: each then reads its own write
+                        const u32 nw = bm[ts >> 5] & ~(1u << (ts & 31));
+                        bm[ts >> 5] = nw;
+                        if (!nw) atomicAnd(&sm[ts >> 10], ~(1u << ((ts >> 5) & 31)));
+                        ts = ps;
+                        merged = true;
+                    }
+                    if (!merged) break;
+                    r = re;
+                }
+            }
+            __syncthreads();
+            dprof(prof, 2 + (31 - __clz(w)) - 7, tlast);
+            continue;
+        }
+        if (w >= wave_w) {
             const u32 lane = tid & 63, wv = tid >> 6;
             for (u32 a0 = wv * 2 * w; a0 + w < n; a0 += 2 * w * (NT / 64)) {
                 const u32 m = a0 + w, hi = min(m + w, n);
@@ -955,6 +1017,24 @@ u32 duval_span_bytes(const Geom& geo) {
     return force == DUVAL_SPAN ? DUVAL_SPAN : DUVAL_CH * 64;
 }
 
+// First tree level of k_duval_span merged by whole waves (64-byte comparison steps, the level's
+// merges one after another) instead of a thread per merge (4-byte steps, merges in parallel).
+// Full batches keep the thread form up to 4 KiB (text: short factors, many independent merges
+// hide each other's latency); batches of few blocks are latency-bound per workgroup and long
+// factors (images, periodic data) make the 4-byte comparison chains the span's critical path.
+// KOLM_DUVAL_WAVE overrides (read per call).
+static u32 duval_wave_w(const Geom& geo) {
+    if (const char* e = getenv("KOLM_DUVAL_WAVE")) return std::max<u32>(DUVAL_CH, (u32)atoi(e));
+    (void)geo;
+    return DUVAL_WAVE_W;
+}
+// Lane groups per merge at every tree level (span_less_grp); KOLM_DUVAL_GRP=0: a thread per
+// merge below wave_w, a wave per merge from it (read per call)
+static u32 duval_grp() {
+    const char* e = getenv("KOLM_DUVAL_GRP");
+    return e && atoi(e) == 0 ? 0u : 1u;
+}
+
 void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fstart, uint4* fpre, u32* nfac,
                    u32* stack, u32* fcount, u32* tile_tmp, hipStream_t s, KTimer* kt) {
     if (!geo.N) return;
@@ -970,9 +1050,9 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fsta
     {
         KScope k(kt, KT_LYNDON, "k_duval_span", N);  // text once (+ 4 B per factor start)
         if (span == DUVAL_SPAN)
-            k_duval_span<256><<<nch, 256, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, dprof_buf());
+            k_duval_span<256><<<nch, 256, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, dprof_buf(), DUVAL_WAVE_W, duval_grp());
         else
-            k_duval_span<64><<<nch, 64, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, dprof_buf());
+            k_duval_span<64><<<nch, 64, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, dprof_buf(), duval_wave_w(geo), duval_grp());
     }
     {
         KScope k(kt, KT_LYNDON, "k_duval_merge", (u64)nch * 8);
