@@ -1123,6 +1123,21 @@ void launch_zero_spans(const ZeroSpans& z, hipStream_t s) {
     for (int k = 0; k < 6; ++k) tot += z.p[k] ? z.n[k] : 0;
     if (tot) k_zero_spans<<<cdiv(tot, 256), 256, 0, s>>>(z);
 }
+__global__ void k_pack_spans(PackSpans ps, u32* dst) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int k = 0; k < 6; ++k) {
+        if (i < ps.n[k]) {
+            dst[ps.o[k] + i] = ps.p[k][i];
+            return;
+        }
+        i -= ps.n[k];
+    }
+}
+void launch_pack_spans(const PackSpans& ps, u32* dst, hipStream_t s) {
+    u64 tot = 0;
+    for (int k = 0; k < 6; ++k) tot += ps.n[k];
+    if (tot) k_pack_spans<<<cdiv(tot, 256), 256, 0, s>>>(ps, dst);
+}
 void launch_classify_bins(const Seg* cur, u32 ncur, const u32* ncur_dev, const SortArgs& a, const Lists& L,
                           const Level& lv0, const Bins& bn, hipStream_t s, bool bins_zeroed) {
     if (!ncur) return;

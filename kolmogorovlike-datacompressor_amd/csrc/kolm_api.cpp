@@ -165,6 +165,21 @@ struct kolm_ctx {
     std::mutex mu;
     std::map<std::string, DevBuf> bufs;
     u32* h_cnt = nullptr;  // pinned mirror of the counters
+    // pinned landing buffer of a batch's packed small results (one device-to-host copy per
+    // host round trip instead of one per array: each copy is a blit launch of ~15-25 us)
+    u32* h_tail = nullptr;
+    size_t h_tail_cap = 0;
+    u32* tail_host(size_t words) {
+        if (words > h_tail_cap) {
+            if (h_tail) KOLM_HIP_CHECK(hipHostFree(h_tail));
+            h_tail = nullptr;
+            h_tail_cap = 0;
+            const size_t cap = std::max<size_t>(words + (words >> 2), 4096);
+            KOLM_HIP_CHECK(hipHostMalloc((void**)&h_tail, cap * sizeof(u32), hipHostMallocDefault));
+            h_tail_cap = cap;
+        }
+        return h_tail;
+    }
     hipEvent_t ev[8] = {};
     // per-launch timing of kernel families (kolm_ctx_set_timing)
     bool timing = false;
@@ -950,8 +965,16 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         TScope t(c, KOLM_KT_SIZES, "k_cheap_sizes", N);
         launch_cheap_sizes(ce, ms);
     }
-    if (!serial) {
-        // the BBWT gather's predecessor bytes on the index stream, off the sort chain
+    // The BBWT gather's predecessor bytes on the index stream, off the sort chain — but
+    // prevc waits for the Lyndon factors, and the LZ77 parse queued behind it on that stream
+    // waits too.  Batches of under 16 blocks, where LZ77 (the stitch's one-wave-per-block
+    // walk) is as long as the sort chain, run prevc inline on the sort stream (~15 us per
+    // MiB) so the parse starts at once: BASELINE config 2 2.15 -> 1.90 ms, config 5 6.55 ->
+    // 6.21 ms; config 4's 32-block shard measured 6.84 -> 7.30 ms that way (the parse then
+    // competes with Lyndon and round 0 for CUs), so it keeps the index-stream form.
+    // KOLM_PREVC_IDX = 0 / 1 forces it.
+    static const int prevc_idx = getenv("KOLM_PREVC_IDX") ? atoi(getenv("KOLM_PREVC_IDX")) : -1;
+    if (!serial && (prevc_idx >= 0 ? prevc_idx != 0 : nb >= 16)) {
         KOLM_HIP_CHECK(hipStreamWaitEvent(ms, ev[5], 0));
         P.prevc();
         KOLM_HIP_CHECK(hipEventRecord(ev[6], ms));
@@ -1034,12 +1057,25 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     }
     std::vector<u64> off(nb + 1);
     std::vector<u32> rpres(want_rp ? (u64)nb * RP_RS_N : 0), win(nb);
-    KOLM_HIP_CHECK(hipMemcpyAsync(off.data(), e.off, sizeof(u64) * (nb + 1), hipMemcpyDeviceToHost, s));
-    KOLM_HIP_CHECK(hipMemcpyAsync(win.data(), e.method, sizeof(u32) * nb, hipMemcpyDeviceToHost, s));
-    KOLM_HIP_CHECK(hipMemcpyAsync(c->h_cnt, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
-    if (want_rp)
-        KOLM_HIP_CHECK(hipMemcpyAsync(rpres.data(), rpa.result, sizeof(u32) * rpres.size(), hipMemcpyDeviceToHost, s));
-    c->sync();
+    {
+        // offsets, winners, counters (and Re-Pair results) in one packed copy
+        PackSpans ps{};
+        const u32 w_off = 2 * (nb + 1), w_win = nb, w_rp = (u32)rpres.size();
+        ps.p[0] = reinterpret_cast<const u32*>(e.off), ps.n[0] = w_off, ps.o[0] = 0;
+        ps.p[1] = e.method, ps.n[1] = w_win, ps.o[1] = w_off;
+        ps.p[2] = cnt, ps.n[2] = C_N, ps.o[2] = w_off + w_win;
+        ps.p[3] = rpa.result, ps.n[3] = w_rp, ps.o[3] = w_off + w_win + C_N;
+        const u32 words = w_off + w_win + C_N + w_rp;
+        u32* dtail = c->get<u32>("tail", words);
+        u32* htail = c->tail_host(words);
+        launch_pack_spans(ps, dtail, s);
+        KOLM_HIP_CHECK(hipMemcpyAsync(htail, dtail, sizeof(u32) * words, hipMemcpyDeviceToHost, s));
+        c->sync();
+        std::memcpy(off.data(), htail, sizeof(u64) * (nb + 1));
+        std::memcpy(win.data(), htail + w_off, sizeof(u32) * nb);
+        std::memcpy(c->h_cnt, htail + w_off + w_win, sizeof(u32) * C_N);
+        if (w_rp) std::memcpy(rpres.data(), htail + w_off + w_win + C_N, sizeof(u32) * w_rp);
+    }
     if (want_rp && rpa.prof) {
         // per-section wall-clock of the Re-Pair kernel (100 MHz ticks), summed over blocks
         std::vector<u64> pr((u64)nb * RP_P_N);
@@ -1098,13 +1134,25 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         if (want_v2 && (used & (1u << KOLM_M_V2NEW))) launch_v2_emit(geo, v2.pb, v2.meta, e.method, e.off, v2.U, v2.L, d_arena, s);
     }
     KOLM_HIP_CHECK(hipEventRecord(ev[4], s));
-    if (h_sizes)
-        KOLM_HIP_CHECK(hipMemcpyAsync(h_sizes, e.sizes, sizeof(u32) * nb * KOLM_NCAND, hipMemcpyDeviceToHost, s));
-    if (h_method) KOLM_HIP_CHECK(hipMemcpyAsync(h_method, e.method, sizeof(u32) * nb, hipMemcpyDeviceToHost, s));
-    KOLM_HIP_CHECK(hipMemcpyAsync(c->h_cnt, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
     std::vector<u32> ntok(want_lz ? nb : 0);
-    if (want_lz) KOLM_HIP_CHECK(hipMemcpyAsync(ntok.data(), z.ntok, sizeof(u32) * nb, hipMemcpyDeviceToHost, s));
-    c->sync();
+    {
+        // sizes, counters and LZ77 token counts in one packed copy (the winners are on the host)
+        PackSpans ps{};
+        const u32 w_sz = h_sizes ? nb * KOLM_NCAND : 0, w_nt = (u32)ntok.size();
+        ps.p[0] = e.sizes, ps.n[0] = w_sz, ps.o[0] = 0;
+        ps.p[1] = cnt, ps.n[1] = C_N, ps.o[1] = w_sz;
+        ps.p[2] = z.ntok, ps.n[2] = w_nt, ps.o[2] = w_sz + C_N;
+        const u32 words = w_sz + C_N + w_nt;
+        u32* dtail = c->get<u32>("tail", words);
+        u32* htail = c->tail_host(words);
+        launch_pack_spans(ps, dtail, s);
+        KOLM_HIP_CHECK(hipMemcpyAsync(htail, dtail, sizeof(u32) * words, hipMemcpyDeviceToHost, s));
+        c->sync();
+        if (h_sizes) std::memcpy(h_sizes, htail, sizeof(u32) * w_sz);
+        if (h_method) std::memcpy(h_method, win.data(), sizeof(u32) * nb);
+        std::memcpy(c->h_cnt, htail + w_sz, sizeof(u32) * C_N);
+        if (w_nt) std::memcpy(ntok.data(), htail + w_sz + C_N, sizeof(u32) * w_nt);
+    }
     if (want_v2) {
         KOLM_HIP_CHECK(hipDeviceSynchronize());
         for (auto& kv : c->bufs) {
@@ -1326,6 +1374,7 @@ int kolm_ctx_destroy(kolm_ctx* c) {
         for (auto& e : c->evr) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evpool) KOLM_HIP_CHECK(hipEventDestroy(e));
         KOLM_HIP_CHECK(hipHostFree(c->h_cnt));
+        if (c->h_tail) KOLM_HIP_CHECK(hipHostFree(c->h_tail));
         for (int i = 0; i < kolm_ctx::NSTAGE; ++i) {
             if (c->stage[i]) KOLM_HIP_CHECK(hipHostFree(c->stage[i]));
             if (c->stage_ev[i]) KOLM_HIP_CHECK(hipEventDestroy(c->stage_ev[i]));

@@ -281,6 +281,14 @@ struct ZeroSpans {
     u32 n[6];
 };
 void launch_zero_spans(const ZeroSpans& z, hipStream_t s);
+// Up to 6 u32 ranges (p[k], n[k] words) copied to dst + o[k] by one launch: the small results
+// of a batch (offsets, winners, counters) gathered for a single device-to-host copy
+struct PackSpans {
+    const u32* p[6];
+    u32 n[6];
+    u32 o[6];
+};
+void launch_pack_spans(const PackSpans& ps, u32* dst, hipStream_t s);
 // ncur: the list length, or (ncur_dev set) a bound for the grid with the length in ncur_dev
 void launch_classify_bins(const Seg* cur, u32 ncur, const u32* ncur_dev, const SortArgs& a, const Lists& L,
                           const Level& lv0, const Bins& bn, hipStream_t s, bool bins_zeroed = false);
