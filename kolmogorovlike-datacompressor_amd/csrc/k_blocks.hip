@@ -277,6 +277,7 @@ __device__ inline void dprof(u64* prof, u32 k, u64& last) {
     if (prof && threadIdx.x == 0) {
         const u64 now = wall_clock64();
         atomicAdd((unsigned long long*)&prof[k], (unsigned long long)(now - last));
+        atomicMax((unsigned long long*)&prof[24 + k], (unsigned long long)(now - last));  // slowest workgroup
         last = now;
     }
 }
@@ -998,8 +999,8 @@ u64* dprof_buf() {
     static u64* prof = nullptr;
     static const bool dp = getenv("KOLM_DUVAL_PROF") && atoi(getenv("KOLM_DUVAL_PROF"));
     if (dp && !prof) {
-        KOLM_HIP_CHECK(hipMalloc(&prof, 24 * sizeof(u64)));
-        KOLM_HIP_CHECK(hipMemset(prof, 0, 24 * sizeof(u64)));
+        KOLM_HIP_CHECK(hipMalloc(&prof, 40 * sizeof(u64)));
+        KOLM_HIP_CHECK(hipMemset(prof, 0, 40 * sizeof(u64)));
     }
     return prof;
 }
@@ -1060,12 +1061,12 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fsta
                                              dprof_buf());
     }
     if (u64* prof = dprof_buf()) {
-        u64 h[24];
+        u64 h[40];
         KOLM_HIP_CHECK(hipStreamSynchronize(s));
         KOLM_HIP_CHECK(hipMemcpy(h, prof, sizeof h, hipMemcpyDeviceToHost));
-        KOLM_HIP_CHECK(hipMemset(prof, 0, 24 * sizeof(u64)));
-        fprintf(stderr, "[kolm] duval_span us per workgroup:");
-        for (int k = 0; k < 11; ++k) fprintf(stderr, " %d:%.1f", k, (double)h[k] / nch / 100.0);
+        KOLM_HIP_CHECK(hipMemset(prof, 0, 40 * sizeof(u64)));
+        fprintf(stderr, "[kolm] duval_span us per workgroup (mean/max):");
+        for (int k = 0; k < 11; ++k) fprintf(stderr, " %d:%.1f/%.1f", k, (double)h[k] / nch / 100.0, (double)h[24 + k] / 100.0);
         fprintf(stderr, " | merge us per block mean %.1f max %.1f, compares/block %.1f, 512-B steps/block %.1f, "
                 "span factors/block %.1f\n", (double)h[11] / geo.nb / 100.0, (double)h[12] / 100.0,
                 (double)h[13] / geo.nb, (double)h[14] / geo.nb, (double)h[15] / geo.nb);

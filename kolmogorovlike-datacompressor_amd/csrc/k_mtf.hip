@@ -241,6 +241,140 @@ __global__ __launch_bounds__(64 * CW) void k_mtf_compose(ChunkGeom cg, const u8*
     }
 }
 
+// The same composition in three launches and three levels, so the
+// dependent mtf_apply chain of a block is ~55 steps instead of 2 * 64 + 16 (one gradient BMP
+// block: 1024 chunks of 1 KiB).  A block's chunks form CP_R ranges of CP_S-range groups:
+//   k_mtf_cp1: a wave per range composes its chunk summaries from the identity;
+//   k_mtf_cp2: a workgroup per block, a wave per group: composes its ranges' summaries into
+//              the group's, wave 0 chains the group summaries, each wave re-walks its ranges
+//              and writes every range's entry state;
+//   k_mtf_cp3: a wave per range re-walks its chunks from its entry state, writing the state at
+//              every chunk start.
+constexpr u32 CP_W = 16;          // waves per workgroup of cp1 / cp3
+constexpr u32 CP_G = 8;           // groups per block (waves of cp2)
+constexpr u32 CP_S = 16;          // ranges per group
+constexpr u32 CP_R = CP_G * CP_S;  // ranges per block
+
+__device__ inline u32 mtf_ident(u32 lane) {
+    return (4 * lane) | ((4 * lane + 1) << 8) | ((4 * lane + 2) << 16) | ((4 * lane + 3) << 24);
+}
+
+// a range's chunks [k0, k1) of block b
+__device__ inline void cp_range(const ChunkGeom& cg, u32 b, u32 r, u32& k0, u32& k1) {
+    const u32 nch = (cg.geo.end(b) - cg.geo.base(b) + cg.csz - 1) / cg.csz;
+    const u32 per = (nch + CP_R - 1) / CP_R;
+    k0 = min(r * per, nch);
+    k1 = min(k0 + per, nch);
+}
+
+__global__ __launch_bounds__(64 * CP_W) void k_mtf_cp1(ChunkGeom cg, const u8* summary, const u16* scnt, u32* rst,
+                                                      u32* rdist) {
+    __shared__ u32 st[CP_W][64];
+    __shared__ u8 nst[CP_W][256];
+    __shared__ u32 member[CP_W][8];
+    __shared__ u32 uni[CP_W][8];
+    const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const u32 gr = blockIdx.x * CP_W + w, b = gr / CP_R, r = gr - b * CP_R;
+    if (b >= cg.geo.nb) return;  // whole waves (wave-level sync only)
+    u32 k0, k1;
+    cp_range(cg, b, r, k0, k1);
+    st[w][lane] = mtf_ident(lane);
+    if (lane < 8) uni[w][lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (u32 k = k0; k < k1; ++k) {
+        const u32 c = b * cg.cpb + k;
+        const u8* sm = summary + (u64)c * 256;
+        const u32 cnt = scnt[c];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const u32 i = 4 * lane + j;
+            if (i < cnt) atomicOr(&uni[w][sm[i] >> 5], 1u << (sm[i] & 31));
+        }
+        mtf_apply(st[w], nst[w], member[w], sm, cnt);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    rst[(u64)gr * 64 + lane] = st[w][lane];
+    if (lane == 0) {
+        u32 d = 0;
+        for (int q = 0; q < 8; ++q) d += __popc(uni[w][q]);
+        rdist[gr] = d;
+    }
+}
+
+__global__ __launch_bounds__(64 * CP_G) void k_mtf_cp2(const u32* rst, const u32* rdist, u32* rentry) {
+    __shared__ u32 st[CP_G][64];
+    __shared__ u8 nst[CP_G][256];
+    __shared__ u32 member[CP_G][8];
+    __shared__ u32 uni[CP_G][8];
+    __shared__ u8 gsum[CP_G][256];
+    __shared__ u32 gentry[CP_G][64];
+    __shared__ u32 gdist[CP_G];
+    const u32 lane = threadIdx.x & 63, g = threadIdx.x >> 6, b = blockIdx.x;
+    const u64 r0 = (u64)b * CP_R + g * CP_S;
+    // (a) the group's summary: its ranges' summaries composed from the identity
+    st[g][lane] = mtf_ident(lane);
+    if (lane < 8) uni[g][lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (u32 v = 0; v < CP_S; ++v) {
+        const u8* sm = reinterpret_cast<const u8*>(rst + (r0 + v) * 64);
+        const u32 cnt = rdist[r0 + v];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const u32 i = 4 * lane + j;
+            if (i < cnt) atomicOr(&uni[g][sm[i] >> 5], 1u << (sm[i] & 31));
+        }
+        mtf_apply(st[g], nst[g], member[g], sm, cnt);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    reinterpret_cast<u32*>(gsum[g])[lane] = st[g][lane];
+    if (lane == 0) {
+        u32 d = 0;
+        for (int q = 0; q < 8; ++q) d += __popc(uni[g][q]);
+        gdist[g] = d;
+    }
+    __syncthreads();
+    // (b) wave 0 chains the group summaries: gentry[g] = state entering group g
+    if (g == 0) {
+        st[0][lane] = mtf_ident(lane);
+        __builtin_amdgcn_wave_barrier();
+        for (u32 v = 0; v < CP_G; ++v) {
+            gentry[v][lane] = st[0][lane];
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (v + 1 < CP_G) mtf_apply(st[0], nst[0], member[0], gsum[v], gdist[v]);
+        }
+    }
+    __syncthreads();
+    // (c) each group re-walks its ranges from its entry state
+    st[g][lane] = gentry[g][lane];
+    __builtin_amdgcn_wave_barrier();
+    for (u32 v = 0; v < CP_S; ++v) {
+        rentry[(r0 + v) * 64 + lane] = st[g][lane];
+        mtf_apply(st[g], nst[g], member[g], reinterpret_cast<const u8*>(rst + (r0 + v) * 64), rdist[r0 + v]);
+    }
+}
+
+__global__ __launch_bounds__(64 * CP_W) void k_mtf_cp3(ChunkGeom cg, const u8* summary, const u16* scnt,
+                                                      const u32* rentry, u8* states) {
+    __shared__ u32 st[CP_W][64];
+    __shared__ u8 nst[CP_W][256];
+    __shared__ u32 member[CP_W][8];
+    const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const u32 gr = blockIdx.x * CP_W + w, b = gr / CP_R, r = gr - b * CP_R;
+    if (b >= cg.geo.nb) return;
+    u32 k0, k1;
+    cp_range(cg, b, r, k0, k1);
+    st[w][lane] = rentry[(u64)gr * 64 + lane];
+    __builtin_amdgcn_wave_barrier();
+    for (u32 k = k0; k < k1; ++k) {
+        const u32 c = b * cg.cpb + k;
+        reinterpret_cast<u32*>(states + (u64)c * 256)[lane] = st[w][lane];
+        mtf_apply(st[w], nst[w], member[w], summary + (u64)c * 256, scnt[c]);
+    }
+}
+
 constexpr int RT = 128;  // threads per workgroup in the replay kernel
 
 // Rice-k bit lengths of the 5 BBWT candidates (PY:2028-2073: flags 0, bit-plane, nibble,
@@ -529,8 +663,18 @@ u32 mtf_chunk_bytes(const Geom& geo) {
     return csz;
 }
 
+// The three-launch compose (k_mtf_cp1..3) for every batch (one A/B call: config 2 1.90 -> 1.75
+// ms, config 5 6.23 -> 6.09 ms, 256 MiB text MTF family 1.91 -> 1.76 ms); KOLM_MTF_CP = 0: the
+// one-workgroup-per-block k_mtf_compose (read per call)
+bool mtf_cp_mode(const Geom& geo) {
+    const char* e = getenv("KOLM_MTF_CP");
+    (void)geo;
+    return e ? atoi(e) != 0 : true;
+}
+u64 mtf_cp_words(const Geom& geo) { return (u64)geo.nb * CP_R * 129; }
+
 void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summary_cnt, u8* states,
-                hipStream_t s, KTimer* kt, u64* bits, int rice_k) {
+                hipStream_t s, KTimer* kt, u64* bits, int rice_k, u32* cp_scratch) {
     if (!geo.N) return;
     const u32 csz = mtf_chunk_bytes(geo);
     ChunkGeom cg{geo, (geo.bs + csz - 1) / csz, csz};
@@ -542,10 +686,19 @@ void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summar
     }
     {
         KScope k(kt, KT_MTF, "k_mtf_compose", (u64)nchunks * 512);
-        if (csz < MTF_CHUNK || geo.nb < 64)
+        if (cp_scratch && mtf_cp_mode(geo)) {
+            u32* rst = cp_scratch;                           // [nb * CP_R][64]
+            u32* rentry = cp_scratch + (u64)geo.nb * CP_R * 64;  // [nb * CP_R][64]
+            u32* rdist = rentry + (u64)geo.nb * CP_R * 64;        // [nb * CP_R]
+            const u32 g13 = (geo.nb * CP_R + CP_W - 1) / CP_W;
+            k_mtf_cp1<<<g13, 64 * CP_W, 0, s>>>(cg, summary, summary_cnt, rst, rdist);
+            k_mtf_cp2<<<geo.nb, 64 * CP_G, 0, s>>>(rst, rdist, rentry);
+            k_mtf_cp3<<<g13, 64 * CP_W, 0, s>>>(cg, summary, summary_cnt, rentry, states);
+        } else if (csz < MTF_CHUNK || geo.nb < 64) {
             k_mtf_compose<16><<<geo.nb, 64 * 16, 0, s>>>(cg, summary, summary_cnt, states);
-        else
+        } else {
             k_mtf_compose<8><<<geo.nb, 64 * 8, 0, s>>>(cg, summary, summary_cnt, states);
+        }
     }
     if (mtf_wave_mode(geo)) {
         KScope k(kt, KT_MTF, "k_mtf_wave", 2 * N + (u64)nchunks * 256);

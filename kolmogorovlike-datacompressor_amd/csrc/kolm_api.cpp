@@ -699,7 +699,8 @@ struct Pipeline {
         const u64 nch = (u64)((geo.bs + csz - 1) / csz) * geo.nb + 1;
         u8* out = c->get<u8>("mtf", N);
         launch_mtf(geo, in, out, c->get<u8>("mtf_sum", nch * 256), c->get<u16>("mtf_cnt", nch),
-                   c->get<u8>("mtf_states", nch * 256), c->active, c->kt(), bits, 2);
+                   c->get<u8>("mtf_states", nch * 256), c->active, c->kt(), bits, 2,
+                   mtf_cp_mode(geo) ? c->get<u32>("mtf_cp", mtf_cp_words(geo)) : nullptr);
         return out;
     }
 

@@ -376,8 +376,11 @@ u32 launch_round0_msd(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt
 // bit counts of the 5 BBWT candidates (counters 0..4, see k_entropy.hip) — no extra pass
 bool mtf_wave_mode(const Geom& geo);  // position-parallel MTF replay (batches of few blocks)
 u32 mtf_chunk_bytes(const Geom& geo);  // bytes per MTF chunk of this batch (launch_mtf's choice)
+bool mtf_cp_mode(const Geom& geo);     // three-launch compose (batches of few blocks)
+u64 mtf_cp_words(const Geom& geo);    // its scratch (u32 words)
+// cp_scratch ([mtf_cp_words], used when mtf_cp_mode): range states of the three-launch compose
 void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summary_cnt, u8* states,
-                hipStream_t s, KTimer* kt = nullptr, u64* bits = nullptr, int rice_k = 2);
+                hipStream_t s, KTimer* kt = nullptr, u64* bits = nullptr, int rice_k = 2, u32* cp_scratch = nullptr);
 
 // ---- k_entropy.hip: cheap sizes, Rice sizes / emission, MDL, emission of simple models ----
 struct EmitArgs {
