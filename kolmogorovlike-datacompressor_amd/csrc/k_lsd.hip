@@ -867,9 +867,14 @@ __global__ __launch_bounds__(WG) void k_alpha_codes(const u32* pres, u8* code, u
 // hist0 (optional): the first LSD pass's per-tile digit counts (digit 0 of KA), so that
 // pass needs no histogram kernel of its own; top: the counts of KB's top byte instead (the
 // first MSD digit of the MSD round 0, k_r0m.hip, which passes sh = 64 - C w).
+// part (0 or sh): the sh padding bits below the C codes hold the top sh bits of character C's
+// code (sh <= w), so round 0 also splits positions tied on C characters by most of the next one;
+// the doubling rounds still start from h = C (groups equal on C characters and the partial one
+// refine consistently: doubling compares (group(p), group(p + h)), and group(p + h) orders
+// character h fully)
 __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32 C, u32 w, u32 sh, u32* KA, u32* KB,
                                                   u32* hist0, u32 top, u32 segS = 0, u32 seglt = 0,
-                                                  ScanParts sp = ScanParts{}) {
+                                                  ScanParts sp = ScanParts{}, u32 part = 0) {
     __shared__ __align__(16) u8 tx[LSD_T + 64];
     __shared__ u8 cd[256];
     __shared__ u32 h0[WG / 64][256];
@@ -885,7 +890,7 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
     }
     const u32 N = (u32)g.geo.N;
     cd[threadIdx.x] = code[(u64)b * 256 + threadIdx.x];
-    const u32 n = min(hi + C, N) - lo;
+    const u32 n = min(hi + C + (part ? 1u : 0u), N) - lo;
     if ((((uintptr_t)g.text + lo) & 3) == 0) {  // dword copies (a dword that starts before N is allocated)
         const u32* src = reinterpret_cast<const u32*>(g.text + lo);
         u32* dst = reinterpret_cast<u32*>(tx);
@@ -914,17 +919,21 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
     u64 key = 0;
     for (u32 k = 0; k < C; ++k) key = (key << w) | (i0 + k < n ? cd[tx[i0 + k]] : 0u);
     u32 ka[LSD_PT], kb[LSD_PT];
+    const u32 psh = w - part;  // the partial character: its code's top `part` bits
 #pragma unroll
     for (u32 e = 0; e < LSD_PT; ++e) {
-        ka[e] = (u32)(key << sh);
-        kb[e] = (u32)((key << sh) >> 32);
         const u32 x = i0 + e + C;
-        key = ((key << w) | (x < n ? cd[tx[x]] : 0u)) & mask;
+        const u32 nc = x < n ? cd[tx[x]] : 0u;
+        const u64 kk = (key << sh) | (part ? (u64)(nc >> psh) : 0ull);
+        ka[e] = (u32)kk;
+        kb[e] = (u32)(kk >> 32);
+        key = ((key << w) | nc) & mask;
     }
+    const u32 need = C + (part ? 1u : 0u);  // characters read per position
 #pragma unroll
     for (u32 e = 0; e < LSD_PT; ++e) {
         const u32 p = lo + i0 + e;
-        if (p < hi && fed[e] < C) {  // the C characters wrap inside the factor
+        if (p < hi && fed[e] < need) {  // the characters wrap inside the factor
             u32 fs, m;
             g.fac.locate(g.geo, p, fs, m);
             u32 t = p - fs;
@@ -933,8 +942,9 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
                 k2 = (k2 << w) | cd[g.text[fs + t]];
                 if (++t == m) t = 0;
             }
-            ka[e] = (u32)(k2 << sh);
-            kb[e] = (u32)((k2 << sh) >> 32);
+            const u64 kk = (k2 << sh) | (part ? (u64)(cd[g.text[fs + t]] >> psh) : 0ull);
+            ka[e] = (u32)kk;
+            kb[e] = (u32)(kk >> 32);
         }
     }
     const u32 p0 = lo + i0;
@@ -1163,6 +1173,9 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
             }
         }
     } else {
+        // the padding bits carry the next character's top bits (KOLM_R0_PART=0: zero padding)
+        const char* pte = getenv("KOLM_R0_PART");
+        const u32 part = (pte && atoi(pte) == 0) ? 0u : std::min(sh, t.w);
         // per-(block, part) totals for the one-part-long scans (KOLM_LSD_SCAN2=0: per-block scans)
         const char* s2e = getenv("KOLM_LSD_SCAN2");
         const bool parts = !(s2e && atoi(s2e) == 0) && t.swc && g.tpb > 1;
@@ -1181,7 +1194,8 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
         {
             // text + FEd 2 (+ factor starts near factor ends), KA 4 (+ KB 4)
             KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6));
-            k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist, 0, 0, 0, spp());
+            k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist, 0, 0, 0, spp(),
+                                          part);
         }
         // the first half's passes 2 -> 3 exchange one packed word per element (digit 3 and the
         // position inside the block) when a block position fits 24 bits (KOLM_LSD_PACK=0: off)
