@@ -168,12 +168,20 @@ __device__ u32 wave_lcp8(const LText& t, u32 p, u32 q, u32 start, u32 maxl, u32 
 // search of the 4096-byte window (LDS copy) until it lands on a recorded token; an
 // unresolved last token on the path is recomputed exactly.
 // =====================================================================================
-constexpr u32 LZL_NW = LZL_HOME + LZ_WINDOW + LZL_LEAD;  // window positions indexed (8256)
-constexpr u32 LZL_TXT = LZL_NW + LZL_CAPX + 32;         // text window + alignment + compare slack
-constexpr u32 LZL_ISL = LZL_HOME + LZL_LEAD;            // islot entries [hs - LEAD, he)
-constexpr u32 LZL_NCHAIN = LZL_HOME / LZL_CHUNK;        // 16 chains, 4 per wave
-static_assert(LZL_NCHAIN == 16, "4 chains of 16 lanes per wave, 4 waves");
-static_assert(LZL_ISL * 2 + ((LZL_NW + 63) / 64) * 8 <= LZL_NW * 2, "islot + head bitmap fit the sort scratch");
+// Geometry of one k_lz_local variant: HOME positions per workgroup, LPC lanes per chain (the
+// candidates a chain compares per batch); 256 threads either way (4 waves, 64 / LPC chains each).
+template <u32 HOME, u32 LPC>
+struct LzlGeom {
+    static constexpr u32 NW = HOME + LZ_WINDOW + LZL_LEAD;  // window positions indexed
+    static constexpr u32 TXT = NW + LZL_CAPX + 32;          // text window + alignment + compare slack
+    static constexpr u32 ISL = HOME + LZL_LEAD;             // islot entries [hs - LEAD, he)
+    static constexpr u32 NCHAIN = HOME / LZL_CHUNK;
+    static constexpr u32 CPW = 64 / LPC;                    // chains per wave
+    static constexpr u32 BW = ISL + 4 * ((NW + 63) / 64);   // B: islot + head bitmap (u16 words)
+    static constexpr u32 PER = (NW + 255) / 256;            // window elements per lane in the sort
+    static_assert(NCHAIN == 4 * CPW, "4 waves of 64 / LPC chains");
+    static_assert(NW < (1u << 14), "window offsets in 14 bits (the winner key)");
+};
 
 // LDS text without bounds checks (every access is inside the loaded window by construction)
 struct WinText {
@@ -193,7 +201,6 @@ __device__ inline u32 hash3(const u8* t, u32 x) {
     return (k * 0x9E3779B1u) >> (32 - LZL_HB);
 }
 
-constexpr u32 LZL_PER = (LZL_NW + 255) / 256;  // window elements per lane (33)
 
 // Stable counting sort of the nw window positions by hash into A (one pass).  Wave w owns
 // the contiguous position range [w*Q, (w+1)*Q): per-wave bucket counts (LDS atomics),
@@ -203,21 +210,22 @@ constexpr u32 LZL_PER = (LZL_NW + 255) / 256;  // window elements per lane (33)
 // is needed between its steps).
 // hist: [4][LZL_NBK] 16-bit counters / offsets (window positions < 2^16; a count is added
 // to its dword with the half's shift, plain 16-bit stores otherwise)
+template <u32 PER>
 __device__ void lzl_bucket(const u8* t, u16* A, u32 nw, u16* hist, u32* sh) {
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     constexpr u32 R = LZL_NBK / 256;  // buckets per thread in the scan
     const u32 Q = (nw + 3) / 4;
     const u32 b0 = min(w * Q, nw), b1 = min(b0 + Q, nw);
-    u32 hv[LZL_PER];
+    u32 hv[PER];
 #pragma unroll
-    for (u32 k = 0; k < LZL_PER; ++k) {
+    for (u32 k = 0; k < PER; ++k) {
         const u32 e = b0 + k * 64 + lane;
         hv[k] = e < b1 ? hash3(t, e) : 0u;
     }
     for (u32 i = tid; i < 2 * LZL_NBK; i += 256) reinterpret_cast<u32*>(hist)[i] = 0;
     __syncthreads();
 #pragma unroll
-    for (u32 k = 0; k < LZL_PER; ++k)
+    for (u32 k = 0; k < PER; ++k)
         if (b0 + k * 64 + lane < b1)
             atomicAdd(reinterpret_cast<u32*>(hist) + ((w * LZL_NBK + hv[k]) >> 1), 1u << (16 * (hv[k] & 1)));
     __syncthreads();
@@ -246,7 +254,7 @@ __device__ void lzl_bucket(const u8* t, u16* A, u32 nw, u16* hist, u32* sh) {
     __syncthreads();
     const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
 #pragma unroll
-    for (u32 k = 0; k < LZL_PER; ++k) {
+    for (u32 k = 0; k < PER; ++k) {
         if (b0 + k * 64 >= b1) break;  // wave-uniform
         const u32 e = b0 + k * 64 + lane;
         const bool valid = e < b1;
@@ -273,25 +281,35 @@ __device__ inline u32 lzl_gs(const u64* bm, u32 k) {
     return wi * 64 + 63 - (u32)__clzll(m);
 }
 
-__device__ inline u64 grp_mask(u32 lane) { return 0xFFFFull << (lane & 48); }
+// the lanes of this lane's chain (LPC consecutive lanes)
+template <u32 LPC>
+__device__ inline u64 grp_mask(u32 lane) { return ((1ull << LPC) - 1ull) << (lane & (64 - LPC)); }
 
-// max over the 16 lanes of a DPP row, in every lane of the row (quad butterflies + row rotates)
-__device__ inline u32 row_max16(u32 v) {
+// max over the LPC (16 or 8) lanes of this lane's chain, in every lane of it: quad butterflies,
+// then row rotates (16) or the half-row mirror (8)
+template <u32 LPC>
+__device__ inline u32 grp_max(u32 v) {
+    static_assert(LPC == 16 || LPC == 8, "chains of 16 or 8 lanes");
     v = max(v, KOLM_DPP(0u, v, 0xB1, 0xF));   // quad_perm [1,0,3,2]
     v = max(v, KOLM_DPP(0u, v, 0x4E, 0xF));   // quad_perm [2,3,0,1]
-    v = max(v, KOLM_DPP(0u, v, 0x124, 0xF));  // row_ror:4
-    v = max(v, KOLM_DPP(0u, v, 0x128, 0xF));  // row_ror:8
+    if (LPC == 16) {
+        v = max(v, KOLM_DPP(0u, v, 0x124, 0xF));  // row_ror:4
+        v = max(v, KOLM_DPP(0u, v, 0x128, 0xF));  // row_ror:8
+    } else {
+        v = max(v, KOLM_DPP(0u, v, 0x141, 0xF));  // row_half_mirror
+    }
     return v;
 }
 
 // Longest match at p for this lane's 16-lane chain (act: the chain has a position to
 // score).  Exact up to lim = min(block end, chunk end + LZL_CAPX) - p (<= 576): unres when
 // the best candidate reaches lim short of the block end.
+template <u32 LPC>
 __device__ void lzl_best(const u8* txt, u32 tlo, const u16* A, const u64* bm, const u16* isl, u32 lo, u32 ilo,
                          bool act, u32 p, u32 lim, u32 end, u32& out_len, u32& out_dist, bool& unres, u32& nlong,
                          u32& nbatch) {
-    const u32 lane = threadIdx.x & 63, hl = lane & 15;
-    const u64 GM = grp_mask(lane);
+    const u32 lane = threadIdx.x & 63, hl = lane & (LPC - 1);
+    const u64 GM = grp_mask<LPC>(lane);
     const WinText T{txt, tlo};
     u32 best = 0, bd = 0;
     bool go = act && p + (u32)LZ_MIN <= end;
@@ -307,7 +325,7 @@ __device__ void lzl_best(const u8* txt, u32 tlo, const u16* A, const u64* bm, co
     const u64 pv = go ? lds8(txt, pr) : 0ull;  // p's first 8 bytes, once per token
     while (__ballot(go)) {
         ++nbatch;
-        const u32 qn = (go && k0 > 16 + hl) ? (u32)A[k0 - 17 - hl] : 0u;  // next batch
+        const u32 qn = (go && k0 > LPC + hl) ? (u32)A[k0 - LPC - 1 - hl] : 0u;  // next batch
         bool valid = go && k0 > gs + hl;
         const u32 q = lo + qa;
         valid = valid && (p - q <= (u32)LZ_WINDOW);
@@ -349,14 +367,14 @@ __device__ void lzl_best(const u8* txt, u32 tlo, const u16* A, const u64* bm, co
         }
         // max length, ties -> largest position (= smallest distance): one 28-bit key per
         // lane (length <= 576 < 2^14, window offset < 2^14), maximised over the DPP row
-        const u32 key = row_max16(l >= (u32)LZ_MIN ? (l << 14) | (q - lo) : 0u);
+        const u32 key = grp_max<LPC>(l >= (u32)LZ_MIN ? (l << 14) | (q - lo) : 0u);
         if ((key >> 14) > best) {
             best = key >> 14;
             bd = p - (lo + (key & 0x3FFFu));
         }
         if (best >= lim || inwin != GM) go = false;
         qa = qn;
-        k0 -= 16;
+        k0 -= LPC;
     }
     unres = false;
     if (best < (u32)LZ_MIN) {
@@ -369,20 +387,22 @@ __device__ void lzl_best(const u8* txt, u32 tlo, const u16* A, const u64* bm, co
     out_dist = bd;
 }
 
+template <u32 HOME, u32 LPC>
 __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
-    __shared__ __align__(16) u8 txt[LZL_TXT];
-    __shared__ __align__(16) u16 A[LZL_NW];
+    using G = LzlGeom<HOME, LPC>;
+    __shared__ __align__(16) u8 txt[G::TXT];
+    __shared__ __align__(16) u16 A[G::NW];
     // islot of [ilo, he) + head bitmap; the sort's histograms live here before them
-    __shared__ __align__(16) u16 B[LZL_ISL + 4 * ((LZL_NW + 63) / 64)];
+    __shared__ __align__(16) u16 B[G::BW];
     __shared__ u32 sh[4];
     u16* hist = B;  // the counting sort's 16-bit histograms (dead once the islot array is written)
     static_assert(sizeof(u16) * 4 * LZL_NBK <= sizeof(B), "histograms alias the islot array + bitmap");
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const u32 b = blockIdx.x / hpb, h = blockIdx.x - b * hpb;
     const u32 base = z.geo.base(b), end = z.geo.end(b);
-    const u32 hs = base + h * LZL_HOME;
+    const u32 hs = base + h * HOME;
     if (hs >= end) return;
-    const u32 he = min(hs + (u32)LZL_HOME, end);
+    const u32 he = min(hs + HOME, end);
     const u32 lo = hs - base > (u32)(LZ_WINDOW + LZL_LEAD) ? hs - LZ_WINDOW - LZL_LEAD : base;
     const u32 ilo = hs - base > (u32)LZL_LEAD ? hs - LZL_LEAD : base;
     const u32 hi = min(end, he + (u32)LZL_CAPX);
@@ -408,10 +428,10 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
     const u8* tw = txt + (lo - tlo);  // window text at window offset 0
     if (z.prof) t1 = wall_clock64();
     u16* isl = B;
-    u64* bm = reinterpret_cast<u64*>(B + LZL_ISL);  // disjoint from the sort's histograms
+    u64* bm = reinterpret_cast<u64*>(B + G::ISL);  // disjoint from the sort's histograms
     for (u32 i = tid; i < (nw + 63) / 64; i += 256) bm[i] = 0;
     if (nw) {
-        lzl_bucket(tw, A, nw, hist, sh);
+        lzl_bucket<G::PER>(tw, A, nw, hist, sh);
         // group-head bitmap = the starts of the non-empty buckets: after the placement, wave
         // 3's offset of bucket d is the bucket's end (bucket-major / wave-minor layout)
         for (u32 d = tid; d < LZL_NBK; d += 256) {
@@ -428,13 +448,13 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
     if (z.prof) t2 = wall_clock64();
     __syncthreads();
     if (z.prof) t3 = wall_clock64();
-    // 16 chains: chain g of wave w parses chunk cid = 4w + g
-    const u32 hl = lane & 15;
-    const u32 cid = w * 4 + (lane >> 4);
+    // NCHAIN chains: chain g of wave w parses chunk cid = CPW w + g
+    const u32 hl = lane & (LPC - 1);
+    const u32 cid = w * G::CPW + lane / LPC;
     const u32 s = hs + cid * LZL_CHUNK;
     const bool has = s < end;
     const u32 e = has ? min(s + (u32)LZL_CHUNK, end) : 0u;
-    const u32 c = b * z.cpb + h * LZL_NCHAIN + cid;
+    const u32 c = b * z.cpb + h * G::NCHAIN + cid;
     const u32 lend = has ? min(end, e + (u32)LZL_CAPX) : 0u;
     u32 q = has ? ((cid == 0 && hs == base) ? s : s - lead) : 0u;
     u32 ntok = 0, off = 0, nlong = 0, nbuf = 0, nstep = 0, nbatch = 0;
@@ -445,7 +465,7 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
         const bool act = has && q < e;
         u32 len, dist;
         bool unres;
-        lzl_best(txt, tlo, A, bm, isl, lo, ilo, act, q, act ? lend - q : 0u, end, len, dist, unres, nlong, nbatch);
+        lzl_best<LPC>(txt, tlo, A, bm, isl, lo, ilo, act, q, act ? lend - q : 0u, end, len, dist, unres, nlong, nbatch);
         if (act) {
             if (q >= s) {
                 if (hl == nbuf) {
@@ -454,8 +474,8 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
                     bdist = dist;
                     boff = off;
                 }
-                if (++nbuf == 16) {
-                    const u32 slot = s + ntok + 1 - 16 + hl;
+                if (++nbuf == LPC) {
+                    const u32 slot = s + ntok + 1 - LPC + hl;
                     z.tok_pos[slot] = bpos;
                     z.tok_len[slot] = blen;
                     z.tok_dist[slot] = bdist;
@@ -912,14 +932,24 @@ const char* lz_spec_name() { return "k_lz_local"; }
 
 void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
     if (!z.geo.nb) return;
-    const u32 hpb = (z.geo.bs + LZL_HOME - 1) / LZL_HOME;
+    // 4 KiB homes, 16 chains of 16 lanes (4 workgroups per CU).  KOLM_LZ_GEOM = 1 (A/B): 8 KiB
+    // homes parsed by 32 chains of 8 lanes — 2 workgroups per CU (110 KB of LDS instead of 138 KB),
+    // half the instructions per chain step, the same 64 chains per CU — measured slower beside the
+    // sort (parse 31.4 -> 36.1 ms, step 35.7 -> 39.9 ms): 2 waves per SIMD no longer hide the
+    // chains' dependent LDS latency
+    static const int geom = getenv("KOLM_LZ_GEOM") ? atoi(getenv("KOLM_LZ_GEOM")) : 0;
+    const u32 home = geom == 1 ? 8192u : 4096u;
+    const u32 hpb = (z.geo.bs + home - 1) / home;
     {
         // text window (LZL_NW + LZL_CAPX bytes per 4 KiB home: ~2.1 B per position) +
         // 16 B per token (added by the caller once the token count is known)
         static const u32 lead =
             getenv("KOLM_LZ_LEAD") ? std::min<u32>(atoi(getenv("KOLM_LZ_LEAD")), LZL_LEAD) : LZL_LEAD;
         KScope k(kt, KT_LZPARSE, "k_lz_local", z.geo.N * 2);
-        k_lz_local<<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb, lead);
+        if (geom == 1)
+            k_lz_local<8192, 8><<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb, lead);
+        else
+            k_lz_local<4096, 16><<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb, lead);
     }
     {
         KScope k(kt, KT_LZPARSE, "k_lz_stitch", (u64)z.cpb * z.geo.nb * 16);
