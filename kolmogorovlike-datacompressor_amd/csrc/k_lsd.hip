@@ -867,8 +867,8 @@ __global__ __launch_bounds__(WG) void k_alpha_codes(const u32* pres, u8* code, u
 // hist0 (optional): the first LSD pass's per-tile digit counts (digit 0 of KA), so that
 // pass needs no histogram kernel of its own; top: the counts of KB's top byte instead (the
 // first MSD digit of the MSD round 0, k_r0m.hip, which passes sh = 64 - C w).
-// part (0 or sh): the sh padding bits below the C codes hold the top sh bits of character C's
-// code (sh <= w), so round 0 also splits positions tied on C characters by most of the next one;
+// part (0 .. min(sh, w)): the top `part` of the sh padding bits below the C codes hold the top
+// `part` bits of character C's code, so round 0 also splits positions tied on C characters by most of the next one;
 // the doubling rounds still start from h = C (groups equal on C characters and the partial one
 // refine consistently: doubling compares (group(p), group(p + h)), and group(p + h) orders
 // character h fully)
@@ -919,12 +919,12 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
     u64 key = 0;
     for (u32 k = 0; k < C; ++k) key = (key << w) | (i0 + k < n ? cd[tx[i0 + k]] : 0u);
     u32 ka[LSD_PT], kb[LSD_PT];
-    const u32 psh = w - part;  // the partial character: its code's top `part` bits
+    const u32 psh = w - part, plo = sh - part;  // the partial character: its code's top `part` bits, right below character C - 1
 #pragma unroll
     for (u32 e = 0; e < LSD_PT; ++e) {
         const u32 x = i0 + e + C;
         const u32 nc = x < n ? cd[tx[x]] : 0u;
-        const u64 kk = (key << sh) | (part ? (u64)(nc >> psh) : 0ull);
+        const u64 kk = (key << sh) | (part ? (u64)(nc >> psh) << plo : 0ull);
         ka[e] = (u32)kk;
         kb[e] = (u32)(kk >> 32);
         key = ((key << w) | nc) & mask;
@@ -942,7 +942,7 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
                 k2 = (k2 << w) | cd[g.text[fs + t]];
                 if (++t == m) t = 0;
             }
-            const u64 kk = (k2 << sh) | (part ? (u64)(cd[g.text[fs + t]] >> psh) : 0ull);
+            const u64 kk = (k2 << sh) | (part ? (u64)(cd[g.text[fs + t]] >> psh) << plo : 0ull);
             ka[e] = (u32)kk;
             kb[e] = (u32)(kk >> 32);
         }
@@ -1173,9 +1173,10 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
             }
         }
     } else {
-        // the padding bits carry the next character's top bits (KOLM_R0_PART=0: zero padding)
+        // the padding bits carry the next character's top bits (KOLM_R0_PART = n: its top n bits
+        // only, 0: zero padding)
         const char* pte = getenv("KOLM_R0_PART");
-        const u32 part = (pte && atoi(pte) == 0) ? 0u : std::min(sh, t.w);
+        const u32 part = std::min(pte ? (u32)std::max(0, atoi(pte)) : 8u, std::min(sh, t.w));
         // per-(block, part) totals for the one-part-long scans (KOLM_LSD_SCAN2=0: per-block scans)
         const char* s2e = getenv("KOLM_LSD_SCAN2");
         const bool parts = !(s2e && atoi(s2e) == 0) && t.swc && g.tpb > 1;
