@@ -83,7 +83,12 @@ __device__ inline void load16nt(const u32* X, u32 i0, u32 hi, u32 (&v)[LSD_PT]) 
 // where a pass reads its (key, position) pairs: keys by position (first pass) or pairs
 // SRC_PK: one packed word per element, (digit 3 of the key) << 24 | position - block base (the
 // first half's last pass reads what its previous pass wrote that way: 8 bytes less per element)
-enum Src { SRC_KP = 1, SRC_PAIR = 2, SRC_PK = 3 };
+// SRC_REC: (key, position) as one u64 record per element (key in the low word)
+enum Src { SRC_KP = 1, SRC_PAIR = 2, SRC_PK = 3, SRC_REC = 4 };
+// what a pass writes: (key, position) pairs in two arrays, the packed word, or u64 records (one
+// 8-byte store per element: half the write transactions of the two arrays' 4-byte stores,
+// which a probe measured 1.5-1.8x faster on LSD run patterns, tools/scatter_probe.hip)
+enum Out { OUT_PAIR = 0, OUT_PK = 1, OUT_REC = 2 };
 
 // Per-(block, part) digit totals for k_lsd_scan2: a block's tiles form parts of 2^plt tiles.
 struct ScanParts {
@@ -128,7 +133,21 @@ __global__ __launch_bounds__(WG) void k_lsd_hist(LsdGeom g, const u32* K, u32* h
     u32 lo, hi, b;
     if (g.range(xcd_tile(), lo, hi, b)) {
         const u32 i0 = lo + tid * LSD_PT;
-        if ((lo & 3) == 0 && hi - lo == LSD_T) {
+        if (SRC == SRC_REC) {  // keys in the low words of the records
+            if ((lo & 1) == 0 && hi - lo == LSD_T) {
+                const uint4* p = reinterpret_cast<const uint4*>(K + 2 * (u64)lo);
+                uint4 v[LSD_PT / 2];
+#pragma unroll
+                for (u32 q = 0; q < LSD_PT / 2; ++q) v[q] = p[q * WG + tid];
+#pragma unroll
+                for (u32 q = 0; q < LSD_PT / 2; ++q) {
+                    h.add(digit<P>(v[q].x));
+                    h.add(digit<P>(v[q].z));
+                }
+            } else {
+                for (u32 i = i0; i < min(i0 + LSD_PT, hi); ++i) h.add(digit<P>(K[2 * (u64)i]));
+            }
+        } else if ((lo & 3) == 0 && hi - lo == LSD_T) {
             // a whole aligned tile: four 16-byte loads per thread, lane-contiguous (a wave
             // reads 1 KiB per instruction; the order of the keys is irrelevant here).  The
             // per-thread-contiguous form (lanes 64 B apart) ran at ~2 TB/s.
@@ -346,11 +365,13 @@ __global__ __launch_bounds__(WG) void k_lsd_scatter(LsdGeom g, const u32* Kin, c
 // per digit the waves' counts become bases (tile base + counts of the lower waves), and
 // pass 2 writes every element to base + offset.  Same order as k_lsd_scatter: (wave, step,
 // lane) is tile order.
-// OPK: write the packed word (digit 3 << 24 | position - block base) instead of (key, position)
-template <int P, int SRC, int G, int OPK = 0>
+// OUT: OUT_PK writes the packed word (digit 3 << 24 | position - block base), OUT_REC u64
+// records at Kout, OUT_PAIR (key, position) to Kout / Pout
+template <int P, int SRC, int G, int OUT = OUT_PAIR>
 __global__ __launch_bounds__(WG) void k_lsd_scatter_w(LsdGeom g, const u32* Kin, const u32* Pin, u32* Kout,
                                                      u32* Pout, const u32* Kg, const u32* hist) {
     static_assert(SRC != SRC_PK || P == 3, "packed words hold digit 3 only");
+    static_assert(OUT != OUT_PK || P == 2, "a packed word carries the next digit, 3");
     // few registers on purpose (keys and positions, offsets in LDS): the pass runs beside
     // the LZ77 parse, which holds 4 waves per SIMD, and a 108-VGPR version of this kernel
     // was starved for the parse's whole duration (one pass 1.7 -> 11 ms)
@@ -371,8 +392,14 @@ __global__ __launch_bounds__(WG) void k_lsd_scatter_w(LsdGeom g, const u32* Kin,
         key[j] = 0;
         pos[j] = 0;
         if (i < hi) {
-            key[j] = Kin[i];
-            pos[j] = SRC == SRC_KP ? i : SRC == SRC_PK ? g.geo.base(b) + (key[j] & 0xFFFFFFu) : Pin[i];
+            if (SRC == SRC_REC) {
+                const u64 r = reinterpret_cast<const u64*>(Kin)[i];
+                key[j] = (u32)r;
+                pos[j] = (u32)(r >> 32);
+            } else {
+                key[j] = Kin[i];
+                pos[j] = SRC == SRC_KP ? i : SRC == SRC_PK ? g.geo.base(b) + (key[j] & 0xFFFFFFu) : Pin[i];
+            }
         }
     }
     // G: the next key gathered by position up front (its latency under the ranking; at
@@ -415,8 +442,10 @@ __global__ __launch_bounds__(WG) void k_lsd_scatter_w(LsdGeom g, const u32* Kin,
     for (u32 j = 0; j < LSD_PT; ++j) {
         if (q0 + j * 64 + lane < hi) {
             const u32 dst = wc[w][digit<P>(key[j])] + lw[j * 64];
-            if (OPK) {
+            if (OUT == OUT_PK) {
                 Kout[dst] = (key[j] & 0xFF000000u) | (pos[j] - g.geo.base(b));
+            } else if (OUT == OUT_REC) {
+                reinterpret_cast<u64*>(Kout)[dst] = ((u64)pos[j] << 32) | (G ? kg[G ? j : 0] : key[j]);
             } else {
                 Kout[dst] = G ? kg[G ? j : 0] : key[j];
                 Pout[dst] = pos[j];
@@ -996,7 +1025,7 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
     }
 }
 
-template <int P, int SRC, int G, int OPK>
+template <int P, int SRC, int G, int OUT>
 void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kout, u32* pout, const u32* kg,
               u32* hist, bool counted, hipStream_t s, KTimer* kt, const ScanParts& sp) {
     static const std::string hn = "k_lsd_hist<" + std::to_string(P) + ", " + std::to_string(SRC) + ">";
@@ -1005,12 +1034,12 @@ void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kou
     static const int sw = getenv("KOLM_LSD_SW") ? atoi(getenv("KOLM_LSD_SW")) : 2;
     const bool use_w = sw == 2 || (sw == 1 && SRC == SRC_PAIR);
     static const std::string tail = "<" + std::to_string(P) + ", " + std::to_string(SRC) + ", " + std::to_string(G) +
-                                    (OPK ? ", 1>" : ">");
+                                    (OUT ? ", " + std::to_string(OUT) + ">" : std::string(">"));
     static const std::string sn_w = "k_lsd_scatter_w" + tail, sn_p = "k_lsd_scatter" + tail;
     const std::string& sn = use_w ? sn_w : sn_p;
     const u64 N = g.geo.N, H = (u64)nt * 1024;  // H: per-tile histogram bytes
     if (!counted) {  // counted: the producer of kin wrote the tile histograms
-        KScope k(kt, KT_LSD, hn.c_str(), 4 * N + H);
+        KScope k(kt, KT_LSD, hn.c_str(), (SRC == SRC_REC ? 8 : 4) * N + H);
         k_lsd_hist<P, SRC><<<nt, WG, 0, s>>>(g, kin, hist, sp);
     }
     if (sp.cur) {
@@ -1034,13 +1063,13 @@ void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kou
     {
         // key + position in (the first pass reads the key by position only) and out; G: + the gather
         // bytes in: key (+ position unless implicit or packed); out: key + position, or the packed word
-        const u64 in = SRC == SRC_PAIR ? 8 : 4, outb = OPK ? 4 : 8;
+        const u64 in = (SRC == SRC_PAIR || SRC == SRC_REC) ? 8 : 4, outb = OUT == OUT_PK ? 4 : 8;
         KScope k(kt, KT_LSD, sn.c_str(), (in + outb) * N + (G ? 4 * N : 0) + H);
         // k_lsd_scatter_w (three barriers per tile; 256 MiB text, overlapped: 1.5-1.7 -> 0.9-1.0
         // ms per pass)
-        if (use_w || OPK || SRC == SRC_PK)
-            k_lsd_scatter_w<P, SRC, G, OPK><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
-        else if constexpr (SRC != SRC_PK)
+        if (use_w || OUT != OUT_PAIR || SRC == SRC_PK || SRC == SRC_REC)
+            k_lsd_scatter_w<P, SRC, G, OUT><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
+        else if constexpr (SRC != SRC_PK && SRC != SRC_REC)
             k_lsd_scatter<P, SRC, G><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
     }
 }
@@ -1084,6 +1113,23 @@ void sweep_pass(int P, bool src_kp, bool gat, int nm, const LsdGeom& g, u32 S, u
     }
 }
 
+// The eight passes of record mode (8-byte keys, both halves 4 passes): the first half KA
+// (positions) -> records -> records -> packed words -> records with KB gathered; the second half
+// records -> records -> records -> records -> (K2, SA) pairs for the group heads
+void run_pass_rec(u32 idx, const LsdGeom& g, u32 nt, const u32* kin, u32* kout, u32* pout, const u32* kg,
+                  u32* hist, hipStream_t s, KTimer* kt, const ScanParts& sp) {
+    switch (idx) {
+        case 0: return lsd_pass<0, SRC_KP, 0, OUT_REC>(g, nt, kin, nullptr, kout, nullptr, nullptr, hist, true, s, kt, sp);
+        case 1: return lsd_pass<1, SRC_REC, 0, OUT_REC>(g, nt, kin, nullptr, kout, nullptr, nullptr, hist, false, s, kt, sp);
+        case 2: return lsd_pass<2, SRC_REC, 0, OUT_PK>(g, nt, kin, nullptr, kout, nullptr, nullptr, hist, false, s, kt, sp);
+        case 3: return lsd_pass<3, SRC_PK, 1, OUT_REC>(g, nt, kin, nullptr, kout, nullptr, kg, hist, false, s, kt, sp);
+        case 4: return lsd_pass<0, SRC_REC, 0, OUT_REC>(g, nt, kin, nullptr, kout, nullptr, nullptr, hist, false, s, kt, sp);
+        case 5: return lsd_pass<1, SRC_REC, 0, OUT_REC>(g, nt, kin, nullptr, kout, nullptr, nullptr, hist, false, s, kt, sp);
+        case 6: return lsd_pass<2, SRC_REC, 0, OUT_REC>(g, nt, kin, nullptr, kout, nullptr, nullptr, hist, false, s, kt, sp);
+        default: return lsd_pass<3, SRC_REC, 0, OUT_PAIR>(g, nt, kin, nullptr, kout, pout, nullptr, hist, false, s, kt, sp);
+    }
+}
+
 using PassFn = void (*)(const LsdGeom&, u32, const u32*, const u32*, u32*, u32*, const u32*, u32*, bool, hipStream_t,
                         KTimer*, const ScanParts&);
 template <int P>
@@ -1095,8 +1141,8 @@ constexpr PassFn pass_of(int src_kp, int gat) {
 void run_pass(int P, bool src_kp, bool gat, const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kout,
               u32* pout, const u32* kg, u32* hist, bool counted, hipStream_t s, KTimer* kt, int pk,
               const ScanParts& sp) {
-    if (pk == 1) return lsd_pass<2, SRC_PAIR, 0, 1>(g, nt, kin, pin, kout, pout, kg, hist, counted, s, kt, sp);
-    if (pk == 2) return lsd_pass<3, SRC_PK, 1, 0>(g, nt, kin, pin, kout, pout, kg, hist, counted, s, kt, sp);
+    if (pk == 1) return lsd_pass<2, SRC_PAIR, 0, OUT_PK>(g, nt, kin, pin, kout, pout, kg, hist, counted, s, kt, sp);
+    if (pk == 2) return lsd_pass<3, SRC_PK, 1, OUT_PAIR>(g, nt, kin, pin, kout, pout, kg, hist, counted, s, kt, sp);
     const int a = src_kp ? 1 : 0, c = gat ? 1 : 0;
     const PassFn f = P == 0 ? pass_of<0>(a, c) : P == 1 ? pass_of<1>(a, c) : P == 2 ? pass_of<2>(a, c) : pass_of<3>(a, c);
     f(g, nt, kin, pin, kout, pout, kg, hist, counted, s, kt, sp);
@@ -1218,7 +1264,19 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
         // position inside the block) when a block position fits 24 bits (KOLM_LSD_PACK=0: off)
         const char* pke = getenv("KOLM_LSD_PACK");
         const bool pack = !(pke && atoi(pke) == 0) && pa == 4 && pb > 0 && geo.bs <= (1u << 24);
-        for (u32 q = 0; q < pa; ++q) {
+        // record mode (KOLM_LSD_REC=0: off) for 8-byte keys: the pairs between passes as u64 records
+        const char* rce = getenv("KOLM_LSD_REC");
+        const bool rec = !(rce && atoi(rce) == 0) && pack && pb == 4 && t.rec[0] && t.rec[1];
+        if (rec) {
+            u32* R2[2] = {reinterpret_cast<u32*>(t.rec[0]), reinterpret_cast<u32*>(t.rec[1])};
+            // inputs / outputs per pass: KA -> R0 -> R1 -> K22 (packed) -> R0 -> R1 -> R0 -> R1 -> (K2, SA)
+            const u32* in[8] = {t.RK, R2[0], R2[1], t.K22, R2[0], R2[1], R2[0], R2[1]};
+            u32* out[8] = {R2[0], R2[1], t.K22, R2[0], R2[1], R2[0], R2[1], t.K2};
+            for (u32 q = 0; q < 8; ++q, ++pidx)
+                run_pass_rec(q, g, nt, in[q], out[q], q == 7 ? t.SA : nullptr, q == 3 ? t.KP : nullptr, t.hist, s, kt,
+                             spp());
+        }
+        for (u32 q = 0; q < (rec ? 0u : pa); ++q) {
             const bool first = q == 0, gat = q + 1 == pa && pb > 0;
             const int pk = pack ? (q == 2 ? 1 : q == 3 ? 2 : 0) : 0;
             run_pass((int)q, first, gat, g, nt, first ? t.RK : K[o ^ 1], first ? nullptr : S[o ^ 1], K[o], S[o],
@@ -1226,7 +1284,7 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
             o ^= 1;
             ++pidx;
         }
-        for (u32 q = 0; q < pb; ++q) {
+        for (u32 q = 0; q < (rec ? 0u : pb); ++q) {
             run_pass((int)q, false, false, g, nt, K[o ^ 1], S[o ^ 1], K[o], S[o], nullptr, t.hist, false, s, kt, 0,
                      spp());
             o ^= 1;

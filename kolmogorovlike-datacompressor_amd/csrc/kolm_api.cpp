@@ -478,6 +478,8 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
                      c->get<u32>("r0hist", nt * 256), c->get<u32>("r0tmax", nt), c->get<u32>("r0tmin", nt),
                      c->get<u32>("r0cmax", nt), c->get<u32>("r0cmin", nt), c->get<u32>("r0hf", nt * WG),
                      c->get<u32>("r0swc", (u64)2 * geo.nb * 16 * 256)};
+            r.rec[0] = c->get<u64>("r0rec0", N);
+            r.rec[1] = c->get<u64>("r0rec1", N);
             out.r0_chars = C;
             if (dbg) fprintf(stderr, "[kolm] round 0: %u characters of %u bits\n", C, w);
             if (r0_msd_mode()) {

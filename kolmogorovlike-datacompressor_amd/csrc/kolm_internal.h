@@ -345,6 +345,7 @@ struct R0Bufs {
     u32 *tmax, *tmin, *cmax, *cmin;  // [lsd_tiles]
     u32* HF;   // [lsd_tiles * WG] group-head masks (LSD_T / WG slots per thread)
     u32* swc = nullptr;  // [2 * nb * 16 * 256] per-(block, part) digit totals of the LSD scans / sweep passes
+    u64* rec[2] = {nullptr, nullptr};  // [N] each: the LSD passes' (key, position) records (record mode)
 };
 // per-block code tables for round 0 (alphabet compaction), max code width of the batch
 u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w, u32* h_w, bool compact,
