@@ -255,12 +255,18 @@ __global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur_in, c
         ltiles = 0;
     }
     __syncthreads();
-    const u32 stride = gridDim.x * 256;
+    // each workgroup walks one contiguous share of the list (concurrent workgroups then work
+    // in different regions of it, so the per-(class, bin) atomics of MODE 1 / 2 do not pile on
+    // the same few counters; KOLM_CLS_CHUNK=0: the grid-stride walk)
+    const u32 per = ((ncur + gridDim.x * 256 - 1) / (gridDim.x * 256)) * 256;
+    const u32 wbeg = a.cls_chunk ? min(blockIdx.x * per, ncur) : blockIdx.x * 256;
+    const u32 wend = a.cls_chunk ? min(wbeg + per, ncur) : ncur;
+    const u32 stride = a.cls_chunk ? 256u : gridDim.x * 256;
     const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     if (MODE == 2) {
-        for (u32 i0 = blockIdx.x * 256; i0 < ncur; i0 += stride) {
+        for (u32 i0 = wbeg; i0 < wend; i0 += stride) {
             Seg s;
-            const int c = seg_class(a, cur, ncur, i0 + tid, s);
+            const int c = seg_class(a, cur, wend, i0 + tid, s);
             const u32 key = (c >= 0 && c < NCLASS) ? (u32)c * CLS_NBIN + (s.start >> bn.bsh) : ~0u;
             u64 pend = __ballot(key != ~0u);
             u32 dst = 0;
@@ -279,9 +285,9 @@ __global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur_in, c
         return;
     }
     // pass 1: counts
-    for (u32 i0 = blockIdx.x * 256; i0 < ncur; i0 += stride) {
+    for (u32 i0 = wbeg; i0 < wend; i0 += stride) {
         Seg s;
-        const int c = seg_class(a, cur, ncur, i0 + tid, s);
+        const int c = seg_class(a, cur, wend, i0 + tid, s);
         if (MODE == 1) {
             const u32 key = (c >= 0 && c < NCLASS) ? (u32)c * CLS_NBIN + (s.start >> bn.bsh) : ~0u;
             u64 bp = __ballot(key != ~0u);
@@ -329,9 +335,9 @@ __global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur_in, c
     __syncthreads();
     if (MODE == 1 && lcnt[NCLASS] == 0) return;  // small segments are placed by MODE 2
     // pass 2: writes
-    for (u32 i0 = blockIdx.x * 256; i0 < ncur; i0 += stride) {
+    for (u32 i0 = wbeg; i0 < wend; i0 += stride) {
         Seg s;
-        const int c = seg_class(a, cur, ncur, i0 + tid, s);
+        const int c = seg_class(a, cur, wend, i0 + tid, s);
         u64 pend = __ballot(MODE == 1 ? c == NCLASS : c >= 0);
         u32 li = 0;
         while (pend) {

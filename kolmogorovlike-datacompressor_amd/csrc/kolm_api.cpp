@@ -372,6 +372,8 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
     // large groups are few anyway — 256 MiB text: 41.8 vs 37.5 ms per step with it)
     static const int med = getenv("KOLM_MED_SORT") ? atoi(getenv("KOLM_MED_SORT")) : -1;
     a.med = (med > 0 || (med < 0 && geo.nb < 64)) ? 1u : 0u;
+    static const bool cls_chunk = !(getenv("KOLM_CLS_CHUNK") && atoi(getenv("KOLM_CLS_CHUNK")) == 0);
+    a.cls_chunk = cls_chunk ? 1u : 0u;
 
     u32* cnt = c->get<u32>("counters", C_N);
     Lists L{};

@@ -235,6 +235,7 @@ struct SortArgs {
     const u32* KP;     // [N] this round's key by position (k_keypos), or null: keys gathered directly
     u32 key_bits;      // keys of this round are < 2^key_bits (small sort packs key|index in 32 bits)
     u32* KA;           // cyclic round 0 with 8 characters: k_keypos also writes characters 4..7 here
+    u32 cls_chunk;     // k_classify: one contiguous share of the list per workgroup (else grid-stride)
     u32 xcd;           // class lists are position-ordered: per-class kernels map workgroups to
                        // XCD-contiguous list ranges (k_classify_bins)
 };
