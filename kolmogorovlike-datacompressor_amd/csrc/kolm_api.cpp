@@ -961,14 +961,24 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         KOLM_HIP_CHECK(hipEventRecord(ej[3], s));
         KOLM_HIP_CHECK(hipStreamWaitEvent(ms, ej[3], 0));
     }
-    c->active = ms;
+    // Batches of fewer than 64 blocks: the xor / lfsr sizes and (below) the BBWT's predecessor
+    // bytes go to the third stream when Re-Pair does not use it, so the LZ77 parse at the head of
+    // the index stream starts at once instead of behind them (prevc waits for the Lyndon factors):
+    // config 4's 32-block shard 6.30 -> 6.20-6.27 ms.  On full batches the early parse competes
+    // with Lyndon and round 0 (256 MiB: 34.5 -> 35.2 ms), so they keep the index-stream order.
+    // KOLM_SIDE_STREAM = 0 / 1 forces it.
+    static const int side_env = getenv("KOLM_SIDE_STREAM") ? atoi(getenv("KOLM_SIDE_STREAM")) : -1;
+    const bool side = (side_env >= 0 ? side_env != 0 : nb < 64) && !serial && !want_rp;
+    hipStream_t xs = side ? c->rp : ms;
+    if (side) KOLM_HIP_CHECK(hipStreamWaitEvent(c->rp, ev[0], 0));
+    c->active = xs;
     {
         EmitArgs ce{};
         ce.geo = geo;
         ce.text = d_text;
         ce.bits = d_bits;
         TScope t(c, KOLM_KT_SIZES, "k_cheap_sizes", N);
-        launch_cheap_sizes(ce, ms);
+        launch_cheap_sizes(ce, xs);
     }
     // The BBWT gather's predecessor bytes on the index stream, off the sort chain — but
     // prevc waits for the Lyndon factors, and the LZ77 parse queued behind it on that stream
@@ -980,11 +990,13 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     // KOLM_PREVC_IDX = 0 / 1 forces it.
     static const int prevc_idx = getenv("KOLM_PREVC_IDX") ? atoi(getenv("KOLM_PREVC_IDX")) : -1;
     if (!serial && (prevc_idx >= 0 ? prevc_idx != 0 : nb >= 16)) {
-        KOLM_HIP_CHECK(hipStreamWaitEvent(ms, ev[5], 0));
+        KOLM_HIP_CHECK(hipStreamWaitEvent(xs, ev[5], 0));
         P.prevc();
-        KOLM_HIP_CHECK(hipEventRecord(ev[6], ms));
+        KOLM_HIP_CHECK(hipEventRecord(ev[6], xs));
         P.prevc_ready = ev[6];
     }
+    if (side) KOLM_HIP_CHECK(hipEventRecord(ev[7], xs));  // the sizes, joined before the MDL
+    c->active = ms;
     KOLM_HIP_CHECK(hipEventRecord(ej[0], ms));
     LzArgs z = P.lz_args();
     const bool want_lz = (mask >> KOLM_M_LZ77) & 1u || (h_force != nullptr);
@@ -1055,6 +1067,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     u32* cnt = c->get<u32>("counters", C_N);
     KOLM_HIP_CHECK(hipMemsetAsync(cnt + C_STATUS, 0, sizeof(u32), s));
     if (want_rp) KOLM_HIP_CHECK(hipStreamWaitEvent(s, c->evr[0], 0));
+    if (side) KOLM_HIP_CHECK(hipStreamWaitEvent(s, ev[7], 0));
     {
         TScope t(c, KOLM_KT_SIZES, "k_mdl+offsets", (u64)nb * 120);
         launch_mdl(e, want_lz ? z.lz_size : nullptr, want_rp ? rpa.result : nullptr, want_v2 ? v2.size : nullptr,
