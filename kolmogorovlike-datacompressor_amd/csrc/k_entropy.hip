@@ -349,7 +349,13 @@ __global__ __launch_bounds__(WG) void k_rice_emit(TileG tg, const u8* seq, const
     const u64 gstart = off[b] * 8 + toff[blockIdx.x];  // tile start bit (global)
     const u32 lead = (u32)(gstart & 31);               // bit offset inside first word
     const u64 w0 = gstart >> 5;
-    for (u32 i = threadIdx.x; i < lds_words; i += WG) lds[i] = 0;
+    // total bits of the tile; only the words the tile's code reaches are cleared (a few hundred
+    // of the lds_words sized for the worst case)
+    __shared__ u32 tot;
+    if (threadIdx.x == WG - 1) tot = my + cnt;
+    __syncthreads();
+    const u32 nclr = min(lds_words, ((lead + tot + 31) >> 5) + 3);
+    for (u32 i = threadIdx.x; i < nclr; i += WG) lds[i] = 0;
     __syncthreads();
     u32 pos = lead + my;
     if (cnt <= 64) {
@@ -392,10 +398,6 @@ __global__ __launch_bounds__(WG) void k_rice_emit(TileG tg, const u8* seq, const
             pos += 1 + k;
         }
     }
-    __syncthreads();
-    // total bits of the tile
-    __shared__ u32 tot;
-    if (threadIdx.x == WG - 1) tot = pos - lead;
     __syncthreads();
     const u32 nwords = (lead + tot + 31) >> 5;
     u32* a32 = reinterpret_cast<u32*>(arena);

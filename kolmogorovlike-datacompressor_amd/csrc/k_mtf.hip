@@ -380,25 +380,47 @@ constexpr int RT = 128;  // threads per workgroup in the replay kernel
 // Rice-k bit lengths of the 5 BBWT candidates (PY:2028-2073: flags 0, bit-plane, nibble,
 // bit reverse, Gray) accumulated while the MTF indices are produced (counter order of
 // k_entropy.hip: 0 plain, 1 bit-plane, 2 nibble, 3 bit reverse, 4 Gray).
+// Four bytes at a time (SWAR): the per-byte maps act on a whole word, v >> k on every byte
+// is one shift and mask, and V_SAD_U8 sums the four bytes into the counter.
 struct RiceAcc {
     u32 c[5] = {0, 0, 0, 0, 0};
     int k;
+    u32 kk = 0, km = 0;  // shift and per-byte mask of v >> k (k >= 8: every byte shifts to 0)
+    __device__ inline void init(int rk) {
+        k = rk;
+        kk = rk < 8 ? (u32)rk : 0u;
+        km = rk < 8 ? (0xFFu >> rk) * 0x01010101u : 0u;
+    }
     __device__ inline u32 rb(u32 v) const { return (v >> k) + 1 + k; }
+    // sum over the 4 bytes x of x >> k, added to a
+    __device__ inline u32 sum4(u32 w, u32 a) const { return __builtin_amdgcn_sad_u8((w >> kk) & km, 0u, a); }
     __device__ inline void add(u32 v) {
         c[0] += rb(v);
         c[2] += rb(((v & 0x0Fu) << 4) | (v >> 4));
         c[3] += rb(__brev(v) >> 24);
         c[4] += rb(v ^ (v >> 1));
     }
-    // one 8-byte bit-plane group (PY:1100-1120), bytes little-endian in lo / hi
+    // add() of the four bytes of o
+    __device__ inline void add4(u32 o) {
+        const u32 one = 4 * (1 + k);
+        c[0] = sum4(o, c[0] + one);
+        c[2] = sum4(((o & 0x0F0F0F0Fu) << 4) | ((o >> 4) & 0x0F0F0F0Fu), c[2] + one);  // nibble swap
+        c[3] = sum4(__brev(o), c[3] + one);  // byte order reversed too: the sum does not see it
+        c[4] = sum4(o ^ ((o >> 1) & 0x7F7F7F7Fu), c[4] + one);  // Gray
+    }
+    // one 8-byte bit-plane group (PY:1100-1120), bytes little-endian in lo / hi: plane b's
+    // value has byte i's bit b at bit 7 - i.  With the bytes reversed (byte 7 - i at i) that is
+    // the 8x8 bit-matrix transpose (byte r, bit c) -> (byte c, bit r), three delta swaps; the
+    // order of the 8 plane values does not matter to the sum
     __device__ inline void group(u32 lo, u32 hi) {
-#pragma unroll
-        for (int bit = 0; bit < 8; ++bit) {
-            u32 v = 0;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) v |= (((i < 4 ? lo >> (8 * i) : hi >> (8 * (i - 4))) >> (7 - bit)) & 1u) << (7 - i);
-            c[1] += rb(v);
-        }
+        u64 x = ((u64)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
+        u64 t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+        x ^= t ^ (t << 7);
+        t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+        x ^= t ^ (t << 14);
+        t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+        x ^= t ^ (t << 28);
+        c[1] = sum4((u32)(x >> 32), sum4((u32)x, c[1] + 8 * (1 + k)));
     }
 };
 
@@ -462,7 +484,7 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
         return 4 * w + j;
     };
     RiceAcc acc;
-    acc.k = rice_k;
+    acc.init(rice_k);
     if (!valid) return;
     if (((lo | hi) & 63) == 0) {
         // 64 bytes in / 64 bytes out per step as four back-to-back 16-byte accesses, so a
@@ -480,12 +502,9 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
                 const u32 wq = q % 4 == 0 ? v[q / 4].x : q % 4 == 1 ? v[q / 4].y : q % 4 == 2 ? v[q / 4].z : v[q / 4].w;
                 u32 o = 0;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const u32 m = step((wq >> (8 * j)) & 0xFF);
-                    if (bits) acc.add(m);
-                    o |= m << (8 * j);
-                }
+                for (int j = 0; j < 4; ++j) o |= step((wq >> (8 * j)) & 0xFF) << (8 * j);
                 ov[q] = o;
+                if (bits) acc.add4(o);
                 if (bits && (q & 1)) acc.group(ov[q - 1], o);
             }
 #pragma unroll
@@ -502,12 +521,9 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
             for (int q = 0; q < 4; ++q) {
                 u32 o = 0;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const u32 m = step((wv[q] >> (8 * j)) & 0xFF);
-                    if (bits) acc.add(m);
-                    o |= m << (8 * j);
-                }
+                for (int j = 0; j < 4; ++j) o |= step((wv[q] >> (8 * j)) & 0xFF) << (8 * j);
                 ov[q] = o;
+                if (bits) acc.add4(o);
             }
             *reinterpret_cast<uint4*>(out + i) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
             if (bits) {
@@ -573,7 +589,7 @@ __global__ __launch_bounds__(256) void k_mtf_wave(ChunkGeom cg, const u8* in, co
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
     RiceAcc acc;
-    acc.k = rice_k;
+    acc.init(rice_k);
     const u64 below = (1ull << lane) - 1ull;  // lanes before this one
     for (u32 p = lo; p < hi; p += 64) {
         const u32 i = p + lane;
@@ -642,9 +658,10 @@ __global__ __launch_bounds__(256) void k_mtf_wave(ChunkGeom cg, const u8* in, co
 }  // namespace
 
 // The position-parallel replay (k_mtf_wave, 1 KiB chunks) for batches of few blocks;
-// KOLM_MTF_WAVE = 0 / 1 forces it off / on.
+// KOLM_MTF_WAVE = 0 / 1 forces it off / on (read per call).
 bool mtf_wave_mode(const Geom& geo) {
-    static const int force = getenv("KOLM_MTF_WAVE") ? atoi(getenv("KOLM_MTF_WAVE")) : -1;
+    const char* e = getenv("KOLM_MTF_WAVE");
+    const int force = e ? atoi(e) : -1;
     return force >= 0 ? force != 0 : geo.nb < 64;
 }
 

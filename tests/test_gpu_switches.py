@@ -9,6 +9,8 @@ payload with the oracle (PY:351-423 BBWT order, PY:460 MTF, PY:1413 Rice, PY:235
   KOLM_LSD_PACK=0   no packed first-half pass;  KOLM_LSD_SCAN2=0: per-block LSD scans
   KOLM_MTF_CP=0     one-workgroup-per-block MTF compose
   KOLM_DUVAL_GRP=0  Duval span merges a thread per merge (a wave from level 4096)
+  KOLM_MTF_WAVE=0   the per-thread MTF replay (and its SWAR Rice sums) on batches of few blocks,
+                    with chunks of 128..512 bytes and ragged block ends
 """
 import pytest
 
@@ -25,6 +27,7 @@ SWITCHES = [
     {"KOLM_LSD_PACK": "0", "KOLM_LSD_SCAN2": "0"},
     {"KOLM_MTF_CP": "0"},
     {"KOLM_DUVAL_GRP": "0"},
+    {"KOLM_MTF_WAVE": "0"},
 ]
 
 
