@@ -992,7 +992,63 @@ __global__ __launch_bounds__(256) void k_bbwt_gather(Geom geo, const u32* SA, co
     }
 }
 
+// Early BBWT gather (bbwt_early_round): the slots outside the still-active segments of a
+// doubling round hold their final SA entries — later rounds only reorder slots inside those
+// segments — so their BBWT bytes can be gathered while the last rounds run.  BM: one bit per
+// slot, set for the slots of the active segments (one thread per segment; words inside a
+// segment are written whole, the partial end words by atomic OR).
+__global__ __launch_bounds__(256) void k_mark_active(const Seg* cur, const u32* ncur, u32 bound, u64* bm) {
+    const u32 i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= min(bound, *ncur)) return;
+    const Seg sg = cur[i];
+    if (!sg.len) return;
+    const u32 a = sg.start, e = sg.start + sg.len;  // [a, e)
+    const u32 wa = a >> 6, we = (e - 1) >> 6;
+    const u64 ma = ~0ull << (a & 63), me = ~0ull >> (63 - ((e - 1) & 63));
+    if (wa == we) {
+        atomicOr((unsigned long long*)&bm[wa], (unsigned long long)(ma & me));
+        return;
+    }
+    atomicOr((unsigned long long*)&bm[wa], (unsigned long long)ma);
+    for (u32 w = wa + 1; w < we; ++w) bm[w] = ~0ull;
+    atomicOr((unsigned long long*)&bm[we], (unsigned long long)me);
+}
+
+// k_bbwt_gather for the slots whose BM bit is set only: 16 consecutive slots per thread, one
+// 16-bit piece of the mask each (most are zero: a few percent of the slots stay active)
+__global__ __launch_bounds__(256) void k_bbwt_gather_m(Geom geo, const u32* SA, const u8* prevc, u8* out,
+                                                       const u64* bm) {
+    const u32 g0 = xcd_tile() * 4096u + 16u * threadIdx.x;
+    if (g0 >= geo.N) return;
+    u32 m = (u32)(bm[g0 >> 6] >> (g0 & 63)) & 0xFFFFu;
+    while (m) {
+        const u32 g = g0 + (u32)__ffs(m) - 1;
+        if (g < geo.N) out[g] = prevc[SA[g]];
+        m &= m - 1;
+    }
+}
+
 }  // namespace
+
+// The doubling round after whose classification the early BBWT gather starts (KOLM_EARLY_GATHER,
+// read per call; 0: off).  Round 3 (text: ~0.2 % of the slots still active): one A/B call, two
+// runs each (profiles/r05/ab_early_gather_*): the sort stream ends 0.4 ms sooner (ms_sa 32.2 ->
+// 31.8 ms) while the step stays at 34.1-34.3 ms, bound by the LZ77 stream it joins; config 4's
+// shard 6.26 / 6.41 -> 6.20 / 6.23 ms.  Round 2 (~9 % active) costs more than it saves (35.0 ms:
+// its gather competes with round 2's sorts and the parse).
+u32 bbwt_early_round() {
+    const char* e = getenv("KOLM_EARLY_GATHER");
+    return e ? (u32)atoi(e) : 3u;
+}
+
+void launch_mark_active(const Seg* cur, const u32* ncur_dev, u32 bound, u64* bm, hipStream_t s) {
+    if (bound) k_mark_active<<<(bound + 255) / 256, 256, 0, s>>>(cur, ncur_dev, bound, bm);
+}
+void launch_bbwt_gather_masked(const Geom& geo, const u32* SA, const u8* prevc, u8* out, const u64* bm,
+                               hipStream_t s) {
+    if (!geo.N) return;
+    k_bbwt_gather_m<<<(u32)((geo.N + 4095) / 4096), 256, 0, s>>>(geo, SA, prevc, out, bm);
+}
 
 // KOLM_DUVAL_PROF=1 (debug): per-phase wall-clock of k_duval_span and k_duval_merge
 u64* dprof_buf() {

@@ -162,6 +162,7 @@ struct kolm_ctx {
     std::unique_ptr<CopyPool> pool;
     hipEvent_t evj[4] = {};        // join events
     hipEvent_t evr[2] = {};        // Re-Pair start / done
+    hipEvent_t evg[2] = {};        // early BBWT gather: slots marked / gathered
     std::mutex mu;
     std::map<std::string, DevBuf> bufs;
     u32* h_cnt = nullptr;  // pinned mirror of the counters
@@ -345,8 +346,11 @@ struct SortOut {
 // Segmented prefix-doubling suffix sort of every block of the batch (k_sort.hip).
 // after_round0 (optional) runs on the host right after round 0 is enqueued (cyclic pass),
 // before the pass waits for its counts: encode_batch hooks the LZ77 launch there.
+// at_round (optional) runs on the host once round r's segment list `cur` is classified (its
+// device count at ncur_dev, at most `bound`), before the round's sorts are enqueued.
+using RoundHook = std::function<void(u32 round, const Seg* cur, u32 bound, const u32* ncur_dev)>;
 SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Factors fac, const u8* FEd,
-                  const std::function<void()>& after_round0 = {}) {
+                  const std::function<void()>& after_round0 = {}, const RoundHook& at_round = {}) {
     hipStream_t s = c->active;
     const u64 N = geo.N;
     SortOut out;
@@ -541,6 +545,10 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             for (int k = 0; k < NCLASS; ++k) fprintf(stderr, " %d:%u/%u", k, h[C_CLS + k], h[C_CLSE + k]);
             fprintf(stderr, "\n");
         }
+        if (at_round) {
+            at_round(round, cur, ncur, ncur_dev);
+            c->active = s;
+        }
         {
             // Dense rounds: keys by position first (sequential pass), then one gather per
             // slot; sparse rounds gather the key inputs per active slot directly.
@@ -675,18 +683,52 @@ struct Pipeline {
         TScope t(c, KOLM_KT_LYNDON, "k_prevc", N * 3);  // flag 1 + text 1 + prevc 1 (+ factor starts)
         launch_prevc(geo, text, c->get<u8>("flag", N), factors(), c->get<u8>("prevc", N), c->active);
     }
+    // early_gather: the encode path allows the early BBWT gather on the third stream (idle:
+    // no Re-Pair, prevc computed on another stream)
+    bool early_gather = false;
     u8* cyclic(const std::function<void()>& after_round0 = {}, u8* out = nullptr) {
         const u64 N = geo.N;
-        SortOut cyc = sort_pass(c, geo, text, true, factors(), c->get<u8>("FEd", N), after_round0);
         if (!out) out = c->get<u8>("bbwt", N);
         u8* prevc = c->get<u8>("prevc", N);
-        if (prevc_ready)
-            KOLM_HIP_CHECK(hipStreamWaitEvent(c->active, prevc_ready, 0));
-        else
-            this->prevc();
-        {
+        u32* SA = c->get<u32>("SA", N);
+        // Early BBWT gather (bbwt_early_round() = R > 0): once doubling round R's segments are
+        // classified, every slot outside them holds its final SA entry, so the third stream
+        // gathers every slot's BBWT byte beside the remaining rounds (and the LZ77 parse), and
+        // the slots of round R's segments — whose early bytes may be stale — are gathered
+        // again after the last round
+        const u32 er = early_gather && prevc_ready ? bbwt_early_round() : 0u;
+        bool early = false;
+        const RoundHook hook = [&](u32 round, const Seg* cur, u32 bound, const u32* ncur_dev) {
+            if (early || round != er) return;
+            hipStream_t s = c->active, x = c->rp;
+            u64* bm = c->get<u64>("bbwt_bm", (N + 63) / 64);
+            KOLM_HIP_CHECK(hipMemsetAsync(bm, 0, sizeof(u64) * ((N + 63) / 64), s));
+            launch_mark_active(cur, ncur_dev, bound, bm, s);
+            KOLM_HIP_CHECK(hipEventRecord(c->evg[0], s));
+            KOLM_HIP_CHECK(hipStreamWaitEvent(x, c->evg[0], 0));
+            KOLM_HIP_CHECK(hipStreamWaitEvent(x, prevc_ready, 0));
+            c->active = x;
+            {
+                TScope t(c, KOLM_KT_LYNDON, "k_bbwt_gather (early)", N * 6);
+                launch_bbwt_gather(geo, SA, prevc, out, x);
+            }
+            KOLM_HIP_CHECK(hipEventRecord(c->evg[1], x));
+            c->active = s;
+            early = true;
+        };
+        SortOut cyc = sort_pass(c, geo, text, true, factors(), c->get<u8>("FEd", N), after_round0,
+                                er ? hook : RoundHook{});
+        if (early) {
+            KOLM_HIP_CHECK(hipStreamWaitEvent(c->active, c->evg[1], 0));
+            TScope t(c, KOLM_KT_LYNDON, "k_bbwt_gather", N / 8 + N / 16);  // the mask + about 1/16 of the slots
+            launch_bbwt_gather_masked(geo, SA, prevc, out, c->get<u64>("bbwt_bm", (N + 63) / 64), c->active);
+        } else {
+            if (prevc_ready)
+                KOLM_HIP_CHECK(hipStreamWaitEvent(c->active, prevc_ready, 0));
+            else
+                this->prevc();
             TScope t(c, KOLM_KT_LYNDON, "k_bbwt_gather", N * 6);  // SA 4 + prevc 1 + out 1
-            launch_bbwt_gather(geo, c->get<u32>("SA", N), prevc, out, c->active);
+            launch_bbwt_gather(geo, SA, prevc, out, c->active);
         }
         st.cyc_rounds = cyc.rounds;
         st.cyc_active = cyc.active;
@@ -1007,6 +1049,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         KOLM_HIP_CHECK(hipEventRecord(ej[1], ms));
     };
     u8* bw = nullptr;
+    P.early_gather = !serial && !want_rp;  // the third stream is free for the early BBWT gather
     if (overlap >= 2 && !serial) {
         // the LZ77 parse (latency-bound) waits for round 0 of the cyclic sort and then runs
         // beside the doubling rounds; the 3-gram index runs beside Lyndon + round 0
@@ -1021,6 +1064,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         c->active = s;
         bw = P.cyclic();
     }
+    P.early_gather = false;
     // per-block doubling rounds of the omega-order sort (R per block)
     KOLM_HIP_CHECK(hipMemcpyAsync(c->h_cnt + H_RSUM, c->get<u64>("rsum", 1), sizeof(u64), hipMemcpyDeviceToHost, s));
     KOLM_HIP_CHECK(hipEventRecord(ev[1], s));
@@ -1271,6 +1315,7 @@ int ctx_create(int device, kolm_ctx** out) {
         c->serial = getenv("KOLM_SERIAL") && atoi(getenv("KOLM_SERIAL")) != 0;
         for (auto& e : c->evj) KOLM_HIP_CHECK(hipEventCreate(&e));
         for (auto& e : c->evr) KOLM_HIP_CHECK(hipEventCreate(&e));
+        for (auto& e : c->evg) KOLM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_cnt, sizeof(u32) * H_N, hipHostMallocDefault));
         for (auto& e : c->ev) KOLM_HIP_CHECK(hipEventCreate(&e));
         *out = c.release();
@@ -1390,6 +1435,7 @@ int kolm_ctx_destroy(kolm_ctx* c) {
         for (auto& e : c->ev) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evj) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evr) KOLM_HIP_CHECK(hipEventDestroy(e));
+        for (auto& e : c->evg) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evpool) KOLM_HIP_CHECK(hipEventDestroy(e));
         KOLM_HIP_CHECK(hipHostFree(c->h_cnt));
         if (c->h_tail) KOLM_HIP_CHECK(hipHostFree(c->h_tail));

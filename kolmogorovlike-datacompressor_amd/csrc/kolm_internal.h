@@ -326,6 +326,12 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fsta
                    u32* stack, u32* fcount, u32* tile_tmp, hipStream_t s, KTimer* kt = nullptr);
 void launch_prevc(const Geom& geo, const u8* text, const u8* flag, Factors fac, u8* prevc, hipStream_t s);
 void launch_bbwt_gather(const Geom& geo, const u32* SA, const u8* prevc, u8* out, hipStream_t s);
+// early BBWT gather: bm[slot] bit = the slot lies in one of the *ncur_dev (<= bound) segments of cur;
+// the masked gather writes out[g] = prevc[SA[g]] for the slots whose bit is set
+u32 bbwt_early_round();
+void launch_mark_active(const Seg* cur, const u32* ncur_dev, u32 bound, u64* bm, hipStream_t s);
+void launch_bbwt_gather_masked(const Geom& geo, const u32* SA, const u8* prevc, u8* out, const u64* bm,
+                               hipStream_t s);
 
 // ---- k_lsd.hip: per-block LSD radix passes: round 0 of the cyclic sort ----
 u32 lsd_tiles(const Geom& geo);

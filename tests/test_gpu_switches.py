@@ -11,6 +11,8 @@ payload with the oracle (PY:351-423 BBWT order, PY:460 MTF, PY:1413 Rice, PY:235
   KOLM_DUVAL_GRP=0  Duval span merges a thread per merge (a wave from level 4096)
   KOLM_MTF_WAVE=0   the per-thread MTF replay (and its SWAR Rice sums) on batches of few blocks,
                     with chunks of 128..512 bytes and ragged block ends
+  KOLM_EARLY_GATHER=0/1/2  one BBWT gather after the rounds / the early gather on the third stream
+                    from doubling round 1 / 2 on, the slots of that round's segments again after them
 """
 import pytest
 
@@ -28,6 +30,9 @@ SWITCHES = [
     {"KOLM_MTF_CP": "0"},
     {"KOLM_DUVAL_GRP": "0"},
     {"KOLM_MTF_WAVE": "0"},
+    {"KOLM_EARLY_GATHER": "0"},
+    {"KOLM_EARLY_GATHER": "1"},
+    {"KOLM_EARLY_GATHER": "2"},
 ]
 
 
