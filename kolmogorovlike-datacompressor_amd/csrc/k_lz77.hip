@@ -614,9 +614,17 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
             }
             for (u32 i = h + ((n - min(h, n)) & ~15u) + lane; i < n; i += 64) win[i] = z.text[tlo + i];
         } else if (((uintptr_t)z.text & 3) == 0) {
+            // 4 dwords per lane in flight before their LDS stores (one wave copies ~5 KB: the
+            // one-dword loop waited a round trip per dword, ~13 us per window)
             const u32* src = reinterpret_cast<const u32*>(z.text + tlo);
             u32* dst = reinterpret_cast<u32*>(win);
-            for (u32 i = lane; i < n / 4; i += 64) dst[i] = src[i];
+            const u32 nd = n / 4;
+            u32 i = lane;
+            for (; i + 192 < nd; i += 256) {
+                const u32 v0 = src[i], v1 = src[i + 64], v2 = src[i + 128], v3 = src[i + 192];
+                dst[i] = v0, dst[i + 64] = v1, dst[i + 128] = v2, dst[i + 192] = v3;
+            }
+            for (; i < nd; i += 64) dst[i] = src[i];
             for (u32 i = (n & ~3u) + lane; i < n; i += 64) win[i] = z.text[tlo + i];
         } else {
             for (u32 i = lane; i < n; i += 64) win[i] = z.text[tlo + i];
@@ -630,6 +638,20 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
     const LText t{z.text, win, wlo & ~3u, whi};
     const u32 maxl = end - q;
     const u32 capl = min((u32)LZ_CAP, maxl);
+    // 8-byte candidate compares in the 5 KB-window form (the 62 KiB form keeps byte compares:
+    // with them ROCm's gfx950 backend emits an invalid V_CMP on src_shared_base there)
+    constexpr bool V8 = !HF;
+    // 8 bytes at y (little-endian; 0 past the block end): the LDS window when they lie in it
+    const u32 wl = wlo & ~3u, wh = whi;
+    auto tx8 = [&](u32 y) -> u64 {
+        if (y >= wl && y + 8 <= wh) return lds8(win, y - wl);
+        if (y + 12 <= end) return glob8(z.text, y);
+        u64 v = 0;
+        for (u32 k = 0; k < 8; ++k)
+            if (y + k < end) v |= (u64)z.text[y + k] << (8 * k);
+        return v;
+    };
+    const u64 qv = V8 ? tx8(q) : 0ull;  // q's first 8 bytes
     const u8 c0 = t[q], c1 = t[q + 1], c2 = t[q + 2];
     u32 best = 0, bd = 0;
     const u32 hlo = q - dmax, hn = min(end, q + dmax) - hlo;  // fingerprints over [hlo, hlo + hn]
@@ -663,6 +685,7 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
         const bool hfm = HF && best > 2 * LZ_CAP;
         bool ok;
         u32 l = 0;
+        u64 dx = 0;  // (non-fingerprint mode) x's first 8 bytes ^ q's
         if (hfm) {
             // inside the loop best + 1 < dmax, so x + best + 1 <= q + best + 1 <= hlo + hn
             if (!hbuilt) {
@@ -680,7 +703,15 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
             ok = d <= dmax && (hh[x + L - hlo] - hh[x - hlo]) * (hbd0 * blane) == hq;
             if (ok) l = capl;
         } else {
-            ok = d <= dmax && t[x] == c0 && t[x + 1] == c1 && t[x + 2] == c2;
+            ok = d <= dmax;
+            if (V8) {
+                if (ok) {
+                    dx = tx8(x) ^ qv;  // x + 8 <= q + 8: inside the window or the block
+                    ok = (dx & 0xFFFFFFull) == 0;  // the same 3-gram
+                }
+            } else {
+                ok = ok && t[x] == c0 && t[x + 1] == c1 && t[x + 2] == c2;
+            }
             if (ok && bd && d <= best + bd) ok = d % bd != 0;
             if (ok && best) ok = best < maxl && t[x + best] == t[q + best];
         }
@@ -694,9 +725,26 @@ __device__ void bf_match(const LzArgs& z, u8* win, u32& wlo, u32& whi, u32 q, u3
                 ok = ok && t[x + y] == t[q + y];
             }
         }
-        if (ok && !hfm) {
+        if (ok && !hfm && !V8) {
             l = LZ_MIN;
             while (l < capl && t[x + l] == t[q + l]) ++l;
+        } else if (ok && !hfm) {
+            // exact length up to capl, 8 bytes per step (x + l < q + l <= end: bytes read past
+            // the block end only lie beyond capl, which clamps them)
+            if (dx) {
+                l = (u32)(__ffsll((long long)dx) - 1) >> 3;
+            } else {
+                l = 8;
+                while (l < capl) {
+                    const u64 dl = tx8(x + l) ^ tx8(q + l);
+                    if (dl) {
+                        l += (u32)(__ffsll((long long)dl) - 1) >> 3;
+                        break;
+                    }
+                    l += 8;
+                }
+            }
+            l = min(l, capl);
         }
         // capped candidates in ascending distance, each extended by the whole wave unless it
         // cannot be strictly longer than the longest one so far (`bb`): that needs a match at
@@ -768,7 +816,36 @@ __global__ __launch_bounds__(64) void k_lz_stitch_l(LzArgs z) {
         const u32 fp_l = (have && nt_l) ? z.tok_pos[sl] : NONE;
         u32 o_first = 0, o_fix0 = 0, o_nfix = 0, o_fixb = 0, o_off = 0;
         const u32 kn = min(64u, nck - kb);
+        const u32 ex_prev = (u32)__shfl_up((int)ex_l, 1);  // the previous chunk's exit (lanes >= 1)
         for (u32 j = 0; j < kn; ++j) {
+            // Runs of chunks taken whole, lane-parallel: chunk l is taken whole when its first
+            // recorded token starts at its entry and its last token is resolved; inside a run the
+            // entry of chunk l is chunk l-1's exit, so a ballot finds the run and a scan gives
+            // every chunk's output offset (one serial step per chunk before: ~0.9 ms per batch)
+            if (z.stitch_runs) {
+                const u32 pred = lane == j ? entry : ex_prev;
+                const bool ok = lane >= j && lane < kn && !(ex_l & LZ_UNRES) && fp_l == pred;
+                const u64 bad = ~__ballot(ok) & (~0ull << j);
+                const u32 jn = min(kn, bad ? (u32)__ffsll((long long)bad) - 1 : 64u);
+                if (jn > j) {
+                    const bool inrun = lane >= j && lane < jn;
+                    const u32 bv = inrun ? by_l : 0u;
+                    const u32 incl = wave_incl_scan(bv, OpAddU(), 0u);
+                    const u32 nv = wave_reduce(inrun ? nt_l : 0u, OpAddU(), 0u);
+                    if (inrun) {
+                        o_first = 0;
+                        o_fix0 = base + fi;
+                        o_nfix = 0;
+                        o_fixb = 0;
+                        o_off = boff + incl - bv;
+                    }
+                    boff += (u32)__builtin_amdgcn_readlane((int)incl, 63);
+                    ntot += nv;
+                    entry = (u32)__builtin_amdgcn_readlane((int)ex_l, (int)(jn - 1));
+                    j = jn;
+                    if (j >= kn) break;
+                }
+            }
             const u32 s = base + ((kb + j) << z.cshift);
             const u32 e = min(s + CH, bend);
             const u32 nt = __builtin_amdgcn_readlane(nt_l, j), ex = __builtin_amdgcn_readlane(ex_l, j);

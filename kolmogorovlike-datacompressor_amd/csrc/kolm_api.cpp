@@ -782,6 +782,8 @@ struct Pipeline {
         z.nfix = c->get<u32>("counters", C_N) + C_NFIX;
         static const bool lz_prof = getenv("KOLM_LZ_PROF") && atoi(getenv("KOLM_LZ_PROF")) != 0;
         if (lz_prof) z.prof = c->get<u64>("lz_prof", 32);
+        const char* sr = getenv("KOLM_STITCH_RUNS");
+        z.stitch_runs = sr && atoi(sr) == 0 ? 0u : 1u;
         return z;
     }
 

@@ -469,6 +469,7 @@ struct LzArgs {
     u32 cshift;        // chunk = 1 << cshift bytes (LZL_CHUNK)
     u32* nfix;         // [1] fix-up tokens computed by the stitch (statistics)
     u64* prof;         // [8] optional k_lz_local phase clocks (KOLM_LZ_PROF=1), null = off
+    u32 stitch_runs;   // k_lz_stitch_l takes runs of whole chunks lane-parallel (KOLM_STITCH_RUNS=0: off)
 };
 void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr);
 const char* lz_spec_name();  // the speculative-parse kernel in use (timing / roofline)
