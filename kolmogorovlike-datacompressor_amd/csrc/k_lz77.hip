@@ -1020,8 +1020,12 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
     {
         // text window (LZL_NW + LZL_CAPX bytes per 4 KiB home: ~2.1 B per position) +
         // 16 B per token (added by the caller once the token count is known)
+        // lead-in bytes parsed before each chain's chunk (at most LZL_LEAD, the window's margin):
+        // 48 since the stitch's fix-up searches got cheaper (round 5, two A/B calls, profiles/r05/
+        // ab_lz_lead_*: 33.67-33.76 ms per step at 48 and 56 against 33.84-34.30 at 64; 32 and 40
+        // measured 34.09-34.44 and 34.18).  KOLM_LZ_LEAD overrides.
         static const u32 lead =
-            getenv("KOLM_LZ_LEAD") ? std::min<u32>(atoi(getenv("KOLM_LZ_LEAD")), LZL_LEAD) : LZL_LEAD;
+            getenv("KOLM_LZ_LEAD") ? std::min<u32>(atoi(getenv("KOLM_LZ_LEAD")), LZL_LEAD) : 48u;
         KScope k(kt, KT_LZPARSE, "k_lz_local", z.geo.N * 2);
         if (geom == 1)
             k_lz_local<8192, 8><<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb, lead);
