@@ -521,6 +521,230 @@ __global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
     }
 }
 
+// ULEB128 byte count of v (PY:111-124), branch-free
+__device__ inline u32 uleb_n(u32 v) {
+    return 1u + (v >= (1u << 7)) + (v >= (1u << 14)) + (v >= (1u << 21)) + (v >= (1u << 28));
+}
+
+// =====================================================================================
+// k_lz_chains: the same speculative parse as k_lz_local (same window, index, chunks,
+// lead-ins and token records, so k_lz_stitch_l and k_lz_emit are unchanged) with chains
+// that advance independently.  In k_lz_local the four chains of a wave step their tokens
+// together: a token step lasts as many candidate batches as the chain with the most
+// candidates needs (2.4 batches per step against 1.5 per token on text), and every step
+// pays the token setup once more.  Here one loop trip runs one candidate batch for every
+// chain with a token in progress, then finishes the tokens whose walk ended in that batch
+// and sets up those chains' next tokens, so a chain never waits for another chain's
+// candidates.  The bucket heads are flags in the index itself (bit 15 of A: the first slot
+// of a hash bucket), so a walk ends at the first flagged slot or at the first candidate
+// out of the 4096-byte window, with no bitmap scan per token.
+// =====================================================================================
+constexpr u32 LZC_HEAD = 0x8000u;   // A[slot] flag: first slot of its hash bucket
+constexpr u32 LZC_NOSLOT = 0x10000u;  // prefetched entry below slot 0 (treated as out of window)
+
+template <u32 HOME, u32 LPC>
+__global__ __launch_bounds__(256) void k_lz_chains(LzArgs z, u32 hpb, u32 lead) {
+    using G = LzlGeom<HOME, LPC>;
+    __shared__ __align__(16) u8 txt[G::TXT];
+    __shared__ __align__(16) u16 A[G::NW];
+    __shared__ __align__(16) u16 B[G::BW];  // islot of [ilo, he); the sort's histograms before it
+    __shared__ u32 sh[4];
+    u16* hist = B;
+    static_assert(sizeof(u16) * 4 * LZL_NBK <= sizeof(B), "histograms alias the islot array");
+    static_assert(G::NW <= 0x3FFFu + 1u, "window offsets below the head flag");
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u32 b = blockIdx.x / hpb, h = blockIdx.x - b * hpb;
+    const u32 base = z.geo.base(b), end = z.geo.end(b);
+    const u32 hs = base + h * HOME;
+    if (hs >= end) return;
+    const u32 he = min(hs + HOME, end);
+    const u32 lo = hs - base > (u32)(LZ_WINDOW + LZL_LEAD) ? hs - LZ_WINDOW - LZL_LEAD : base;
+    const u32 ilo = hs - base > (u32)LZL_LEAD ? hs - LZL_LEAD : base;
+    const u32 hi = min(end, he + (u32)LZL_CAPX);
+    const u32 tlo = lo & ~3u;
+    u64 t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+    if (z.prof) t0 = wall_clock64();
+    {
+        const u32 n = hi - tlo;
+        if (((uintptr_t)z.text & 3) == 0) {
+            const u32* src = reinterpret_cast<const u32*>(z.text + tlo);
+            u32* dst = reinterpret_cast<u32*>(txt);
+            for (u32 i = tid; i < n / 4; i += 256) dst[i] = src[i];
+            for (u32 i = (n & ~3u) + tid; i < n; i += 256) txt[i] = z.text[tlo + i];
+        } else {
+            for (u32 i = tid; i < n; i += 256) txt[i] = z.text[tlo + i];
+        }
+    }
+    __syncthreads();
+    const u32 lim3 = end - base >= 3 ? end - 2 : base;
+    const u32 top = min(he, lim3);
+    const u32 nw = top > lo ? top - lo : 0u;
+    const u8* tw = txt + (lo - tlo);
+    if (z.prof) t1 = wall_clock64();
+    u16* isl = B;
+    if (nw) {
+        lzl_bucket<G::PER>(tw, A, nw, hist, sh);
+        // flag the first slot of every non-empty bucket (wave 3's offsets are the bucket ends)
+        for (u32 d = tid; d < LZL_NBK; d += 256) {
+            const u32 e = hist[3 * LZL_NBK + d], st = d ? hist[3 * LZL_NBK + d - 1] : 0u;
+            if (e > st) A[st] = (u16)(A[st] | LZC_HEAD);
+        }
+        __syncthreads();  // the islot writes below overwrite the histograms
+    }
+    for (u32 j = tid; j < nw; j += 256) {
+        const u32 x = A[j] & 0x7FFFu;
+        if (lo + x >= ilo) isl[lo + x - ilo] = (u16)j;
+    }
+    if (z.prof) t2 = wall_clock64();
+    __syncthreads();
+    if (z.prof) t3 = wall_clock64();
+
+    const u32 hl = lane & (LPC - 1);
+    const u64 GM = grp_mask<LPC>(lane);
+    const u32 gb = lane & (64 - LPC);                     // the chain's first lane
+    const u64 below = ((1ull << hl) - 1ull) << gb;        // lanes of the chain before this one
+    const u32 cid = w * G::CPW + lane / LPC;
+    const u32 s = hs + cid * LZL_CHUNK;
+    const bool has = s < end;
+    const u32 e = has ? min(s + (u32)LZL_CHUNK, end) : 0u;
+    const u32 c = b * z.cpb + h * G::NCHAIN + cid;
+    const u32 lend = has ? min(end, e + (u32)LZL_CAPX) : 0u;
+    const WinText T{txt, tlo};
+    u32 p = has ? ((cid == 0 && hs == base) ? s : s - lead) : 0u;
+    bool alive = has && p < e, walk = false;
+    u32 k = 0, qa = LZC_NOSLOT, best = 0, bd = 0, lim = 0, capl = 0;
+    u64 pv = 0;
+    u32 ntok = 0, off = 0, nlong = 0, nbuf = 0, nstep = 0, nbatch = 0;
+    u32 bpos = 0, blen = 0, bdist = 0, boff = 0;
+    bool un = false;
+    for (;;) {
+        // set up the next token of every chain that has none in progress
+        const bool need = alive && !walk;
+        if (__ballot(need)) {
+            if (need) {
+                best = 0;
+                bd = 0;
+                lim = lend - p;
+                capl = min((u32)LZ_CAP, lim);
+                k = p + (u32)LZ_MIN <= end ? (u32)isl[p - ilo] : 0u;
+                pv = lds8(txt, p - tlo);
+                qa = k > hl ? (u32)A[k - 1 - hl] : LZC_NOSLOT;
+                walk = true;
+            }
+        }
+        if (!__ballot(alive)) break;
+        ++nstep;
+        ++nbatch;
+        // one candidate batch per walking chain: slot k-1-hl (ascending distance)
+        const u32 qn = (walk && k > LPC + hl) ? (u32)A[k - LPC - 1 - hl] : LZC_NOSLOT;  // next batch
+        const u32 q = lo + (qa & 0x3FFFu);
+        const bool head = walk && (qa & LZC_HEAD);
+        const bool bad = walk && ((qa & LZC_NOSLOT) || p - q > (u32)LZ_WINDOW);
+        const u64 hm = __ballot(head) & GM, bm = __ballot(bad) & GM;
+        const bool valid = walk && !(hm & below) && !(bm & (below | (1ull << lane)));
+        u32 l = 0;
+        if (valid) {
+            const u32 qr = q - tlo;
+            const u64 d0 = pv ^ lds8(txt, qr);
+            if ((d0 & 0xFFFFFFull) == 0) {  // the same 3-gram, not only the same hash
+                if (d0) {
+                    l = (u32)(__ffsll((long long)d0) - 1) >> 3;
+                } else if (best < 8 || (best < lim && T[p + best] == T[q + best])) {
+                    const u32 pr = p - tlo;
+                    l = 8;
+#pragma unroll
+                    for (int kk = 1; kk < LZ_CAP / 8; ++kk) {
+                        if (l >= capl) break;
+                        const u64 d = lds8(txt, pr + 8 * kk) ^ lds8(txt, qr + 8 * kk);
+                        if (d) {
+                            l += (u32)(__ffsll((long long)d) - 1) >> 3;
+                            break;
+                        }
+                        l += 8;
+                    }
+                }
+                l = min(l, capl);
+            }
+        }
+        u64 longm = __ballot(valid && l >= capl && capl < lim);
+        while (longm) {
+            const u32 j = (u32)__ffsll((long long)longm) - 1;
+            const u32 pj = __builtin_amdgcn_readlane(p, j), qj = __builtin_amdgcn_readlane(q, j);
+            const u32 cj = __builtin_amdgcn_readlane(capl, j), mj = __builtin_amdgcn_readlane(lim, j);
+            const u32 lj = wave_lcp(T, pj, qj, cj, mj);
+            if (lane == j) l = lj;
+            longm &= longm - 1;
+            ++nlong;
+        }
+        const u32 key = grp_max<LPC>(valid && l >= (u32)LZ_MIN ? (l << 14) | (q - lo) : 0u);
+        if (walk && (key >> 14) > best) {
+            best = key >> 14;
+            bd = p - (lo + (key & 0x3FFFu));
+        }
+        qa = qn;
+        k = k > LPC ? k - LPC : 0u;
+        // a walk ends at its bucket's first slot, at the window's end or at a full-length match
+        const bool fin = walk && ((hm | bm) != 0 || best >= lim);
+        if (__ballot(fin)) {
+            if (fin) {
+                const u32 len = best >= (u32)LZ_MIN ? best : 0u;
+                const u32 dist = len ? bd : 0u;
+                un = un || (len && best >= lim && lim < end - p);
+                if (p >= s) {
+                    if (hl == nbuf) {
+                        bpos = p;
+                        blen = len;
+                        bdist = dist;
+                        boff = off;
+                    }
+                    if (++nbuf == LPC) {
+                        const u32 slot = s + ntok + 1 - LPC + hl;
+                        z.tok_pos[slot] = bpos;
+                        z.tok_len[slot] = blen;
+                        z.tok_dist[slot] = bdist;
+                        z.tok_off[slot] = boff;
+                        nbuf = 0;
+                    }
+                    ++ntok;
+                    off += len ? 1u + uleb_n(len) + uleb_n(dist) : 2u;
+                }
+                p += len ? len : 1u;
+                alive = p < e;
+                walk = false;
+            }
+        }
+    }
+    if (has && hl < nbuf) {
+        const u32 slot = s + ntok - nbuf + hl;
+        z.tok_pos[slot] = bpos;
+        z.tok_len[slot] = blen;
+        z.tok_dist[slot] = bdist;
+        z.tok_off[slot] = boff;
+    }
+    if (has && hl == 0) {
+        z.c_ntok[c] = ntok;
+        z.c_exit[c] = p | (un ? LZ_UNRES : 0u);
+        z.c_bytes[c] = off;
+    }
+    nlong = wave_reduce(nlong, OpAddU(), 0u);
+    if (lane == 0 && nlong) atomicAdd(z.nlong, nlong);
+    if (z.prof) {
+        if (lane == 0) {
+            atomicAdd(z.prof + 4, (u64)nstep);
+            atomicAdd(z.prof + 5, (u64)nbatch);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const u64 t4 = wall_clock64();
+            atomicAdd(z.prof + 0, t1 - t0);
+            atomicAdd(z.prof + 1, t2 - t1);
+            atomicAdd(z.prof + 2, t3 - t2);
+            atomicAdd(z.prof + 3, t4 - t3);
+            atomicAdd(z.prof + 6, (u64)1);
+        }
+    }
+}
+
 // Exact longest match at q (PY:1686-1708 semantics: ascending distance, strictly longer
 // wins, unbounded length) by brute force over the window, from an LDS copy of the text
 // [wlo, whi) refreshed when q's window is not inside it.  One wave.
@@ -1027,7 +1251,10 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
         static const u32 lead =
             getenv("KOLM_LZ_LEAD") ? std::min<u32>(atoi(getenv("KOLM_LZ_LEAD")), LZL_LEAD) : 48u;
         KScope k(kt, KT_LZPARSE, "k_lz_local", z.geo.N * 2);
-        if (geom == 1)
+        static const int chains = getenv("KOLM_LZ_CHAINS") ? atoi(getenv("KOLM_LZ_CHAINS")) : 1;
+        if (chains && geom != 1)
+            k_lz_chains<4096, 16><<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb, lead);
+        else if (geom == 1)
             k_lz_local<8192, 8><<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb, lead);
         else
             k_lz_local<4096, 16><<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb, lead);

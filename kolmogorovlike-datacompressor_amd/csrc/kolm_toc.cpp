@@ -365,45 +365,75 @@ int kolm_toc_read(const uint8_t* buf, uint64_t n, uint32_t* fields, uint64_t* pa
             return KOLM_ECAP;
         }
         const u64 n_runs = hd.uleb(), K = hd.uleb();
-        // a prefix code over at most 65535 runs is at most 32 deep (Fibonacci weights), so
-        // longer code lengths are rejected (and canonical() never shifts by 64)
-        std::vector<Code> codes;
+        // PY keeps the code lengths as read, of any size, and numbers the codes with Python
+        // integers (PY:1302-1311, 1318-1329).  Lengths here are u64 and the code values are
+        // never formed: decoding tracks d = (bits read so far) - (first code of that length),
+        // below.  A repeated symbol keeps its last length (dict semantics).
+        struct LCode {
+            u64 sym, len;
+        };
+        std::vector<LCode> codes;
         std::unordered_map<u64, size_t> at;
         for (u64 i = 0; i < K; ++i) {
             const u64 sym = hd.uleb(), len = hd.uleb();
-            if (len > 32) throw Fail{"Huffman code length out of range"};
             const auto it = at.find(sym);
-            if (it != at.end()) {  // a repeated symbol keeps its last length (dict semantics)
-                codes[it->second].len = (u32)len;
+            if (it != at.end()) {
+                codes[it->second].len = len;
             } else {
                 at.emplace(sym, codes.size());
-                codes.push_back(Code{sym, (u32)len, 0});
+                codes.push_back(LCode{sym, len});
             }
         }
         const u64 k_runs = hd.uleb();
         const u64 tail = hd.uleb();  // FIXED: last block's length; CDC: k of the length deltas
         if (k_runs > 63 || (mode == 1 && tail > 63)) throw Fail{"Rice parameter out of range"};
-        canonical(codes);
-        // canonical decode table: the codes of length L are first[L] .. first[L] + cnt[L] - 1,
-        // their symbols codes[idx[L] ..] (sorted by (len, sym))
-        u64 first[33] = {}, cnt[33] = {}, idx[33] = {};
-        u32 maxlen = 0;
-        for (size_t i = codes.size(); i-- > 0;) {
-            const Code& c = codes[i];
-            if (!c.len) continue;
-            first[c.len] = c.bits, idx[c.len] = i, ++cnt[c.len];
-            maxlen = std::max(maxlen, c.len);
+        // canonical order (length, symbol), as PY's numbering walks it
+        std::sort(codes.begin(), codes.end(), [](const LCode& x, const LCode& y) {
+            return x.len != y.len ? x.len < y.len : x.sym < y.sym;
+        });
+        // lengths present: (L, count, index of the first code of length L); length-0 symbols
+        // take code numbers too (PY's counter runs over them) but never decode (PY reads from
+        // length 1 on)
+        struct Lvl {
+            u64 len, cnt, idx;
+        };
+        std::vector<Lvl> lv;
+        for (size_t i = 0; i < codes.size(); ++i) {
+            if (lv.empty() || lv.back().len != codes[i].len) lv.push_back(Lvl{codes[i].len, 0, i});
+            ++lv.back().cnt;
         }
+        const u64 maxlen = lv.empty() ? 0 : lv.back().len;
+        // PY numbers length L's codes nc_L .. nc_L + cnt_L - 1 with nc_(L+1) = 2 (nc_L + cnt_L)
+        // (over every L, cnt_L = 0 where no code has length L).  After reading L bits, value v_L,
+        // d_L = v_L - nc_L obeys d_(L+1) = 2 (d_L - cnt_L) + bit and a symbol decodes at the first
+        // L with 0 <= d_L < cnt_L.  Once d_L < 0 it stays negative; once d_L >= 2^40 (> 2 cnt_L)
+        // it only grows: no later length can match, and PY reads on to maxlen and fails.
         BitIn br{buf + bits_at, bit_bytes};
         std::vector<u64> syms;
+        const int64_t DBIG = (int64_t)1 << 40;
         for (u64 r = 0; r < n_runs; ++r) {
-            u64 v = 0;
+            int64_t d = 0;
+            u64 cntL = 0;  // cnt of the previous length
+            size_t li = 0;
             bool hit = false;
-            for (u32 L = 1; L <= maxlen && !hit; ++L) {
-                v = (v << 1) | br.bit();
-                if (cnt[L] && v - first[L] < cnt[L]) {
-                    syms.push_back(codes[idx[L] + (v - first[L])].sym);
-                    hit = true;
+            if (!lv.empty() && lv[0].len == 0) cntL = lv[0].cnt, li = 1;  // length 0 precedes length 1
+            for (u64 L = 1; L <= maxlen; ++L) {
+                d = 2 * (d - (int64_t)cntL) + (int64_t)br.bit();
+                cntL = 0;
+                if (li < lv.size() && lv[li].len == L) {
+                    cntL = lv[li].cnt;
+                    if (d >= 0 && (u64)d < cntL) {
+                        syms.push_back(codes[lv[li].idx + (u64)d].sym);
+                        hit = true;
+                        break;
+                    }
+                    ++li;
+                }
+                if (d < 0 || d >= DBIG) {
+                    // PY reads the rest of maxlen bits, then fails (or runs out of bits first)
+                    const u64 left = maxlen - L;
+                    if (left > 8 * (bit_bytes - (br.at >> 3))) throw Fail{"BitReader: out of data"};
+                    break;
                 }
             }
             if (!hit) throw Fail{"Huffman decode failed"};
