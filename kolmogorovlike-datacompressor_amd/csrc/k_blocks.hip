@@ -141,9 +141,9 @@ __global__ __launch_bounds__(WG) void k_fed(TileGeom tg, const u8* flag, const u
 
 // ---------------------------------------------------------------------------------
 // Parallel Duval (restates PY:326-349 exactly) in two levels.
-//   k_duval_span: one workgroup per DUVAL_SPAN-byte span of a block, staged in LDS.
+//   k_duval_span: one workgroup per 8 KiB span of a block (duval_span_bytes), staged in LDS.
 //     Every thread runs Duval on its DUVAL_CH-byte chunk, then the chunk factorizations
-//     are merged pairwise up a binary tree (8 levels) inside LDS; factor starts are kept
+//     are merged pairwise up a binary tree (6 levels) inside LDS; factor starts are kept
 //     as a bitmap.  Merge rule (concatenation of two factorizations): for Lyndon words
 //     x < y, xy is Lyndon, so pushing the right part's factors on the stack of the left
 //     part's factors and merging while stack[-2] < stack[-1] gives the (unique) Lyndon
@@ -153,9 +153,8 @@ __global__ __launch_bounds__(WG) void k_fed(TileGeom tg, const u8* flag, const u
 //     the same rule (comparisons read the text from global memory).
 // ---------------------------------------------------------------------------------
 constexpr u32 DUVAL_CH = 128;                 // bytes per thread
-constexpr u32 DUVAL_SPAN = DUVAL_CH * 256;    // bytes per workgroup (32 KiB)
 constexpr u32 DUVAL_PAD = 4;                  // LDS pad per chunk (bank spread)
-constexpr u32 DUVAL_WAVE_W = 4096;            // tree levels merged by whole waves (<= 4 merges; see duval_wave_w)
+constexpr u32 DUVAL_WAVE_W = 4096;            // tree levels merged by whole waves (from this width on)
 constexpr u32 DUVAL_PF = 64;                  // factors per span with a cached 32-byte prefix
 
 __device__ inline u32 lds_addr(u32 q) { return q + (q / DUVAL_CH) * DUVAL_PAD; }
@@ -1030,16 +1029,12 @@ __global__ __launch_bounds__(256) void k_bbwt_gather_m(Geom geo, const u32* SA, 
 
 }  // namespace
 
-// The doubling round after whose classification the early BBWT gather starts (KOLM_EARLY_GATHER,
-// read per call; 0: off).  Round 3 (text: ~0.2 % of the slots still active): one A/B call, two
-// runs each (profiles/r05/ab_early_gather_*): the sort stream ends 0.4 ms sooner (ms_sa 32.2 ->
-// 31.8 ms) while the step stays at 34.1-34.3 ms, bound by the LZ77 stream it joins; config 4's
-// shard 6.26 / 6.41 -> 6.20 / 6.23 ms.  Round 2 (~9 % active) costs more than it saves (35.0 ms:
-// its gather competes with round 2's sorts and the parse).
-u32 bbwt_early_round() {
-    const char* e = getenv("KOLM_EARLY_GATHER");
-    return e ? (u32)atoi(e) : 3u;
-}
+// The doubling round after whose classification the early BBWT gather starts.  Round 3 (text:
+// ~0.2 % of the slots still active): one A/B call, two runs each (profiles/r05/ab_early_gather_*):
+// the sort stream ends 0.4 ms sooner (ms_sa 32.2 -> 31.8 ms); config 4's shard 6.26 / 6.41 ->
+// 6.20 / 6.23 ms.  Round 2 (~9 % active) costs more than it saves (35.0 ms: its gather competes
+// with round 2's sorts and the parse).
+u32 bbwt_early_round() { return 3u; }
 
 void launch_mark_active(const Seg* cur, const u32* ncur_dev, u32 bound, u64* bm, hipStream_t s) {
     if (bound) k_mark_active<<<(bound + 255) / 256, 256, 0, s>>>(cur, ncur_dev, bound, bm);
@@ -1063,33 +1058,15 @@ u64* dprof_buf() {
 
 // Lyndon factorisation of every block (parallel Duval + merge) -> factor-start lists,
 // flags and FEd.
-// Bytes per Duval span: 8 KiB (64-thread workgroups, 4x as many as 32 KiB spans) for every batch:
-// the span pass's tree levels are latency-bound per workgroup, and the merge absorbs the extra
-// span factorisations in batches.  Config 5: span 1.82 -> 1.19 ms, merge 0.18 -> 0.41 ms, 8.82 ->
+// Bytes per Duval span: 8 KiB (64-thread workgroups) for every batch: the span pass's tree
+// levels are latency-bound per workgroup, and the merge absorbs the extra span factorisations
+// in batches.  Against 32 KiB spans: config 5 span 1.82 -> 1.19 ms, merge 0.18 -> 0.41 ms, 8.82 ->
 // 8.54 ms per call; 256 MiB text (two alternating A/B runs): Lyndon family 4.37 -> 3.94 ms, step
-// 37.08 -> 36.58 ms.  KOLM_DUVAL_SPAN = 32768 restores DUVAL_SPAN.
+// 37.08 -> 36.58 ms.  Every tree level merges with lane groups (span_less_grp; a thread per merge
+// measured slower, round 5), whole waves from level DUVAL_WAVE_W.
 u32 duval_span_bytes(const Geom& geo) {
     (void)geo;
-    static const u32 force = getenv("KOLM_DUVAL_SPAN") ? (u32)atoi(getenv("KOLM_DUVAL_SPAN")) : 0u;
-    return force == DUVAL_SPAN ? DUVAL_SPAN : DUVAL_CH * 64;
-}
-
-// First tree level of k_duval_span merged by whole waves (64-byte comparison steps, the level's
-// merges one after another) instead of a thread per merge (4-byte steps, merges in parallel).
-// Full batches keep the thread form up to 4 KiB (text: short factors, many independent merges
-// hide each other's latency); batches of few blocks are latency-bound per workgroup and long
-// factors (images, periodic data) make the 4-byte comparison chains the span's critical path.
-// KOLM_DUVAL_WAVE overrides (read per call).
-static u32 duval_wave_w(const Geom& geo) {
-    if (const char* e = getenv("KOLM_DUVAL_WAVE")) return std::max<u32>(DUVAL_CH, (u32)atoi(e));
-    (void)geo;
-    return DUVAL_WAVE_W;
-}
-// Lane groups per merge at every tree level (span_less_grp); KOLM_DUVAL_GRP=0: a thread per
-// merge below wave_w, a wave per merge from it (read per call)
-static u32 duval_grp() {
-    const char* e = getenv("KOLM_DUVAL_GRP");
-    return e && atoi(e) == 0 ? 0u : 1u;
+    return DUVAL_CH * 64;
 }
 
 void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fstart, uint4* fpre, u32* nfac,
@@ -1106,10 +1083,7 @@ void launch_lyndon(const Geom& geo, const u8* text, u8* flag, u8* FEd, u32* fsta
     KOLM_HIP_CHECK(hipMemsetAsync(flag, 0, geo.N, s));
     {
         KScope k(kt, KT_LYNDON, "k_duval_span", N);  // text once (+ 4 B per factor start)
-        if (span == DUVAL_SPAN)
-            k_duval_span<256><<<nch, 256, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, dprof_buf(), DUVAL_WAVE_W, duval_grp());
-        else
-            k_duval_span<64><<<nch, 64, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, dprof_buf(), duval_wave_w(geo), duval_grp());
+        k_duval_span<64><<<nch, 64, 0, s>>>(geo, cpb, text, fstart, fpre, nfac, dprof_buf(), DUVAL_WAVE_W, 1u);
     }
     {
         KScope k(kt, KT_LYNDON, "k_duval_merge", (u64)nch * 8);

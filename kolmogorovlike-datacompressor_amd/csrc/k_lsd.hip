@@ -297,74 +297,17 @@ __global__ __launch_bounds__(NP * WG) void k_lsd_scanp(LsdGeom g, u32* hist) {
     }
 }
 
-// Stable scatter of one tile by digit P: element order e = j*WG + tid; each wave ranks
-// its 64 elements per digit with ballots, per-wave counts are combined in (j, wave)
-// order.  SRC_KP reads the keys by position (positions implicit).
-// G: the pass writes Kg[position] as the key (the next digit set, gathered by position)
-// instead of the key it sorted by — the last pass of the 8-character sort's first half.
-template <int P, int SRC, int G>
-__global__ __launch_bounds__(WG) void k_lsd_scatter(LsdGeom g, const u32* Kin, const u32* Pin,
-                                                   u32* Kout, u32* Pout, const u32* Kg, const u32* hist) {
-    __shared__ u32 wcnt[WG / 64][256];
-    __shared__ u32 running[256];
-    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    u32 lo, hi, b;
-    if (!g.range(xcd_tile(), lo, hi, b)) return;
-    running[tid] = hist[(u64)xcd_tile() * 256 + tid];
-#pragma unroll
-    for (int i = 0; i < WG / 64; ++i) wcnt[i][tid] = 0;
-    __syncthreads();
-    const u64 lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (u32 j = 0; j < LSD_PT; ++j) {
-        const u32 i = lo + j * WG + tid;
-        const bool valid = i < hi;
-        u32 key = 0, pos = 0, dg = 0;
-        if (valid) {
-            if (SRC == SRC_KP) {
-                key = Kin[i];
-                pos = i;
-            } else {
-                key = Kin[i];
-                pos = Pin[i];
-            }
-            dg = digit<P>(key);
-        }
-        u64 m = __ballot(valid);
-#pragma unroll
-        for (u32 bit = 0; bit < 8; ++bit) {
-            const u64 bal = __ballot((dg >> bit) & 1u);
-            m &= ((dg >> bit) & 1u) ? bal : ~bal;
-        }
-        const u32 rank = __popcll(m & lt_mask);
-        if (valid && rank == 0) wcnt[w][dg] = __popcll(m);
-        __syncthreads();
-        if (valid) {
-            u32 pre = running[dg];
-            for (u32 q = 0; q < w; ++q) pre += wcnt[q][dg];
-            const u32 dst = pre + rank;
-            Kout[dst] = G ? Kg[pos] : key;
-            Pout[dst] = pos;
-        }
-        __syncthreads();
-        u32 add = 0;
-#pragma unroll
-        for (int q = 0; q < WG / 64; ++q) {
-            add += wcnt[q][tid];
-            wcnt[q][tid] = 0;
-        }
-        running[tid] += add;
-        __syncthreads();
-    }
-}
 
-// The same stable scatter with three barriers per tile instead of three per 256 elements:
-// wave w owns the contiguous quarter [lo + 1024 w, lo + 1024 (w + 1)) of the tile (64
+// Stable scatter of one tile by digit P with three barriers per tile (round 2 replaced a form
+// with three per 256 elements): wave w owns the contiguous quarter [lo + 1024 w, lo + 1024 (w + 1)) of the tile (64
 // elements per step, 16 steps, all held in registers).  Pass 1: every element's offset
 // among its wave's equal digits (ballot match; the digit's leader advances the wave's LDS
 // counter — a wave's LDS operations retire in order, so no barrier between steps).  Then
 // per digit the waves' counts become bases (tile base + counts of the lower waves), and
-// pass 2 writes every element to base + offset.  Same order as k_lsd_scatter: (wave, step,
-// lane) is tile order.
+// pass 2 writes every element to base + offset; (wave, step, lane) is tile order, so the
+// scatter is stable.  SRC_KP reads the keys by position (positions implicit).  G: the pass
+// writes Kg[position] as the key (the next digit set, gathered by position) instead of the
+// key it sorted by — the last pass of the 8-character sort's first half.
 // OUT: OUT_PK writes the packed word (digit 3 << 24 | position - block base), OUT_REC u64
 // records at Kout, OUT_PAIR (key, position) to Kout / Pout
 template <int P, int SRC, int G, int OUT = OUT_PAIR>
@@ -450,121 +393,6 @@ __global__ __launch_bounds__(WG) void k_lsd_scatter_w(LsdGeom g, const u32* Kin,
                 Kout[dst] = G ? kg[G ? j : 0] : key[j];
                 Pout[dst] = pos[j];
             }
-        }
-    }
-}
-
-// LSD pass without a histogram pass ("sweep"): every block is cut into S segments of 2^lt
-// tiles; one workgroup per (block, segment) walks its tiles in order with running per-digit
-// destinations in LDS (k_lsd_scatter_w's ranking per tile), so no per-tile histograms or scan
-// launch are needed.  The bases come from per-(block, segment) digit counts that the previous
-// pass (or k_keypos_r0, for the first) accumulated: while it scatters, every element also
-// counts the NEXT pass's digit (NM: 0 none, 1 digit P + 1 of the same key, 2 digit 0 of the
-// gathered key Kg) for the segment its destination slot falls in (LDS, one global atomic per
-// nonzero (segment, digit) per workgroup).
-constexpr u32 SW_SMAX = 8;  // segments per block (8 KB of next-digit counters: the kernel's 21 KB of
-                            // LDS still fits beside the LZ77 parse's 137.7 KB per CU)
-constexpr u32 LSD_TS = 12;
-static_assert((1u << LSD_TS) == LSD_T, "sweep segments are counted in 2^12-element tiles");
-template <int P, int SRC, int G, int NM>
-__global__ __launch_bounds__(WG) void k_lsd_sweep(LsdGeom g, u32 S, u32 lt, const u32* Kin, const u32* Pin, u32* Kout,
-                                                  u32* Pout, const u32* Kg, const u32* cin, u32* cout) {
-    __shared__ u32 wc[WG / 64][256];
-    __shared__ u32 running[256];
-    __shared__ u16 loc[LSD_T];
-    __shared__ u32 nc[NM ? SW_SMAX : 1][256];
-    __shared__ u32 sh[WG / 64];
-    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const u32 id = xcd_tile();  // (block, segment): one block's segments on one XCD
-    const u32 b = id / S, sg = id - b * S;
-    const u32 base = g.geo.base(b), bend = g.geo.end(b);
-    {
-        u32 tot = 0, pre = 0;
-        for (u32 q = 0; q < S; ++q) {
-            const u32 c = cin[((u64)b * S + q) * 256 + tid];
-            tot += c;
-            pre += q < sg ? c : 0u;
-        }
-        const u32 incl = wave_incl_scan(tot, OpAddU(), 0u);
-        if (lane == 63) sh[w] = incl;
-        __syncthreads();
-        u32 carry = 0;
-        for (u32 i = 0; i < w; ++i) carry += sh[i];
-        running[tid] = base + carry + incl - tot + pre;
-        if (NM) {
-            for (u32 q = 0; q < S; ++q) nc[q][tid] = 0;
-        }
-    }
-    const u32 k0 = sg << lt, k1 = min(g.tpb, (sg + 1) << lt);
-    const u64 lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    u16* lw = loc + w * (LSD_T / 4) + lane;
-    for (u32 kt = k0; kt < k1; ++kt) {
-        const u32 lo = base + kt * LSD_T;
-        if (lo >= bend) break;
-        const u32 hi = min(lo + LSD_T, bend);
-#pragma unroll
-        for (int i = 0; i < WG / 64; ++i) wc[i][tid] = 0;
-        u32 key[LSD_PT], pos[LSD_PT];
-        const u32 q0 = lo + w * (LSD_T / 4);
-#pragma unroll
-        for (u32 j = 0; j < LSD_PT; ++j) {
-            const u32 i = q0 + j * 64 + lane;
-            key[j] = 0;
-            pos[j] = 0;
-            if (i < hi) {
-                key[j] = Kin[i];
-                pos[j] = SRC == SRC_KP ? i : Pin[i];
-            }
-        }
-        u32 kg[G ? LSD_PT : 1];
-        if (G) {
-#pragma unroll
-            for (u32 j = 0; j < LSD_PT; ++j) kg[j] = q0 + j * 64 + lane < hi ? Kg[pos[j]] : 0u;
-        }
-        __syncthreads();
-#pragma unroll
-        for (u32 j = 0; j < LSD_PT; ++j) {
-            const bool valid = q0 + j * 64 + lane < hi;
-            const u32 dg = digit<P>(key[j]);
-            u64 m = __ballot(valid);
-#pragma unroll
-            for (u32 bit = 0; bit < 8; ++bit) {
-                const u64 bal = __ballot((dg >> bit) & 1u);
-                m &= ((dg >> bit) & 1u) ? bal : ~bal;
-            }
-            const u32 rank = __popcll(m & lt_mask);
-            const u32 pre = valid ? wc[w][dg] : 0u;
-            lw[j * 64] = (u16)(pre + rank);
-            if (valid && rank == 0) wc[w][dg] = pre + (u32)__popcll(m);
-        }
-        __syncthreads();
-        {
-            u32 acc = running[tid];
-#pragma unroll
-            for (int q = 0; q < WG / 64; ++q) {
-                const u32 c = wc[q][tid];
-                wc[q][tid] = acc;
-                acc += c;
-            }
-            running[tid] = acc;
-        }
-        __syncthreads();
-#pragma unroll
-        for (u32 j = 0; j < LSD_PT; ++j) {
-            if (q0 + j * 64 + lane < hi) {
-                const u32 dst = wc[w][digit<P>(key[j])] + lw[j * 64];
-                const u32 kout = G ? kg[G ? j : 0] : key[j];
-                Kout[dst] = kout;
-                Pout[dst] = pos[j];
-                if (NM) atomicAdd(&nc[(dst - base) >> (LSD_TS + lt)][NM == 2 ? digit<0>(kout) : digit<(P + 1) & 3>(kout)], 1u);
-            }
-        }
-        __syncthreads();
-    }
-    if (NM) {
-        for (u32 q = 0; q < S; ++q) {
-            const u32 v = nc[q][tid];
-            if (v) atomicAdd(&cout[((u64)b * S + q) * 256 + tid], v);
         }
     }
 }
@@ -914,15 +742,14 @@ __global__ __launch_bounds__(WG) void k_alpha_codes(const u32* pres, u8* code, u
 // append the next); positions whose C characters wrap inside their Lyndon factor (FEd <
 // C) are rebuilt from the factor record.
 // hist0 (optional): the first LSD pass's per-tile digit counts (digit 0 of KA), so that
-// pass needs no histogram kernel of its own; top: the counts of KB's top byte instead (the
-// first MSD digit of the MSD round 0, k_r0m.hip, which passes sh = 64 - C w).
+// pass needs no histogram kernel of its own.
 // part (0 .. min(sh, w)): the top `part` of the sh padding bits below the C codes hold the top
 // `part` bits of character C's code, so round 0 also splits positions tied on C characters by most of the next one;
 // the doubling rounds still start from h = C (groups equal on C characters and the partial one
 // refine consistently: doubling compares (group(p), group(p + h)), and group(p + h) orders
 // character h fully)
 __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32 C, u32 w, u32 sh, u32* KA, u32* KB,
-                                                  u32* hist0, u32 top, u32 segS = 0, u32 seglt = 0,
+                                                  u32* hist0,
                                                   ScanParts sp = ScanParts{}, u32 part = 0) {
     __shared__ __align__(16) u8 tx[LSD_T + 64];
     __shared__ u8 cd[256];
@@ -930,7 +757,7 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
     u32 lo, hi, b;
     const u32 tile = xcd_tile();
     if (!g.range(tile, lo, hi, b)) {  // a tile past its block's end (the whole workgroup)
-        if (hist0 && !segS) hist0[(u64)tile * 256 + threadIdx.x] = 0;
+        if (hist0) hist0[(u64)tile * 256 + threadIdx.x] = 0;
         return;
     }
     if (hist0) h0.clear();
@@ -1009,19 +836,14 @@ __global__ __launch_bounds__(WG) void k_keypos_r0(LsdGeom g, const u8* code, u32
     if (hist0) {
 #pragma unroll
         for (u32 e = 0; e < LSD_PT; ++e)
-            if (p0 + e < hi) h0.add(top ? kb[e] >> 24 : digit<0>(ka[e]));
+            if (p0 + e < hi) h0.add(digit<0>(ka[e]));
     }
     }
     if (hist0) {
         __syncthreads();
         const u32 v = h0.total(threadIdx.x);
-        if (!segS) {
-            hist0[(u64)tile * 256 + threadIdx.x] = v;
-            add_part_total(g, sp, tile, v);
-        } else if (v) {  // sweep passes: counts per (block, segment of 2^seglt tiles), zeroed by the host
-            const u32 seg = (tile - b * g.tpb) >> seglt;
-            atomicAdd(&hist0[((u64)b * segS + seg) * 256 + threadIdx.x], v);
-        }
+        hist0[(u64)tile * 256 + threadIdx.x] = v;
+        add_part_total(g, sp, tile, v);
     }
 }
 
@@ -1029,14 +851,9 @@ template <int P, int SRC, int G, int OUT>
 void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kout, u32* pout, const u32* kg,
               u32* hist, bool counted, hipStream_t s, KTimer* kt, const ScanParts& sp) {
     static const std::string hn = "k_lsd_hist<" + std::to_string(P) + ", " + std::to_string(SRC) + ">";
-    // A/B switch KOLM_LSD_SW: 0 = k_lsd_scatter everywhere, 1 = except the first pass (keys
-    // by position), 2 = k_lsd_scatter_w everywhere (default); the timer carries the launched name
-    static const int sw = getenv("KOLM_LSD_SW") ? atoi(getenv("KOLM_LSD_SW")) : 2;
-    const bool use_w = sw == 2 || (sw == 1 && SRC == SRC_PAIR);
-    static const std::string tail = "<" + std::to_string(P) + ", " + std::to_string(SRC) + ", " + std::to_string(G) +
-                                    (OUT ? ", " + std::to_string(OUT) + ">" : std::string(">"));
-    static const std::string sn_w = "k_lsd_scatter_w" + tail, sn_p = "k_lsd_scatter" + tail;
-    const std::string& sn = use_w ? sn_w : sn_p;
+    // the timer carries the launched name
+    static const std::string sn = "k_lsd_scatter_w<" + std::to_string(P) + ", " + std::to_string(SRC) + ", " +
+                                  std::to_string(G) + (OUT ? ", " + std::to_string(OUT) + ">" : std::string(">"));
     const u64 N = g.geo.N, H = (u64)nt * 1024;  // H: per-tile histogram bytes
     if (!counted) {  // counted: the producer of kin wrote the tile histograms
         KScope k(kt, KT_LSD, hn.c_str(), (SRC == SRC_REC ? 8 : 4) * N + H);
@@ -1067,49 +884,7 @@ void lsd_pass(const LsdGeom& g, u32 nt, const u32* kin, const u32* pin, u32* kou
         KScope k(kt, KT_LSD, sn.c_str(), (in + outb) * N + (G ? 4 * N : 0) + H);
         // k_lsd_scatter_w (three barriers per tile; 256 MiB text, overlapped: 1.5-1.7 -> 0.9-1.0
         // ms per pass)
-        if (use_w || OUT != OUT_PAIR || SRC == SRC_PK || SRC == SRC_REC)
-            k_lsd_scatter_w<P, SRC, G, OUT><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
-        else if constexpr (SRC != SRC_PK && SRC != SRC_REC)
-            k_lsd_scatter<P, SRC, G><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
-    }
-}
-
-// one sweep pass (k_lsd_sweep): nm = the next pass's digit mode (0 none, 1 P + 1, 2 digit 0 of Kg)
-template <int P, int SRC, int G, int NM>
-void sweep_one(const LsdGeom& g, u32 S, u32 lt, const u32* kin, const u32* pin, u32* kout, u32* pout, const u32* kg,
-               const u32* cin, u32* cout, hipStream_t s, KTimer* kt) {
-    static const std::string nm = "k_lsd_sweep<" + std::to_string(P) + ", " + std::to_string(SRC) + ", " +
-                                  std::to_string(G) + ", " + std::to_string(NM) + ">";
-    const u64 N = g.geo.N;
-    KScope k(kt, KT_LSD, nm.c_str(), (SRC == SRC_KP ? 12 : 16) * N + (G ? 4 * N : 0));
-    k_lsd_sweep<P, SRC, G, NM><<<g.geo.nb * S, WG, 0, s>>>(g, S, lt, kin, pin, kout, pout, kg, cin, cout);
-}
-template <int P, int SRC>
-void sweep_pg(int gat, int nm, const LsdGeom& g, u32 S, u32 lt, const u32* kin, const u32* pin, u32* kout, u32* pout,
-              const u32* kg, const u32* cin, u32* cout, hipStream_t s, KTimer* kt) {
-    if (gat) {
-        if constexpr (P == 3 && SRC == SRC_PAIR) sweep_one<P, SRC, 1, 2>(g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
-        return;
-    }
-    if (nm == 1) {
-        if constexpr (P < 3) sweep_one<P, SRC, 0, 1>(g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
-    } else {
-        sweep_one<P, SRC, 0, 0>(g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
-    }
-}
-void sweep_pass(int P, bool src_kp, bool gat, int nm, const LsdGeom& g, u32 S, u32 lt, const u32* kin, const u32* pin,
-                u32* kout, u32* pout, const u32* kg, const u32* cin, u32* cout, hipStream_t s, KTimer* kt) {
-    if (src_kp) {  // the first pass: keys by position
-        switch (P) {
-            case 0: return sweep_pg<0, SRC_KP>(gat, nm, g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
-            default: return;
-        }
-    }
-    switch (P) {
-        case 0: return sweep_pg<0, SRC_PAIR>(gat, nm, g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
-        case 1: return sweep_pg<1, SRC_PAIR>(gat, nm, g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
-        case 2: return sweep_pg<2, SRC_PAIR>(gat, nm, g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
-        default: return sweep_pg<3, SRC_PAIR>(gat, nm, g, S, lt, kin, pin, kout, pout, kg, cin, cout, s, kt);
+        k_lsd_scatter_w<P, SRC, G, OUT><<<nt, WG, 0, s>>>(g, kin, pin, kout, pout, kg, hist);
     }
 }
 
@@ -1151,15 +926,6 @@ void run_pass(int P, bool src_kp, bool gat, const LsdGeom& g, u32 nt, const u32*
 }  // namespace
 
 u32 lsd_tiles(const Geom& geo) { return (geo.bs + LSD_T - 1) / LSD_T * geo.nb; }
-
-// MSD round 0 (k_r0m.hip): the keys left-aligned in 64 bits by position (KL = low word, KH =
-// high word) and the per-LSD-tile counts of KH's top byte
-void launch_r0_keys64(const Geom& geo, const R0Bufs& t, u32* KL, u32* KH, u32* hist, hipStream_t s, KTimer* kt) {
-    LsdGeom g{geo, (geo.bs + LSD_T - 1) / LSD_T, t.text, t.FEd, t.fac};
-    const u32 nt = g.tpb * geo.nb;
-    KScope k(kt, KT_KEYGEN, "k_keypos_r0", geo.N * 10);
-    k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, 64 - t.chars * t.w, KL, KH, hist, 1);
-}
 
 // Per-block code tables (alphabet compaction); returns the max code width w of the batch
 // (one host round trip).  compact = false: identity codes, w = 8.
@@ -1207,41 +973,11 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
     u32* S[2] = {t.SA, t.SA2};
     const u32 T = pa + pb;
     int o = (T & 1) ? 0 : 1;  // output pair of the first pass: the last one lands in (K2, SA)
-    // KOLM_LSD_SWEEP=1: sweep passes (no histogram / scan launches; measured slower);
-    // default: per-tile histogram + scan + scatter launches
-    const char* swe = getenv("KOLM_LSD_SWEEP");
-    const bool sweep = swe && atoi(swe) != 0 && t.swc;
-    if (sweep) {
-        u32 lt = 0;
-        while (((g.tpb + (1u << lt) - 1) >> lt) > SW_SMAX) ++lt;
-        const u32 SS = (g.tpb + (1u << lt) - 1) >> lt;
-        const u64 cw = (u64)geo.nb * SS * 256;
-        u32* cnt[2] = {t.swc, t.swc + cw};
-        KOLM_HIP_CHECK(hipMemsetAsync(cnt[0], 0, sizeof(u32) * cw, s));
-        {
-            KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6));
-            k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, cnt[0], 0, SS, lt);
-        }
-        u32 pidx = 0;
-        for (u32 half = 0; half < 2; ++half) {
-            const u32 np = half ? pb : pa;
-            for (u32 q = 0; q < np; ++q, ++pidx) {
-                const bool first = half == 0 && q == 0, gat = half == 0 && q + 1 == pa && pb > 0;
-                const int nm = q + 1 < np ? 1 : (half == 0 && pb > 0 ? 2 : 0);
-                if (nm) KOLM_HIP_CHECK(hipMemsetAsync(cnt[(pidx + 1) & 1], 0, sizeof(u32) * cw, s));
-                sweep_pass((int)q, first, gat, nm, g, SS, lt, first ? t.RK : K[o ^ 1], first ? nullptr : S[o ^ 1], K[o],
-                           S[o], gat ? t.KP : nullptr, cnt[pidx & 1], cnt[(pidx + 1) & 1], s, kt);
-                o ^= 1;
-            }
-        }
-    } else {
-        // the padding bits carry the next character's top bits (KOLM_R0_PART = n: its top n bits
-        // only, 0: zero padding)
-        const char* pte = getenv("KOLM_R0_PART");
-        const u32 part = std::min(pte ? (u32)std::max(0, atoi(pte)) : 8u, std::min(sh, t.w));
-        // per-(block, part) totals for the one-part-long scans (KOLM_LSD_SCAN2=0: per-block scans)
-        const char* s2e = getenv("KOLM_LSD_SCAN2");
-        const bool parts = !(s2e && atoi(s2e) == 0) && t.swc && g.tpb > 1;
+    {
+        // the padding bits carry the next character's top bits
+        const u32 part = std::min(sh, t.w);
+        // per-(block, part) totals for the one-part-long scans
+        const bool parts = t.swc && g.tpb > 1;
         ScanParts sp[2];
         if (parts) {
             u32 plt = 0;
@@ -1257,16 +993,14 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
         {
             // text + FEd 2 (+ factor starts near factor ends), KA 4 (+ KB 4)
             KScope k(kt, KT_KEYGEN, "k_keypos_r0", N * (pb ? 10 : 6));
-            k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist, 0, 0, 0, spp(),
+            k_keypos_r0<<<nt, WG, 0, s>>>(g, t.code, t.chars, t.w, sh, t.RK, pb ? t.KP : nullptr, t.hist, spp(),
                                           part);
         }
         // the first half's passes 2 -> 3 exchange one packed word per element (digit 3 and the
-        // position inside the block) when a block position fits 24 bits (KOLM_LSD_PACK=0: off)
-        const char* pke = getenv("KOLM_LSD_PACK");
-        const bool pack = !(pke && atoi(pke) == 0) && pa == 4 && pb > 0 && geo.bs <= (1u << 24);
-        // record mode (KOLM_LSD_REC=0: off) for 8-byte keys: the pairs between passes as u64 records
-        const char* rce = getenv("KOLM_LSD_REC");
-        const bool rec = !(rce && atoi(rce) == 0) && pack && pb == 4 && t.rec[0] && t.rec[1];
+        // position inside the block) when a block position fits 24 bits
+        const bool pack = pa == 4 && pb > 0 && geo.bs <= (1u << 24);
+        // record mode for 8-byte keys: the pairs between passes as u64 records
+        const bool rec = pack && pb == 4 && t.rec[0] && t.rec[1];
         if (rec) {
             u32* R2[2] = {reinterpret_cast<u32*>(t.rec[0]), reinterpret_cast<u32*>(t.rec[1])};
             // inputs / outputs per pass: KA -> R0 -> R1 -> K22 (packed) -> R0 -> R1 -> R0 -> R1 -> (K2, SA)
@@ -1291,10 +1025,9 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
             ++pidx;
         }
     }
-    // RK through position windows (k_r0_rk) when every block has at most 256 of them;
-    // KOLM_R0F_WIN=0: the direct scatter
-    static const bool win_ok = !(getenv("KOLM_R0F_WIN") && atoi(getenv("KOLM_R0F_WIN")) == 0);
-    const bool win = win_ok && geo.bs <= 256 * R0_WIN;
+    // RK through position windows (k_r0_rk) when every block has at most 256 of them, else
+    // the direct scatter
+    const bool win = geo.bs <= 256 * R0_WIN;
     {
         // K 4 (+ SA 4 + the KA gather 4) read, head masks written
         KScope k(kt, KT_LSD, "k_r0_tile_heads", (pb || win ? 12 : 4) * N);
@@ -1328,11 +1061,9 @@ void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u
     {
         // SA 4 read, RK 4 scattered (+ head masks, 8 B per new segment)
         KScope k(kt, KT_LSD, "k_r0_final", 8 * N);
-        // A/B switches: KOLM_R0F_PARTS position windows per block, KOLM_R0F_XCD tile mapping
-        // (default: two windows on XCD-contiguous tiles, 256 MiB text 3.24 -> 2.42 ms per step)
-        static const u32 parts = getenv("KOLM_R0F_PARTS") ? std::max(1, atoi(getenv("KOLM_R0F_PARTS"))) : 2u;
-        static const u32 xcd = getenv("KOLM_R0F_XCD") ? (u32)atoi(getenv("KOLM_R0F_XCD")) : 1u;
-        static const u32 ntl = getenv("KOLM_R0F_NT") ? (u32)atoi(getenv("KOLM_R0F_NT")) : 0u;
+        // two position windows per block on XCD-contiguous tiles (256 MiB text 3.24 -> 2.42 ms per
+        // step against one window)
+        constexpr u32 parts = 2, xcd = 1, ntl = 0;
         const u32 step = (geo.bs + parts - 1) / parts;
         for (u32 q = 0; q < parts; ++q)
             k_r0_final<<<nt, WG, 0, s>>>(g, t.HF, t.SA, t.cmax, t.cmin, t.RK, next, next_cnt, blk_split, q * step,

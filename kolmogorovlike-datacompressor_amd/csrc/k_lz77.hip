@@ -177,9 +177,10 @@ struct LzlGeom {
     static constexpr u32 ISL = HOME + LZL_LEAD;             // islot entries [hs - LEAD, he)
     static constexpr u32 NCHAIN = HOME / LZL_CHUNK;
     static constexpr u32 CPW = 64 / LPC;                    // chains per wave
-    static constexpr u32 BW = ISL + 4 * ((NW + 63) / 64);   // B: islot + head bitmap (u16 words)
-    static constexpr u32 PER = (NW + 255) / 256;            // window elements per lane in the sort
-    static_assert(NCHAIN == 4 * CPW, "4 waves of 64 / LPC chains");
+    static constexpr u32 NWV = NCHAIN / CPW;                // waves per workgroup
+    static constexpr u32 NT = 64 * NWV;                     // threads per workgroup
+    static constexpr u32 PER = (NW + NT - 1) / NT;          // window elements per lane in the sort
+    static_assert(NCHAIN % CPW == 0, "whole waves of 64 / LPC chains");
     static_assert(NW < (1u << 14), "window offsets in 14 bits (the winner key)");
 };
 
@@ -210,11 +211,12 @@ __device__ inline u32 hash3(const u8* t, u32 x) {
 // is needed between its steps).
 // hist: [4][LZL_NBK] 16-bit counters / offsets (window positions < 2^16; a count is added
 // to its dword with the half's shift, plain 16-bit stores otherwise)
-template <u32 PER>
+template <u32 PER, u32 NWV = 4>
 __device__ void lzl_bucket(const u8* t, u16* A, u32 nw, u16* hist, u32* sh) {
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    constexpr u32 R = LZL_NBK / 256;  // buckets per thread in the scan
-    const u32 Q = (nw + 3) / 4;
+    constexpr u32 NT = 64 * NWV;
+    constexpr u32 R = (LZL_NBK + NT - 1) / NT;  // buckets per thread in the scan
+    const u32 Q = (nw + NWV - 1) / NWV;
     const u32 b0 = min(w * Q, nw), b1 = min(b0 + Q, nw);
     u32 hv[PER];
 #pragma unroll
@@ -222,7 +224,7 @@ __device__ void lzl_bucket(const u8* t, u16* A, u32 nw, u16* hist, u32* sh) {
         const u32 e = b0 + k * 64 + lane;
         hv[k] = e < b1 ? hash3(t, e) : 0u;
     }
-    for (u32 i = tid; i < 2 * LZL_NBK; i += 256) reinterpret_cast<u32*>(hist)[i] = 0;
+    for (u32 i = tid; i < NWV * LZL_NBK / 2; i += NT) reinterpret_cast<u32*>(hist)[i] = 0;
     __syncthreads();
 #pragma unroll
     for (u32 k = 0; k < PER; ++k)
@@ -230,12 +232,12 @@ __device__ void lzl_bucket(const u8* t, u16* A, u32 nw, u16* hist, u32* sh) {
             atomicAdd(reinterpret_cast<u32*>(hist) + ((w * LZL_NBK + hv[k]) >> 1), 1u << (16 * (hv[k] & 1)));
     __syncthreads();
     {
-        u32 h[4][R], tot = 0;
+        u32 h[NWV][R], tot = 0;
 #pragma unroll
         for (u32 r = 0; r < R; ++r)
 #pragma unroll
-            for (u32 q = 0; q < 4; ++q) {
-                h[q][r] = hist[q * LZL_NBK + tid * R + r];
+            for (u32 q = 0; q < NWV; ++q) {
+                h[q][r] = tid * R + r < LZL_NBK ? hist[q * LZL_NBK + tid * R + r] : 0u;
                 tot += h[q][r];
             }
         const u32 incl = wave_incl_scan(tot, OpAddU(), 0u);
@@ -246,8 +248,8 @@ __device__ void lzl_bucket(const u8* t, u16* A, u32 nw, u16* hist, u32* sh) {
 #pragma unroll
         for (u32 r = 0; r < R; ++r)
 #pragma unroll
-            for (u32 q = 0; q < 4; ++q) {
-                hist[q * LZL_NBK + tid * R + r] = (u16)ex;
+            for (u32 q = 0; q < NWV; ++q) {
+                if (tid * R + r < LZL_NBK) hist[q * LZL_NBK + tid * R + r] = (u16)ex;
                 ex += h[q][r];
             }
     }
@@ -273,14 +275,6 @@ __device__ void lzl_bucket(const u8* t, u16* A, u32 nw, u16* hist, u32* sh) {
     __syncthreads();
 }
 
-// first slot of slot k's hash bucket (slot 0 is always a head)
-__device__ inline u32 lzl_gs(const u64* bm, u32 k) {
-    u32 wi = k >> 6;
-    u64 m = bm[wi] & (~0ull >> (63 - (k & 63)));
-    while (!m) m = bm[--wi];
-    return wi * 64 + 63 - (u32)__clzll(m);
-}
-
 // the lanes of this lane's chain (LPC consecutive lanes)
 template <u32 LPC>
 __device__ inline u64 grp_mask(u32 lane) { return ((1ull << LPC) - 1ull) << (lane & (64 - LPC)); }
@@ -301,236 +295,14 @@ __device__ inline u32 grp_max(u32 v) {
     return v;
 }
 
-// Longest match at p for this lane's 16-lane chain (act: the chain has a position to
-// score).  Exact up to lim = min(block end, chunk end + LZL_CAPX) - p (<= 576): unres when
-// the best candidate reaches lim short of the block end.
-template <u32 LPC>
-__device__ void lzl_best(const u8* txt, u32 tlo, const u16* A, const u64* bm, const u16* isl, u32 lo, u32 ilo,
-                         bool act, u32 p, u32 lim, u32 end, u32& out_len, u32& out_dist, bool& unres, u32& nlong,
-                         u32& nbatch) {
-    const u32 lane = threadIdx.x & 63, hl = lane & (LPC - 1);
-    const u64 GM = grp_mask<LPC>(lane);
-    const WinText T{txt, tlo};
-    u32 best = 0, bd = 0;
-    bool go = act && p + (u32)LZ_MIN <= end;
-    u32 k0 = 0, gs = 0, qa = 0;
-    if (go) {
-        k0 = isl[p - ilo];
-        qa = k0 > hl ? (u32)A[k0 - 1 - hl] : 0u;  // first batch, issued beside the bitmap load
-        gs = lzl_gs(bm, k0);
-        go = k0 > gs;
-    }
-    const u32 capl = min((u32)LZ_CAP, lim);
-    const u32 pr = p - tlo;
-    const u64 pv = go ? lds8(txt, pr) : 0ull;  // p's first 8 bytes, once per token
-    while (__ballot(go)) {
-        ++nbatch;
-        const u32 qn = (go && k0 > LPC + hl) ? (u32)A[k0 - LPC - 1 - hl] : 0u;  // next batch
-        bool valid = go && k0 > gs + hl;
-        const u32 q = lo + qa;
-        valid = valid && (p - q <= (u32)LZ_WINDOW);
-        const u64 inwin = __ballot(valid) & GM;
-        u32 l = 0;
-        if (valid) {
-            const u32 qr = q - tlo;
-            const u64 d0 = pv ^ lds8(txt, qr);
-            if ((d0 & 0xFFFFFFull) == 0) {  // same 3-gram (not just the same hash)
-                if (d0) {
-                    l = (u32)(__ffsll((long long)d0) - 1) >> 3;
-                } else if (best < 8 || (best < lim && T[p + best] == T[q + best])) {
-                    // a longer candidate must match at `best`
-                    l = 8;
-#pragma unroll
-                    for (int k = 1; k < LZ_CAP / 8; ++k) {
-                        if (l >= capl) break;
-                        const u64 d = lds8(txt, pr + 8 * k) ^ lds8(txt, qr + 8 * k);
-                        if (d) {
-                            l += (u32)(__ffsll((long long)d) - 1) >> 3;
-                            break;
-                        }
-                        l += 8;
-                    }
-                }
-                l = min(l, capl);
-            }
-        }
-        // capped candidates extended exactly (up to lim), one at a time by the whole wave
-        u64 longm = __ballot(l >= capl && capl < lim);
-        while (longm) {
-            const u32 j = (u32)__ffsll((long long)longm) - 1;
-            const u32 pj = __builtin_amdgcn_readlane(p, j), qj = __builtin_amdgcn_readlane(q, j);
-            const u32 cj = __builtin_amdgcn_readlane(capl, j), mj = __builtin_amdgcn_readlane(lim, j);
-            const u32 lj = wave_lcp(T, pj, qj, cj, mj);
-            if (lane == j) l = lj;
-            longm &= longm - 1;
-            ++nlong;
-        }
-        // max length, ties -> largest position (= smallest distance): one 28-bit key per
-        // lane (length <= 576 < 2^14, window offset < 2^14), maximised over the DPP row
-        const u32 key = grp_max<LPC>(l >= (u32)LZ_MIN ? (l << 14) | (q - lo) : 0u);
-        if ((key >> 14) > best) {
-            best = key >> 14;
-            bd = p - (lo + (key & 0x3FFFu));
-        }
-        if (best >= lim || inwin != GM) go = false;
-        qa = qn;
-        k0 -= LPC;
-    }
-    unres = false;
-    if (best < (u32)LZ_MIN) {
-        best = 0;
-        bd = 0;
-    } else {
-        unres = best >= lim && lim < end - p;
-    }
-    out_len = best;
-    out_dist = bd;
-}
-
-template <u32 HOME, u32 LPC>
-__global__ __launch_bounds__(256) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
-    using G = LzlGeom<HOME, LPC>;
-    __shared__ __align__(16) u8 txt[G::TXT];
-    __shared__ __align__(16) u16 A[G::NW];
-    // islot of [ilo, he) + head bitmap; the sort's histograms live here before them
-    __shared__ __align__(16) u16 B[G::BW];
-    __shared__ u32 sh[4];
-    u16* hist = B;  // the counting sort's 16-bit histograms (dead once the islot array is written)
-    static_assert(sizeof(u16) * 4 * LZL_NBK <= sizeof(B), "histograms alias the islot array + bitmap");
-    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const u32 b = blockIdx.x / hpb, h = blockIdx.x - b * hpb;
-    const u32 base = z.geo.base(b), end = z.geo.end(b);
-    const u32 hs = base + h * HOME;
-    if (hs >= end) return;
-    const u32 he = min(hs + HOME, end);
-    const u32 lo = hs - base > (u32)(LZ_WINDOW + LZL_LEAD) ? hs - LZ_WINDOW - LZL_LEAD : base;
-    const u32 ilo = hs - base > (u32)LZL_LEAD ? hs - LZL_LEAD : base;
-    const u32 hi = min(end, he + (u32)LZL_CAPX);
-    const u32 tlo = lo & ~3u;  // LDS origin (dword aligned)
-    u64 t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-    if (z.prof) t0 = wall_clock64();
-    {
-        const u32 n = hi - tlo;
-        if (((uintptr_t)z.text & 3) == 0) {
-            const u32* src = reinterpret_cast<const u32*>(z.text + tlo);
-            u32* dst = reinterpret_cast<u32*>(txt);
-            for (u32 i = tid; i < n / 4; i += 256) dst[i] = src[i];
-            for (u32 i = (n & ~3u) + tid; i < n; i += 256) txt[i] = z.text[tlo + i];
-        } else {
-            for (u32 i = tid; i < n; i += 256) txt[i] = z.text[tlo + i];
-        }
-    }
-    __syncthreads();
-    // 3-gram positions of the window: [lo, min(he, end - 2))
-    const u32 lim3 = end - base >= 3 ? end - 2 : base;
-    const u32 top = min(he, lim3);
-    const u32 nw = top > lo ? top - lo : 0u;
-    const u8* tw = txt + (lo - tlo);  // window text at window offset 0
-    if (z.prof) t1 = wall_clock64();
-    u16* isl = B;
-    u64* bm = reinterpret_cast<u64*>(B + G::ISL);  // disjoint from the sort's histograms
-    for (u32 i = tid; i < (nw + 63) / 64; i += 256) bm[i] = 0;
-    if (nw) {
-        lzl_bucket<G::PER>(tw, A, nw, hist, sh);
-        // group-head bitmap = the starts of the non-empty buckets: after the placement, wave
-        // 3's offset of bucket d is the bucket's end (bucket-major / wave-minor layout)
-        for (u32 d = tid; d < LZL_NBK; d += 256) {
-            const u32 e = hist[3 * LZL_NBK + d], st = d ? hist[3 * LZL_NBK + d - 1] : 0u;
-            if (e > st) atomicOr(&bm[st >> 6], 1ull << (st & 63));
-        }
-        __syncthreads();  // the islot writes below overwrite the histograms
-    }
-    // islot of [ilo, he)
-    for (u32 j = tid; j < nw; j += 256) {
-        const u32 x = A[j];
-        if (lo + x >= ilo) isl[lo + x - ilo] = (u16)j;
-    }
-    if (z.prof) t2 = wall_clock64();
-    __syncthreads();
-    if (z.prof) t3 = wall_clock64();
-    // NCHAIN chains: chain g of wave w parses chunk cid = CPW w + g
-    const u32 hl = lane & (LPC - 1);
-    const u32 cid = w * G::CPW + lane / LPC;
-    const u32 s = hs + cid * LZL_CHUNK;
-    const bool has = s < end;
-    const u32 e = has ? min(s + (u32)LZL_CHUNK, end) : 0u;
-    const u32 c = b * z.cpb + h * G::NCHAIN + cid;
-    const u32 lend = has ? min(end, e + (u32)LZL_CAPX) : 0u;
-    u32 q = has ? ((cid == 0 && hs == base) ? s : s - lead) : 0u;
-    u32 ntok = 0, off = 0, nlong = 0, nbuf = 0, nstep = 0, nbatch = 0;
-    u32 bpos = 0, blen = 0, bdist = 0, boff = 0;
-    bool un = false;
-    while (__ballot(has && q < e)) {
-        ++nstep;
-        const bool act = has && q < e;
-        u32 len, dist;
-        bool unres;
-        lzl_best<LPC>(txt, tlo, A, bm, isl, lo, ilo, act, q, act ? lend - q : 0u, end, len, dist, unres, nlong, nbatch);
-        if (act) {
-            if (q >= s) {
-                if (hl == nbuf) {
-                    bpos = q;
-                    blen = len;
-                    bdist = dist;
-                    boff = off;
-                }
-                if (++nbuf == LPC) {
-                    const u32 slot = s + ntok + 1 - LPC + hl;
-                    z.tok_pos[slot] = bpos;
-                    z.tok_len[slot] = blen;
-                    z.tok_dist[slot] = bdist;
-                    z.tok_off[slot] = boff;
-                    nbuf = 0;
-                }
-                ++ntok;
-                off += tok_bytes(len, dist);
-            }
-            un = un || unres;
-            q += len ? len : 1;
-        }
-    }
-    if (has && hl < nbuf) {
-        const u32 slot = s + ntok - nbuf + hl;
-        z.tok_pos[slot] = bpos;
-        z.tok_len[slot] = blen;
-        z.tok_dist[slot] = bdist;
-        z.tok_off[slot] = boff;
-    }
-    if (has && hl == 0) {
-        z.c_ntok[c] = ntok;
-        z.c_exit[c] = q | (un ? LZ_UNRES : 0u);
-        z.c_bytes[c] = off;
-    }
-    nlong = wave_reduce(nlong, OpAddU(), 0u);
-    if (lane == 0 && nlong) atomicAdd(z.nlong, nlong);
-    if (z.prof) {
-        // per-phase wall clock (100 MHz) summed over workgroups; wave loop trip counts
-        if (lane == 0) {
-            atomicAdd(z.prof + 4, (u64)nstep);
-            atomicAdd(z.prof + 5, (u64)nbatch);
-        }
-        __syncthreads();
-        if (tid == 0) {
-            const u64 t4 = wall_clock64();
-            atomicAdd(z.prof + 0, t1 - t0);
-            atomicAdd(z.prof + 1, t2 - t1);
-            atomicAdd(z.prof + 2, t3 - t2);
-            atomicAdd(z.prof + 3, t4 - t3);
-            atomicAdd(z.prof + 6, (u64)1);
-        }
-    }
-}
-
 // ULEB128 byte count of v (PY:111-124), branch-free
 __device__ inline u32 uleb_n(u32 v) {
     return 1u + (v >= (1u << 7)) + (v >= (1u << 14)) + (v >= (1u << 21)) + (v >= (1u << 28));
 }
 
 // =====================================================================================
-// k_lz_chains: the same speculative parse as k_lz_local (same window, index, chunks,
-// lead-ins and token records, so k_lz_stitch_l and k_lz_emit are unchanged) with chains
-// that advance independently.  In k_lz_local the four chains of a wave step their tokens
-// together: a token step lasts as many candidate batches as the chain with the most
+// k_lz_local's chains advance independently (round 6).  Before, the four chains of a wave
+// stepped their tokens together: a token step lasts as many candidate batches as the chain with the most
 // candidates needs (2.4 batches per step against 1.5 per token on text), and every step
 // pays the token setup once more.  Here one loop trip runs one candidate batch for every
 // chain with a token in progress, then finishes the tokens whose walk ended in that batch
@@ -540,17 +312,18 @@ __device__ inline u32 uleb_n(u32 v) {
 // out of the 4096-byte window, with no bitmap scan per token.
 // =====================================================================================
 constexpr u32 LZC_HEAD = 0x8000u;   // A[slot] flag: first slot of its hash bucket
-constexpr u32 LZC_NOSLOT = 0x10000u;  // prefetched entry below slot 0 (treated as out of window)
 
 template <u32 HOME, u32 LPC>
-__global__ __launch_bounds__(256) void k_lz_chains(LzArgs z, u32 hpb, u32 lead) {
+__global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
     using G = LzlGeom<HOME, LPC>;
     __shared__ __align__(16) u8 txt[G::TXT];
     __shared__ __align__(16) u16 A[G::NW];
-    __shared__ __align__(16) u16 B[G::BW];  // islot of [ilo, he); the sort's histograms before it
-    __shared__ u32 sh[4];
+    constexpr u32 NT = G::NT;
+    // islot of [ilo, he); the sort's histograms before it
+    __shared__ __align__(16) u16 B[G::ISL > G::NWV * LZL_NBK ? G::ISL : G::NWV * LZL_NBK];
+    __shared__ u32 sh[G::NWV];
     u16* hist = B;
-    static_assert(sizeof(u16) * 4 * LZL_NBK <= sizeof(B), "histograms alias the islot array");
+    
     static_assert(G::NW <= 0x3FFFu + 1u, "window offsets below the head flag");
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const u32 b = blockIdx.x / hpb, h = blockIdx.x - b * hpb;
@@ -569,10 +342,10 @@ __global__ __launch_bounds__(256) void k_lz_chains(LzArgs z, u32 hpb, u32 lead) 
         if (((uintptr_t)z.text & 3) == 0) {
             const u32* src = reinterpret_cast<const u32*>(z.text + tlo);
             u32* dst = reinterpret_cast<u32*>(txt);
-            for (u32 i = tid; i < n / 4; i += 256) dst[i] = src[i];
-            for (u32 i = (n & ~3u) + tid; i < n; i += 256) txt[i] = z.text[tlo + i];
+            for (u32 i = tid; i < n / 4; i += NT) dst[i] = src[i];
+            for (u32 i = (n & ~3u) + tid; i < n; i += NT) txt[i] = z.text[tlo + i];
         } else {
-            for (u32 i = tid; i < n; i += 256) txt[i] = z.text[tlo + i];
+            for (u32 i = tid; i < n; i += NT) txt[i] = z.text[tlo + i];
         }
     }
     __syncthreads();
@@ -583,15 +356,15 @@ __global__ __launch_bounds__(256) void k_lz_chains(LzArgs z, u32 hpb, u32 lead) 
     if (z.prof) t1 = wall_clock64();
     u16* isl = B;
     if (nw) {
-        lzl_bucket<G::PER>(tw, A, nw, hist, sh);
-        // flag the first slot of every non-empty bucket (wave 3's offsets are the bucket ends)
-        for (u32 d = tid; d < LZL_NBK; d += 256) {
-            const u32 e = hist[3 * LZL_NBK + d], st = d ? hist[3 * LZL_NBK + d - 1] : 0u;
+        lzl_bucket<G::PER, G::NWV>(tw, A, nw, hist, sh);
+        // flag the first slot of every non-empty bucket (the last wave's offsets are the bucket ends)
+        for (u32 d = tid; d < LZL_NBK; d += NT) {
+            const u32 e = hist[(G::NWV - 1) * LZL_NBK + d], st = d ? hist[(G::NWV - 1) * LZL_NBK + d - 1] : 0u;
             if (e > st) A[st] = (u16)(A[st] | LZC_HEAD);
         }
         __syncthreads();  // the islot writes below overwrite the histograms
     }
-    for (u32 j = tid; j < nw; j += 256) {
+    for (u32 j = tid; j < nw; j += NT) {
         const u32 x = A[j] & 0x7FFFu;
         if (lo + x >= ilo) isl[lo + x - ilo] = (u16)j;
     }
@@ -611,60 +384,64 @@ __global__ __launch_bounds__(256) void k_lz_chains(LzArgs z, u32 hpb, u32 lead) 
     const u32 lend = has ? min(end, e + (u32)LZL_CAPX) : 0u;
     const WinText T{txt, tlo};
     u32 p = has ? ((cid == 0 && hs == base) ? s : s - lead) : 0u;
-    bool alive = has && p < e, walk = false;
-    u32 k = 0, qa = LZC_NOSLOT, best = 0, bd = 0, lim = 0, capl = 0;
+    bool alive = has && p < e;
+    u32 k = 0, qa = 0, best = 0, bd = 0, lim = 0, capl = 0;
+    bool qok = false;  // qa holds the entry of this lane's slot (false: below slot 0)
     u64 pv = 0;
-    u32 ntok = 0, off = 0, nlong = 0, nbuf = 0, nstep = 0, nbatch = 0;
+    u32 ntok = 0, off = 0, nlong = 0, nbuf = 0, nbatch = 0;
     u32 bpos = 0, blen = 0, bdist = 0, boff = 0;
     bool un = false;
-    for (;;) {
-        // set up the next token of every chain that has none in progress
-        const bool need = alive && !walk;
-        if (__ballot(need)) {
-            if (need) {
-                best = 0;
-                bd = 0;
-                lim = lend - p;
-                capl = min((u32)LZ_CAP, lim);
-                k = p + (u32)LZ_MIN <= end ? (u32)isl[p - ilo] : 0u;
-                pv = lds8(txt, p - tlo);
-                qa = k > hl ? (u32)A[k - 1 - hl] : LZC_NOSLOT;
-                walk = true;
-            }
-        }
-        if (!__ballot(alive)) break;
-        ++nstep;
+    // a token's setup: p's slot in the index, its first 8 bytes and the first batch's entry
+    auto setup = [&]() {
+        best = 0;
+        bd = 0;
+        lim = lend - p;
+        capl = min((u32)LZ_CAP, lim);
+        k = p + (u32)LZ_MIN <= end ? (u32)isl[p - ilo] : 0u;
+        pv = lds8(txt, p - tlo);
+        qok = k > hl;
+        qa = A[qok ? k - 1 - hl : 0u];
+    };
+    if (alive) setup();
+    while (__ballot(alive)) {
         ++nbatch;
-        // one candidate batch per walking chain: slot k-1-hl (ascending distance)
-        const u32 qn = (walk && k > LPC + hl) ? (u32)A[k - LPC - 1 - hl] : LZC_NOSLOT;  // next batch
+        // one candidate batch per chain: slot k-1-hl (ascending distance); the walk stops at the
+        // bucket's first slot (flagged, itself a candidate) or before the first slot out of the
+        // window (or below slot 0)
         const u32 q = lo + (qa & 0x3FFFu);
-        const bool head = walk && (qa & LZC_HEAD);
-        const bool bad = walk && ((qa & LZC_NOSLOT) || p - q > (u32)LZ_WINDOW);
-        const u64 hm = __ballot(head) & GM, bm = __ballot(bad) & GM;
-        const bool valid = walk && !(hm & below) && !(bm & (below | (1ull << lane)));
+        const u32 qr = q - tlo;
+        // the candidate's first 8 bytes, loaded for every lane (an entry past the walk's end
+        // still lies in the window)
+        const u32* cw = reinterpret_cast<const u32*>(txt) + (qr >> 2);
+        const u32 c0 = cw[0], c1 = cw[1], c2 = cw[2];
+        // the next batch's entries, in the same LDS round trip (loaded unconditionally from a
+        // clamped slot: no branch splits the loads)
+        const bool qnok = k > LPC + hl;
+        const u32 qn = A[qnok ? k - LPC - 1 - hl : 0u];
+        const u64 cv = ((u64)__builtin_amdgcn_alignbyte(c2, c1, qr & 3) << 32) | __builtin_amdgcn_alignbyte(c1, c0, qr & 3);
+        const bool bad = !qok || p - q > (u32)LZ_WINDOW;
+        const u64 sm = __ballot(alive && (bad || (qa & LZC_HEAD))) & GM;
+        const bool valid = alive && !bad && !(sm & below);
         u32 l = 0;
-        if (valid) {
-            const u32 qr = q - tlo;
-            const u64 d0 = pv ^ lds8(txt, qr);
-            if ((d0 & 0xFFFFFFull) == 0) {  // the same 3-gram, not only the same hash
-                if (d0) {
-                    l = (u32)(__ffsll((long long)d0) - 1) >> 3;
-                } else if (best < 8 || (best < lim && T[p + best] == T[q + best])) {
-                    const u32 pr = p - tlo;
-                    l = 8;
+        const u64 d0 = pv ^ cv;
+        if (valid && (d0 & 0xFFFFFFull) == 0) {  // the same 3-gram, not only the same hash
+            if (d0) {
+                l = (u32)(__ffsll((long long)d0) - 1) >> 3;
+            } else if (best < 8 || (best < lim && T[p + best] == T[q + best])) {
+                const u32 pr = p - tlo;
+                l = 8;
 #pragma unroll
-                    for (int kk = 1; kk < LZ_CAP / 8; ++kk) {
-                        if (l >= capl) break;
-                        const u64 d = lds8(txt, pr + 8 * kk) ^ lds8(txt, qr + 8 * kk);
-                        if (d) {
-                            l += (u32)(__ffsll((long long)d) - 1) >> 3;
-                            break;
-                        }
-                        l += 8;
+                for (int kk = 1; kk < LZ_CAP / 8; ++kk) {
+                    if (l >= capl) break;
+                    const u64 d = lds8(txt, pr + 8 * kk) ^ lds8(txt, qr + 8 * kk);
+                    if (d) {
+                        l += (u32)(__ffsll((long long)d) - 1) >> 3;
+                        break;
                     }
+                    l += 8;
                 }
-                l = min(l, capl);
             }
+            l = min(l, capl);
         }
         u64 longm = __ballot(valid && l >= capl && capl < lim);
         while (longm) {
@@ -677,14 +454,14 @@ __global__ __launch_bounds__(256) void k_lz_chains(LzArgs z, u32 hpb, u32 lead) 
             ++nlong;
         }
         const u32 key = grp_max<LPC>(valid && l >= (u32)LZ_MIN ? (l << 14) | (q - lo) : 0u);
-        if (walk && (key >> 14) > best) {
+        if ((key >> 14) > best) {
             best = key >> 14;
             bd = p - (lo + (key & 0x3FFFu));
         }
         qa = qn;
+        qok = qnok;
         k = k > LPC ? k - LPC : 0u;
-        // a walk ends at its bucket's first slot, at the window's end or at a full-length match
-        const bool fin = walk && ((hm | bm) != 0 || best >= lim);
+        const bool fin = alive && (sm != 0 || best >= lim);
         if (__ballot(fin)) {
             if (fin) {
                 const u32 len = best >= (u32)LZ_MIN ? best : 0u;
@@ -710,7 +487,7 @@ __global__ __launch_bounds__(256) void k_lz_chains(LzArgs z, u32 hpb, u32 lead) 
                 }
                 p += len ? len : 1u;
                 alive = p < e;
-                walk = false;
+                if (alive) setup();  // the next token's loads issue before the loop turns
             }
         }
     }
@@ -730,8 +507,265 @@ __global__ __launch_bounds__(256) void k_lz_chains(LzArgs z, u32 hpb, u32 lead) 
     if (lane == 0 && nlong) atomicAdd(z.nlong, nlong);
     if (z.prof) {
         if (lane == 0) {
-            atomicAdd(z.prof + 4, (u64)nstep);
+            atomicAdd(z.prof + 4, (u64)nbatch);
             atomicAdd(z.prof + 5, (u64)nbatch);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const u64 t4 = wall_clock64();
+            atomicAdd(z.prof + 0, t1 - t0);
+            atomicAdd(z.prof + 1, t2 - t1);
+            atomicAdd(z.prof + 2, t3 - t2);
+            atomicAdd(z.prof + 3, t4 - t3);
+            atomicAdd(z.prof + 6, (u64)1);
+        }
+    }
+}
+
+// =====================================================================================
+// k_lz_lanes: a chain per LANE over 64-byte chunks, candidates from hash chains.
+//
+// k_lz_local gives each chain 16 lanes (the 16 nearest candidates of a token compared at
+// once) and a workgroup 16 chains: the LDS a chain needs (its share of the 4 KiB home plus
+// the 4 KiB history, indexed) leaves room for 64 chains per CU, and every token costs a
+// whole-wave instruction stream (~185 VALU per trip).  Here every lane is a chain: it walks
+// its token's candidates one per trip, nearest first, through a per-position hash chain
+// prv[x] = the previous window position whose 3-gram has x's hash (one LDS round trip per
+// candidate: the candidate's text and its own prv entry are independent loads).  A
+// workgroup of NWV waves owns a home of NWV x 64 chunks of 64 bytes (16 KiB at four waves):
+// the window [home - 4096 - LZL_LEAD, home end + LZL_CAPX) costs 3 bytes of LDS per
+// position (text + prv), so a CU holds 512 chains instead of 64 and a trip is ~35 VALU for
+// 64 chains instead of ~185 for 4.
+//
+// Index build: each wave takes a contiguous quarter of the window's 3-gram positions, 64 at
+// a time in order; a lane's previous same-hash position is the nearest lower lane of its
+// match-any group (LZC_HB ballots) or, for the group's lowest lane, the wave's running head
+// table; the group's highest lane updates the head.  After a barrier the first occurrences
+// of each later quarter take the last occurrence from the heads of the quarters before it.
+//
+// The chunk / token records are those of k_lz_local (LzArgs, cshift 6), so k_lz_stitch_l
+// and k_lz_emit run unchanged: a chain starts `lead` bytes before its chunk (tokens before
+// the chunk start not recorded); matches are exact up to LZL_CAPX past the chunk end, a
+// longer one ends the chunk unresolved for the stitch.
+// =====================================================================================
+constexpr u32 LZC_CH = 64;                 // chunk bytes (one lane)
+constexpr u32 LZC_CSHIFT = 6;
+static_assert((1u << LZC_CSHIFT) == LZC_CH, "chunk shift");
+constexpr u32 LZC_HB = 11;                 // hash bits of the chains
+constexpr u32 LZC_NB = 1u << LZC_HB;
+constexpr u16 LZC_NONE = 0xFFFFu;
+__device__ inline u32 hash3c(const u8* t, u32 x) {
+    const u32 k = ((u32)t[x] << 16) | ((u32)t[x + 1] << 8) | t[x + 2];
+    return (k * 0x9E3779B1u) >> (32 - LZC_HB);
+}
+
+template <u32 NWV>
+struct LzcGeom {
+    static constexpr u32 NT = 64 * NWV;                    // threads = chains
+    static constexpr u32 HOME = NT * LZC_CH;                 // home bytes
+    static constexpr u32 NW = HOME + LZ_WINDOW + LZL_LEAD;   // window positions
+    static constexpr u32 TXT = NW + LZL_CAPX + 32;           // text window + alignment + compare slack
+    static_assert(NW < LZC_NONE, "window offsets in 16 bits");
+};
+
+
+template <u32 NWV>
+__global__ __launch_bounds__(64 * NWV) void k_lz_lanes(LzArgs z, u32 hpb, u32 lead) {
+    using G = LzcGeom<NWV>;
+    constexpr u32 NT = G::NT;
+    __shared__ __align__(16) u8 txt[G::TXT];
+    __shared__ __align__(16) u16 prv[G::NW];
+    __shared__ __align__(16) u16 heads[NWV][LZC_NB];
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u32 b = blockIdx.x / hpb, h = blockIdx.x - b * hpb;
+    const u32 base = z.geo.base(b), end = z.geo.end(b);
+    const u32 hs = base + h * G::HOME;
+    if (hs >= end) return;
+    const u32 he = min(hs + G::HOME, end);
+    const u32 lo = hs - base > (u32)(LZ_WINDOW + LZL_LEAD) ? hs - LZ_WINDOW - LZL_LEAD : base;
+    const u32 hi = min(end, he + (u32)LZL_CAPX);
+    const u32 tlo = lo & ~3u;
+    u64 t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+    if (z.prof) t0 = wall_clock64();
+    {
+        const u32 n = hi - tlo;
+        if (((uintptr_t)z.text & 15) == 0) {  // 16-byte loads (tlo is 4-aligned)
+            const u32 hd = (16 - (tlo & 15)) & 15;
+            for (u32 i = tid; i < min(hd, n); i += NT) txt[i] = z.text[tlo + i];
+            const uint4* src = reinterpret_cast<const uint4*>(z.text + tlo + hd);
+            const u32 n16 = (n - min(hd, n)) / 16;
+            for (u32 i = tid; i < n16; i += NT) {
+                const uint4 v = src[i];
+                u32* d = reinterpret_cast<u32*>(txt + hd + 16 * i);
+                d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
+            }
+            for (u32 i = hd + 16 * n16 + tid; i < n; i += NT) txt[i] = z.text[tlo + i];
+        } else {
+            for (u32 i = tid; i < n; i += NT) txt[i] = z.text[tlo + i];
+        }
+    }
+    for (u32 i = tid; i < NWV * LZC_NB / 2; i += NT) reinterpret_cast<u32*>(&heads[0][0])[i] = 0xFFFFFFFFu;
+    __syncthreads();
+    if (z.prof) t1 = wall_clock64();
+    // ---- index: prv of every 3-gram position of the window [lo, top) ----
+    const u32 lim3 = end - base >= 3 ? end - 2 : base;
+    const u32 top = min(he, lim3);
+    const u32 nw = top > lo ? top - lo : 0u;
+    const u8* tw = txt + (lo - tlo);
+    const u32 Q = (nw + NWV - 1) / NWV;
+    const u32 r0 = min(w * Q, nw), r1 = min(r0 + Q, nw);
+    const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const u64 gt = lane < 63 ? (~0ull << (lane + 1)) : 0ull;
+    for (u32 x0 = r0; x0 < r1; x0 += 64) {  // wave-uniform
+        const u32 x = x0 + lane;
+        const bool valid = x < r1;
+        const u32 hv = valid ? hash3c(tw, x) : 0u;
+        u64 m = __ballot(valid);
+#pragma unroll
+        for (u32 bit = 0; bit < LZC_HB; ++bit) {
+            const u64 bal = __ballot((hv >> bit) & 1u);
+            m &= ((hv >> bit) & 1u) ? bal : ~bal;
+        }
+        if (valid) {
+            const u64 lower = m & lt;
+            const u32 pv = lower ? x0 + 63 - (u32)__clzll(lower) : (u32)heads[w][hv];
+            prv[x] = (u16)pv;
+            if (!(m & gt)) heads[w][hv] = (u16)x;
+        }
+    }
+    __syncthreads();
+    if (w) {
+        // a later quarter's first occurrence of a hash: the last one of the quarters before it
+        for (u32 x = r0 + lane; x < r1; x += 64) {
+            if (prv[x] != LZC_NONE) continue;
+            const u32 hv = hash3c(tw, x);
+            u32 pv = LZC_NONE;
+            for (u32 v = w; v-- > 0;) {
+                pv = heads[v][hv];
+                if (pv != LZC_NONE) break;
+            }
+            prv[x] = (u16)pv;
+        }
+    }
+    if (z.prof) t2 = wall_clock64();
+    __syncthreads();
+    if (z.prof) t3 = wall_clock64();
+
+    // ---- parse: chain tid owns chunk [s, e) ----
+    const WinText T{txt, tlo};
+    const u32 s = hs + tid * LZC_CH;
+    const bool has = s < end;
+    const u32 e = has ? min(s + LZC_CH, end) : 0u;
+    const u32 c = b * z.cpb + h * NT + tid;
+    const u32 lend = has ? min(end, e + (u32)LZL_CAPX) : 0u;
+    u32 p = has ? ((tid == 0 && hs == base) ? s : (s - base > lead ? s - lead : base)) : 0u;
+    bool alive = has && p < e;
+    u32 q = NONE, best = 0, bd = 0, lim = 0, capl = 0, ntok = 0, off = 0, nlong = 0, ntrip = 0;
+    u64 pv = 0;
+    bool un = false;
+    // a candidate at q (q < p) is in the walk while it is within the window
+    auto first_cand = [&](u32 x) -> u32 {
+        if (x + (u32)LZ_MIN > end) return NONE;
+        const u32 v = prv[x - lo];
+        return v == LZC_NONE ? NONE : lo + v;
+    };
+    auto setup = [&]() {
+        best = 0;
+        bd = 0;
+        lim = lend - p;
+        capl = min((u32)LZ_CAP, lim);
+        pv = lds8(txt, p - tlo);
+        q = first_cand(p);
+    };
+    // one token: record it (tokens from the chunk start on), advance
+    auto finish = [&]() {
+        const u32 len = best >= (u32)LZ_MIN ? best : 0u;
+        const u32 dist = len ? bd : 0u;
+        un = un || (len && best >= lim && lim < end - p);
+        if (p >= s) {
+            const u32 slot = s + ntok;
+            z.tok_pos[slot] = p;
+            z.tok_len[slot] = len;
+            z.tok_dist[slot] = dist;
+            z.tok_off[slot] = off;
+            ++ntok;
+            off += len ? 1u + uleb_n(len) + uleb_n(dist) : 2u;
+        }
+        p += len ? len : 1u;
+        alive = p < e;
+    };
+    if (alive) setup();
+    while (__ballot(alive)) {
+        ++ntrip;
+        const bool ok = alive && q != NONE && p - q <= (u32)LZ_WINDOW;
+        u32 l = 0, qc = q;
+        if (ok) {
+            const u32 qr = q - tlo;
+            const u32* cw = reinterpret_cast<const u32*>(txt) + (qr >> 2);
+            const u32 c0 = cw[0], c1 = cw[1], c2 = cw[2];
+            const u32 qn = prv[q - lo];  // the next candidate, in the same LDS round trip
+            const u64 cv = ((u64)__builtin_amdgcn_alignbyte(c2, c1, qr & 3) << 32) |
+                           __builtin_amdgcn_alignbyte(c1, c0, qr & 3);
+            const u64 d0 = pv ^ cv;
+            if ((d0 & 0xFFFFFFull) == 0) {  // the same 3-gram, not only the same hash
+                if (d0) {
+                    l = (u32)(__ffsll((long long)d0) - 1) >> 3;
+                } else if (best < 8 || (best < lim && T[p + best] == T[q + best])) {
+                    // a strictly longer match must also match at `best`
+                    const u32 pr = p - tlo;
+                    l = 8;
+#pragma unroll
+                    for (int kk = 1; kk < LZ_CAP / 8; ++kk) {
+                        if (l >= capl) break;
+                        const u64 d = lds8(txt, pr + 8 * kk) ^ lds8(txt, qr + 8 * kk);
+                        if (d) {
+                            l += (u32)(__ffsll((long long)d) - 1) >> 3;
+                            break;
+                        }
+                        l += 8;
+                    }
+                }
+                l = min(l, capl);
+            }
+            q = qn == LZC_NONE ? NONE : lo + qn;
+        }
+        // capped candidates extended exactly (up to lim), one at a time by the whole wave
+        u64 longm = __ballot(ok && l >= capl && capl < lim);
+        while (longm) {
+            const u32 j = (u32)__ffsll((long long)longm) - 1;
+            const u32 pj = __builtin_amdgcn_readlane(p, j), qj = __builtin_amdgcn_readlane(qc, j);
+            const u32 cj = __builtin_amdgcn_readlane(capl, j), mj = __builtin_amdgcn_readlane(lim, j);
+            const u32 lj = wave_lcp(T, pj, qj, cj, mj);
+            if (lane == j) l = lj;
+            longm &= longm - 1;
+            ++nlong;
+        }
+        if (ok && l >= (u32)LZ_MIN && l > best) {  // strictly longer wins: the nearest of equals stays
+            best = l;
+            bd = p - qc;
+        }
+        const bool fin = alive && (!ok || q == NONE || p - q > (u32)LZ_WINDOW || best >= lim);
+        if (fin) {
+            finish();
+            // tokens with no candidate at all (literals) are finished on the spot
+            while (alive) {
+                setup();
+                if (q != NONE && p - q <= (u32)LZ_WINDOW) break;
+                finish();
+            }
+        }
+    }
+    if (has) {
+        z.c_ntok[c] = ntok;
+        z.c_exit[c] = p | (un ? LZ_UNRES : 0u);
+        z.c_bytes[c] = off;
+    }
+    nlong = wave_reduce(nlong, OpAddU(), 0u);
+    if (lane == 0 && nlong) atomicAdd(z.nlong, nlong);
+    if (z.prof) {
+        if (lane == 0) {
+            atomicAdd(z.prof + 4, (u64)ntrip);
+            atomicAdd(z.prof + 5, (u64)ntrip);
         }
         __syncthreads();
         if (tid == 0) {
@@ -1231,15 +1265,21 @@ __global__ __launch_bounds__(256) void k_lz_emit(LzArgs z, const u32* method, co
 
 const char* lz_spec_name() { return "k_lz_local"; }
 
+// The parse form (read per call; tests switch it): 1 = a chain per lane over 64-byte chunks
+// (k_lz_lanes, default), 0 = 16-lane chains over 256-byte chunks (k_lz_local)
+static int lz_lanes_mode() {
+    const char* e = getenv("KOLM_LZ_LANES");
+    return e ? atoi(e) : 1;
+}
+u32 lz_chunk_shift() { return lz_lanes_mode() ? LZC_CSHIFT : 8u; }
+
 void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
     if (!z.geo.nb) return;
-    // 4 KiB homes, 16 chains of 16 lanes (4 workgroups per CU).  KOLM_LZ_GEOM = 1 (A/B): 8 KiB
-    // homes parsed by 32 chains of 8 lanes — 2 workgroups per CU (110 KB of LDS instead of 138 KB),
-    // half the instructions per chain step, the same 64 chains per CU — measured slower beside the
-    // sort (parse 31.4 -> 36.1 ms, step 35.7 -> 39.9 ms): 2 waves per SIMD no longer hide the
-    // chains' dependent LDS latency
-    static const int geom = getenv("KOLM_LZ_GEOM") ? atoi(getenv("KOLM_LZ_GEOM")) : 0;
-    const u32 home = geom == 1 ? 8192u : 4096u;
+    // 4 KiB homes, 16 chains of 16 lanes (4 workgroups per CU, LDS-limited).  Measured and
+    // removed: 8 KiB homes parsed by 32 chains of 8 lanes (round 5: 2 waves per SIMD no longer hide
+    // the chains' LDS latency, step 35.7 -> 39.9 ms) and 5 KiB homes in 5-wave workgroups (round 6:
+    // step 33.4 -> 36.7 ms beside the sort stream)
+    constexpr u32 home = 4096u;
     const u32 hpb = (z.geo.bs + home - 1) / home;
     {
         // text window (LZL_NW + LZL_CAPX bytes per 4 KiB home: ~2.1 B per position) +
@@ -1251,18 +1291,18 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
         static const u32 lead =
             getenv("KOLM_LZ_LEAD") ? std::min<u32>(atoi(getenv("KOLM_LZ_LEAD")), LZL_LEAD) : 48u;
         KScope k(kt, KT_LZPARSE, "k_lz_local", z.geo.N * 2);
-        static const int chains = getenv("KOLM_LZ_CHAINS") ? atoi(getenv("KOLM_LZ_CHAINS")) : 1;
-        if (chains && geom != 1)
-            k_lz_chains<4096, 16><<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb, lead);
-        else if (geom == 1)
-            k_lz_local<8192, 8><<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb, lead);
-        else
-            k_lz_local<4096, 16><<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb, lead);
+        if (z.cshift == LZC_CSHIFT) {
+            constexpr u32 NWV = 4;
+            const u32 hpl = (z.geo.bs + LzcGeom<NWV>::HOME - 1) / LzcGeom<NWV>::HOME;
+            k_lz_lanes<NWV><<<z.geo.nb * hpl, LzcGeom<NWV>::NT, 0, s>>>(z, hpl, lead);
+        } else {
+            k_lz_local<home, 16><<<z.geo.nb * hpb, LzlGeom<home, 16>::NT, 0, s>>>(z, hpb, lead);
+        }
     }
     {
         KScope k(kt, KT_LZPARSE, "k_lz_stitch", (u64)z.cpb * z.geo.nb * 16);
         // KOLM_LZ_BIGWIN = 0 / 1 forces the window; default: 62 KiB (+ fingerprints) below 64 blocks
-        static const int bw = getenv("KOLM_LZ_BIGWIN") ? atoi(getenv("KOLM_LZ_BIGWIN")) : -1;
+        const int bw = getenv("KOLM_LZ_BIGWIN") ? atoi(getenv("KOLM_LZ_BIGWIN")) : -1;  // read per call (tests)
         if (bw == 1 || (bw < 0 && z.geo.nb < 64))
             k_lz_stitch_l<BF_WIN_BIG><<<z.geo.nb, 64, 0, s>>>(z);
         else

@@ -4,9 +4,10 @@
 //     (distinct symbols of the chunk, most recent first) ++ (previous state minus them),
 // so the state entering every chunk is obtained by composing chunk summaries:
 //   1. k_mtf_summary : one thread per chunk scans it backwards -> its recency list;
-//   2. k_mtf_compose : one wave per block folds the summaries in order, writing the
-//                      256-byte state at the start of every chunk (lane l holds entries
-//                      4l..4l+3; stable compaction by ballot/popcount);
+//   2. k_mtf_cp1..3  : the summaries composed in three levels (ranges of chunks by a wave
+//                      each, the ranges of a block chained by one workgroup, the ranges
+//                      re-walked), writing the 256-byte state at the start of every chunk
+//                      (lane l holds entries 4l..4l+3; stable compaction by ballot/popcount);
 //   3. k_mtf_replay  : one thread per chunk replays MTF from its start state with the
 //                      table in LDS (word-interleaved per thread -> no bank conflicts),
 //                      zero-byte search 4 entries per compare.
@@ -157,89 +158,6 @@ __device__ inline void mtf_apply(u32* st, u8* nst, u32* member, const u8* sm, u3
     __builtin_amdgcn_wave_barrier();
 }
 
-// Per block, CW waves split the chunks into CW ranges.  Phase 1: each wave composes its
-// range's summaries starting from the identity state; the first d entries of the result
-// (d = distinct symbols of the range) are the range's own recency summary.  Phase 2: wave
-// 0 chains the range summaries into each range's entry state.  Phase 3: each wave
-// re-walks its range from its entry state and publishes the state at every chunk start.
-// CW = 8 waves per block; 16 for the small chunks of batches of few blocks (more summaries
-// per block to fold: one gradient / checker block at 128-byte chunks has 8192)
-template <int CW>
-__global__ __launch_bounds__(64 * CW) void k_mtf_compose(ChunkGeom cg, const u8* summary, const u16* scnt,
-                                                         u8* states) {
-    __shared__ u32 st[CW][64];
-    __shared__ u8 nst[CW][256];
-    __shared__ u32 member[CW][8];
-    __shared__ u32 uni[CW][8];
-    __shared__ u32 entry[CW][64];
-    __shared__ u32 dist[CW];
-    const u32 b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const u32 ident = (4 * lane) | ((4 * lane + 1) << 8) | ((4 * lane + 2) << 16) | ((4 * lane + 3) << 24);
-    // chunks of this block that exist
-    u32 nch = 0;
-    {
-        const u32 lo0 = cg.geo.base(b), e = cg.geo.end(b);
-        nch = (e - lo0 + cg.csz - 1) / cg.csz;
-    }
-    const u32 per = (nch + CW - 1) / CW;
-    const u32 k0 = min(w * per, nch), k1 = min(k0 + per, nch);
-    // phase 1
-    st[w][lane] = ident;
-    if (lane < 8) uni[w][lane] = 0;
-    __builtin_amdgcn_wave_barrier();
-    for (u32 k = k0; k < k1; ++k) {
-        const u32 c = b * cg.cpb + k;
-        const u8* sm = summary + (u64)c * 256;
-        const u32 cnt = scnt[c];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const u32 i = 4 * lane + j;
-            if (i < cnt) atomicOr(&uni[w][sm[i] >> 5], 1u << (sm[i] & 31));
-        }
-        mtf_apply(st[w], nst[w], member[w], sm, cnt);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {
-        u32 d = 0;
-        for (int q = 0; q < 8; ++q) d += __popc(uni[w][q]);
-        dist[w] = d;
-    }
-    __syncthreads();
-    // phase 2 (wave 0): entry[0] = identity, entry[v] = entry[v-1] after range v-1
-    if (w == 0) {
-        entry[0][lane] = ident;
-        __builtin_amdgcn_wave_barrier();
-        for (u32 v = 1; v < CW; ++v) {
-            // range v-1's summary = first dist[v-1] bytes of its phase-1 state
-            u8 tmp[4];
-            const u32 word = st[v - 1][lane];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) tmp[j] = (word >> (8 * j)) & 0xFF;
-            __builtin_amdgcn_wave_barrier();
-            // copy the summary out of st[v-1] before st[0] changes it (v-1 == 0 case)
-            u8* sumbuf = reinterpret_cast<u8*>(entry[v]);  // scratch: entry[v] is written below
-            for (int j = 0; j < 4; ++j) sumbuf[4 * lane + j] = tmp[j];
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            if (v == 1) st[0][lane] = ident;  // phase-1 state of range 0 consumed above
-            __builtin_amdgcn_wave_barrier();
-            mtf_apply(st[0], nst[0], member[0], sumbuf, dist[v - 1]);
-            entry[v][lane] = st[0][lane];
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
-    __syncthreads();
-    // phase 3
-    st[w][lane] = entry[w][lane];
-    __builtin_amdgcn_wave_barrier();
-    for (u32 k = k0; k < k1; ++k) {
-        const u32 c = b * cg.cpb + k;
-        reinterpret_cast<u32*>(states + (u64)c * 256)[lane] = st[w][lane];
-        mtf_apply(st[w], nst[w], member[w], summary + (u64)c * 256, scnt[c]);
-    }
-}
 
 // The same composition in three launches and three levels, so the
 // dependent mtf_apply chain of a block is ~55 steps instead of 2 * 64 + 16 (one gradient BMP
@@ -557,7 +475,7 @@ __global__ __launch_bounds__(RT) void k_mtf_replay(ChunkGeom cg, const u8* in, c
 }
 
 // Position-parallel replay for batches of few blocks: one wave per chunk, 64 bytes per step
-// with one lane per byte, from the chunk's entry state S (k_mtf_compose).  With Seen = the
+// with one lane per byte, from the chunk's entry state S (k_mtf_cp3).  With Seen = the
 // distinct symbols of the chunk before byte i (most recent first), MTF's list before i is
 // Seen ++ (S minus Seen), so byte i = s gets
 //   * if s occurred before in the chunk (last at p): the number of distinct symbols in (p, i);
@@ -681,13 +599,8 @@ u32 mtf_chunk_bytes(const Geom& geo) {
 }
 
 // The three-launch compose (k_mtf_cp1..3) for every batch (one A/B call: config 2 1.90 -> 1.75
-// ms, config 5 6.23 -> 6.09 ms, 256 MiB text MTF family 1.91 -> 1.76 ms); KOLM_MTF_CP = 0: the
-// one-workgroup-per-block k_mtf_compose (read per call)
-bool mtf_cp_mode(const Geom& geo) {
-    const char* e = getenv("KOLM_MTF_CP");
-    (void)geo;
-    return e ? atoi(e) != 0 : true;
-}
+// ms, config 5 6.23 -> 6.09 ms, 256 MiB text MTF family 1.91 -> 1.76 ms against the round-4
+// compose, one workgroup per block)
 u64 mtf_cp_words(const Geom& geo) { return (u64)geo.nb * CP_R * 129; }
 
 void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summary_cnt, u8* states,
@@ -703,7 +616,7 @@ void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summar
     }
     {
         KScope k(kt, KT_MTF, "k_mtf_compose", (u64)nchunks * 512);
-        if (cp_scratch && mtf_cp_mode(geo)) {
+        {
             u32* rst = cp_scratch;                           // [nb * CP_R][64]
             u32* rentry = cp_scratch + (u64)geo.nb * CP_R * 64;  // [nb * CP_R][64]
             u32* rdist = rentry + (u64)geo.nb * CP_R * 64;        // [nb * CP_R]
@@ -711,10 +624,6 @@ void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summar
             k_mtf_cp1<<<g13, 64 * CP_W, 0, s>>>(cg, summary, summary_cnt, rst, rdist);
             k_mtf_cp2<<<geo.nb, 64 * CP_G, 0, s>>>(rst, rdist, rentry);
             k_mtf_cp3<<<g13, 64 * CP_W, 0, s>>>(cg, summary, summary_cnt, rentry, states);
-        } else if (csz < MTF_CHUNK || geo.nb < 64) {
-            k_mtf_compose<16><<<geo.nb, 64 * 16, 0, s>>>(cg, summary, summary_cnt, states);
-        } else {
-            k_mtf_compose<8><<<geo.nb, 64 * 8, 0, s>>>(cg, summary, summary_cnt, states);
         }
     }
     if (mtf_wave_mode(geo)) {

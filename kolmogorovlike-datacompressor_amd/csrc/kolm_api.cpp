@@ -313,13 +313,6 @@ TScope::~TScope() noexcept(false) {
     }
 }
 
-// round 0 of the cyclic sort: 1 = MSD radix partitions + LDS bucket sorts (k_r0m.hip),
-// 0 = eight LSD passes (k_lsd.hip); KOLM_R0_MSD overrides (read per batch: tests switch it)
-int r0_msd_mode() {
-    const char* e = getenv("KOLM_R0_MSD");
-    return e ? atoi(e) : 0;
-}
-
 std::mutex g_mu;
 kolm_ctx* g_default = nullptr;
 std::vector<kolm_ctx*> g_multi;  // per-device contexts of kolm_encode_blocks_multi
@@ -488,24 +481,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             r.rec[1] = c->get<u64>("r0rec1", N);
             out.r0_chars = C;
             if (dbg) fprintf(stderr, "[kolm] round 0: %u characters of %u bits\n", C, w);
-            if (r0_msd_mode()) {
-                R0MBufs mb{};
-                mb.x0 = c->get<u32>("r0m_x0", N);
-                mb.x1 = c->get<u32>("r0m_x1", N);
-                mb.hist = c->get<u32>("r0m_hist", r0m_tile_cap(N, geo.nb, geo.bs) * 256);
-                mb.cnt = c->get<u32>("r0m_cnt", 16);
-                static const char* const fn[R0M_NCLS] = {"r0m_f0", "r0m_f1", "r0m_f2", "r0m_f3", "r0m_f4", "r0m_f5",
-                                                         "r0m_f6", "r0m_f7", "r0m_f8", "r0m_f9", "r0m_f10"};
-                for (int k = 0; k < R0M_NCLS; ++k) mb.fin[k] = c->get<u32>(fn[k], 3 * r0m_fin_cap(N, geo.nb, k));
-                for (int k = 0; k < 2; ++k) {
-                    mb.segs[k] = c->get<LSeg>(k ? "r0m_s1" : "r0m_s0", r0m_seg_cap(N, geo.nb));
-                    mb.tiles[k] = c->get<LTile>(k ? "r0m_t1" : "r0m_t0", r0m_tile_cap(N, geo.nb, geo.bs));
-                }
-                const u32 lv = launch_round0_msd(geo, r, nxt, L.next_cnt, a.blk_split, mb, s, c->kt(), h);
-                if (dbg) fprintf(stderr, "[kolm] round 0: %u MSD levels\n", lv);
-            } else {
-                launch_round0(geo, r, nxt, L.next_cnt, a.blk_split, s, c->kt());
-            }
+            launch_round0(geo, r, nxt, L.next_cnt, a.blk_split, s, c->kt());
             out.active += N;
             out.rounds = 1;
             launch_update_done(blk_done, blk_last, a.blk_split, geo.nb, 0, s);
@@ -746,7 +722,7 @@ struct Pipeline {
         u8* out = c->get<u8>("mtf", N);
         launch_mtf(geo, in, out, c->get<u8>("mtf_sum", nch * 256), c->get<u16>("mtf_cnt", nch),
                    c->get<u8>("mtf_states", nch * 256), c->active, c->kt(), bits, 2,
-                   mtf_cp_mode(geo) ? c->get<u32>("mtf_cp", mtf_cp_words(geo)) : nullptr);
+                   c->get<u32>("mtf_cp", mtf_cp_words(geo)));
         return out;
     }
 
@@ -763,8 +739,7 @@ struct Pipeline {
         z.fix_len = c->get<u32>("fix_len", N);
         z.fix_dist = c->get<u32>("fix_dist", N);
         z.fix_off = c->get<u32>("fix_off", N);
-        z.cshift = 8;
-        static_assert(LZL_CHUNK == 256, "chunk shift");
+        z.cshift = lz_chunk_shift();
         z.cpb = (geo.bs + (1u << z.cshift) - 1) >> z.cshift;
         const u64 nch = (u64)z.cpb * geo.nb + 1;
         z.c_ntok = c->get<u32>("c_ntok", nch);
@@ -929,7 +904,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     // LDS-bound parse): 53.8-54.2 ms per 256 MiB for 0, 54.1-54.2 for 1, 55.4-56.2 for 2.
     const bool serial = c->serial;
     // (the MSD round 0's LDS bucket sorts need whole CUs: the parse starts after round 0 there)
-    const int overlap = getenv("KOLM_OVERLAP") ? atoi(getenv("KOLM_OVERLAP")) : (r0_msd_mode() ? 2 : 0);
+    const int overlap = getenv("KOLM_OVERLAP") ? atoi(getenv("KOLM_OVERLAP")) : 0;
     hipStream_t ms = c->stream, s = serial ? c->stream : c->aux;
     Pipeline P{c, geo, d_text};
     hipEvent_t* ev = c->ev;
@@ -1032,7 +1007,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     // 6.21 ms; config 4's 32-block shard measured 6.84 -> 7.30 ms that way (the parse then
     // competes with Lyndon and round 0 for CUs), so it keeps the index-stream form.
     // KOLM_PREVC_IDX = 0 / 1 forces it.
-    static const int prevc_idx = getenv("KOLM_PREVC_IDX") ? atoi(getenv("KOLM_PREVC_IDX")) : -1;
+    const int prevc_idx = getenv("KOLM_PREVC_IDX") ? atoi(getenv("KOLM_PREVC_IDX")) : -1;  // read per call (tests)
     if (!serial && (prevc_idx >= 0 ? prevc_idx != 0 : nb >= 16)) {
         KOLM_HIP_CHECK(hipStreamWaitEvent(xs, ev[5], 0));
         P.prevc();
@@ -1887,6 +1862,12 @@ int kolm_encode_blocks_multi(int ngpu, const uint8_t* data, uint64_t total, uint
                              uint8_t* payload_arena, uint64_t arena_cap, uint64_t* payload_off, kolm_stats* stats) {
     if (ngpu < 1 || (total && !data) || !payload_off || block_size == 0) return KOLM_EARG;
     if ((cand_mask & KOLM_FULL_MASK) == 0) return KOLM_EARG;
+    // One call at a time from encode through the gather: each device's payloads wait in its
+    // context's shared arena between the encode and the reassembly, so a concurrent call on
+    // the same per-device contexts must not start until this one has copied them out
+    // (kolm.h: calls are internally serialised).
+    static std::mutex multi_mu;
+    std::lock_guard<std::mutex> multi_lock(multi_mu);
     const u64 nb64 = (total + block_size - 1) / block_size;
     if (nb64 > 0xFFFFFFFFull) return KOLM_EARG;
     const u32 nb = (u32)nb64;

@@ -118,7 +118,9 @@ struct HostMem {
 // padded to 8 bytes
 inline u64 idx_bytes(u64 nblocks) { return (8 * (nblocks + 1) + 4 * nblocks + 7) & ~7ull; }
 
-enum : int { M_BYTES = 0, M_BLOCKS = 1, M_CAP = 2, M_CAPB = 3, M_N = 4 };
+// meta words every rank contributes to a gather: sizes, the destination's capacities, the
+// destination rank it was called with and whether its own arguments were valid
+enum : int { M_BYTES = 0, M_BLOCKS = 1, M_CAP = 2, M_CAPB = 3, M_DST = 4, M_BAD = 5, M_N = 6 };
 
 }  // namespace
 
@@ -165,25 +167,27 @@ namespace {
 // kolm_encode_blocks_multi's communicator over this process's devices (ncclCommInitAll)
 struct MultiComm {
     std::mutex mu;
-    std::vector<int> devs;
+    std::vector<int> devs;     // the devices of a complete communicator (empty: none)
+    std::vector<int> sdev;     // the device of every communicator / stream slot, set before init
     std::vector<ncclComm_t> comms;
     std::vector<hipStream_t> streams;
-    DevMem dst;  // on devs[0]
+    DevMem dst;  // on sdev[0]
     void reset() noexcept {
         for (size_t i = 0; i < comms.size(); ++i) {
             if (comms[i]) (void)ncclCommDestroy(comms[i]);
-            if (streams[i]) {
-                (void)hipSetDevice(devs[i]);
+            if (i < streams.size() && streams[i]) {
+                (void)hipSetDevice(sdev[i]);
                 (void)hipStreamDestroy(streams[i]);
             }
         }
-        if (!devs.empty()) {
-            (void)hipSetDevice(devs[0]);
+        if (!sdev.empty()) {
+            (void)hipSetDevice(sdev[0]);
             dst.release();
         }
         comms.clear();
         streams.clear();
         devs.clear();
+        sdev.clear();
     }
 };
 MultiComm g_mc;
@@ -209,15 +213,23 @@ int multi_rccl_gather(const std::vector<int>& devs, const std::vector<const u8*>
             return KOLM_ECAP;
         }
         if (g_mc.devs != devs) {
+            // the cache records devs only once the communicators and streams all exist: a
+            // failure part-way leaves it empty, so the next call initialises again
             g_mc.reset();
-            g_mc.comms.assign(G, nullptr);
-            g_mc.streams.assign(G, nullptr);
-            g_mc.devs = devs;
-            KOLM_NCCL_CHECK(ncclCommInitAll(g_mc.comms.data(), G, devs.data()));
-            for (int r = 0; r < G; ++r) {
-                KOLM_HIP_CHECK(hipSetDevice(devs[r]));
-                KOLM_HIP_CHECK(hipStreamCreateWithFlags(&g_mc.streams[r], hipStreamNonBlocking));
+            try {
+                g_mc.sdev = devs;
+                g_mc.comms.assign(G, nullptr);
+                g_mc.streams.assign(G, nullptr);
+                KOLM_NCCL_CHECK(ncclCommInitAll(g_mc.comms.data(), G, devs.data()));
+                for (int r = 0; r < G; ++r) {
+                    KOLM_HIP_CHECK(hipSetDevice(devs[r]));
+                    KOLM_HIP_CHECK(hipStreamCreateWithFlags(&g_mc.streams[r], hipStreamNonBlocking));
+                }
+            } catch (...) {
+                g_mc.reset();
+                throw;
             }
+            g_mc.devs = devs;
         }
         if (!total) return KOLM_OK;
         KOLM_HIP_CHECK(hipSetDevice(devs[0]));
@@ -353,10 +365,15 @@ int kolm_gather_payloads(kolm_comm* c, const void* d_arena, uint64_t nbytes, con
                          const uint64_t* payload_off, uint32_t nblocks, int dst, void* d_dst, uint64_t dst_cap,
                          uint32_t dst_cap_blocks, uint64_t* rank_bytes, uint32_t* rank_blocks, uint32_t* method_all,
                          uint64_t* off_all, int async_op) {
-    if (!c || dst < 0 || dst >= c->nranks || (nbytes && !d_arena) || (nblocks && (!method || !payload_off)))
-        return KOLM_EARG;
-    const bool is_dst = c->rank == dst;
-    if (is_dst && ((!d_dst && dst_cap) || (!method_all && !off_all && dst_cap_blocks))) return KOLM_EARG;
+    if (!c) return KOLM_EARG;
+    // Argument errors are not returned before the collective: a rank that left early would leave
+    // the others blocked in it.  Every rank joins the size all-gather with its own verdict and the
+    // destination it was given, and all of them return KOLM_EARG together if any rank's
+    // arguments are bad or the ranks disagree on the destination.
+    const bool dst_ok = dst >= 0 && dst < c->nranks;
+    const bool is_dst = dst_ok && c->rank == dst;
+    const bool bad = !dst_ok || (nbytes && !d_arena) || (nblocks && (!method || !payload_off)) ||
+                     (is_dst && ((!d_dst && dst_cap) || (!method_all && !off_all && dst_cap_blocks)));
     return cguard([&] {
         std::lock_guard<std::mutex> g(c->mu);
         KOLM_HIP_CHECK(hipSetDevice(c->device));
@@ -369,11 +386,19 @@ int kolm_gather_payloads(kolm_comm* c, const void* d_arena, uint64_t nbytes, con
         mh[M_BLOCKS] = nblocks;
         mh[M_CAP] = is_dst ? dst_cap : 0;
         mh[M_CAPB] = is_dst ? dst_cap_blocks : 0;
+        mh[M_DST] = (u64)(int64_t)dst;
+        mh[M_BAD] = bad ? 1u : 0u;
         KOLM_HIP_CHECK(hipMemcpyAsync(md, mh, 8 * M_N, hipMemcpyHostToDevice, c->stream));
         KOLM_NCCL_CHECK(ncclAllGather(md, md + M_N, M_N, ncclUint64, c->comm, c->stream));
         KOLM_HIP_CHECK(hipMemcpyAsync(mh + M_N, md + M_N, 8ull * M_N * R, hipMemcpyDeviceToHost, c->stream));
         KOLM_HIP_CHECK(hipStreamSynchronize(c->stream));
         const u64* all = mh + M_N;
+        for (int r = 0; r < R; ++r)
+            if (all[r * M_N + M_BAD] || all[r * M_N + M_DST] != (u64)(int64_t)dst) {
+                set_err("kolm_gather_payloads: bad arguments on rank " + std::to_string(r) +
+                        " (null buffers, or destination ranks that differ or are out of range)");
+                return KOLM_EARG;
+            }
         c->rbytes.assign(R, 0);
         c->rblocks.assign(R, 0);
         c->pbase.assign(R + 1, 0);

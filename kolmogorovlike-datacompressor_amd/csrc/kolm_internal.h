@@ -360,33 +360,15 @@ u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w,
 void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s,
                    KTimer* kt = nullptr);
 
-// ---- k_r0m.hip: round 0 as MSD radix partitions + LDS bucket sorts (same outputs) ----
-constexpr int R0M_NCLS = 11;  // final bucket classes of k_r0m.hip
-struct R0MBufs {
-    u32* x0;          // [N] level buffer B: low key words
-    u32* x1;          // [N] level buffer B: positions
-    u32* hist;        // [r0m_hist_rows * 256]
-    u32* cnt;         // [16] counters
-    void* fin[R0M_NCLS];  // final bucket lists per class (12-byte records), capacities r0m_fin_cap
-    LSeg* segs[2];    // next-level segments per level parity [r0m_seg_cap]
-    LTile* tiles[2];  // their tiles [r0m_tile_cap]
-};
-u64 r0m_fin_cap(u64 N, u32 nb, int cls);
-u64 r0m_seg_cap(u64 N, u32 nb);
-u64 r0m_tile_cap(u64 N, u32 nb, u32 bs);
-u32 r0m_tiles(const Geom& geo);
-// returns the number of MSD levels run; h_cnt: pinned host scratch of >= 16 words
-u32 launch_round0_msd(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, R0MBufs& mb,
-                      hipStream_t s, KTimer* kt, u32* h_cnt);
+
 
 // ---- k_mtf.hip ----
 // bits (optional, [nb * 8], zeroed by the caller): the replay also adds each block's Rice-k
 // bit counts of the 5 BBWT candidates (counters 0..4, see k_entropy.hip) — no extra pass
 bool mtf_wave_mode(const Geom& geo);  // position-parallel MTF replay (batches of few blocks)
 u32 mtf_chunk_bytes(const Geom& geo);  // bytes per MTF chunk of this batch (launch_mtf's choice)
-bool mtf_cp_mode(const Geom& geo);     // three-launch compose (batches of few blocks)
 u64 mtf_cp_words(const Geom& geo);    // its scratch (u32 words)
-// cp_scratch ([mtf_cp_words], used when mtf_cp_mode): range states of the three-launch compose
+// cp_scratch ([mtf_cp_words]): range states of the three-launch compose
 void launch_mtf(const Geom& geo, const u8* in, u8* out, u8* summary, u16* summary_cnt, u8* states,
                 hipStream_t s, KTimer* kt = nullptr, u64* bits = nullptr, int rice_k = 2, u32* cp_scratch = nullptr);
 
@@ -473,6 +455,7 @@ struct LzArgs {
 };
 void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr);
 const char* lz_spec_name();  // the speculative-parse kernel in use (timing / roofline)
+u32 lz_chunk_shift();        // log2 of the parse's chunk bytes (LzArgs::cshift) for the form in use
 void launch_lz_emit(const LzArgs& z, const u32* method, const u64* off, u8* arena, hipStream_t s);
 
 // ---- k_repair.hip: exact Re-Pair (candidate 9), one workgroup per block ----

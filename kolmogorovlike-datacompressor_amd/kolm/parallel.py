@@ -236,7 +236,12 @@ class Comm:
         method ids and payload offsets (host arrays, as the encoder returned them) onto
         `dst`.  dst_buf: the destination's DeviceBuffer (default: a grow-only buffer of the
         communicator, sized after a first call that reports the ranks' sizes).  Returns a
-        Gathered record on dst, None elsewhere (a PendingGather of either with async_op)."""
+        Gathered record on dst, None elsewhere (a PendingGather of either with async_op).
+
+        Without dst_buf the payloads of every gather land in that one communicator buffer:
+        a Gathered record (and PendingGather.result()) stays valid only until the next
+        gather_payloads call of this communicator overwrites it.  A caller that keeps
+        several gathers alive (double-buffered steps) passes its own dst_buf per gather."""
         L = self._lib.load()
         R = self.nranks
         meth = np.ascontiguousarray(np.asarray(method, dtype=np.uint32))

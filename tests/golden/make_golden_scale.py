@@ -9,7 +9,8 @@ Adds to tests/golden/large.json, without touching the entries make_golden_large.
     enwik-style text and on the gradient BMP's first 1 MiB;
   * case "enwik_128k_repair": PY's repair_compress (PY:1841-1911, the O(n * rules)
     recount) on 128 KiB of enwik-style text (seed 77), "repair" {len, sha256};
-  * case "bench_block0_repair": the same on block 0 of bench.py's stream (1 MiB).
+  * case "bench_block0_repair": the same on block 0 of bench.py's stream (1 MiB);
+  * case "bench_block0": PY's encode_lz77 on that block.
 Arguments (optional): the case names to (re)compute.
 The GPU and the oracle are checked against these in test_gpu_parity.py / test_oracle.py.
 """
@@ -40,6 +41,9 @@ def inputs():
         # block 0 of bench.py's rank-0 stream (enwik_like(n)[:1 MiB] does not depend on n):
         # PY's Re-Pair of a whole 1 MiB bench block (about an hour)
         ("bench_block0_repair", "repair"): lambda: D.enwik_like(1 << 20),
+        # PY's LZ77 of the same bench block (round 6: the bench's LZ77 stream at 1 MiB rests on PY
+        # itself, not only on the oracle; about 5 minutes)
+        ("bench_block0", "lz77"): lambda: D.enwik_like(1 << 20),
     }
 
 

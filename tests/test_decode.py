@@ -272,3 +272,22 @@ def test_repair_containers_large(kolm_gpu):
     data = D.enwik_like(8 << 20, seed=21) + bytes(1 << 20) + b"abc" * 349_525
     blob = kolm_gpu.compress_blocks_fixed(data, 1 << 20)
     assert kolm_gpu.decompress(blob) == data
+
+
+def test_toc_cases_on_device(kolm_gpu):
+    """The PY-written corner-case containers of tests/golden/toc_cases.json through the device
+    decoders: long / shifted / oversubscribed prefix codes decode as PY decodes them, and the
+    bit-plane blocks with n % 8 != 0 (where PY raises IndexError: the pinned divergence of
+    kolm/decode.py) decode to their input."""
+    import json
+    with open(os.path.join(GOLDEN, "toc_cases.json")) as f:
+        cases = json.load(f)
+    for name, c in cases.items():
+        blob = bytes.fromhex(c["container"])
+        if name.startswith("bitplane"):
+            assert kolm_gpu.decompress(blob) == bytes.fromhex(c["input"]), name
+        elif "ok" in c["py"]:
+            assert kolm_gpu.decompress(blob) == bytes.fromhex(c["py"]["ok"]), name
+        else:
+            with pytest.raises(ValueError, match=c["py"]["message"]):
+                kolm_gpu.decompress(blob)

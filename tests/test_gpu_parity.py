@@ -130,6 +130,18 @@ def test_large_known_answers(kolm_gpu, large_known, case):
         assert len(z) == ref["lz77"]["len"] and sha(z) == ref["lz77"]["sha256"], "lz77"
 
 
+def test_bench_block0_lz77_vs_py(kolm_gpu, large_known):
+    """Block 0 of the bench stream (enwik_like, 1 MiB): the LZ77 stream against sha256 of PY's own
+    encode_lz77 on it (make_golden_scale.py), so the bench's LZ77 at 1 MiB rests on PY itself."""
+    ref = large_known.get("bench_block0")
+    if ref is None or "lz77" not in ref:
+        pytest.skip("no PY LZ77 known answer for bench block 0")
+    data = D.enwik_like(1 << 20)
+    assert sha(data) == ref["input"]["sha256"]
+    z = kolm_gpu.encode_lz77(data)[0]
+    assert len(z) == ref["lz77"]["len"] and sha(z) == ref["lz77"]["sha256"]
+
+
 def _oracle_all(block: bytes):
     return [O.candidate(m, block) for m in range(10)]
 
@@ -306,6 +318,33 @@ def test_encode_blocks_multi(kolm_gpu, ngpu):
     b = _lib.encode_blocks_multi(data, bs, ngpu)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
     assert kolm_gpu.compress_blocks_fixed(data, bs, devices=ngpu) == O.compress_blocks_fixed(data, bs, range(10))
+
+
+def test_encode_blocks_multi_threads(kolm_gpu):
+    """Two host threads calling kolm_encode_blocks_multi at once (each device's
+    payloads wait in its context's arena between the encode and the gather; the calls are
+    serialised inside the library, so neither sees the other's payloads)."""
+    import threading
+    from kolm import _lib
+    ins = [(D.enwik_like(300_000, seed=11), 32768), (D.mixed_corpus()[:500_000], 65536)]
+    want = [_lib.encode_blocks(d, bs) for d, bs in ins]
+    got = [None, None]
+    errs = []
+
+    def run(i):
+        try:
+            for _ in range(3):
+                got[i] = _lib.encode_blocks_multi(ins[i][0], ins[i][1], 1)
+                assert np.array_equal(got[i][1], want[i][1]) and got[i][2] == want[i][2]
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errs, errs
 
 
 RP_LARGE = {

@@ -1,18 +1,14 @@
-"""The measured-and-kept round-5 forms of the cyclic sort and the MTF stage have A/B switches that
-restore the previous form.  Both sides of every switch must stay exact: each case
-runs the hot-path candidates with the switch off and compares every block's sizes and winner
-payload with the oracle (PY:351-423 BBWT order, PY:460 MTF, PY:1413 Rice, PY:2350-2369 MDL).
+"""Product forms chosen by batch shape, forced onto inputs they would not otherwise see (DESIGN.md
+§9; the switches that selected measured-slower forms were removed in round 6).  Each case runs
+the hot-path candidates with the switch set and compares every block's sizes and winner payload
+with the oracle (PY:351-423 BBWT order, PY:460 MTF, PY:1413 Rice, PY:2350-2369 MDL).
 
-  KOLM_LSD_REC=0    LSD passes exchange (key, position) in two u32 arrays instead of u64 records
-  KOLM_R0_PART=0    round 0's padding bits stay zero (no partial next character)
-  KOLM_R0_PART=2    only the top 2 bits of the next character
-  KOLM_LSD_PACK=0   no packed first-half pass;  KOLM_LSD_SCAN2=0: per-block LSD scans
-  KOLM_MTF_CP=0     one-workgroup-per-block MTF compose
-  KOLM_DUVAL_GRP=0  Duval span merges a thread per merge (a wave from level 4096)
   KOLM_MTF_WAVE=0   the per-thread MTF replay (and its SWAR Rice sums) on batches of few blocks,
                     with chunks of 128..512 bytes and ragged block ends
-  KOLM_EARLY_GATHER=0/1/2  one BBWT gather after the rounds / the early gather on the third stream
-                    from doubling round 1 / 2 on, the slots of that round's segments again after them
+  KOLM_MTF_WAVE=1   the position-parallel MTF replay on a batch of 64 blocks or more
+  KOLM_PREVC_IDX=1  k_prevc on the index stream below 16 blocks (with 16+ blocks: the early BBWT
+                    gather from doubling round 3 on the third stream)
+  KOLM_LZ_BIGWIN=0/1  the LZ77 stitch's 5 KiB / 62 KiB brute-force window
 """
 import pytest
 
@@ -23,16 +19,11 @@ from kolm import datagen as D
 pytestmark = pytest.mark.gpu
 
 SWITCHES = [
-    {"KOLM_LSD_REC": "0"},
-    {"KOLM_R0_PART": "0"},
-    {"KOLM_R0_PART": "2"},
-    {"KOLM_LSD_PACK": "0", "KOLM_LSD_SCAN2": "0"},
-    {"KOLM_MTF_CP": "0"},
-    {"KOLM_DUVAL_GRP": "0"},
     {"KOLM_MTF_WAVE": "0"},
-    {"KOLM_EARLY_GATHER": "0"},
-    {"KOLM_EARLY_GATHER": "1"},
-    {"KOLM_EARLY_GATHER": "2"},
+    {"KOLM_MTF_WAVE": "1"},
+    {"KOLM_PREVC_IDX": "1"},
+    {"KOLM_LZ_BIGWIN": "0"},
+    {"KOLM_LZ_BIGWIN": "1"},
 ]
 
 
@@ -44,6 +35,8 @@ def _inputs():
         ("text_64k", text, 65536),
         ("mixed_16k", text[:30000] + rnd[:9000] + bytes(5000) + per[:7000], 16384),
         ("gradient_128k", D.gradient_bmp()[: 1 << 17], 1 << 17),
+        # 20 blocks of 16 KiB: prevc on the index stream and the early BBWT gather (from 16 blocks)
+        ("text_20x16k", D.enwik_like(20 * 16384, seed=58), 16384),
     ]
 
 

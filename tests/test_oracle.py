@@ -88,6 +88,19 @@ def test_oracle_large_known_answers(large_known, case):
         assert (len(z), sha(z)) == (ref["lz77"]["len"], ref["lz77"]["sha256"])
 
 
+def test_oracle_bench_block0_lz77_vs_py(large_known):
+    """The oracle's exhaustive LZ77 on block 0 of the bench stream against PY's own
+    encode_lz77 (make_golden_scale.py): the bench stream's LZ77 answers (bench_stream.json, made
+    by the oracle) rest on PY at the bench's block size."""
+    ref = large_known.get("bench_block0")
+    if ref is None or "lz77" not in ref:
+        pytest.skip("no PY LZ77 known answer for bench block 0")
+    data = D.enwik_like(1 << 20)
+    z = O.encode_lz77(data)
+    assert hashlib.sha256(data).hexdigest() == ref["input"]["sha256"]
+    assert (len(z), hashlib.sha256(z).hexdigest()) == (ref["lz77"]["len"], ref["lz77"]["sha256"])
+
+
 def test_survey_lengths_gradient_lz77():
     """gradient[0:1 MiB] LZ77 stream is 1693900 bytes (reference C++,
     identical to PY); our restatement reproduces the length."""

@@ -8,7 +8,8 @@
 
 typedef uint32_t u32;
 typedef uint8_t u8;
-enum { W = 4096, HOME = 4096, CH = 256, LEAD = 48, LPC = 16 };
+enum { W = 4096, HOME = 4096, CH = 256, LEAD = 48 };
+static u32 LPC = 16;
 
 static const u8* T;
 static int HB = 10;
@@ -33,6 +34,7 @@ int main(int argc, char** argv) {
     FILE* f = fopen(argv[1], "rb");
     u32 mib = argc > 2 ? atoi(argv[2]) : 1;
     if (argc > 3) HB = atoi(argv[3]);
+    if (argc > 4) LPC = atoi(argv[4]);
     N = mib << 20;
     u8* buf = malloc(N + 64);
     N = fread(buf, 1, N, f);
