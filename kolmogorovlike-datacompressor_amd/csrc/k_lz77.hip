@@ -539,7 +539,7 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
 //
 // Index build: each wave takes a contiguous quarter of the window's 3-gram positions, 64 at
 // a time in order; a lane's previous same-hash position is the nearest lower lane of its
-// match-any group (LZC_HB ballots) or, for the group's lowest lane, the wave's running head
+// match-any group (HB ballots) or, for the group's lowest lane, the wave's running head
 // table; the group's highest lane updates the head.  After a barrier the first occurrences
 // of each later quarter take the last occurrence from the heads of the quarters before it.
 //
@@ -551,12 +551,11 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
 constexpr u32 LZC_CH = 64;                 // chunk bytes (one lane)
 constexpr u32 LZC_CSHIFT = 6;
 static_assert((1u << LZC_CSHIFT) == LZC_CH, "chunk shift");
-constexpr u32 LZC_HB = 11;                 // hash bits of the chains
-constexpr u32 LZC_NB = 1u << LZC_HB;
 constexpr u16 LZC_NONE = 0xFFFFu;
+template <u32 HB>  // hash bits of the chains
 __device__ inline u32 hash3c(const u8* t, u32 x) {
     const u32 k = ((u32)t[x] << 16) | ((u32)t[x + 1] << 8) | t[x + 2];
-    return (k * 0x9E3779B1u) >> (32 - LZC_HB);
+    return (k * 0x9E3779B1u) >> (32 - HB);
 }
 
 template <u32 NWV>
@@ -569,10 +568,11 @@ struct LzcGeom {
 };
 
 
-template <u32 NWV>
+template <u32 NWV, u32 HB>
 __global__ __launch_bounds__(64 * NWV) void k_lz_lanes(LzArgs z, u32 hpb, u32 lead) {
     using G = LzcGeom<NWV>;
     constexpr u32 NT = G::NT;
+    constexpr u32 LZC_NB = 1u << HB;
     __shared__ __align__(16) u8 txt[G::TXT];
     __shared__ __align__(16) u16 prv[G::NW];
     __shared__ __align__(16) u16 heads[NWV][LZC_NB];
@@ -619,10 +619,10 @@ __global__ __launch_bounds__(64 * NWV) void k_lz_lanes(LzArgs z, u32 hpb, u32 le
     for (u32 x0 = r0; x0 < r1; x0 += 64) {  // wave-uniform
         const u32 x = x0 + lane;
         const bool valid = x < r1;
-        const u32 hv = valid ? hash3c(tw, x) : 0u;
+        const u32 hv = valid ? hash3c<HB>(tw, x) : 0u;
         u64 m = __ballot(valid);
 #pragma unroll
-        for (u32 bit = 0; bit < LZC_HB; ++bit) {
+        for (u32 bit = 0; bit < HB; ++bit) {
             const u64 bal = __ballot((hv >> bit) & 1u);
             m &= ((hv >> bit) & 1u) ? bal : ~bal;
         }
@@ -638,7 +638,7 @@ __global__ __launch_bounds__(64 * NWV) void k_lz_lanes(LzArgs z, u32 hpb, u32 le
         // a later quarter's first occurrence of a hash: the last one of the quarters before it
         for (u32 x = r0 + lane; x < r1; x += 64) {
             if (prv[x] != LZC_NONE) continue;
-            const u32 hv = hash3c(tw, x);
+            const u32 hv = hash3c<HB>(tw, x);
             u32 pv = LZC_NONE;
             for (u32 v = w; v-- > 0;) {
                 pv = heads[v][hv];
@@ -1292,9 +1292,19 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
             getenv("KOLM_LZ_LEAD") ? std::min<u32>(atoi(getenv("KOLM_LZ_LEAD")), LZL_LEAD) : 48u;
         KScope k(kt, KT_LZPARSE, "k_lz_local", z.geo.N * 2);
         if (z.cshift == LZC_CSHIFT) {
-            constexpr u32 NWV = 4;
-            const u32 hpl = (z.geo.bs + LzcGeom<NWV>::HOME - 1) / LzcGeom<NWV>::HOME;
-            k_lz_lanes<NWV><<<z.geo.nb * hpl, LzcGeom<NWV>::NT, 0, s>>>(z, hpl, lead);
+            // KOLM_LZ_LANES (A/B): 1 = 16 KiB homes, 11 hash bits (78 KB of LDS: 2 workgroups per
+            // CU); 2 = 16 KiB, 10 bits (70 KB); 3 = 8 KiB homes, 11 bits (45 KB: 3 per CU)
+            const int mode = lz_lanes_mode();
+            auto go = [&](auto kern, u32 home, u32 nt) {
+                const u32 hpl = (z.geo.bs + home - 1) / home;
+                kern<<<z.geo.nb * hpl, nt, 0, s>>>(z, hpl, lead);
+            };
+            if (mode == 2)
+                go(k_lz_lanes<4, 10>, LzcGeom<4>::HOME, LzcGeom<4>::NT);
+            else if (mode == 3)
+                go(k_lz_lanes<2, 11>, LzcGeom<2>::HOME, LzcGeom<2>::NT);
+            else
+                go(k_lz_lanes<4, 11>, LzcGeom<4>::HOME, LzcGeom<4>::NT);
         } else {
             k_lz_local<home, 16><<<z.geo.nb * hpb, LzlGeom<home, 16>::NT, 0, s>>>(z, hpb, lead);
         }

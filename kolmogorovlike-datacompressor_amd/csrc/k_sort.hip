@@ -257,7 +257,7 @@ __global__ __launch_bounds__(256) void k_classify(const Seg* cur, u32 ncur_in, c
     __syncthreads();
     // each workgroup walks one contiguous share of the list (concurrent workgroups then work
     // in different regions of it, so the per-(class, bin) atomics of MODE 1 / 2 do not pile on
-    // the same few counters; KOLM_CLS_CHUNK=0: the grid-stride walk)
+    // the same few counters)
     const u32 per = ((ncur + gridDim.x * 256 - 1) / (gridDim.x * 256)) * 256;
     const u32 wbeg = a.cls_chunk ? min(blockIdx.x * per, ncur) : blockIdx.x * 256;
     const u32 wend = a.cls_chunk ? min(wbeg + per, ncur) : ncur;
@@ -1108,11 +1108,6 @@ void launch_iota(u32* SA, u64 N, hipStream_t s) {
 }
 void launch_block_segs(Seg* segs, const Geom& geo, hipStream_t s) {
     if (geo.nb) k_block_segs<<<cdiv(geo.nb, 256), 256, 0, s>>>(segs, geo);
-}
-void launch_classify(const Seg* cur, u32 ncur, const u32* ncur_dev, const SortArgs& a, const Lists& L,
-                     const Level& lv0, hipStream_t s) {
-    if (ncur)
-        k_classify<0><<<std::min<u32>(cdiv(ncur, 256), 2048u), 256, 0, s>>>(cur, ncur, ncur_dev, a, L, lv0, Bins{});
 }
 __global__ void k_zero_spans(ZeroSpans z) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -369,8 +369,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
     // large groups are few anyway — 256 MiB text: 41.8 vs 37.5 ms per step with it)
     static const int med = getenv("KOLM_MED_SORT") ? atoi(getenv("KOLM_MED_SORT")) : -1;
     a.med = (med > 0 || (med < 0 && geo.nb < 64)) ? 1u : 0u;
-    static const bool cls_chunk = !(getenv("KOLM_CLS_CHUNK") && atoi(getenv("KOLM_CLS_CHUNK")) == 0);
-    a.cls_chunk = cls_chunk ? 1u : 0u;
+    a.cls_chunk = 1u;  // k_classify: one contiguous list share per workgroup (1.36 -> 1.29 ms per step)
 
     u32* cnt = c->get<u32>("counters", C_N);
     Lists L{};
@@ -430,8 +429,8 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
     // classes 1..tiny_c: one thread per segment (k_tiny_sort); larger: LDS sorts.  Class 5
     // (17-32 elements) goes to the LDS sort: k_tiny_sort<5> holds 32 64-bit words in 144
     // VGPRs and was starved beside the LZ77 parse (1.0 ms alone, 3.0 overlapped; step 45.7
-    // -> 44.0 ms).  A/B switch KOLM_TINY_C (1..TINY_C)
-    static const int tiny_c = getenv("KOLM_TINY_C") ? std::max(1, std::min(TINY_C, atoi(getenv("KOLM_TINY_C")))) : 4;
+    // -> 44.0 ms); class 4 to the LDS sort as well measured 41.8-41.9 -> 42.0-42.1 ms
+    constexpr int tiny_c = 4;
     for (u32 round = 0; round < 64 && ncur; ++round) {
         a.initial = round == 0 ? 1 : 0;
         a.h = round == 0 ? 0u : (h0 << (round - 1));
@@ -442,8 +441,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
         // the round's counters, split flags and (position-ordered lists) classify bins in one
         // launch: hipMemsetAsync fills are ~4.5 us kernels each on the sort stream (config 5:
         // 151 per batch, 0.68 ms)
-        static const bool bin_lists = !(getenv("KOLM_CLS_BIN") && atoi(getenv("KOLM_CLS_BIN")) == 0);
-        const bool zero_bins = bin_lists && !(round == 0 && cyclic);
+        const bool zero_bins = !(round == 0 && cyclic);
         {
             ZeroSpans z{};
             z.p[0] = L.next_cnt;
@@ -464,14 +462,13 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
         }
         if (round == 0 && cyclic) {
             // round 0: stable LSD passes over the packed codes of the first C rotation
-            // characters (KOLM_R0_ALPHA=0: raw bytes, C = 8), no host round trips but one
-            static const bool compact = !(getenv("KOLM_R0_ALPHA") && atoi(getenv("KOLM_R0_ALPHA")) == 0);
+            // characters (alphabet-compacted codes), no host round trips but one
+            constexpr bool compact = true;
             const u64 nt = lsd_tiles(geo) + 1;
             u8* code = c->get<u8>("r0code", (u64)geo.nb * 256);
             const u32 w = launch_alpha(geo, text, c->get<u32>("r0pres", (u64)geo.nb * 8), code, cnt + C_ALPHA,
                                        h + C_ALPHA, compact, s, c->kt());
-            static const u32 cmax = getenv("KOLM_R0_CMAX") ? (u32)atoi(getenv("KOLM_R0_CMAX")) : 32u;  // A/B (<= 64)
-            const u32 C = std::max<u32>(1, std::min<u32>(std::min<u32>(64, cmax), 64 / w));
+            const u32 C = std::max<u32>(1, std::min<u32>(32, 64 / w));
             h0 = C;
             R0Bufs r{text, FEd, fac, code, C, w, c->get<u32>("KP", N), a.K2, a.SA, a.K22, a.SA2, a.RK,
                      c->get<u32>("r0hist", nt * 256), c->get<u32>("r0tmax", nt), c->get<u32>("r0tmin", nt),
@@ -496,19 +493,13 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             continue;
         }
         {
-            // position-ordered class lists (default; A/B switch KOLM_CLS_BIN=0: arbitrary order)
-            static const bool bin = !(getenv("KOLM_CLS_BIN") && atoi(getenv("KOLM_CLS_BIN")) == 0);
-            TScope t(c, KOLM_KT_CLASSIFY, "k_classify", (u64)ncur * (bin ? 24 : 16));
-            if (bin) {
-                const u32 nbits = bitlen((u32)(N - 1));
-                const Bins bn{c->get<u32>("cls_bins", NCLASS * CLS_NBIN), c->get<u32>("cls_fill", NCLASS * CLS_NBIN),
-                              nbits > 10 ? nbits - 10 : 0u};
-                launch_classify_bins(cur, ncur, ncur_dev, a, L, lv[0], bn, s, zero_bins);
-                a.xcd = 1;
-            } else {
-                launch_classify(cur, ncur, ncur_dev, a, L, lv[0], s);
-                a.xcd = 0;
-            }
+            // position-ordered class lists
+            TScope t(c, KOLM_KT_CLASSIFY, "k_classify", (u64)ncur * 24);
+            const u32 nbits = bitlen((u32)(N - 1));
+            const Bins bn{c->get<u32>("cls_bins", NCLASS * CLS_NBIN), c->get<u32>("cls_fill", NCLASS * CLS_NBIN),
+                          nbits > 10 ? nbits - 10 : 0u};
+            launch_classify_bins(cur, ncur, ncur_dev, a, L, lv[0], bn, s, zero_bins);
+            a.xcd = 1;
         }
         KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
         c->sync();
@@ -529,7 +520,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             // Dense rounds: keys by position first (sequential pass), then one gather per
             // slot; sparse rounds gather the key inputs per active slot directly.
             a.KP = nullptr;
-            static const u64 ddiv = getenv("KOLM_DENSE_DIV") ? strtoull(getenv("KOLM_DENSE_DIV"), nullptr, 10) : 8;  // A/B
+            constexpr u64 ddiv = 8;  // dense when more than 1/8 of the positions are active
             if ((u64)h[C_ACTIVE] * ddiv > N) {
                 u32* KP = c->get<u32>("KP", N);
                 // cyclic: FEd 1 + RK 4 + KP 4 (factor starts only within h of a factor end); linear: RK 4 + KP 4
@@ -757,8 +748,7 @@ struct Pipeline {
         z.nfix = c->get<u32>("counters", C_N) + C_NFIX;
         static const bool lz_prof = getenv("KOLM_LZ_PROF") && atoi(getenv("KOLM_LZ_PROF")) != 0;
         if (lz_prof) z.prof = c->get<u64>("lz_prof", 32);
-        const char* sr = getenv("KOLM_STITCH_RUNS");
-        z.stitch_runs = sr && atoi(sr) == 0 ? 0u : 1u;
+        z.stitch_runs = 1u;
         return z;
     }
 

@@ -293,8 +293,6 @@ void launch_pack_spans(const PackSpans& ps, u32* dst, hipStream_t s);
 // ncur: the list length, or (ncur_dev set) a bound for the grid with the length in ncur_dev
 void launch_classify_bins(const Seg* cur, u32 ncur, const u32* ncur_dev, const SortArgs& a, const Lists& L,
                           const Level& lv0, const Bins& bn, hipStream_t s, bool bins_zeroed = false);
-void launch_classify(const Seg* cur, u32 ncur, const u32* ncur_dev, const SortArgs& a, const Lists& L,
-                     const Level& lv0, hipStream_t s);
 void launch_keypos(const SortArgs& a, u32* KP, hipStream_t s);
 void launch_keygen_small(int c, const Seg* segs, u32 count, const SortArgs& a, hipStream_t s);
 void launch_keygen_large(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
