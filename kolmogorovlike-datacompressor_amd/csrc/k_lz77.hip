@@ -387,7 +387,7 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
     bool alive = has && p < e;
     u32 k = 0, qa = 0, best = 0, bd = 0, lim = 0, capl = 0;
     bool qok = false;  // qa holds the entry of this lane's slot (false: below slot 0)
-    u64 pv = 0;
+    u64 pv = 0, pv1 = 0;  // p's first 16 bytes
     u32 ntok = 0, off = 0, nlong = 0, nbuf = 0, nbatch = 0;
     u32 bpos = 0, blen = 0, bdist = 0, boff = 0;
     bool un = false;
@@ -399,6 +399,7 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
         capl = min((u32)LZ_CAP, lim);
         k = p + (u32)LZ_MIN <= end ? (u32)isl[p - ilo] : 0u;
         pv = lds8(txt, p - tlo);
+        pv1 = lds8(txt, p - tlo + 8);
         qok = k > hl;
         qa = A[qok ? k - 1 - hl : 0u];
     };
@@ -410,39 +411,42 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
         // window (or below slot 0)
         const u32 q = lo + (qa & 0x3FFFu);
         const u32 qr = q - tlo;
-        // the candidate's first 8 bytes, loaded for every lane (an entry past the walk's end
-        // still lies in the window)
+        // the candidate's first 16 bytes, loaded for every lane (an entry past the walk's end
+        // still lies in the window): one LDS round trip decides almost every candidate (on text
+        // 13 % of the same-3-gram candidates share 8 bytes with p, ~0.3 % share 16)
         const u32* cw = reinterpret_cast<const u32*>(txt) + (qr >> 2);
-        const u32 c0 = cw[0], c1 = cw[1], c2 = cw[2];
+        const u32 c0 = cw[0], c1 = cw[1], c2 = cw[2], c3 = cw[3], c4 = cw[4];
         // the next batch's entries, in the same LDS round trip (loaded unconditionally from a
         // clamped slot: no branch splits the loads)
         const bool qnok = k > LPC + hl;
         const u32 qn = A[qnok ? k - LPC - 1 - hl : 0u];
-        const u64 cv = ((u64)__builtin_amdgcn_alignbyte(c2, c1, qr & 3) << 32) | __builtin_amdgcn_alignbyte(c1, c0, qr & 3);
+        const u32 sh = qr & 3;
+        const u64 cv = ((u64)__builtin_amdgcn_alignbyte(c2, c1, sh) << 32) | __builtin_amdgcn_alignbyte(c1, c0, sh);
+        const u64 cv1 = ((u64)__builtin_amdgcn_alignbyte(c4, c3, sh) << 32) | __builtin_amdgcn_alignbyte(c3, c2, sh);
         const bool bad = !qok || p - q > (u32)LZ_WINDOW;
         const u64 sm = __ballot(alive && (bad || (qa & LZC_HEAD))) & GM;
         const bool valid = alive && !bad && !(sm & below);
-        u32 l = 0;
-        const u64 d0 = pv ^ cv;
-        if (valid && (d0 & 0xFFFFFFull) == 0) {  // the same 3-gram, not only the same hash
-            if (d0) {
-                l = (u32)(__ffsll((long long)d0) - 1) >> 3;
-            } else if (best < 8 || (best < lim && T[p + best] == T[q + best])) {
-                const u32 pr = p - tlo;
-                l = 8;
+        const u64 d0 = pv ^ cv, d1 = pv1 ^ cv1;
+        // the same 3-gram (not only the same hash): length from the first differing byte of 16
+        u32 l = (valid && (d0 & 0xFFFFFFull) == 0)
+                    ? (d0 ? (u32)(__ffsll((long long)d0) - 1) >> 3
+                          : d1 ? 8u + ((u32)(__ffsll((long long)d1) - 1) >> 3) : 16u)
+                    : 0u;
+        if (l == 16 && capl > 16 && (best < 16 || (best < lim && T[p + best] == T[q + best]))) {
+            // 16 equal bytes (rare): a strictly longer match must also match at `best`
+            const u32 pr = p - tlo;
 #pragma unroll
-                for (int kk = 1; kk < LZ_CAP / 8; ++kk) {
-                    if (l >= capl) break;
-                    const u64 d = lds8(txt, pr + 8 * kk) ^ lds8(txt, qr + 8 * kk);
-                    if (d) {
-                        l += (u32)(__ffsll((long long)d) - 1) >> 3;
-                        break;
-                    }
-                    l += 8;
+            for (int kk = 2; kk < LZ_CAP / 8; ++kk) {
+                if (l >= capl) break;
+                const u64 d = lds8(txt, pr + 8 * kk) ^ lds8(txt, qr + 8 * kk);
+                if (d) {
+                    l += (u32)(__ffsll((long long)d) - 1) >> 3;
+                    break;
                 }
+                l += 8;
             }
-            l = min(l, capl);
         }
+        l = min(l, capl);
         u64 longm = __ballot(valid && l >= capl && capl < lim);
         while (longm) {
             const u32 j = (u32)__ffsll((long long)longm) - 1;
@@ -509,263 +513,6 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
         if (lane == 0) {
             atomicAdd(z.prof + 4, (u64)nbatch);
             atomicAdd(z.prof + 5, (u64)nbatch);
-        }
-        __syncthreads();
-        if (tid == 0) {
-            const u64 t4 = wall_clock64();
-            atomicAdd(z.prof + 0, t1 - t0);
-            atomicAdd(z.prof + 1, t2 - t1);
-            atomicAdd(z.prof + 2, t3 - t2);
-            atomicAdd(z.prof + 3, t4 - t3);
-            atomicAdd(z.prof + 6, (u64)1);
-        }
-    }
-}
-
-// =====================================================================================
-// k_lz_lanes: a chain per LANE over 64-byte chunks, candidates from hash chains.
-//
-// k_lz_local gives each chain 16 lanes (the 16 nearest candidates of a token compared at
-// once) and a workgroup 16 chains: the LDS a chain needs (its share of the 4 KiB home plus
-// the 4 KiB history, indexed) leaves room for 64 chains per CU, and every token costs a
-// whole-wave instruction stream (~185 VALU per trip).  Here every lane is a chain: it walks
-// its token's candidates one per trip, nearest first, through a per-position hash chain
-// prv[x] = the previous window position whose 3-gram has x's hash (one LDS round trip per
-// candidate: the candidate's text and its own prv entry are independent loads).  A
-// workgroup of NWV waves owns a home of NWV x 64 chunks of 64 bytes (16 KiB at four waves):
-// the window [home - 4096 - LZL_LEAD, home end + LZL_CAPX) costs 3 bytes of LDS per
-// position (text + prv), so a CU holds 512 chains instead of 64 and a trip is ~35 VALU for
-// 64 chains instead of ~185 for 4.
-//
-// Index build: each wave takes a contiguous quarter of the window's 3-gram positions, 64 at
-// a time in order; a lane's previous same-hash position is the nearest lower lane of its
-// match-any group (HB ballots) or, for the group's lowest lane, the wave's running head
-// table; the group's highest lane updates the head.  After a barrier the first occurrences
-// of each later quarter take the last occurrence from the heads of the quarters before it.
-//
-// The chunk / token records are those of k_lz_local (LzArgs, cshift 6), so k_lz_stitch_l
-// and k_lz_emit run unchanged: a chain starts `lead` bytes before its chunk (tokens before
-// the chunk start not recorded); matches are exact up to LZL_CAPX past the chunk end, a
-// longer one ends the chunk unresolved for the stitch.
-// =====================================================================================
-constexpr u32 LZC_CH = 64;                 // chunk bytes (one lane)
-constexpr u32 LZC_CSHIFT = 6;
-static_assert((1u << LZC_CSHIFT) == LZC_CH, "chunk shift");
-constexpr u16 LZC_NONE = 0xFFFFu;
-template <u32 HB>  // hash bits of the chains
-__device__ inline u32 hash3c(const u8* t, u32 x) {
-    const u32 k = ((u32)t[x] << 16) | ((u32)t[x + 1] << 8) | t[x + 2];
-    return (k * 0x9E3779B1u) >> (32 - HB);
-}
-
-template <u32 NWV>
-struct LzcGeom {
-    static constexpr u32 NT = 64 * NWV;                    // threads = chains
-    static constexpr u32 HOME = NT * LZC_CH;                 // home bytes
-    static constexpr u32 NW = HOME + LZ_WINDOW + LZL_LEAD;   // window positions
-    static constexpr u32 TXT = NW + LZL_CAPX + 32;           // text window + alignment + compare slack
-    static_assert(NW < LZC_NONE, "window offsets in 16 bits");
-};
-
-
-template <u32 NWV, u32 HB>
-__global__ __launch_bounds__(64 * NWV) void k_lz_lanes(LzArgs z, u32 hpb, u32 lead) {
-    using G = LzcGeom<NWV>;
-    constexpr u32 NT = G::NT;
-    constexpr u32 LZC_NB = 1u << HB;
-    __shared__ __align__(16) u8 txt[G::TXT];
-    __shared__ __align__(16) u16 prv[G::NW];
-    __shared__ __align__(16) u16 heads[NWV][LZC_NB];
-    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const u32 b = blockIdx.x / hpb, h = blockIdx.x - b * hpb;
-    const u32 base = z.geo.base(b), end = z.geo.end(b);
-    const u32 hs = base + h * G::HOME;
-    if (hs >= end) return;
-    const u32 he = min(hs + G::HOME, end);
-    const u32 lo = hs - base > (u32)(LZ_WINDOW + LZL_LEAD) ? hs - LZ_WINDOW - LZL_LEAD : base;
-    const u32 hi = min(end, he + (u32)LZL_CAPX);
-    const u32 tlo = lo & ~3u;
-    u64 t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-    if (z.prof) t0 = wall_clock64();
-    {
-        const u32 n = hi - tlo;
-        if (((uintptr_t)z.text & 15) == 0) {  // 16-byte loads (tlo is 4-aligned)
-            const u32 hd = (16 - (tlo & 15)) & 15;
-            for (u32 i = tid; i < min(hd, n); i += NT) txt[i] = z.text[tlo + i];
-            const uint4* src = reinterpret_cast<const uint4*>(z.text + tlo + hd);
-            const u32 n16 = (n - min(hd, n)) / 16;
-            for (u32 i = tid; i < n16; i += NT) {
-                const uint4 v = src[i];
-                u32* d = reinterpret_cast<u32*>(txt + hd + 16 * i);
-                d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
-            }
-            for (u32 i = hd + 16 * n16 + tid; i < n; i += NT) txt[i] = z.text[tlo + i];
-        } else {
-            for (u32 i = tid; i < n; i += NT) txt[i] = z.text[tlo + i];
-        }
-    }
-    for (u32 i = tid; i < NWV * LZC_NB / 2; i += NT) reinterpret_cast<u32*>(&heads[0][0])[i] = 0xFFFFFFFFu;
-    __syncthreads();
-    if (z.prof) t1 = wall_clock64();
-    // ---- index: prv of every 3-gram position of the window [lo, top) ----
-    const u32 lim3 = end - base >= 3 ? end - 2 : base;
-    const u32 top = min(he, lim3);
-    const u32 nw = top > lo ? top - lo : 0u;
-    const u8* tw = txt + (lo - tlo);
-    const u32 Q = (nw + NWV - 1) / NWV;
-    const u32 r0 = min(w * Q, nw), r1 = min(r0 + Q, nw);
-    const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    const u64 gt = lane < 63 ? (~0ull << (lane + 1)) : 0ull;
-    for (u32 x0 = r0; x0 < r1; x0 += 64) {  // wave-uniform
-        const u32 x = x0 + lane;
-        const bool valid = x < r1;
-        const u32 hv = valid ? hash3c<HB>(tw, x) : 0u;
-        u64 m = __ballot(valid);
-#pragma unroll
-        for (u32 bit = 0; bit < HB; ++bit) {
-            const u64 bal = __ballot((hv >> bit) & 1u);
-            m &= ((hv >> bit) & 1u) ? bal : ~bal;
-        }
-        if (valid) {
-            const u64 lower = m & lt;
-            const u32 pv = lower ? x0 + 63 - (u32)__clzll(lower) : (u32)heads[w][hv];
-            prv[x] = (u16)pv;
-            if (!(m & gt)) heads[w][hv] = (u16)x;
-        }
-    }
-    __syncthreads();
-    if (w) {
-        // a later quarter's first occurrence of a hash: the last one of the quarters before it
-        for (u32 x = r0 + lane; x < r1; x += 64) {
-            if (prv[x] != LZC_NONE) continue;
-            const u32 hv = hash3c<HB>(tw, x);
-            u32 pv = LZC_NONE;
-            for (u32 v = w; v-- > 0;) {
-                pv = heads[v][hv];
-                if (pv != LZC_NONE) break;
-            }
-            prv[x] = (u16)pv;
-        }
-    }
-    if (z.prof) t2 = wall_clock64();
-    __syncthreads();
-    if (z.prof) t3 = wall_clock64();
-
-    // ---- parse: chain tid owns chunk [s, e) ----
-    const WinText T{txt, tlo};
-    const u32 s = hs + tid * LZC_CH;
-    const bool has = s < end;
-    const u32 e = has ? min(s + LZC_CH, end) : 0u;
-    const u32 c = b * z.cpb + h * NT + tid;
-    const u32 lend = has ? min(end, e + (u32)LZL_CAPX) : 0u;
-    u32 p = has ? ((tid == 0 && hs == base) ? s : (s - base > lead ? s - lead : base)) : 0u;
-    bool alive = has && p < e;
-    u32 q = NONE, best = 0, bd = 0, lim = 0, capl = 0, ntok = 0, off = 0, nlong = 0, ntrip = 0;
-    u64 pv = 0;
-    bool un = false;
-    // a candidate at q (q < p) is in the walk while it is within the window
-    auto first_cand = [&](u32 x) -> u32 {
-        if (x + (u32)LZ_MIN > end) return NONE;
-        const u32 v = prv[x - lo];
-        return v == LZC_NONE ? NONE : lo + v;
-    };
-    auto setup = [&]() {
-        best = 0;
-        bd = 0;
-        lim = lend - p;
-        capl = min((u32)LZ_CAP, lim);
-        pv = lds8(txt, p - tlo);
-        q = first_cand(p);
-    };
-    // one token: record it (tokens from the chunk start on), advance
-    auto finish = [&]() {
-        const u32 len = best >= (u32)LZ_MIN ? best : 0u;
-        const u32 dist = len ? bd : 0u;
-        un = un || (len && best >= lim && lim < end - p);
-        if (p >= s) {
-            const u32 slot = s + ntok;
-            z.tok_pos[slot] = p;
-            z.tok_len[slot] = len;
-            z.tok_dist[slot] = dist;
-            z.tok_off[slot] = off;
-            ++ntok;
-            off += len ? 1u + uleb_n(len) + uleb_n(dist) : 2u;
-        }
-        p += len ? len : 1u;
-        alive = p < e;
-    };
-    if (alive) setup();
-    while (__ballot(alive)) {
-        ++ntrip;
-        const bool ok = alive && q != NONE && p - q <= (u32)LZ_WINDOW;
-        u32 l = 0, qc = q;
-        if (ok) {
-            const u32 qr = q - tlo;
-            const u32* cw = reinterpret_cast<const u32*>(txt) + (qr >> 2);
-            const u32 c0 = cw[0], c1 = cw[1], c2 = cw[2];
-            const u32 qn = prv[q - lo];  // the next candidate, in the same LDS round trip
-            const u64 cv = ((u64)__builtin_amdgcn_alignbyte(c2, c1, qr & 3) << 32) |
-                           __builtin_amdgcn_alignbyte(c1, c0, qr & 3);
-            const u64 d0 = pv ^ cv;
-            if ((d0 & 0xFFFFFFull) == 0) {  // the same 3-gram, not only the same hash
-                if (d0) {
-                    l = (u32)(__ffsll((long long)d0) - 1) >> 3;
-                } else if (best < 8 || (best < lim && T[p + best] == T[q + best])) {
-                    // a strictly longer match must also match at `best`
-                    const u32 pr = p - tlo;
-                    l = 8;
-#pragma unroll
-                    for (int kk = 1; kk < LZ_CAP / 8; ++kk) {
-                        if (l >= capl) break;
-                        const u64 d = lds8(txt, pr + 8 * kk) ^ lds8(txt, qr + 8 * kk);
-                        if (d) {
-                            l += (u32)(__ffsll((long long)d) - 1) >> 3;
-                            break;
-                        }
-                        l += 8;
-                    }
-                }
-                l = min(l, capl);
-            }
-            q = qn == LZC_NONE ? NONE : lo + qn;
-        }
-        // capped candidates extended exactly (up to lim), one at a time by the whole wave
-        u64 longm = __ballot(ok && l >= capl && capl < lim);
-        while (longm) {
-            const u32 j = (u32)__ffsll((long long)longm) - 1;
-            const u32 pj = __builtin_amdgcn_readlane(p, j), qj = __builtin_amdgcn_readlane(qc, j);
-            const u32 cj = __builtin_amdgcn_readlane(capl, j), mj = __builtin_amdgcn_readlane(lim, j);
-            const u32 lj = wave_lcp(T, pj, qj, cj, mj);
-            if (lane == j) l = lj;
-            longm &= longm - 1;
-            ++nlong;
-        }
-        if (ok && l >= (u32)LZ_MIN && l > best) {  // strictly longer wins: the nearest of equals stays
-            best = l;
-            bd = p - qc;
-        }
-        const bool fin = alive && (!ok || q == NONE || p - q > (u32)LZ_WINDOW || best >= lim);
-        if (fin) {
-            finish();
-            // tokens with no candidate at all (literals) are finished on the spot
-            while (alive) {
-                setup();
-                if (q != NONE && p - q <= (u32)LZ_WINDOW) break;
-                finish();
-            }
-        }
-    }
-    if (has) {
-        z.c_ntok[c] = ntok;
-        z.c_exit[c] = p | (un ? LZ_UNRES : 0u);
-        z.c_bytes[c] = off;
-    }
-    nlong = wave_reduce(nlong, OpAddU(), 0u);
-    if (lane == 0 && nlong) atomicAdd(z.nlong, nlong);
-    if (z.prof) {
-        if (lane == 0) {
-            atomicAdd(z.prof + 4, (u64)ntrip);
-            atomicAdd(z.prof + 5, (u64)ntrip);
         }
         __syncthreads();
         if (tid == 0) {
@@ -1265,20 +1012,16 @@ __global__ __launch_bounds__(256) void k_lz_emit(LzArgs z, const u32* method, co
 
 const char* lz_spec_name() { return "k_lz_local"; }
 
-// The parse form (read per call; tests switch it): 1 = a chain per lane over 64-byte chunks
-// (k_lz_lanes, default), 0 = 16-lane chains over 256-byte chunks (k_lz_local)
-static int lz_lanes_mode() {
-    const char* e = getenv("KOLM_LZ_LANES");
-    return e ? atoi(e) : 1;
-}
-u32 lz_chunk_shift() { return lz_lanes_mode() ? LZC_CSHIFT : 8u; }
+u32 lz_chunk_shift() { return 8u; }  // 256-byte chunks
 
 void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
     if (!z.geo.nb) return;
     // 4 KiB homes, 16 chains of 16 lanes (4 workgroups per CU, LDS-limited).  Measured and
     // removed: 8 KiB homes parsed by 32 chains of 8 lanes (round 5: 2 waves per SIMD no longer hide
-    // the chains' LDS latency, step 35.7 -> 39.9 ms) and 5 KiB homes in 5-wave workgroups (round 6:
-    // step 33.4 -> 36.7 ms beside the sort stream)
+    // the chains' LDS latency, step 35.7 -> 39.9 ms), 5 KiB homes in 5-wave workgroups (round 6:
+    // step 33.4 -> 36.7 ms beside the sort stream) and a chain per lane over 64-byte chunks with
+    // hash chains in LDS (round 6: 512 chains per CU, but 64 independent chains per wave take
+    // every branch in every trip — 81 K VALU per wave — k_lz_local alone 8.4 -> 15.6 ms)
     constexpr u32 home = 4096u;
     const u32 hpb = (z.geo.bs + home - 1) / home;
     {
@@ -1291,23 +1034,7 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
         static const u32 lead =
             getenv("KOLM_LZ_LEAD") ? std::min<u32>(atoi(getenv("KOLM_LZ_LEAD")), LZL_LEAD) : 48u;
         KScope k(kt, KT_LZPARSE, "k_lz_local", z.geo.N * 2);
-        if (z.cshift == LZC_CSHIFT) {
-            // KOLM_LZ_LANES (A/B): 1 = 16 KiB homes, 11 hash bits (78 KB of LDS: 2 workgroups per
-            // CU); 2 = 16 KiB, 10 bits (70 KB); 3 = 8 KiB homes, 11 bits (45 KB: 3 per CU)
-            const int mode = lz_lanes_mode();
-            auto go = [&](auto kern, u32 home, u32 nt) {
-                const u32 hpl = (z.geo.bs + home - 1) / home;
-                kern<<<z.geo.nb * hpl, nt, 0, s>>>(z, hpl, lead);
-            };
-            if (mode == 2)
-                go(k_lz_lanes<4, 10>, LzcGeom<4>::HOME, LzcGeom<4>::NT);
-            else if (mode == 3)
-                go(k_lz_lanes<2, 11>, LzcGeom<2>::HOME, LzcGeom<2>::NT);
-            else
-                go(k_lz_lanes<4, 11>, LzcGeom<4>::HOME, LzcGeom<4>::NT);
-        } else {
-            k_lz_local<home, 16><<<z.geo.nb * hpb, LzlGeom<home, 16>::NT, 0, s>>>(z, hpb, lead);
-        }
+        k_lz_local<home, 16><<<z.geo.nb * hpb, LzlGeom<home, 16>::NT, 0, s>>>(z, hpb, lead);
     }
     {
         KScope k(kt, KT_LZPARSE, "k_lz_stitch", (u64)z.cpb * z.geo.nb * 16);

@@ -379,9 +379,8 @@ def test_adversarial_repair(kolm_gpu, kind):
 
 
 def _lz_edge(kind: str) -> bytes:
-    """Inputs aimed at the workgroup-local LZ77 parse (k_lz77.hip): 16 KiB homes of 64-byte
-    chunks (a chain per lane; 4 KiB homes of 256-byte chunks with KOLM_LZ_LANES=0), 48-byte
-    lead-ins, matches resolved exactly only 256 bytes past a chunk."""
+    """Inputs aimed at the workgroup-local LZ77 parse (k_lz77.hip): 4 KiB homes, 256-byte
+    chunks with 48-byte lead-ins, matches resolved exactly only 256 bytes past a chunk."""
     rng = np.random.default_rng(7 + len(kind))
     if kind == "long_copies":     # copies of 300..5000 bytes with sparse mutations: matches
         out = bytearray(rng.integers(0, 256, 6000).astype(np.uint8).tobytes())  # past the cap
@@ -409,25 +408,18 @@ def _lz_edge(kind: str) -> bytes:
     raise ValueError(kind)
 
 
-@pytest.mark.parametrize("lanes", ["1", "0"])
 @pytest.mark.parametrize("kind", ["long_copies", "period4096", "period4097", "text_zero_runs", "random", "text"])
-def test_lz77_local_edges(kolm_gpu, monkeypatch, kind, lanes):
-    monkeypatch.setenv("KOLM_LZ_LANES", lanes)
+def test_lz77_local_edges(kolm_gpu, kind):
     data = _lz_edge(kind)
     assert kolm_gpu.encode_lz77(data)[0] == O.encode_lz77(data)
 
 
-@pytest.mark.parametrize("lanes", ["1", "0"])
-@pytest.mark.parametrize("bs", [63, 64, 65, 255, 256, 257, 4095, 4096, 4097, 4096 + 256 + 63, 12288 + 5,
-                                16383, 16384, 16385, 16384 + 4096 + 47])
-def test_lz77_local_block_geometry(kolm_gpu, monkeypatch, bs, lanes):
-    """Block sizes around the chunk (64 / 256) and home (16 KiB / 4 KiB) sizes of both parse
-    forms in one batch: the last chunk / home of every block is partial; candidates must never
-    cross a block."""
-    monkeypatch.setenv("KOLM_LZ_LANES", lanes)
+@pytest.mark.parametrize("bs", [15, 16, 17, 255, 256, 257, 4095, 4096, 4097, 4096 + 256 + 63, 12288 + 5])
+def test_lz77_local_block_geometry(kolm_gpu, bs):
+    """Block sizes around the 16-byte first compare, the chunk (256) and home (4096) sizes in one
+    batch: the last chunk / home of every block is partial; candidates must never cross a block."""
     from kolm import _lib
-    data = (D.enwik_like(30_000, seed=5) + bytes(700) + D.enwik_like(20_000, seed=6)
-            + (D.enwik_like(9000, seed=7) if bs > 8192 else b""))
+    data = (D.enwik_like(30_000, seed=5) + bytes(700) + D.enwik_like(20_000, seed=6))
     nb = (len(data) + bs - 1) // bs
     _, method, payloads, st = _lib.encode_blocks(data, bs, force=[7] * nb)
     for i in range(nb):
