@@ -465,7 +465,12 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
         qa = qn;
         qok = qnok;
         k = k > LPC ? k - LPC : 0u;
-        const bool fin = alive && (sm != 0 || best >= lim);
+        // Lead-in tokens (p before the chunk start, not recorded) stop after their first batch
+        // of the 16 nearest candidates: the lead-in only has to land on the true path by the
+        // chunk start, and the stitch checks that exactly (a chunk whose first recorded token
+        // is not the true entry is re-parsed there), so a lead-in token shorter than the true
+        // one costs a fix-up at worst, never the result
+        const bool fin = alive && (sm != 0 || best >= lim || p < s);
         if (__ballot(fin)) {
             if (fin) {
                 const u32 len = best >= (u32)LZ_MIN ? best : 0u;

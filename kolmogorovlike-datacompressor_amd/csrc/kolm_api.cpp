@@ -149,6 +149,8 @@ struct kolm_ctx {
     hipStream_t aux = nullptr;     // second stream: Lyndon + cyclic sort chain runs beside LZ77
     hipStream_t active = nullptr;  // stream used by launches / TScope / sync()
     hipStream_t rp = nullptr;      // third stream: Re-Pair (candidate 9), one workgroup per block
+    hipStream_t aux2 = nullptr;    // the sort chain's second stream: half of a round's class sorts
+    hipEvent_t evc[2] = {};        // class-sort fork / join
     bool serial = false;           // every launch of a batch on one stream (kolm_ctx_set_serial; KOLM_SERIAL=1)
     // pinned host staging: an upload ring (input chunks) and the result buffer of
     // kolm_compress_fixed (container bytes, valid until the next call on this context)
@@ -193,7 +195,7 @@ struct kolm_ctx {
         u64 bytes;
         int strm;  // 0 index stream, 1 sort stream, 2 Re-Pair stream
     };
-    int strm_of(hipStream_t s) const { return s == aux ? 1 : s == rp ? 2 : 0; }
+    int strm_of(hipStream_t s) const { return s == aux || s == aux2 ? 1 : s == rp ? 2 : 0; }
     std::vector<Pend> pend;
     struct Acc {
         double ms = 0;
@@ -594,20 +596,48 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
             c->sync();
         }
-        // per element: K2 + SA read, SA + RK write (16 B); per segment record 8 B
+        // per element: K2 + SA read, SA + RK write (16 B); per segment record 8 B.  The classes'
+        // sorts touch disjoint segments: with KOLM_CLS_STREAMS=1 they are split over the sort
+        // stream and a second one (largest classes first, each to the less loaded stream), so
+        // the short grids of one class fill the tail of another's
+        const bool two = getenv("KOLM_CLS_STREAMS") && atoi(getenv("KOLM_CLS_STREAMS")) != 0;  // per call (tests)
+        const bool fork = two && !c->serial && s == c->aux;
+        int on2[NCLASS] = {};
+        if (fork) {
+            int ord[NCLASS];
+            for (int k = 0; k < NCLASS; ++k) ord[k] = k;
+            std::sort(ord, ord + NCLASS, [&](int x, int y) { return h[C_CLSE + x] > h[C_CLSE + y]; });
+            u64 load[2] = {0, 0};
+            for (int i = 0; i < NCLASS; ++i) {
+                const int k = ord[i];
+                if (!h[C_CLS + k] || k == 0) continue;
+                const int t = load[1] < load[0] ? 1 : 0;
+                on2[k] = t;
+                load[t] += h[C_CLSE + k] + 2048;  // + a launch's worth of fixed cost
+            }
+            KOLM_HIP_CHECK(hipEventRecord(c->evc[0], s));
+            KOLM_HIP_CHECK(hipStreamWaitEvent(c->aux2, c->evc[0], 0));
+        }
         for (int k = 0; k < NCLASS; ++k) {
             if (!h[C_CLS + k]) continue;
+            const hipStream_t ks = on2[k] ? c->aux2 : s;
+            c->active = ks;
             if (k >= 1 && k <= tiny_c) {
                 static const char* const tn[6] = {"",          "k_tiny_sort<1>", "k_tiny_sort<2>",
                                                   "k_tiny_sort<3>", "k_tiny_sort<4>", "k_tiny_sort<5>"};
                 // SA + key (KP gather or K2) read, SA + RK write per element; 8 B per segment
                 TScope t(c, KOLM_KT_SMALLSORT, tn[k], (u64)h[C_CLSE + k] * 16 + (u64)h[C_CLS + k] * 8);
-                launch_tiny_sort(k, L.cls[k], h[C_CLS + k], a, L, s);
+                launch_tiny_sort(k, L.cls[k], h[C_CLS + k], a, L, ks);
                 continue;
             }
             const int w32 = a.key_bits + k <= 31 ? 1 : 0;  // matches small_sort_c's choice
             TScope t(c, KOLM_KT_SMALLSORT, kSmallSortName[w32][k], (u64)h[C_CLSE + k] * 16 + (u64)h[C_CLS + k] * 8);
-            launch_small_sort(k, L.cls[k], h[C_CLS + k], a, L, s);
+            launch_small_sort(k, L.cls[k], h[C_CLS + k], a, L, ks);
+        }
+        c->active = s;
+        if (fork) {
+            KOLM_HIP_CHECK(hipEventRecord(c->evc[1], c->aux2));
+            KOLM_HIP_CHECK(hipStreamWaitEvent(s, c->evc[1], 0));
         }
         if (h[C_EQ]) {
             TScope t(c, KOLM_KT_SMALLSORT, "k_finalize_eq", (u64)h[C_EQ] * TILE * 8);
@@ -1278,6 +1308,12 @@ int ctx_create(int device, kolm_ctx** out) {
             KOLM_HIP_CHECK(hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, prio == 1 ? hi : lo));
         }
         KOLM_HIP_CHECK(hipStreamCreateWithFlags(&c->rp, hipStreamNonBlocking));
+        {
+            int lo = 0, hi = 0;
+            KOLM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            KOLM_HIP_CHECK(hipStreamCreateWithPriority(&c->aux2, hipStreamNonBlocking, hi));
+        }
+        for (auto& e : c->evc) KOLM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         c->active = c->stream;
         c->serial = getenv("KOLM_SERIAL") && atoi(getenv("KOLM_SERIAL")) != 0;
         for (auto& e : c->evj) KOLM_HIP_CHECK(hipEventCreate(&e));
@@ -1397,12 +1433,14 @@ int kolm_ctx_destroy(kolm_ctx* c) {
         KOLM_HIP_CHECK(hipStreamSynchronize(c->stream));
         KOLM_HIP_CHECK(hipStreamSynchronize(c->aux));
         KOLM_HIP_CHECK(hipStreamSynchronize(c->rp));
+        KOLM_HIP_CHECK(hipStreamSynchronize(c->aux2));
         for (auto& kv : c->bufs)
             if (kv.second.p) KOLM_HIP_CHECK(hipFree(kv.second.p));
         for (auto& e : c->ev) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evj) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evr) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evg) KOLM_HIP_CHECK(hipEventDestroy(e));
+        for (auto& e : c->evc) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evpool) KOLM_HIP_CHECK(hipEventDestroy(e));
         KOLM_HIP_CHECK(hipHostFree(c->h_cnt));
         if (c->h_tail) KOLM_HIP_CHECK(hipHostFree(c->h_tail));
@@ -1417,6 +1455,7 @@ int kolm_ctx_destroy(kolm_ctx* c) {
         KOLM_HIP_CHECK(hipStreamDestroy(c->stream));
         KOLM_HIP_CHECK(hipStreamDestroy(c->aux));
         KOLM_HIP_CHECK(hipStreamDestroy(c->rp));
+        KOLM_HIP_CHECK(hipStreamDestroy(c->aux2));
         delete c;
         return KOLM_OK;
     });
