@@ -145,6 +145,9 @@ __device__ u32 wave_lcp8(const LText& t, u32 p, u32 q, u32 start, u32 maxl, u32 
     }
 }
 
+constexpr u32 LZL_HB = 10;
+constexpr u32 LZL_NBK = 1u << LZL_HB;
+
 // =====================================================================================
 // Workgroup-local 3-gram index and speculative parse.
 //
@@ -170,9 +173,10 @@ __device__ u32 wave_lcp8(const LText& t, u32 p, u32 q, u32 start, u32 maxl, u32 
 // =====================================================================================
 // Geometry of one k_lz_local variant: HOME positions per workgroup, LPC lanes per chain (the
 // candidates a chain compares per batch); 256 threads either way (4 waves, 64 / LPC chains each).
-template <u32 HOME, u32 LPC>
+// IDX: how the workgroup gets its window's 3-gram index (LzIdx below).
+template <u32 HOME, u32 LPC, u32 IDX>
 struct LzlGeom {
-    static constexpr u32 NW = HOME + LZ_WINDOW + LZL_LEAD;  // window positions indexed
+    static constexpr u32 NW = HOME + LZ_WINDOW + (IDX ? 0u : (u32)LZL_LEAD);  // window positions indexed
     static constexpr u32 TXT = NW + LZL_CAPX + 32;          // text window + alignment + compare slack
     static constexpr u32 ISL = HOME + LZL_LEAD;             // islot entries [hs - LEAD, he)
     static constexpr u32 NCHAIN = HOME / LZL_CHUNK;
@@ -180,8 +184,17 @@ struct LzlGeom {
     static constexpr u32 NWV = NCHAIN / CPW;                // waves per workgroup
     static constexpr u32 NT = 64 * NWV;                     // threads per workgroup
     static constexpr u32 PER = (NW + NT - 1) / NT;          // window elements per lane in the sort
+    static constexpr u32 PER2 = (ISL + NT - 1) / NT;        // islot positions per lane (tile index)
+    static constexpr u32 cmax(u32 a, u32 b) { return a > b ? a : b; }
+    // B: islot (u16 slots; u8 ranks in form 2) and, before it, the sort's histograms (form 0) or the
+    // two tiles' bucket counts (+ the bucket starts in form 1)
+    static constexpr u32 BBYTES = IDX == 0 ? cmax(2 * ISL, NWV * LZL_NBK * 2)
+                                : IDX == 1 ? cmax(2 * ISL, 2 * (3 * LZL_NBK + 16))
+                                           : cmax(ISL, 2 * 2 * LZL_NBK);
+    static constexpr u32 CST = IDX == 2 ? LZL_NBK + 8 : 1;  // form 2: bucket starts, kept for the parse
     static_assert(NCHAIN % CPW == 0, "whole waves of 64 / LPC chains");
     static_assert(NW < (1u << 14), "window offsets in 14 bits (the winner key)");
+    static_assert(IDX == 0 || NT * 4 == LZL_NBK, "tile-index forms: 4 buckets per thread in the start scan");
 };
 
 // LDS text without bounds checks (every access is inside the loaded window by construction)
@@ -195,8 +208,6 @@ struct WinText {
 // positions by hash (ascending position inside a bucket); a candidate whose 3-gram differs
 // is rejected by the first byte compare, so other 3-grams sharing the bucket only cost
 // lanes (about 4096 / 2^LZL_HB of them per token).
-constexpr u32 LZL_HB = 10;
-constexpr u32 LZL_NBK = 1u << LZL_HB;
 __device__ inline u32 hash3(const u8* t, u32 x) {
     const u32 k = ((u32)t[x] << 16) | ((u32)t[x + 1] << 8) | t[x + 2];
     return (k * 0x9E3779B1u) >> (32 - LZL_HB);
@@ -275,6 +286,90 @@ __device__ void lzl_bucket(const u8* t, u16* A, u32 nw, u16* hist, u32* sh) {
     __syncthreads();
 }
 
+// The window's index from a per-tile one (forms 1 and 2 of k_lz_local).  Every position of a
+// block is ranked once, inside its 4 KiB tile, instead of once in each of the two windows that
+// hold it: k_lz_tiles (one workgroup per tile, the stable counting-sort pass of lzl_bucket over
+// the tile alone) writes rank[x], x's rank among the tile's positions of the same hash in
+// position order, and the tile's 1024 bucket counts.  A home's window is its own tile t and
+// tile t - 1, whose bucket lists concatenated per hash (t - 1 first) are the window's bucket
+// lists in position order, so x's slot in the window index is
+//     start(h) + rank[x]                 (x in tile t - 1)
+//     start(h) + cnt_{t-1}(h) + rank[x]  (x in tile t)
+// with start(h) the exclusive scan of cnt_{t-1} + cnt_t: the workgroup places every window
+// position with one coalesced load and one LDS store, no ranking.  (The lead-in positions of
+// the home's first chain lie in tile t - 1; their own candidates before hs - 4096 are left out,
+// which a lead-in may do: the stitch checks where it lands.)
+__global__ __launch_bounds__(256) void k_lz_tiles(LzArgs z, u32 hpb) {
+    constexpr u32 NT = 256, NWV = 4, PER = LZL_HOME / NT;
+    __shared__ __align__(16) u8 txt[LZL_HOME + 16];
+    __shared__ __align__(16) u16 hist[NWV * LZL_NBK];
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u32 b = blockIdx.x / hpb, h = blockIdx.x - b * hpb;
+    const u32 base = z.geo.base(b), end = z.geo.end(b);
+    const u32 ts = base + h * LZL_HOME;
+    if (ts >= end) return;
+    const u32 te = min(ts + (u32)LZL_HOME, end);
+    const u32 lim3 = end - base >= 3 ? end - 2 : base;
+    const u32 top = min(te, lim3);
+    const u32 n = top > ts ? top - ts : 0u;
+    const u32 tlo = ts & ~3u, thi = min(end, te + 2);
+    if (((uintptr_t)z.text & 3) == 0) {
+        const u32* src = reinterpret_cast<const u32*>(z.text + tlo);
+        u32* dst = reinterpret_cast<u32*>(txt);
+        const u32 nd = (thi - tlo) / 4;
+        for (u32 i = tid; i < nd; i += NT) dst[i] = src[i];
+        if (tid < ((thi - tlo) & 3u)) txt[4 * nd + tid] = z.text[tlo + 4 * nd + tid];
+    } else {
+        for (u32 i = tid; i < thi - tlo; i += NT) txt[i] = z.text[tlo + i];
+    }
+    for (u32 i = tid; i < NWV * LZL_NBK / 2; i += NT) reinterpret_cast<u32*>(hist)[i] = 0;
+    __syncthreads();
+    const u8* tt = txt + (ts - tlo);
+    const u32 Q = (n + NWV - 1) / NWV;
+    const u32 b0 = min(w * Q, n), b1 = min(b0 + Q, n);
+    u32 hv[PER];
+#pragma unroll
+    for (u32 k = 0; k < PER; ++k) {
+        const u32 e = min(b0 + k * 64 + lane, LZL_HOME - 1);
+        hv[k] = hash3(tt, e);
+    }
+#pragma unroll
+    for (u32 k = 0; k < PER; ++k)
+        if (b0 + k * 64 + lane < b1)
+            atomicAdd(reinterpret_cast<u32*>(hist) + ((w * LZL_NBK + hv[k]) >> 1), 1u << (16 * (hv[k] & 1)));
+    __syncthreads();
+    // per bucket: the waves' exclusive offsets (wave order = position order) and the tile's count
+    for (u32 d = tid; d < LZL_NBK; d += NT) {
+        u32 run = 0;
+#pragma unroll
+        for (u32 q = 0; q < NWV; ++q) {
+            const u32 cq = hist[q * LZL_NBK + d];
+            hist[q * LZL_NBK + d] = (u16)run;
+            run += cq;
+        }
+        z.tcnt[(u64)blockIdx.x * LZL_NBK + d] = (u16)run;
+    }
+    __syncthreads();
+    const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+#pragma unroll
+    for (u32 k = 0; k < PER; ++k) {
+        if (b0 + k * 64 >= b1) break;  // wave-uniform
+        const u32 e = b0 + k * 64 + lane;
+        const bool valid = e < b1;
+        const u32 dg = hv[k];
+        u64 m = __ballot(valid);
+#pragma unroll
+        for (u32 bit = 0; bit < LZL_HB; ++bit) {
+            const u64 bal = __ballot((dg >> bit) & 1u);
+            m &= ((dg >> bit) & 1u) ? bal : ~bal;
+        }
+        const u32 rank = (u32)__popcll(m & lt);
+        const u32 o = valid ? hist[w * LZL_NBK + dg] : 0u;
+        if (valid) z.rank[ts + e] = (u16)(o + rank);
+        if (valid && rank == 0) hist[w * LZL_NBK + dg] = (u16)(o + (u32)__popcll(m));
+    }
+}
+
 // the lanes of this lane's chain (LPC consecutive lanes)
 template <u32 LPC>
 __device__ inline u64 grp_mask(u32 lane) { return ((1ull << LPC) - 1ull) << (lane & (64 - LPC)); }
@@ -313,17 +408,22 @@ __device__ inline u32 uleb_n(u32 v) {
 // =====================================================================================
 constexpr u32 LZC_HEAD = 0x8000u;   // A[slot] flag: first slot of its hash bucket
 
-template <u32 HOME, u32 LPC>
+// Window index forms (IDX): 0 = the workgroup sorts its whole window in LDS (lzl_bucket);
+// 1 = placed from the tile index (k_lz_tiles), islot as u16 slots; 2 = the same, islot as u8
+// ranks inside the bucket plus the window's bucket starts (31 KB of LDS instead of 33: five
+// workgroups per CU); a rank of 255 or more is found by a binary search of the bucket.
+template <u32 HOME, u32 LPC, u32 IDX>
 __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
-    using G = LzlGeom<HOME, LPC>;
+    using G = LzlGeom<HOME, LPC, IDX>;
     __shared__ __align__(16) u8 txt[G::TXT];
     __shared__ __align__(16) u16 A[G::NW];
     constexpr u32 NT = G::NT;
-    // islot of [ilo, he); the sort's histograms before it
-    __shared__ __align__(16) u16 B[G::ISL > G::NWV * LZL_NBK ? G::ISL : G::NWV * LZL_NBK];
+    // islot of [ilo, he); before it the sort's histograms (form 0) or the tiles' counts (1, 2)
+    __shared__ __align__(16) u8 B[G::BBYTES];
+    __shared__ __align__(16) u16 cst[G::CST];
     __shared__ u32 sh[G::NWV];
-    u16* hist = B;
-    
+    u16* hist = reinterpret_cast<u16*>(B);
+
     static_assert(G::NW <= 0x3FFFu + 1u, "window offsets below the head flag");
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const u32 b = blockIdx.x / hpb, h = blockIdx.x - b * hpb;
@@ -331,7 +431,8 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
     const u32 hs = base + h * HOME;
     if (hs >= end) return;
     const u32 he = min(hs + HOME, end);
-    const u32 lo = hs - base > (u32)(LZ_WINDOW + LZL_LEAD) ? hs - LZ_WINDOW - LZL_LEAD : base;
+    constexpr u32 WSPAN = IDX ? (u32)LZ_WINDOW : (u32)(LZ_WINDOW + LZL_LEAD);
+    const u32 lo = hs - base >= WSPAN ? hs - WSPAN : base;
     const u32 ilo = hs - base > (u32)LZL_LEAD ? hs - LZL_LEAD : base;
     const u32 hi = min(end, he + (u32)LZL_CAPX);
     const u32 tlo = lo & ~3u;
@@ -348,27 +449,120 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
             for (u32 i = tid; i < n; i += NT) txt[i] = z.text[tlo + i];
         }
     }
-    __syncthreads();
     const u32 lim3 = end - base >= 3 ? end - 2 : base;
     const u32 top = min(he, lim3);
     const u32 nw = top > lo ? top - lo : 0u;
     const u8* tw = txt + (lo - tlo);
-    if (z.prof) t1 = wall_clock64();
-    u16* isl = B;
-    if (nw) {
-        lzl_bucket<G::PER, G::NWV>(tw, A, nw, hist, sh);
-        // flag the first slot of every non-empty bucket (the last wave's offsets are the bucket ends)
-        for (u32 d = tid; d < LZL_NBK; d += NT) {
-            const u32 e = hist[(G::NWV - 1) * LZL_NBK + d], st = d ? hist[(G::NWV - 1) * LZL_NBK + d - 1] : 0u;
-            if (e > st) A[st] = (u16)(A[st] | LZC_HEAD);
+    u16* isl = reinterpret_cast<u16*>(B);  // forms 0, 1
+    u8* r8 = B;                            // form 2
+    if constexpr (IDX == 0) {
+        __syncthreads();
+        if (z.prof) t1 = wall_clock64();
+        if (nw) {
+            lzl_bucket<G::PER, G::NWV>(tw, A, nw, hist, sh);
+            // flag the first slot of every non-empty bucket (the last wave's offsets are the bucket ends)
+            for (u32 d = tid; d < LZL_NBK; d += NT) {
+                const u32 e = hist[(G::NWV - 1) * LZL_NBK + d], st = d ? hist[(G::NWV - 1) * LZL_NBK + d - 1] : 0u;
+                if (e > st) A[st] = (u16)(A[st] | LZC_HEAD);
+            }
+            __syncthreads();  // the islot writes below overwrite the histograms
         }
-        __syncthreads();  // the islot writes below overwrite the histograms
+        for (u32 j = tid; j < nw; j += NT) {
+            const u32 x = A[j] & 0x7FFFu;
+            if (lo + x >= ilo) isl[lo + x - ilo] = (u16)j;
+        }
+        if (z.prof) t2 = wall_clock64();
+    } else {
+        // the two tiles' bucket counts (tile t - 1 absent for a block's first home)
+        u16* c0 = reinterpret_cast<u16*>(B);
+        u16* c1 = c0 + LZL_NBK;
+        u16* cs = IDX == 1 ? c1 + LZL_NBK : cst;
+        {
+            const u32* s1 = reinterpret_cast<const u32*>(z.tcnt + (u64)blockIdx.x * LZL_NBK);
+            const u32* s0 = s1 - LZL_NBK / 2;
+            for (u32 i = tid; i < LZL_NBK / 2; i += NT) {
+                reinterpret_cast<u32*>(c1)[i] = s1[i];
+                reinterpret_cast<u32*>(c0)[i] = h ? s0[i] : 0u;
+            }
+        }
+        __syncthreads();
+        if (z.prof) t1 = wall_clock64();
+        {
+            // window bucket starts: exclusive scan of cnt_{t-1} + cnt_t, 4 buckets per thread
+            u32 v[4], tot = 0;
+#pragma unroll
+            for (u32 i = 0; i < 4; ++i) {
+                v[i] = (u32)c0[4 * tid + i] + c1[4 * tid + i];
+                tot += v[i];
+            }
+            const u32 incl = wave_incl_scan(tot, OpAddU(), 0u);
+            if (lane == 63) sh[w] = incl;
+            __syncthreads();
+            u32 ex = incl - tot;
+            for (u32 i = 0; i < w; ++i) ex += sh[i];
+#pragma unroll
+            for (u32 i = 0; i < 4; ++i) {
+                cs[4 * tid + i] = (u16)ex;
+                ex += v[i];
+            }
+            if (tid == NT - 1) cs[LZL_NBK] = (u16)ex;
+        }
+        __syncthreads();
+        // tile t - 1's positions below the islot range: slot = start(h) + rank
+        const u32 p1 = min(ilo, top);
+        for (u32 x0 = lo; x0 < p1; x0 += NT * 4) {
+            u32 r[4];
+#pragma unroll
+            for (u32 i = 0; i < 4; ++i) {
+                const u32 x = x0 + i * NT + tid;
+                r[i] = x < p1 ? (u32)z.rank[x] : 0u;
+            }
+#pragma unroll
+            for (u32 i = 0; i < 4; ++i) {
+                const u32 x = x0 + i * NT + tid;
+                if (x < p1) A[cs[hash3(tw, x - lo)] + r[i]] = (u16)((x - lo) | (r[i] ? 0u : LZC_HEAD));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // [ilo, top): the lead-in (tile t - 1) and the home (tile t, after tile t - 1's entries);
+        // the islot values wait in registers (packed) until the counts are no longer read
+        constexpr u32 KB = IDX == 1 ? 2 : 4;  // islot values per keep word
+        u32 keep[(G::PER2 + KB - 1) / KB] = {};
+#pragma unroll
+        for (u32 i0 = 0; i0 < G::PER2; i0 += 4) {
+            u32 r[4];
+#pragma unroll
+            for (u32 i = i0; i < i0 + 4 && i < G::PER2; ++i) {
+                const u32 x = ilo + i * NT + tid;
+                r[i - i0] = x < top ? (u32)z.rank[x] : 0u;
+            }
+#pragma unroll
+            for (u32 i = i0; i < i0 + 4 && i < G::PER2; ++i) {
+                const u32 x = ilo + i * NT + tid;
+                if (x < top) {
+                    const u32 hh = hash3(tw, x - lo);
+                    const u32 rr = r[i - i0] + (x >= hs ? (u32)c0[hh] : 0u);
+                    const u32 slot = cs[hh] + rr;
+                    A[slot] = (u16)((x - lo) | (rr ? 0u : LZC_HEAD));
+                    keep[i / KB] |= (IDX == 1 ? slot : min(rr, 255u)) << ((32 / KB) * (i % KB));
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (z.prof) t2 = wall_clock64();
+        __syncthreads();  // islot overwrites the counts
+#pragma unroll
+        for (u32 i = 0; i < G::PER2; ++i) {
+            const u32 x = ilo + i * NT + tid;
+            const u32 v = (keep[i / KB] >> ((32 / KB) * (i % KB))) & (IDX == 1 ? 0xFFFFu : 0xFFu);
+            if (x < top) {
+                if constexpr (IDX == 1)
+                    isl[x - ilo] = (u16)v;
+                else
+                    r8[x - ilo] = (u8)v;
+            }
+        }
     }
-    for (u32 j = tid; j < nw; j += NT) {
-        const u32 x = A[j] & 0x7FFFu;
-        if (lo + x >= ilo) isl[lo + x - ilo] = (u16)j;
-    }
-    if (z.prof) t2 = wall_clock64();
     __syncthreads();
     if (z.prof) t3 = wall_clock64();
 
@@ -397,9 +591,26 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
         bd = 0;
         lim = lend - p;
         capl = min((u32)LZ_CAP, lim);
-        k = p + (u32)LZ_MIN <= end ? (u32)isl[p - ilo] : 0u;
         pv = lds8(txt, p - tlo);
         pv1 = lds8(txt, p - tlo + 8);
+        if constexpr (IDX != 2) {
+            k = p + (u32)LZ_MIN <= end ? (u32)isl[p - ilo] : 0u;
+        } else if (p + (u32)LZ_MIN <= end) {
+            const u32 hh = (__builtin_bswap32((u32)pv) >> 8) * 0x9E3779B1u >> (32 - LZL_HB);
+            const u32 rr = r8[p - ilo];
+            k = (u32)cst[hh] + rr;
+            if (rr == 255u) {  // rank >= 255: binary search of the bucket for p's own slot
+                u32 a0 = k, a1 = cst[hh + 1];
+                const u32 tx = p - lo;
+                while (a0 < a1) {
+                    const u32 m = (a0 + a1) >> 1;
+                    if ((A[m] & 0x3FFFu) < tx) a0 = m + 1; else a1 = m;
+                }
+                k = a0;
+            }
+        } else {
+            k = 0;
+        }
         qok = k > hl;
         qa = A[qok ? k - 1 - hl : 0u];
     };
@@ -465,12 +676,9 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
         qa = qn;
         qok = qnok;
         k = k > LPC ? k - LPC : 0u;
-        // Lead-in tokens (p before the chunk start, not recorded) stop after their first batch
-        // of the 16 nearest candidates: the lead-in only has to land on the true path by the
-        // chunk start, and the stitch checks that exactly (a chunk whose first recorded token
-        // is not the true entry is re-parsed there), so a lead-in token shorter than the true
-        // one costs a fix-up at worst, never the result
-        const bool fin = alive && (sm != 0 || best >= lim || p < s);
+        // (round 6: lead-in tokens cut after their first candidate batch left 100x more chunks off
+        // the true path — the stitch's serial fix-ups took the LZ77 stream 31 -> 51 ms per step)
+        const bool fin = alive && (sm != 0 || best >= lim);
         if (__ballot(fin)) {
             if (fin) {
                 const u32 len = best >= (u32)LZ_MIN ? best : 0u;
@@ -1019,7 +1227,20 @@ const char* lz_spec_name() { return "k_lz_local"; }
 
 u32 lz_chunk_shift() { return 8u; }  // 256-byte chunks
 
-void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
+int lz_index_form() {
+    // read per call (tests); default: the in-LDS sort (form 0) until the A/B of the tile forms
+    return getenv("KOLM_LZ_IDX") ? atoi(getenv("KOLM_LZ_IDX")) : 0;
+}
+
+void launch_lz_tiles(const LzArgs& z, hipStream_t s, KTimer* kt) {
+    if (!z.geo.nb || lz_index_form() == 0) return;
+    const u32 hpb = (z.geo.bs + LZL_HOME - 1) / LZL_HOME;
+    // text 1 B + rank 2 B per position + 2 KiB of counts per tile
+    KScope k(kt, KT_LZPARSE, "k_lz_tiles", z.geo.N * 3 + (u64)z.geo.nb * hpb * 2048);
+    k_lz_tiles<<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb);
+}
+
+void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt, bool tiles_done) {
     if (!z.geo.nb) return;
     // 4 KiB homes, 16 chains of 16 lanes (4 workgroups per CU, LDS-limited).  Measured and
     // removed: 8 KiB homes parsed by 32 chains of 8 lanes (round 5: 2 waves per SIMD no longer hide
@@ -1028,18 +1249,26 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
     // hash chains in LDS (round 6: 512 chains per CU, but 64 independent chains per wave take
     // every branch in every trip — 81 K VALU per wave — k_lz_local alone 8.4 -> 15.6 ms)
     constexpr u32 home = 4096u;
+    static_assert(home == (u32)LZL_HOME, "tile index and homes share the 4 KiB geometry");
     const u32 hpb = (z.geo.bs + home - 1) / home;
+    const int idx = lz_index_form();
+    if (!tiles_done) launch_lz_tiles(z, s, kt);
     {
-        // text window (LZL_NW + LZL_CAPX bytes per 4 KiB home: ~2.1 B per position) +
-        // 16 B per token (added by the caller once the token count is known)
         // lead-in bytes parsed before each chain's chunk (at most LZL_LEAD, the window's margin):
         // 48 since the stitch's fix-up searches got cheaper (round 5, two A/B calls, profiles/r05/
         // ab_lz_lead_*: 33.67-33.76 ms per step at 48 and 56 against 33.84-34.30 at 64; 32 and 40
         // measured 34.09-34.44 and 34.18).  KOLM_LZ_LEAD overrides.
         static const u32 lead =
             getenv("KOLM_LZ_LEAD") ? std::min<u32>(atoi(getenv("KOLM_LZ_LEAD")), LZL_LEAD) : 48u;
+        // KOLM_LZ_PAD: extra (unused) LDS bytes per workgroup, to cap the parse's workgroups per CU
+        const u32 pad = getenv("KOLM_LZ_PAD") ? (u32)atoi(getenv("KOLM_LZ_PAD")) : 0u;
         KScope k(kt, KT_LZPARSE, "k_lz_local", z.geo.N * 2);
-        k_lz_local<home, 16><<<z.geo.nb * hpb, LzlGeom<home, 16>::NT, 0, s>>>(z, hpb, lead);
+        if (idx == 0)
+            k_lz_local<home, 16, 0><<<z.geo.nb * hpb, LzlGeom<home, 16, 0>::NT, pad, s>>>(z, hpb, lead);
+        else if (idx == 1)
+            k_lz_local<home, 16, 1><<<z.geo.nb * hpb, LzlGeom<home, 16, 1>::NT, pad, s>>>(z, hpb, lead);
+        else
+            k_lz_local<home, 16, 2><<<z.geo.nb * hpb, LzlGeom<home, 16, 2>::NT, pad, s>>>(z, hpb, lead);
     }
     {
         KScope k(kt, KT_LZPARSE, "k_lz_stitch", (u64)z.cpb * z.geo.nb * 16);

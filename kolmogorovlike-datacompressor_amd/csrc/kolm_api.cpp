@@ -779,14 +779,16 @@ struct Pipeline {
         static const bool lz_prof = getenv("KOLM_LZ_PROF") && atoi(getenv("KOLM_LZ_PROF")) != 0;
         if (lz_prof) z.prof = c->get<u64>("lz_prof", 32);
         z.stitch_runs = 1u;
+        z.rank = c->get<u16>("lz_rank", N + 16);
+        z.tcnt = c->get<u16>("lz_tcnt", (u64)geo.nb * ((geo.bs + LZL_HOME - 1) / LZL_HOME) * 1024 + 16);
         return z;
     }
 
-    void lz(const LzArgs& z) {
+    void lz(const LzArgs& z, bool tiles_done = false) {
         KOLM_HIP_CHECK(hipMemsetAsync(z.nlong, 0, sizeof(u32), c->active));
         KOLM_HIP_CHECK(hipMemsetAsync(z.nfix, 0, sizeof(u32), c->active));
         if (z.prof) KOLM_HIP_CHECK(hipMemsetAsync(z.prof, 0, sizeof(u64) * 32, c->active));
-        launch_lz_parse(z, c->active, c->kt());
+        launch_lz_parse(z, c->active, c->kt(), tiles_done);
     }
 };
 
@@ -1028,6 +1030,13 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     // competes with Lyndon and round 0 for CUs), so it keeps the index-stream form.
     // KOLM_PREVC_IDX = 0 / 1 forces it.
     const int prevc_idx = getenv("KOLM_PREVC_IDX") ? atoi(getenv("KOLM_PREVC_IDX")) : -1;  // read per call (tests)
+    const bool want_lz = (mask >> KOLM_M_LZ77) & 1u || (h_force != nullptr);
+    LzArgs z = P.lz_args();
+    // The LZ77 tile index ahead of the prevc wait, beside Lyndon, when the parse queues behind
+    // prevc on this stream (KOLM_LZ_TEARLY = 0 / 1 forces it)
+    const int tearly_env = getenv("KOLM_LZ_TEARLY") ? atoi(getenv("KOLM_LZ_TEARLY")) : -1;
+    const bool tiles_early = want_lz && !serial && xs == ms && (tearly_env >= 0 ? tearly_env != 0 : true);
+    if (tiles_early) launch_lz_tiles(z, ms, c->kt());
     if (!serial && (prevc_idx >= 0 ? prevc_idx != 0 : nb >= 16)) {
         KOLM_HIP_CHECK(hipStreamWaitEvent(xs, ev[5], 0));
         P.prevc();
@@ -1037,12 +1046,10 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     if (side) KOLM_HIP_CHECK(hipEventRecord(ev[7], xs));  // the sizes, joined before the MDL
     c->active = ms;
     KOLM_HIP_CHECK(hipEventRecord(ej[0], ms));
-    LzArgs z = P.lz_args();
-    const bool want_lz = (mask >> KOLM_M_LZ77) & 1u || (h_force != nullptr);
     auto launch_lz = [&] {
         c->active = ms;
         KOLM_HIP_CHECK(hipEventRecord(ej[2], ms));
-        if (want_lz) P.lz(z);
+        if (want_lz) P.lz(z, tiles_early);
         KOLM_HIP_CHECK(hipEventRecord(ej[1], ms));
     };
     u8* bw = nullptr;

@@ -450,8 +450,16 @@ struct LzArgs {
     u32* nfix;         // [1] fix-up tokens computed by the stitch (statistics)
     u64* prof;         // [8] optional k_lz_local phase clocks (KOLM_LZ_PROF=1), null = off
     u32 stitch_runs;   // k_lz_stitch_l takes runs of whole chunks lane-parallel (KOLM_STITCH_RUNS=0: off)
+    // 4 KiB tile index (k_lz_tiles): rank[x] = x's stable rank among its tile's positions of the
+    // same 3-gram hash, tcnt[tile * 1024 + h] = the tile's count of hash h
+    u16* rank;         // [N]
+    u16* tcnt;         // [nb * tiles per block * 1024]
 };
-void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr);
+// the window-index form of k_lz_local (KOLM_LZ_IDX; 0 = no tile index) and its tile index
+// (k_lz_tiles; launch_lz_parse runs it first unless tiles_done)
+int lz_index_form();
+void launch_lz_tiles(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr);
+void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr, bool tiles_done = false);
 const char* lz_spec_name();  // the speculative-parse kernel in use (timing / roofline)
 u32 lz_chunk_shift();        // log2 of the parse's chunk bytes (LzArgs::cshift) for the form in use
 void launch_lz_emit(const LzArgs& z, const u32* method, const u64* off, u8* arena, hipStream_t s);

@@ -405,10 +405,17 @@ def _lz_edge(kind: str) -> bytes:
         return rng.integers(0, 256, 120_000).astype(np.uint8).tobytes()
     if kind == "text":
         return D.enwik_like(200_000, seed=99)
+    if kind in ("ab_random", "acgt_random"):  # few distinct 3-grams: buckets of ~1000 window
+        sym = np.frombuffer(b"ab" if kind == "ab_random" else b"ACGT", np.uint8)  # positions
+        return sym[rng.integers(0, len(sym), 60_000)].tobytes()
     raise ValueError(kind)
 
 
-@pytest.mark.parametrize("kind", ["long_copies", "period4096", "period4097", "text_zero_runs", "random", "text"])
+LZ_EDGE_KINDS = ["long_copies", "period4096", "period4097", "text_zero_runs", "random", "text", "ab_random",
+                 "acgt_random"]
+
+
+@pytest.mark.parametrize("kind", LZ_EDGE_KINDS)
 def test_lz77_local_edges(kolm_gpu, kind):
     data = _lz_edge(kind)
     assert kolm_gpu.encode_lz77(data)[0] == O.encode_lz77(data)
@@ -425,6 +432,25 @@ def test_lz77_local_block_geometry(kolm_gpu, bs):
     for i in range(nb):
         blk = data[i * bs:(i + 1) * bs]
         assert payloads[i] == O.encode_lz77(blk), f"block {i}"
+
+
+@pytest.mark.parametrize("idx", [0, 1, 2])
+def test_lz77_index_forms(kolm_gpu, monkeypatch, idx):
+    """The three ways k_lz_local gets its window's 3-gram index (KOLM_LZ_IDX, k_lz77.hip): the
+    workgroup's own LDS sort (0), the tile index with u16 slots (1) and with u8 ranks + bucket
+    starts (2, ranks of 255 or more by binary search: the few-3-gram inputs) — every edge input
+    and the block geometries around the tile size, against the oracle (PY:1686-1763)."""
+    from kolm import _lib
+    monkeypatch.setenv("KOLM_LZ_IDX", str(idx))
+    for kind in LZ_EDGE_KINDS:
+        data = _lz_edge(kind)
+        assert kolm_gpu.encode_lz77(data)[0] == O.encode_lz77(data), kind
+    data = (D.enwik_like(30_000, seed=5) + bytes(700) + D.enwik_like(20_000, seed=6))
+    for bs in (255, 4095, 4097, 8192 + 3, 12288 + 5):
+        nb = (len(data) + bs - 1) // bs
+        _, _, payloads, _ = _lib.encode_blocks(data, bs, force=[7] * nb)
+        for i in range(nb):
+            assert payloads[i] == O.encode_lz77(data[i * bs:(i + 1) * bs]), (bs, i)
 
 
 # ---- candidate 10 (v2_new, opt-in; PY:1498-1576 with the automaton evaluated serially) ----
