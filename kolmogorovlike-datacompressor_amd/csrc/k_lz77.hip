@@ -1227,13 +1227,21 @@ const char* lz_spec_name() { return "k_lz_local"; }
 
 u32 lz_chunk_shift() { return 8u; }  // 256-byte chunks
 
-int lz_index_form() {
-    // read per call (tests); default: the in-LDS sort (form 0) until the A/B of the tile forms
-    return getenv("KOLM_LZ_IDX") ? atoi(getenv("KOLM_LZ_IDX")) : 0;
+int lz_index_form(u32 nb) {
+    // Batches of 64 blocks or more: form 0.  There the parse is hidden beside the sort stream
+    // (it ends ~4 ms before it), so the index work inside it costs the step nothing, while the
+    // tile index is one more kernel whose time lands on the sort stream: k_lz_tiles takes ~0.4
+    // ms alone but ~2 ms beside Lyndon or round 0 and slows what it meets (the Lyndon merge 0.27
+    // -> 0.94 ms, the first round-0 pass 0.97 -> 1.73 ms), so form 2 measured 34.1-34.4 ms per
+    // step against 33.2-33.4 for form 0 in every placement (round 6, profiles/r06/ab_lz_idx_*).
+    // Smaller batches: form 2 (config 4's 32-block shard 6.25-6.28 -> 5.92-5.94 ms).
+    // KOLM_LZ_IDX overrides (read per call: tests).
+    if (getenv("KOLM_LZ_IDX")) return atoi(getenv("KOLM_LZ_IDX"));
+    return nb < 64 ? 2 : 0;
 }
 
 void launch_lz_tiles(const LzArgs& z, hipStream_t s, KTimer* kt) {
-    if (!z.geo.nb || lz_index_form() == 0) return;
+    if (!z.geo.nb || lz_index_form(z.geo.nb) == 0) return;
     const u32 hpb = (z.geo.bs + LZL_HOME - 1) / LZL_HOME;
     // text 1 B + rank 2 B per position + 2 KiB of counts per tile
     KScope k(kt, KT_LZPARSE, "k_lz_tiles", z.geo.N * 3 + (u64)z.geo.nb * hpb * 2048);
@@ -1251,7 +1259,7 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt, bool tiles_done
     constexpr u32 home = 4096u;
     static_assert(home == (u32)LZL_HOME, "tile index and homes share the 4 KiB geometry");
     const u32 hpb = (z.geo.bs + home - 1) / home;
-    const int idx = lz_index_form();
+    const int idx = lz_index_form(z.geo.nb);
     if (!tiles_done) launch_lz_tiles(z, s, kt);
     {
         // lead-in bytes parsed before each chain's chunk (at most LZL_LEAD, the window's margin):

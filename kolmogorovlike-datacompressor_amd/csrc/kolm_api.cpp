@@ -1011,6 +1011,17 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     static const int side_env = getenv("KOLM_SIDE_STREAM") ? atoi(getenv("KOLM_SIDE_STREAM")) : -1;
     const bool side = (side_env >= 0 ? side_env != 0 : nb < 64) && !serial && !want_rp;
     hipStream_t xs = side ? c->rp : ms;
+    const bool want_lz = (mask >> KOLM_M_LZ77) & 1u || (h_force != nullptr);
+    LzArgs z = P.lz_args();
+    // Where the LZ77 tile index (k_lz_tiles, forms 1 / 2 of the parse) runs when the parse queues
+    // behind prevc on the index stream: 0 = just before the parse, 1 = ahead of the prevc wait
+    // (beside Lyndon's merge), 2 = first on the index stream (beside the Duval spans); every
+    // placement measured 0.8-1.1 ms slower than form 0 on full batches (lz_index_form).
+    // KOLM_LZ_TEARLY overrides.
+    const int tearly_env = getenv("KOLM_LZ_TEARLY") ? atoi(getenv("KOLM_LZ_TEARLY")) : -1;
+    const int tiles_early = (want_lz && !serial && xs == ms) ? (tearly_env >= 0 ? tearly_env : 0) : 0;
+    c->active = ms;
+    if (tiles_early == 2) launch_lz_tiles(z, ms, c->kt());
     if (side) KOLM_HIP_CHECK(hipStreamWaitEvent(c->rp, ev[0], 0));
     c->active = xs;
     {
@@ -1030,13 +1041,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     // competes with Lyndon and round 0 for CUs), so it keeps the index-stream form.
     // KOLM_PREVC_IDX = 0 / 1 forces it.
     const int prevc_idx = getenv("KOLM_PREVC_IDX") ? atoi(getenv("KOLM_PREVC_IDX")) : -1;  // read per call (tests)
-    const bool want_lz = (mask >> KOLM_M_LZ77) & 1u || (h_force != nullptr);
-    LzArgs z = P.lz_args();
-    // The LZ77 tile index ahead of the prevc wait, beside Lyndon, when the parse queues behind
-    // prevc on this stream (KOLM_LZ_TEARLY = 0 / 1 forces it)
-    const int tearly_env = getenv("KOLM_LZ_TEARLY") ? atoi(getenv("KOLM_LZ_TEARLY")) : -1;
-    const bool tiles_early = want_lz && !serial && xs == ms && (tearly_env >= 0 ? tearly_env != 0 : true);
-    if (tiles_early) launch_lz_tiles(z, ms, c->kt());
+    if (tiles_early == 1) launch_lz_tiles(z, ms, c->kt());
     if (!serial && (prevc_idx >= 0 ? prevc_idx != 0 : nb >= 16)) {
         KOLM_HIP_CHECK(hipStreamWaitEvent(xs, ev[5], 0));
         P.prevc();
@@ -1049,7 +1054,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     auto launch_lz = [&] {
         c->active = ms;
         KOLM_HIP_CHECK(hipEventRecord(ej[2], ms));
-        if (want_lz) P.lz(z, tiles_early);
+        if (want_lz) P.lz(z, tiles_early != 0);
         KOLM_HIP_CHECK(hipEventRecord(ej[1], ms));
     };
     u8* bw = nullptr;

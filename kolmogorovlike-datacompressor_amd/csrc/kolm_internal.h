@@ -455,9 +455,9 @@ struct LzArgs {
     u16* rank;         // [N]
     u16* tcnt;         // [nb * tiles per block * 1024]
 };
-// the window-index form of k_lz_local (KOLM_LZ_IDX; 0 = no tile index) and its tile index
-// (k_lz_tiles; launch_lz_parse runs it first unless tiles_done)
-int lz_index_form();
+// the window-index form of k_lz_local for a batch of nb blocks (KOLM_LZ_IDX; 0 = no tile index)
+// and its tile index (k_lz_tiles; launch_lz_parse runs it first unless tiles_done)
+int lz_index_form(u32 nb);
 void launch_lz_tiles(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr);
 void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr, bool tiles_done = false);
 const char* lz_spec_name();  // the speculative-parse kernel in use (timing / roofline)
