@@ -60,11 +60,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 GOLDEN = os.path.join(REPO, "tests", "golden")
 # what stops a kernel short of the HBM roof when it is not bandwidth (measured)
 LIMITER = {
-    "k_lz_local": "instruction issue + LDS latency (SQ counters, profiles/r06/sq_lz_local.txt): per wave ~20 K "
-                  "VALU, ~9 K SALU, ~1.2 K LDS instructions; a wave issues 44 % of its cycles, waits on LDS data "
-                  "37 %, stalls on issue 19 %; 4 waves per SIMD (33 KB of LDS per workgroup: the text window, "
-                  "its 3-gram index and the slot of every home position); HBM traffic is only the text window "
-                  "and the token records, so the HBM contract fraction is not its bound",
+    "k_lz_local": "instruction issue + LDS latency (SQ counters of this build, profiles/r06/sq_lz_local.txt): "
+                  "per wave 20.8 K VALU, 8.7 K SALU, 1.3 K LDS instructions; a wave issues 47 % of its cycles, "
+                  "waits on data 33 %, stalls on issue 20 %, 35 % of its LDS cycles are bank conflicts; 4 waves "
+                  "per SIMD (33 KB of LDS per workgroup: the text window, its 3-gram index and the slot of every "
+                  "home position); HBM traffic is only the text window and the token records (PMC 1.53 GB per "
+                  "launch), so the HBM contract fraction is not its bound",
     "k_repair": "latency: one workgroup per block, barrier-separated batches of dependent global accesses",
     "k_duval_span": "LDS latency: sequential Duval over each thread's 128-byte chunk, then tree merges of "
                     "adjacent factorisations (dependent LDS byte compares / bitmap scans); reads the text once",

@@ -1240,7 +1240,7 @@ int lz_index_form(u32 nb) {
     return nb < 64 ? 2 : 0;
 }
 
-void launch_lz_tiles(const LzArgs& z, hipStream_t s, KTimer* kt) {
+static void launch_lz_tiles(const LzArgs& z, hipStream_t s, KTimer* kt) {
     if (!z.geo.nb || lz_index_form(z.geo.nb) == 0) return;
     const u32 hpb = (z.geo.bs + LZL_HOME - 1) / LZL_HOME;
     // text 1 B + rank 2 B per position + 2 KiB of counts per tile
@@ -1248,7 +1248,7 @@ void launch_lz_tiles(const LzArgs& z, hipStream_t s, KTimer* kt) {
     k_lz_tiles<<<z.geo.nb * hpb, 256, 0, s>>>(z, hpb);
 }
 
-void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt, bool tiles_done) {
+void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
     if (!z.geo.nb) return;
     // 4 KiB homes, 16 chains of 16 lanes (4 workgroups per CU, LDS-limited).  Measured and
     // removed: 8 KiB homes parsed by 32 chains of 8 lanes (round 5: 2 waves per SIMD no longer hide
@@ -1260,7 +1260,7 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt, bool tiles_done
     static_assert(home == (u32)LZL_HOME, "tile index and homes share the 4 KiB geometry");
     const u32 hpb = (z.geo.bs + home - 1) / home;
     const int idx = lz_index_form(z.geo.nb);
-    if (!tiles_done) launch_lz_tiles(z, s, kt);
+    launch_lz_tiles(z, s, kt);
     {
         // lead-in bytes parsed before each chain's chunk (at most LZL_LEAD, the window's margin):
         // 48 since the stitch's fix-up searches got cheaper (round 5, two A/B calls, profiles/r05/
@@ -1268,8 +1268,9 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt, bool tiles_done
         // measured 34.09-34.44 and 34.18).  KOLM_LZ_LEAD overrides.
         static const u32 lead =
             getenv("KOLM_LZ_LEAD") ? std::min<u32>(atoi(getenv("KOLM_LZ_LEAD")), LZL_LEAD) : 48u;
-        // KOLM_LZ_PAD: extra (unused) LDS bytes per workgroup, to cap the parse's workgroups per CU
-        const u32 pad = getenv("KOLM_LZ_PAD") ? (u32)atoi(getenv("KOLM_LZ_PAD")) : 0u;
+        // (round 6: the parse capped at 3 workgroups per CU by extra LDS measured 33.3 -> 34.2-34.3 ms
+        // per step with form 0, 34.1 -> 33.9-34.0 with form 2)
+        constexpr u32 pad = 0;
         KScope k(kt, KT_LZPARSE, "k_lz_local", z.geo.N * 2);
         if (idx == 0)
             k_lz_local<home, 16, 0><<<z.geo.nb * hpb, LzlGeom<home, 16, 0>::NT, pad, s>>>(z, hpb, lead);

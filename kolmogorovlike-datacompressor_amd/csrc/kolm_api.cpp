@@ -149,8 +149,6 @@ struct kolm_ctx {
     hipStream_t aux = nullptr;     // second stream: Lyndon + cyclic sort chain runs beside LZ77
     hipStream_t active = nullptr;  // stream used by launches / TScope / sync()
     hipStream_t rp = nullptr;      // third stream: Re-Pair (candidate 9), one workgroup per block
-    hipStream_t aux2 = nullptr;    // the sort chain's second stream: half of a round's class sorts
-    hipEvent_t evc[2] = {};        // class-sort fork / join
     bool serial = false;           // every launch of a batch on one stream (kolm_ctx_set_serial; KOLM_SERIAL=1)
     // pinned host staging: an upload ring (input chunks) and the result buffer of
     // kolm_compress_fixed (container bytes, valid until the next call on this context)
@@ -195,7 +193,7 @@ struct kolm_ctx {
         u64 bytes;
         int strm;  // 0 index stream, 1 sort stream, 2 Re-Pair stream
     };
-    int strm_of(hipStream_t s) const { return s == aux || s == aux2 ? 1 : s == rp ? 2 : 0; }
+    int strm_of(hipStream_t s) const { return s == aux ? 1 : s == rp ? 2 : 0; }
     std::vector<Pend> pend;
     struct Acc {
         double ms = 0;
@@ -596,48 +594,22 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
             c->sync();
         }
-        // per element: K2 + SA read, SA + RK write (16 B); per segment record 8 B.  The classes'
-        // sorts touch disjoint segments: with KOLM_CLS_STREAMS=1 they are split over the sort
-        // stream and a second one (largest classes first, each to the less loaded stream), so
-        // the short grids of one class fill the tail of another's
-        const bool two = getenv("KOLM_CLS_STREAMS") && atoi(getenv("KOLM_CLS_STREAMS")) != 0;  // per call (tests)
-        const bool fork = two && !c->serial && s == c->aux;
-        int on2[NCLASS] = {};
-        if (fork) {
-            int ord[NCLASS];
-            for (int k = 0; k < NCLASS; ++k) ord[k] = k;
-            std::sort(ord, ord + NCLASS, [&](int x, int y) { return h[C_CLSE + x] > h[C_CLSE + y]; });
-            u64 load[2] = {0, 0};
-            for (int i = 0; i < NCLASS; ++i) {
-                const int k = ord[i];
-                if (!h[C_CLS + k] || k == 0) continue;
-                const int t = load[1] < load[0] ? 1 : 0;
-                on2[k] = t;
-                load[t] += h[C_CLSE + k] + 2048;  // + a launch's worth of fixed cost
-            }
-            KOLM_HIP_CHECK(hipEventRecord(c->evc[0], s));
-            KOLM_HIP_CHECK(hipStreamWaitEvent(c->aux2, c->evc[0], 0));
-        }
+        // per element: K2 + SA read, SA + RK write (16 B); per segment record 8 B.  (Round 6
+        // measured and removed: the classes' sorts split over the sort stream and a second one —
+        // 33.31-33.36 -> 33.58-33.59 ms per step, config 5 6.07 -> 6.27 ms.)
         for (int k = 0; k < NCLASS; ++k) {
             if (!h[C_CLS + k]) continue;
-            const hipStream_t ks = on2[k] ? c->aux2 : s;
-            c->active = ks;
             if (k >= 1 && k <= tiny_c) {
                 static const char* const tn[6] = {"",          "k_tiny_sort<1>", "k_tiny_sort<2>",
                                                   "k_tiny_sort<3>", "k_tiny_sort<4>", "k_tiny_sort<5>"};
                 // SA + key (KP gather or K2) read, SA + RK write per element; 8 B per segment
                 TScope t(c, KOLM_KT_SMALLSORT, tn[k], (u64)h[C_CLSE + k] * 16 + (u64)h[C_CLS + k] * 8);
-                launch_tiny_sort(k, L.cls[k], h[C_CLS + k], a, L, ks);
+                launch_tiny_sort(k, L.cls[k], h[C_CLS + k], a, L, s);
                 continue;
             }
             const int w32 = a.key_bits + k <= 31 ? 1 : 0;  // matches small_sort_c's choice
             TScope t(c, KOLM_KT_SMALLSORT, kSmallSortName[w32][k], (u64)h[C_CLSE + k] * 16 + (u64)h[C_CLS + k] * 8);
-            launch_small_sort(k, L.cls[k], h[C_CLS + k], a, L, ks);
-        }
-        c->active = s;
-        if (fork) {
-            KOLM_HIP_CHECK(hipEventRecord(c->evc[1], c->aux2));
-            KOLM_HIP_CHECK(hipStreamWaitEvent(s, c->evc[1], 0));
+            launch_small_sort(k, L.cls[k], h[C_CLS + k], a, L, s);
         }
         if (h[C_EQ]) {
             TScope t(c, KOLM_KT_SMALLSORT, "k_finalize_eq", (u64)h[C_EQ] * TILE * 8);
@@ -784,11 +756,11 @@ struct Pipeline {
         return z;
     }
 
-    void lz(const LzArgs& z, bool tiles_done = false) {
+    void lz(const LzArgs& z) {
         KOLM_HIP_CHECK(hipMemsetAsync(z.nlong, 0, sizeof(u32), c->active));
         KOLM_HIP_CHECK(hipMemsetAsync(z.nfix, 0, sizeof(u32), c->active));
         if (z.prof) KOLM_HIP_CHECK(hipMemsetAsync(z.prof, 0, sizeof(u64) * 32, c->active));
-        launch_lz_parse(z, c->active, c->kt(), tiles_done);
+        launch_lz_parse(z, c->active, c->kt());
     }
 };
 
@@ -1013,15 +985,8 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     hipStream_t xs = side ? c->rp : ms;
     const bool want_lz = (mask >> KOLM_M_LZ77) & 1u || (h_force != nullptr);
     LzArgs z = P.lz_args();
-    // Where the LZ77 tile index (k_lz_tiles, forms 1 / 2 of the parse) runs when the parse queues
-    // behind prevc on the index stream: 0 = just before the parse, 1 = ahead of the prevc wait
-    // (beside Lyndon's merge), 2 = first on the index stream (beside the Duval spans); every
-    // placement measured 0.8-1.1 ms slower than form 0 on full batches (lz_index_form).
-    // KOLM_LZ_TEARLY overrides.
-    const int tearly_env = getenv("KOLM_LZ_TEARLY") ? atoi(getenv("KOLM_LZ_TEARLY")) : -1;
-    const int tiles_early = (want_lz && !serial && xs == ms) ? (tearly_env >= 0 ? tearly_env : 0) : 0;
-    c->active = ms;
-    if (tiles_early == 2) launch_lz_tiles(z, ms, c->kt());
+    // (k_lz_tiles, the tile index of the parse's forms 1 / 2, runs right before the parse: placed
+    // ahead of the prevc wait or first on the index stream it measured no better)
     if (side) KOLM_HIP_CHECK(hipStreamWaitEvent(c->rp, ev[0], 0));
     c->active = xs;
     {
@@ -1041,7 +1006,6 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     // competes with Lyndon and round 0 for CUs), so it keeps the index-stream form.
     // KOLM_PREVC_IDX = 0 / 1 forces it.
     const int prevc_idx = getenv("KOLM_PREVC_IDX") ? atoi(getenv("KOLM_PREVC_IDX")) : -1;  // read per call (tests)
-    if (tiles_early == 1) launch_lz_tiles(z, ms, c->kt());
     if (!serial && (prevc_idx >= 0 ? prevc_idx != 0 : nb >= 16)) {
         KOLM_HIP_CHECK(hipStreamWaitEvent(xs, ev[5], 0));
         P.prevc();
@@ -1054,7 +1018,7 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     auto launch_lz = [&] {
         c->active = ms;
         KOLM_HIP_CHECK(hipEventRecord(ej[2], ms));
-        if (want_lz) P.lz(z, tiles_early != 0);
+        if (want_lz) P.lz(z);
         KOLM_HIP_CHECK(hipEventRecord(ej[1], ms));
     };
     u8* bw = nullptr;
@@ -1320,12 +1284,6 @@ int ctx_create(int device, kolm_ctx** out) {
             KOLM_HIP_CHECK(hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, prio == 1 ? hi : lo));
         }
         KOLM_HIP_CHECK(hipStreamCreateWithFlags(&c->rp, hipStreamNonBlocking));
-        {
-            int lo = 0, hi = 0;
-            KOLM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            KOLM_HIP_CHECK(hipStreamCreateWithPriority(&c->aux2, hipStreamNonBlocking, hi));
-        }
-        for (auto& e : c->evc) KOLM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         c->active = c->stream;
         c->serial = getenv("KOLM_SERIAL") && atoi(getenv("KOLM_SERIAL")) != 0;
         for (auto& e : c->evj) KOLM_HIP_CHECK(hipEventCreate(&e));
@@ -1445,14 +1403,12 @@ int kolm_ctx_destroy(kolm_ctx* c) {
         KOLM_HIP_CHECK(hipStreamSynchronize(c->stream));
         KOLM_HIP_CHECK(hipStreamSynchronize(c->aux));
         KOLM_HIP_CHECK(hipStreamSynchronize(c->rp));
-        KOLM_HIP_CHECK(hipStreamSynchronize(c->aux2));
         for (auto& kv : c->bufs)
             if (kv.second.p) KOLM_HIP_CHECK(hipFree(kv.second.p));
         for (auto& e : c->ev) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evj) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evr) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evg) KOLM_HIP_CHECK(hipEventDestroy(e));
-        for (auto& e : c->evc) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evpool) KOLM_HIP_CHECK(hipEventDestroy(e));
         KOLM_HIP_CHECK(hipHostFree(c->h_cnt));
         if (c->h_tail) KOLM_HIP_CHECK(hipHostFree(c->h_tail));
@@ -1467,7 +1423,6 @@ int kolm_ctx_destroy(kolm_ctx* c) {
         KOLM_HIP_CHECK(hipStreamDestroy(c->stream));
         KOLM_HIP_CHECK(hipStreamDestroy(c->aux));
         KOLM_HIP_CHECK(hipStreamDestroy(c->rp));
-        KOLM_HIP_CHECK(hipStreamDestroy(c->aux2));
         delete c;
         return KOLM_OK;
     });

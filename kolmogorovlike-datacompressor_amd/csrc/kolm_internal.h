@@ -455,11 +455,10 @@ struct LzArgs {
     u16* rank;         // [N]
     u16* tcnt;         // [nb * tiles per block * 1024]
 };
-// the window-index form of k_lz_local for a batch of nb blocks (KOLM_LZ_IDX; 0 = no tile index)
-// and its tile index (k_lz_tiles; launch_lz_parse runs it first unless tiles_done)
+// the window-index form of k_lz_local for a batch of nb blocks (KOLM_LZ_IDX; 0 = no tile index);
+// launch_lz_parse runs the tile index (k_lz_tiles) first for forms 1 and 2
 int lz_index_form(u32 nb);
-void launch_lz_tiles(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr);
-void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr, bool tiles_done = false);
+void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt = nullptr);
 const char* lz_spec_name();  // the speculative-parse kernel in use (timing / roofline)
 u32 lz_chunk_shift();        // log2 of the parse's chunk bytes (LzArgs::cshift) for the form in use
 void launch_lz_emit(const LzArgs& z, const u32* method, const u64* off, u8* arena, hipStream_t s);

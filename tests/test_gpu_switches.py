@@ -9,7 +9,6 @@ with the oracle (PY:351-423 BBWT order, PY:460 MTF, PY:1413 Rice, PY:2350-2369 M
   KOLM_PREVC_IDX=1  k_prevc on the index stream below 16 blocks (with 16+ blocks: the early BBWT
                     gather from doubling round 3 on the third stream)
   KOLM_LZ_BIGWIN=0/1  the LZ77 stitch's 5 KiB / 62 KiB brute-force window
-  KOLM_CLS_STREAMS=1  a round's class sorts split over two streams
   KOLM_LZ_IDX=0     the LZ77 parse's in-LDS window sort (the full-batch form) on batches under 64 blocks
 """
 import pytest
@@ -26,7 +25,6 @@ SWITCHES = [
     {"KOLM_PREVC_IDX": "1"},
     {"KOLM_LZ_BIGWIN": "0"},
     {"KOLM_LZ_BIGWIN": "1"},
-    {"KOLM_CLS_STREAMS": "1"},
     {"KOLM_LZ_IDX": "0"},
 ]
 
