@@ -939,6 +939,17 @@ u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w,
         KOLM_HIP_CHECK(hipStreamSynchronize(s));
         return 8;
     }
+    launch_alpha_async(geo, text, pres, code, d_w, h_w, s, kt);
+    KOLM_HIP_CHECK(hipStreamSynchronize(s));
+    return alpha_width(*h_w);
+}
+
+void launch_alpha_async(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w, u32* h_w, hipStream_t s,
+                        KTimer* kt) {
+    if (!geo.N) {
+        *h_w = 8;
+        return;
+    }
     const u32 parts = (geo.bs + AL_PER - 1) / AL_PER;
     KOLM_HIP_CHECK(hipMemsetAsync(pres, 0, sizeof(u32) * 8 * geo.nb, s));
     KOLM_HIP_CHECK(hipMemsetAsync(d_w, 0, sizeof(u32), s));
@@ -948,9 +959,9 @@ u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w,
         k_alpha_codes<<<geo.nb, WG, 0, s>>>(pres, code, d_w);
     }
     KOLM_HIP_CHECK(hipMemcpyAsync(h_w, d_w, sizeof(u32), hipMemcpyDeviceToHost, s));
-    KOLM_HIP_CHECK(hipStreamSynchronize(s));
-    return std::max<u32>(1, std::min<u32>(8, *h_w));
 }
+
+u32 alpha_width(u32 h_w) { return std::max<u32>(1, std::min<u32>(8, h_w)); }
 
 // Round 0 of the cyclic sort: a stable sort of every block's positions by the packed codes
 // of their first C rotation characters (k_keypos_r0: KA = low 32 bits -> RK, KB = high bits

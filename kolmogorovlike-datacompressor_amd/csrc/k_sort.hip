@@ -389,9 +389,12 @@ __global__ __launch_bounds__(256) void k_bin_scan(Bins bn) {
 // ------------------------------------------------------------------------------------
 // key generation
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(WG) void k_keygen_small(const Seg* segs, u32 count, int c, SortArgs a) {
+// One launch for every class of the round (KgClasses): workgroup t belongs to the class whose
+// workgroup range [wg0[c], wg0[c + 1]) holds it (one launch per class before: ~8 short grids per
+// round, each with its own ramp-up and drain)
+__device__ __attribute__((always_inline)) inline void keygen_small_body(const Seg* segs, u32 count, int c, const SortArgs& a, u32 tile) {
     const u32 spt = TILE >> c;
-    const u32 first = (a.xcd ? xcd_tile() : blockIdx.x) * spt;
+    const u32 first = tile * spt;
     const u32 mask = (1u << c) - 1;
     if (a.KP) {
         // dense rounds: K2[g] = KP[SA[g]].  All loads staged before the first store (the
@@ -430,6 +433,16 @@ __global__ __launch_bounds__(WG) void k_keygen_small(const Seg* segs, u32 count,
         const u32 b = a.geo.block_of(s.start);
         a.K2[g] = make_key(a, a.SA[g], a.geo.base(b), a.geo.end(b));
     }
+}
+
+__global__ __launch_bounds__(WG) void k_keygen_small(KgClasses kc, SortArgs a) {
+    const u32 t = blockIdx.x;
+    int c = 1;
+    while (c + 1 < NCLASS && kc.wg0[c + 1] <= t) ++c;
+    // XCD-contiguous tiles inside the class (each class's list is in position order: one XCD's
+    // workgroups then gather RK / KP from one part of each block)
+    const u32 w = t - kc.wg0[c], G = kc.wg0[c + 1] - kc.wg0[c];
+    keygen_small_body(kc.segs[c], kc.count[c], c, a, a.xcd ? xcd_map(w, G) : w);
 }
 
 __global__ __launch_bounds__(WG) void k_keygen_large(const LTile* tiles, const LSeg* segs, SortArgs a) {
@@ -1161,8 +1174,15 @@ void launch_keypos(const SortArgs& a, u32* KP, hipStream_t s) {
     k_keypos<<<grid, 256, 0, s>>>(a, KP);
 }
 
-void launch_keygen_small(int c, const Seg* segs, u32 count, const SortArgs& a, hipStream_t s) {
-    if (count) k_keygen_small<<<cdiv(count, TILE >> c), WG, 0, s>>>(segs, count, c, a);
+void launch_keygen_small(KgClasses kc, const SortArgs& a, hipStream_t s) {
+    u32 n = 0;
+    for (int c = 1; c < NCLASS; ++c) {
+        kc.wg0[c] = n;
+        n += kc.count[c] ? cdiv(kc.count[c], TILE >> c) : 0u;
+    }
+    kc.wg0[0] = 0;
+    kc.wg0[NCLASS] = n;
+    if (n) k_keygen_small<<<n, WG, 0, s>>>(kc, a);
 }
 void launch_keygen_large(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
                          hipStream_t s) {

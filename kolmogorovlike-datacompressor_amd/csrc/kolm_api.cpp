@@ -124,6 +124,7 @@ enum : int {
     C_CDC = 40,      // FastCDC cut count
     C_N = 48,
     H_RSUM = C_N,    // host mirror only (2 words): summed per-block cyclic rounds
+    H_ALPHA = C_N + 4,  // host mirror only: the batch's code width from the early alphabet pass
     H_N = C_N + 16
 };
 
@@ -163,6 +164,7 @@ struct kolm_ctx {
     hipEvent_t evj[4] = {};        // join events
     hipEvent_t evr[2] = {};        // Re-Pair start / done
     hipEvent_t evg[2] = {};        // early BBWT gather: slots marked / gathered
+    hipEvent_t eva = nullptr;      // the early alphabet pass's width copied to the host
     std::mutex mu;
     std::map<std::string, DevBuf> bufs;
     u32* h_cnt = nullptr;  // pinned mirror of the counters
@@ -342,8 +344,12 @@ struct SortOut {
 // at_round (optional) runs on the host once round r's segment list `cur` is classified (its
 // device count at ncur_dev, at most `bound`), before the round's sorts are enqueued.
 using RoundHook = std::function<void(u32 round, const Seg* cur, u32 bound, const u32* ncur_dev)>;
+// alpha_ready (optional): the batch's code tables were built by launch_alpha_async before Lyndon
+// (on another stream, the width in h_cnt[H_ALPHA] once the event completes), so round 0 starts
+// without a host round trip of its own
 SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Factors fac, const u8* FEd,
-                  const std::function<void()>& after_round0 = {}, const RoundHook& at_round = {}) {
+                  const std::function<void()>& after_round0 = {}, const RoundHook& at_round = {},
+                  hipEvent_t alpha_ready = nullptr) {
     hipStream_t s = c->active;
     const u64 N = geo.N;
     SortOut out;
@@ -466,8 +472,15 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             constexpr bool compact = true;
             const u64 nt = lsd_tiles(geo) + 1;
             u8* code = c->get<u8>("r0code", (u64)geo.nb * 256);
-            const u32 w = launch_alpha(geo, text, c->get<u32>("r0pres", (u64)geo.nb * 8), code, cnt + C_ALPHA,
-                                       h + C_ALPHA, compact, s, c->kt());
+            u32 w;
+            if (alpha_ready) {
+                KOLM_HIP_CHECK(hipStreamWaitEvent(s, alpha_ready, 0));
+                KOLM_HIP_CHECK(hipEventSynchronize(alpha_ready));
+                w = alpha_width(h[H_ALPHA]);
+            } else {
+                w = launch_alpha(geo, text, c->get<u32>("r0pres", (u64)geo.nb * 8), code, cnt + C_ALPHA, h + C_ALPHA,
+                                 compact, s, c->kt());
+            }
             const u32 C = std::max<u32>(1, std::min<u32>(32, 64 / w));
             h0 = C;
             R0Bufs r{text, FEd, fac, code, C, w, c->get<u32>("KP", N), a.K2, a.SA, a.K22, a.SA2, a.RK,
@@ -530,11 +543,18 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             }
             // algorithmic bytes per element: SA read + key inputs + K2 write
             const u64 per = a.KP ? 12 : a.initial ? (cyclic ? 20 : 11) : (cyclic ? 20 : 12);
+            KgClasses kc{};
+            u64 kg_elems = 0;
             for (int k = 1; k < NCLASS; ++k) {
+                kc.segs[k] = L.cls[k];
                 if (!h[C_CLS + k]) continue;
                 if (a.KP && k <= tiny_c) continue;  // k_tiny_sort gathers KP itself
-                TScope t(c, KOLM_KT_KEYGEN, "k_keygen_small", (u64)h[C_CLSE + k] * per);
-                launch_keygen_small(k, L.cls[k], h[C_CLS + k], a, s);
+                kc.count[k] = h[C_CLS + k];
+                kg_elems += h[C_CLSE + k];
+            }
+            if (kg_elems) {
+                TScope t(c, KOLM_KT_KEYGEN, "k_keygen_small", kg_elems * per);
+                launch_keygen_small(kc, a, s);
             }
             if (h[C_L0TILE]) {
                 TScope t(c, KOLM_KT_KEYGEN, "k_keygen_large", (u64)h[C_L0ELEM] * per);
@@ -597,6 +617,9 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
         // per element: K2 + SA read, SA + RK write (16 B); per segment record 8 B.  (Round 6
         // measured and removed: the classes' sorts split over the sort stream and a second one —
         // 33.31-33.36 -> 33.58-33.59 ms per step, config 5 6.07 -> 6.27 ms.)
+        // (Round 6 measured and removed: classes 1..4 in one launch — merged, the kernel holds the
+        // largest class's registers, 38-60 VGPRs against 20-34 for classes 1-3 alone, and beside the
+        // LZ77 parse that cost the 256 MiB step 33.1-33.3 -> 35.7-35.8 ms)
         for (int k = 0; k < NCLASS; ++k) {
             if (!h[C_CLS + k]) continue;
             if (k >= 1 && k <= tiny_c) {
@@ -655,6 +678,7 @@ struct Pipeline {
     // early_gather: the encode path allows the early BBWT gather on the third stream (idle:
     // no Re-Pair, prevc computed on another stream)
     bool early_gather = false;
+    hipEvent_t alpha_ready = nullptr;  // set when the alphabet pass ran early (launch_alpha_async)
     u8* cyclic(const std::function<void()>& after_round0 = {}, u8* out = nullptr) {
         const u64 N = geo.N;
         if (!out) out = c->get<u8>("bbwt", N);
@@ -686,7 +710,7 @@ struct Pipeline {
             early = true;
         };
         SortOut cyc = sort_pass(c, geo, text, true, factors(), c->get<u8>("FEd", N), after_round0,
-                                er ? hook : RoundHook{});
+                                er ? hook : RoundHook{}, alpha_ready);
         if (early) {
             KOLM_HIP_CHECK(hipStreamWaitEvent(c->active, c->evg[1], 0));
             TScope t(c, KOLM_KT_LYNDON, "k_bbwt_gather", N / 8 + N / 16);  // the mask + about 1/16 of the slots
@@ -983,6 +1007,16 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     static const int side_env = getenv("KOLM_SIDE_STREAM") ? atoi(getenv("KOLM_SIDE_STREAM")) : -1;
     const bool side = (side_env >= 0 ? side_env != 0 : nb < 64) && !serial && !want_rp;
     hipStream_t xs = side ? c->rp : ms;
+    // Round 0's alphabet (per-block code tables + the batch's code width, one host read) on the
+    // side / index stream beside Lyndon instead of on the sort stream after it: the host reads the
+    // width while Lyndon runs, and round 0 follows Lyndon without a round trip of its own
+    if (nb < 64) {
+        c->active = xs;
+        launch_alpha_async(geo, d_text, c->get<u32>("r0pres", (u64)nb * 8), c->get<u8>("r0code", (u64)nb * 256),
+                           c->get<u32>("r0w", 1), c->h_cnt + H_ALPHA, xs, c->kt());
+        KOLM_HIP_CHECK(hipEventRecord(c->eva, xs));
+        P.alpha_ready = c->eva;
+    }
     const bool want_lz = (mask >> KOLM_M_LZ77) & 1u || (h_force != nullptr);
     LzArgs z = P.lz_args();
     // (k_lz_tiles, the tile index of the parse's forms 1 / 2, runs right before the parse: placed
@@ -1289,6 +1323,7 @@ int ctx_create(int device, kolm_ctx** out) {
         for (auto& e : c->evj) KOLM_HIP_CHECK(hipEventCreate(&e));
         for (auto& e : c->evr) KOLM_HIP_CHECK(hipEventCreate(&e));
         for (auto& e : c->evg) KOLM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        KOLM_HIP_CHECK(hipEventCreateWithFlags(&c->eva, hipEventDisableTiming));
         KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_cnt, sizeof(u32) * H_N, hipHostMallocDefault));
         for (auto& e : c->ev) KOLM_HIP_CHECK(hipEventCreate(&e));
         *out = c.release();
@@ -1409,6 +1444,7 @@ int kolm_ctx_destroy(kolm_ctx* c) {
         for (auto& e : c->evj) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evr) KOLM_HIP_CHECK(hipEventDestroy(e));
         for (auto& e : c->evg) KOLM_HIP_CHECK(hipEventDestroy(e));
+        KOLM_HIP_CHECK(hipEventDestroy(c->eva));
         for (auto& e : c->evpool) KOLM_HIP_CHECK(hipEventDestroy(e));
         KOLM_HIP_CHECK(hipHostFree(c->h_cnt));
         if (c->h_tail) KOLM_HIP_CHECK(hipHostFree(c->h_tail));

@@ -186,11 +186,13 @@ enum : int { KT_CLASSIFY = 0, KT_KEYGEN, KT_MSD, KT_SMALLSORT, KT_LSD, KT_LZPARS
 // round-robin over the 8 XCDs, so give each XCD a contiguous range of tiles — tiles of
 // one block then share an L2 (random accesses inside a block's arrays stay L2-local).
 // Bijective for any grid size.
-__device__ inline u32 xcd_tile() {
-    const u32 w = blockIdx.x, G = gridDim.x;
+// workgroup w of a range of G workgroups -> tile index such that the workgroups one XCD runs
+// (consecutive dispatches go round-robin over the 8 XCDs) take contiguous tiles
+__device__ inline u32 xcd_map(u32 w, u32 G) {
     const u32 x = w & 7, j = w >> 3, q = G >> 3, r = G & 7;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
 }
+__device__ inline u32 xcd_tile() { return xcd_map(blockIdx.x, gridDim.x); }
 
 // Lyndon factors of every block as sorted factor-start lists (k_duval_merge): block b's
 // count[b] starts sit at start[geo.base(b) ..], the first one = base(b).  Read only where
@@ -294,7 +296,14 @@ void launch_pack_spans(const PackSpans& ps, u32* dst, hipStream_t s);
 void launch_classify_bins(const Seg* cur, u32 ncur, const u32* ncur_dev, const SortArgs& a, const Lists& L,
                           const Level& lv0, const Bins& bn, hipStream_t s, bool bins_zeroed = false);
 void launch_keypos(const SortArgs& a, u32* KP, hipStream_t s);
-void launch_keygen_small(int c, const Seg* segs, u32 count, const SortArgs& a, hipStream_t s);
+// the round's key gathers of every small class in one launch: class c's segments segs[c] (count[c]
+// of them; 0 = not launched), wg0 filled by the launcher
+struct KgClasses {
+    const Seg* segs[NCLASS];
+    u32 count[NCLASS];
+    u32 wg0[NCLASS + 1];
+};
+void launch_keygen_small(KgClasses kc, const SortArgs& a, hipStream_t s);
 void launch_keygen_large(const LTile* tiles, u32 ntiles, const LSeg* segs, const SortArgs& a,
                          hipStream_t s);
 constexpr u32 MED_T = 8192;  // the medium sort's capacity (one 1024-thread workgroup per large group)
@@ -355,6 +364,11 @@ struct R0Bufs {
 // per-block code tables for round 0 (alphabet compaction), max code width of the batch
 u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w, u32* h_w, bool compact,
                  hipStream_t s, KTimer* kt = nullptr);
+// the same without the host wait: the width lands in *h_w (pinned) once stream s passes this point;
+// alpha_width() turns it into the width launch_alpha returns
+void launch_alpha_async(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w, u32* h_w, hipStream_t s,
+                        KTimer* kt = nullptr);
+u32 alpha_width(u32 h_w);
 void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s,
                    KTimer* kt = nullptr);
 
