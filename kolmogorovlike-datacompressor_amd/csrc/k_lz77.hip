@@ -186,11 +186,9 @@ struct LzlGeom {
     static constexpr u32 PER = (NW + NT - 1) / NT;          // window elements per lane in the sort
     static constexpr u32 PER2 = (ISL + NT - 1) / NT;        // islot positions per lane (tile index)
     static constexpr u32 cmax(u32 a, u32 b) { return a > b ? a : b; }
-    // B: islot (u16 slots; u8 ranks in form 2) and, before it, the sort's histograms (form 0) or the
-    // two tiles' bucket counts (+ the bucket starts in form 1)
-    static constexpr u32 BBYTES = IDX == 0 ? cmax(2 * ISL, NWV * LZL_NBK * 2)
-                                : IDX == 1 ? cmax(2 * ISL, 2 * (3 * LZL_NBK + 16))
-                                           : cmax(ISL, 2 * 2 * LZL_NBK);
+    // B: islot (u16 slots in form 0, u8 ranks in form 2) and, before it, the sort's histograms
+    // (form 0) or the two tiles' bucket counts (form 2)
+    static constexpr u32 BBYTES = IDX == 0 ? cmax(2 * ISL, NWV * LZL_NBK * 2) : cmax(ISL, 2 * 2 * LZL_NBK);
     static constexpr u32 CST = IDX == 2 ? LZL_NBK + 8 : 1;  // form 2: bucket starts, kept for the parse
     static_assert(NCHAIN % CPW == 0, "whole waves of 64 / LPC chains");
     static_assert(NW < (1u << 14), "window offsets in 14 bits (the winner key)");
@@ -286,7 +284,7 @@ __device__ void lzl_bucket(const u8* t, u16* A, u32 nw, u16* hist, u32* sh) {
     __syncthreads();
 }
 
-// The window's index from a per-tile one (forms 1 and 2 of k_lz_local).  Every position of a
+// The window's index from a per-tile one (form 2 of k_lz_local).  Every position of a
 // block is ranked once, inside its 4 KiB tile, instead of once in each of the two windows that
 // hold it: k_lz_tiles (one workgroup per tile, the stable counting-sort pass of lzl_bucket over
 // the tile alone) writes rank[x], x's rank among the tile's positions of the same hash in
@@ -409,9 +407,10 @@ __device__ inline u32 uleb_n(u32 v) {
 constexpr u32 LZC_HEAD = 0x8000u;   // A[slot] flag: first slot of its hash bucket
 
 // Window index forms (IDX): 0 = the workgroup sorts its whole window in LDS (lzl_bucket);
-// 1 = placed from the tile index (k_lz_tiles), islot as u16 slots; 2 = the same, islot as u8
-// ranks inside the bucket plus the window's bucket starts (31 KB of LDS instead of 33: five
-// workgroups per CU); a rank of 255 or more is found by a binary search of the bucket.
+// 2 = placed from the tile index (k_lz_tiles), islot as u8 ranks inside the bucket plus the
+// window's bucket starts (31 KB of LDS instead of 33: five workgroups per CU); a rank of 255 or
+// more is found by a binary search of the bucket.  (Form 1, the tile index with u16 islot slots at
+// four workgroups per CU, measured between the two and was removed.)
 template <u32 HOME, u32 LPC, u32 IDX>
 __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_local(LzArgs z, u32 hpb, u32 lead) {
     using G = LzlGeom<HOME, LPC, IDX>;
@@ -476,7 +475,7 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
         // the two tiles' bucket counts (tile t - 1 absent for a block's first home)
         u16* c0 = reinterpret_cast<u16*>(B);
         u16* c1 = c0 + LZL_NBK;
-        u16* cs = IDX == 1 ? c1 + LZL_NBK : cst;
+        u16* cs = cst;
         {
             const u32* s1 = reinterpret_cast<const u32*>(z.tcnt + (u64)blockIdx.x * LZL_NBK);
             const u32* s0 = s1 - LZL_NBK / 2;
@@ -526,7 +525,7 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
         }
         // [ilo, top): the lead-in (tile t - 1) and the home (tile t, after tile t - 1's entries);
         // the islot values wait in registers (packed) until the counts are no longer read
-        constexpr u32 KB = IDX == 1 ? 2 : 4;  // islot values per keep word
+        constexpr u32 KB = 4;  // u8 ranks per keep word
         u32 keep[(G::PER2 + KB - 1) / KB] = {};
 #pragma unroll
         for (u32 i0 = 0; i0 < G::PER2; i0 += 4) {
@@ -542,9 +541,8 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
                 if (x < top) {
                     const u32 hh = hash3(tw, x - lo);
                     const u32 rr = r[i - i0] + (x >= hs ? (u32)c0[hh] : 0u);
-                    const u32 slot = cs[hh] + rr;
-                    A[slot] = (u16)((x - lo) | (rr ? 0u : LZC_HEAD));
-                    keep[i / KB] |= (IDX == 1 ? slot : min(rr, 255u)) << ((32 / KB) * (i % KB));
+                    A[cs[hh] + rr] = (u16)((x - lo) | (rr ? 0u : LZC_HEAD));
+                    keep[i / KB] |= min(rr, 255u) << ((32 / KB) * (i % KB));
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -554,12 +552,9 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
 #pragma unroll
         for (u32 i = 0; i < G::PER2; ++i) {
             const u32 x = ilo + i * NT + tid;
-            const u32 v = (keep[i / KB] >> ((32 / KB) * (i % KB))) & (IDX == 1 ? 0xFFFFu : 0xFFu);
+            const u32 v = (keep[i / KB] >> ((32 / KB) * (i % KB))) & 0xFFu;
             if (x < top) {
-                if constexpr (IDX == 1)
-                    isl[x - ilo] = (u16)v;
-                else
-                    r8[x - ilo] = (u8)v;
+                r8[x - ilo] = (u8)v;
             }
         }
     }
@@ -593,7 +588,7 @@ __global__ __launch_bounds__(64 * (HOME / LZL_CHUNK) / (64 / LPC)) void k_lz_loc
         capl = min((u32)LZ_CAP, lim);
         pv = lds8(txt, p - tlo);
         pv1 = lds8(txt, p - tlo + 8);
-        if constexpr (IDX != 2) {
+        if constexpr (IDX == 0) {
             k = p + (u32)LZ_MIN <= end ? (u32)isl[p - ilo] : 0u;
         } else if (p + (u32)LZ_MIN <= end) {
             const u32 hh = (__builtin_bswap32((u32)pv) >> 8) * 0x9E3779B1u >> (32 - LZL_HB);
@@ -1274,8 +1269,6 @@ void launch_lz_parse(const LzArgs& z, hipStream_t s, KTimer* kt) {
         KScope k(kt, KT_LZPARSE, "k_lz_local", z.geo.N * 2);
         if (idx == 0)
             k_lz_local<home, 16, 0><<<z.geo.nb * hpb, LzlGeom<home, 16, 0>::NT, pad, s>>>(z, hpb, lead);
-        else if (idx == 1)
-            k_lz_local<home, 16, 1><<<z.geo.nb * hpb, LzlGeom<home, 16, 1>::NT, pad, s>>>(z, hpb, lead);
         else
             k_lz_local<home, 16, 2><<<z.geo.nb * hpb, LzlGeom<home, 16, 2>::NT, pad, s>>>(z, hpb, lead);
     }
