@@ -922,7 +922,6 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     // LDS-bound parse): 53.8-54.2 ms per 256 MiB for 0, 54.1-54.2 for 1, 55.4-56.2 for 2.
     const bool serial = c->serial;
     // (the MSD round 0's LDS bucket sorts need whole CUs: the parse starts after round 0 there)
-    const int overlap = getenv("KOLM_OVERLAP") ? atoi(getenv("KOLM_OVERLAP")) : 0;
     hipStream_t ms = c->stream, s = serial ? c->stream : c->aux;
     Pipeline P{c, geo, d_text};
     hipEvent_t* ev = c->ev;
@@ -994,10 +993,6 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     c->active = s;
     P.lyndon();
     KOLM_HIP_CHECK(hipEventRecord(ev[5], s));
-    if (overlap == 1) {
-        KOLM_HIP_CHECK(hipEventRecord(ej[3], s));
-        KOLM_HIP_CHECK(hipStreamWaitEvent(ms, ej[3], 0));
-    }
     // Batches of fewer than 64 blocks: the xor / lfsr sizes and (below) the BBWT's predecessor
     // bytes go to the third stream when Re-Pair does not use it, so the LZ77 parse at the head of
     // the index stream starts at once instead of behind them (prevc waits for the Lyndon factors):
@@ -1057,20 +1052,11 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
     };
     u8* bw = nullptr;
     P.early_gather = !serial && !want_rp;  // the third stream is free for the early BBWT gather
-    if (overlap >= 2 && !serial) {
-        // the LZ77 parse (latency-bound) waits for round 0 of the cyclic sort and then runs
-        // beside the doubling rounds; the 3-gram index runs beside Lyndon + round 0
-        c->active = s;
-        bw = P.cyclic([&] {
-            KOLM_HIP_CHECK(hipEventRecord(ej[3], s));
-            KOLM_HIP_CHECK(hipStreamWaitEvent(ms, ej[3], 0));
-            launch_lz();
-        });
-    } else {
-        launch_lz();
-        c->active = s;
-        bw = P.cyclic();
-    }
+    // The parse starts at once (behind prevc on full batches); started after Lyndon or after round
+    // 0 it measured 0-0.4 / 1.5-2 ms slower (rounds 3-4) and 0.9-2.2 ms slower in round 6 (§4)
+    launch_lz();
+    c->active = s;
+    bw = P.cyclic();
     P.early_gather = false;
     // per-block doubling rounds of the omega-order sort (R per block)
     KOLM_HIP_CHECK(hipMemcpyAsync(c->h_cnt + H_RSUM, c->get<u64>("rsum", 1), sizeof(u64), hipMemcpyDeviceToHost, s));
@@ -1310,12 +1296,12 @@ int ctx_create(int device, kolm_ctx** out) {
         c->device = device;
         {
             // the sort chain (aux) is the critical path: give it the higher priority so its
-            // workgroups dispatch ahead of the LZ77 stream (KOLM_PRIO=0: equal, 2: LZ77 higher)
+            // workgroups dispatch ahead of the LZ77 stream (equal priorities and the LZ77 stream
+            // higher measured slower, rounds 2-3)
             int lo = 0, hi = 0;
             KOLM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            const int prio = getenv("KOLM_PRIO") ? atoi(getenv("KOLM_PRIO")) : 1;
-            KOLM_HIP_CHECK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio == 2 ? hi : lo));
-            KOLM_HIP_CHECK(hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, prio == 1 ? hi : lo));
+            KOLM_HIP_CHECK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, lo));
+            KOLM_HIP_CHECK(hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, hi));
         }
         KOLM_HIP_CHECK(hipStreamCreateWithFlags(&c->rp, hipStreamNonBlocking));
         c->active = c->stream;
