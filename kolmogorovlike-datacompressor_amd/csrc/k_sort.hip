@@ -1126,6 +1126,10 @@ __global__ void k_zero_spans(ZeroSpans z) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     for (int k = 0; k < 6; ++k) {
         if (i < z.n[k]) {
+            if (k == 3 && z.done) {  // the previous round's k_update_done, fused
+                if (z.p[3][i]) z.last[i] = z.round + 1;
+                else if (!z.done[i]) z.done[i] = z.round + 1;
+            }
             z.p[k][i] = 0;
             return;
         }

@@ -437,6 +437,9 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
     // VGPRs and was starved beside the LZ77 parse (1.0 ms alone, 3.0 overlapped; step 45.7
     // -> 44.0 ms); class 4 to the LDS sort as well measured 41.8-41.9 -> 42.0-42.1 ms
     constexpr int tiny_c = 4;
+    // the end-of-round k_update_done (cyclic) runs inside the next round's k_zero_spans, which
+    // zeroes the split flags it reads (one launch less per round)
+    int pend_done = -1;
     for (u32 round = 0; round < 64 && ncur; ++round) {
         a.initial = round == 0 ? 1 : 0;
         a.h = round == 0 ? 0u : (h0 << (round - 1));
@@ -458,6 +461,12 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             z.n[2] = C_N - C_CLSE;
             z.p[3] = a.blk_split;
             z.n[3] = (u32)geo.nb;
+            if (pend_done >= 0) {  // the previous round's done / last update rides on this launch
+                z.done = blk_done;
+                z.last = blk_last;
+                z.round = (u32)pend_done;
+                pend_done = -1;
+            }
             if (zero_bins) {
                 z.p[4] = c->get<u32>("cls_bins", NCLASS * CLS_NBIN);
                 z.n[4] = NCLASS * CLS_NBIN;
@@ -494,7 +503,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             launch_round0(geo, r, nxt, L.next_cnt, a.blk_split, s, c->kt());
             out.active += N;
             out.rounds = 1;
-            launch_update_done(blk_done, blk_last, a.blk_split, geo.nb, 0, s);
+            pend_done = 0;  // folded into the next round's k_zero_spans
             if (after_round0) {
                 after_round0();
                 c->active = s;
@@ -585,9 +594,14 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             const u32 ntiles = lvl ? 2 * (nelem0 / TILE) + 1 : ntiles0;
             const u32* dseg = lvl ? lc.nseg : nullptr;
             const u32* dtile = lvl ? lc.ntiles : nullptr;
-            KOLM_HIP_CHECK(hipMemsetAsync(ln.nseg, 0, sizeof(u32), s));
-            KOLM_HIP_CHECK(hipMemsetAsync(ln.ntiles, 0, sizeof(u32), s));
-            KOLM_HIP_CHECK(hipMemsetAsync(ln.nelem, 0, sizeof(u32), s));
+            {
+                // the next level's three counters in one launch (three fill kernels before)
+                ZeroSpans zl{};
+                zl.p[0] = ln.nseg, zl.n[0] = 1;
+                zl.p[1] = ln.ntiles, zl.n[1] = 1;
+                zl.p[2] = ln.nelem, zl.n[2] = 1;
+                launch_zero_spans(zl, s);
+            }
             if (a.med) {
                 TScope t(c, KOLM_KT_SMALLSORT, "k_small_sort<13> (medium)", (u64)nelem0 * 16);
                 launch_med_sort(lc.segs, nseg, lc.nseg, a, L, s);
@@ -638,13 +652,14 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             TScope t(c, KOLM_KT_SMALLSORT, "k_finalize_eq", (u64)h[C_EQ] * TILE * 8);
             launch_finalize_eq(L.eq, h[C_EQ], a, L, s);
         }
-        if (cyclic) launch_update_done(blk_done, blk_last, a.blk_split, geo.nb, round, s);
+        if (cyclic) pend_done = (int)round;  // folded into the next round's k_zero_spans
         round_done(round);
         // the next list holds unresolved segments of >= 2 active elements each
         ncur = (u32)std::min<u64>(h[C_ACTIVE] / 2 + geo.nb, N / 2 + geo.nb);
         ncur_dev = L.next_cnt;
         std::swap(cur, nxt);
     }
+    if (pend_done >= 0) launch_update_done(blk_done, blk_last, a.blk_split, geo.nb, (u32)pend_done, s);
     if (cyclic) launch_rounds_sum(blk_last, geo.nb, c->get<u64>("rsum", 1), s);
     return out;
 }

@@ -282,6 +282,11 @@ void launch_block_segs(Seg* segs, const Geom& geo, hipStream_t s);
 struct ZeroSpans {
     u32* p[6];
     u32 n[6];
+    // optional (done != null): p[3] holds the per-block split flags of the previous round, which
+    // fold into done / last (k_update_done's rule for round `round`) before they are zeroed
+    u32* done = nullptr;
+    u32* last = nullptr;
+    u32 round = 0;
 };
 void launch_zero_spans(const ZeroSpans& z, hipStream_t s);
 // Up to 6 u32 ranges (p[k], n[k] words) copied to dst + o[k] by one launch: the small results
