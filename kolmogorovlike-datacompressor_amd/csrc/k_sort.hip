@@ -759,24 +759,21 @@ __device__ inline void sort_epilogue(KT (&r)[8], const Seg* ss, u8* ssplit, cons
     }
 }
 
-template <int C, class KT, u32 T = TILE, u32 NT = WG>
-__global__ __launch_bounds__(NT) void k_small_sort(const Seg* segs, u32 count, SortArgs a, Lists L) {
+// The small sort of class C for the workgroup's tile `tile` of the class list, on LDS arrays its
+// kernel provides (k_small_sort: one class per launch; k_small_sort_all: classes 5..11 of one
+// round in one launch, arrays sized for the smallest class).
+template <int C, class KT, u32 T, u32 NT>
+__device__ __attribute__((always_inline)) inline void small_sort_body(const Seg* segs, u32 count, SortArgs a, Lists L,
+                                                                     u32 tile, KT* sk, u32* sa_l, Seg* ss, u32* sh,
+                                                                     u32* last_hi, u8* ssplit) {
     static_assert(T == 8 * NT, "8 elements per thread");
-    constexpr u32 NWV = NT / 64;
     constexpr u32 PT = T / NT;
     constexpr u32 S = 1u << C;
     constexpr u32 SPT = T / S;
     constexpr bool W32 = sizeof(KT) == 4;
     constexpr KT NONEK = ~(KT)0;
-    // one pad word per 64: the per-thread 8-element runs (8*tid + e) hit 64 distinct banks
-    __shared__ KT sk[T + T / 64];
-    __shared__ u32 sa_l[W32 ? T : 1];
-    __shared__ Seg ss[SPT];
-    __shared__ u32 sh[NWV];
-    __shared__ u32 last_hi[NT];
-    __shared__ u8 ssplit[SPT];  // sub-array split by this round's key
     const u32 tid = threadIdx.x;
-    const u32 first = (a.xcd ? xcd_tile() : blockIdx.x) * SPT;
+    const u32 first = tile * SPT;
     const u32 nthis = min(SPT, count - first);
     for (u32 i = tid; i < SPT; i += NT) {
         ss[i] = i < nthis ? segs[first + i] : Seg{0, 0};
@@ -837,6 +834,48 @@ __global__ __launch_bounds__(NT) void k_small_sort(const Seg* segs, u32 count, S
         reg_stage<1>(r, tid, k, S);
     }
     sort_epilogue<C, KT, T, NT>(r, ss, ssplit, sa_l, sh, last_hi, a, L);
+}
+
+template <int C, class KT, u32 T = TILE, u32 NT = WG>
+__global__ __launch_bounds__(NT) void k_small_sort(const Seg* segs, u32 count, SortArgs a, Lists L) {
+    constexpr u32 SPT = T >> C;
+    constexpr bool W32 = sizeof(KT) == 4;
+    // one pad word per 64: the per-thread 8-element runs (8*tid + e) hit 64 distinct banks
+    __shared__ KT sk[T + T / 64];
+    __shared__ u32 sa_l[W32 ? T : 1];
+    __shared__ Seg ss[SPT];
+    __shared__ u32 sh[NT / 64];
+    __shared__ u32 last_hi[NT];
+    __shared__ u8 ssplit[SPT];  // sub-array split by this round's key
+    small_sort_body<C, KT, T, NT>(segs, count, a, L, a.xcd ? xcd_tile() : blockIdx.x, sk, sa_l, ss, sh, last_hi,
+                                  ssplit);
+}
+
+// classes 5..11 of a round in one launch (every class sorts TILE elements per workgroup in the
+// same LDS arrays; the per-segment arrays are sized for class 5); workgroup t belongs to the class
+// whose range [wg0[c], wg0[c + 1]) holds it, tiles XCD-contiguous inside each class
+template <class KT>
+__global__ __launch_bounds__(WG) void k_small_sort_all(SsClasses sc, SortArgs a, Lists L) {
+    constexpr u32 T = TILE, NT = WG, SPT = T >> 5;
+    constexpr bool W32 = sizeof(KT) == 4;
+    __shared__ KT sk[T + T / 64];
+    __shared__ u32 sa_l[W32 ? T : 1];
+    __shared__ Seg ss[SPT];
+    __shared__ u32 sh[NT / 64];
+    __shared__ u32 last_hi[NT];
+    __shared__ u8 ssplit[SPT];
+    const u32 t = blockIdx.x;
+    int c = 5;
+    while (c < 11 && sc.wg0[c + 1] <= t) ++c;
+    const u32 w = t - sc.wg0[c], G = sc.wg0[c + 1] - sc.wg0[c];
+    const u32 tile = a.xcd ? xcd_map(w, G) : w;
+    switch (c) {
+#define KOLM_SS_CASE(K) \
+    case K: small_sort_body<K, KT, T, NT>(sc.segs[K], sc.count[K], a, L, tile, sk, sa_l, ss, sh, last_hi, ssplit); break;
+        KOLM_SS_CASE(5) KOLM_SS_CASE(6) KOLM_SS_CASE(7) KOLM_SS_CASE(8) KOLM_SS_CASE(9) KOLM_SS_CASE(10)
+        default: small_sort_body<11, KT, T, NT>(sc.segs[11], sc.count[11], a, L, tile, sk, sa_l, ss, sh, last_hi, ssplit); break;
+#undef KOLM_SS_CASE
+    }
 }
 
 // Medium sort (batches of few blocks): one 1024-thread workgroup sorts one large group of
@@ -1248,6 +1287,19 @@ void launch_small_sort(int c, const Seg* segs, u32 count, const SortArgs& a, con
         case 11: small_sort_c<11>(segs, count, a, L, s); break;
         default: break;
     }
+}
+void launch_small_sorts(SsClasses sc, bool w32, const SortArgs& a, const Lists& L, hipStream_t s) {
+    u32 n = 0;
+    for (int c = 5; c <= 11; ++c) {
+        sc.wg0[c] = n;
+        n += sc.count[c] ? cdiv(sc.count[c], TILE >> c) : 0u;
+    }
+    sc.wg0[12] = n;
+    if (!n) return;
+    if (w32)
+        k_small_sort_all<u32><<<n, WG, 0, s>>>(sc, a, L);
+    else
+        k_small_sort_all<u64><<<n, WG, 0, s>>>(sc, a, L);
 }
 void launch_med_sort(const LSeg* segs, u32 nseg, const u32* ndev, const SortArgs& a, const Lists& L,
                      hipStream_t s) {

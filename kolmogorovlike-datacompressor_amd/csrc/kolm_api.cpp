@@ -644,9 +644,26 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
                 launch_tiny_sort(k, L.cls[k], h[C_CLS + k], a, L, s);
                 continue;
             }
+            if (k >= 5) continue;  // classes 5..11: below, one launch per sort-word width
             const int w32 = a.key_bits + k <= 31 ? 1 : 0;  // matches small_sort_c's choice
             TScope t(c, KOLM_KT_SMALLSORT, kSmallSortName[w32][k], (u64)h[C_CLSE + k] * 16 + (u64)h[C_CLS + k] * 8);
             launch_small_sort(k, L.cls[k], h[C_CLS + k], a, L, s);
+        }
+        for (int w32 = 1; w32 >= 0; --w32) {
+            // classes 5..11 in one launch per sort-word width (k_small_sort_all; one launch per
+            // class before: up to 7 short grids per round)
+            SsClasses sc{};
+            u64 els = 0, segs = 0;
+            for (int k = 5; k < NCLASS; ++k) {
+                sc.segs[k] = L.cls[k];
+                if (!h[C_CLS + k] || (a.key_bits + k <= 31 ? 1 : 0) != w32) continue;
+                sc.count[k] = h[C_CLS + k];
+                els += h[C_CLSE + k];
+                segs += h[C_CLS + k];
+            }
+            if (!segs) continue;
+            TScope t(c, KOLM_KT_SMALLSORT, w32 ? "k_small_sort_all<u32>" : "k_small_sort_all<u64>", els * 16 + segs * 8);
+            launch_small_sorts(sc, w32 != 0, a, L, s);
         }
         if (h[C_EQ]) {
             TScope t(c, KOLM_KT_SMALLSORT, "k_finalize_eq", (u64)h[C_EQ] * TILE * 8);

@@ -328,6 +328,14 @@ constexpr int TINY_C = 5;  // classes 1..TINY_C (<= 32 elements): one thread per
 void launch_tiny_sort(int c, const Seg* segs, u32 count, const SortArgs& a, const Lists& L, hipStream_t s);
 void launch_small_sort(int c, const Seg* segs, u32 count, const SortArgs& a, const Lists& L,
                        hipStream_t s);
+// classes 5..11 of a round in one launch (those with count 0 skipped; wg0 filled by the launcher),
+// 32-bit (w32) or 64-bit sort words for all of them
+struct SsClasses {
+    const Seg* segs[NCLASS];
+    u32 count[NCLASS];
+    u32 wg0[NCLASS + 1];
+};
+void launch_small_sorts(SsClasses sc, bool w32, const SortArgs& a, const Lists& L, hipStream_t s);
 void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists& L, hipStream_t s);
 void launch_rounds_sum(const u32* blk_last, u32 nb, u64* out, hipStream_t s);
 void launch_update_done(u32* blk_done, u32* blk_last, const u32* blk_split, u32 nb, u32 round, hipStream_t s);
