@@ -945,20 +945,22 @@ u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w,
 }
 
 void launch_alpha_async(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w, u32* h_w, hipStream_t s,
-                        KTimer* kt) {
+                        KTimer* kt, bool zeroed) {
     if (!geo.N) {
-        *h_w = 8;
+        if (h_w) *h_w = 8;
         return;
     }
     const u32 parts = (geo.bs + AL_PER - 1) / AL_PER;
-    KOLM_HIP_CHECK(hipMemsetAsync(pres, 0, sizeof(u32) * 8 * geo.nb, s));
-    KOLM_HIP_CHECK(hipMemsetAsync(d_w, 0, sizeof(u32), s));
+    if (!zeroed) {  // (zeroed: the caller's k_zero_spans cleared pres and *d_w)
+        KOLM_HIP_CHECK(hipMemsetAsync(pres, 0, sizeof(u32) * 8 * geo.nb, s));
+        KOLM_HIP_CHECK(hipMemsetAsync(d_w, 0, sizeof(u32), s));
+    }
     {
         KScope k(kt, KT_LSD, "k_alpha_present", geo.N);
         k_alpha_present<<<parts * geo.nb, WG, 0, s>>>(geo, text, parts, pres);
         k_alpha_codes<<<geo.nb, WG, 0, s>>>(pres, code, d_w);
     }
-    KOLM_HIP_CHECK(hipMemcpyAsync(h_w, d_w, sizeof(u32), hipMemcpyDeviceToHost, s));
+    if (h_w) KOLM_HIP_CHECK(hipMemcpyAsync(h_w, d_w, sizeof(u32), hipMemcpyDeviceToHost, s));
 }
 
 u32 alpha_width(u32 h_w) { return std::max<u32>(1, std::min<u32>(8, h_w)); }

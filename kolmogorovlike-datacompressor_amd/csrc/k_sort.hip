@@ -1288,6 +1288,18 @@ void launch_small_sort(int c, const Seg* segs, u32 count, const SortArgs& a, con
         default: break;
     }
 }
+// One wave: each lane stores at most one counter word (n <= 64), then lane 0's system-scope
+// release store of the sequence number (the release waits for the wave's earlier stores and
+// makes them visible to the host first).
+__global__ __launch_bounds__(64) void k_counts_to_host(const u32* cnt, u32* hdst, u32 n, u32* hseq, u32 seq) {
+    const u32 i = threadIdx.x;
+    if (i < n) __hip_atomic_store(hdst + i, cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (i == 0) __hip_atomic_store(hseq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+void launch_counts_to_host(const u32* cnt, u32* hdst, u32 n, u32* hseq, u32 seq, hipStream_t s) {
+    if (n > 64) throw HipError(hipErrorInvalidValue, "launch_counts_to_host: more than 64 words", __LINE__);
+    k_counts_to_host<<<1, 64, 0, s>>>(cnt, hdst, n, hseq, seq);
+}
 void launch_small_sorts(SsClasses sc, bool w32, const SortArgs& a, const Lists& L, hipStream_t s) {
     u32 n = 0;
     for (int c = 5; c <= 11; ++c) {

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <sys/mman.h>  // madvise (kolm_result_copy)
 #include <condition_variable>
@@ -168,6 +169,11 @@ struct kolm_ctx {
     std::mutex mu;
     std::map<std::string, DevBuf> bufs;
     u32* h_cnt = nullptr;  // pinned mirror of the counters
+    // fine-grained (coherent) host words the sort stream's per-round counters are stored into by
+    // k_counts_to_host: [0, 64) the counters, [64] the sequence number written after them
+    u32* h_rt = nullptr;
+    u32* d_rt = nullptr;  // the same buffer as the device addresses it
+    u32 rt_seq = 0;
     // pinned landing buffer of a batch's packed small results (one device-to-host copy per
     // host round trip instead of one per array: each copy is a blit launch of ~15-25 us)
     u32* h_tail = nullptr;
@@ -279,6 +285,26 @@ struct kolm_ctx {
     u64 bytes_held(const char* name) const {
         const auto it = bufs.find(name);
         return it == bufs.end() ? 0 : it->second.cap;
+    }
+    // The doubling rounds' counter read-back: one wave stores the counters into coherent host
+    // memory and then a sequence number (system-scope release), the host spins on that word — no
+    // blit dispatch and no stream query between the last kernel and the host's next launch.  A
+    // stream error or a finished stream without the flag ends the wait with an error.
+    void read_counts(u32* h, const u32* cnt, u32 n, hipStream_t s) {
+        const u32 seq = ++rt_seq;
+        kolm::launch_counts_to_host(cnt, d_rt, n, d_rt + 64, seq, s);
+        volatile u32* f = h_rt + 64;
+        for (u32 it = 1; *f != seq; ++it) {
+            if (it % 1024 == 0) {
+                const hipError_t e = hipStreamQuery(s);
+                if (e == hipErrorNotReady) continue;
+                KOLM_HIP_CHECK(e);
+                if (*f != seq) throw kolm::HipError(hipErrorUnknown, "counter flag not seen after the stream finished", __LINE__);
+            }
+            __builtin_ia32_pause();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        for (u32 i = 0; i < n; ++i) h[i] = ((volatile u32*)h_rt)[i];
     }
     // Host round trips (per-round counters) spin on the stream instead of sleeping in
     // hipStreamSynchronize: the sort stream idles for the host's wake-up otherwise.
@@ -467,6 +493,11 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
                 z.round = (u32)pend_done;
                 pend_done = -1;
             }
+            if (round == 0 && cyclic && !alpha_ready) {
+                // the alphabet pass's presence bits (its width word cnt[C_ALPHA] is in span 1)
+                z.p[4] = c->get<u32>("r0pres", (u64)geo.nb * 8);
+                z.n[4] = (u32)geo.nb * 8;
+            }
             if (zero_bins) {
                 z.p[4] = c->get<u32>("cls_bins", NCLASS * CLS_NBIN);
                 z.n[4] = NCLASS * CLS_NBIN;
@@ -478,7 +509,6 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
         if (round == 0 && cyclic) {
             // round 0: stable LSD passes over the packed codes of the first C rotation
             // characters (alphabet-compacted codes), no host round trips but one
-            constexpr bool compact = true;
             const u64 nt = lsd_tiles(geo) + 1;
             u8* code = c->get<u8>("r0code", (u64)geo.nb * 256);
             u32 w;
@@ -487,8 +517,11 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
                 KOLM_HIP_CHECK(hipEventSynchronize(alpha_ready));
                 w = alpha_width(h[H_ALPHA]);
             } else {
-                w = launch_alpha(geo, text, c->get<u32>("r0pres", (u64)geo.nb * 8), code, cnt + C_ALPHA, h + C_ALPHA,
-                                 compact, s, c->kt());
+                // the width back through the counter flag (no fills, no blit, no blocking sync)
+                launch_alpha_async(geo, text, c->get<u32>("r0pres", (u64)geo.nb * 8), code, cnt + C_ALPHA, nullptr,
+                                   s, c->kt(), true);
+                c->read_counts(h + C_ALPHA, cnt + C_ALPHA, 1, s);
+                w = alpha_width(h[C_ALPHA]);
             }
             const u32 C = std::max<u32>(1, std::min<u32>(32, 64 / w));
             h0 = C;
@@ -523,8 +556,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             launch_classify_bins(cur, ncur, ncur_dev, a, L, lv[0], bn, s, zero_bins);
             a.xcd = 1;
         }
-        KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
-        c->sync();
+        c->read_counts(h, cnt, C_N, s);
         if (h[C_ACTIVE] == 0) break;
         out.active += h[C_ACTIVE];
         out.rounds = round + 1;
@@ -624,10 +656,7 @@ SortOut sort_pass(kolm_ctx* c, const Geom& geo, const u8* text, bool cyclic, Fac
             }
             hi = shift;
         }
-        if (lvl) {  // the MSD levels appended segments to the class lists: fresh counts
-            KOLM_HIP_CHECK(hipMemcpyAsync(h, cnt, sizeof(u32) * C_N, hipMemcpyDeviceToHost, s));
-            c->sync();
-        }
+        if (lvl) c->read_counts(h, cnt, C_N, s);  // the MSD levels appended segments to the class lists
         // per element: K2 + SA read, SA + RK write (16 B); per segment record 8 B.  (Round 6
         // measured and removed: the classes' sorts split over the sort stream and a second one —
         // 33.31-33.36 -> 33.58-33.59 ms per step, config 5 6.07 -> 6.27 ms.)
@@ -1343,6 +1372,9 @@ int ctx_create(int device, kolm_ctx** out) {
         for (auto& e : c->evg) KOLM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         KOLM_HIP_CHECK(hipEventCreateWithFlags(&c->eva, hipEventDisableTiming));
         KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_cnt, sizeof(u32) * H_N, hipHostMallocDefault));
+        KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_rt, 4096, hipHostMallocCoherent | hipHostMallocMapped));
+        std::memset(c->h_rt, 0, 4096);
+        KOLM_HIP_CHECK(hipHostGetDevicePointer((void**)&c->d_rt, c->h_rt, 0));
         for (auto& e : c->ev) KOLM_HIP_CHECK(hipEventCreate(&e));
         *out = c.release();
         return KOLM_OK;
@@ -1465,6 +1497,7 @@ int kolm_ctx_destroy(kolm_ctx* c) {
         KOLM_HIP_CHECK(hipEventDestroy(c->eva));
         for (auto& e : c->evpool) KOLM_HIP_CHECK(hipEventDestroy(e));
         KOLM_HIP_CHECK(hipHostFree(c->h_cnt));
+        if (c->h_rt) KOLM_HIP_CHECK(hipHostFree(c->h_rt));
         if (c->h_tail) KOLM_HIP_CHECK(hipHostFree(c->h_tail));
         for (int i = 0; i < kolm_ctx::NSTAGE; ++i) {
             if (c->stage[i]) KOLM_HIP_CHECK(hipHostFree(c->stage[i]));

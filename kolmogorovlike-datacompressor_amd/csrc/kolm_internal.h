@@ -336,6 +336,8 @@ struct SsClasses {
     u32 wg0[NCLASS + 1];
 };
 void launch_small_sorts(SsClasses sc, bool w32, const SortArgs& a, const Lists& L, hipStream_t s);
+// the per-round counters into coherent host memory, then `seq` into *hseq (one wave)
+void launch_counts_to_host(const u32* cnt, u32* hdst, u32 n, u32* hseq, u32 seq, hipStream_t s);
 void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists& L, hipStream_t s);
 void launch_rounds_sum(const u32* blk_last, u32 nb, u64* out, hipStream_t s);
 void launch_update_done(u32* blk_done, u32* blk_last, const u32* blk_split, u32 nb, u32 round, hipStream_t s);
@@ -380,7 +382,7 @@ u32 launch_alpha(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w,
 // the same without the host wait: the width lands in *h_w (pinned) once stream s passes this point;
 // alpha_width() turns it into the width launch_alpha returns
 void launch_alpha_async(const Geom& geo, const u8* text, u32* pres, u8* code, u32* d_w, u32* h_w, hipStream_t s,
-                        KTimer* kt = nullptr);
+                        KTimer* kt = nullptr, bool zeroed = false);
 u32 alpha_width(u32 h_w);
 void launch_round0(const Geom& geo, const R0Bufs& t, Seg* next, u32* next_cnt, u32* blk_split, hipStream_t s,
                    KTimer* kt = nullptr);
