@@ -1288,17 +1288,26 @@ void launch_small_sort(int c, const Seg* segs, u32 count, const SortArgs& a, con
         default: break;
     }
 }
-// One wave: each lane stores at most one counter word (n <= 64), then lane 0's system-scope
-// release store of the sequence number (the release waits for the wave's earlier stores and
-// makes them visible to the host first).
-__global__ __launch_bounds__(64) void k_counts_to_host(const u32* cnt, u32* hdst, u32 n, u32* hseq, u32 seq) {
-    const u32 i = threadIdx.x;
-    if (i < n) __hip_atomic_store(hdst + i, cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (i == 0) __hip_atomic_store(hseq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+// Up to 6 u32 spans into coherent host memory (hdst[o[k] + j] = p[k][j]), then each wave's
+// sequence word: lane 0's system-scope release store waits for the wave's earlier stores and
+// makes them visible to the host first, so the host reads the spans once every wave's word
+// holds `seq` (no blit, no stream query).
+__global__ __launch_bounds__(256) void k_spans_to_host(PackSpans ps, u32* hdst, u32* hseq, u32 seq) {
+    for (int k = 0; k < 6; ++k)
+        for (u32 j = threadIdx.x; j < ps.n[k]; j += blockDim.x)
+            __hip_atomic_store(hdst + ps.o[k] + j, ps.p[k][j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if ((threadIdx.x & 63) == 0)
+        __hip_atomic_store(hseq + (threadIdx.x >> 6), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-void launch_counts_to_host(const u32* cnt, u32* hdst, u32 n, u32* hseq, u32 seq, hipStream_t s) {
-    if (n > 64) throw HipError(hipErrorInvalidValue, "launch_counts_to_host: more than 64 words", __LINE__);
-    k_counts_to_host<<<1, 64, 0, s>>>(cnt, hdst, n, hseq, seq);
+u32 launch_spans_to_host(const PackSpans& ps, u32* hdst, u32* hseq, u32 seq, hipStream_t s) {
+    u32 tot = 0;
+    for (int k = 0; k < 6; ++k) tot += ps.p[k] ? ps.n[k] : 0;
+    const u32 waves = std::max<u32>(1, std::min<u32>(4, (tot + 255) / 256));
+    PackSpans q = ps;
+    for (int k = 0; k < 6; ++k)
+        if (!q.p[k]) q.n[k] = 0;
+    k_spans_to_host<<<1, 64 * waves, 0, s>>>(q, hdst, hseq, seq);
+    return waves;
 }
 void launch_small_sorts(SsClasses sc, bool w32, const SortArgs& a, const Lists& L, hipStream_t s) {
     u32 n = 0;

@@ -169,8 +169,8 @@ struct kolm_ctx {
     std::mutex mu;
     std::map<std::string, DevBuf> bufs;
     u32* h_cnt = nullptr;  // pinned mirror of the counters
-    // fine-grained (coherent) host words the sort stream's per-round counters are stored into by
-    // k_counts_to_host: [0, 64) the counters, [64] the sequence number written after them
+    // fine-grained (coherent) host words small device results are stored into by k_spans_to_host
+    // (read_spans below): RT_WORDS result words, then one sequence word per wave
     u32* h_rt = nullptr;
     u32* d_rt = nullptr;  // the same buffer as the device addresses it
     u32 rt_seq = 0;
@@ -286,25 +286,46 @@ struct kolm_ctx {
         const auto it = bufs.find(name);
         return it == bufs.end() ? 0 : it->second.cap;
     }
-    // The doubling rounds' counter read-back: one wave stores the counters into coherent host
-    // memory and then a sequence number (system-scope release), the host spins on that word — no
-    // blit dispatch and no stream query between the last kernel and the host's next launch.  A
-    // stream error or a finished stream without the flag ends the wait with an error.
-    void read_counts(u32* h, const u32* cnt, u32 n, hipStream_t s) {
+    // Small device results back to the host (the doubling rounds' counters, the batch's
+    // offsets / winners / sizes): k_spans_to_host stores the spans into coherent host memory
+    // and then each wave's sequence word (system-scope release), and the host spins on those
+    // words — no blit dispatch and no stream query between the last kernel and the host's next
+    // launch.  A stream error, or a finished stream without the words, ends the wait with an
+    // error.  Returns the spans' words (h_rt[o[k] + j]).
+    static constexpr u32 RT_WORDS = 16384;  // h_rt: RT_WORDS result words, then 4 sequence words
+    const u32* read_spans(const kolm::PackSpans& ps, hipStream_t s) {
         const u32 seq = ++rt_seq;
-        kolm::launch_counts_to_host(cnt, d_rt, n, d_rt + 64, seq, s);
-        volatile u32* f = h_rt + 64;
-        for (u32 it = 1; *f != seq; ++it) {
+        const u32 waves = kolm::launch_spans_to_host(ps, d_rt, d_rt + RT_WORDS, seq, s);
+        volatile u32* f = h_rt + RT_WORDS;
+        for (u32 w = 0, it = 1; w < waves; ++it) {
+            if (f[w] == seq) {
+                ++w;
+                continue;
+            }
             if (it % 1024 == 0) {
                 const hipError_t e = hipStreamQuery(s);
-                if (e == hipErrorNotReady) continue;
-                KOLM_HIP_CHECK(e);
-                if (*f != seq) throw kolm::HipError(hipErrorUnknown, "counter flag not seen after the stream finished", __LINE__);
+                if (e != hipErrorNotReady) {
+                    KOLM_HIP_CHECK(e);
+                    if (f[w] != seq)
+                        throw kolm::HipError(hipErrorUnknown, "result words not seen after the stream finished", __LINE__);
+                }
             }
             __builtin_ia32_pause();
         }
         std::atomic_thread_fence(std::memory_order_acquire);
-        for (u32 i = 0; i < n; ++i) h[i] = ((volatile u32*)h_rt)[i];
+        return h_rt;
+    }
+    static bool fits_rt(const kolm::PackSpans& ps) {
+        u64 end = 0;
+        for (int k = 0; k < 6; ++k)
+            if (ps.p[k]) end = std::max<u64>(end, (u64)ps.o[k] + ps.n[k]);
+        return end <= RT_WORDS;
+    }
+    void read_counts(u32* h, const u32* cnt, u32 n, hipStream_t s) {
+        kolm::PackSpans ps{};
+        ps.p[0] = cnt, ps.n[0] = n, ps.o[0] = 0;
+        const volatile u32* r = read_spans(ps, s);
+        for (u32 i = 0; i < n; ++i) h[i] = r[i];
     }
     // Host round trips (per-round counters) spin on the stream instead of sleeping in
     // hipStreamSynchronize: the sort stream idles for the host's wake-up otherwise.
@@ -1182,11 +1203,17 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         ps.p[2] = cnt, ps.n[2] = C_N, ps.o[2] = w_off + w_win;
         ps.p[3] = rpa.result, ps.n[3] = w_rp, ps.o[3] = w_off + w_win + C_N;
         const u32 words = w_off + w_win + C_N + w_rp;
-        u32* dtail = c->get<u32>("tail", words);
-        u32* htail = c->tail_host(words);
-        launch_pack_spans(ps, dtail, s);
-        KOLM_HIP_CHECK(hipMemcpyAsync(htail, dtail, sizeof(u32) * words, hipMemcpyDeviceToHost, s));
-        c->sync();
+        const u32* htail;
+        if (kolm_ctx::fits_rt(ps)) {
+            htail = c->read_spans(ps, s);  // straight into coherent host memory
+        } else {
+            u32* dtail = c->get<u32>("tail", words);
+            u32* ht = c->tail_host(words);
+            launch_pack_spans(ps, dtail, s);
+            KOLM_HIP_CHECK(hipMemcpyAsync(ht, dtail, sizeof(u32) * words, hipMemcpyDeviceToHost, s));
+            c->sync();
+            htail = ht;
+        }
         std::memcpy(off.data(), htail, sizeof(u64) * (nb + 1));
         std::memcpy(win.data(), htail + w_off, sizeof(u32) * nb);
         std::memcpy(c->h_cnt, htail + w_off + w_win, sizeof(u32) * C_N);
@@ -1259,11 +1286,17 @@ int encode_batch(kolm_ctx* c, const u8* d_text, u64 N, u32 bs, const u32* h_boun
         ps.p[1] = cnt, ps.n[1] = C_N, ps.o[1] = w_sz;
         ps.p[2] = z.ntok, ps.n[2] = w_nt, ps.o[2] = w_sz + C_N;
         const u32 words = w_sz + C_N + w_nt;
-        u32* dtail = c->get<u32>("tail", words);
-        u32* htail = c->tail_host(words);
-        launch_pack_spans(ps, dtail, s);
-        KOLM_HIP_CHECK(hipMemcpyAsync(htail, dtail, sizeof(u32) * words, hipMemcpyDeviceToHost, s));
-        c->sync();
+        const u32* htail;
+        if (kolm_ctx::fits_rt(ps)) {
+            htail = c->read_spans(ps, s);  // straight into coherent host memory
+        } else {
+            u32* dtail = c->get<u32>("tail", words);
+            u32* ht = c->tail_host(words);
+            launch_pack_spans(ps, dtail, s);
+            KOLM_HIP_CHECK(hipMemcpyAsync(ht, dtail, sizeof(u32) * words, hipMemcpyDeviceToHost, s));
+            c->sync();
+            htail = ht;
+        }
         if (h_sizes) std::memcpy(h_sizes, htail, sizeof(u32) * w_sz);
         if (h_method) std::memcpy(h_method, win.data(), sizeof(u32) * nb);
         std::memcpy(c->h_cnt, htail + w_sz, sizeof(u32) * C_N);
@@ -1372,8 +1405,9 @@ int ctx_create(int device, kolm_ctx** out) {
         for (auto& e : c->evg) KOLM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         KOLM_HIP_CHECK(hipEventCreateWithFlags(&c->eva, hipEventDisableTiming));
         KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_cnt, sizeof(u32) * H_N, hipHostMallocDefault));
-        KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_rt, 4096, hipHostMallocCoherent | hipHostMallocMapped));
-        std::memset(c->h_rt, 0, 4096);
+        KOLM_HIP_CHECK(hipHostMalloc((void**)&c->h_rt, sizeof(u32) * (kolm_ctx::RT_WORDS + 64),
+                                    hipHostMallocCoherent | hipHostMallocMapped));
+        std::memset(c->h_rt, 0, sizeof(u32) * (kolm_ctx::RT_WORDS + 64));
         KOLM_HIP_CHECK(hipHostGetDevicePointer((void**)&c->d_rt, c->h_rt, 0));
         for (auto& e : c->ev) KOLM_HIP_CHECK(hipEventCreate(&e));
         *out = c.release();

@@ -297,6 +297,8 @@ struct PackSpans {
     u32 o[6];
 };
 void launch_pack_spans(const PackSpans& ps, u32* dst, hipStream_t s);
+// the spans into coherent host memory, then `seq` into hseq[w] for each of the returned waves
+u32 launch_spans_to_host(const PackSpans& ps, u32* hdst, u32* hseq, u32 seq, hipStream_t s);
 // ncur: the list length, or (ncur_dev set) a bound for the grid with the length in ncur_dev
 void launch_classify_bins(const Seg* cur, u32 ncur, const u32* ncur_dev, const SortArgs& a, const Lists& L,
                           const Level& lv0, const Bins& bn, hipStream_t s, bool bins_zeroed = false);
@@ -336,8 +338,6 @@ struct SsClasses {
     u32 wg0[NCLASS + 1];
 };
 void launch_small_sorts(SsClasses sc, bool w32, const SortArgs& a, const Lists& L, hipStream_t s);
-// the per-round counters into coherent host memory, then `seq` into *hseq (one wave)
-void launch_counts_to_host(const u32* cnt, u32* hdst, u32 n, u32* hseq, u32 seq, hipStream_t s);
 void launch_finalize_eq(const Seg* eq, u32 count, const SortArgs& a, const Lists& L, hipStream_t s);
 void launch_rounds_sum(const u32* blk_last, u32 nb, u64* out, hipStream_t s);
 void launch_update_done(u32* blk_done, u32* blk_last, const u32* blk_split, u32 nb, u32 round, hipStream_t s);
